@@ -1,0 +1,160 @@
+/*
+ * orbx.h -- C ABI of the MI355X-native ORB extraction + Hamming matching library
+ * (liborbx.so, built from orbslam2commentedbyxcm_amd/csrc/).
+ *
+ * This is the drop-in boundary for ORB-SLAM2's per-frame hot path.  Every entry
+ * point names the reference interface it replaces (paths relative to the
+ * reference repository, xcmworkharder/OrbSlam2CommentedByXcm):
+ *
+ *   ORBextractor::ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+ *       include/ORBextractor.h:93, src/ORBextractor.cc:438-550  -> orbx_extractor_create
+ *   ORBextractor::operator()(image, mask, keypoints, descriptors)
+ *       include/ORBextractor.h:111, src/ORBextractor.cc:1513-1629 -> orbx_extract,
+ *       orbx_extract_batch, orbx_extract_batch_device
+ *   ORBextractor::Get{Levels,ScaleFactor,ScaleFactors,InverseScaleFactors,
+ *       ScaleSigmaSquares,InverseScaleSigmaSquares}
+ *       include/ORBextractor.h:119-159                              -> orbx_extractor_levels
+ *   ORBextractor::mvImagePyramid (public member read by Frame::ComputeStereoMatches)
+ *       include/ORBextractor.h:162, src/Frame.cc:682,782,810,816    -> orbx_pyramid_level
+ *   ORBmatcher::DescriptorDistance(a, b)
+ *       include/ORBmatcher.h:65, src/ORBmatcher.cc:1983-2003        -> orbx_hamming,
+ *       orbx_hamming_matrix_device
+ *   ORBmatcher candidate scoring inside SearchByProjection / SearchForTriangulation
+ *       src/ORBmatcher.cc:61-173, 1620-1789, 1792-1924, 850-1056     -> orbx_window_match
+ *
+ * Conventions: every function returns an int status (ORBX_OK = 0, ORBX_EMPTY = 1
+ * for the reference's silent empty-image no-op, negative on error) and never
+ * throws.  All pointers are plain host or device pointers; no C++ or torch types
+ * cross this boundary.  One extractor owns one HIP stream and is not re-entrant
+ * (like the reference's stateful ORBextractor); distinct extractors may be used
+ * from distinct threads concurrently (Frame.cc:127-131).
+ */
+#ifndef ORBX_H
+#define ORBX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBX_OK 0
+#define ORBX_EMPTY 1
+#define ORBX_ERR_ARG -1
+#define ORBX_ERR_HIP -2
+#define ORBX_ERR_CAPACITY -3
+#define ORBX_ERR_UNSUPPORTED -4
+#define ORBX_ERR_STATE -5
+
+#define ORBX_MAX_LEVELS 32
+
+/* Binary-identical to cv::KeyPoint {Point2f pt; float size, angle, response; int octave, class_id;} */
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orbx_keypoint;
+
+/* The five YAML parameters of Tracking.cc:129-149 (ORBextractor.{nFeatures,scaleFactor,
+ * nLevels,iniThFAST,minThFAST}). */
+typedef struct {
+    int nfeatures;
+    float scale_factor;
+    int nlevels;
+    int ini_th_fast;
+    int min_th_fast;
+} orbx_extractor_params;
+
+typedef struct orbx_extractor orbx_extractor;
+
+/* ORBextractor::ORBextractor.  Selects HIP device `device`, creates one stream. */
+int orbx_extractor_create(const orbx_extractor_params* params, int device, orbx_extractor** out);
+void orbx_extractor_destroy(orbx_extractor* ex);
+
+/* GetLevels/GetScaleFactors/...: each non-null array receives nlevels floats. */
+int orbx_extractor_levels(const orbx_extractor* ex, int* nlevels, float* scale, float* inv_scale,
+                          float* sigma2, float* inv_sigma2);
+/* mnFeaturesPerLevel (ORBextractor.h:212): nlevels ints. */
+int orbx_extractor_features_per_level(const orbx_extractor* ex, int* features);
+
+/* Upper bound on keypoints one W x H frame can produce (size `cap` with it). */
+int orbx_extractor_max_keypoints(orbx_extractor* ex, int width, int height, int* max_kps);
+
+/* ORBextractor::operator() on one host image (row stride in bytes).  Keypoints in
+ * the reference order (level-major, octree-list order), coordinates scaled to level
+ * 0; descriptors n x 32 bytes.  Returns ORBX_EMPTY (outputs untouched) for an empty
+ * image, ORBX_ERR_CAPACITY if more than `cap` keypoints were found (*n_out then
+ * holds the required count). */
+int orbx_extract(orbx_extractor* ex, const uint8_t* img, int width, int height, size_t stride,
+                 orbx_keypoint* kps, uint8_t* desc, int cap, int* n_out);
+
+/* The same for B host images of one size; frame b writes kps[b*cap ...],
+ * desc[b*cap*32 ...] and n_per_frame[b]. */
+int orbx_extract_batch(orbx_extractor* ex, int batch, const uint8_t* const* imgs, int width,
+                       int height, size_t stride, orbx_keypoint* kps, uint8_t* desc, int cap,
+                       int* n_per_frame);
+
+/* Device-resident fast path: d_imgs holds B frames (frame b at d_imgs + b*frame_pitch,
+ * rows `stride` bytes apart) already in HBM; outputs are device pointers as above.
+ * Work is enqueued on the extractor's stream (or on `stream` if non-null, a
+ * hipStream_t) and the call returns without synchronising.  n_per_frame[b] receives
+ * the full count even when it exceeds cap (only cap keypoints are then written). */
+int orbx_extract_batch_device(orbx_extractor* ex, int batch, const uint8_t* d_imgs,
+                              size_t frame_pitch, int width, int height, size_t stride,
+                              orbx_keypoint* d_kps, uint8_t* d_desc, int cap, int* d_n_per_frame,
+                              void* stream);
+
+/* The extractor's hipStream_t (as void*). */
+void* orbx_extractor_stream(orbx_extractor* ex);
+
+/* Per-stage timing of the last orbx_extract_batch_device call (requires
+ * orbx_extractor_set_timing(ex, 1) beforehand).  Names are static strings. */
+int orbx_extractor_set_timing(orbx_extractor* ex, int enable);
+int orbx_extractor_stage_times(orbx_extractor* ex, int max_stages, const char** names, float* ms,
+                               int* n_stages);
+
+/* mvImagePyramid[level] of frame `frame` of the last extraction: copies the level
+ * ROI (w x h) into host memory `dst` with row stride dst_stride. */
+int orbx_pyramid_level(orbx_extractor* ex, int frame, int level, uint8_t* dst, size_t dst_stride,
+                       int* w, int* h);
+/* Device pointer + row pitch of a pyramid level of the last device extraction. */
+int orbx_pyramid_level_device(orbx_extractor* ex, int frame, int level, const uint8_t** d_ptr,
+                              size_t* pitch, int* w, int* h);
+
+/* ORBmatcher::DescriptorDistance on two 32-byte host descriptors; returns 0..256. */
+int orbx_hamming(const uint8_t* a32, const uint8_t* b32);
+
+/* dist[i*nb + j] = Hamming(a_i, b_j) for device descriptor arrays (32 B rows). */
+int orbx_hamming_matrix_device(const uint8_t* d_a, int na, const uint8_t* d_b, int nb,
+                               int32_t* d_dist, void* stream);
+
+/* Windowed candidate scoring shared by the SearchByProjection overloads and
+ * SearchForTriangulation: for query q (32 B descriptor at d_qdesc + 32*q) the
+ * candidates are d_cand[d_cand_off[q] .. d_cand_off[q+1]) (indices into the target
+ * descriptor array, in the reference's iteration order).  Outputs per query:
+ * best/second-best distance, best candidate position (index into the target array,
+ * -1 if none), and the target levels of best and second (as SearchByProjection
+ * tracks them, ORBmatcher.cc:140-152).  `tie_last` = 0: strict < keeps the first
+ * equal candidate (SearchByProjection); 1: the last equal candidate wins the best
+ * slot (SearchForTriangulation, ORBmatcher.cc:955).  Device pointers, async. */
+int orbx_window_match_device(const uint8_t* d_qdesc, int nq, const uint8_t* d_tdesc,
+                             const int32_t* d_tlevel, const int32_t* d_cand_off,
+                             const int32_t* d_cand, int tie_last, int32_t* d_best_idx,
+                             int32_t* d_best_dist, int32_t* d_best_level, int32_t* d_second_dist,
+                             int32_t* d_second_level, void* stream);
+
+/* Host-pointer convenience wrapper of orbx_window_match_device (synchronous). */
+int orbx_window_match(int device, const uint8_t* qdesc, int nq, const uint8_t* tdesc, int nt,
+                      const int32_t* tlevel, const int32_t* cand_off, const int32_t* cand,
+                      int tie_last, int32_t* best_idx, int32_t* best_dist, int32_t* best_level,
+                      int32_t* second_dist, int32_t* second_level);
+
+/* Library / device info. */
+const char* orbx_version(void);
+int orbx_device_count(int* n);
+const char* orbx_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBX_H */

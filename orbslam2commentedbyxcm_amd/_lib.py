@@ -1,0 +1,104 @@
+"""ctypes binding of liborbx.so (include/orbx.h).
+
+The HIP library is the product: if it is missing this module raises instead of
+falling back to any CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(__file__).resolve().parent / "liborbx.so"
+
+ORBX_OK = 0
+ORBX_EMPTY = 1
+ORBX_ERR_ARG = -1
+ORBX_ERR_HIP = -2
+ORBX_ERR_CAPACITY = -3
+ORBX_ERR_UNSUPPORTED = -4
+ORBX_ERR_STATE = -5
+
+# == cv::KeyPoint / orbx_keypoint (28 bytes)
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+EXPORTED = [
+    "orbx_extractor_create", "orbx_extractor_destroy", "orbx_extractor_levels",
+    "orbx_extractor_features_per_level", "orbx_extractor_max_keypoints", "orbx_extract",
+    "orbx_extract_batch", "orbx_extract_batch_device", "orbx_extractor_stream",
+    "orbx_extractor_set_timing", "orbx_extractor_stage_times", "orbx_pyramid_level",
+    "orbx_pyramid_level_device", "orbx_hamming", "orbx_hamming_matrix_device",
+    "orbx_window_match_device", "orbx_window_match", "orbx_version", "orbx_device_count",
+    "orbx_last_error",
+]
+
+
+class ExtractorParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int), ("scale_factor", C.c_float), ("nlevels", C.c_int),
+                ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int)]
+
+
+class OrbxError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"orbx error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load liborbx.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError(f"{LIB_PATH} not built: run `python -m orbslam2commentedbyxcm_amd.build`")
+    L = C.CDLL(str(LIB_PATH))
+    vp, ip, u8p = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_uint8)
+    fp = C.POINTER(C.c_float)
+    L.orbx_extractor_create.argtypes = [C.POINTER(ExtractorParams), C.c_int, C.POINTER(vp)]
+    L.orbx_extractor_destroy.argtypes = [vp]
+    L.orbx_extractor_destroy.restype = None
+    L.orbx_extractor_levels.argtypes = [vp, ip, fp, fp, fp, fp]
+    L.orbx_extractor_features_per_level.argtypes = [vp, ip]
+    L.orbx_extractor_max_keypoints.argtypes = [vp, C.c_int, C.c_int, ip]
+    L.orbx_extract.argtypes = [vp, u8p, C.c_int, C.c_int, C.c_size_t, vp, u8p, C.c_int, ip]
+    L.orbx_extract_batch.argtypes = [vp, C.c_int, C.POINTER(u8p), C.c_int, C.c_int, C.c_size_t, vp, u8p,
+                                     C.c_int, ip]
+    L.orbx_extract_batch_device.argtypes = [vp, C.c_int, vp, C.c_size_t, C.c_int, C.c_int, C.c_size_t, vp, vp,
+                                            C.c_int, vp, vp]
+    L.orbx_extractor_stream.argtypes = [vp]
+    L.orbx_extractor_stream.restype = vp
+    L.orbx_extractor_set_timing.argtypes = [vp, C.c_int]
+    L.orbx_extractor_stage_times.argtypes = [vp, C.c_int, C.POINTER(C.c_char_p), fp, ip]
+    L.orbx_pyramid_level.argtypes = [vp, C.c_int, C.c_int, u8p, C.c_size_t, ip, ip]
+    L.orbx_pyramid_level_device.argtypes = [vp, C.c_int, C.c_int, C.POINTER(vp), C.POINTER(C.c_size_t), ip, ip]
+    L.orbx_hamming.argtypes = [u8p, u8p]
+    L.orbx_hamming_matrix_device.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp]
+    L.orbx_window_match_device.argtypes = [vp, C.c_int, vp, vp, vp, vp, C.c_int, vp, vp, vp, vp, vp, vp]
+    i32p = C.POINTER(C.c_int32)
+    L.orbx_window_match.argtypes = [C.c_int, u8p, C.c_int, u8p, C.c_int, i32p, i32p, i32p, C.c_int, i32p, i32p,
+                                    i32p, i32p, i32p]
+    L.orbx_version.restype = C.c_char_p
+    L.orbx_device_count.argtypes = [ip]
+    L.orbx_last_error.restype = C.c_char_p
+    _lib = L
+    return L
+
+
+def check(rc: int, allow=(ORBX_OK,)) -> int:
+    if rc in allow:
+        return rc
+    msg = lib().orbx_last_error().decode(errors="replace")
+    raise OrbxError(rc, msg)
+
+
+def u8ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+def i32ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_int32))

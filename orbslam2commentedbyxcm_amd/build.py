@@ -1,0 +1,76 @@
+"""Build liborbx.so (HIP, gfx950) in-tree with hipcc.
+
+    python -m orbslam2commentedbyxcm_amd.build        # incremental
+    python -m orbslam2commentedbyxcm_amd.build --clean
+
+The shared library lands next to this file so that it travels with the repository
+snapshot to the GPU box (it is git-ignored, not gpurun-ignored).  Every translation
+unit is compiled with -ffp-contract=off: the reference is built -std=c++11 (ISO),
+under which GCC does not contract a*b+c into FMA, and the descriptor / fastAtan2
+float expressions must round identically (hazard H4).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+OBJ = PKG / "_obj"
+LIB = PKG / "liborbx.so"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("ORBX_ARCH", "gfx950")
+
+SOURCES = ["orbx_geometry.cpp", "orbx_extract.hip", "orbx_match.hip", "orbx_api.cpp"]
+HEADERS = ["orbx_geometry.h", "orbx_kernels.h", "orb_pattern.inc"]
+FLAGS = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
+         f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+         f"-I{ROOT / 'include'}", f"-I{CSRC}"]
+
+
+def _newer(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _compile(src: str) -> Path:
+    out = OBJ / (src + ".o")
+    deps = [CSRC / src, ROOT / "include" / "orbx.h"] + [CSRC / h for h in HEADERS]
+    if _newer(out, deps):
+        cmd = [HIPCC, *FLAGS, "-c", str(CSRC / src), "-o", str(out)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src}:\n{r.stdout}\n{r.stderr}")
+    return out
+
+
+def build(verbose: bool = False) -> Path:
+    OBJ.mkdir(exist_ok=True)
+    with cf.ThreadPoolExecutor(max_workers=min(4, len(SOURCES))) as pool:
+        objs = list(pool.map(_compile, SOURCES))
+    if _newer(LIB, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(LIB), *map(str, objs)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print(f"built {LIB}")
+    return LIB
+
+
+def clean() -> None:
+    shutil.rmtree(OBJ, ignore_errors=True)
+    LIB.unlink(missing_ok=True)
+
+
+if __name__ == "__main__":
+    if "--clean" in sys.argv:
+        clean()
+    build(verbose=True)

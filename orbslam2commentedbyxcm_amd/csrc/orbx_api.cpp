@@ -1,0 +1,446 @@
+// orbx_api.cpp -- the extern "C" boundary (include/orbx.h) over the HIP kernels.
+//
+// One orbx_extractor == one reference ORBextractor instance: it owns a HIP stream,
+// the device plan for the last frame size, device buffers sized for the largest
+// batch seen, and (like the reference's mvImagePyramid) keeps the pyramid of the
+// last extraction until the next call.  No function throws across the ABI.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "orbx.h"
+#include "orbx_kernels.h"
+
+using namespace orbx;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* what) {
+    g_last_error = what ? what : "";
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+    g_last_error = std::string(where) + ": " + hipGetErrorString(e);
+    return ORBX_ERR_HIP;
+}
+
+#define HIP_TRY(expr)                                      \
+    do {                                                   \
+        hipError_t _e = (expr);                            \
+        if (_e != hipSuccess) return hip_fail(_e, #expr);  \
+    } while (0)
+
+template <typename T>
+hipError_t dalloc(T** p, size_t n) {
+    if (n == 0) n = 1;
+    return hipMalloc((void**)p, sizeof(T) * n);
+}
+
+}  // namespace
+
+struct orbx_extractor {
+    int device = 0;
+    OrbParams prm{};
+    hipStream_t stream = nullptr;
+    Plan plan;
+    DeviceBuffers db;
+    bool timing = false;
+    hipEvent_t ev[kStages + 1] = {};
+    float stage_ms[kStages] = {};
+    bool have_times = false;
+    // host-API staging
+    uint8_t* d_in = nullptr;
+    size_t d_in_bytes = 0;
+    orbx_keypoint* d_kps = nullptr;
+    uint8_t* d_desc = nullptr;
+    int* d_n = nullptr;
+    size_t d_out_cap = 0;  // keypoint slots
+    int d_n_cap = 0;
+    int last_batch = 0;
+    bool have_pyramid = false;
+};
+
+namespace {
+
+void free_buffers(DeviceBuffers& db) {
+    void* ptrs[] = {db.lv, db.cells, db.rtab, db.pyr, db.blur, db.slots, db.cell_count,
+                    db.keys, db.key_node, db.kept, db.kept_count, db.status};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    db = DeviceBuffers();
+}
+
+// (Re)plan for a frame size and make sure buffers hold `batch` frames.
+int prepare(orbx_extractor* ex, int W, int H, int batch) {
+    HIP_TRY(hipSetDevice(ex->device));
+    const bool same_size = ex->plan.ok && ex->plan.W == W && ex->plan.H == H;
+    if (!same_size) {
+        HIP_TRY(hipStreamSynchronize(ex->stream));
+        free_buffers(ex->db);
+        ex->have_pyramid = false;
+        if (!make_plan(ex->plan, ex->prm, W, H)) return fail(ORBX_ERR_UNSUPPORTED, ex->plan.why);
+    }
+    if (ex->db.batch_cap >= batch && same_size) return ORBX_OK;
+    HIP_TRY(hipStreamSynchronize(ex->stream));
+    const Plan& p = ex->plan;
+    DeviceBuffers& db = ex->db;
+    free_buffers(db);
+    ex->have_pyramid = false;
+    const size_t B = (size_t)batch;
+    HIP_TRY(dalloc(&db.lv, kMaxLevels));
+    HIP_TRY(dalloc(&db.cells, p.cells.size()));
+    HIP_TRY(dalloc(&db.rtab, p.rtab.size()));
+    HIP_TRY(dalloc(&db.pyr, B * (size_t)p.pyr_frame_bytes));
+    HIP_TRY(dalloc(&db.blur, B * (size_t)p.pyr_frame_bytes));
+    HIP_TRY(dalloc(&db.slots, B * (size_t)p.slots_per_frame));
+    HIP_TRY(dalloc(&db.cell_count, B * p.cells.size()));
+    HIP_TRY(dalloc(&db.keys, B * (size_t)p.keys_per_frame));
+    HIP_TRY(dalloc(&db.key_node, B * (size_t)p.keys_per_frame));
+    HIP_TRY(dalloc(&db.kept, B * (size_t)p.kept_per_frame));
+    HIP_TRY(dalloc(&db.kept_count, B * (size_t)p.L));
+    HIP_TRY(dalloc(&db.status, B));
+    HIP_TRY(hipMemcpyAsync(db.lv, p.lv, sizeof(LevelGeom) * kMaxLevels, hipMemcpyHostToDevice, ex->stream));
+    HIP_TRY(hipMemcpyAsync(db.cells, p.cells.data(), sizeof(CellGeom) * p.cells.size(), hipMemcpyHostToDevice,
+                           ex->stream));
+    HIP_TRY(hipMemcpyAsync(db.rtab, p.rtab.data(), sizeof(int16_t) * p.rtab.size(), hipMemcpyHostToDevice,
+                           ex->stream));
+    HIP_TRY(hipMemsetAsync(db.pyr, 0, B * (size_t)p.pyr_frame_bytes, ex->stream));
+    HIP_TRY(hipMemsetAsync(db.blur, 0, B * (size_t)p.pyr_frame_bytes, ex->stream));
+    HIP_TRY(hipStreamSynchronize(ex->stream));
+    db.batch_cap = batch;
+    return ORBX_OK;
+}
+
+int max_kps_of(const Plan& p) {
+    int s = 0;
+    for (int l = 0; l < p.L; l++) s += p.lv[l].ncap;
+    return s;
+}
+
+int run_device(orbx_extractor* ex, int batch, const uint8_t* d_imgs, size_t frame_pitch, int W, int H,
+               size_t stride, orbx_keypoint* d_kps, uint8_t* d_desc, int cap, int* d_n, hipStream_t stream) {
+    int rc = prepare(ex, W, H, batch);
+    if (rc != ORBX_OK) return rc;
+    hipEvent_t* ev = nullptr;
+    if (ex->timing) {
+        for (int i = 0; i <= kStages; i++)
+            if (!ex->ev[i]) HIP_TRY(hipEventCreate(&ex->ev[i]));
+        ev = ex->ev;
+    }
+    hipError_t e = launch_extract(ex->plan, ex->db, batch, d_imgs, frame_pitch, stride, d_kps, d_desc, cap, d_n,
+                                  stream, ev);
+    if (e != hipSuccess) return hip_fail(e, "launch_extract");
+    ex->have_times = ex->timing;
+    ex->last_batch = batch;
+    ex->have_pyramid = true;
+    return ORBX_OK;
+}
+
+int check_status(orbx_extractor* ex, int batch) {
+    std::vector<int> st((size_t)batch);
+    HIP_TRY(hipMemcpy(st.data(), ex->db.status, sizeof(int) * (size_t)batch, hipMemcpyDeviceToHost));
+    for (int b = 0; b < batch; b++)
+        if (st[(size_t)b]) return fail(ORBX_ERR_STATE, "octree kernel reported an internal overflow");
+    return ORBX_OK;
+}
+
+int ensure_host_staging(orbx_extractor* ex, size_t in_bytes, size_t out_slots, int nframes) {
+    if (ex->d_in_bytes < in_bytes) {
+        if (ex->d_in) (void)hipFree(ex->d_in);
+        ex->d_in = nullptr;
+        HIP_TRY(dalloc(&ex->d_in, in_bytes));
+        ex->d_in_bytes = in_bytes;
+    }
+    if (ex->d_out_cap < out_slots) {
+        if (ex->d_kps) (void)hipFree(ex->d_kps);
+        if (ex->d_desc) (void)hipFree(ex->d_desc);
+        ex->d_kps = nullptr;
+        ex->d_desc = nullptr;
+        HIP_TRY(dalloc(&ex->d_kps, out_slots));
+        HIP_TRY(dalloc(&ex->d_desc, out_slots * 32));
+        ex->d_out_cap = out_slots;
+    }
+    if (ex->d_n_cap < nframes) {
+        if (ex->d_n) (void)hipFree(ex->d_n);
+        ex->d_n = nullptr;
+        HIP_TRY(dalloc(&ex->d_n, (size_t)nframes));
+        ex->d_n_cap = nframes;
+    }
+    return ORBX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* orbx_version(void) { return "orbx 0.1 (gfx950)"; }
+
+const char* orbx_last_error(void) { return g_last_error.c_str(); }
+
+int orbx_device_count(int* n) {
+    if (!n) return fail(ORBX_ERR_ARG, "null");
+    int c = 0;
+    HIP_TRY(hipGetDeviceCount(&c));
+    *n = c;
+    return ORBX_OK;
+}
+
+int orbx_extractor_create(const orbx_extractor_params* params, int device, orbx_extractor** out) {
+    if (!params || !out) return fail(ORBX_ERR_ARG, "null argument");
+    *out = nullptr;
+    orbx_extractor* ex = new (std::nothrow) orbx_extractor();
+    if (!ex) return fail(ORBX_ERR_ARG, "out of host memory");
+    if (!init_params(ex->prm, params->nfeatures, params->scale_factor, params->nlevels, params->ini_th_fast,
+                     params->min_th_fast)) {
+        delete ex;
+        return fail(ORBX_ERR_ARG, "invalid ORB parameters");
+    }
+    ex->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = upload_constants(ex->prm);
+    if (e != hipSuccess) {
+        delete ex;
+        return hip_fail(e, "orbx_extractor_create");
+    }
+    *out = ex;
+    return ORBX_OK;
+}
+
+void orbx_extractor_destroy(orbx_extractor* ex) {
+    if (!ex) return;
+    (void)hipSetDevice(ex->device);
+    if (ex->stream) (void)hipStreamSynchronize(ex->stream);
+    free_buffers(ex->db);
+    if (ex->d_in) (void)hipFree(ex->d_in);
+    if (ex->d_kps) (void)hipFree(ex->d_kps);
+    if (ex->d_desc) (void)hipFree(ex->d_desc);
+    if (ex->d_n) (void)hipFree(ex->d_n);
+    for (auto& e : ex->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ex->stream) (void)hipStreamDestroy(ex->stream);
+    delete ex;
+}
+
+int orbx_extractor_levels(const orbx_extractor* ex, int* nlevels, float* scale, float* inv_scale, float* sigma2,
+                          float* inv_sigma2) {
+    if (!ex) return fail(ORBX_ERR_ARG, "null extractor");
+    const int L = ex->prm.nlevels;
+    if (nlevels) *nlevels = L;
+    if (scale) std::memcpy(scale, ex->prm.scale, sizeof(float) * L);
+    if (inv_scale) std::memcpy(inv_scale, ex->prm.inv_scale, sizeof(float) * L);
+    if (sigma2) std::memcpy(sigma2, ex->prm.sigma2, sizeof(float) * L);
+    if (inv_sigma2) std::memcpy(inv_sigma2, ex->prm.inv_sigma2, sizeof(float) * L);
+    return ORBX_OK;
+}
+
+int orbx_extractor_features_per_level(const orbx_extractor* ex, int* features) {
+    if (!ex || !features) return fail(ORBX_ERR_ARG, "null argument");
+    std::memcpy(features, ex->prm.features, sizeof(int) * ex->prm.nlevels);
+    return ORBX_OK;
+}
+
+int orbx_extractor_max_keypoints(orbx_extractor* ex, int width, int height, int* max_kps) {
+    if (!ex || !max_kps) return fail(ORBX_ERR_ARG, "null argument");
+    Plan p;
+    if (!make_plan(p, ex->prm, width, height)) return fail(ORBX_ERR_UNSUPPORTED, p.why);
+    *max_kps = max_kps_of(p);
+    return ORBX_OK;
+}
+
+void* orbx_extractor_stream(orbx_extractor* ex) { return ex ? (void*)ex->stream : nullptr; }
+
+int orbx_extractor_set_timing(orbx_extractor* ex, int enable) {
+    if (!ex) return fail(ORBX_ERR_ARG, "null extractor");
+    ex->timing = enable != 0;
+    return ORBX_OK;
+}
+
+int orbx_extractor_stage_times(orbx_extractor* ex, int max_stages, const char** names, float* ms, int* n_stages) {
+    if (!ex) return fail(ORBX_ERR_ARG, "null extractor");
+    if (!ex->have_times) return fail(ORBX_ERR_STATE, "no timed extraction yet");
+    HIP_TRY(hipEventSynchronize(ex->ev[kStages - 1]));
+    int n = kStages < max_stages ? kStages : max_stages;
+    for (int i = 0; i < n; i++) {
+        float t = 0.f;
+        if (i < kStages - 1)
+            HIP_TRY(hipEventElapsedTime(&t, ex->ev[i], ex->ev[i + 1]));
+        else
+            HIP_TRY(hipEventElapsedTime(&t, ex->ev[0], ex->ev[kStages - 1]));
+        if (names) names[i] = kStageNames[i];
+        if (ms) ms[i] = t;
+    }
+    if (n_stages) *n_stages = n;
+    return ORBX_OK;
+}
+
+int orbx_extract_batch_device(orbx_extractor* ex, int batch, const uint8_t* d_imgs, size_t frame_pitch, int width,
+                              int height, size_t stride, orbx_keypoint* d_kps, uint8_t* d_desc, int cap,
+                              int* d_n_per_frame, void* stream) {
+    if (!ex || batch < 0 || cap < 0) return fail(ORBX_ERR_ARG, "bad argument");
+    if (batch == 0) return ORBX_OK;
+    if (width <= 0 || height <= 0 || !d_imgs) return ORBX_EMPTY;  // ORBextractor.cc:1517-1518
+    if (stride < (size_t)width || !d_kps || !d_desc || !d_n_per_frame) return fail(ORBX_ERR_ARG, "bad buffers");
+    hipStream_t s = stream ? (hipStream_t)stream : ex->stream;
+    return run_device(ex, batch, d_imgs, frame_pitch, width, height, stride, d_kps, d_desc, cap, d_n_per_frame, s);
+}
+
+int orbx_extract_batch(orbx_extractor* ex, int batch, const uint8_t* const* imgs, int width, int height,
+                       size_t stride, orbx_keypoint* kps, uint8_t* desc, int cap, int* n_per_frame) {
+    if (!ex || batch < 0 || cap < 0 || !imgs) return fail(ORBX_ERR_ARG, "bad argument");
+    if (batch == 0) return ORBX_OK;
+    if (width <= 0 || height <= 0) return ORBX_EMPTY;
+    if (stride < (size_t)width || !n_per_frame) return fail(ORBX_ERR_ARG, "bad buffers");
+    HIP_TRY(hipSetDevice(ex->device));
+    const size_t fbytes = (size_t)width * height;
+    int rc = ensure_host_staging(ex, fbytes * batch, (size_t)batch * (cap > 0 ? cap : 1), batch);
+    if (rc != ORBX_OK) return rc;
+    for (int b = 0; b < batch; b++)
+        HIP_TRY(hipMemcpy2DAsync(ex->d_in + fbytes * b, width, imgs[b], stride, width, height, hipMemcpyHostToDevice,
+                                 ex->stream));
+    rc = run_device(ex, batch, ex->d_in, fbytes, width, height, (size_t)width, ex->d_kps, ex->d_desc,
+                    cap > 0 ? cap : 1, ex->d_n, ex->stream);
+    if (rc != ORBX_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(n_per_frame, ex->d_n, sizeof(int) * batch, hipMemcpyDeviceToHost, ex->stream));
+    HIP_TRY(hipStreamSynchronize(ex->stream));
+    rc = check_status(ex, batch);
+    if (rc != ORBX_OK) return rc;
+    int overflow = 0;
+    for (int b = 0; b < batch; b++) {
+        const int n = n_per_frame[b] < cap ? n_per_frame[b] : cap;
+        if (n_per_frame[b] > cap) overflow = 1;
+        if (n > 0) {
+            if (kps)
+                HIP_TRY(hipMemcpyAsync(kps + (size_t)b * cap, ex->d_kps + (size_t)b * cap, sizeof(orbx_keypoint) * n,
+                                       hipMemcpyDeviceToHost, ex->stream));
+            if (desc)
+                HIP_TRY(hipMemcpyAsync(desc + (size_t)b * cap * 32, ex->d_desc + (size_t)b * cap * 32, (size_t)n * 32,
+                                       hipMemcpyDeviceToHost, ex->stream));
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(ex->stream));
+    return overflow ? fail(ORBX_ERR_CAPACITY, "more keypoints than cap") : ORBX_OK;
+}
+
+int orbx_extract(orbx_extractor* ex, const uint8_t* img, int width, int height, size_t stride, orbx_keypoint* kps,
+                 uint8_t* desc, int cap, int* n_out) {
+    if (!ex || !n_out) return fail(ORBX_ERR_ARG, "bad argument");
+    if (!img || width <= 0 || height <= 0) return ORBX_EMPTY;
+    const uint8_t* imgs[1] = {img};
+    return orbx_extract_batch(ex, 1, imgs, width, height, stride, kps, desc, cap, n_out);
+}
+
+int orbx_pyramid_level_device(orbx_extractor* ex, int frame, int level, const uint8_t** d_ptr, size_t* pitch,
+                              int* w, int* h) {
+    if (!ex || !ex->have_pyramid) return fail(ORBX_ERR_STATE, "no extraction yet");
+    if (frame < 0 || frame >= ex->last_batch || level < 0 || level >= ex->plan.L) return fail(ORBX_ERR_ARG, "range");
+    const LevelGeom& g = ex->plan.lv[level];
+    if (d_ptr) *d_ptr = ex->db.pyr + (size_t)frame * ex->plan.pyr_frame_bytes + g.off;
+    if (pitch) *pitch = (size_t)g.pitch;
+    if (w) *w = g.w;
+    if (h) *h = g.h;
+    return ORBX_OK;
+}
+
+int orbx_pyramid_level(orbx_extractor* ex, int frame, int level, uint8_t* dst, size_t dst_stride, int* w, int* h) {
+    const uint8_t* src = nullptr;
+    size_t pitch = 0;
+    int lw = 0, lh = 0;
+    int rc = orbx_pyramid_level_device(ex, frame, level, &src, &pitch, &lw, &lh);
+    if (rc != ORBX_OK) return rc;
+    if (w) *w = lw;
+    if (h) *h = lh;
+    if (!dst) return ORBX_OK;
+    if (dst_stride < (size_t)lw) return fail(ORBX_ERR_ARG, "dst_stride");
+    HIP_TRY(hipSetDevice(ex->device));
+    HIP_TRY(hipMemcpy2DAsync(dst, dst_stride, src, pitch, lw, lh, hipMemcpyDeviceToHost, ex->stream));
+    HIP_TRY(hipStreamSynchronize(ex->stream));
+    return ORBX_OK;
+}
+
+int orbx_hamming(const uint8_t* a32, const uint8_t* b32) {
+    if (!a32 || !b32) return fail(ORBX_ERR_ARG, "null descriptor");
+    int d = 0;
+    for (int i = 0; i < 4; i++) {
+        uint64_t x, y;
+        std::memcpy(&x, a32 + 8 * i, 8);
+        std::memcpy(&y, b32 + 8 * i, 8);
+        d += __builtin_popcountll(x ^ y);
+    }
+    return d;
+}
+
+int orbx_hamming_matrix_device(const uint8_t* d_a, int na, const uint8_t* d_b, int nb, int32_t* d_dist,
+                               void* stream) {
+    if (na < 0 || nb < 0 || (na && !d_a) || (nb && !d_b) || (na && nb && !d_dist))
+        return fail(ORBX_ERR_ARG, "bad argument");
+    hipError_t e = launch_hamming_matrix(d_a, na, d_b, nb, d_dist, (hipStream_t)stream);
+    return e == hipSuccess ? ORBX_OK : hip_fail(e, "hamming_matrix");
+}
+
+int orbx_window_match_device(const uint8_t* d_qdesc, int nq, const uint8_t* d_tdesc, const int32_t* d_tlevel,
+                             const int32_t* d_cand_off, const int32_t* d_cand, int tie_last, int32_t* d_best_idx,
+                             int32_t* d_best_dist, int32_t* d_best_level, int32_t* d_second_dist,
+                             int32_t* d_second_level, void* stream) {
+    if (nq < 0) return fail(ORBX_ERR_ARG, "nq");
+    if (nq == 0) return ORBX_OK;
+    if (!d_qdesc || !d_cand_off || !d_best_idx || !d_best_dist || !d_best_level || !d_second_dist || !d_second_level)
+        return fail(ORBX_ERR_ARG, "null buffer");
+    hipError_t e = launch_window_match(d_qdesc, nq, d_tdesc, d_tlevel, d_cand_off, d_cand, tie_last, d_best_idx,
+                                       d_best_dist, d_best_level, d_second_dist, d_second_level, (hipStream_t)stream);
+    return e == hipSuccess ? ORBX_OK : hip_fail(e, "window_match");
+}
+
+int orbx_window_match(int device, const uint8_t* qdesc, int nq, const uint8_t* tdesc, int nt, const int32_t* tlevel,
+                      const int32_t* cand_off, const int32_t* cand, int tie_last, int32_t* best_idx,
+                      int32_t* best_dist, int32_t* best_level, int32_t* second_dist, int32_t* second_level) {
+    if (nq < 0 || nt < 0 || !cand_off) return fail(ORBX_ERR_ARG, "bad argument");
+    if (nq == 0) return ORBX_OK;
+    const int ncand = cand_off[nq];
+    for (int i = 0; i < ncand; i++)
+        if (cand[i] < 0 || cand[i] >= nt) return fail(ORBX_ERR_ARG, "candidate index out of range");
+    HIP_TRY(hipSetDevice(device));
+    uint8_t *dq = nullptr, *dt = nullptr;
+    int32_t *dl = nullptr, *doff = nullptr, *dc = nullptr, *dout = nullptr;
+    auto cleanup = [&]() {
+        void* ps[] = {dq, dt, dl, doff, dc, dout};
+        for (void* p : ps)
+            if (p) (void)hipFree(p);
+    };
+    hipError_t e = hipSuccess;
+    do {
+        if ((e = dalloc(&dq, (size_t)nq * 32)) != hipSuccess) break;
+        if ((e = dalloc(&dt, (size_t)nt * 32)) != hipSuccess) break;
+        if ((e = dalloc(&dl, (size_t)nt)) != hipSuccess) break;
+        if ((e = dalloc(&doff, (size_t)nq + 1)) != hipSuccess) break;
+        if ((e = dalloc(&dc, (size_t)ncand)) != hipSuccess) break;
+        if ((e = dalloc(&dout, (size_t)nq * 5)) != hipSuccess) break;
+        if ((e = hipMemcpy(dq, qdesc, (size_t)nq * 32, hipMemcpyHostToDevice)) != hipSuccess) break;
+        if (nt && (e = hipMemcpy(dt, tdesc, (size_t)nt * 32, hipMemcpyHostToDevice)) != hipSuccess) break;
+        if (nt && tlevel && (e = hipMemcpy(dl, tlevel, sizeof(int32_t) * nt, hipMemcpyHostToDevice)) != hipSuccess) break;
+        if ((e = hipMemcpy(doff, cand_off, sizeof(int32_t) * (nq + 1), hipMemcpyHostToDevice)) != hipSuccess) break;
+        if (ncand && (e = hipMemcpy(dc, cand, sizeof(int32_t) * ncand, hipMemcpyHostToDevice)) != hipSuccess) break;
+        e = launch_window_match(dq, nq, dt, tlevel ? dl : nullptr, doff, dc, tie_last, dout, dout + nq, dout + 2 * nq,
+                                dout + 3 * nq, dout + 4 * nq, nullptr);
+        if (e != hipSuccess) break;
+        std::vector<int32_t> h((size_t)nq * 5);
+        if ((e = hipMemcpy(h.data(), dout, sizeof(int32_t) * nq * 5, hipMemcpyDeviceToHost)) != hipSuccess) break;
+        std::memcpy(best_idx, h.data(), sizeof(int32_t) * nq);
+        std::memcpy(best_dist, h.data() + nq, sizeof(int32_t) * nq);
+        std::memcpy(best_level, h.data() + 2 * nq, sizeof(int32_t) * nq);
+        std::memcpy(second_dist, h.data() + 3 * nq, sizeof(int32_t) * nq);
+        std::memcpy(second_level, h.data() + 4 * nq, sizeof(int32_t) * nq);
+    } while (0);
+    cleanup();
+    return e == hipSuccess ? ORBX_OK : hip_fail(e, "orbx_window_match");
+}
+
+}  // extern "C"

@@ -1,0 +1,832 @@
+// orbx_extract.hip -- MI355X (gfx950) kernels for ORB-SLAM2's ORBextractor::operator().
+//
+// Pipeline for a batch of B frames of one size (one launch per stage, every stage
+// covers all frames and, except the pyramid, all levels at once):
+//   1. k_copy_level0 + k_resize (x L-1) : image pyramid, ORBextractor.cc:1635-1694
+//   2. k_fast_cells   : per 30-px cell FAST-9 score, window-local NMS, iniTh -> minTh
+//                       fallback, ordered compaction            cc:1025-1122
+//   3. k_octree       : DistributeOctTree, one workgroup per (frame, level)  cc:667-1013
+//   4. k_blur         : GaussianBlur 7x7 sigma 2 REFLECT_101 per level       cc:1587-1595
+//   5. k_describe     : IC angle + steered BRIEF + level scaling + output    cc:59-172,1597-1627
+// Bit-exactness: integer arithmetic everywhere except fastAtan2/cos/sin/cvRound,
+// which follow the reference's float expression order (built -ffp-contract=off).
+#include <hip/hip_runtime.h>
+
+#include "orbx_kernels.h"
+
+namespace orbx {
+
+const char* const kStageNames[kStages] = {"pyramid", "fast_cells", "octree", "blur", "describe", "total"};
+
+__constant__ int8_t c_pattern[1024];
+__constant__ int c_umax[16];
+
+static const int8_t kPatternHost[1024] = {
+#include "orb_pattern.inc"
+};
+
+hipError_t upload_constants(const OrbParams& prm) {
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), kPatternHost, sizeof(kPatternHost));
+    if (e != hipSuccess) return e;
+    return hipMemcpyToSymbol(HIP_SYMBOL(c_umax), prm.umax, sizeof(prm.umax));
+}
+
+// Orders this lane's LDS accesses against the other lanes of its wave.
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// ------------------------------------------------------------------ pyramid
+
+// Level 0 = the input frame copied into the pyramid block (ORBextractor.cc:1688-1690;
+// the REFLECT_101 border is never read by extraction).
+__global__ __launch_bounds__(256) void k_copy_level0(const uint8_t* __restrict__ src, size_t frame_pitch,
+                                                     size_t stride, int w, uint8_t* __restrict__ pyr,
+                                                     long long fb, int pitch) {
+    const int f = blockIdx.z, y = blockIdx.y;
+    const int x = (blockIdx.x * 256 + threadIdx.x) * 4;
+    const uint8_t* s = src + (size_t)f * frame_pitch + (size_t)y * stride;
+    uint8_t* d = pyr + (size_t)f * fb + (size_t)y * pitch;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (x + k < w) d[x + k] = s[x + k];
+}
+
+// cv::resize(level l-1 ROI, level l, INTER_LINEAR), OpenCV 3.3.1 fixed point:
+// h = S[sx0]*a0 + S[sx1]*a1 (exact), dst = ((b0*(h0>>4))>>16 + (b1*(h1>>4))>>16 + 2)>>2.
+__global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, long long fb,
+                                                const LevelGeom* __restrict__ lv, int l,
+                                                const int16_t* __restrict__ rtab) {
+    const LevelGeom& g = lv[l];
+    const LevelGeom& p = lv[l - 1];
+    const int f = blockIdx.z, dy = blockIdx.y;
+    const int dx = blockIdx.x * 256 + threadIdx.x;
+    if (dx >= g.w) return;
+    const int16_t* yt = rtab + g.ytab_off + 4 * dy;
+    const int16_t* xt = rtab + g.xtab_off + 4 * dx;
+    const uint8_t* base = pyr + (size_t)f * fb + p.off;
+    const uint8_t* S0 = base + (size_t)yt[0] * p.pitch;
+    const uint8_t* S1 = base + (size_t)yt[1] * p.pitch;
+    const int a0 = xt[2], a1 = xt[3];
+    const int h0 = S0[xt[0]] * a0 + S0[xt[1]] * a1;
+    const int h1 = S1[xt[0]] * a0 + S1[xt[1]] * a1;
+    const int b0 = yt[2], b1 = yt[3];
+    int v = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
+    v = v < 0 ? 0 : (v > 255 ? 255 : v);
+    pyr[(size_t)f * fb + g.off + (size_t)dy * g.pitch + dx] = (uint8_t)v;
+}
+
+// ------------------------------------------------------------------ FAST cells
+
+constexpr int kTileDim = kCellMax + 6;  // sub-image (window + 3-px ring margin)
+
+// FAST-9/16 corner strength M = max over the 16 contiguous 9-arcs of
+// max(min(v - ring), min(ring - v)).  At threshold t the pixel is a corner iff
+// M > t, and cornerScore<16> returns max(t, M) - 1 = M - 1 (threshold-independent).
+__device__ __forceinline__ int fast_strength(const uint8_t* t, int v) {
+    // ring offsets (dx, dy) of features2d makeOffsets(16), on a kTileDim-pitch tile
+    const int off[16] = {0 + 3 * kTileDim,  1 + 3 * kTileDim,  2 + 2 * kTileDim,  3 + 1 * kTileDim,
+                         3,                 3 - 1 * kTileDim,  2 - 2 * kTileDim,  1 - 3 * kTileDim,
+                         0 - 3 * kTileDim, -1 - 3 * kTileDim, -2 - 2 * kTileDim, -3 - 1 * kTileDim,
+                         -3,               -3 + 1 * kTileDim, -2 + 2 * kTileDim, -1 + 3 * kTileDim};
+    int d[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) d[k] = v - (int)t[off[k]];
+    int amax = -1024, bmin = 1024;
+#pragma unroll
+    for (int s = 0; s < 16; s++) {
+        int mn = d[s], mx = d[s];
+#pragma unroll
+        for (int i = 1; i < 9; i++) {
+            const int x = d[(s + i) & 15];
+            mn = x < mn ? x : mn;
+            mx = x > mx ? x : mx;
+        }
+        amax = mn > amax ? mn : amax;
+        bmin = mx < bmin ? mx : bmin;
+    }
+    const int M = amax > -bmin ? amax : -bmin;
+    return M > 0 ? M : 0;
+}
+
+// One wave per cell.  Reproduces cv::FAST(cell, kps, t, true) for t = iniThFAST and,
+// if that leaves the cell empty, t = minThFAST (ORBextractor.cc:1091-1104), with the
+// window-local non-max suppression of FAST_t (neighbours outside the detection window
+// or below threshold score 0), and writes the cell's keypoints in raster order.
+__global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ pyr, long long fb,
+                                                    const LevelGeom* __restrict__ lv,
+                                                    const CellGeom* __restrict__ cells, int ncells,
+                                                    int ini_th, int min_th, uint32_t* __restrict__ slots,
+                                                    int slots_pf, int* __restrict__ cell_count) {
+    __shared__ uint8_t s_tile[4][kTileDim * kTileDim];
+    __shared__ uint8_t s_m[4][kCellMax * kCellMax];
+    __shared__ unsigned long long s_mask[4][kCellMax];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ci = blockIdx.x * 4 + wave;
+    const int f = blockIdx.y;
+    if (ci >= ncells) return;  // whole wave exits; no block barriers below
+    const CellGeom c = cells[ci];
+    const LevelGeom& g = lv[c.level];
+    const uint8_t* src = pyr + (size_t)f * fb + g.off + (size_t)c.y0 * g.pitch + c.x0;
+    uint8_t* tile = s_tile[wave];
+    uint8_t* msc = s_m[wave];
+    for (int r = 0; r < c.rows; r++)
+        for (int col = lane; col < c.cols; col += 64) tile[r * kTileDim + col] = src[(size_t)r * g.pitch + col];
+    wave_lds_fence();
+    const int wr = c.rows - 6, wc = c.cols - 6;  // detection window [3,rows-3) x [3,cols-3)
+    int count = 0;
+    if (wr > 0 && wc > 0) {
+        for (int r = 0; r < wr; r++) {
+            if (lane < wc) {
+                const uint8_t* p = tile + (r + 3) * kTileDim + lane + 3;
+                msc[r * kCellMax + lane] = (uint8_t)fast_strength(p, p[0]);
+            }
+        }
+        wave_lds_fence();
+        for (int pass = 0; pass < 2; pass++) {
+            int t = pass == 0 ? ini_th : min_th;
+            t = t < 0 ? 0 : (t > 255 ? 255 : t);
+            count = 0;
+            for (int r = 0; r < wr; r++) {
+                bool keep = false;
+                if (lane < wc) {
+                    const int m = msc[r * kCellMax + lane];
+                    if (m > t) {
+                        const int s = m - 1;
+                        int nb = 0;
+#pragma unroll
+                        for (int dy = -1; dy <= 1; dy++) {
+                            const int rr = r + dy;
+                            if (rr < 0 || rr >= wr) continue;
+#pragma unroll
+                            for (int dx = -1; dx <= 1; dx++) {
+                                if (dx == 0 && dy == 0) continue;
+                                const int cc = lane + dx;
+                                if (cc < 0 || cc >= wc) continue;
+                                const int mn = msc[rr * kCellMax + cc];
+                                const int sn = mn > t ? mn - 1 : 0;
+                                nb = sn > nb ? sn : nb;
+                            }
+                        }
+                        keep = s > nb;
+                    }
+                }
+                const unsigned long long mask = __ballot(keep);
+                if (lane == 0) s_mask[wave][r] = mask;
+                count += __popcll(mask);
+            }
+            if (count > 0) break;
+        }
+        wave_lds_fence();
+        uint32_t* out = slots + (size_t)f * slots_pf + c.slot_off;
+        int running = 0;
+        const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+        for (int r = 0; r < wr; r++) {
+            const unsigned long long mask = s_mask[wave][r];
+            if ((mask >> lane) & 1ull) {
+                const int idx = running + __popcll(mask & below);
+                const int xr = c.x0 + 3 + lane - kMinBorder;  // relative to minBorderX
+                const int yr = c.y0 + 3 + r - kMinBorder;
+                const int resp = msc[r * kCellMax + lane] - 1;
+                out[idx] = (uint32_t)xr | ((uint32_t)yr << 12) | ((uint32_t)resp << 24);
+            }
+            running += __popcll(mask);
+        }
+    }
+    if (lane == 0) cell_count[(size_t)f * ncells + ci] = count;
+}
+
+// ------------------------------------------------------------------ block helpers
+
+// In-place exclusive scan of a[0..n) by a 256-thread block; returns the total.
+// `tmp` holds >= 8 ints of LDS.  All threads must call it.
+__device__ int block_exscan(int* a, int n, int* tmp) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int carry = 0;
+    for (int base = 0; base < n; base += 256) {
+        const int i = base + tid;
+        const int v = i < n ? a[i] : 0;
+        int x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) tmp[wave] = x;
+        __syncthreads();
+        int wbase = 0;
+        for (int k = 0; k < wave; k++) wbase += tmp[k];
+        const int chunk_total = tmp[0] + tmp[1] + tmp[2] + tmp[3];
+        if (i < n) a[i] = carry + wbase + x - v;
+        carry += chunk_total;
+        __syncthreads();
+    }
+    return carry;
+}
+
+__device__ __forceinline__ int key_x(uint32_t k) { return (int)(k & 0xfffu); }
+__device__ __forceinline__ int key_y(uint32_t k) { return (int)((k >> 12) & 0xfffu); }
+__device__ __forceinline__ int key_resp(uint32_t k) { return (int)(k >> 24); }
+
+// ExtractorNode::DivideNode quadrant (ORBextractor.cc:587-641): halves are
+// ceil(width/2), ceil(height/2); n1 UL, n2 UR, n3 BL, n4 BR.
+__device__ __forceinline__ int quadrant(int x, int y, int x0, int y0, int x1, int y1) {
+    const int mx = x0 + ((x1 - x0 + 1) >> 1);
+    const int my = y0 + ((y1 - y0 + 1) >> 1);
+    return x < mx ? (y < my ? 0 : 2) : (y < my ? 1 : 3);
+}
+
+__device__ __forceinline__ void child_box(int q, int x0, int y0, int x1, int y1, int& cx0, int& cy0,
+                                          int& cx1, int& cy1) {
+    const int mx = x0 + ((x1 - x0 + 1) >> 1);
+    const int my = y0 + ((y1 - y0 + 1) >> 1);
+    cx0 = (q & 1) ? mx : x0;
+    cx1 = (q & 1) ? x1 : mx;
+    cy0 = (q & 2) ? my : y0;
+    cy1 = (q & 2) ? y1 : my;
+}
+
+// ------------------------------------------------------------------ octree
+
+// Node list, stored in list order (front first).  Two buffers, swapped every step.
+struct NodeBuf {
+    int16_t *x0, *y0, *x1, *y1;
+    int* cnt;
+    int* crank;     // creation rank within the step that created the node
+    uint8_t* inV;   // member of vSizeAndPointerToNode (created last step with >1 key)
+};
+
+// One workgroup per (level, frame): gathers the level's FAST keypoints in cell order
+// and runs ORBextractor::DistributeOctTree (ORBextractor.cc:667-1013) as a sequence of
+// data-parallel list rewrites that reproduce the std::list order exactly:
+//  * a full pass (cc:779-862) splits every node with >1 key; children are pushed to
+//    the front, so the new list is [children of the last split node (n4..n1), ...,
+//    children of the first split node, then the surviving single-key nodes in order];
+//  * the final phase (cc:888-971) splits vSizeAndPointerToNode sorted by (size, node
+//    address) from the back until the list holds N nodes.  Node addresses are taken
+//    in allocation order (hazard H1), i.e. ties go to the later-created
+//    node first;
+//  * each surviving node keeps its max-response key, first (lowest index) on ties
+//    (cc:984-1009).
+__global__ __launch_bounds__(256) void k_octree(const LevelGeom* __restrict__ lv, int L,
+                                                const uint32_t* __restrict__ slots, int slots_pf,
+                                                const CellGeom* __restrict__ cells,
+                                                const int* __restrict__ cell_count, int ncells_total,
+                                                uint32_t* __restrict__ keys, int* __restrict__ key_node,
+                                                int keys_pf, uint32_t* __restrict__ kept, int kept_pf,
+                                                int* __restrict__ kept_count, int* __restrict__ status,
+                                                int NC) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ int s_tmp[8];
+    __shared__ int s_scal[16];
+    __shared__ int s_off[256];
+    __shared__ int s_map[kMaxIni];
+    __shared__ int s_icnt[kMaxIni];
+
+    const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const LevelGeom& g = lv[l];
+    const int N = g.N;
+
+    // LDS carve-up (NC nodes)
+    unsigned long long* best = (unsigned long long*)smem;               // NC u64
+    int* ccnt = (int*)(best + NC);                                      // 4*NC
+    int* sa = ccnt + 4 * NC;                                            // NC
+    int* sb = sa + NC;                                                  // NC
+    int* sc = sb + NC;                                                  // NC
+    int* cntb = sc + NC;                                                // 2*NC
+    int* crkb = cntb + 2 * NC;                                          // 2*NC
+    int16_t* boxb = (int16_t*)(crkb + 2 * NC);                          // 8*NC
+    uint8_t* inVb = (uint8_t*)(boxb + 8 * NC);                          // 2*NC
+    NodeBuf nb[2];
+    for (int b = 0; b < 2; b++) {
+        nb[b].x0 = boxb + (4 * b + 0) * NC;
+        nb[b].y0 = boxb + (4 * b + 1) * NC;
+        nb[b].x1 = boxb + (4 * b + 2) * NC;
+        nb[b].y1 = boxb + (4 * b + 3) * NC;
+        nb[b].cnt = cntb + b * NC;
+        nb[b].crank = crkb + b * NC;
+        nb[b].inV = inVb + b * NC;
+    }
+
+    uint32_t* K = keys + (size_t)f * keys_pf + g.key_off;
+    int* KN = key_node + (size_t)f * keys_pf + g.key_off;
+
+    // ---- 1. gather candidates in cell order (vToDistributeKeys, cc:1054-1122)
+    int n = 0;
+    for (int cb = 0; cb < g.ncells; cb += 256) {
+        const int nc = g.ncells - cb < 256 ? g.ncells - cb : 256;
+        if (tid < nc) s_off[tid] = cell_count[(size_t)f * ncells_total + g.cell_first + cb + tid];
+        __syncthreads();
+        const int tot = block_exscan(s_off, nc, s_tmp);
+        for (int k = wave; k < nc; k += 4) {
+            const CellGeom& c = cells[g.cell_first + cb + k];
+            const uint32_t* src = slots + (size_t)f * slots_pf + c.slot_off;
+            const int cnt = (k + 1 < nc ? s_off[k + 1] : tot) - s_off[k];
+            for (int i = lane; i < cnt; i += 64) K[n + s_off[k] + i] = src[i];
+        }
+        n += tot;
+        __syncthreads();
+    }
+    __threadfence_block();
+
+    // ---- 2. root nodes (cc:674-742)
+    if (tid < g.nIni) s_icnt[tid] = 0;
+    __syncthreads();
+    for (int k = tid; k < n; k += 256) {
+        const int idx = (int)((float)key_x(K[k]) / g.hX);
+        atomicAdd(&s_icnt[idx], 1);
+        KN[k] = idx;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int j = 0;
+        for (int i = 0; i < g.nIni; i++) {
+            if (s_icnt[i] > 0) {
+                s_map[i] = j;
+                nb[0].x0[j] = (int16_t)g.ini_x0[i];
+                nb[0].x1[j] = (int16_t)g.ini_x0[i + 1];
+                nb[0].y0[j] = 0;
+                nb[0].y1[j] = (int16_t)g.height_rel;
+                nb[0].cnt[j] = s_icnt[i];
+                nb[0].crank[j] = i;
+                nb[0].inV[j] = 0;
+                j++;
+            } else {
+                s_map[i] = -1;
+            }
+        }
+        s_scal[0] = j;  // size
+    }
+    __syncthreads();
+    for (int k = tid; k < n; k += 256) KN[k] = s_map[KN[k]];
+    __syncthreads();
+
+    int cur = 0;
+    int size = s_scal[0];
+    int guard = 0;
+    bool finish = false;
+    bool final_phase = false;
+
+    // ---- 3. full passes (cc:758-873)
+    while (!finish && !final_phase) {
+        if (++guard > 64) { if (tid == 0) atomicOr(&status[f], kStatusIterations); break; }
+        const NodeBuf& A = nb[cur];
+        const NodeBuf& B = nb[cur ^ 1];
+        const int prev = size;
+        for (int j = tid; j < size; j += 256) {
+            ccnt[4 * j] = ccnt[4 * j + 1] = ccnt[4 * j + 2] = ccnt[4 * j + 3] = 0;
+        }
+        if (tid == 0) s_scal[1] = 0;
+        __syncthreads();
+        for (int k = tid; k < n; k += 256) {
+            const int nd = KN[k];
+            if (A.cnt[nd] >= 2) {
+                const uint32_t kk = K[k];
+                const int q = quadrant(key_x(kk), key_y(kk), A.x0[nd], A.y0[nd], A.x1[nd], A.y1[nd]);
+                atomicAdd(&ccnt[4 * nd + q], 1);
+            }
+        }
+        __syncthreads();
+        int g2 = 0;
+        for (int j = tid; j < size; j += 256) {
+            const bool split = A.cnt[j] >= 2;
+            int ne = 0;
+            if (split)
+                for (int q = 0; q < 4; q++) {
+                    ne += ccnt[4 * j + q] > 0;
+                    g2 += ccnt[4 * j + q] > 1;
+                }
+            sa[j] = ne;
+            sb[j] = split ? 0 : 1;
+            sc[j] = ne;
+        }
+        if (g2) atomicAdd(&s_scal[1], g2);
+        __syncthreads();
+        const int C = block_exscan(sa, size, s_tmp);
+        const int T = block_exscan(sb, size, s_tmp);
+        const int G = s_scal[1];
+        const int nsize = C + T;
+        if (nsize > NC) { if (tid == 0) atomicOr(&status[f], kStatusNodeOverflow); finish = true; break; }
+        for (int j = tid; j < size; j += 256) {
+            if (A.cnt[j] >= 2) {
+                const int ne = sc[j];
+                const int P = C - sa[j] - ne;  // block of the children: sum of ne over later split nodes
+                int r = 0;
+                for (int q = 0; q < 4; q++) {
+                    const int cq = ccnt[4 * j + q];
+                    if (cq > 0) {
+                        const int pos = P + (ne - 1 - r);  // pushed front in n1..n4 order
+                        int cx0, cy0, cx1, cy1;
+                        child_box(q, A.x0[j], A.y0[j], A.x1[j], A.y1[j], cx0, cy0, cx1, cy1);
+                        B.x0[pos] = (int16_t)cx0;
+                        B.y0[pos] = (int16_t)cy0;
+                        B.x1[pos] = (int16_t)cx1;
+                        B.y1[pos] = (int16_t)cy1;
+                        B.cnt[pos] = cq;
+                        B.crank[pos] = sa[j] + r;
+                        B.inV[pos] = cq > 1;
+                        ccnt[4 * j + q] = pos;
+                        r++;
+                    }
+                }
+            } else {
+                const int pos = C + sb[j];
+                B.x0[pos] = A.x0[j];
+                B.y0[pos] = A.y0[j];
+                B.x1[pos] = A.x1[j];
+                B.y1[pos] = A.y1[j];
+                B.cnt[pos] = A.cnt[j];
+                B.crank[pos] = A.crank[j];
+                B.inV[pos] = 0;
+                sb[j] = pos;
+            }
+        }
+        __syncthreads();
+        for (int k = tid; k < n; k += 256) {
+            const int nd = KN[k];
+            if (A.cnt[nd] >= 2) {
+                const uint32_t kk = K[k];
+                const int q = quadrant(key_x(kk), key_y(kk), A.x0[nd], A.y0[nd], A.x1[nd], A.y1[nd]);
+                KN[k] = ccnt[4 * nd + q];
+            } else {
+                KN[k] = sb[nd];
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+        size = nsize;
+        if (size >= N || size == prev)
+            finish = true;
+        else if (size + G * 3 > N)
+            final_phase = true;
+    }
+
+    // ---- 4. final phase (cc:888-971)
+    while (!finish && final_phase) {
+        if (++guard > 4096) { if (tid == 0) atomicOr(&status[f], kStatusIterations); break; }
+        const NodeBuf& A = nb[cur];
+        const NodeBuf& B = nb[cur ^ 1];
+        const int prev = size;
+        // processing order: vPrev sorted ascending by (size, address), walked from the back
+        if (tid == 0) s_scal[2] = 0;
+        __syncthreads();
+        int nvloc = 0;
+        for (int j = tid; j < size; j += 256) {
+            sc[j] = -1;  // rank of node j in processing order, -1 if not in vPrev
+            if (A.inV[j]) {
+                nvloc++;
+                const int cj = A.cnt[j], rj = A.crank[j];
+                int r = 0;
+                for (int i = 0; i < size; i++)
+                    if (A.inV[i] && (A.cnt[i] > cj || (A.cnt[i] == cj && A.crank[i] > rj))) r++;
+                sc[j] = r;
+            }
+            ccnt[4 * j] = ccnt[4 * j + 1] = ccnt[4 * j + 2] = ccnt[4 * j + 3] = 0;
+        }
+        if (nvloc) atomicAdd(&s_scal[2], nvloc);
+        __syncthreads();
+        const int nv = s_scal[2];
+        if (nv == 0) { finish = true; break; }
+        for (int j = tid; j < size; j += 256)
+            if (sc[j] >= 0) sa[sc[j]] = j;  // sa[r] = node processed r-th
+        for (int k = tid; k < n; k += 256) {
+            const int nd = KN[k];
+            if (A.inV[nd]) {
+                const uint32_t kk = K[k];
+                const int q = quadrant(key_x(kk), key_y(kk), A.x0[nd], A.y0[nd], A.x1[nd], A.y1[nd]);
+                atomicAdd(&ccnt[4 * nd + q], 1);
+            }
+        }
+        __syncthreads();
+        // sb[r] = ne of the r-th processed node
+        for (int r = tid; r < nv; r += 256) {
+            const int j = sa[r];
+            int ne = 0;
+            for (int q = 0; q < 4; q++) ne += ccnt[4 * j + q] > 0;
+            sb[r] = ne;
+        }
+        __syncthreads();
+        // K = first r where prev + sum_{i<=r}(ne_i - 1) >= N (break after it), else nv-1
+        if (tid == 0) {
+            int s = prev, kk = nv - 1, e = 0;
+            for (int r = 0; r < nv; r++) {
+                s += sb[r] - 1;
+                if (s >= N) { kk = r; break; }
+            }
+            s_scal[3] = kk;
+            for (int r = 0; r <= kk; r++) e += sb[r];
+            s_scal[4] = e;  // children created
+            s_scal[5] = s;  // new size
+        }
+        __syncthreads();
+        const int Kp = s_scal[3], Cc = s_scal[4], nsize = s_scal[5];
+        if (nsize > NC) { if (tid == 0) atomicOr(&status[f], kStatusNodeOverflow); finish = true; break; }
+        // exclusive scan of ne over processing order -> creation ranks / blocks
+        const int E_total = block_exscan(sb, Kp + 1, s_tmp);
+        (void)E_total;
+        // processed flag per node, then position of unprocessed nodes
+        for (int j = tid; j < size; j += 256) {
+            const int r = sc[j];
+            sc[j] = (r >= 0 && r <= Kp) ? r : -1;
+        }
+        __syncthreads();
+        // D_j = number of processed nodes before j (list order)
+        for (int j = tid; j < size; j += 256) sa[j] = sc[j] >= 0 ? 1 : 0;
+        __syncthreads();
+        block_exscan(sa, size, s_tmp);
+        for (int j = tid; j < size; j += 256) {
+            const int r = sc[j];
+            if (r < 0) {
+                const int pos = Cc + j - sa[j];
+                B.x0[pos] = A.x0[j];
+                B.y0[pos] = A.y0[j];
+                B.x1[pos] = A.x1[j];
+                B.y1[pos] = A.y1[j];
+                B.cnt[pos] = A.cnt[j];
+                B.crank[pos] = A.crank[j];
+                B.inV[pos] = 0;
+                sa[j] = pos;
+            } else {
+                int ne = 0;
+                for (int q = 0; q < 4; q++) ne += ccnt[4 * j + q] > 0;
+                const int Er = sb[r];
+                const int Bk = Cc - Er - ne;
+                int rr = 0;
+                for (int q = 0; q < 4; q++) {
+                    const int cq = ccnt[4 * j + q];
+                    if (cq > 0) {
+                        const int pos = Bk + (ne - 1 - rr);
+                        int cx0, cy0, cx1, cy1;
+                        child_box(q, A.x0[j], A.y0[j], A.x1[j], A.y1[j], cx0, cy0, cx1, cy1);
+                        B.x0[pos] = (int16_t)cx0;
+                        B.y0[pos] = (int16_t)cy0;
+                        B.x1[pos] = (int16_t)cx1;
+                        B.y1[pos] = (int16_t)cy1;
+                        B.cnt[pos] = cq;
+                        B.crank[pos] = Er + rr;
+                        B.inV[pos] = cq > 1;
+                        ccnt[4 * j + q] = pos;
+                        rr++;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        for (int k = tid; k < n; k += 256) {
+            const int nd = KN[k];
+            if (sc[nd] >= 0) {
+                const uint32_t kk = K[k];
+                const int q = quadrant(key_x(kk), key_y(kk), A.x0[nd], A.y0[nd], A.x1[nd], A.y1[nd]);
+                KN[k] = ccnt[4 * nd + q];
+            } else {
+                KN[k] = sa[nd];
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+        size = nsize;
+        if (size >= N || size == prev) finish = true;
+    }
+
+    // ---- 5. best key per node (cc:984-1009)
+    for (int j = tid; j < size; j += 256) best[j] = 0ull;
+    __syncthreads();
+    for (int k = tid; k < n; k += 256) {
+        const unsigned long long v = ((unsigned long long)key_resp(K[k]) << 32) | (0xffffffffu - (unsigned)k);
+        atomicMax(&best[KN[k]], v);
+    }
+    __syncthreads();
+    const int outn = size < g.ncap ? size : g.ncap;
+    uint32_t* out = kept + (size_t)f * kept_pf + g.out_off;
+    for (int j = tid; j < outn; j += 256) {
+        const unsigned k = 0xffffffffu - (unsigned)(best[j] & 0xffffffffull);
+        out[j] = K[k];
+    }
+    if (tid == 0) {
+        kept_count[(size_t)f * L + l] = outn;
+        if (size > g.ncap) atomicOr(&status[f], kStatusNodeOverflow);
+    }
+}
+
+// ------------------------------------------------------------------ blur
+
+__device__ __forceinline__ int reflect101(int i, int n) {
+    i = i < 0 ? -i : i;
+    return i >= n ? 2 * n - 2 - i : i;
+}
+
+// GaussianBlur(level ROI clone, 7x7, sigma 2, BORDER_REFLECT_101), OpenCV 3.3.1
+// 8U fixed point: taps {18,34,49,55,49,34,18}, exact integer rows, column
+// (sum + 2^15) >> 16, saturate.  64 x 16 output tile per workgroup.
+__global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                              long long fb, const LevelGeom* __restrict__ lv, int L) {
+    __shared__ uint8_t s_in[22][72];
+    __shared__ int s_row[22][64];
+    const int tile = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    int l = 0;
+    while (l + 1 < L && tile >= lv[l + 1].tile_first) l++;
+    const LevelGeom& g = lv[l];
+    const int t = tile - g.tile_first;
+    const int X0 = (t % g.tiles_x) * 64, Y0 = (t / g.tiles_x) * 16;
+    const uint8_t* img = pyr + (size_t)f * fb + g.off;
+    for (int i = tid; i < 22 * 70; i += 256) {
+        const int r = i / 70, c = i - r * 70;
+        const int gy = reflect101(Y0 + r - 3, g.h), gx = reflect101(X0 + c - 3, g.w);
+        s_in[r][c] = img[(size_t)gy * g.pitch + gx];
+    }
+    __syncthreads();
+    for (int i = tid; i < 22 * 64; i += 256) {
+        const int r = i >> 6, c = i & 63;
+        const uint8_t* p = &s_in[r][c];
+        s_row[r][c] = 18 * (p[0] + p[6]) + 34 * (p[1] + p[5]) + 49 * (p[2] + p[4]) + 55 * p[3];
+    }
+    __syncthreads();
+    uint8_t* out = blur + (size_t)f * fb + g.off;
+    for (int i = tid; i < 16 * 64; i += 256) {
+        const int r = i >> 6, c = i & 63;
+        const int y = Y0 + r, x = X0 + c;
+        if (y < g.h && x < g.w) {
+            const int s = 18 * (s_row[r][c] + s_row[r + 6][c]) + 34 * (s_row[r + 1][c] + s_row[r + 5][c]) +
+                          49 * (s_row[r + 2][c] + s_row[r + 4][c]) + 55 * s_row[r + 3][c];
+            const int v = (s + (1 << 15)) >> 16;
+            out[(size_t)y * g.pitch + x] = (uint8_t)(v > 255 ? 255 : v);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ angle + descriptor
+
+// cv::fastAtan2 (OpenCV 3.3.1), degrees; float ops in the reference order.
+__device__ float fast_atan2(float y, float x) {
+    const float deg = (float)(180.0 / 3.14159265358979323846);
+    const float p1 = 0.9997878412794807f * deg;
+    const float p3 = -0.3258083974640975f * deg;
+    const float p5 = 0.1555786518463281f * deg;
+    const float p7 = -0.04432655554792128f * deg;
+    const float eps = (float)2.2204460492503131e-16;
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = __fdiv_rn(ay, ax + eps);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = __fdiv_rn(ax, ay + eps);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+__device__ __forceinline__ int cv_round(float v) { return (int)rintf(v); }
+
+// One wave per kept keypoint slot: IC_Angle on the level (cc:59-106), rBRIEF on the
+// blurred level (cc:118-172), coordinate scaling (cc:1613-1622), output in the
+// reference's level-major order.
+__global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ pyr,
+                                                  const uint8_t* __restrict__ blur, long long fb,
+                                                  const LevelGeom* __restrict__ lv, int L,
+                                                  const uint32_t* __restrict__ kept, int kept_pf,
+                                                  const int* __restrict__ kept_count,
+                                                  orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                  int cap, int* __restrict__ n_out) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int slot = blockIdx.x * 4 + wave;
+    const int f = blockIdx.y;
+    if (slot >= kept_pf) return;
+    int l = 0;
+    while (l + 1 < L && slot >= lv[l + 1].out_off) l++;
+    const LevelGeom& g = lv[l];
+    const int i = slot - g.out_off;
+    const int* kc = kept_count + (size_t)f * L;
+    int base = 0, total = 0;
+    for (int l2 = 0; l2 < L; l2++) {
+        const int c = kc[l2];
+        if (l2 < l) base += c;
+        total += c;
+    }
+    if (slot == 0 && lane == 0) n_out[f] = total;
+    if (i >= kc[l]) return;
+    const int o = base + i;
+    if (o >= cap) return;
+    const uint32_t key = kept[(size_t)f * kept_pf + slot];
+    const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
+    const int resp = key_resp(key);
+
+    // IC angle: lanes 0..30 own columns u = -15..15 of the circular patch
+    int m10 = 0, m01 = 0;
+    if (lane < 31) {
+        const int u = lane - 15;
+        const int au = u < 0 ? -u : u;
+        const uint8_t* col = pyr + (size_t)f * fb + g.off + (size_t)y * g.pitch + x + u;
+        m10 = u * (int)col[0];
+        for (int v = 1; v <= 15; v++) {
+            if (au <= c_umax[v]) {
+                const int plus = col[(size_t)v * g.pitch];
+                const int minus = col[-(long)v * g.pitch];
+                m10 += u * (plus + minus);
+                m01 += v * (plus - minus);
+            }
+        }
+    }
+#pragma unroll
+    for (int o2 = 32; o2 > 0; o2 >>= 1) {
+        m10 += __shfl_xor(m10, o2);
+        m01 += __shfl_xor(m01, o2);
+    }
+    const float angle = fast_atan2((float)m01, (float)m10);
+
+    // steered BRIEF on the blurred level
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    const float rad = angle * factorPI;
+    const float a = (float)cos((double)rad), b = (float)sin((double)rad);
+    const uint8_t* center = blur + (size_t)f * fb + g.off + (size_t)y * g.pitch + x;
+    const int step = g.pitch;
+    unsigned long long words[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int p = k * 64 + lane;
+        const float x0 = (float)c_pattern[4 * p], y0 = (float)c_pattern[4 * p + 1];
+        const float x1 = (float)c_pattern[4 * p + 2], y1 = (float)c_pattern[4 * p + 3];
+        const int t0 = center[cv_round(x0 * b + y0 * a) * step + cv_round(x0 * a - y0 * b)];
+        const int t1 = center[cv_round(x1 * b + y1 * a) * step + cv_round(x1 * a - y1 * b)];
+        words[k] = __ballot(t0 < t1);
+    }
+    if (lane < 4) {
+        unsigned long long* d = (unsigned long long*)(desc + ((size_t)f * cap + o) * 32);
+        d[lane] = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+    }
+    if (lane == 0) {
+        float fx = (float)x, fy = (float)y;
+        if (l != 0) {
+            fx = fx * g.scale;
+            fy = fy * g.scale;
+        }
+        orbx_keypoint kp;
+        kp.x = fx;
+        kp.y = fy;
+        kp.size = g.kp_size;
+        kp.angle = angle;
+        kp.response = (float)resp;
+        kp.octave = l;
+        kp.class_id = -1;
+        kps[(size_t)f * cap + o] = kp;
+    }
+}
+
+// ------------------------------------------------------------------ host launch
+
+hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, const uint8_t* d_imgs,
+                          size_t frame_pitch, size_t stride, void* kps, uint8_t* desc, int cap,
+                          int* n_per_frame, hipStream_t stream, hipEvent_t* ev) {
+    const int L = plan.L;
+    const long long fb = plan.pyr_frame_bytes;
+    const int ncells = (int)plan.cells.size();
+    if (ev) (void)hipEventRecord(ev[0], stream);
+    (void)hipMemsetAsync(db.status, 0, sizeof(int) * (size_t)batch, stream);
+    {
+        const LevelGeom& g0 = plan.lv[0];
+        dim3 grid((g0.w + 1023) / 1024, g0.h, batch);
+        hipLaunchKernelGGL(k_copy_level0, grid, dim3(256), 0, stream, d_imgs, frame_pitch, stride, g0.w,
+                           db.pyr, fb, g0.pitch);
+        for (int l = 1; l < L; l++) {
+            const LevelGeom& g = plan.lv[l];
+            dim3 gr((g.w + 255) / 256, g.h, batch);
+            hipLaunchKernelGGL(k_resize, gr, dim3(256), 0, stream, db.pyr, fb, db.lv, l, db.rtab);
+        }
+    }
+    if (ev) (void)hipEventRecord(ev[1], stream);
+    {
+        dim3 grid((ncells + 3) / 4, batch);
+        hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), 0, stream, db.pyr, fb, db.lv, db.cells, ncells,
+                           plan.prm.ini_th, plan.prm.min_th, db.slots, plan.slots_per_frame, db.cell_count);
+    }
+    if (ev) (void)hipEventRecord(ev[2], stream);
+    {
+        const int NC = (plan.max_ncap + 63) & ~63;
+        const size_t lds = (size_t)NC * (8 + 16 + 12 + 8 + 8 + 16 + 2);
+        dim3 grid(L, batch);
+        hipLaunchKernelGGL(k_octree, grid, dim3(256), lds, stream, db.lv, L, db.slots, plan.slots_per_frame,
+                           db.cells, db.cell_count, ncells, db.keys, db.key_node, plan.keys_per_frame,
+                           db.kept, plan.kept_per_frame, db.kept_count, db.status, NC);
+    }
+    if (ev) (void)hipEventRecord(ev[3], stream);
+    {
+        dim3 grid(plan.tiles_total, batch);
+        hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, stream, db.pyr, db.blur, fb, db.lv, L);
+    }
+    if (ev) (void)hipEventRecord(ev[4], stream);
+    {
+        dim3 grid((plan.kept_per_frame + 3) / 4, batch);
+        hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, stream, db.pyr, db.blur, fb, db.lv, L, db.kept,
+                           plan.kept_per_frame, db.kept_count, (orbx_keypoint*)kps, desc, cap, n_per_frame);
+    }
+    if (ev) (void)hipEventRecord(ev[5], stream);
+    return hipGetLastError();
+}
+
+}  // namespace orbx

@@ -1,0 +1,213 @@
+// orbx_geometry.cpp -- host-side extraction plan (see orbx_geometry.h).
+// Compiled with -ffp-contract=off: every float expression below restates a
+// reference expression operation by operation.
+#include "orbx_geometry.h"
+
+#include <cmath>
+#include <cstring>
+
+namespace orbx {
+
+static int cv_round(double v) { return (int)std::lrint(v); }   // cvRound: round half to even
+static int cv_roundf(float v) { return (int)std::lrintf(v); }
+
+// ORBextractor::ORBextractor, ORBextractor.cc:438-550
+bool init_params(OrbParams& p, int nfeatures, float scale_factor, int nlevels, int ini, int min) {
+    if (nlevels < 1 || nlevels > kMaxLevels || nfeatures < 0 || !(scale_factor > 1.0f)) return false;
+    p.nfeatures = nfeatures;
+    p.scale_factor = (double)scale_factor;
+    p.nlevels = nlevels;
+    p.ini_th = ini;
+    p.min_th = min;
+    p.scale[0] = 1.0f;
+    p.sigma2[0] = 1.0f;
+    for (int i = 1; i < nlevels; i++) {
+        p.scale[i] = (float)((double)p.scale[i - 1] * p.scale_factor);   // cc:458
+        p.sigma2[i] = p.scale[i] * p.scale[i];                            // cc:460
+    }
+    for (int i = 0; i < nlevels; i++) {
+        p.inv_scale[i] = 1.0f / p.scale[i];                               // cc:468
+        p.inv_sigma2[i] = 1.0f / p.sigma2[i];                             // cc:469
+    }
+    const float factor = (float)(1.0f / p.scale_factor);                   // cc:480
+    float desired = (float)nfeatures * (1 - factor) /
+                    (1 - (float)std::pow((double)factor, (double)nlevels));  // cc:485
+    int sum = 0;
+    for (int level = 0; level < nlevels - 1; level++) {                    // cc:490-498
+        p.features[level] = cv_roundf(desired);
+        sum += p.features[level];
+        desired *= factor;
+    }
+    p.features[nlevels - 1] = nfeatures - sum > 0 ? nfeatures - sum : 0;  // cc:500
+    // umax, cc:519-549
+    const int vmax = (int)std::floor(15 * std::sqrt(2.f) / 2 + 1);
+    const int vmin = (int)std::ceil(15 * std::sqrt(2.f) / 2);
+    const double hp2 = 15 * 15;
+    int v, v0;
+    for (v = 0; v <= vmax; ++v) p.umax[v] = cv_round(std::sqrt(hp2 - v * v));
+    for (v = 15, v0 = 0; v >= vmin; --v) {
+        while (p.umax[v0] == p.umax[v0 + 1]) ++v0;
+        p.umax[v] = v0;
+        ++v0;
+    }
+    return true;
+}
+
+// OpenCV 3.3.1 resize(INTER_LINEAR) coefficient tables for CV_8U (11-bit fixed point).
+static void resize_tables(int sw, int sh, int dw, int dh, int16_t* xtab, int16_t* ytab) {
+    const double inv_scale_x = (double)dw / sw, inv_scale_y = (double)dh / sh;
+    const double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
+    int xmax = dw;
+    std::vector<int> sxs(dw);
+    std::vector<float> fxs(dw);
+    for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = (int)std::floor(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx + 1 >= sw) {
+            if (dx < xmax) xmax = dx;
+            if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+        }
+        sxs[dx] = sx;
+        fxs[dx] = fx;
+    }
+    for (int dx = 0; dx < dw; dx++) {
+        int16_t* t = xtab + 4 * dx;
+        if (dx < xmax) {
+            t[0] = (int16_t)sxs[dx];
+            t[1] = (int16_t)(sxs[dx] + 1);
+            t[2] = (int16_t)cv_roundf((1.f - fxs[dx]) * 2048);
+            t[3] = (int16_t)cv_roundf(fxs[dx] * 2048);
+        } else {  // HResizeLinear tail: D = S[sx] * INTER_RESIZE_COEF_SCALE
+            t[0] = (int16_t)sxs[dx];
+            t[1] = (int16_t)sxs[dx];
+            t[2] = 2048;
+            t[3] = 0;
+        }
+    }
+    for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = (int)std::floor(fy);
+        fy -= sy;
+        int16_t* t = ytab + 4 * dy;
+        auto clip = [&](int y) { return y < 0 ? 0 : (y >= sh ? sh - 1 : y); };
+        t[0] = (int16_t)clip(sy);
+        t[1] = (int16_t)clip(sy + 1);
+        t[2] = (int16_t)cv_roundf((1.f - fy) * 2048);
+        t[3] = (int16_t)cv_roundf(fy * 2048);
+    }
+}
+
+bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
+    plan = Plan();
+    plan.prm = prm;
+    plan.W = W;
+    plan.H = H;
+    plan.L = prm.nlevels;
+    if (W <= 0 || H <= 0) { plan.why = "empty image"; return false; }
+    long long off = 0;
+    int cell_first = 0, key_off = 0, out_off = 0, tile_first = 0, slot_off = 0;
+    int prev_w = W, prev_h = H;
+    for (int l = 0; l < prm.nlevels; l++) {
+        LevelGeom& g = plan.lv[l];
+        std::memset(&g, 0, sizeof(g));
+        const float s = prm.inv_scale[l];
+        g.w = cv_roundf((float)W * s);                 // cc:1643
+        g.h = cv_roundf((float)H * s);
+        if (g.w < 2 * kEdge + 8 || g.h < 2 * kEdge + 8) { plan.why = "pyramid level too small"; return false; }
+        if (g.w - 2 * kMinBorder >= 4096 || g.h - 2 * kMinBorder >= 4096) { plan.why = "frame too large"; return false; }
+        g.pitch = (g.w + 63) & ~63;
+        g.off = off;
+        off += (long long)g.pitch * g.h;
+        off = (off + 255) & ~255LL;
+        g.scale = prm.scale[l];
+        g.kp_size = (float)(int)(31 * prm.scale[l]);  // cc:1140
+        g.N = prm.features[l];
+
+        // FAST cell grid, cc:1025-1085
+        const int minBorderX = kMinBorder, minBorderY = kMinBorder;
+        const int maxBorderX = g.w - kEdge + 3, maxBorderY = g.h - kEdge + 3;
+        const float width = (float)(maxBorderX - minBorderX);
+        const float height = (float)(maxBorderY - minBorderY);
+        const int nCols = (int)(width / 30.f);
+        const int nRows = (int)(height / 30.f);
+        if (nCols <= 0 || nRows <= 0) { plan.why = "level narrower than one FAST cell"; return false; }
+        const int wCell = (int)std::ceil(width / nCols);
+        const int hCell = (int)std::ceil(height / nRows);
+        g.cell_first = cell_first;
+        g.key_off = key_off;
+        int level_cap = 0;
+        for (int i = 0; i < nRows; i++) {
+            const float iniY = (float)(minBorderY + i * hCell);
+            float maxY = iniY + hCell + 6;
+            if (iniY >= maxBorderY - 3) continue;
+            if (maxY > maxBorderY) maxY = (float)maxBorderY;
+            for (int j = 0; j < nCols; j++) {
+                const float iniX = (float)(minBorderX + j * wCell);
+                float maxX = iniX + wCell + 6;
+                if (iniX >= maxBorderX - 6) continue;
+                if (maxX > maxBorderX) maxX = (float)maxBorderX;
+                CellGeom c{};
+                c.level = l;
+                c.x0 = (int)iniX;
+                c.y0 = (int)iniY;
+                c.cols = (int)maxX - c.x0;
+                c.rows = (int)maxY - c.y0;
+                const int wc = c.cols > 6 ? c.cols - 6 : 0, wr = c.rows > 6 ? c.rows - 6 : 0;
+                if (wc > kCellMax || wr > kCellMax) { plan.why = "FAST cell wider than 64 px"; return false; }
+                c.slot_off = slot_off;
+                c.slot_cap = ((wc + 1) / 2) * ((wr + 1) / 2);
+                slot_off += c.slot_cap;
+                level_cap += c.slot_cap;
+                plan.cells.push_back(c);
+            }
+        }
+        g.ncells = (int)plan.cells.size() - cell_first;
+        cell_first = (int)plan.cells.size();
+        g.key_cap = level_cap;
+        key_off += level_cap;
+        if (level_cap > plan.max_key_cap) plan.max_key_cap = level_cap;
+
+        // octree roots, cc:674-699
+        const int minX = minBorderX, maxX = maxBorderX, minY = minBorderY, maxY = maxBorderY;
+        g.nIni = (int)std::round((float)(maxX - minX) / (maxY - minY));
+        if (g.nIni < 1 || g.nIni > kMaxIni) { plan.why = "aspect ratio outside octree support"; return false; }
+        g.hX = (float)(maxX - minX) / g.nIni;
+        for (int i = 0; i <= g.nIni; i++) g.ini_x0[i] = (int)(g.hX * (float)i);
+        g.height_rel = maxY - minY;
+        int ncap = g.N + 4;
+        if (4 * g.nIni + 4 > ncap) ncap = 4 * g.nIni + 4;
+        g.ncap = ncap;
+        g.out_off = out_off;
+        out_off += ncap;
+        if (ncap > plan.max_ncap) plan.max_ncap = ncap;
+
+        // blur tiles (64 x 16 outputs)
+        g.tiles_x = (g.w + 63) / 64;
+        g.tiles_y = (g.h + 15) / 16;
+        g.tile_first = tile_first;
+        tile_first += g.tiles_x * g.tiles_y;
+
+        // resize tables
+        if (l > 0) {
+            g.xtab_off = (int)plan.rtab.size();
+            plan.rtab.resize(plan.rtab.size() + 4 * (size_t)g.w);
+            g.ytab_off = (int)plan.rtab.size();
+            plan.rtab.resize(plan.rtab.size() + 4 * (size_t)g.h);
+            resize_tables(prev_w, prev_h, g.w, g.h, plan.rtab.data() + g.xtab_off, plan.rtab.data() + g.ytab_off);
+        }
+        prev_w = g.w;
+        prev_h = g.h;
+    }
+    plan.pyr_frame_bytes = off;
+    plan.slots_per_frame = slot_off;
+    plan.keys_per_frame = key_off;
+    plan.kept_per_frame = out_off;
+    plan.tiles_total = tile_first;
+    if (plan.rtab.empty()) plan.rtab.push_back(0);
+    plan.ok = true;
+    return true;
+}
+
+}  // namespace orbx

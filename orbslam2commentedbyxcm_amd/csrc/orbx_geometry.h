@@ -1,0 +1,90 @@
+// orbx_geometry.h -- host-side plan of one (params, W, H) extraction configuration.
+//
+// Everything that depends only on the ORB parameters and the frame size is computed
+// once on the host, with the reference's exact float/double/int conversions, and
+// uploaded as small tables: level sizes (ORBextractor.cc:1641-1643), the FAST cell
+// grid (cc:1025-1085), octree root nodes (cc:674-699), resize coefficient tables
+// (OpenCV 3.3.1 resize INTER_LINEAR), per-level budgets and scales (cc:438-500).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace orbx {
+
+constexpr int kMaxLevels = 32;
+constexpr int kEdge = 19;        // EDGE_THRESHOLD, ORBextractor.cc:46
+constexpr int kMinBorder = 16;   // EDGE_THRESHOLD - 3, ORBextractor.cc:1032
+constexpr int kMaxIni = 16;      // octree root nodes supported per level
+constexpr int kCellMax = 64;     // max detection-window width/height of a FAST cell
+
+// Parameters + derived per-level members (ORBextractor.h:204-219).
+struct OrbParams {
+    int nfeatures = 1000;
+    double scale_factor = 1.2;   // double member, ORBextractor.h:207
+    int nlevels = 8;
+    int ini_th = 20;
+    int min_th = 7;
+    float scale[kMaxLevels], inv_scale[kMaxLevels], sigma2[kMaxLevels], inv_sigma2[kMaxLevels];
+    int features[kMaxLevels];
+    int umax[16];
+};
+bool init_params(OrbParams& p, int nfeatures, float scale_factor, int nlevels, int ini, int min);
+
+// One level of one frame, as laid out on the device.
+struct LevelGeom {
+    int w, h;              // ROI size
+    int pitch;             // row pitch (bytes) of this level in the pyramid/blur buffers
+    int pad0;
+    long long off;         // byte offset of the level inside one frame's pyramid block
+    // FAST cells
+    int cell_first, ncells;
+    // candidates (per-frame key region)
+    int key_off, key_cap;
+    // octree
+    int N;                 // mnFeaturesPerLevel[level]
+    int nIni;
+    float hX;
+    int ncap;              // node capacity = max kept keypoints
+    int out_off;           // offset of this level's kept slots in a frame's kept array
+    int ini_x0[kMaxIni + 1];  // root node x boundaries: node i = [ini_x0[i], ini_x0[i+1])
+    int height_rel;        // maxY - minY (root node bottom)
+    // output
+    float scale;           // mvScaleFactor[level]
+    float kp_size;         // (float)(int)(PATCH_SIZE * scale)
+    // blur tiles
+    int tile_first, tiles_x, tiles_y;
+    // resize tables (levels >= 1)
+    int xtab_off, ytab_off;  // offsets (in int16 units) into the resize table buffer
+};
+
+// One FAST cell: sub-image [y0, y0+rows) x [x0, x0+cols) of its level ROI.
+struct CellGeom {
+    int level;
+    int x0, y0, cols, rows;
+    int slot_off;          // offset of this cell's candidate slots in the frame's slot array
+    int slot_cap;
+    int pad;
+};
+
+struct Plan {
+    int W = 0, H = 0, L = 0;
+    OrbParams prm;
+    LevelGeom lv[kMaxLevels];
+    std::vector<CellGeom> cells;
+    std::vector<int16_t> rtab;      // resize tables: per level xtab (w*4) then ytab (h*4)
+    long long pyr_frame_bytes = 0;  // one frame's pyramid block (levels 0..L-1)
+    int slots_per_frame = 0;        // candidate slots per frame (sum of cell caps)
+    int keys_per_frame = 0;         // candidate key capacity per frame
+    int kept_per_frame = 0;         // sum of ncap
+    int tiles_total = 0;            // blur tiles per frame
+    int max_ncap = 0;
+    int max_key_cap = 0;
+    bool ok = false;
+    const char* why = nullptr;
+};
+
+bool make_plan(Plan& plan, const OrbParams& prm, int W, int H);
+
+}  // namespace orbx

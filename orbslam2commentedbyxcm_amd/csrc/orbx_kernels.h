@@ -1,0 +1,53 @@
+// orbx_kernels.h -- launch interface of the extraction kernels (orbx_extract.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "orbx.h"
+#include "orbx_geometry.h"
+
+namespace orbx {
+
+// Device-resident buffers for one extractor configuration and batch capacity.
+struct DeviceBuffers {
+    int batch_cap = 0;
+    LevelGeom* lv = nullptr;         // [L]
+    CellGeom* cells = nullptr;       // [ncells]
+    int16_t* rtab = nullptr;         // resize tables
+    uint8_t* pyr = nullptr;          // [B][pyr_frame_bytes] image pyramid (level ROIs)
+    uint8_t* blur = nullptr;         // [B][pyr_frame_bytes] Gaussian-blurred levels
+    uint32_t* slots = nullptr;       // [B][slots_per_frame] packed FAST keypoints per cell
+    int* cell_count = nullptr;       // [B][ncells]
+    uint32_t* keys = nullptr;        // [B][keys_per_frame] packed candidates per level
+    int* key_node = nullptr;         // [B][keys_per_frame] octree node of each candidate
+    uint32_t* kept = nullptr;        // [B][kept_per_frame] kept keypoints (octree list order)
+    int* kept_count = nullptr;       // [B][L]
+    int* status = nullptr;           // [B] error flags
+};
+
+// Kernel status bits (DeviceBuffers::status)
+enum : int { kStatusNodeOverflow = 1, kStatusIterations = 2 };
+
+constexpr int kStages = 6;
+extern const char* const kStageNames[kStages];
+
+// Pattern + umax into __constant__ memory (idempotent).
+hipError_t upload_constants(const OrbParams& prm);
+
+// Enqueue the whole extraction of `batch` device frames on `stream`.
+// kps: orbx_keypoint[batch*cap], desc: uint8[batch*cap*32], n_per_frame: int[batch].
+// ev (nullable) holds kStages+1 events recorded between the stages.
+hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, const uint8_t* d_imgs,
+                          size_t frame_pitch, size_t stride, void* kps, uint8_t* desc, int cap,
+                          int* n_per_frame, hipStream_t stream, hipEvent_t* ev);
+
+// dist[i*nb+j] = Hamming(a_i, b_j)
+hipError_t launch_hamming_matrix(const uint8_t* a, int na, const uint8_t* b, int nb, int32_t* dist,
+                                 hipStream_t stream);
+
+hipError_t launch_window_match(const uint8_t* qdesc, int nq, const uint8_t* tdesc, const int32_t* tlevel,
+                               const int32_t* cand_off, const int32_t* cand, int tie_last,
+                               int32_t* best_idx, int32_t* best_dist, int32_t* best_level,
+                               int32_t* second_dist, int32_t* second_level, hipStream_t stream);
+
+}  // namespace orbx

@@ -1,0 +1,153 @@
+"""ORBextractor -- host-side mirror of ORB_SLAM2::ORBextractor over liborbx.so.
+
+Same constructor arguments, call operator, getters and public ``mvImagePyramid`` as
+include/ORBextractor.h:76-220; every call runs on the MI355X through the C ABI.
+Keypoints come back as a structured array with cv::KeyPoint's fields
+(x, y, size, angle, response, octave, class_id) in the reference order
+(level-major, octree-list order within a level, ORBextractor.cc:1573-1628).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+
+class ORBextractor:
+    HARRIS_SCORE = 0
+    FAST_SCORE = 1
+
+    def __init__(self, nfeatures: int, scaleFactor: float, nlevels: int, iniThFAST: int, minThFAST: int,
+                 device: int = 0):
+        self._h = None
+        prm = L.ExtractorParams(int(nfeatures), float(scaleFactor), int(nlevels), int(iniThFAST), int(minThFAST))
+        h = C.c_void_p()
+        L.check(L.lib().orbx_extractor_create(C.byref(prm), int(device), C.byref(h)))
+        self._h = h
+        self.nfeatures = int(nfeatures)
+        self.scaleFactor = float(scaleFactor)
+        self.nlevels = int(nlevels)
+        self.iniThFAST = int(iniThFAST)
+        self.minThFAST = int(minThFAST)
+        self.device = int(device)
+        self._last_batch = 0
+        self._pyr_cache = None
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            L.lib().orbx_extractor_destroy(self._h)
+            self._h = None
+
+    # ---- getters (ORBextractor.h:119-159)
+    def _levels(self):
+        n = self.nlevels
+        arrs = [np.zeros(n, dtype=np.float32) for _ in range(4)]
+        ptrs = [a.ctypes.data_as(C.POINTER(C.c_float)) for a in arrs]
+        L.check(L.lib().orbx_extractor_levels(self._h, None, *ptrs))
+        return arrs
+
+    def GetLevels(self) -> int:
+        return self.nlevels
+
+    def GetScaleFactor(self) -> float:
+        return self.scaleFactor
+
+    def GetScaleFactors(self) -> np.ndarray:
+        return self._levels()[0]
+
+    def GetInverseScaleFactors(self) -> np.ndarray:
+        return self._levels()[1]
+
+    def GetScaleSigmaSquares(self) -> np.ndarray:
+        return self._levels()[2]
+
+    def GetInverseScaleSigmaSquares(self) -> np.ndarray:
+        return self._levels()[3]
+
+    def features_per_level(self) -> np.ndarray:
+        out = np.zeros(self.nlevels, dtype=np.int32)
+        L.check(L.lib().orbx_extractor_features_per_level(self._h, out.ctypes.data_as(C.POINTER(C.c_int))))
+        return out
+
+    def max_keypoints(self, width: int, height: int) -> int:
+        n = C.c_int()
+        L.check(L.lib().orbx_extractor_max_keypoints(self._h, width, height, C.byref(n)))
+        return n.value
+
+    # ---- operator() (ORBextractor.cc:1513-1629)
+    def __call__(self, image: np.ndarray, mask=None):
+        """Returns (keypoints, descriptors); an empty image returns (None, None) untouched."""
+        img = np.asarray(image)
+        if img.size == 0:
+            return None, None
+        if img.dtype != np.uint8 or img.ndim != 2:
+            raise TypeError("ORBextractor expects a single-channel uint8 image (CV_8UC1)")
+        kps, desc, n = self.extract_batch(img[None])
+        return kps[0][: n[0]].copy(), desc[0][: n[0]].copy()
+
+    def extract_batch(self, images: np.ndarray, cap: int | None = None):
+        """B host frames (B, H, W) uint8 -> (kps[B, cap], desc[B, cap, 32], n[B])."""
+        imgs = np.asarray(images)
+        if imgs.dtype != np.uint8 or imgs.ndim != 3:
+            raise TypeError("expected (B, H, W) uint8 frames")
+        B, H, W = imgs.shape
+        cap = cap or self.max_keypoints(W, H)
+        kps = np.zeros((B, cap), dtype=L.KEYPOINT_DTYPE)
+        desc = np.zeros((B, cap, 32), dtype=np.uint8)
+        n = np.zeros(B, dtype=np.int32)
+        rows = [np.ascontiguousarray(imgs[b]) for b in range(B)]
+        ptrs = (C.POINTER(C.c_uint8) * B)(*[L.u8ptr(r) for r in rows])
+        rc = L.lib().orbx_extract_batch(self._h, B, ptrs, W, H, W, kps.ctypes.data, L.u8ptr(desc), cap,
+                                        n.ctypes.data_as(C.POINTER(C.c_int)))
+        L.check(rc)
+        self._last_batch = B
+        self._pyr_cache = None
+        return kps, desc, n
+
+    def extract_batch_device(self, frames, kps_out, desc_out, n_out, stream=None):
+        """Device-resident path.  frames: CUDA/HIP uint8 tensor (B, H, W) (any object with
+        data_ptr()/shape/stride()); outputs: preallocated device tensors
+        kps_out (B, cap, 7) 4-byte words, desc_out (B, cap, 32) uint8, n_out (B,) int32.
+        Enqueued on `stream` (a torch.cuda.Stream or raw handle) or the extractor's own."""
+        B, H, W = frames.shape
+        cap = desc_out.shape[1]
+        s = None
+        if stream is not None:
+            s = C.c_void_p(getattr(stream, "cuda_stream", stream))
+        rc = L.lib().orbx_extract_batch_device(self._h, B, C.c_void_p(frames.data_ptr()), frames.stride(0), W, H,
+                                               frames.stride(1), C.c_void_p(kps_out.data_ptr()),
+                                               C.c_void_p(desc_out.data_ptr()), cap, C.c_void_p(n_out.data_ptr()), s)
+        L.check(rc)
+        self._last_batch = B
+        self._pyr_cache = None
+
+    def stream_handle(self) -> int:
+        return L.lib().orbx_extractor_stream(self._h) or 0
+
+    def set_timing(self, enable: bool = True) -> None:
+        L.check(L.lib().orbx_extractor_set_timing(self._h, 1 if enable else 0))
+
+    def stage_times(self) -> dict:
+        names = (C.c_char_p * 16)()
+        ms = (C.c_float * 16)()
+        n = C.c_int()
+        L.check(L.lib().orbx_extractor_stage_times(self._h, 16, names, ms, C.byref(n)))
+        return {names[i].decode(): float(ms[i]) for i in range(n.value)}
+
+    # ---- mvImagePyramid (ORBextractor.h:162)
+    def pyramid_level(self, level: int, frame: int = 0) -> np.ndarray:
+        w, h = C.c_int(), C.c_int()
+        L.check(L.lib().orbx_pyramid_level(self._h, frame, level, None, 0, C.byref(w), C.byref(h)))
+        out = np.zeros((h.value, w.value), dtype=np.uint8)
+        L.check(L.lib().orbx_pyramid_level(self._h, frame, level, L.u8ptr(out), w.value, None, None))
+        return out
+
+    @property
+    def mvImagePyramid(self):
+        if self._last_batch == 0:
+            return []
+        if self._pyr_cache is None:
+            self._pyr_cache = [self.pyramid_level(lv) for lv in range(self.nlevels)]
+        return self._pyr_cache

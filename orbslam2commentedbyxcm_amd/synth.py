@@ -1,0 +1,80 @@
+"""Seeded synthetic grayscale frames.
+
+No TUM/KITTI/EuRoC data exists on either machine, so every test and the bench use
+these frames.  A frame is a u8 canvas of random rotated rectangles and ellipses,
+plus an 8-px-lattice value-noise texture (+-24, bilinear) and +-6 per-pixel noise,
+saturated.  That is corner-rich enough to exceed the per-level budgets at
+iniThFAST=20 while leaving flat cells that exercise the minThFAST fallback
+(ORBextractor.cc:1091-1104).
+
+Stereo pairs: the right image is the left shifted by a piecewise-constant integer
+disparity field (32x32 blocks, d in [0, max_disp]).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+__all__ = ["frame", "frames", "stereo_pair"]
+
+
+def _rng(seed: int) -> np.random.Generator:
+    return np.random.Generator(np.random.PCG64(int(seed)))
+
+
+def frame(seed: int, width: int = 640, height: int = 480, n_shapes: int = 200) -> np.ndarray:
+    """One synthetic frame, shape (height, width), dtype uint8, C-contiguous."""
+    g = _rng(seed)
+    img = np.full((height, width), g.integers(0, 256), dtype=np.int32)
+    yy, xx = np.mgrid[0:height, 0:width]
+    for _ in range(n_shapes):
+        cx = g.integers(0, width)
+        cy = g.integers(0, height)
+        a = g.integers(6, max(8, width // 8))
+        b = g.integers(6, max(8, height // 8))
+        th = g.uniform(0.0, np.pi)
+        level = g.integers(0, 256)
+        kind = g.integers(0, 2)
+        r = int(np.ceil(np.hypot(a, b))) + 1
+        x0, x1 = max(0, cx - r), min(width, cx + r + 1)
+        y0, y1 = max(0, cy - r), min(height, cy + r + 1)
+        if x0 >= x1 or y0 >= y1:
+            continue
+        dx = xx[y0:y1, x0:x1] - cx
+        dy = yy[y0:y1, x0:x1] - cy
+        c, s = np.cos(th), np.sin(th)
+        u = dx * c + dy * s
+        v = -dx * s + dy * c
+        if kind == 0:
+            m = (np.abs(u) <= a) & (np.abs(v) <= b)
+        else:
+            m = (u / a) ** 2 + (v / b) ** 2 <= 1.0
+        img[y0:y1, x0:x1][m] = level
+    # value-noise texture: +-24 on an 8-px lattice, bilinear (integer arithmetic)
+    gh, gw = height // 8 + 2, width // 8 + 2
+    lat = g.integers(-24, 25, size=(gh, gw)).astype(np.int32)
+    iy, fy = yy // 8, yy % 8
+    ix, fx = xx // 8, xx % 8
+    tex = (lat[iy, ix] * (8 - fx) * (8 - fy) + lat[iy, ix + 1] * fx * (8 - fy)
+           + lat[iy + 1, ix] * (8 - fx) * fy + lat[iy + 1, ix + 1] * fx * fy) // 64
+    img = img + tex + g.integers(-6, 7, size=(height, width))
+    return np.ascontiguousarray(np.clip(img, 0, 255).astype(np.uint8))
+
+
+def frames(n: int, width: int = 640, height: int = 480, first_seed: int = 0) -> np.ndarray:
+    """Batch of n frames, shape (n, height, width) uint8; frame i uses seed first_seed+i."""
+    out = np.empty((n, height, width), dtype=np.uint8)
+    for i in range(n):
+        out[i] = frame(first_seed + i, width, height)
+    return out
+
+
+def stereo_pair(seed: int, width: int = 1241, height: int = 376, max_disp: int = 64):
+    """(left, right, disparity) with right(x) = left(x + d) for a blockwise d field."""
+    left = frame(seed, width, height)
+    g = _rng(seed + 1_000_003)
+    bh, bw = (height + 31) // 32, (width + 31) // 32
+    dblk = g.integers(0, max_disp + 1, size=(bh, bw))
+    disp = np.repeat(np.repeat(dblk, 32, axis=0), 32, axis=1)[:height, :width]
+    xs = np.minimum(np.arange(width)[None, :] + disp, width - 1)
+    right = np.take_along_axis(left, xs, axis=1)
+    return left, np.ascontiguousarray(right), disp.astype(np.int32)
