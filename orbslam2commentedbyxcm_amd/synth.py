@@ -60,11 +60,24 @@ def frame(seed: int, width: int = 640, height: int = 480, n_shapes: int = 200) -
     return np.ascontiguousarray(np.clip(img, 0, 255).astype(np.uint8))
 
 
-def frames(n: int, width: int = 640, height: int = 480, first_seed: int = 0) -> np.ndarray:
-    """Batch of n frames, shape (n, height, width) uint8; frame i uses seed first_seed+i."""
+def _frame_args(args):
+    return frame(*args)
+
+
+def frames(n: int, width: int = 640, height: int = 480, first_seed: int = 0, workers: int = 1) -> np.ndarray:
+    """Batch of n frames, shape (n, height, width) uint8; frame i uses seed first_seed+i.
+
+    workers > 1 renders in a process pool (call it before the process touches the GPU)."""
     out = np.empty((n, height, width), dtype=np.uint8)
-    for i in range(n):
-        out[i] = frame(first_seed + i, width, height)
+    args = [(first_seed + i, width, height) for i in range(n)]
+    if workers > 1 and n > 1:
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(min(workers, n)) as pool:
+            for i, f in enumerate(pool.imap(_frame_args, args, chunksize=4)):
+                out[i] = f
+    else:
+        for i, a in enumerate(args):
+            out[i] = frame(*a)
     return out
 
 
