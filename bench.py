@@ -54,12 +54,12 @@ def stage_bytes(W, H, n_kps, nlevels=8, scale=1.2):
     return {
         # read input, write every level (level 0 copied), read levels 0..L-2 as resize sources
         "pyramid": A[0] + P + (P - A[-1]),
-        # read every level once (FAST ring + NMS from LDS), write ~4 B per candidate (small)
-        "fast_cells": P,
+        # read every level once, write its Gaussian-blurred copy and its FAST strength map
+        "score_blur": 3 * P,
+        # read the strength map of every FAST detection window once
+        "fast_cells": sum((w - 38) * (h - 38) for (w, h) in level_areas(W, H, nlevels, scale)),
         # candidates in, kept keypoints out: 4 B each, ~3x n_kps candidates per level budget
         "octree": 8 * n_kps,
-        # read every level, write the blurred level
-        "blur": 2 * P,
         # 28 B keypoint + 32 B descriptor out per keypoint (patch reads are L2 hits)
         "describe": 60 * n_kps,
         # SURVEY.md §8(d) canonical whole-pipeline figure

@@ -71,7 +71,7 @@ struct orbx_extractor {
 namespace {
 
 void free_buffers(DeviceBuffers& db) {
-    void* ptrs[] = {db.lv, db.cells, db.rtab, db.pyr, db.blur, db.slots, db.cell_count,
+    void* ptrs[] = {db.lv, db.cells, db.rtab, db.pyr, db.blur, db.score, db.slots, db.cell_count,
                     db.keys, db.key_node, db.kept, db.kept_count, db.status};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -100,6 +100,7 @@ int prepare(orbx_extractor* ex, int W, int H, int batch) {
     HIP_TRY(dalloc(&db.rtab, p.rtab.size()));
     HIP_TRY(dalloc(&db.pyr, B * (size_t)p.pyr_frame_bytes));
     HIP_TRY(dalloc(&db.blur, B * (size_t)p.pyr_frame_bytes));
+    HIP_TRY(dalloc(&db.score, B * (size_t)p.pyr_frame_bytes));
     HIP_TRY(dalloc(&db.slots, B * (size_t)p.slots_per_frame));
     HIP_TRY(dalloc(&db.cell_count, B * p.cells.size()));
     HIP_TRY(dalloc(&db.keys, B * (size_t)p.keys_per_frame));

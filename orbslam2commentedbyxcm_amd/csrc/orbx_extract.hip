@@ -16,7 +16,7 @@
 
 namespace orbx {
 
-const char* const kStageNames[kStages] = {"pyramid", "fast_cells", "octree", "blur", "describe", "total"};
+const char* const kStageNames[kStages] = {"pyramid", "score_blur", "fast_cells", "octree", "describe", "total"};
 
 __constant__ int8_t c_pattern[1024];
 __constant__ int c_umax[16];
@@ -40,87 +40,194 @@ __device__ __forceinline__ void wave_lds_fence() {
 // ------------------------------------------------------------------ pyramid
 
 // Level 0 = the input frame copied into the pyramid block (ORBextractor.cc:1688-1690;
-// the REFLECT_101 border is never read by extraction).
+// the REFLECT_101 border is never read by extraction).  16 bytes per lane when the
+// rows are 16-byte aligned.
 __global__ __launch_bounds__(256) void k_copy_level0(const uint8_t* __restrict__ src, size_t frame_pitch,
-                                                     size_t stride, int w, uint8_t* __restrict__ pyr,
-                                                     long long fb, int pitch) {
-    const int f = blockIdx.z, y = blockIdx.y;
-    const int x = (blockIdx.x * 256 + threadIdx.x) * 4;
-    const uint8_t* s = src + (size_t)f * frame_pitch + (size_t)y * stride;
-    uint8_t* d = pyr + (size_t)f * fb + (size_t)y * pitch;
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-        if (x + k < w) d[x + k] = s[x + k];
+                                                     size_t stride, int w, int h, uint8_t* __restrict__ pyr,
+                                                     long long fb, int pitch, int vec16) {
+    const int f = blockIdx.y;
+    const uint8_t* s = src + (size_t)f * frame_pitch;
+    uint8_t* d = pyr + (size_t)f * fb;
+    if (vec16) {
+        const int per_row = w >> 4;
+        const int total = per_row * h;
+        for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+            const int y = i / per_row, x = (i - y * per_row) << 4;
+            *(uint4*)(d + (size_t)y * pitch + x) = *(const uint4*)(s + (size_t)y * stride + x);
+        }
+    } else {
+        const int total = w * h;
+        for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+            const int y = i / w, x = i - y * w;
+            d[(size_t)y * pitch + x] = s[(size_t)y * stride + x];
+        }
+    }
 }
+
+constexpr int kRszTW = 64, kRszTH = 16;           // resize output tile
+constexpr int kRszSW = 192, kRszSH = 48;          // max staged source region
 
 // cv::resize(level l-1 ROI, level l, INTER_LINEAR), OpenCV 3.3.1 fixed point:
 // h = S[sx0]*a0 + S[sx1]*a1 (exact), dst = ((b0*(h0>>4))>>16 + (b1*(h1>>4))>>16 + 2)>>2.
+// One 64x16 output tile per workgroup; its source rows/columns are staged in LDS.
 __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, long long fb,
                                                 const LevelGeom* __restrict__ lv, int l,
                                                 const int16_t* __restrict__ rtab) {
+    __shared__ uint8_t s_src[kRszSH][kRszSW];
     const LevelGeom& g = lv[l];
     const LevelGeom& p = lv[l - 1];
-    const int f = blockIdx.z, dy = blockIdx.y;
-    const int dx = blockIdx.x * 256 + threadIdx.x;
-    if (dx >= g.w) return;
-    const int16_t* yt = rtab + g.ytab_off + 4 * dy;
-    const int16_t* xt = rtab + g.xtab_off + 4 * dx;
-    const uint8_t* base = pyr + (size_t)f * fb + p.off;
-    const uint8_t* S0 = base + (size_t)yt[0] * p.pitch;
-    const uint8_t* S1 = base + (size_t)yt[1] * p.pitch;
-    const int a0 = xt[2], a1 = xt[3];
-    const int h0 = S0[xt[0]] * a0 + S0[xt[1]] * a1;
-    const int h1 = S1[xt[0]] * a0 + S1[xt[1]] * a1;
-    const int b0 = yt[2], b1 = yt[3];
-    int v = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
-    v = v < 0 ? 0 : (v > 255 ? 255 : v);
-    pyr[(size_t)f * fb + g.off + (size_t)dy * g.pitch + dx] = (uint8_t)v;
+    const int f = blockIdx.z, X0 = blockIdx.x * kRszTW, Y0 = blockIdx.y * kRszTH;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int16_t* xt = rtab + g.xtab_off;
+    const int16_t* yt = rtab + g.ytab_off;
+    const int xe = min(X0 + kRszTW, g.w) - 1, ye = min(Y0 + kRszTH, g.h) - 1;
+    const int sx_lo = xt[4 * X0], sx_hi = xt[4 * xe + 1];
+    const int sy_lo = yt[4 * Y0], sy_hi = yt[4 * ye + 1];
+    const int ncols = sx_hi - sx_lo + 1, nrows = sy_hi - sy_lo + 1;
+    const uint8_t* base = pyr + (size_t)f * fb + p.off + (size_t)sy_lo * p.pitch + sx_lo;
+    for (int r = wave; r < nrows; r += 4)
+        for (int c = lane; c < ncols; c += 64) s_src[r][c] = base[(size_t)r * p.pitch + c];
+    __syncthreads();
+    const int ry = tid >> 4, cx = (tid & 15) * 4;
+    const int dy = Y0 + ry;
+    if (dy >= g.h) return;
+    const int r0 = yt[4 * dy] - sy_lo, r1 = yt[4 * dy + 1] - sy_lo;
+    const int b0 = yt[4 * dy + 2], b1 = yt[4 * dy + 3];
+    uint32_t packed = 0;
+    const int nvalid = min(4, g.w - (X0 + cx));
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if (k < nvalid) {
+            const int dx = X0 + cx + k;
+            const int2 t = *(const int2*)(xt + 4 * dx);  // sx0, sx1, a0, a1 as 4 x int16
+            const int sx0 = (int16_t)(t.x & 0xffff) - sx_lo, sx1 = (int16_t)(t.x >> 16) - sx_lo;
+            const int a0 = (int16_t)(t.y & 0xffff), a1 = (int16_t)(t.y >> 16);
+            const int h0 = s_src[r0][sx0] * a0 + s_src[r0][sx1] * a1;
+            const int h1 = s_src[r1][sx0] * a0 + s_src[r1][sx1] * a1;
+            int v = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
+            v = v < 0 ? 0 : (v > 255 ? 255 : v);
+            packed |= (uint32_t)v << (8 * k);
+        }
+    }
+    uint8_t* out = pyr + (size_t)f * fb + g.off + (size_t)dy * g.pitch + X0 + cx;
+    if (nvalid == 4) {
+        *(uint32_t*)out = packed;
+    } else {
+        for (int k = 0; k < nvalid; k++) out[k] = (uint8_t)(packed >> (8 * k));
+    }
+}
+
+// ------------------------------------------------------------------ FAST score + blur
+
+typedef short short2_t __attribute__((ext_vector_type(2)));
+
+// FAST-9/16 corner strength M = max over the 16 contiguous 9-arcs of
+// max(min(v - ring), min(ring - v)).  At threshold t the pixel is a corner iff
+// M > t, and cornerScore<16> then returns max(t, M) - 1 = M - 1, independent of t
+// (features2d/fast.cpp FAST_t / fast_score.cpp cornerScore<16>).  Both signs are
+// evaluated at once in packed int16 lanes: (v - x, x - v).
+__device__ __forceinline__ int fast_strength(const uint8_t* c, int pitch) {
+    const int off[16] = {0 + 3 * pitch,  1 + 3 * pitch,  2 + 2 * pitch,  3 + 1 * pitch,
+                         3,              3 - 1 * pitch,  2 - 2 * pitch,  1 - 3 * pitch,
+                         0 - 3 * pitch, -1 - 3 * pitch, -2 - 2 * pitch, -3 - 1 * pitch,
+                         -3,            -3 + 1 * pitch, -2 + 2 * pitch, -1 + 3 * pitch};
+    const int v = c[0];
+    const short2_t V = __builtin_bit_cast(short2_t, (int)(v - (v << 16)));   // (v, -v)
+    short2_t d[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int x = c[off[k]];
+        d[k] = V - __builtin_bit_cast(short2_t, (int)(x - (x << 16)));       // (v - x, x - v)
+    }
+    short2_t m2[16], m4[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(d[k], d[(k + 1) & 15]);
+#pragma unroll
+    for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
+    short2_t best = __builtin_elementwise_min(__builtin_elementwise_min(m4[0], m4[4]), d[8]);
+#pragma unroll
+    for (int k = 1; k < 16; k++) {
+        const short2_t m9 = __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]), d[(k + 8) & 15]);
+        best = __builtin_elementwise_max(best, m9);
+    }
+    const int M = best.x > best.y ? best.x : best.y;
+    return M > 0 ? M : 0;
+}
+
+__device__ __forceinline__ int reflect101(int i, int n) {
+    i = i < 0 ? -i : i;
+    return i >= n ? 2 * n - 2 - i : i;
+}
+
+constexpr int kTW = 64, kTH = 32;  // level tile (outputs) of k_level_tiles
+
+// One 64x32 tile of one pyramid level per workgroup, all levels and frames in one
+// launch.  The tile plus a 3-pixel REFLECT_101 margin is staged in LDS once and
+// feeds both per-pixel products of the level:
+//  * the FAST strength map M (pixels of the FAST detection area [19, w-19) x [19, h-19)),
+//  * GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of the level ROI clone
+//    (ORBextractor.cc:1587-1595), OpenCV 3.3.1 8U fixed point: taps
+//    {18,34,49,55,49,34,18}, exact integer rows, column (sum + 2^15) >> 16, saturate.
+__global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                                     uint8_t* __restrict__ score, long long fb,
+                                                     const LevelGeom* __restrict__ lv, int L) {
+    __shared__ uint8_t s_in[kTH + 6][kTW + 8];
+    __shared__ uint16_t s_row[kTH + 6][kTW];
+    const int tile = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    int l = 0;
+    while (l + 1 < L && tile >= lv[l + 1].tile_first) l++;
+    const LevelGeom& g = lv[l];
+    const int t = tile - g.tile_first;
+    const int ty = t / g.tiles_x;
+    const int X0 = (t - ty * g.tiles_x) * kTW, Y0 = ty * kTH;
+    const uint8_t* img = pyr + (size_t)f * fb + g.off;
+    const int gx0 = reflect101(X0 + lane - 3, g.w);
+    const int gx1 = reflect101(X0 + 64 + (lane < 6 ? lane : 0) - 3, g.w);
+    for (int r = wave; r < kTH + 6; r += 4) {
+        const uint8_t* row = img + (size_t)reflect101(Y0 + r - 3, g.h) * g.pitch;
+        s_in[r][lane] = row[gx0];
+        if (lane < 6) s_in[r][64 + lane] = row[gx1];
+    }
+    __syncthreads();
+    for (int i = tid; i < (kTH + 6) * kTW; i += 256) {
+        const int r = i >> 6, c = i & 63;
+        const uint8_t* p = &s_in[r][c];
+        s_row[r][c] = (uint16_t)(18 * (p[0] + p[6]) + 34 * (p[1] + p[5]) + 49 * (p[2] + p[4]) + 55 * p[3]);
+    }
+    __syncthreads();
+    uint8_t* bout = blur + (size_t)f * fb + g.off;
+    uint8_t* mout = score + (size_t)f * fb + g.off;
+    const int x = X0 + lane;
+    const bool xin = x < g.w;
+    const bool xdet = x >= kEdge && x < g.w - kEdge;
+    for (int r = wave; r < kTH; r += 4) {
+        const int y = Y0 + r;
+        if (y < g.h && xin) {
+            const int s = 18 * ((int)s_row[r][lane] + s_row[r + 6][lane]) + 34 * ((int)s_row[r + 1][lane] + s_row[r + 5][lane]) +
+                          49 * ((int)s_row[r + 2][lane] + s_row[r + 4][lane]) + 55 * (int)s_row[r + 3][lane];
+            const int v = (s + (1 << 15)) >> 16;
+            bout[(size_t)y * g.pitch + x] = (uint8_t)(v > 255 ? 255 : v);
+            int m = 0;
+            if (xdet && y >= kEdge && y < g.h - kEdge) m = fast_strength(&s_in[r + 3][lane + 3], kTW + 8);
+            mout[(size_t)y * g.pitch + x] = (uint8_t)m;
+        }
+    }
 }
 
 // ------------------------------------------------------------------ FAST cells
 
-constexpr int kTileDim = kCellMax + 6;  // sub-image (window + 3-px ring margin)
-
-// FAST-9/16 corner strength M = max over the 16 contiguous 9-arcs of
-// max(min(v - ring), min(ring - v)).  At threshold t the pixel is a corner iff
-// M > t, and cornerScore<16> returns max(t, M) - 1 = M - 1 (threshold-independent).
-__device__ __forceinline__ int fast_strength(const uint8_t* t, int v) {
-    // ring offsets (dx, dy) of features2d makeOffsets(16), on a kTileDim-pitch tile
-    const int off[16] = {0 + 3 * kTileDim,  1 + 3 * kTileDim,  2 + 2 * kTileDim,  3 + 1 * kTileDim,
-                         3,                 3 - 1 * kTileDim,  2 - 2 * kTileDim,  1 - 3 * kTileDim,
-                         0 - 3 * kTileDim, -1 - 3 * kTileDim, -2 - 2 * kTileDim, -3 - 1 * kTileDim,
-                         -3,               -3 + 1 * kTileDim, -2 + 2 * kTileDim, -1 + 3 * kTileDim};
-    int d[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = v - (int)t[off[k]];
-    int amax = -1024, bmin = 1024;
-#pragma unroll
-    for (int s = 0; s < 16; s++) {
-        int mn = d[s], mx = d[s];
-#pragma unroll
-        for (int i = 1; i < 9; i++) {
-            const int x = d[(s + i) & 15];
-            mn = x < mn ? x : mn;
-            mx = x > mx ? x : mx;
-        }
-        amax = mn > amax ? mn : amax;
-        bmin = mx < bmin ? mx : bmin;
-    }
-    const int M = amax > -bmin ? amax : -bmin;
-    return M > 0 ? M : 0;
-}
-
 // One wave per cell.  Reproduces cv::FAST(cell, kps, t, true) for t = iniThFAST and,
-// if that leaves the cell empty, t = minThFAST (ORBextractor.cc:1091-1104), with the
-// window-local non-max suppression of FAST_t (neighbours outside the detection window
-// or below threshold score 0), and writes the cell's keypoints in raster order.
-__global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ pyr, long long fb,
+// if that leaves the cell empty, t = minThFAST (ORBextractor.cc:1091-1104), from the
+// strength map M: corner iff M > t, score M - 1, FAST_t's non-max suppression over the
+// 8-neighbourhood where neighbours outside the cell's detection window or below the
+// threshold score 0.  Writes the cell's keypoints in raster order.
+__global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ score, long long fb,
                                                     const LevelGeom* __restrict__ lv,
                                                     const CellGeom* __restrict__ cells, int ncells,
                                                     int ini_th, int min_th, uint32_t* __restrict__ slots,
                                                     int slots_pf, int* __restrict__ cell_count) {
-    __shared__ uint8_t s_tile[4][kTileDim * kTileDim];
-    __shared__ uint8_t s_m[4][kCellMax * kCellMax];
+    __shared__ uint8_t s_m[4][kCellMax + 2][kCellMax + 2];
     __shared__ unsigned long long s_mask[4][kCellMax];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ci = blockIdx.x * 4 + wave;
@@ -128,21 +235,17 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
     if (ci >= ncells) return;  // whole wave exits; no block barriers below
     const CellGeom c = cells[ci];
     const LevelGeom& g = lv[c.level];
-    const uint8_t* src = pyr + (size_t)f * fb + g.off + (size_t)c.y0 * g.pitch + c.x0;
-    uint8_t* tile = s_tile[wave];
-    uint8_t* msc = s_m[wave];
-    for (int r = 0; r < c.rows; r++)
-        for (int col = lane; col < c.cols; col += 64) tile[r * kTileDim + col] = src[(size_t)r * g.pitch + col];
-    wave_lds_fence();
     const int wr = c.rows - 6, wc = c.cols - 6;  // detection window [3,rows-3) x [3,cols-3)
     int count = 0;
     if (wr > 0 && wc > 0) {
-        for (int r = 0; r < wr; r++) {
-            if (lane < wc) {
-                const uint8_t* p = tile + (r + 3) * kTileDim + lane + 3;
-                msc[r * kCellMax + lane] = (uint8_t)fast_strength(p, p[0]);
-            }
-        }
+        const uint8_t* src = score + (size_t)f * fb + g.off + (size_t)(c.y0 + 3) * g.pitch + c.x0 + 3;
+        uint8_t(*m)[kCellMax + 2] = s_m[wave];
+        // window M with a zero frame: m[r+1][c+1] = M(r, c)
+        for (int r = 0; r < wr + 2; r++)
+            for (int col = lane; col < wc + 2; col += 64) m[r][col] = 0;
+        wave_lds_fence();
+        for (int r = 0; r < wr; r++)
+            if (lane < wc) m[r + 1][lane + 1] = src[(size_t)r * g.pitch + lane];
         wave_lds_fence();
         for (int pass = 0; pass < 2; pass++) {
             int t = pass == 0 ? ini_th : min_th;
@@ -151,25 +254,19 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
             for (int r = 0; r < wr; r++) {
                 bool keep = false;
                 if (lane < wc) {
-                    const int m = msc[r * kCellMax + lane];
-                    if (m > t) {
-                        const int s = m - 1;
+                    const int mc = m[r + 1][lane + 1];
+                    if (mc > t) {
                         int nb = 0;
 #pragma unroll
-                        for (int dy = -1; dy <= 1; dy++) {
-                            const int rr = r + dy;
-                            if (rr < 0 || rr >= wr) continue;
+                        for (int dy = 0; dy < 3; dy++)
 #pragma unroll
-                            for (int dx = -1; dx <= 1; dx++) {
-                                if (dx == 0 && dy == 0) continue;
-                                const int cc = lane + dx;
-                                if (cc < 0 || cc >= wc) continue;
-                                const int mn = msc[rr * kCellMax + cc];
+                            for (int dx = 0; dx < 3; dx++) {
+                                if (dx == 1 && dy == 1) continue;
+                                const int mn = m[r + dy][lane + dx];
                                 const int sn = mn > t ? mn - 1 : 0;
                                 nb = sn > nb ? sn : nb;
                             }
-                        }
-                        keep = s > nb;
+                        keep = mc - 1 > nb;
                     }
                 }
                 const unsigned long long mask = __ballot(keep);
@@ -188,7 +285,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
                 const int idx = running + __popcll(mask & below);
                 const int xr = c.x0 + 3 + lane - kMinBorder;  // relative to minBorderX
                 const int yr = c.y0 + 3 + r - kMinBorder;
-                const int resp = msc[r * kCellMax + lane] - 1;
+                const int resp = m[r + 1][lane + 1] - 1;
                 out[idx] = (uint32_t)xr | ((uint32_t)yr << 12) | ((uint32_t)resp << 24);
             }
             running += __popcll(mask);
@@ -610,52 +707,6 @@ __global__ __launch_bounds__(256) void k_octree(const LevelGeom* __restrict__ lv
     }
 }
 
-// ------------------------------------------------------------------ blur
-
-__device__ __forceinline__ int reflect101(int i, int n) {
-    i = i < 0 ? -i : i;
-    return i >= n ? 2 * n - 2 - i : i;
-}
-
-// GaussianBlur(level ROI clone, 7x7, sigma 2, BORDER_REFLECT_101), OpenCV 3.3.1
-// 8U fixed point: taps {18,34,49,55,49,34,18}, exact integer rows, column
-// (sum + 2^15) >> 16, saturate.  64 x 16 output tile per workgroup.
-__global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-                                              long long fb, const LevelGeom* __restrict__ lv, int L) {
-    __shared__ uint8_t s_in[22][72];
-    __shared__ int s_row[22][64];
-    const int tile = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
-    int l = 0;
-    while (l + 1 < L && tile >= lv[l + 1].tile_first) l++;
-    const LevelGeom& g = lv[l];
-    const int t = tile - g.tile_first;
-    const int X0 = (t % g.tiles_x) * 64, Y0 = (t / g.tiles_x) * 16;
-    const uint8_t* img = pyr + (size_t)f * fb + g.off;
-    for (int i = tid; i < 22 * 70; i += 256) {
-        const int r = i / 70, c = i - r * 70;
-        const int gy = reflect101(Y0 + r - 3, g.h), gx = reflect101(X0 + c - 3, g.w);
-        s_in[r][c] = img[(size_t)gy * g.pitch + gx];
-    }
-    __syncthreads();
-    for (int i = tid; i < 22 * 64; i += 256) {
-        const int r = i >> 6, c = i & 63;
-        const uint8_t* p = &s_in[r][c];
-        s_row[r][c] = 18 * (p[0] + p[6]) + 34 * (p[1] + p[5]) + 49 * (p[2] + p[4]) + 55 * p[3];
-    }
-    __syncthreads();
-    uint8_t* out = blur + (size_t)f * fb + g.off;
-    for (int i = tid; i < 16 * 64; i += 256) {
-        const int r = i >> 6, c = i & 63;
-        const int y = Y0 + r, x = X0 + c;
-        if (y < g.h && x < g.w) {
-            const int s = 18 * (s_row[r][c] + s_row[r + 6][c]) + 34 * (s_row[r + 1][c] + s_row[r + 5][c]) +
-                          49 * (s_row[r + 2][c] + s_row[r + 4][c]) + 55 * s_row[r + 3][c];
-            const int v = (s + (1 << 15)) >> 16;
-            out[(size_t)y * g.pitch + x] = (uint8_t)(v > 255 ? 255 : v);
-        }
-    }
-}
-
 // ------------------------------------------------------------------ angle + descriptor
 
 // cv::fastAtan2 (OpenCV 3.3.1), degrees; float ops in the reference order.
@@ -790,22 +841,29 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     (void)hipMemsetAsync(db.status, 0, sizeof(int) * (size_t)batch, stream);
     {
         const LevelGeom& g0 = plan.lv[0];
-        dim3 grid((g0.w + 1023) / 1024, g0.h, batch);
-        hipLaunchKernelGGL(k_copy_level0, grid, dim3(256), 0, stream, d_imgs, frame_pitch, stride, g0.w,
-                           db.pyr, fb, g0.pitch);
+        const int vec16 = ((uintptr_t)d_imgs % 16 == 0) && (stride % 16 == 0) && (frame_pitch % 16 == 0) &&
+                          (g0.w % 16 == 0);
+        dim3 grid(64, batch);
+        hipLaunchKernelGGL(k_copy_level0, grid, dim3(256), 0, stream, d_imgs, frame_pitch, stride, g0.w, g0.h,
+                           db.pyr, fb, g0.pitch, vec16);
         for (int l = 1; l < L; l++) {
             const LevelGeom& g = plan.lv[l];
-            dim3 gr((g.w + 255) / 256, g.h, batch);
+            dim3 gr((g.w + kRszTW - 1) / kRszTW, (g.h + kRszTH - 1) / kRszTH, batch);
             hipLaunchKernelGGL(k_resize, gr, dim3(256), 0, stream, db.pyr, fb, db.lv, l, db.rtab);
         }
     }
     if (ev) (void)hipEventRecord(ev[1], stream);
     {
-        dim3 grid((ncells + 3) / 4, batch);
-        hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), 0, stream, db.pyr, fb, db.lv, db.cells, ncells,
-                           plan.prm.ini_th, plan.prm.min_th, db.slots, plan.slots_per_frame, db.cell_count);
+        dim3 grid(plan.tiles_total, batch);
+        hipLaunchKernelGGL(k_level_tiles, grid, dim3(256), 0, stream, db.pyr, db.blur, db.score, fb, db.lv, L);
     }
     if (ev) (void)hipEventRecord(ev[2], stream);
+    {
+        dim3 grid((ncells + 3) / 4, batch);
+        hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), 0, stream, db.score, fb, db.lv, db.cells, ncells,
+                           plan.prm.ini_th, plan.prm.min_th, db.slots, plan.slots_per_frame, db.cell_count);
+    }
+    if (ev) (void)hipEventRecord(ev[3], stream);
     {
         const int NC = (plan.max_ncap + 63) & ~63;
         const size_t lds = (size_t)NC * (8 + 16 + 12 + 8 + 8 + 16 + 2);
@@ -813,11 +871,6 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
         hipLaunchKernelGGL(k_octree, grid, dim3(256), lds, stream, db.lv, L, db.slots, plan.slots_per_frame,
                            db.cells, db.cell_count, ncells, db.keys, db.key_node, plan.keys_per_frame,
                            db.kept, plan.kept_per_frame, db.kept_count, db.status, NC);
-    }
-    if (ev) (void)hipEventRecord(ev[3], stream);
-    {
-        dim3 grid(plan.tiles_total, batch);
-        hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, stream, db.pyr, db.blur, fb, db.lv, L);
     }
     if (ev) (void)hipEventRecord(ev[4], stream);
     {

@@ -183,9 +183,9 @@ bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
         out_off += ncap;
         if (ncap > plan.max_ncap) plan.max_ncap = ncap;
 
-        // blur tiles (64 x 16 outputs)
+        // score/blur tiles (64 x 32 outputs)
         g.tiles_x = (g.w + 63) / 64;
-        g.tiles_y = (g.h + 15) / 16;
+        g.tiles_y = (g.h + 31) / 32;
         g.tile_first = tile_first;
         tile_first += g.tiles_x * g.tiles_y;
 
@@ -196,6 +196,17 @@ bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
             g.ytab_off = (int)plan.rtab.size();
             plan.rtab.resize(plan.rtab.size() + 4 * (size_t)g.h);
             resize_tables(prev_w, prev_h, g.w, g.h, plan.rtab.data() + g.xtab_off, plan.rtab.data() + g.ytab_off);
+            // the resize kernel stages each 64x16 output tile's source region in LDS
+            const int16_t* xt = plan.rtab.data() + g.xtab_off;
+            const int16_t* yt = plan.rtab.data() + g.ytab_off;
+            for (int x0 = 0; x0 < g.w; x0 += 64) {
+                const int xe = (x0 + 64 < g.w ? x0 + 64 : g.w) - 1;
+                if (xt[4 * xe + 1] - xt[4 * x0] + 1 > 192) { plan.why = "scale factor too large"; return false; }
+            }
+            for (int y0 = 0; y0 < g.h; y0 += 16) {
+                const int ye = (y0 + 16 < g.h ? y0 + 16 : g.h) - 1;
+                if (yt[4 * ye + 1] - yt[4 * y0] + 1 > 48) { plan.why = "scale factor too large"; return false; }
+            }
         }
         prev_w = g.w;
         prev_h = g.h;
