@@ -149,6 +149,85 @@ int orbx_window_match(int device, const uint8_t* qdesc, int nq, const uint8_t* t
                       int tie_last, int32_t* best_idx, int32_t* best_dist, int32_t* best_level,
                       int32_t* second_dist, int32_t* second_level);
 
+/* ------------------------------------------------------------------ matcher */
+
+/* The Frame / KeyFrame fields the ORBmatcher functions read (include/Frame.h,
+ * include/KeyFrame.h), as plain host arrays. */
+typedef struct {
+    int n;                       /* N */
+    const orbx_keypoint* keys;   /* mvKeysUn */
+    const uint8_t* desc;         /* mDescriptors, n x 32 */
+    const float* u_right;        /* mvuRight (n) or NULL (monocular) */
+    float fx, fy, cx, cy, bf, b; /* fx, fy, cx, cy, mbf, mb */
+    float min_x, max_x, min_y, max_y; /* mnMinX, mnMaxX, mnMinY, mnMaxY */
+    int nlevels;
+    const float* scale_factors;  /* mvScaleFactors */
+    const float* level_sigma2;   /* mvLevelSigma2 */
+    float Tcw[12];               /* mTcw rows 0..2, row-major */
+} orbx_frame_view;
+
+/* MapPoint fields, indexed by MapPoint id (the ids stand in for MapPoint*). */
+typedef struct {
+    int n;
+    const float* pos;            /* GetWorldPos(), n x 3 (may be NULL where unused) */
+    const uint8_t* desc;         /* GetDescriptor(), n x 32 */
+    const int32_t* observations; /* Observations() */
+    const uint8_t* bad;          /* isBad() or NULL */
+} orbx_mappoints;
+
+/* Frame::IsInFrustum outputs per MapPoint id (Frame.cc:412-477), read by
+ * SearchByProjection(Frame&, vector<MapPoint*>, th). */
+typedef struct {
+    const uint8_t* in_view;      /* mbTrackInView */
+    const float* proj_x;         /* mTrackProjX */
+    const float* proj_y;         /* mTrackProjY */
+    const float* proj_xr;        /* mTrackProjXR */
+    const int32_t* scale_level;  /* mnTrackScaleLevel */
+    const float* view_cos;       /* mTrackViewCos */
+} orbx_track;
+
+typedef struct orbx_matcher orbx_matcher;
+
+/* ORBmatcher::ORBmatcher(nnratio, checkOri) (ORBmatcher.h:57), bound to HIP device
+ * `device` with its own stream and scratch buffers. */
+int orbx_matcher_create(int device, float nnratio, int check_ori, orbx_matcher** out);
+void orbx_matcher_destroy(orbx_matcher* m);
+
+/* SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoints, const float th)
+ * ORBmatcher.cc:61-173.  frame_mp (F.mvpMapPoints as MapPoint ids, -1 = NULL) is
+ * updated in place; queries = vpMapPoints ids in order. */
+int orbx_search_by_projection_local(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp,
+                                    const int32_t* queries, int nq, const orbx_mappoints* mps,
+                                    const orbx_track* trk, float th, int* nmatches);
+
+/* SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono)
+ * ORBmatcher.cc:1620-1789 (TrackWithMotionModel, Tracking.cc:966-994). */
+int orbx_search_by_projection_frame(orbx_matcher* m, const orbx_frame_view* cur, int32_t* cur_mp,
+                                    const orbx_frame_view* last, const int32_t* last_mp,
+                                    const uint8_t* last_outlier, const orbx_mappoints* mps, float th,
+                                    int mono, int* nmatches);
+
+/* SearchForTriangulation(KF1, KF2, F12, vMatchedPairs, bOnlyStereo)
+ * ORBmatcher.cc:850-1056 (LocalMapping::CreateNewMapPoints, LocalMapping.cc:305).
+ * DBoW2 FeatureVectors as CSR: node ids ascending (fv_node[k]), keypoints of node k
+ * at fv_idx[fv_off[k] .. fv_off[k+1]).  pairs receives (idx1, idx2) in idx1 order
+ * (capacity 2*kf1->n ints); *npairs the count. */
+int orbx_search_for_triangulation(orbx_matcher* m, const orbx_frame_view* kf1, const uint8_t* kf1_has_mp,
+                                  const int32_t* fv1_node, const int32_t* fv1_off, const int32_t* fv1_idx,
+                                  int fv1_n, const orbx_frame_view* kf2, const uint8_t* kf2_has_mp,
+                                  const int32_t* fv2_node, const int32_t* fv2_off, const int32_t* fv2_idx,
+                                  int fv2_n, const float* F12, int only_stereo, int32_t* pairs, int* npairs);
+
+/* Frame::ComputeStereoMatches (Frame.cc:673-885) for the last orbx_extract_batch of
+ * `ex` where frame `left_frame` / `right_frame` hold the left / right images and
+ * keys_* / desc_* their extracted keypoints.  maxD = mbf / minZ (this fork reads mb
+ * before it is set, Frame.cc:711-713; upstream's value is fx).  Writes mvuRight and
+ * mvDepth (n_left floats each, -1 = no match). */
+int orbx_compute_stereo_matches(orbx_matcher* m, orbx_extractor* ex, int left_frame, int right_frame,
+                                const orbx_frame_view* left, const orbx_keypoint* keys_r,
+                                const uint8_t* desc_r, int n_right, float max_disparity, float* u_right,
+                                float* depth);
+
 /* Library / device info. */
 const char* orbx_version(void);
 int orbx_device_count(int* n);

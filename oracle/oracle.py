@@ -182,3 +182,145 @@ def cos_sin(angle_deg: float):
 
 def cpu_threads() -> int:
     return len(os.sched_getaffinity(0))
+
+
+# ------------------------------------------------------------------ matcher restatements
+
+F32P = C.POINTER(C.c_float)
+I32P = C.POINTER(C.c_int32)
+U8P = C.POINTER(C.c_uint8)
+
+
+class OraFrame(C.Structure):
+    _fields_ = [("n", C.c_int), ("keys", C.c_void_p), ("desc", U8P), ("u_right", F32P),
+                ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("bf", C.c_float), ("b", C.c_float), ("min_x", C.c_float), ("max_x", C.c_float),
+                ("min_y", C.c_float), ("max_y", C.c_float), ("nlevels", C.c_int),
+                ("scale_factors", F32P), ("level_sigma2", F32P), ("Tcw", C.c_float * 12)]
+
+
+class OraMapPoints(C.Structure):
+    _fields_ = [("n", C.c_int), ("pos", F32P), ("desc", U8P), ("observations", I32P), ("bad", U8P)]
+
+
+class OraTrack(C.Structure):
+    _fields_ = [("in_view", U8P), ("proj_x", F32P), ("proj_y", F32P), ("proj_xr", F32P),
+                ("scale_level", I32P), ("view_cos", F32P)]
+
+
+def _frame(view, keep):
+    """Build an OraFrame from an object with the FrameView attributes."""
+    keys = np.ascontiguousarray(view.keys, dtype=KEYPOINT_DTYPE)
+    desc = np.ascontiguousarray(view.desc, dtype=np.uint8)
+    sf = np.ascontiguousarray(view.scale_factors, dtype=np.float32)
+    sg = np.ascontiguousarray(view.level_sigma2 if view.level_sigma2 is not None else sf * sf, dtype=np.float32)
+    ur = None if view.u_right is None else np.ascontiguousarray(view.u_right, dtype=np.float32)
+    T = np.eye(4, dtype=np.float32) if view.Tcw is None else np.ascontiguousarray(view.Tcw, dtype=np.float32)
+    keep += [keys, desc, sf, sg, ur]
+    f = OraFrame()
+    f.n = len(keys)
+    f.keys = keys.ctypes.data
+    f.desc = desc.ctypes.data_as(U8P)
+    f.u_right = ur.ctypes.data_as(F32P) if ur is not None else None
+    f.fx, f.fy, f.cx, f.cy, f.bf, f.b = view.fx, view.fy, view.cx, view.cy, view.bf, view.b
+    f.min_x, f.max_x, f.min_y, f.max_y = view.min_x, view.max_x, view.min_y, view.max_y
+    f.nlevels = len(sf)
+    f.scale_factors = sf.ctypes.data_as(F32P)
+    f.level_sigma2 = sg.ctypes.data_as(F32P)
+    f.Tcw[:] = list(T[:3, :4].reshape(-1))
+    keep.append(f)
+    return f
+
+
+def _mappoints(mps, keep):
+    d = np.ascontiguousarray(mps.desc, dtype=np.uint8)
+    o = np.ascontiguousarray(mps.observations, dtype=np.int32)
+    p = None if mps.pos is None else np.ascontiguousarray(mps.pos, dtype=np.float32)
+    b = None if mps.bad is None else np.ascontiguousarray(mps.bad, dtype=np.uint8)
+    keep += [d, o, p, b]
+    m = OraMapPoints()
+    m.n = len(d)
+    m.pos = p.ctypes.data_as(F32P) if p is not None else None
+    m.desc = d.ctypes.data_as(U8P)
+    m.observations = o.ctypes.data_as(I32P)
+    m.bad = b.ctypes.data_as(U8P) if b is not None else None
+    keep.append(m)
+    return m
+
+
+def sbp_local(F, frame_mp, queries, mps, track, th, nnratio):
+    """ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th); frame_mp updated in place."""
+    keep = []
+    f = _frame(F, keep)
+    m = _mappoints(mps, keep)
+    a = [np.ascontiguousarray(track.in_view, np.uint8), np.ascontiguousarray(track.proj_x, np.float32),
+         np.ascontiguousarray(track.proj_y, np.float32), np.ascontiguousarray(track.proj_xr, np.float32),
+         np.ascontiguousarray(track.scale_level, np.int32), np.ascontiguousarray(track.view_cos, np.float32)]
+    t = OraTrack(a[0].ctypes.data_as(U8P), a[1].ctypes.data_as(F32P), a[2].ctypes.data_as(F32P),
+                 a[3].ctypes.data_as(F32P), a[4].ctypes.data_as(I32P), a[5].ctypes.data_as(F32P))
+    q = np.ascontiguousarray(queries, dtype=np.int32)
+    L = lib()
+    L.ora_sbp_local.argtypes = [C.c_void_p, I32P, I32P, C.c_int, C.c_void_p, C.c_void_p, C.c_float, C.c_float]
+    return L.ora_sbp_local(C.addressof(f), frame_mp.ctypes.data_as(I32P), q.ctypes.data_as(I32P), len(q),
+                           C.addressof(m), C.addressof(t), th, nnratio)
+
+
+def sbp_frame(cur, cur_mp, last, last_mp, mps, th, mono, check_ori, last_outlier=None):
+    keep = []
+    fc = _frame(cur, keep)
+    fl = _frame(last, keep)
+    m = _mappoints(mps, keep)
+    lm = np.ascontiguousarray(last_mp, dtype=np.int32)
+    lo = None if last_outlier is None else np.ascontiguousarray(last_outlier, dtype=np.uint8)
+    L = lib()
+    L.ora_sbp_frame.argtypes = [C.c_void_p, I32P, C.c_void_p, I32P, U8P, C.c_void_p, C.c_float, C.c_int, C.c_int]
+    return L.ora_sbp_frame(C.addressof(fc), cur_mp.ctypes.data_as(I32P), C.addressof(fl), lm.ctypes.data_as(I32P),
+                           lo.ctypes.data_as(U8P) if lo is not None else None, C.addressof(m), th,
+                           1 if mono else 0, 1 if check_ori else 0)
+
+
+def search_for_triangulation(kf1, has1, fv1, kf2, has2, fv2, F12, only_stereo, check_ori):
+    keep = []
+    f1 = _frame(kf1, keep)
+    f2 = _frame(kf2, keep)
+    h1 = np.ascontiguousarray(has1, np.uint8)
+    h2 = np.ascontiguousarray(has2, np.uint8)
+    n1, o1, i1 = (np.ascontiguousarray(x, np.int32) for x in fv1)
+    n2, o2, i2 = (np.ascontiguousarray(x, np.int32) for x in fv2)
+    F = np.ascontiguousarray(F12, np.float32).reshape(9)
+    pairs = np.zeros((max(len(kf1.keys), 1), 2), np.int32)
+    L = lib()
+    L.ora_search_for_triangulation.argtypes = [C.c_void_p, U8P, I32P, I32P, I32P, C.c_int, C.c_void_p, U8P, I32P,
+                                               I32P, I32P, C.c_int, F32P, C.c_int, C.c_int, I32P]
+    n = L.ora_search_for_triangulation(C.addressof(f1), h1.ctypes.data_as(U8P), n1.ctypes.data_as(I32P),
+                                       o1.ctypes.data_as(I32P), i1.ctypes.data_as(I32P), len(n1), C.addressof(f2),
+                                       h2.ctypes.data_as(U8P), n2.ctypes.data_as(I32P), o2.ctypes.data_as(I32P),
+                                       i2.ctypes.data_as(I32P), len(n2), F.ctypes.data_as(F32P),
+                                       1 if only_stereo else 0, 1 if check_ori else 0, pairs.ctypes.data_as(I32P))
+    return pairs[:n].copy()
+
+
+def compute_stereo_matches(left, keys_r, desc_r, levels_l, levels_r, maxD):
+    keep = []
+    f = _frame(left, keep)
+    kr = np.ascontiguousarray(keys_r, dtype=KEYPOINT_DTYPE)
+    dr = np.ascontiguousarray(desc_r, dtype=np.uint8)
+    nl = len(levels_l)
+    ll = [np.ascontiguousarray(x) for x in levels_l]
+    lr = [np.ascontiguousarray(x) for x in levels_r]
+    pl = (U8P * nl)(*[_u8(x) for x in ll])
+    pr = (U8P * nl)(*[_u8(x) for x in lr])
+    w = np.array([x.shape[1] for x in ll], np.int32)
+    h = np.array([x.shape[0] for x in ll], np.int32)
+    inv = (np.float32(1) / np.ascontiguousarray(left.scale_factors, np.float32)).astype(np.float32)
+    n = len(left.keys)
+    ur = np.zeros(max(n, 1), np.float32)
+    dp = np.zeros(max(n, 1), np.float32)
+    L = lib()
+    L.ora_compute_stereo_matches.argtypes = [C.c_void_p, C.c_void_p, U8P, C.c_int, C.POINTER(U8P), C.POINTER(U8P),
+                                             I32P, I32P, F32P, C.c_float, F32P, F32P]
+    L.ora_compute_stereo_matches.restype = None
+    L.ora_compute_stereo_matches(C.addressof(f), kr.ctypes.data, dr.ctypes.data_as(U8P), len(kr), pl, pr,
+                                 w.ctypes.data_as(I32P), h.ctypes.data_as(I32P), inv.ctypes.data_as(F32P), maxD,
+                                 ur.ctypes.data_as(F32P), dp.ctypes.data_as(F32P))
+    return ur[:n].copy(), dp[:n].copy()

@@ -1,0 +1,572 @@
+/*
+ * orbx_oracle_match.c -- TEST INFRASTRUCTURE ONLY: CPU restatement of the ORBmatcher /
+ * Frame matching functions on the hot path (parity checker, never the product).
+ *
+ *   AssignFeaturesToGrid / PosInGrid / GetFeaturesInArea   Frame.cc:351-370, 488-567
+ *   ComputeThreeMaxima                                      ORBmatcher.cc:1935-1977
+ *   SearchByProjection(Frame&, vector<MapPoint*>, th)       ORBmatcher.cc:61-173 (a11)
+ *   SearchByProjection(Frame&, const Frame&, th, bMono)     ORBmatcher.cc:1620-1789 (a12)
+ *   SearchForTriangulation(KF1, KF2, F12, pairs, stereo)    ORBmatcher.cc:850-1056 (a15)
+ *   Frame::ComputeStereoMatches                             Frame.cc:673-885 (a18)
+ *
+ * Object-graph inputs (Frame, MapPoint, KeyFrame, FeatureVector) are passed as the
+ * plain arrays they hold.  Geometric products (Rcw*x + t) are evaluated in float,
+ * left to right -- OpenCV 3.3.1's small-matrix gemm accumulation is not pinned here
+ * ("parity unpinned").
+ */
+#include "orbx_oracle_match.h"
+
+#include <limits.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+enum { TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30 };
+
+/* ---------------------------------------------------------------- grid */
+
+/* Frame::PosInGrid, Frame.cc:558-567 */
+static int pos_in_grid(const ora_frame* f, float inv_w, float inv_h, const ora_keypoint* kp, int* px, int* py) {
+    *px = (int)roundf((kp->x - f->min_x) * inv_w);
+    *py = (int)roundf((kp->y - f->min_y) * inv_h);
+    if (*px < 0 || *px >= ORA_GRID_COLS || *py < 0 || *py >= ORA_GRID_ROWS) return 0;
+    return 1;
+}
+
+/* Frame::AssignFeaturesToGrid, Frame.cc:351-370 (grid cell lists in index order);
+ * mfGridElementWidthInv = FRAME_GRID_COLS / (mnMaxX - mnMinX), Frame.cc:157-159 */
+void ora_grid_build(const ora_frame* f, ora_grid* g) {
+    g->inv_w = (float)ORA_GRID_COLS / (f->max_x - f->min_x);
+    g->inv_h = (float)ORA_GRID_ROWS / (f->max_y - f->min_y);
+    int* cnt = (int*)calloc(ORA_GRID_COLS * ORA_GRID_ROWS, sizeof(int));
+    int* cell = (int*)malloc(sizeof(int) * (size_t)(f->n ? f->n : 1));
+    for (int i = 0; i < f->n; i++) {
+        int px, py;
+        if (pos_in_grid(f, g->inv_w, g->inv_h, &f->keys[i], &px, &py)) {
+            cell[i] = px * ORA_GRID_ROWS + py;
+            cnt[cell[i]]++;
+        } else
+            cell[i] = -1;
+    }
+    g->start[0] = 0;
+    for (int c = 0; c < ORA_GRID_COLS * ORA_GRID_ROWS; c++) g->start[c + 1] = g->start[c] + cnt[c];
+    g->idx = (int*)malloc(sizeof(int) * (size_t)(g->start[ORA_GRID_COLS * ORA_GRID_ROWS] + 1));
+    memset(cnt, 0, sizeof(int) * ORA_GRID_COLS * ORA_GRID_ROWS);
+    for (int i = 0; i < f->n; i++)
+        if (cell[i] >= 0) g->idx[g->start[cell[i]] + cnt[cell[i]]++] = i;
+    free(cnt);
+    free(cell);
+}
+
+void ora_grid_free(ora_grid* g) {
+    free(g->idx);
+    g->idx = NULL;
+}
+
+/* Frame::GetFeaturesInArea, Frame.cc:488-548 */
+int ora_features_in_area(const ora_frame* f, const ora_grid* g, float x, float y, float r, int minLevel,
+                         int maxLevel, int* out, int cap) {
+    int n = 0;
+    int t;
+    t = (int)floorf((x - f->min_x - r) * g->inv_w);
+    const int nMinCellX = t > 0 ? t : 0;
+    if (nMinCellX >= ORA_GRID_COLS) return 0;
+    t = (int)ceilf((x - f->min_x + r) * g->inv_w);
+    const int nMaxCellX = t < ORA_GRID_COLS - 1 ? t : ORA_GRID_COLS - 1;
+    if (nMaxCellX < 0) return 0;
+    t = (int)floorf((y - f->min_y - r) * g->inv_h);
+    const int nMinCellY = t > 0 ? t : 0;
+    if (nMinCellY >= ORA_GRID_ROWS) return 0;
+    t = (int)ceilf((y - f->min_y + r) * g->inv_h);
+    const int nMaxCellY = t < ORA_GRID_ROWS - 1 ? t : ORA_GRID_ROWS - 1;
+    if (nMaxCellY < 0) return 0;
+    const int bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+    for (int ix = nMinCellX; ix <= nMaxCellX; ix++) {
+        for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+            const int c = ix * ORA_GRID_ROWS + iy;
+            for (int j = g->start[c]; j < g->start[c + 1]; j++) {
+                const ora_keypoint* kp = &f->keys[g->idx[j]];
+                if (bCheckLevels) {
+                    if (kp->octave < minLevel) continue;
+                    if (maxLevel >= 0)
+                        if (kp->octave > maxLevel) continue;
+                }
+                const float distx = kp->x - x;
+                const float disty = kp->y - y;
+                if (fabsf(distx) < r && fabsf(disty) < r) {
+                    if (n < cap) out[n] = g->idx[j];
+                    n++;
+                }
+            }
+        }
+    }
+    return n;
+}
+
+/* ---------------------------------------------------------------- helpers */
+
+static int hamming(const uint8_t* a, const uint8_t* b) {
+    int d = 0;
+    for (int i = 0; i < 32; i++) d += __builtin_popcount((unsigned)(a[i] ^ b[i]));
+    return d;
+}
+
+/* ORBmatcher::ComputeThreeMaxima, ORBmatcher.cc:1935-1977 */
+void ora_compute_three_maxima(const int* histo_sizes, int L, int* ind1, int* ind2, int* ind3) {
+    int max1 = 0, max2 = 0, max3 = 0;
+    for (int i = 0; i < L; i++) {
+        const int s = histo_sizes[i];
+        if (s > max1) {
+            max3 = max2; max2 = max1; max1 = s;
+            *ind3 = *ind2; *ind2 = *ind1; *ind1 = i;
+        } else if (s > max2) {
+            max3 = max2; max2 = s;
+            *ind3 = *ind2; *ind2 = i;
+        } else if (s > max3) {
+            max3 = s;
+            *ind3 = i;
+        }
+    }
+    if (max2 < 0.1f * (float)max1) {
+        *ind2 = -1;
+        *ind3 = -1;
+    } else if (max3 < 0.1f * (float)max1) {
+        *ind3 = -1;
+    }
+}
+
+/* Rotation-consistency histogram (ORBmatcher.cc:1750-1786): entries are pushed in
+ * match order; bins outside the three maxima are un-matched. */
+typedef struct {
+    int* items[HISTO_LENGTH];
+    int size[HISTO_LENGTH];
+} rot_hist;
+
+static void hist_init(rot_hist* h, int cap) {
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+        h->items[i] = (int*)malloc(sizeof(int) * (size_t)(cap + 1));
+        h->size[i] = 0;
+    }
+}
+
+static void hist_free(rot_hist* h) {
+    for (int i = 0; i < HISTO_LENGTH; i++) free(h->items[i]);
+}
+
+static void hist_push(rot_hist* h, float angle_a, float angle_b, int item) {
+    const float factor = HISTO_LENGTH / 360.0f;
+    float rot = angle_a - angle_b;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)roundf(rot * factor);
+    if (bin == HISTO_LENGTH) bin = 0;
+    h->items[bin][h->size[bin]++] = item;
+}
+
+static void project(const float* Tcw, const float* X, float* xc) {
+    for (int r = 0; r < 3; r++) xc[r] = Tcw[4 * r] * X[0] + Tcw[4 * r + 1] * X[1] + Tcw[4 * r + 2] * X[2] + Tcw[4 * r + 3];
+}
+
+/* ---------------------------------------------------------------- a11 */
+
+/* ORBmatcher::RadiusByViewingCos, ORBmatcher.cc:176-183 */
+static float radius_by_viewing_cos(float viewCos) { return viewCos > 0.998 ? 2.5f : 4.0f; }
+
+/* ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th), ORBmatcher.cc:61-173.
+ * frame_mp[i]: MapPoint id of keypoint i or -1 (F.mvpMapPoints), updated in place.
+ * queries: the vpMapPoints list (MapPoint ids).  Per-MapPoint arrays: descriptor,
+ * Observations(), isBad(), and the IsInFrustum outputs (Frame.cc:412-477). */
+int ora_sbp_local(const ora_frame* f, int32_t* frame_mp, const int32_t* queries, int nq, const ora_mappoints* mps,
+                  const ora_track* trk, float th, float nnratio) {
+    ora_grid g;
+    ora_grid_build(f, &g);
+    int* cand = (int*)malloc(sizeof(int) * (size_t)(f->n + 1));
+    int nmatches = 0;
+    const int bFactor = th != 1.0;
+    for (int iMP = 0; iMP < nq; iMP++) {
+        const int mp = queries[iMP];
+        if (!trk->in_view[mp]) continue;
+        if (mps->bad && mps->bad[mp]) continue;
+        const int nPredictedLevel = trk->scale_level[mp];
+        float r = radius_by_viewing_cos(trk->view_cos[mp]);
+        if (bFactor) r *= th;
+        const int nc = ora_features_in_area(f, &g, trk->proj_x[mp], trk->proj_y[mp], r * f->scale_factors[nPredictedLevel],
+                                            nPredictedLevel - 1, nPredictedLevel, cand, f->n + 1);
+        if (nc == 0) continue;
+        const uint8_t* dMP = mps->desc + (size_t)mp * 32;
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        for (int c = 0; c < nc; c++) {
+            const int idx = cand[c];
+            if (frame_mp[idx] >= 0)
+                if (mps->observations[frame_mp[idx]] > 0) continue;
+            if (f->u_right && f->u_right[idx] > 0) {
+                const float er = fabsf(trk->proj_xr[mp] - f->u_right[idx]);
+                if (er > r * f->scale_factors[nPredictedLevel]) continue;
+            }
+            const int dist = hamming(dMP, f->desc + (size_t)idx * 32);
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestLevel2 = bestLevel;
+                bestLevel = f->keys[idx].octave;
+                bestIdx = idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = f->keys[idx].octave;
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= TH_HIGH) {
+            if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+            frame_mp[bestIdx] = mp;
+            nmatches++;
+        }
+    }
+    free(cand);
+    ora_grid_free(&g);
+    return nmatches;
+}
+
+/* ---------------------------------------------------------------- a12 */
+
+/* ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono),
+ * ORBmatcher.cc:1620-1789.  cur_mp in/out; MapPoint arrays give GetWorldPos(),
+ * GetDescriptor() and Observations(). */
+int ora_sbp_frame(const ora_frame* cur, int32_t* cur_mp, const ora_frame* last, const int32_t* last_mp,
+                  const uint8_t* last_outlier, const ora_mappoints* mps, float th, int bMono, int check_ori) {
+    ora_grid g;
+    ora_grid_build(cur, &g);
+    int* cand = (int*)malloc(sizeof(int) * (size_t)(cur->n + 1));
+    rot_hist hist;
+    hist_init(&hist, cur->n);
+    int nmatches = 0;
+    /* twc = -Rcw^T tcw; tlc = Rlw*twc + tlw (cc:1637-1643) */
+    const float* T = cur->Tcw;
+    float twc[3];
+    for (int c = 0; c < 3; c++) twc[c] = -(T[c] * T[3] + T[4 + c] * T[7] + T[8 + c] * T[11]);
+    float tlc[3];
+    project(last->Tcw, twc, tlc);
+    const int bForward = tlc[2] > cur->b && !bMono;
+    const int bBackward = -tlc[2] > cur->b && !bMono;
+    for (int i = 0; i < last->n; i++) {
+        const int mp = last_mp[i];
+        if (mp < 0) continue;
+        if (last_outlier && last_outlier[i]) continue;
+        float x3Dc[3];
+        project(cur->Tcw, mps->pos + 3 * (size_t)mp, x3Dc);
+        const float xc = x3Dc[0], yc = x3Dc[1];
+        const float invzc = (float)(1.0 / x3Dc[2]);
+        if (invzc < 0) continue;
+        const float u = cur->fx * xc * invzc + cur->cx;
+        const float v = cur->fy * yc * invzc + cur->cy;
+        if (u < cur->min_x || u > cur->max_x) continue;
+        if (v < cur->min_y || v > cur->max_y) continue;
+        const int nLastOctave = last->keys[i].octave;
+        const float radius = th * cur->scale_factors[nLastOctave];
+        int nc;
+        if (bForward)
+            nc = ora_features_in_area(cur, &g, u, v, radius, nLastOctave, -1, cand, cur->n + 1);
+        else if (bBackward)
+            nc = ora_features_in_area(cur, &g, u, v, radius, 0, nLastOctave, cand, cur->n + 1);
+        else
+            nc = ora_features_in_area(cur, &g, u, v, radius, nLastOctave - 1, nLastOctave + 1, cand, cur->n + 1);
+        if (nc == 0) continue;
+        const uint8_t* dMP = mps->desc + (size_t)mp * 32;
+        int bestDist = 256, bestIdx2 = -1;
+        for (int c = 0; c < nc; c++) {
+            const int i2 = cand[c];
+            if (cur_mp[i2] >= 0)
+                if (mps->observations[cur_mp[i2]] > 0) continue;
+            if (cur->u_right && cur->u_right[i2] > 0) {
+                const float ur = u - cur->bf * invzc;
+                const float er = fabsf(ur - cur->u_right[i2]);
+                if (er > radius) continue;
+            }
+            const int dist = hamming(dMP, cur->desc + (size_t)i2 * 32);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx2 = i2;
+            }
+        }
+        if (bestDist <= TH_HIGH) {
+            cur_mp[bestIdx2] = mp;
+            nmatches++;
+            if (check_ori) hist_push(&hist, last->keys[i].angle, cur->keys[bestIdx2].angle, bestIdx2);
+        }
+    }
+    if (check_ori) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        ora_compute_three_maxima(hist.size, HISTO_LENGTH, &ind1, &ind2, &ind3);
+        for (int b = 0; b < HISTO_LENGTH; b++) {
+            if (b != ind1 && b != ind2 && b != ind3) {
+                for (int j = 0; j < hist.size[b]; j++) {
+                    cur_mp[hist.items[b][j]] = -1;
+                    nmatches--;
+                }
+            }
+        }
+    }
+    hist_free(&hist);
+    free(cand);
+    ora_grid_free(&g);
+    return nmatches;
+}
+
+/* ---------------------------------------------------------------- a15 */
+
+/* ORBmatcher::CheckDistEpipolarLine, ORBmatcher.cc:186-213 */
+static int check_dist_epipolar_line(const ora_keypoint* kp1, const ora_keypoint* kp2, const float* F12,
+                                    const float* sigma2) {
+    const float a = kp1->x * F12[0] + kp1->y * F12[3] + F12[6];
+    const float b = kp1->x * F12[1] + kp1->y * F12[4] + F12[7];
+    const float c = kp1->x * F12[2] + kp1->y * F12[5] + F12[8];
+    const float num = a * kp2->x + b * kp2->y + c;
+    const float den = a * a + b * b;
+    if (den == 0) return 0;
+    const float dsqr = num * num / den;
+    return dsqr < 3.84 * sigma2[kp2->octave];
+}
+
+/* ORBmatcher::SearchForTriangulation, ORBmatcher.cc:850-1056.  kf*_has_mp[i]: the
+ * keyframe keypoint already has a MapPoint.  FeatureVectors as CSR: fv*_node[k]
+ * (ascending node ids), keypoints of node k at fv*_idx[fv*_off[k] .. fv*_off[k+1]).
+ * F12 row-major 3x3.  Writes pairs (idx1, idx2) in idx1 order; returns the count. */
+int ora_search_for_triangulation(const ora_frame* kf1, const uint8_t* kf1_has_mp, const int32_t* fv1_node,
+                                 const int32_t* fv1_off, const int32_t* fv1_idx, int fv1_n, const ora_frame* kf2,
+                                 const uint8_t* kf2_has_mp, const int32_t* fv2_node, const int32_t* fv2_off,
+                                 const int32_t* fv2_idx, int fv2_n, const float* F12, int bOnlyStereo,
+                                 int check_ori, int32_t* pairs /* 2*kf1->n */) {
+    /* Cw = KF1 camera centre = -R1^T t1; C2 = R2w*Cw + t2w (cc:858-865) */
+    const float* T1 = kf1->Tcw;
+    float Cw[3];
+    for (int c = 0; c < 3; c++) Cw[c] = -(T1[c] * T1[3] + T1[4 + c] * T1[7] + T1[8 + c] * T1[11]);
+    float C2[3];
+    project(kf2->Tcw, Cw, C2);
+    const float invz = 1.0f / C2[2];
+    const float ex = kf2->fx * C2[0] * invz + kf2->cx;
+    const float ey = kf2->fy * C2[1] * invz + kf2->cy;
+
+    uint8_t* vbMatched2 = (uint8_t*)calloc((size_t)kf2->n + 1, 1);
+    int32_t* vMatches12 = (int32_t*)malloc(sizeof(int32_t) * (size_t)(kf1->n + 1));
+    for (int i = 0; i < kf1->n; i++) vMatches12[i] = -1;
+    rot_hist hist;
+    hist_init(&hist, kf1->n);
+    int nmatches = 0;
+    int f1 = 0, f2 = 0;
+    while (f1 < fv1_n && f2 < fv2_n) {
+        if (fv1_node[f1] == fv2_node[f2]) {
+            for (int i1 = fv1_off[f1]; i1 < fv1_off[f1 + 1]; i1++) {
+                const int idx1 = fv1_idx[i1];
+                if (kf1_has_mp[idx1]) continue;
+                const int bStereo1 = kf1->u_right && kf1->u_right[idx1] >= 0;
+                if (bOnlyStereo && !bStereo1) continue;
+                const ora_keypoint* kp1 = &kf1->keys[idx1];
+                const uint8_t* d1 = kf1->desc + (size_t)idx1 * 32;
+                int bestDist = TH_LOW, bestIdx2 = -1;
+                for (int i2 = fv2_off[f2]; i2 < fv2_off[f2 + 1]; i2++) {
+                    const int idx2 = fv2_idx[i2];
+                    if (vbMatched2[idx2] || kf2_has_mp[idx2]) continue;
+                    const int bStereo2 = kf2->u_right && kf2->u_right[idx2] >= 0;
+                    if (bOnlyStereo && !bStereo2) continue;
+                    const int dist = hamming(d1, kf2->desc + (size_t)idx2 * 32);
+                    if (dist > TH_LOW || dist > bestDist) continue;
+                    const ora_keypoint* kp2 = &kf2->keys[idx2];
+                    if (!bStereo1 && !bStereo2) {
+                        const float distex = ex - kp2->x;
+                        const float distey = ey - kp2->y;
+                        if (distex * distex + distey * distey < 100 * kf2->scale_factors[kp2->octave]) continue;
+                    }
+                    if (check_dist_epipolar_line(kp1, kp2, F12, kf2->level_sigma2)) {
+                        bestIdx2 = idx2;
+                        bestDist = dist;
+                    }
+                }
+                if (bestIdx2 >= 0) {
+                    vMatches12[idx1] = bestIdx2;
+                    vbMatched2[bestIdx2] = 1;
+                    nmatches++;
+                    if (check_ori) hist_push(&hist, kp1->angle, kf2->keys[bestIdx2].angle, idx1);
+                }
+            }
+            f1++;
+            f2++;
+        } else if (fv1_node[f1] < fv2_node[f2]) {
+            while (f1 < fv1_n && fv1_node[f1] < fv2_node[f2]) f1++;  /* lower_bound */
+        } else {
+            while (f2 < fv2_n && fv2_node[f2] < fv1_node[f1]) f2++;
+        }
+    }
+    if (check_ori) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        ora_compute_three_maxima(hist.size, HISTO_LENGTH, &ind1, &ind2, &ind3);
+        for (int b = 0; b < HISTO_LENGTH; b++) {
+            if (b == ind1 || b == ind2 || b == ind3) continue;
+            for (int j = 0; j < hist.size[b]; j++) {
+                vMatches12[hist.items[b][j]] = -1;
+                nmatches--;
+            }
+        }
+    }
+    int np = 0;
+    for (int i = 0; i < kf1->n; i++) {
+        if (vMatches12[i] < 0) continue;
+        pairs[2 * np] = i;
+        pairs[2 * np + 1] = vMatches12[i];
+        np++;
+    }
+    hist_free(&hist);
+    free(vbMatched2);
+    free(vMatches12);
+    return np;
+}
+
+/* ---------------------------------------------------------------- a18 */
+
+/* Frame::ComputeStereoMatches, Frame.cc:673-885, this fork's semantics: the
+ * median-based outlier pass runs inside the per-keypoint loop (after every left
+ * keypoint that is not skipped by a `continue`), on the entries collected so far;
+ * an empty list is skipped (the reference reads vDistIdx[0] of an empty vector,
+ * whose value cannot matter because the marking loop then runs zero times).
+ * maxD is passed explicitly: the fork computes mbf/mb with mb not yet set
+ * (Frame.cc:711-713, mb is assigned at Frame.cc:174); upstream's value is fx.
+ * levels_l/levels_r: pyramid level ROIs (w_l x h_l, row stride w_l). */
+void ora_compute_stereo_matches(const ora_frame* left, const ora_keypoint* keys_r, const uint8_t* desc_r, int nr,
+                                const uint8_t* const* levels_l, const uint8_t* const* levels_r, const int* level_w,
+                                const int* level_h, const float* inv_scale, float maxD, float* u_right,
+                                float* depth) {
+    const int N = left->n;
+    for (int i = 0; i < N; i++) u_right[i] = -1.0f, depth[i] = -1.0f;
+    const int thOrbDist = (TH_HIGH + TH_LOW) / 2;
+    const int nRows = level_h[0];
+    /* vRowIndices: right keypoint indices per image row (cc:693-708) */
+    int* rcnt = (int*)calloc((size_t)nRows + 1, sizeof(int));
+    for (int pass = 0; pass < 2; pass++) {
+        for (int iR = 0; iR < nr; iR++) {
+            const float kpY = keys_r[iR].y;
+            const float r = 2.0f * left->scale_factors[keys_r[iR].octave];
+            const int maxr = (int)ceilf(kpY + r);
+            const int minr = (int)floorf(kpY - r);
+            for (int yi = minr; yi <= maxr; yi++) {
+                if (yi < 0 || yi >= nRows) continue; /* never happens for keypoints >= 19 px from the border */
+                if (pass == 0) rcnt[yi + 1]++;
+            }
+        }
+        if (pass == 0)
+            for (int y = 0; y < nRows; y++) rcnt[y + 1] += rcnt[y];
+    }
+    int* rows = (int*)malloc(sizeof(int) * (size_t)(rcnt[nRows] + 1));
+    int* fill = (int*)calloc((size_t)nRows, sizeof(int));
+    for (int iR = 0; iR < nr; iR++) {
+        const float kpY = keys_r[iR].y;
+        const float r = 2.0f * left->scale_factors[keys_r[iR].octave];
+        const int maxr = (int)ceilf(kpY + r);
+        const int minr = (int)floorf(kpY - r);
+        for (int yi = minr; yi <= maxr; yi++)
+            if (yi >= 0 && yi < nRows) rows[rcnt[yi] + fill[yi]++] = iR;
+    }
+    const float minD = 0;
+    /* vDistIdx as (dist, iL) pairs kept sorted */
+    int* vd = (int*)malloc(sizeof(int) * 2 * (size_t)(N + 1));
+    int nvd = 0;
+    for (int iL = 0; iL < N; iL++) {
+        const ora_keypoint* kpL = &left->keys[iL];
+        const int levelL = kpL->octave;
+        const float vL = kpL->y, uL = kpL->x;
+        const int row = (int)vL;
+        if (rcnt[row + 1] - rcnt[row] == 0) continue;
+        const float minU = uL - maxD;
+        const float maxU = uL - minD;
+        if (maxU < 0) continue;
+        int bestDist = TH_HIGH;
+        int bestIdxR = 0;
+        const uint8_t* dL = left->desc + (size_t)iL * 32;
+        for (int c = rcnt[row]; c < rcnt[row + 1]; c++) {
+            const int iR = rows[c];
+            const ora_keypoint* kpR = &keys_r[iR];
+            if (kpR->octave < levelL - 1 || kpR->octave > levelL + 1) continue;
+            const float uR = kpR->x;
+            if (uR >= minU && uR <= maxU) {
+                const int dist = hamming(dL, desc_r + (size_t)iR * 32);
+                if (dist < bestDist) {
+                    bestDist = dist;
+                    bestIdxR = iR;
+                }
+            }
+        }
+        if (bestDist < thOrbDist) {
+            const float uR0 = keys_r[bestIdxR].x;
+            const float scaleFactor = inv_scale[levelL];
+            const float scaleduL = roundf(kpL->x * scaleFactor);
+            const float scaledvL = roundf(kpL->y * scaleFactor);
+            const float scaleduR0 = roundf(uR0 * scaleFactor);
+            const int w = 5, L = 5;
+            const int lw = level_w[levelL];
+            const uint8_t* IL = levels_l[levelL];
+            const uint8_t* IR = levels_r[levelL];
+            const int yl0 = (int)scaledvL - w, xl0 = (int)scaleduL - w;
+            const float cl = (float)IL[(size_t)(yl0 + w) * lw + xl0 + w];
+            int bestDistS = INT_MAX;
+            int bestincR = 0;
+            float vDists[11];
+            const float iniu = scaleduR0 + L - w;
+            const float endu = scaleduR0 + L + w + 1;
+            if (iniu < 0 || endu >= level_w[levelL]) continue;
+            for (int incR = -L; incR <= +L; incR++) {
+                const int xr0 = (int)(scaleduR0 + incR - w);
+                const float cr = (float)IR[(size_t)(yl0 + w) * lw + xr0 + w];
+                double acc = 0;
+                for (int yy = 0; yy < 2 * w + 1; yy++)
+                    for (int xx = 0; xx < 2 * w + 1; xx++) {
+                        const float a = (float)IL[(size_t)(yl0 + yy) * lw + xl0 + xx] - cl;
+                        const float b = (float)IR[(size_t)(yl0 + yy) * lw + xr0 + xx] - cr;
+                        acc += fabs((double)a - (double)b);
+                    }
+                const float dist = (float)acc;  /* cv::norm(IL, IR, NORM_L1) */
+                if (dist < bestDistS) {
+                    bestDistS = (int)dist;
+                    bestincR = incR;
+                }
+                vDists[L + incR] = dist;
+            }
+            if (bestincR == -L || bestincR == L) continue;
+            const float dist1 = vDists[L + bestincR - 1];
+            const float dist2 = vDists[L + bestincR];
+            const float dist3 = vDists[L + bestincR + 1];
+            const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+            if (deltaR < -1 || deltaR > 1) continue;
+            float bestuR = left->scale_factors[levelL] * (scaleduR0 + (float)bestincR + deltaR);
+            float disparity = (uL - bestuR);
+            if (disparity >= minD && disparity < maxD) {
+                if (disparity <= 0) {
+                    disparity = 0.01f;
+                    bestuR = (float)(uL - 0.01);
+                }
+                depth[iL] = left->bf / disparity;
+                u_right[iL] = bestuR;
+                /* insert (bestDistS, iL) keeping (dist, idx) order */
+                int pos = nvd;
+                while (pos > 0 && (vd[2 * (pos - 1)] > bestDistS ||
+                                   (vd[2 * (pos - 1)] == bestDistS && vd[2 * (pos - 1) + 1] > iL))) {
+                    vd[2 * pos] = vd[2 * (pos - 1)];
+                    vd[2 * pos + 1] = vd[2 * (pos - 1) + 1];
+                    pos--;
+                }
+                vd[2 * pos] = bestDistS;
+                vd[2 * pos + 1] = iL;
+                nvd++;
+            }
+        }
+        /* outlier pass inside the loop (Frame.cc:868-884) */
+        if (nvd > 0) {
+            const float median = (float)vd[2 * (nvd / 2)];
+            const float thDist = 1.5f * 1.4f * median;
+            for (int i = nvd - 1; i >= 0; i--) {
+                if ((float)vd[2 * i] < thDist) break;
+                u_right[vd[2 * i + 1]] = -1;
+                depth[vd[2 * i + 1]] = -1;
+            }
+        }
+    }
+    free(vd);
+    free(rows);
+    free(fill);
+    free(rcnt);
+}

@@ -1,0 +1,77 @@
+/* orbx_oracle_match.h -- TEST INFRASTRUCTURE ONLY: CPU restatement of the matching
+ * functions (see orbx_oracle_match.c).  Parity status: "parity unpinned" against the
+ * reference binary (OpenCV/Eigen-dependent reference cannot be built here). */
+#ifndef ORBX_ORACLE_MATCH_H
+#define ORBX_ORACLE_MATCH_H
+
+#include <stdint.h>
+
+#include "orbx_oracle.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORA_GRID_COLS 64 /* FRAME_GRID_COLS, Frame.h:37 */
+#define ORA_GRID_ROWS 48 /* FRAME_GRID_ROWS, Frame.h:38 */
+
+/* The Frame / KeyFrame fields the matchers read (Frame.h). */
+typedef struct {
+    int n;                     /* N */
+    const ora_keypoint* keys;  /* mvKeysUn */
+    const uint8_t* desc;       /* mDescriptors, n x 32 */
+    const float* u_right;      /* mvuRight or NULL */
+    float fx, fy, cx, cy, bf, b;
+    float min_x, max_x, min_y, max_y; /* mnMinX, mnMaxX, mnMinY, mnMaxY */
+    int nlevels;
+    const float* scale_factors;  /* mvScaleFactors */
+    const float* level_sigma2;   /* mvLevelSigma2 */
+    float Tcw[12];               /* mTcw rows 0..2, row-major */
+} ora_frame;
+
+typedef struct {
+    float inv_w, inv_h;
+    int start[ORA_GRID_COLS * ORA_GRID_ROWS + 1]; /* cell c = ix*ROWS + iy */
+    int* idx;
+} ora_grid;
+
+typedef struct {
+    int n;
+    const float* pos;            /* GetWorldPos(), n x 3 */
+    const uint8_t* desc;         /* GetDescriptor(), n x 32 */
+    const int32_t* observations; /* Observations() */
+    const uint8_t* bad;          /* isBad() or NULL */
+} ora_mappoints;
+
+/* Frame::IsInFrustum outputs per MapPoint (Frame.cc:412-477) */
+typedef struct {
+    const uint8_t* in_view;     /* mbTrackInView */
+    const float* proj_x;        /* mTrackProjX */
+    const float* proj_y;        /* mTrackProjY */
+    const float* proj_xr;       /* mTrackProjXR */
+    const int32_t* scale_level; /* mnTrackScaleLevel */
+    const float* view_cos;      /* mTrackViewCos */
+} ora_track;
+
+void ora_grid_build(const ora_frame* f, ora_grid* g);
+void ora_grid_free(ora_grid* g);
+int ora_features_in_area(const ora_frame* f, const ora_grid* g, float x, float y, float r, int minLevel, int maxLevel,
+                         int* out, int cap);
+void ora_compute_three_maxima(const int* histo_sizes, int L, int* ind1, int* ind2, int* ind3);
+int ora_sbp_local(const ora_frame* f, int32_t* frame_mp, const int32_t* queries, int nq, const ora_mappoints* mps,
+                  const ora_track* trk, float th, float nnratio);
+int ora_sbp_frame(const ora_frame* cur, int32_t* cur_mp, const ora_frame* last, const int32_t* last_mp,
+                  const uint8_t* last_outlier, const ora_mappoints* mps, float th, int bMono, int check_ori);
+int ora_search_for_triangulation(const ora_frame* kf1, const uint8_t* kf1_has_mp, const int32_t* fv1_node,
+                                 const int32_t* fv1_off, const int32_t* fv1_idx, int fv1_n, const ora_frame* kf2,
+                                 const uint8_t* kf2_has_mp, const int32_t* fv2_node, const int32_t* fv2_off,
+                                 const int32_t* fv2_idx, int fv2_n, const float* F12, int bOnlyStereo, int check_ori,
+                                 int32_t* pairs);
+void ora_compute_stereo_matches(const ora_frame* left, const ora_keypoint* keys_r, const uint8_t* desc_r, int nr,
+                                const uint8_t* const* levels_l, const uint8_t* const* levels_r, const int* level_w,
+                                const int* level_h, const float* inv_scale, float maxD, float* u_right, float* depth);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

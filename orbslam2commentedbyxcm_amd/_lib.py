@@ -31,7 +31,8 @@ EXPORTED = [
     "orbx_extractor_set_timing", "orbx_extractor_stage_times", "orbx_pyramid_level",
     "orbx_pyramid_level_device", "orbx_hamming", "orbx_hamming_matrix_device",
     "orbx_window_match_device", "orbx_window_match", "orbx_version", "orbx_device_count",
-    "orbx_last_error",
+    "orbx_last_error", "orbx_matcher_create", "orbx_matcher_destroy", "orbx_search_by_projection_local",
+    "orbx_search_by_projection_frame", "orbx_search_for_triangulation", "orbx_compute_stereo_matches",
 ]
 
 
@@ -82,6 +83,14 @@ def lib() -> C.CDLL:
     i32p = C.POINTER(C.c_int32)
     L.orbx_window_match.argtypes = [C.c_int, u8p, C.c_int, u8p, C.c_int, i32p, i32p, i32p, C.c_int, i32p, i32p,
                                     i32p, i32p, i32p]
+    L.orbx_matcher_create.argtypes = [C.c_int, C.c_float, C.c_int, C.POINTER(vp)]
+    L.orbx_matcher_destroy.argtypes = [vp]
+    L.orbx_matcher_destroy.restype = None
+    L.orbx_search_by_projection_local.argtypes = [vp, vp, i32p, i32p, C.c_int, vp, vp, C.c_float, ip]
+    L.orbx_search_by_projection_frame.argtypes = [vp, vp, i32p, vp, i32p, u8p, vp, C.c_float, C.c_int, ip]
+    L.orbx_search_for_triangulation.argtypes = [vp, vp, u8p, i32p, i32p, i32p, C.c_int, vp, u8p, i32p, i32p, i32p,
+                                                C.c_int, fp, C.c_int, i32p, ip]
+    L.orbx_compute_stereo_matches.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, u8p, C.c_int, C.c_float, fp, fp]
     L.orbx_version.restype = C.c_char_p
     L.orbx_device_count.argtypes = [ip]
     L.orbx_last_error.restype = C.c_char_p

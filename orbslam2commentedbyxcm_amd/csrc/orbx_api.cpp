@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "orbx.h"
+#include "orbx_error.h"
 #include "orbx_kernels.h"
 
 using namespace orbx;
@@ -21,6 +22,12 @@ using namespace orbx;
 namespace {
 
 thread_local std::string g_last_error;
+
+}  // namespace
+
+void orbx::set_last_error(const std::string& msg) { g_last_error = msg; }
+
+namespace {
 
 int fail(int code, const char* what) {
     g_last_error = what ? what : "";

@@ -5,6 +5,7 @@
 
 #include "orbx.h"
 #include "orbx_geometry.h"
+#include "orbx_match_types.h"
 
 namespace orbx {
 
@@ -45,6 +46,14 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
 // dist[i*nb+j] = Hamming(a_i, b_j)
 hipError_t launch_hamming_matrix(const uint8_t* a, int na, const uint8_t* b, int nb, int32_t* dist,
                                  hipStream_t stream);
+
+hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned long long* scratch,
+                              const long long* d_scratch_off, int max_n, int max_nq, hipStream_t stream);
+
+hipError_t launch_triangulation(const TriProblem* d_probs, int nprob, unsigned long long* scratch, int max_n2,
+                                int max_nq, hipStream_t stream);
+
+hipError_t launch_stereo(const StereoProblem& pb, StereoResult* out, hipStream_t stream);
 
 hipError_t launch_window_match(const uint8_t* qdesc, int nq, const uint8_t* tdesc, const int32_t* tlevel,
                                const int32_t* cand_off, const int32_t* cand, int tie_last,

@@ -111,6 +111,492 @@ __global__ __launch_bounds__(256) void k_window_match(const uint8_t* __restrict_
     }
 }
 
+// ------------------------------------------------------------------ projection search
+
+__device__ __forceinline__ bool kp_blocked(int fmp, const ProjParams& P) {
+    if (fmp < 0) return false;
+    return P.blocked_mode == 1 || P.mp_obs[fmp] > 0;
+}
+
+struct CellRange {
+    int x0, x1, y0, y1;
+    bool empty;
+};
+
+// Frame::GetFeaturesInArea cell range (Frame.cc:495-515), same float expressions.
+__device__ __forceinline__ CellRange cell_range(const ProjProblem& pb, float x, float y, float r) {
+    CellRange c;
+    int t = (int)floorf((x - pb.min_x - r) * pb.inv_w);
+    c.x0 = t > 0 ? t : 0;
+    t = (int)ceilf((x - pb.min_x + r) * pb.inv_w);
+    c.x1 = t < kGridCols - 1 ? t : kGridCols - 1;
+    t = (int)floorf((y - pb.min_y - r) * pb.inv_h);
+    c.y0 = t > 0 ? t : 0;
+    t = (int)ceilf((y - pb.min_y + r) * pb.inv_h);
+    c.y1 = t < kGridRows - 1 ? t : kGridRows - 1;
+    c.empty = c.x0 >= kGridCols || c.x1 < 0 || c.y0 >= kGridRows || c.y1 < 0;
+    return c;
+}
+
+constexpr unsigned long long kNoKey = ~0ull;
+
+// Top-2 (distance, candidate order) keys of query Q over the frame's keypoints, with the
+// candidate set of GetFeaturesInArea + the overload's filters.  Candidate order is
+// the reference's iteration order: grid column, grid row, keypoint index.
+__device__ void score_query(const ProjProblem& pb, const ProjParams& P, const ProjQuery& Q,
+                            const unsigned long long q0, const unsigned long long q1, const unsigned long long q2,
+                            const unsigned long long q3, const float* kx, const float* ky, const int* meta,
+                            const int* fmp, unsigned long long& k1, unsigned long long& k2) {
+    const int lane = threadIdx.x & 63;
+    k1 = kNoKey;
+    k2 = kNoKey;
+    const CellRange cr = cell_range(pb, Q.u, Q.v, Q.r);
+    if (!cr.empty) {
+        const bool check_levels = (Q.min_level > 0) || (Q.max_level >= 0);
+        for (int i = lane; i < pb.n; i += 64) {
+            const int m = meta[i];
+            const int cell = m >> 8;
+            if (cell == 0xfff) continue;
+            const int cx = cell / kGridRows, cy = cell - cx * kGridRows;
+            if (cx < cr.x0 || cx > cr.x1 || cy < cr.y0 || cy > cr.y1) continue;
+            const int oct = m & 0xff;
+            if (check_levels) {
+                if (oct < Q.min_level) continue;
+                if (Q.max_level >= 0 && oct > Q.max_level) continue;
+            }
+            const float distx = kx[i] - Q.u;
+            const float disty = ky[i] - Q.v;
+            if (!(fabsf(distx) < Q.r && fabsf(disty) < Q.r)) continue;
+            if (Q.post_min >= 0 && (oct < Q.post_min || oct > Q.post_max)) continue;
+            if (kp_blocked(fmp[i], P)) continue;
+            if (Q.er_max >= 0.f && pb.u_right && pb.u_right[i] > 0) {
+                const float er = fabsf(Q.ur - pb.u_right[i]);
+                if (er > Q.er_max) continue;
+            }
+            const unsigned long long* t = (const unsigned long long*)(pb.desc + (size_t)i * 32);
+            const int d = __popcll(q0 ^ t[0]) + __popcll(q1 ^ t[1]) + __popcll(q2 ^ t[2]) + __popcll(q3 ^ t[3]);
+            const unsigned long long key = ((unsigned long long)d << 25) | ((unsigned long long)cell << 13) | (unsigned)i;
+            if (key < k1) { k2 = k1; k1 = key; }
+            else if (key < k2) { k2 = key; }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long o1 = __shfl_xor(k1, o), o2 = __shfl_xor(k2, o);
+        const unsigned long long hi = k1 < o1 ? o1 : k1;
+        const unsigned long long lo2 = k2 < o2 ? k2 : o2;
+        k1 = k1 < o1 ? k1 : o1;
+        k2 = hi < lo2 ? hi : lo2;
+    }
+}
+
+__device__ __forceinline__ int key_idx(unsigned long long k) { return (int)(k & 0x1fffu); }
+__device__ __forceinline__ int key_dist(unsigned long long k) { return (int)(k >> 25); }
+
+// One workgroup per problem (one SearchByProjection call).  Waves score the queries in
+// parallel against the keypoints' initial mvpMapPoints state; wave 0 then replays the
+// reference's sequential loop: each query claims its best keypoint in order, and a
+// query whose best (or, with the ratio test, second) keypoint was claimed by an
+// earlier query is re-scored against the current state.  Finally the rotation
+// histogram (ORBmatcher.cc:1750-1786) un-matches bins outside the three maxima.
+__global__ __launch_bounds__(256) void k_proj_search(const ProjProblem* __restrict__ probs, ProjParams P,
+                                                     unsigned long long* __restrict__ scratch,
+                                                     const long long* __restrict__ scratch_off) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ int s_hist[kHistoLength];
+    const ProjProblem pb = probs[blockIdx.x];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = pb.n;
+    float* kx = (float*)smem;
+    float* ky = kx + n;
+    int* meta = (int*)(ky + n);
+    int* fmp = meta + n;
+    int* mlist = fmp + n;                                                // matched kp per accepted query
+    int* mbin = mlist + pb.nq;                                           // its rotation bin
+    unsigned long long* keys2 = scratch + scratch_off[blockIdx.x];      // 2 per query
+    for (int i = tid; i < n; i += 256) {
+        const orbx_keypoint kp = pb.keys[i];
+        kx[i] = kp.x;
+        ky[i] = kp.y;
+        const int px = (int)roundf((kp.x - pb.min_x) * pb.inv_w);  // Frame::PosInGrid, Frame.cc:558-567
+        const int py = (int)roundf((kp.y - pb.min_y) * pb.inv_h);
+        const int cell = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? 0xfff : px * kGridRows + py;
+        meta[i] = (kp.octave & 0xff) | (cell << 8);
+        fmp[i] = pb.frame_mp[i];
+    }
+    if (tid < kHistoLength) s_hist[tid] = 0;
+    __syncthreads();
+    for (int q = wave; q < pb.nq; q += 4) {
+        const ProjQuery Q = pb.q[q];
+        unsigned long long k1 = kNoKey, k2 = kNoKey;
+        if (Q.mp >= 0) {
+            const unsigned long long* qd = (const unsigned long long*)(pb.qdesc + (size_t)q * 32);
+            score_query(pb, P, Q, qd[0], qd[1], qd[2], qd[3], kx, ky, meta, fmp, k1, k2);
+        }
+        if (lane == 0) {
+            keys2[2 * q] = k1;
+            keys2[2 * q + 1] = k2;
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        int nmatch = 0, nrec = 0;
+        const float factor = kHistoLength / 360.0f;
+        for (int q = 0; q < pb.nq; q++) {
+            const ProjQuery Q = pb.q[q];
+            if (Q.mp < 0) continue;
+            unsigned long long k1 = keys2[2 * q], k2 = keys2[2 * q + 1];
+            bool stale = (k1 != kNoKey && kp_blocked(fmp[key_idx(k1)], P)) ||
+                         (P.ratio_mode && k2 != kNoKey && kp_blocked(fmp[key_idx(k2)], P));
+            if (stale) {
+                const unsigned long long* qd = (const unsigned long long*)(pb.qdesc + (size_t)q * 32);
+                score_query(pb, P, Q, qd[0], qd[1], qd[2], qd[3], kx, ky, meta, fmp, k1, k2);
+            }
+            if (k1 == kNoKey) continue;
+            const int bestDist = key_dist(k1);
+            if (bestDist > P.accept_th) continue;
+            const int idx1 = key_idx(k1);
+            if (P.ratio_mode) {
+                const int bestLevel = meta[idx1] & 0xff;
+                const int bestLevel2 = k2 == kNoKey ? -1 : (meta[key_idx(k2)] & 0xff);
+                const int bestDist2 = k2 == kNoKey ? 256 : key_dist(k2);
+                if (bestLevel == bestLevel2 && (float)bestDist > P.nnratio * (float)bestDist2) continue;
+            }
+            if (lane == 0) fmp[idx1] = Q.mp;
+            nmatch++;
+            if (P.check_ori) {
+                float rot = Q.angle - pb.keys[idx1].angle;
+                if (rot < 0.0f) rot += 360.0f;
+                int bin = (int)roundf(rot * factor);
+                if (bin == kHistoLength) bin = 0;
+                if (lane == 0) {
+                    mlist[nrec] = idx1;
+                    mbin[nrec] = bin;
+                    s_hist[bin]++;
+                }
+                nrec++;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        if (P.check_ori) {
+            // ComputeThreeMaxima, ORBmatcher.cc:1935-1977
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < kHistoLength; i++) {
+                const int s = s_hist[i];
+                if (s > max1) {
+                    max3 = max2; max2 = max1; max1 = s;
+                    ind3 = ind2; ind2 = ind1; ind1 = i;
+                } else if (s > max2) {
+                    max3 = max2; max2 = s;
+                    ind3 = ind2; ind2 = i;
+                } else if (s > max3) {
+                    max3 = s;
+                    ind3 = i;
+                }
+            }
+            if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+            else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+            for (int m = lane; m < nrec; m += 64) {
+                const int b = mbin[m];
+                if (b != ind1 && b != ind2 && b != ind3) fmp[mlist[m]] = -1;
+            }
+            int bad = 0;
+            for (int m = lane; m < nrec; m += 64) {
+                const int b = mbin[m];
+                bad += (b != ind1 && b != ind2 && b != ind3);
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o);
+            nmatch -= bad;
+        }
+        if (lane == 0) *pb.nmatches = nmatch;
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) pb.frame_mp[i] = fmp[i];
+}
+
+hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned long long* scratch,
+                              const long long* d_scratch_off, int max_n, int max_nq, hipStream_t stream) {
+    if (nprob <= 0) return hipSuccess;
+    const size_t lds = (size_t)max_n * 16 + (size_t)max_nq * 8;
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_proj_search, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_proj_search, dim3(nprob), dim3(256), lds, stream, d_probs, P, scratch, d_scratch_off);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ triangulation
+
+// One query of SearchForTriangulation = one unmatched KF1 keypoint inside a vocabulary
+// node shared with KF2 (ORBmatcher.cc:886-1019), in the reference's visiting order.
+__device__ void score_tri(const TriProblem& pb, const TriQuery& Q, const uint8_t* matched2,
+                          unsigned long long& best) {
+    const int lane = threadIdx.x & 63;
+    best = kNoKey;
+    const orbx_keypoint kp1 = pb.keys1[Q.idx1];
+    const unsigned long long* d1 = (const unsigned long long*)(pb.desc1 + (size_t)Q.idx1 * 32);
+    const unsigned long long q0 = d1[0], q1 = d1[1], q2 = d1[2], q3 = d1[3];
+    // epipolar line of kp1 in KF2 (CheckDistEpipolarLine, ORBmatcher.cc:186-213)
+    const float* F = pb.F12;
+    const float a = kp1.x * F[0] + kp1.y * F[3] + F[6];
+    const float b = kp1.x * F[1] + kp1.y * F[4] + F[7];
+    const float c = kp1.x * F[2] + kp1.y * F[5] + F[8];
+    for (int p = Q.beg + lane; p < Q.end; p += 64) {
+        const int idx2 = pb.fv2_idx[p];
+        if (matched2[idx2] || pb.has_mp2[idx2]) continue;
+        const bool stereo2 = pb.u_right2 && pb.u_right2[idx2] >= 0;
+        if (pb.only_stereo && !stereo2) continue;
+        const unsigned long long* t = (const unsigned long long*)(pb.desc2 + (size_t)idx2 * 32);
+        const int dist = __popcll(q0 ^ t[0]) + __popcll(q1 ^ t[1]) + __popcll(q2 ^ t[2]) + __popcll(q3 ^ t[3]);
+        if (dist > 50) continue;  // TH_LOW; the running bestDist bound is applied by the key order
+        const orbx_keypoint kp2 = pb.keys2[idx2];
+        if (!Q.stereo1 && !stereo2) {
+            const float distex = pb.ex - kp2.x;
+            const float distey = pb.ey - kp2.y;
+            if (distex * distex + distey * distey < 100 * pb.scale2[kp2.octave]) continue;
+        }
+        const float num = a * kp2.x + b * kp2.y + c;
+        const float den = a * a + b * b;
+        if (den == 0) continue;
+        const float dsqr = num * num / den;
+        if (!((double)dsqr < 3.84 * (double)pb.sigma2_2[kp2.octave])) continue;
+        // accepted candidates replace the best on dist <= bestDist: min distance, last position
+        const unsigned long long key = ((unsigned long long)dist << 32) | (0xffffffffu - (unsigned)(p - Q.beg));
+        best = key < best ? key : best;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long ob = __shfl_xor(best, o);
+        best = ob < best ? ob : best;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_triangulation(const TriProblem* __restrict__ probs,
+                                                       unsigned long long* __restrict__ scratch) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ int s_hist[kHistoLength];
+    const TriProblem pb = probs[blockIdx.x];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint8_t* matched2 = smem;  // vbMatched2, n2 bytes
+    int* mlist = (int*)(smem + ((pb.n2 + 15) & ~15));
+    int* mbin = mlist + pb.nq;
+    for (int i = tid; i < pb.n2; i += 256) matched2[i] = 0;
+    if (tid < kHistoLength) s_hist[tid] = 0;
+    __syncthreads();
+    unsigned long long* keys = scratch + pb.scratch_off;
+    for (int q = wave; q < pb.nq; q += 4) {
+        unsigned long long best;
+        score_tri(pb, pb.q[q], matched2, best);
+        if (lane == 0) keys[q] = best;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        int nrec = 0;
+        const float factor = kHistoLength / 360.0f;
+        for (int q = 0; q < pb.nq; q++) {
+            const TriQuery Q = pb.q[q];
+            unsigned long long best = keys[q];
+            if (best != kNoKey) {
+                const int idx2 = pb.fv2_idx[Q.beg + (int)(0xffffffffu - (unsigned)(best & 0xffffffffu))];
+                if (matched2[idx2]) score_tri(pb, Q, matched2, best);
+            }
+            int idx2 = -1;
+            if (best != kNoKey) idx2 = pb.fv2_idx[Q.beg + (int)(0xffffffffu - (unsigned)(best & 0xffffffffu))];
+            if (lane == 0) pb.matches12[Q.idx1] = idx2;
+            if (idx2 < 0) continue;
+            if (lane == 0) matched2[idx2] = 1;
+            if (pb.check_ori) {
+                float rot = pb.keys1[Q.idx1].angle - pb.keys2[idx2].angle;
+                if (rot < 0.0f) rot += 360.0f;
+                int bin = (int)roundf(rot * factor);
+                if (bin == kHistoLength) bin = 0;
+                if (lane == 0) {
+                    mlist[nrec] = Q.idx1;
+                    mbin[nrec] = bin;
+                    s_hist[bin]++;
+                }
+                nrec++;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        if (pb.check_ori) {
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < kHistoLength; i++) {
+                const int s = s_hist[i];
+                if (s > max1) {
+                    max3 = max2; max2 = max1; max1 = s;
+                    ind3 = ind2; ind2 = ind1; ind1 = i;
+                } else if (s > max2) {
+                    max3 = max2; max2 = s;
+                    ind3 = ind2; ind2 = i;
+                } else if (s > max3) {
+                    max3 = s;
+                    ind3 = i;
+                }
+            }
+            if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+            else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+            for (int m = lane; m < nrec; m += 64) {
+                const int b = mbin[m];
+                if (b != ind1 && b != ind2 && b != ind3) pb.matches12[mlist[m]] = -1;
+            }
+        }
+    }
+}
+
+hipError_t launch_triangulation(const TriProblem* d_probs, int nprob, unsigned long long* scratch, int max_n2,
+                                int max_nq, hipStream_t stream) {
+    if (nprob <= 0) return hipSuccess;
+    const size_t lds = (size_t)((max_n2 + 15) & ~15) + (size_t)max_nq * 8;
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_triangulation, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_triangulation, dim3(nprob), dim3(256), lds, stream, d_probs, scratch);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ stereo
+
+// One wave per left keypoint: Frame::ComputeStereoMatches' row-band Hamming search,
+// 11x11 SAD refinement on the pyramid level over shifts -5..5 and the parabola fit
+// (Frame.cc:724-866).  The per-keypoint results feed the host's sequential outlier
+// pass (Frame.cc:868-884).
+__global__ __launch_bounds__(256) void k_stereo(StereoProblem pb, StereoResult* __restrict__ out) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int iL = blockIdx.x * 4 + wave;
+    if (iL >= pb.nl) return;
+    StereoResult res;
+    res.reach_sort = 0;
+    res.pushed = 0;
+    res.dist = 0;
+    res.u_right = -1.f;
+    res.depth = -1.f;
+    const orbx_keypoint kpL = pb.keys_l[iL];
+    const int levelL = kpL.octave;
+    const float vL = kpL.y, uL = kpL.x;
+    const int row = (int)vL;
+    const int cbeg = pb.row_off[row], cend = pb.row_off[row + 1];
+    const float minD = 0.f;
+    if (cend == cbeg || uL - minD < 0) {
+        if (lane == 0) out[iL] = res;
+        return;
+    }
+    const float minU = uL - pb.max_d, maxU = uL - minD;
+    const unsigned long long* dl = (const unsigned long long*)(pb.desc_l + (size_t)iL * 32);
+    const unsigned long long q0 = dl[0], q1 = dl[1], q2 = dl[2], q3 = dl[3];
+    unsigned long long best = kNoKey;
+    for (int p = cbeg + lane; p < cend; p += 64) {
+        const int iR = pb.row_idx[p];
+        const orbx_keypoint kpR = pb.keys_r[iR];
+        if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
+        const float uR = kpR.x;
+        if (uR >= minU && uR <= maxU) {
+            const unsigned long long* t = (const unsigned long long*)(pb.desc_r + (size_t)iR * 32);
+            const int d = __popcll(q0 ^ t[0]) + __popcll(q1 ^ t[1]) + __popcll(q2 ^ t[2]) + __popcll(q3 ^ t[3]);
+            const unsigned long long key = ((unsigned long long)d << 32) | (unsigned)(p - cbeg);
+            best = key < best ? key : best;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long ob = __shfl_xor(best, o);
+        best = ob < best ? ob : best;
+    }
+    res.reach_sort = 1;
+    const int bestDist = best == kNoKey ? 100 : (int)(best >> 32);  // starts at TH_HIGH, strict <
+    if (bestDist < 75) {                                             // thOrbDist = (TH_HIGH + TH_LOW) / 2
+        const int bestIdxR = pb.row_idx[cbeg + (int)(best & 0xffffffffu)];
+        const float uR0 = pb.keys_r[bestIdxR].x;
+        const float scaleFactor = pb.inv_scale[levelL];
+        const float scaleduL = roundf(kpL.x * scaleFactor);
+        const float scaledvL = roundf(kpL.y * scaleFactor);
+        const float scaleduR0 = roundf(uR0 * scaleFactor);
+        const int w = 5, L = 5;
+        const float iniu = scaleduR0 + L - w;
+        const float endu = scaleduR0 + L + w + 1;
+        if (iniu < 0 || endu >= pb.level_w[levelL]) {
+            res.reach_sort = 0;
+            if (lane == 0) out[iL] = res;
+            return;
+        }
+        const int pitch = pb.level_pitch[levelL];
+        const uint8_t* IL = pb.lev_l[levelL];
+        const uint8_t* IR = pb.lev_r[levelL];
+        const int yl0 = (int)scaledvL - w, xl0 = (int)scaleduL - w;
+        const int cl = IL[(size_t)(yl0 + w) * pitch + xl0 + w];
+        float vd[11];
+        int bestDistS = 0x7fffffff, bestincR = 0;
+#pragma unroll
+        for (int incR = -L; incR <= L; incR++) {
+            const int xr0 = (int)(scaleduR0 + incR - w);
+            const int cr = IR[(size_t)(yl0 + w) * pitch + xr0 + w];
+            int acc = 0;
+            for (int k = lane; k < 121; k += 64) {
+                const int yy = k / 11, xx = k - yy * 11;
+                const int a = (int)IL[(size_t)(yl0 + yy) * pitch + xl0 + xx] - cl;
+                const int b = (int)IR[(size_t)(yl0 + yy) * pitch + xr0 + xx] - cr;
+                acc += a > b ? a - b : b - a;
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+            const float dist = (float)acc;  // cv::norm(IL, IR, NORM_L1) on integer-valued floats
+            if (dist < (float)bestDistS) {
+                bestDistS = (int)dist;
+                bestincR = incR;
+            }
+            vd[L + incR] = dist;
+        }
+        if (bestincR == -L || bestincR == L) {
+            res.reach_sort = 0;
+            if (lane == 0) out[iL] = res;
+            return;
+        }
+        float dist1 = vd[0], dist2 = vd[0], dist3 = vd[0];
+#pragma unroll
+        for (int k = 0; k < 11; k++) {
+            if (k == L + bestincR - 1) dist1 = vd[k];
+            if (k == L + bestincR) dist2 = vd[k];
+            if (k == L + bestincR + 1) dist3 = vd[k];
+        }
+        const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+        if (deltaR < -1 || deltaR > 1) {
+            res.reach_sort = 0;
+            if (lane == 0) out[iL] = res;
+            return;
+        }
+        float bestuR = pb.scale[levelL] * (scaleduR0 + (float)bestincR + deltaR);
+        float disparity = (uL - bestuR);
+        if (disparity >= minD && disparity < pb.max_d) {
+            if (disparity <= 0) {
+                disparity = 0.01f;
+                bestuR = (float)((double)uL - 0.01);
+            }
+            res.depth = pb.bf / disparity;
+            res.u_right = bestuR;
+            res.pushed = 1;
+            res.dist = bestDistS;
+        }
+    }
+    if (lane == 0) out[iL] = res;
+}
+
+hipError_t launch_stereo(const StereoProblem& pb, StereoResult* out, hipStream_t stream) {
+    if (pb.nl <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_stereo, dim3((pb.nl + 3) / 4), dim3(256), 0, stream, pb, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_hamming_matrix(const uint8_t* a, int na, const uint8_t* b, int nb, int32_t* dist,
                                  hipStream_t stream) {
     if (na <= 0 || nb <= 0) return hipSuccess;

@@ -1,0 +1,109 @@
+// orbx_match_types.h -- device-side records of the projection-search matcher.
+//
+// One "problem" = one ORBmatcher::SearchByProjection call: the keypoints of the frame
+// being searched (mvKeysUn, mDescriptors, mvuRight, mvpMapPoints) and the ordered
+// list of projected queries (MapPoints).  Shared by host and device code.
+#pragma once
+
+#include <cstdint>
+
+#include "orbx.h"
+
+namespace orbx {
+
+constexpr int kGridCols = 64;  // FRAME_GRID_COLS, Frame.h:37
+constexpr int kGridRows = 48;  // FRAME_GRID_ROWS, Frame.h:38
+constexpr int kHistoLength = 30;  // ORBmatcher::HISTO_LENGTH, ORBmatcher.cc:40
+
+// One projected MapPoint, in the reference's iteration order.
+struct ProjQuery {
+    float u, v;           // window centre (projection)
+    float ur;             // projected right-image u (stereo check)
+    float r;              // GetFeaturesInArea radius
+    float er_max;         // reject if |ur - mvuRight| > er_max where mvuRight > 0; < 0 = no check
+    int min_level, max_level;  // GetFeaturesInArea level arguments
+    int post_min, post_max;    // extra candidate level filter [post_min, post_max] (-1 = none)
+    int mp;               // MapPoint id written to mvpMapPoints on a match; < 0 = skip query
+    float angle;          // keypoint angle of the query (rotation histogram)
+    int pad[2];
+};
+
+struct ProjProblem {
+    const orbx_keypoint* keys;  // n keypoints of the searched frame (mvKeysUn)
+    const uint8_t* desc;        // n x 32
+    const float* u_right;       // n or null
+    int32_t* frame_mp;          // n, in/out: mvpMapPoints as MapPoint ids, -1 = NULL
+    int n;
+    const ProjQuery* q;         // nq queries
+    const uint8_t* qdesc;       // nq x 32 MapPoint descriptors
+    int nq;
+    float min_x, min_y, inv_w, inv_h;  // mnMinX, mnMinY, mfGridElementWidthInv/HeightInv
+    int32_t* nmatches;          // out
+};
+
+// Call-level semantics of the SearchByProjection overload being executed.
+struct ProjParams {
+    const int32_t* mp_obs;  // Observations() per MapPoint id (blocked_mode 0)
+    int blocked_mode;       // 0: skip kp if mvpMapPoints[i] && ->Observations() > 0 (a11, a12)
+                            // 1: skip kp if mvpMapPoints[i] (a13, a14)
+    int accept_th;          // best distance threshold (<=): TH_HIGH, ORBdist or TH_LOW
+    int ratio_mode;         // 1: reject if bestLevel==bestLevel2 && best > nnratio*second (a11)
+    float nnratio;
+    int check_ori;          // rotation-consistency histogram (a12, a13)
+};
+
+// SearchForTriangulation: one unmatched KF1 keypoint of a shared vocabulary node.
+struct TriQuery {
+    int idx1;       // KF1 keypoint
+    int beg, end;   // its node's KF2 keypoints: fv2_idx[beg..end)
+    int stereo1;    // mvuRight[idx1] >= 0
+};
+
+struct TriProblem {
+    const orbx_keypoint* keys1;
+    const uint8_t* desc1;
+    const orbx_keypoint* keys2;
+    const uint8_t* desc2;
+    const float* u_right2;      // or null
+    const uint8_t* has_mp2;     // KF2 keypoint already has a MapPoint
+    const int32_t* fv2_idx;
+    const float* scale2;        // KF2 mvScaleFactors
+    const float* sigma2_2;      // KF2 mvLevelSigma2
+    float F12[9];
+    float ex, ey;               // epipole of KF1's centre in KF2
+    int only_stereo;
+    int check_ori;
+    int n2;
+    const TriQuery* q;
+    int nq;
+    int32_t* matches12;         // out: vMatches12 (KF1 n), pre-filled with -1
+    long long scratch_off;
+};
+
+struct StereoProblem {
+    const orbx_keypoint* keys_l;
+    const uint8_t* desc_l;
+    int nl;
+    const orbx_keypoint* keys_r;
+    const uint8_t* desc_r;
+    const int32_t* row_off;     // vRowIndices as CSR over image rows
+    const int32_t* row_idx;
+    const uint8_t* lev_l[32];   // mvImagePyramid ROIs of the left / right extractor
+    const uint8_t* lev_r[32];
+    int level_pitch[32];
+    int level_w[32];
+    float scale[32];            // mvScaleFactors
+    float inv_scale[32];        // mvInvScaleFactors
+    float bf;                   // mbf
+    float max_d;                // maxD = mbf / minZ
+};
+
+struct StereoResult {
+    int reach_sort;  // the iteration reaches the in-loop outlier pass (no `continue`)
+    int pushed;      // (dist, iL) was appended to vDistIdx
+    int dist;        // SAD distance pushed
+    float u_right;
+    float depth;
+};
+
+}  // namespace orbx

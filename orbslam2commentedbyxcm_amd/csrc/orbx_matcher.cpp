@@ -1,0 +1,521 @@
+// orbx_matcher.cpp -- host side of the ORBmatcher drop-in (include/orbx.h).
+//
+// Each entry point restates the reference function's object-graph walk on the host
+// (projection of MapPoints, query filtering, vocabulary-node merge, row bands) and
+// hands the dense part -- candidate windows, Hamming scoring, the ordered commit --
+// to one kernel launch on the matcher's stream.  MapPoint* pointers are represented
+// by integer ids; mvpMapPoints arrays hold ids (-1 = NULL).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "orbx.h"
+#include "orbx_error.h"
+#include "orbx_kernels.h"
+
+using namespace orbx;
+
+namespace {
+
+int fail(int code, const char* what) {
+    set_last_error(what);
+    return code;
+}
+
+#define HIP_TRY(expr)                                                               \
+    do {                                                                            \
+        hipError_t _e = (expr);                                                     \
+        if (_e != hipSuccess) {                                                     \
+            set_last_error(std::string(#expr) + ": " + hipGetErrorString(_e));      \
+            return ORBX_ERR_HIP;                                                    \
+        }                                                                           \
+    } while (0)
+
+constexpr int TH_HIGH = 100;  // ORBmatcher.cc:38
+constexpr int TH_LOW = 50;    // ORBmatcher.cc:39
+
+// Grow-only device arena, reset per call.
+struct Arena {
+    char* base = nullptr;
+    size_t cap = 0, used = 0;
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (base) (void)hipFree(base);
+        base = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc((void**)&base, bytes);
+        if (e == hipSuccess) cap = bytes;
+        return e;
+    }
+    template <typename T>
+    T* take(size_t n) {
+        used = (used + 255) & ~(size_t)255;
+        T* p = (T*)(base + used);
+        used += sizeof(T) * (n ? n : 1);
+        return p;
+    }
+};
+
+size_t pad(size_t b) { return ((b + 255) & ~(size_t)255) + 256; }
+
+// x_c = R x + t, float products summed left to right (gemm accumulation unpinned)
+void project(const float* Tcw, const float* X, float* xc) {
+    for (int r = 0; r < 3; r++)
+        xc[r] = Tcw[4 * r] * X[0] + Tcw[4 * r + 1] * X[1] + Tcw[4 * r + 2] * X[2] + Tcw[4 * r + 3];
+}
+
+// camera centre -R^T t
+void centre(const float* Tcw, float* c) {
+    for (int k = 0; k < 3; k++) c[k] = -(Tcw[k] * Tcw[3] + Tcw[4 + k] * Tcw[7] + Tcw[8 + k] * Tcw[11]);
+}
+
+}  // namespace
+
+struct orbx_matcher {
+    int device = 0;
+    float nnratio = 0.6f;
+    int check_ori = 1;
+    hipStream_t stream = nullptr;
+    Arena arena;
+};
+
+namespace {
+
+// Upload one frame view + queries and run k_proj_search for a single problem.
+int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const std::vector<ProjQuery>& qs,
+             const std::vector<uint8_t>& qdesc, const orbx_mappoints* mps, const ProjParams& base_params,
+             int* nmatches) {
+    const int n = f->n, nq = (int)qs.size();
+    if (nq == 0 || n == 0) {
+        if (nmatches) *nmatches = 0;
+        return ORBX_OK;
+    }
+    HIP_TRY(hipSetDevice(m->device));
+    const int nobs = mps->n;
+    size_t need = pad(sizeof(orbx_keypoint) * n) + pad((size_t)n * 32) + pad(sizeof(float) * n) +
+                  pad(sizeof(int32_t) * n) + pad(sizeof(ProjQuery) * nq) + pad((size_t)nq * 32) +
+                  pad(sizeof(int32_t) * (nobs ? nobs : 1)) + pad(sizeof(ProjProblem)) + pad(16 * (size_t)nq) +
+                  pad(sizeof(long long)) + pad(sizeof(int32_t));
+    HIP_TRY(m->arena.reserve(need));
+    m->arena.used = 0;
+    auto* d_keys = m->arena.take<orbx_keypoint>(n);
+    auto* d_desc = m->arena.take<uint8_t>((size_t)n * 32);
+    auto* d_ur = m->arena.take<float>(n);
+    auto* d_fmp = m->arena.take<int32_t>(n);
+    auto* d_q = m->arena.take<ProjQuery>(nq);
+    auto* d_qd = m->arena.take<uint8_t>((size_t)nq * 32);
+    auto* d_obs = m->arena.take<int32_t>(nobs ? nobs : 1);
+    auto* d_prob = m->arena.take<ProjProblem>(1);
+    auto* d_scr = m->arena.take<unsigned long long>(2 * (size_t)nq);
+    auto* d_off = m->arena.take<long long>(1);
+    auto* d_nm = m->arena.take<int32_t>(1);
+    hipStream_t s = m->stream;
+    HIP_TRY(hipMemcpyAsync(d_keys, f->keys, sizeof(orbx_keypoint) * n, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_desc, f->desc, (size_t)n * 32, hipMemcpyHostToDevice, s));
+    if (f->u_right) HIP_TRY(hipMemcpyAsync(d_ur, f->u_right, sizeof(float) * n, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_fmp, frame_mp, sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_q, qs.data(), sizeof(ProjQuery) * nq, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_qd, qdesc.data(), (size_t)nq * 32, hipMemcpyHostToDevice, s));
+    if (nobs && mps->observations)
+        HIP_TRY(hipMemcpyAsync(d_obs, mps->observations, sizeof(int32_t) * nobs, hipMemcpyHostToDevice, s));
+    ProjProblem pb{};
+    pb.keys = d_keys;
+    pb.desc = d_desc;
+    pb.u_right = f->u_right ? d_ur : nullptr;
+    pb.frame_mp = d_fmp;
+    pb.n = n;
+    pb.q = d_q;
+    pb.qdesc = d_qd;
+    pb.nq = nq;
+    pb.min_x = f->min_x;
+    pb.min_y = f->min_y;
+    pb.inv_w = (float)kGridCols / (f->max_x - f->min_x);  // Frame.cc:157-159
+    pb.inv_h = (float)kGridRows / (f->max_y - f->min_y);
+    pb.nmatches = d_nm;
+    const long long zero = 0;
+    HIP_TRY(hipMemcpyAsync(d_prob, &pb, sizeof(pb), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_off, &zero, sizeof(zero), hipMemcpyHostToDevice, s));
+    ProjParams P = base_params;
+    P.mp_obs = d_obs;
+    HIP_TRY(launch_proj_search(d_prob, 1, P, d_scr, d_off, n, nq, s));
+    int nm = 0;
+    HIP_TRY(hipMemcpyAsync(frame_mp, d_fmp, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&nm, d_nm, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (nmatches) *nmatches = nm;
+    return ORBX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int orbx_matcher_create(int device, float nnratio, int check_ori, orbx_matcher** out) {
+    if (!out) return fail(ORBX_ERR_ARG, "null out");
+    *out = nullptr;
+    orbx_matcher* m = new (std::nothrow) orbx_matcher();
+    if (!m) return fail(ORBX_ERR_ARG, "out of host memory");
+    m->device = device;
+    m->nnratio = nnratio;
+    m->check_ori = check_ori ? 1 : 0;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete m;
+        set_last_error(std::string("orbx_matcher_create: ") + hipGetErrorString(e));
+        return ORBX_ERR_HIP;
+    }
+    *out = m;
+    return ORBX_OK;
+}
+
+void orbx_matcher_destroy(orbx_matcher* m) {
+    if (!m) return;
+    (void)hipSetDevice(m->device);
+    if (m->stream) (void)hipStreamSynchronize(m->stream);
+    if (m->arena.base) (void)hipFree(m->arena.base);
+    if (m->stream) (void)hipStreamDestroy(m->stream);
+    delete m;
+}
+
+// ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th), ORBmatcher.cc:61-173
+int orbx_search_by_projection_local(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp,
+                                    const int32_t* queries, int nq, const orbx_mappoints* mps, const orbx_track* trk,
+                                    float th, int* nmatches) {
+    if (!m || !f || !frame_mp || !mps || !trk || (nq && !queries)) return fail(ORBX_ERR_ARG, "null argument");
+    const bool bFactor = th != 1.0;  // ORBmatcher.cc:66
+    std::vector<ProjQuery> qs;
+    std::vector<uint8_t> qd;
+    qs.reserve(nq);
+    qd.reserve((size_t)nq * 32);
+    for (int i = 0; i < nq; i++) {
+        const int mp = queries[i];
+        if (mp < 0 || mp >= mps->n) return fail(ORBX_ERR_ARG, "MapPoint id out of range");
+        if (!trk->in_view[mp]) continue;
+        if (mps->bad && mps->bad[mp]) continue;
+        const int pred = trk->scale_level[mp];
+        if (pred < 0 || pred >= f->nlevels) return fail(ORBX_ERR_ARG, "predicted level out of range");
+        float r = trk->view_cos[mp] > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos, ORBmatcher.cc:176-183
+        if (bFactor) r *= th;
+        ProjQuery q{};
+        q.u = trk->proj_x[mp];
+        q.v = trk->proj_y[mp];
+        q.ur = trk->proj_xr[mp];
+        q.r = r * f->scale_factors[pred];
+        q.er_max = r * f->scale_factors[pred];
+        q.min_level = pred - 1;
+        q.max_level = pred;
+        q.post_min = -1;
+        q.post_max = -1;
+        q.mp = mp;
+        q.angle = 0.f;
+        qs.push_back(q);
+        qd.insert(qd.end(), mps->desc + (size_t)mp * 32, mps->desc + (size_t)mp * 32 + 32);
+    }
+    ProjParams P{};
+    P.blocked_mode = 0;
+    P.accept_th = TH_HIGH;
+    P.ratio_mode = 1;
+    P.nnratio = m->nnratio;
+    P.check_ori = 0;
+    return run_proj(m, f, frame_mp, qs, qd, mps, P, nmatches);
+}
+
+// ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono), ORBmatcher.cc:1620-1789
+int orbx_search_by_projection_frame(orbx_matcher* m, const orbx_frame_view* cur, int32_t* cur_mp,
+                                    const orbx_frame_view* last, const int32_t* last_mp, const uint8_t* last_outlier,
+                                    const orbx_mappoints* mps, float th, int mono, int* nmatches) {
+    if (!m || !cur || !cur_mp || !last || !last_mp || !mps || !mps->pos) return fail(ORBX_ERR_ARG, "null argument");
+    float twc[3], tlc[3];
+    centre(cur->Tcw, twc);       // twc = -Rcw^T tcw (cc:1637)
+    project(last->Tcw, twc, tlc);  // tlc = Rlw*twc + tlw (cc:1643)
+    const bool bForward = tlc[2] > cur->b && !mono;
+    const bool bBackward = -tlc[2] > cur->b && !mono;
+    std::vector<ProjQuery> qs;
+    std::vector<uint8_t> qd;
+    for (int i = 0; i < last->n; i++) {
+        const int mp = last_mp[i];
+        if (mp < 0) continue;
+        if (mp >= mps->n) return fail(ORBX_ERR_ARG, "MapPoint id out of range");
+        if (last_outlier && last_outlier[i]) continue;
+        float x3Dc[3];
+        project(cur->Tcw, mps->pos + 3 * (size_t)mp, x3Dc);
+        const float xc = x3Dc[0], yc = x3Dc[1];
+        const float invzc = (float)(1.0 / x3Dc[2]);
+        if (invzc < 0) continue;
+        const float u = cur->fx * xc * invzc + cur->cx;
+        const float v = cur->fy * yc * invzc + cur->cy;
+        if (u < cur->min_x || u > cur->max_x) continue;
+        if (v < cur->min_y || v > cur->max_y) continue;
+        const int nLastOctave = last->keys[i].octave;
+        const float radius = th * cur->scale_factors[nLastOctave];
+        ProjQuery q{};
+        q.u = u;
+        q.v = v;
+        q.ur = u - cur->bf * invzc;
+        q.r = radius;
+        q.er_max = radius;
+        if (bForward) {
+            q.min_level = nLastOctave;
+            q.max_level = -1;
+        } else if (bBackward) {
+            q.min_level = 0;
+            q.max_level = nLastOctave;
+        } else {
+            q.min_level = nLastOctave - 1;
+            q.max_level = nLastOctave + 1;
+        }
+        q.post_min = -1;
+        q.post_max = -1;
+        q.mp = mp;
+        q.angle = last->keys[i].angle;
+        qs.push_back(q);
+        qd.insert(qd.end(), mps->desc + (size_t)mp * 32, mps->desc + (size_t)mp * 32 + 32);
+    }
+    ProjParams P{};
+    P.blocked_mode = 0;
+    P.accept_th = TH_HIGH;
+    P.ratio_mode = 0;
+    P.check_ori = m->check_ori;
+    return run_proj(m, cur, cur_mp, qs, qd, mps, P, nmatches);
+}
+
+// ORBmatcher::SearchForTriangulation, ORBmatcher.cc:850-1056
+int orbx_search_for_triangulation(orbx_matcher* m, const orbx_frame_view* kf1, const uint8_t* kf1_has_mp,
+                                  const int32_t* fv1_node, const int32_t* fv1_off, const int32_t* fv1_idx, int fv1_n,
+                                  const orbx_frame_view* kf2, const uint8_t* kf2_has_mp, const int32_t* fv2_node,
+                                  const int32_t* fv2_off, const int32_t* fv2_idx, int fv2_n, const float* F12,
+                                  int only_stereo, int32_t* pairs, int* npairs) {
+    if (!m || !kf1 || !kf2 || !kf1_has_mp || !kf2_has_mp || !F12 || !pairs || !npairs)
+        return fail(ORBX_ERR_ARG, "null argument");
+    // epipole of KF1's centre in KF2 (cc:858-865)
+    float Cw[3], C2[3];
+    centre(kf1->Tcw, Cw);
+    project(kf2->Tcw, Cw, C2);
+    const float invz = 1.0f / C2[2];
+    const float ex = kf2->fx * C2[0] * invz + kf2->cx;
+    const float ey = kf2->fy * C2[1] * invz + kf2->cy;
+    // queries in the reference's visiting order: shared nodes ascending (cc:886-1019)
+    std::vector<TriQuery> qs;
+    int f1 = 0, f2 = 0;
+    while (f1 < fv1_n && f2 < fv2_n) {
+        if (fv1_node[f1] == fv2_node[f2]) {
+            for (int i1 = fv1_off[f1]; i1 < fv1_off[f1 + 1]; i1++) {
+                const int idx1 = fv1_idx[i1];
+                if (idx1 < 0 || idx1 >= kf1->n) return fail(ORBX_ERR_ARG, "feature index out of range");
+                if (kf1_has_mp[idx1]) continue;
+                const bool bStereo1 = kf1->u_right && kf1->u_right[idx1] >= 0;
+                if (only_stereo && !bStereo1) continue;
+                TriQuery q;
+                q.idx1 = idx1;
+                q.beg = fv2_off[f2];
+                q.end = fv2_off[f2 + 1];
+                q.stereo1 = bStereo1 ? 1 : 0;
+                qs.push_back(q);
+            }
+            f1++;
+            f2++;
+        } else if (fv1_node[f1] < fv2_node[f2]) {
+            f1 = (int)(std::lower_bound(fv1_node + f1, fv1_node + fv1_n, fv2_node[f2]) - fv1_node);
+        } else {
+            f2 = (int)(std::lower_bound(fv2_node + f2, fv2_node + fv2_n, fv1_node[f1]) - fv2_node);
+        }
+    }
+    *npairs = 0;
+    if (qs.empty()) return ORBX_OK;
+    HIP_TRY(hipSetDevice(m->device));
+    const int n1 = kf1->n, n2 = kf2->n, nq = (int)qs.size();
+    const int nfv2 = fv2_off[fv2_n];
+    const size_t need = pad(sizeof(orbx_keypoint) * n1) + pad((size_t)n1 * 32) + pad(sizeof(orbx_keypoint) * n2) +
+                        pad((size_t)n2 * 32) + pad(sizeof(float) * n2) + pad(n2) + pad(sizeof(int32_t) * nfv2) +
+                        2 * pad(sizeof(float) * 32) + pad(sizeof(TriQuery) * nq) + pad(sizeof(int32_t) * n1) +
+                        pad(sizeof(TriProblem)) + pad(8 * (size_t)nq);
+    HIP_TRY(m->arena.reserve(need));
+    m->arena.used = 0;
+    auto* d_k1 = m->arena.take<orbx_keypoint>(n1);
+    auto* d_d1 = m->arena.take<uint8_t>((size_t)n1 * 32);
+    auto* d_k2 = m->arena.take<orbx_keypoint>(n2);
+    auto* d_d2 = m->arena.take<uint8_t>((size_t)n2 * 32);
+    auto* d_ur2 = m->arena.take<float>(n2);
+    auto* d_mp2 = m->arena.take<uint8_t>(n2);
+    auto* d_fv2 = m->arena.take<int32_t>(nfv2);
+    auto* d_sc2 = m->arena.take<float>(32);
+    auto* d_sg2 = m->arena.take<float>(32);
+    auto* d_q = m->arena.take<TriQuery>(nq);
+    auto* d_m12 = m->arena.take<int32_t>(n1);
+    auto* d_prob = m->arena.take<TriProblem>(1);
+    auto* d_scr = m->arena.take<unsigned long long>(nq);
+    hipStream_t s = m->stream;
+    HIP_TRY(hipMemcpyAsync(d_k1, kf1->keys, sizeof(orbx_keypoint) * n1, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_d1, kf1->desc, (size_t)n1 * 32, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_k2, kf2->keys, sizeof(orbx_keypoint) * n2, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_d2, kf2->desc, (size_t)n2 * 32, hipMemcpyHostToDevice, s));
+    if (kf2->u_right) HIP_TRY(hipMemcpyAsync(d_ur2, kf2->u_right, sizeof(float) * n2, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_mp2, kf2_has_mp, n2, hipMemcpyHostToDevice, s));
+    if (nfv2) HIP_TRY(hipMemcpyAsync(d_fv2, fv2_idx, sizeof(int32_t) * nfv2, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_sc2, kf2->scale_factors, sizeof(float) * kf2->nlevels, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_sg2, kf2->level_sigma2, sizeof(float) * kf2->nlevels, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_q, qs.data(), sizeof(TriQuery) * nq, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(d_m12, 0xff, sizeof(int32_t) * n1, s));
+    TriProblem pb{};
+    pb.keys1 = d_k1;
+    pb.desc1 = d_d1;
+    pb.keys2 = d_k2;
+    pb.desc2 = d_d2;
+    pb.u_right2 = kf2->u_right ? d_ur2 : nullptr;
+    pb.has_mp2 = d_mp2;
+    pb.fv2_idx = d_fv2;
+    pb.scale2 = d_sc2;
+    pb.sigma2_2 = d_sg2;
+    std::memcpy(pb.F12, F12, sizeof(pb.F12));
+    pb.ex = ex;
+    pb.ey = ey;
+    pb.only_stereo = only_stereo ? 1 : 0;
+    pb.check_ori = m->check_ori;
+    pb.n2 = n2;
+    pb.q = d_q;
+    pb.nq = nq;
+    pb.matches12 = d_m12;
+    pb.scratch_off = 0;
+    HIP_TRY(hipMemcpyAsync(d_prob, &pb, sizeof(pb), hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_triangulation(d_prob, 1, d_scr, n2, nq, s));
+    std::vector<int32_t> m12((size_t)n1);
+    HIP_TRY(hipMemcpyAsync(m12.data(), d_m12, sizeof(int32_t) * n1, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    int np = 0;
+    for (int i = 0; i < n1; i++) {  // vMatchedPairs in idx1 order (cc:1045-1053)
+        if (m12[(size_t)i] < 0) continue;
+        pairs[2 * np] = i;
+        pairs[2 * np + 1] = m12[(size_t)i];
+        np++;
+    }
+    *npairs = np;
+    return ORBX_OK;
+}
+
+// Frame::ComputeStereoMatches, Frame.cc:673-885
+int orbx_compute_stereo_matches(orbx_matcher* m, orbx_extractor* ex, int left_frame, int right_frame,
+                                const orbx_frame_view* left, const orbx_keypoint* keys_r, const uint8_t* desc_r,
+                                int n_right, float max_disparity, float* u_right, float* depth) {
+    if (!m || !ex || !left || !u_right || !depth || (n_right && (!keys_r || !desc_r)))
+        return fail(ORBX_ERR_ARG, "null argument");
+    const int N = left->n;
+    for (int i = 0; i < N; i++) {
+        u_right[i] = -1.0f;
+        depth[i] = -1.0f;
+    }
+    if (N == 0) return ORBX_OK;
+    StereoProblem pb{};
+    int nRows = 0;
+    for (int l = 0; l < left->nlevels && l < 32; l++) {
+        const uint8_t* pl = nullptr;
+        const uint8_t* pr = nullptr;
+        size_t pitch = 0;
+        int w = 0, h = 0;
+        int rc = orbx_pyramid_level_device(ex, left_frame, l, &pl, &pitch, &w, &h);
+        if (rc != ORBX_OK) return rc;
+        rc = orbx_pyramid_level_device(ex, right_frame, l, &pr, nullptr, nullptr, nullptr);
+        if (rc != ORBX_OK) return rc;
+        pb.lev_l[l] = pl;
+        pb.lev_r[l] = pr;
+        pb.level_pitch[l] = (int)pitch;
+        pb.level_w[l] = w;
+        pb.scale[l] = left->scale_factors[l];
+        pb.inv_scale[l] = 1.0f / left->scale_factors[l];  // mvInvScaleFactors (ORBextractor.cc:468)
+        if (l == 0) nRows = h;
+    }
+    // vRowIndices (cc:693-708): right keypoint indices per row band
+    std::vector<int32_t> off((size_t)nRows + 1, 0);
+    auto band = [&](int iR, int& minr, int& maxr) {
+        const float kpY = keys_r[iR].y;
+        const float r = 2.0f * left->scale_factors[keys_r[iR].octave];
+        maxr = (int)std::ceil(kpY + r);
+        minr = (int)std::floor(kpY - r);
+    };
+    for (int iR = 0; iR < n_right; iR++) {
+        int a, b;
+        band(iR, a, b);
+        for (int yi = std::max(a, 0); yi <= std::min(b, nRows - 1); yi++) off[(size_t)yi + 1]++;
+    }
+    for (int y = 0; y < nRows; y++) off[(size_t)y + 1] += off[(size_t)y];
+    std::vector<int32_t> idx((size_t)off[(size_t)nRows] + 1);
+    std::vector<int32_t> fillc((size_t)nRows, 0);
+    for (int iR = 0; iR < n_right; iR++) {
+        int a, b;
+        band(iR, a, b);
+        for (int yi = std::max(a, 0); yi <= std::min(b, nRows - 1); yi++)
+            idx[(size_t)off[(size_t)yi] + fillc[(size_t)yi]++] = iR;
+    }
+    for (int i = 0; i < N; i++)
+        if (left->keys[i].y < 0 || (int)left->keys[i].y >= nRows) return fail(ORBX_ERR_ARG, "left keypoint row");
+    HIP_TRY(hipSetDevice(m->device));
+    const int nidx = off[(size_t)nRows];
+    const size_t need = pad(sizeof(orbx_keypoint) * N) + pad((size_t)N * 32) + pad(sizeof(orbx_keypoint) * n_right) +
+                        pad((size_t)n_right * 32) + pad(sizeof(int32_t) * (nRows + 1)) +
+                        pad(sizeof(int32_t) * (nidx + 1)) + pad(sizeof(StereoResult) * N);
+    HIP_TRY(m->arena.reserve(need));
+    m->arena.used = 0;
+    auto* d_kl = m->arena.take<orbx_keypoint>(N);
+    auto* d_dl = m->arena.take<uint8_t>((size_t)N * 32);
+    auto* d_kr = m->arena.take<orbx_keypoint>(n_right);
+    auto* d_dr = m->arena.take<uint8_t>((size_t)n_right * 32);
+    auto* d_off = m->arena.take<int32_t>(nRows + 1);
+    auto* d_idx = m->arena.take<int32_t>(nidx + 1);
+    auto* d_res = m->arena.take<StereoResult>(N);
+    // the extractor's stream produced the pyramids: order this stream after it
+    hipStream_t s = m->stream;
+    HIP_TRY(hipStreamSynchronize((hipStream_t)orbx_extractor_stream(ex)));
+    HIP_TRY(hipMemcpyAsync(d_kl, left->keys, sizeof(orbx_keypoint) * N, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_dl, left->desc, (size_t)N * 32, hipMemcpyHostToDevice, s));
+    if (n_right) {
+        HIP_TRY(hipMemcpyAsync(d_kr, keys_r, sizeof(orbx_keypoint) * n_right, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(d_dr, desc_r, (size_t)n_right * 32, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(hipMemcpyAsync(d_off, off.data(), sizeof(int32_t) * (nRows + 1), hipMemcpyHostToDevice, s));
+    if (nidx) HIP_TRY(hipMemcpyAsync(d_idx, idx.data(), sizeof(int32_t) * nidx, hipMemcpyHostToDevice, s));
+    pb.keys_l = d_kl;
+    pb.desc_l = d_dl;
+    pb.nl = N;
+    pb.keys_r = d_kr;
+    pb.desc_r = d_dr;
+    pb.row_off = d_off;
+    pb.row_idx = d_idx;
+    pb.bf = left->bf;
+    pb.max_d = max_disparity;
+    HIP_TRY(launch_stereo(pb, d_res, s));
+    std::vector<StereoResult> res((size_t)N);
+    HIP_TRY(hipMemcpyAsync(res.data(), d_res, sizeof(StereoResult) * N, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    // Sequential outlier pass of this fork (Frame.cc:868-884): after every left keypoint
+    // that reaches it, vDistIdx (sorted by (dist, iL)) is re-scanned from the back and
+    // entries with dist >= 1.5f*1.4f*median are invalidated.  An empty vDistIdx is
+    // skipped (the reference's vDistIdx[0] read on an empty vector has no effect
+    // because its marking loop then runs zero times).
+    std::vector<std::pair<int, int>> vd;
+    vd.reserve((size_t)N);
+    for (int iL = 0; iL < N; iL++) {
+        const StereoResult& r = res[(size_t)iL];
+        if (r.pushed) {
+            u_right[iL] = r.u_right;
+            depth[iL] = r.depth;
+            const std::pair<int, int> e(r.dist, iL);
+            vd.insert(std::upper_bound(vd.begin(), vd.end(), e), e);
+        }
+        if (!r.reach_sort || vd.empty()) continue;
+        const float median = (float)vd[vd.size() / 2].first;
+        const float thDist = 1.5f * 1.4f * median;
+        for (int i = (int)vd.size() - 1; i >= 0; i--) {
+            if ((float)vd[(size_t)i].first < thDist) break;
+            u_right[vd[(size_t)i].second] = -1;
+            depth[vd[(size_t)i].second] = -1;
+        }
+    }
+    return ORBX_OK;
+}
+
+}  // extern "C"

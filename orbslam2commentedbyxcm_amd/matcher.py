@@ -1,0 +1,242 @@
+"""ORBmatcher -- host-side mirror of ORB_SLAM2::ORBmatcher over liborbx.so.
+
+Constructor (nnratio, checkOri), the TH_HIGH / TH_LOW / HISTO_LENGTH constants and
+DescriptorDistance as in include/ORBmatcher.h:57-228; the search functions take the
+Frame / KeyFrame / MapPoint state as arrays (FrameView, MapPoints, Track) because
+the object graph stays with the caller.  MapPoint* pointers are integer ids and
+mvpMapPoints arrays hold ids (-1 = NULL).  Every call runs on the MI355X.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib as L
+
+F32P = C.POINTER(C.c_float)
+I32P = C.POINTER(C.c_int32)
+U8P = C.POINTER(C.c_uint8)
+
+
+class _FrameViewC(C.Structure):
+    _fields_ = [("n", C.c_int), ("keys", C.c_void_p), ("desc", U8P), ("u_right", F32P),
+                ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("bf", C.c_float), ("b", C.c_float), ("min_x", C.c_float), ("max_x", C.c_float),
+                ("min_y", C.c_float), ("max_y", C.c_float), ("nlevels", C.c_int),
+                ("scale_factors", F32P), ("level_sigma2", F32P), ("Tcw", C.c_float * 12)]
+
+
+class _MapPointsC(C.Structure):
+    _fields_ = [("n", C.c_int), ("pos", F32P), ("desc", U8P), ("observations", I32P), ("bad", U8P)]
+
+
+class _TrackC(C.Structure):
+    _fields_ = [("in_view", U8P), ("proj_x", F32P), ("proj_y", F32P), ("proj_xr", F32P),
+                ("scale_level", I32P), ("view_cos", F32P)]
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+@dataclass
+class FrameView:
+    """The Frame / KeyFrame members the matcher reads (include/Frame.h)."""
+    keys: np.ndarray                   # mvKeysUn, KEYPOINT_DTYPE
+    desc: np.ndarray                   # mDescriptors (n, 32) uint8
+    fx: float = 500.0
+    fy: float = 500.0
+    cx: float = 320.0
+    cy: float = 240.0
+    bf: float = 0.0                    # mbf
+    b: float = 0.0                     # mb
+    min_x: float = 0.0
+    max_x: float = 640.0
+    min_y: float = 0.0
+    max_y: float = 480.0
+    scale_factors: np.ndarray = None   # mvScaleFactors
+    level_sigma2: np.ndarray = None    # mvLevelSigma2
+    Tcw: np.ndarray = None             # 3x4 (or 4x4) float
+    u_right: np.ndarray | None = None  # mvuRight
+    _keep: list = field(default_factory=list, repr=False)
+
+    def c(self) -> _FrameViewC:
+        keys = np.ascontiguousarray(self.keys, dtype=L.KEYPOINT_DTYPE)
+        desc = np.ascontiguousarray(self.desc, dtype=np.uint8)
+        sf = _f32(self.scale_factors)
+        sg = _f32(self.level_sigma2 if self.level_sigma2 is not None else sf * sf)
+        ur = None if self.u_right is None else _f32(self.u_right)
+        T = np.eye(4, dtype=np.float32) if self.Tcw is None else _f32(self.Tcw)
+        self._keep = [keys, desc, sf, sg, ur]
+        v = _FrameViewC()
+        v.n = len(keys)
+        v.keys = keys.ctypes.data
+        v.desc = desc.ctypes.data_as(U8P)
+        v.u_right = ur.ctypes.data_as(F32P) if ur is not None else None
+        v.fx, v.fy, v.cx, v.cy, v.bf, v.b = self.fx, self.fy, self.cx, self.cy, self.bf, self.b
+        v.min_x, v.max_x, v.min_y, v.max_y = self.min_x, self.max_x, self.min_y, self.max_y
+        v.nlevels = len(sf)
+        v.scale_factors = sf.ctypes.data_as(F32P)
+        v.level_sigma2 = sg.ctypes.data_as(F32P)
+        v.Tcw[:] = list(T[:3, :4].reshape(-1))
+        return v
+
+
+@dataclass
+class MapPoints:
+    desc: np.ndarray                       # GetDescriptor() (m, 32)
+    observations: np.ndarray               # Observations() (m,)
+    pos: np.ndarray | None = None          # GetWorldPos() (m, 3)
+    bad: np.ndarray | None = None          # isBad() (m,)
+    _keep: list = field(default_factory=list, repr=False)
+
+    def c(self) -> _MapPointsC:
+        d = np.ascontiguousarray(self.desc, dtype=np.uint8)
+        o = np.ascontiguousarray(self.observations, dtype=np.int32)
+        p = None if self.pos is None else _f32(self.pos)
+        b = None if self.bad is None else np.ascontiguousarray(self.bad, dtype=np.uint8)
+        self._keep = [d, o, p, b]
+        v = _MapPointsC()
+        v.n = len(d)
+        v.pos = p.ctypes.data_as(F32P) if p is not None else None
+        v.desc = d.ctypes.data_as(U8P)
+        v.observations = o.ctypes.data_as(I32P)
+        v.bad = b.ctypes.data_as(U8P) if b is not None else None
+        return v
+
+
+@dataclass
+class Track:
+    """Frame::IsInFrustum outputs per MapPoint id (Frame.cc:412-477)."""
+    in_view: np.ndarray
+    proj_x: np.ndarray
+    proj_y: np.ndarray
+    proj_xr: np.ndarray
+    scale_level: np.ndarray
+    view_cos: np.ndarray
+    _keep: list = field(default_factory=list, repr=False)
+
+    def c(self) -> _TrackC:
+        a = [np.ascontiguousarray(self.in_view, np.uint8), _f32(self.proj_x), _f32(self.proj_y),
+             _f32(self.proj_xr), np.ascontiguousarray(self.scale_level, np.int32), _f32(self.view_cos)]
+        self._keep = a
+        v = _TrackC()
+        v.in_view = a[0].ctypes.data_as(U8P)
+        v.proj_x, v.proj_y, v.proj_xr = (x.ctypes.data_as(F32P) for x in a[1:4])
+        v.scale_level = a[4].ctypes.data_as(I32P)
+        v.view_cos = a[5].ctypes.data_as(F32P)
+        return v
+
+
+def feature_vector_csr(nodes_per_kp: np.ndarray):
+    """DBoW2::FeatureVector (node -> ascending keypoint indices, FeatureVector.cpp:31-45)
+    as CSR (node ids, offsets, indices) from each keypoint's node id (-1 = none)."""
+    nodes_per_kp = np.asarray(nodes_per_kp)
+    valid = np.nonzero(nodes_per_kp >= 0)[0]
+    order = valid[np.lexsort((valid, nodes_per_kp[valid]))]
+    node_ids, starts = np.unique(nodes_per_kp[order], return_index=True)
+    off = np.append(starts, len(order)).astype(np.int32)
+    return node_ids.astype(np.int32), off, order.astype(np.int32)
+
+
+class ORBmatcher:
+    TH_HIGH = 100
+    TH_LOW = 50
+    HISTO_LENGTH = 30
+
+    def __init__(self, nnratio: float = 0.6, checkOri: bool = True, device: int = 0):
+        self.mfNNratio = float(nnratio)
+        self.mbCheckOrientation = bool(checkOri)
+        self.device = int(device)
+        self._h = None
+        h = C.c_void_p()
+        L.check(L.lib().orbx_matcher_create(self.device, self.mfNNratio, 1 if checkOri else 0, C.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            L.lib().orbx_matcher_destroy(self._h)
+            self._h = None
+
+    @staticmethod
+    def DescriptorDistance(a: np.ndarray, b: np.ndarray) -> int:
+        """ORBmatcher::DescriptorDistance (ORBmatcher.cc:1983-2003)."""
+        a = np.ascontiguousarray(a, dtype=np.uint8)
+        b = np.ascontiguousarray(b, dtype=np.uint8)
+        return L.lib().orbx_hamming(L.u8ptr(a), L.u8ptr(b))
+
+    # SearchByProjection(Frame&, const vector<MapPoint*>&, th)  ORBmatcher.cc:61-173
+    def SearchByProjectionLocal(self, F: FrameView, frame_mp: np.ndarray, queries, mps: MapPoints, track: Track,
+                                th: float = 1.0) -> int:
+        q = np.ascontiguousarray(queries, dtype=np.int32)
+        assert frame_mp.dtype == np.int32 and frame_mp.flags.c_contiguous
+        fv, mv, tv = F.c(), mps.c(), track.c()
+        n = C.c_int()
+        L.check(L.lib().orbx_search_by_projection_local(self._h, C.addressof(fv), frame_mp.ctypes.data_as(I32P),
+                                                        q.ctypes.data_as(I32P), len(q), C.addressof(mv), C.addressof(tv),
+                                                        float(th), C.byref(n)))
+        return n.value
+
+    # SearchByProjection(Frame& Cur, const Frame& Last, th, bMono)  ORBmatcher.cc:1620-1789
+    def SearchByProjectionFrame(self, cur: FrameView, cur_mp: np.ndarray, last: FrameView, last_mp: np.ndarray,
+                                mps: MapPoints, th: float, bMono: bool, last_outlier=None) -> int:
+        assert cur_mp.dtype == np.int32 and cur_mp.flags.c_contiguous
+        lm = np.ascontiguousarray(last_mp, dtype=np.int32)
+        lo = None if last_outlier is None else np.ascontiguousarray(last_outlier, dtype=np.uint8)
+        cv_, lv, mv = cur.c(), last.c(), mps.c()
+        n = C.c_int()
+        L.check(L.lib().orbx_search_by_projection_frame(self._h, C.addressof(cv_), cur_mp.ctypes.data_as(I32P),
+                                                        C.addressof(lv), lm.ctypes.data_as(I32P),
+                                                        lo.ctypes.data_as(U8P) if lo is not None else None,
+                                                        C.addressof(mv), float(th), 1 if bMono else 0, C.byref(n)))
+        return n.value
+
+    # SearchForTriangulation(KF1, KF2, F12, vMatchedPairs, bOnlyStereo)  ORBmatcher.cc:850-1056
+    def SearchForTriangulation(self, kf1: FrameView, kf1_has_mp, fv1, kf2: FrameView, kf2_has_mp, fv2, F12,
+                               bOnlyStereo: bool = False):
+        m1 = np.ascontiguousarray(kf1_has_mp, dtype=np.uint8)
+        m2 = np.ascontiguousarray(kf2_has_mp, dtype=np.uint8)
+        n1, o1, i1 = (np.ascontiguousarray(x, dtype=np.int32) for x in fv1)
+        n2, o2, i2 = (np.ascontiguousarray(x, dtype=np.int32) for x in fv2)
+        F = _f32(F12).reshape(9)
+        v1, v2 = kf1.c(), kf2.c()
+        pairs = np.zeros((max(len(kf1.keys), 1), 2), dtype=np.int32)
+        npairs = C.c_int()
+        L.check(L.lib().orbx_search_for_triangulation(
+            self._h, C.addressof(v1), m1.ctypes.data_as(U8P), n1.ctypes.data_as(I32P), o1.ctypes.data_as(I32P),
+            i1.ctypes.data_as(I32P), len(n1), C.addressof(v2), m2.ctypes.data_as(U8P), n2.ctypes.data_as(I32P),
+            o2.ctypes.data_as(I32P), i2.ctypes.data_as(I32P), len(n2), F.ctypes.data_as(F32P),
+            1 if bOnlyStereo else 0, pairs.ctypes.data_as(I32P), C.byref(npairs)))
+        return pairs[: npairs.value].copy()
+
+    # Frame::ComputeStereoMatches  Frame.cc:673-885
+    def ComputeStereoMatches(self, extractor, left_frame: int, right_frame: int, left: FrameView, keys_r, desc_r,
+                             maxD: float):
+        kr = np.ascontiguousarray(keys_r, dtype=L.KEYPOINT_DTYPE)
+        dr = np.ascontiguousarray(desc_r, dtype=np.uint8)
+        lv = left.c()
+        n = len(left.keys)
+        ur = np.zeros(max(n, 1), dtype=np.float32)
+        dp = np.zeros(max(n, 1), dtype=np.float32)
+        L.check(L.lib().orbx_compute_stereo_matches(self._h, extractor._h, left_frame, right_frame, C.addressof(lv),
+                                                    kr.ctypes.data, dr.ctypes.data_as(U8P), len(kr), float(maxD),
+                                                    ur.ctypes.data_as(F32P), dp.ctypes.data_as(F32P)))
+        return ur[:n].copy(), dp[:n].copy()
+
+    def score_windows(self, qdesc, tdesc, tlevel, cand_off, cand, tie_last: bool = False) -> dict:
+        """Batched candidate scoring (best / second-best Hamming) on the GPU."""
+        q = np.ascontiguousarray(qdesc, dtype=np.uint8)
+        t = np.ascontiguousarray(tdesc, dtype=np.uint8)
+        lv = np.ascontiguousarray(tlevel, dtype=np.int32)
+        off = np.ascontiguousarray(cand_off, dtype=np.int32)
+        c = np.ascontiguousarray(cand, dtype=np.int32)
+        nq = len(off) - 1
+        out = {k: np.zeros(nq, dtype=np.int32) for k in
+               ("best_idx", "best_dist", "best_level", "second_dist", "second_level")}
+        L.check(L.lib().orbx_window_match(self.device, L.u8ptr(q), nq, L.u8ptr(t), len(t), L.i32ptr(lv),
+                                          L.i32ptr(off), L.i32ptr(c), 1 if tie_last else 0,
+                                          *(L.i32ptr(out[k]) for k in ("best_idx", "best_dist", "best_level",
+                                                                       "second_dist", "second_level"))))
+        return out

@@ -81,6 +81,31 @@ def frames(n: int, width: int = 640, height: int = 480, first_seed: int = 0, wor
     return out
 
 
+def shifted_pair(seed: int, width: int = 640, height: int = 480, dx: int = 7, dy: int = -4, margin: int = 32):
+    """Two views of one canvas, the second shifted by (dx, dy) pixels: a pixel (x, y) of
+    the first view appears at (x - dx, y - dy) in the second (a fronto-parallel scene
+    under camera translation)."""
+    canvas = frame(seed, width + 2 * margin, height + 2 * margin)
+    a = canvas[margin:margin + height, margin:margin + width]
+    b = canvas[margin + dy:margin + dy + height, margin + dx:margin + dx + width]
+    return np.ascontiguousarray(a), np.ascontiguousarray(b)
+
+
+def sequence(seed: int, n: int, width: int = 640, height: int = 480, step: int = 3, margin: int = 64):
+    """n views of one canvas along a random walk of up to `step` px per frame (for
+    frame-to-frame matching benchmarks).  Returns (frames (n, h, w), offsets (n, 2))."""
+    canvas = frame(seed, width + 2 * margin, height + 2 * margin)
+    g = _rng(seed + 7)
+    off = np.zeros((n, 2), dtype=np.int64)
+    for i in range(1, n):
+        off[i] = np.clip(off[i - 1] + g.integers(-step, step + 1, 2), -margin, margin)
+    out = np.empty((n, height, width), dtype=np.uint8)
+    for i in range(n):
+        ox, oy = margin + off[i, 0], margin + off[i, 1]
+        out[i] = canvas[oy:oy + height, ox:ox + width]
+    return out, off
+
+
 def stereo_pair(seed: int, width: int = 1241, height: int = 376, max_disp: int = 64):
     """(left, right, disparity) with right(x) = left(x + d) for a blockwise d field."""
     left = frame(seed, width, height)

@@ -1,0 +1,93 @@
+"""Synthetic matching scenes: two views of one textured canvas related by a camera
+translation, keypoints/descriptors from the extraction oracle, MapPoints
+back-projected from the first view.  Used by the GPU matcher parity tests."""
+from __future__ import annotations
+
+import numpy as np
+
+from orbslam2commentedbyxcm_amd import synth
+from orbslam2commentedbyxcm_amd.matcher import FrameView, MapPoints, Track, feature_vector_csr
+
+FX = FY = 500.0
+CX, CY = 320.0, 240.0
+Z0 = 5.0
+
+
+def _view(O, img, T, u_right=None, bf=0.0, b=0.0):
+    p = O.params(1000, 1.2, 8, 20, 7)
+    kps, desc, _ = O.extract(img, p)
+    sf = np.array(p.scale[:8], np.float32)
+    sg = np.array(p.sigma2[:8], np.float32)
+    h, w = img.shape
+    return FrameView(keys=kps, desc=desc, fx=FX, fy=FY, cx=CX, cy=CY, bf=bf, b=b, min_x=0.0, max_x=float(w),
+                     min_y=0.0, max_y=float(h), scale_factors=sf, level_sigma2=sg, Tcw=T, u_right=u_right)
+
+
+def two_views(O, seed=0, dx=7, dy=-4, stereo=False):
+    a, bimg = synth.shifted_pair(seed, 640, 480, dx, dy)
+    TA = np.eye(4, dtype=np.float32)
+    TB = np.eye(4, dtype=np.float32)
+    TB[0, 3] = -dx * Z0 / FX
+    TB[1, 3] = -dy * Z0 / FY
+    bf = 0.54 * FX if stereo else 0.0
+    b = bf / FX if stereo else 0.0
+    A = _view(O, a, TA, bf=bf, b=b)
+    B = _view(O, bimg, TB, bf=bf, b=b)
+    if stereo:
+        rng = np.random.default_rng(seed + 11)
+        for V in (A, B):
+            ur = V.keys["x"] - bf / Z0 + rng.normal(0, 0.5, len(V.keys)).astype(np.float32)
+            ur[rng.random(len(V.keys)) < 0.3] = -1.0
+            V.u_right = ur.astype(np.float32)
+    return A, B
+
+
+def mappoints_from(A, seed=0, obs_zero_frac=0.1):
+    rng = np.random.default_rng(seed + 3)
+    n = len(A.keys)
+    z = (Z0 + rng.normal(0, 0.01, n)).astype(np.float32)
+    x = ((A.keys["x"] - CX) / FX * z).astype(np.float32)
+    y = ((A.keys["y"] - CY) / FY * z).astype(np.float32)
+    pos = np.stack([x, y, z], 1).astype(np.float32)
+    obs = rng.integers(1, 4, n).astype(np.int32)
+    obs[rng.random(n) < obs_zero_frac] = 0
+    return MapPoints(desc=A.desc.copy(), observations=obs, pos=pos, bad=(rng.random(n) < 0.03).astype(np.uint8))
+
+
+def local_track(A, B, mps, seed=0):
+    """IsInFrustum outputs for projecting A's MapPoints into B."""
+    rng = np.random.default_rng(seed + 5)
+    n = len(A.keys)
+    T = B.Tcw
+    P = mps.pos
+    xc = P[:, 0] + T[0, 3]
+    yc = P[:, 1] + T[1, 3]
+    z = P[:, 2]
+    u = (FX * xc / z + CX + rng.normal(0, 0.7, n)).astype(np.float32)
+    v = (FY * yc / z + CY + rng.normal(0, 0.7, n)).astype(np.float32)
+    return Track(in_view=(rng.random(n) < 0.92).astype(np.uint8), proj_x=u, proj_y=v,
+                 proj_xr=(u - (B.bf / z if B.bf else 0)).astype(np.float32),
+                 scale_level=np.clip(A.keys["octave"] + rng.integers(-1, 2, n), 0, 7).astype(np.int32),
+                 view_cos=rng.uniform(0.995, 1.0, n).astype(np.float32))
+
+
+def fundamental(A, B):
+    """ComputeF12 (LocalMapping.cc:606-625) for K1 = K2 = K."""
+    K = np.array([[FX, 0, CX], [0, FY, CY], [0, 0, 1]], np.float32)
+    R1, t1 = A.Tcw[:3, :3], A.Tcw[:3, 3]
+    R2, t2 = B.Tcw[:3, :3], B.Tcw[:3, 3]
+    R12 = R1 @ R2.T
+    t12 = -R1 @ R2.T @ t2 + t1
+    tx = np.array([[0, -t12[2], t12[1]], [t12[2], 0, -t12[0]], [-t12[1], t12[0], 0]], np.float32)
+    Ki = np.linalg.inv(K).astype(np.float32)
+    return (Ki.T @ tx @ R12 @ Ki).astype(np.float32)
+
+
+def vocab_nodes(V, nnodes=40, levelsup_bits=3):
+    """Synthetic vocabulary node per keypoint (stands in for DBoW2 transform at levelsup 4)."""
+    d = V.desc.astype(np.int64)
+    return ((d[:, 0] >> levelsup_bits) ^ (d[:, 5] & 7)) % nnodes
+
+
+def fv(V, **kw):
+    return feature_vector_csr(vocab_nodes(V, **kw))

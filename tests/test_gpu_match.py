@@ -1,0 +1,119 @@
+"""GPU parity of the ORBmatcher drop-in (liborbx.so) against the CPU oracle.
+
+Match assignments (mvpMapPoints / vMatchedPairs / mvuRight / mvDepth) must be
+identical: the kernels reproduce the reference's candidate order, tie rules,
+sequential claiming and rotation-histogram filtering (hazards H5, H6).
+"""
+import numpy as np
+import pytest
+
+import match_scenes as S
+from orbslam2commentedbyxcm_amd import ORBextractor, synth
+from orbslam2commentedbyxcm_amd.matcher import FrameView, ORBmatcher
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("seed,stereo,th,preassign", [(0, False, 15.0, False), (1, False, 7.0, True),
+                                                       (2, True, 7.0, False), (3, True, 15.0, True)])
+def test_search_by_projection_frame(oracle, orbx_built, seed, stereo, th, preassign):
+    A, B = S.two_views(oracle, seed, stereo=stereo)
+    mps = S.mappoints_from(A, seed)
+    rng = np.random.default_rng(seed)
+    last_mp = np.arange(len(A.keys), dtype=np.int32)
+    last_mp[rng.random(len(A.keys)) < 0.1] = -1
+    outlier = (rng.random(len(A.keys)) < 0.05).astype(np.uint8)
+    cur0 = np.full(len(B.keys), -1, np.int32)
+    if preassign:
+        sel = rng.random(len(B.keys)) < 0.1
+        cur0[sel] = rng.integers(0, len(A.keys), sel.sum())
+    for check_ori in (True, False):
+        m = ORBmatcher(0.9, check_ori)
+        cur_gpu = cur0.copy()
+        n_gpu = m.SearchByProjectionFrame(B, cur_gpu, A, last_mp, mps, th, not stereo, last_outlier=outlier)
+        cur_ref = cur0.copy()
+        n_ref = oracle.sbp_frame(B, cur_ref, A, last_mp, mps, th, not stereo, check_ori, last_outlier=outlier)
+        assert n_gpu == n_ref
+        assert np.array_equal(cur_gpu, cur_ref), np.nonzero(cur_gpu != cur_ref)[0][:10]
+        assert n_ref > 50  # the scene really matches
+
+
+@pytest.mark.parametrize("seed,th,nnratio", [(0, 1.0, 0.8), (1, 3.0, 0.8), (2, 5.0, 0.6)])
+def test_search_by_projection_local(oracle, orbx_built, seed, th, nnratio):
+    A, B = S.two_views(oracle, seed, stereo=seed == 2)
+    mps = S.mappoints_from(A, seed)
+    trk = S.local_track(A, B, mps, seed)
+    rng = np.random.default_rng(seed + 1)
+    queries = rng.permutation(len(A.keys)).astype(np.int32)
+    f0 = np.full(len(B.keys), -1, np.int32)
+    sel = rng.random(len(B.keys)) < 0.15
+    f0[sel] = rng.integers(0, len(A.keys), sel.sum())
+    m = ORBmatcher(nnratio, False)
+    fg = f0.copy()
+    ng = m.SearchByProjectionLocal(B, fg, queries, mps, trk, th)
+    fr = f0.copy()
+    nr = oracle.sbp_local(B, fr, queries, mps, trk, th, nnratio)
+    assert ng == nr and nr > 50
+    assert np.array_equal(fg, fr), np.nonzero(fg != fr)[0][:10]
+
+
+@pytest.mark.parametrize("seed,stereo,only_stereo,check_ori", [(0, False, False, False), (1, True, False, False),
+                                                                (2, True, True, False), (3, False, False, True)])
+def test_search_for_triangulation(oracle, orbx_built, seed, stereo, only_stereo, check_ori):
+    A, B = S.two_views(oracle, seed, stereo=stereo)
+    rng = np.random.default_rng(seed + 9)
+    has1 = (rng.random(len(A.keys)) < 0.2).astype(np.uint8)
+    has2 = (rng.random(len(B.keys)) < 0.2).astype(np.uint8)
+    fv1, fv2 = S.fv(A), S.fv(B)
+    F12 = S.fundamental(A, B)
+    m = ORBmatcher(0.6, check_ori)
+    pg = m.SearchForTriangulation(A, has1, fv1, B, has2, fv2, F12, only_stereo)
+    pr = oracle.search_for_triangulation(A, has1, fv1, B, has2, fv2, F12, only_stereo, check_ori)
+    assert np.array_equal(pg, pr), (len(pg), len(pr))
+    assert len(pr) > 20
+
+
+@pytest.mark.parametrize("seed,W,H", [(0, 640, 480), (1, 1241, 376)])
+def test_compute_stereo_matches(oracle, orbx_built, seed, W, H):
+    left, right, _ = synth.stereo_pair(seed, W, H, max_disp=48)
+    nf = 2000 if W > 1000 else 1000
+    ex = ORBextractor(nf, 1.2, 8, 20, 7)
+    kps, desc, n = ex.extract_batch(np.stack([left, right]))
+    kl, dl = kps[0][: n[0]], desc[0][: n[0]]
+    kr, dr = kps[1][: n[1]], desc[1][: n[1]]
+    p = oracle.params(nf, 1.2, 8, 20, 7)
+    sf = np.array(p.scale[:8], np.float32)
+    fx = 718.856
+    bf = 386.1448
+    view = FrameView(keys=kl, desc=dl, fx=fx, fy=fx, cx=W / 2, cy=H / 2, bf=bf, b=bf / fx, max_x=W, max_y=H,
+                     scale_factors=sf, level_sigma2=sf * sf)
+    m = ORBmatcher(0.6, True)
+    ur_g, dp_g = m.ComputeStereoMatches(ex, 0, 1, view, kr, dr, maxD=fx)
+    ur_r, dp_r = oracle.compute_stereo_matches(view, kr, dr, oracle.pyramid(left, p), oracle.pyramid(right, p), fx)
+    assert np.array_equal(ur_g, ur_r), np.nonzero(ur_g != ur_r)[0][:10]
+    assert np.array_equal(dp_g, dp_r)
+    assert (ur_r >= 0).sum() > 100
+
+
+def test_descriptor_distance_and_windows(oracle, orbx_built):
+    rng = np.random.default_rng(0)
+    q = rng.integers(0, 256, (300, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, (900, 32), dtype=np.uint8)
+    t[::7] = q[rng.integers(0, 300, len(t[::7]))]  # exact duplicates -> ties at distance 0
+    lv = rng.integers(0, 8, 900).astype(np.int32)
+    counts = rng.integers(0, 40, 300)
+    off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+    cand = rng.integers(0, 900, off[-1]).astype(np.int32)
+    m = ORBmatcher()
+    for tie_last in (False, True):
+        res = m.score_windows(q, t, lv, off, cand, tie_last)
+        for i in range(300):
+            c = cand[off[i]:off[i + 1]]
+            if len(c) == 0:
+                assert res["best_idx"][i] == -1
+                continue
+            d = np.array([oracle.descriptor_distance(q[i], t[j]) for j in c])
+            order = np.lexsort((-np.arange(len(c)) if tie_last else np.arange(len(c)), d))
+            assert res["best_dist"][i] == d[order[0]] and res["best_idx"][i] == c[order[0]]
+            if not tie_last and len(c) > 1:
+                assert res["second_dist"][i] == d[order[1]] and res["second_level"][i] == lv[c[order[1]]]
