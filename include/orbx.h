@@ -207,6 +207,19 @@ int orbx_search_by_projection_frame(orbx_matcher* m, const orbx_frame_view* cur,
                                     const uint8_t* last_outlier, const orbx_mappoints* mps, float th,
                                     int mono, int* nmatches);
 
+/* Batched TrackWithMotionModel matching (Tracking.cc:966-994) over a device-resident
+ * sequence produced by orbx_extract_batch_device: for b >= 1, frame b (CurrentFrame)
+ * is matched against frame b-1 (LastFrame) with SearchByProjection(..., th, bMono=1)
+ * semantics (ORBmatcher.cc:1620-1789).  Every keypoint i of frame b-1 carries
+ * MapPoint id i at depth `depth` on its viewing ray (Observations() > 0).  d_Tcw: B x 12
+ * floats (rows 0..2 of each mTcw).  Outputs (device): d_cur_mp [B][cap] (frame 0 stays
+ * -1) and d_nmatches [B].  Asynchronous on `stream` (or the matcher's stream). */
+int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* d_kps, const uint8_t* d_desc,
+                               const int32_t* d_n, int cap, const float* d_Tcw, float fx, float fy, float cx,
+                               float cy, float min_x, float max_x, float min_y, float max_y,
+                               const float* scale_factors, int nlevels, float depth, float th,
+                               int32_t* d_cur_mp, int32_t* d_nmatches, void* stream);
+
 /* SearchForTriangulation(KF1, KF2, F12, vMatchedPairs, bOnlyStereo)
  * ORBmatcher.cc:850-1056 (LocalMapping::CreateNewMapPoints, LocalMapping.cc:305).
  * DBoW2 FeatureVectors as CSR: node ids ascending (fv_node[k]), keypoints of node k

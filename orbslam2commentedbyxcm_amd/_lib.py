@@ -33,6 +33,7 @@ EXPORTED = [
     "orbx_window_match_device", "orbx_window_match", "orbx_version", "orbx_device_count",
     "orbx_last_error", "orbx_matcher_create", "orbx_matcher_destroy", "orbx_search_by_projection_local",
     "orbx_search_by_projection_frame", "orbx_search_for_triangulation", "orbx_compute_stereo_matches",
+    "orbx_match_sequence_device",
 ]
 
 
@@ -57,6 +58,14 @@ def lib() -> C.CDLL:
         return _lib
     if not LIB_PATH.exists():
         raise ImportError(f"{LIB_PATH} not built: run `python -m orbslam2commentedbyxcm_amd.build`")
+    # torch bundles its own libamdhip64.so.7 (and HSA runtime).  Two HIP runtimes in one
+    # process cannot both open the GPU, so when torch is installed it is loaded first and
+    # liborbx.so binds to the same runtime (same SONAME); without torch liborbx.so uses
+    # the system ROCm runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(str(LIB_PATH))
     vp, ip, u8p = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_uint8)
     fp = C.POINTER(C.c_float)
@@ -91,6 +100,9 @@ def lib() -> C.CDLL:
     L.orbx_search_for_triangulation.argtypes = [vp, vp, u8p, i32p, i32p, i32p, C.c_int, vp, u8p, i32p, i32p, i32p,
                                                 C.c_int, fp, C.c_int, i32p, ip]
     L.orbx_compute_stereo_matches.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, u8p, C.c_int, C.c_float, fp, fp]
+    L.orbx_match_sequence_device.argtypes = [vp, C.c_int, vp, vp, vp, C.c_int, vp, C.c_float, C.c_float, C.c_float,
+                                             C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, fp, C.c_int,
+                                             C.c_float, C.c_float, vp, vp, vp]
     L.orbx_version.restype = C.c_char_p
     L.orbx_device_count.argtypes = [ip]
     L.orbx_last_error.restype = C.c_char_p

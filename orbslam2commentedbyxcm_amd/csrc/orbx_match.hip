@@ -317,6 +317,80 @@ __global__ __launch_bounds__(256) void k_proj_search(const ProjProblem* __restri
     for (int i = tid; i < n; i += 256) pb.frame_mp[i] = fmp[i];
 }
 
+// Batched TrackWithMotionModel matching over a device-resident sequence: problem p
+// matches frame p+1 (CurrentFrame) against frame p (LastFrame).  Every keypoint of
+// the last frame carries a MapPoint at depth `depth` on its viewing ray; projection
+// and query construction follow SearchByProjection(Frame&, const Frame&, th, bMono=true)
+// (ORBmatcher.cc:1644-1701).  One thread per last-frame keypoint slot.
+__global__ __launch_bounds__(256) void k_seq_build(SeqArgs A, ProjQuery* __restrict__ queries,
+                                                   ProjProblem* __restrict__ probs,
+                                                   long long* __restrict__ scratch_off) {
+    const int p = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int nlast = A.n[p];
+    if (i == 0) {
+        ProjProblem pb{};
+        pb.keys = A.kps + (size_t)(p + 1) * A.cap;
+        pb.desc = A.desc + (size_t)(p + 1) * A.cap * 32;
+        pb.u_right = nullptr;
+        pb.frame_mp = A.cur_mp + (size_t)(p + 1) * A.cap;
+        pb.n = A.n[p + 1] < A.cap ? A.n[p + 1] : A.cap;
+        pb.q = queries + (size_t)p * A.cap;
+        pb.qdesc = A.desc + (size_t)p * A.cap * 32;
+        pb.nq = nlast < A.cap ? nlast : A.cap;
+        pb.min_x = A.min_x;
+        pb.min_y = A.min_y;
+        pb.inv_w = (float)kGridCols / (A.max_x - A.min_x);
+        pb.inv_h = (float)kGridRows / (A.max_y - A.min_y);
+        pb.nmatches = A.nmatches + p + 1;
+        probs[p] = pb;
+        scratch_off[p] = (long long)p * 2 * A.cap;
+    }
+    if (i >= A.cap) return;
+    ProjQuery q{};
+    q.mp = -1;
+    if (i < nlast) {
+        const orbx_keypoint kp = A.kps[(size_t)p * A.cap + i];
+        const float* Tl = A.Tcw + 12 * (size_t)p;
+        const float* Tc = A.Tcw + 12 * (size_t)(p + 1);
+        // MapPoint: last-frame camera point on the keypoint ray, to world: Xw = Rl^T (Xc - tl)
+        const float z = A.depth;
+        const float Xc[3] = {(kp.x - A.cx) / A.fx * z, (kp.y - A.cy) / A.fy * z, z};
+        float Xw[3];
+        for (int c = 0; c < 3; c++)
+            Xw[c] = Tl[c] * (Xc[0] - Tl[3]) + Tl[4 + c] * (Xc[1] - Tl[7]) + Tl[8 + c] * (Xc[2] - Tl[11]);
+        float x3Dc[3];
+        for (int r = 0; r < 3; r++)
+            x3Dc[r] = Tc[4 * r] * Xw[0] + Tc[4 * r + 1] * Xw[1] + Tc[4 * r + 2] * Xw[2] + Tc[4 * r + 3];
+        const float invzc = (float)(1.0 / (double)x3Dc[2]);
+        const float u = A.fx * x3Dc[0] * invzc + A.cx;
+        const float v = A.fy * x3Dc[1] * invzc + A.cy;
+        if (!(invzc < 0) && !(u < A.min_x || u > A.max_x) && !(v < A.min_y || v > A.max_y)) {
+            const int o = kp.octave;
+            q.u = u;
+            q.v = v;
+            q.ur = u - A.bf * invzc;
+            q.r = A.th * A.scale[o];
+            q.er_max = q.r;
+            q.min_level = o - 1;  // bMono: GetFeaturesInArea(u, v, radius, nLastOctave-1, nLastOctave+1)
+            q.max_level = o + 1;
+            q.post_min = -1;
+            q.post_max = -1;
+            q.mp = i;
+            q.angle = kp.angle;
+        }
+    }
+    queries[(size_t)p * A.cap + i] = q;
+}
+
+hipError_t launch_seq_build(const SeqArgs& A, int npairs, ProjQuery* queries, ProjProblem* probs,
+                            long long* scratch_off, hipStream_t stream) {
+    if (npairs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_seq_build, dim3((A.cap + 255) / 256, npairs), dim3(256), 0, stream, A, queries, probs,
+                       scratch_off);
+    return hipGetLastError();
+}
+
 hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned long long* scratch,
                               const long long* d_scratch_off, int max_n, int max_nq, hipStream_t stream) {
     if (nprob <= 0) return hipSuccess;

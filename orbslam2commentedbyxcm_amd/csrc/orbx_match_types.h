@@ -52,6 +52,22 @@ struct ProjParams {
     int check_ori;          // rotation-consistency histogram (a12, a13)
 };
 
+// Batched frame-to-frame matching over an extracted device sequence.
+struct SeqArgs {
+    const orbx_keypoint* kps;  // [B][cap]
+    const uint8_t* desc;       // [B][cap][32]
+    const int32_t* n;          // [B]
+    int cap;
+    const float* Tcw;          // [B][12]
+    float fx, fy, cx, cy, bf;
+    float min_x, max_x, min_y, max_y;
+    float depth;               // MapPoint depth along the last frame's rays
+    float th;                  // search radius factor
+    float scale[32];           // mvScaleFactors
+    int32_t* cur_mp;           // [B][cap] out (pre-filled -1)
+    int32_t* nmatches;         // [B] out
+};
+
 // SearchForTriangulation: one unmatched KF1 keypoint of a shared vocabulary node.
 struct TriQuery {
     int idx1;       // KF1 keypoint

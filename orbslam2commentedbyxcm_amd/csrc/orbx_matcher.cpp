@@ -285,6 +285,66 @@ int orbx_search_by_projection_frame(orbx_matcher* m, const orbx_frame_view* cur,
     return run_proj(m, cur, cur_mp, qs, qd, mps, P, nmatches);
 }
 
+// Batched SearchByProjection(CurrentFrame, LastFrame, th, bMono=true) over a device
+// sequence written by orbx_extract_batch_device (see include/orbx.h).
+int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* d_kps, const uint8_t* d_desc,
+                               const int32_t* d_n, int cap, const float* d_Tcw, float fx, float fy, float cx,
+                               float cy, float min_x, float max_x, float min_y, float max_y,
+                               const float* scale_factors, int nlevels, float depth, float th, int32_t* d_cur_mp,
+                               int32_t* d_nmatches, void* stream) {
+    if (!m || batch < 0 || cap <= 0 || !scale_factors || nlevels < 1 || nlevels > 32) return fail(ORBX_ERR_ARG, "bad argument");
+    if (batch == 0) return ORBX_OK;
+    if (!d_kps || !d_desc || !d_n || !d_Tcw || !d_cur_mp || !d_nmatches) return fail(ORBX_ERR_ARG, "null buffer");
+    HIP_TRY(hipSetDevice(m->device));
+    hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+    const int npairs = batch - 1;
+    const size_t need = pad(sizeof(ProjQuery) * (size_t)(npairs > 0 ? npairs : 1) * cap) +
+                        pad(sizeof(ProjProblem) * (size_t)(npairs > 0 ? npairs : 1)) +
+                        pad(sizeof(long long) * (size_t)(npairs > 0 ? npairs : 1)) +
+                        pad(sizeof(unsigned long long) * 2 * (size_t)(npairs > 0 ? npairs : 1) * cap);
+    if (m->arena.cap < need) {
+        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(m->arena.reserve(need));
+    }
+    m->arena.used = 0;
+    auto* d_q = m->arena.take<ProjQuery>((size_t)(npairs > 0 ? npairs : 1) * cap);
+    auto* d_prob = m->arena.take<ProjProblem>(npairs > 0 ? npairs : 1);
+    auto* d_off = m->arena.take<long long>(npairs > 0 ? npairs : 1);
+    auto* d_scr = m->arena.take<unsigned long long>(2 * (size_t)(npairs > 0 ? npairs : 1) * cap);
+    HIP_TRY(hipMemsetAsync(d_cur_mp, 0xff, sizeof(int32_t) * (size_t)batch * cap, s));
+    HIP_TRY(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * (size_t)batch, s));
+    if (npairs == 0) return ORBX_OK;
+    SeqArgs A{};
+    A.kps = d_kps;
+    A.desc = d_desc;
+    A.n = d_n;
+    A.cap = cap;
+    A.Tcw = d_Tcw;
+    A.fx = fx;
+    A.fy = fy;
+    A.cx = cx;
+    A.cy = cy;
+    A.bf = 0.f;
+    A.min_x = min_x;
+    A.max_x = max_x;
+    A.min_y = min_y;
+    A.max_y = max_y;
+    A.depth = depth;
+    A.th = th;
+    for (int l = 0; l < nlevels; l++) A.scale[l] = scale_factors[l];
+    A.cur_mp = d_cur_mp;
+    A.nmatches = d_nmatches;
+    HIP_TRY(launch_seq_build(A, npairs, d_q, d_prob, d_off, s));
+    ProjParams P{};
+    P.mp_obs = nullptr;
+    P.blocked_mode = 1;  // every MapPoint of the sequence has Observations() > 0
+    P.accept_th = TH_HIGH;
+    P.ratio_mode = 0;
+    P.check_ori = m->check_ori;
+    HIP_TRY(launch_proj_search(d_prob, npairs, P, d_scr, d_off, cap, cap, s));
+    return ORBX_OK;
+}
+
 // ORBmatcher::SearchForTriangulation, ORBmatcher.cc:850-1056
 int orbx_search_for_triangulation(orbx_matcher* m, const orbx_frame_view* kf1, const uint8_t* kf1_has_mp,
                                   const int32_t* fv1_node, const int32_t* fv1_off, const int32_t* fv1_idx, int fv1_n,

@@ -225,6 +225,20 @@ class ORBmatcher:
                                                     ur.ctypes.data_as(F32P), dp.ctypes.data_as(F32P)))
         return ur[:n].copy(), dp[:n].copy()
 
+    def match_sequence_device(self, d_kps, d_desc, d_n, d_Tcw, d_cur_mp, d_nmatches, scale_factors, fx, fy, cx, cy,
+                              width, height, depth: float = 5.0, th: float = 15.0, stream=None) -> None:
+        """Batched TrackWithMotionModel matching of frame b against b-1 (device tensors:
+        kps (B, cap, 7) int32 words, desc (B, cap, 32) u8, n (B,), Tcw (B, 12) f32,
+        outputs cur_mp (B, cap) int32 and nmatches (B,) int32)."""
+        B, cap = d_desc.shape[0], d_desc.shape[1]
+        sf = _f32(scale_factors)
+        s = None if stream is None else C.c_void_p(getattr(stream, "cuda_stream", stream))
+        L.check(L.lib().orbx_match_sequence_device(
+            self._h, B, C.c_void_p(d_kps.data_ptr()), C.c_void_p(d_desc.data_ptr()), C.c_void_p(d_n.data_ptr()),
+            cap, C.c_void_p(d_Tcw.data_ptr()), fx, fy, cx, cy, 0.0, float(width), 0.0, float(height),
+            sf.ctypes.data_as(F32P), len(sf), depth, th, C.c_void_p(d_cur_mp.data_ptr()),
+            C.c_void_p(d_nmatches.data_ptr()), s))
+
     def score_windows(self, qdesc, tdesc, tlevel, cand_off, cand, tie_last: bool = False) -> dict:
         """Batched candidate scoring (best / second-best Hamming) on the GPU."""
         q = np.ascontiguousarray(qdesc, dtype=np.uint8)

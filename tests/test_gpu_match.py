@@ -117,3 +117,61 @@ def test_descriptor_distance_and_windows(oracle, orbx_built):
             assert res["best_dist"][i] == d[order[0]] and res["best_idx"][i] == c[order[0]]
             if not tie_last and len(c) > 1:
                 assert res["second_dist"][i] == d[order[1]] and res["second_level"][i] == lv[c[order[1]]]
+
+
+def test_match_sequence_device(oracle, orbx_built):
+    """Batched frame-to-frame matching on device-resident frames == per-pair oracle."""
+    import torch
+
+    from orbslam2commentedbyxcm_amd.matcher import MapPoints
+
+    B = 6
+    frames, off = synth.sequence(3, B)
+    dev = torch.device("cuda", 0)
+    ex = ORBextractor(1000, 1.2, 8, 20, 7)
+    cap = ex.max_keypoints(640, 480)
+    d_frames = torch.from_numpy(frames).to(dev)
+    d_kps = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)
+    d_desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
+    d_n = torch.empty((B,), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    ex.extract_batch_device(d_frames, d_kps, d_desc, d_n)
+    fx = fy = 500.0
+    cx, cy, z = 320.0, 240.0, 5.0
+    T = np.zeros((B, 12), np.float32)
+    for b in range(B):
+        T[b] = np.array([1, 0, 0, -off[b, 0] * z / fx, 0, 1, 0, -off[b, 1] * z / fy, 0, 0, 1, 0], np.float32)
+    d_T = torch.from_numpy(T).to(dev)
+    d_mp = torch.empty((B, cap), dtype=torch.int32, device=dev)
+    d_nm = torch.empty((B,), dtype=torch.int32, device=dev)
+    sf = ex.GetScaleFactors()
+    m = ORBmatcher(0.9, True)
+    m.match_sequence_device(d_kps, d_desc, d_n, d_T, d_mp, d_nm, sf, fx, fy, cx, cy, 640, 480, depth=z, th=15.0,
+                            stream=ex.stream_handle())
+    torch.cuda.synchronize()
+    n = d_n.cpu().numpy()
+    kps = d_kps.cpu().numpy().view(np.uint8).reshape(B, cap, 28).view(oracle.KEYPOINT_DTYPE).reshape(B, cap)
+    desc = d_desc.cpu().numpy()
+    mp = d_mp.cpu().numpy()
+    nm = d_nm.cpu().numpy()
+    assert (mp[0] == -1).all() and nm[0] == 0
+    F32 = np.float32
+    for p in range(B - 1):
+        lk, ld = kps[p][: n[p]], desc[p][: n[p]]
+        ck, cd = kps[p + 1][: n[p + 1]], desc[p + 1][: n[p + 1]]
+        Tl = T[p]
+        xc0 = (lk["x"] - F32(cx)) / F32(fx) * F32(z)
+        xc1 = (lk["y"] - F32(cy)) / F32(fy) * F32(z)
+        xc2 = np.full(len(lk), F32(z), np.float32)
+        Xw = np.stack([Tl[c] * (xc0 - Tl[3]) + Tl[4 + c] * (xc1 - Tl[7]) + Tl[8 + c] * (xc2 - Tl[11])
+                       for c in range(3)], 1).astype(np.float32)
+        mps = MapPoints(desc=ld, observations=np.ones(len(lk), np.int32), pos=Xw)
+        last = FrameView(keys=lk, desc=ld, fx=fx, fy=fy, cx=cx, cy=cy, max_x=640.0, max_y=480.0, scale_factors=sf,
+                         Tcw=np.vstack([Tl.reshape(3, 4), [0, 0, 0, 1]]).astype(np.float32))
+        cur = FrameView(keys=ck, desc=cd, fx=fx, fy=fy, cx=cx, cy=cy, max_x=640.0, max_y=480.0, scale_factors=sf,
+                        Tcw=np.vstack([T[p + 1].reshape(3, 4), [0, 0, 0, 1]]).astype(np.float32))
+        ref = np.full(len(ck), -1, np.int32)
+        nr = oracle.sbp_frame(cur, ref, last, np.arange(len(lk), dtype=np.int32), mps, 15.0, True, True)
+        assert nm[p + 1] == nr
+        assert np.array_equal(mp[p + 1][: n[p + 1]], ref)
+        assert nr > 200
