@@ -1,20 +1,24 @@
 #!/usr/bin/env python3
-"""bench.py -- ORB extraction throughput on MI355X (BASELINE.json metric).
+"""bench.py -- ORB extract + match throughput on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Workload (BASELINE.json configs[1]): a batch of B=256 synthetic 640x480 grayscale
-frames, nFeatures=1000, scaleFactor 1.2, 8 levels, FAST 20/7, extract-only, with a
-bit-exact descriptor check of a few frames against the CPU oracle outside the timed
-region.  A "step" = ORBextractor::operator() over the whole batch (device-resident
-frames in HBM -> keypoints + descriptors in HBM), one launch sequence on the
-extractor's HIP stream.  N>1: one process per GPU, each rank extracts its own batch
-(frames are independent: no data-path collective), "scaling": "weak".
+Workload (BASELINE.json configs[1], 640x480, nFeatures=1000, scale 1.2, 8 levels,
+FAST 20/7): each rank holds a batch of B=256 synthetic grayscale frames in HBM -- 256
+views of one textured canvas along a random camera walk (data: synthetic).  One step =
+  1. ORBextractor::operator() on all 256 frames (orbx_extract_batch_device), and
+  2. TrackWithMotionModel matching of every frame against its predecessor
+     (SearchByProjection(CurrentFrame, LastFrame, th=15, bMono) semantics, batched:
+     orbx_match_sequence_device),
+both enqueued on the extractor's HIP stream; inputs and outputs stay in HBM.  N>1: one
+process per GPU over RCCL, each rank its own batch (frames are independent: no
+data-path collective), "scaling": "weak".
 
-Prints ONE JSON line on rank 0 (contract in the task statement): value = frames/s
-of the whole job; roofline for the dominant kernel (HIP-event timed per stage on the
-extractor's stream); cpu_baseline = the oracle (C restatement) on this host.
+Prints ONE JSON line on rank 0: value = frames/s of the whole job; roofline for the
+dominant kernel (HIP events on the extractor's stream; algorithmic bytes in
+DESIGN.md §Roofline); cpu_baseline = the oracle (C restatement) on this host's cores;
+parity = bit-exact check of a few frames and one matched pair against the oracle.
 """
 from __future__ import annotations
 
@@ -31,6 +35,10 @@ sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+FX = FY = 500.0
+CX, CY = 320.0, 240.0
+DEPTH = 5.0
+TH = 15.0  # Tracking.cc:985 (mono / RGB-D search radius factor)
 
 
 def level_areas(W, H, nlevels=8, scale=1.2):
@@ -41,34 +49,35 @@ def level_areas(W, H, nlevels=8, scale=1.2):
     out = []
     for l in range(nlevels):
         inv = np.float32(1.0) / s[l]
-        w = int(np.rint(np.float32(W) * inv))
-        h = int(np.rint(np.float32(H) * inv))
-        out.append((w, h))
+        out.append((int(np.rint(np.float32(W) * inv)), int(np.rint(np.float32(H) * inv))))
     return out
 
 
 def stage_bytes(W, H, n_kps, nlevels=8, scale=1.2):
     """Algorithmic bytes per frame of each stage."""
-    A = [w * h for (w, h) in level_areas(W, H, nlevels, scale)]
+    lv = level_areas(W, H, nlevels, scale)
+    A = [w * h for (w, h) in lv]
     P = sum(A)
     return {
         # read input, write every level (level 0 copied), read levels 0..L-2 as resize sources
         "pyramid": A[0] + P + (P - A[-1]),
         # read every level once, write its Gaussian-blurred copy and its FAST strength map
         "score_blur": 3 * P,
-        # read the strength map of every FAST detection window once
-        "fast_cells": sum((w - 38) * (h - 38) for (w, h) in level_areas(W, H, nlevels, scale)),
-        # candidates in, kept keypoints out: 4 B each, ~3x n_kps candidates per level budget
+        # read the strength map of every FAST detection window once, write 4 B per kept candidate
+        "fast_cells": sum((w - 38) * (h - 38) for (w, h) in lv),
+        # candidates in, kept keypoints out (4 B each)
         "octree": 8 * n_kps,
-        # 28 B keypoint + 32 B descriptor out per keypoint (patch reads are L2 hits)
+        # 28 B keypoint + 32 B descriptor out per keypoint (patch reads hit L2)
         "describe": 60 * n_kps,
-        # SURVEY.md §8(d) canonical whole-pipeline figure
+        # matching: query + candidate descriptors and keypoints read once, 4 B assignment out
+        "match": (32 + 28) * 2 * n_kps + 4 * n_kps,
+        # SURVEY.md §8(d) canonical whole-extraction figure
         "total": A[0] + (P - A[0]) + 3 * P + 60 * n_kps,
     }
 
 
 def cpu_baseline(frames_np, seconds: float, threads: int):
-    """Oracle (TEST INFRASTRUCTURE) on host cores: frames/s over a bounded sample."""
+    """Oracle (TEST INFRASTRUCTURE) on host cores: extracted frames/s over a bounded sample."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import oracle as O
@@ -92,6 +101,47 @@ def cpu_baseline(frames_np, seconds: float, threads: int):
     return sum(done) / el, sum(done), el
 
 
+def poses(off):
+    """mTcw (rows 0..2) of each view: pure translation making pixel shifts consistent at DEPTH."""
+    T = np.zeros((len(off), 12), np.float32)
+    for b in range(len(off)):
+        T[b] = [1, 0, 0, -off[b, 0] * DEPTH / FX, 0, 1, 0, -off[b, 1] * DEPTH / FY, 0, 0, 1, 0]
+    return T
+
+
+def check_parity(frames_np, T, kps_all, desc_all, n_host, mp_all, nm_all, nframes, sf):
+    """Bit-exact check of the first frames' extraction and of pair (0 -> 1)'s matches."""
+    from oracle import oracle as O
+    from orbslam2commentedbyxcm_amd.matcher import FrameView, MapPoints
+    O.build()
+    p = O.params(1000, 1.2, 8, 20, 7)
+    ok = True
+    ref = []
+    for b in range(nframes):
+        kr, dr, _ = O.extract(frames_np[b], p)
+        n = int(n_host[b])
+        kg = kps_all[b, :n].view(np.uint8).reshape(n, 28)
+        ok &= n == len(kr) and np.array_equal(kg, kr.view(np.uint8).reshape(len(kr), 28)) \
+            and np.array_equal(desc_all[b, :n], dr)
+        ref.append((kr, dr))
+    F32 = np.float32
+    (lk, ld), (ck, cd) = ref[0], ref[1]
+    Tl = T[0]
+    xc0 = (lk["x"] - F32(CX)) / F32(FX) * F32(DEPTH)
+    xc1 = (lk["y"] - F32(CY)) / F32(FY) * F32(DEPTH)
+    xc2 = np.full(len(lk), F32(DEPTH), np.float32)
+    Xw = np.stack([Tl[c] * (xc0 - Tl[3]) + Tl[4 + c] * (xc1 - Tl[7]) + Tl[8 + c] * (xc2 - Tl[11])
+                   for c in range(3)], 1).astype(np.float32)
+    mps = MapPoints(desc=ld, observations=np.ones(len(lk), np.int32), pos=Xw)
+    mk = lambda k, d, t: FrameView(keys=k, desc=d, fx=FX, fy=FY, cx=CX, cy=CY, max_x=640.0, max_y=480.0,  # noqa
+                                   scale_factors=sf, Tcw=np.vstack([t.reshape(3, 4), [0, 0, 0, 1]]).astype(np.float32))
+    cur_ref = np.full(len(ck), -1, np.int32)
+    nr = O.sbp_frame(mk(ck, cd, T[1]), cur_ref, mk(lk, ld, T[0]), np.arange(len(lk), dtype=np.int32), mps, TH,
+                     True, True)
+    ok &= int(nm_all[1]) == nr and np.array_equal(mp_all[1, :len(ck)], cur_ref)
+    return {"frames_checked": nframes, "pairs_checked": 1, "bit_exact": bool(ok), "matches_pair0": int(nr)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -100,6 +150,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--no-match", action="store_true", help="extraction only")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, available cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -110,11 +161,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
     B, W, H = args.batch, args.width, args.height
+    match = not args.no_match
 
-    # Render frames before anything touches the GPU (the pool forks).
-    frames_np = None
     from orbslam2commentedbyxcm_amd import synth
-    frames_np = synth.frames(B, W, H, first_seed=rank * B, workers=min(16, os.cpu_count() or 1))
+    frames_np, off = synth.sequence(1000 + rank, B, W, H)
+    T = poses(off)
 
     import torch
     import torch.distributed as dist
@@ -125,17 +176,26 @@ def main():
     dev = torch.device("cuda", local_rank)
 
     from orbslam2commentedbyxcm_amd import ORBextractor
+    from orbslam2commentedbyxcm_amd.matcher import ORBmatcher
     ex = ORBextractor(1000, 1.2, 8, 20, 7, device=local_rank)
+    matcher = ORBmatcher(0.9, True, device=local_rank)  # TrackWithMotionModel, Tracking.cc:968
+    sf = ex.GetScaleFactors()
     cap = ex.max_keypoints(W, H)
     d_frames = torch.from_numpy(frames_np).to(dev)
+    d_T = torch.from_numpy(T).to(dev)
     d_kps = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)
     d_desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
     d_n = torch.empty((B,), dtype=torch.int32, device=dev)
-    sync_all = torch.cuda.synchronize
-    sync_all(dev)  # frames uploaded on torch's stream before the extractor's stream reads them
+    d_mp = torch.empty((B, cap), dtype=torch.int32, device=dev)
+    d_nm = torch.empty((B,), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)  # uploads on torch's stream finish before the extractor's stream reads them
+    stream = ex.stream_handle()
 
     def step():
         ex.extract_batch_device(d_frames, d_kps, d_desc, d_n)
+        if match:
+            matcher.match_sequence_device(d_kps, d_desc, d_n, d_T, d_mp, d_nm, sf, FX, FY, CX, CY, W, H,
+                                          depth=DEPTH, th=TH, stream=stream)
 
     def sync():
         torch.cuda.synchronize(dev)
@@ -160,56 +220,47 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    total_frames = B * args.steps * world
-    value = total_frames / elapsed
+    value = B * args.steps * world / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
-    # keypoint statistics of this batch
     n_host = d_n.cpu().numpy()
     mean_kps = float(n_host.mean())
+    mean_matches = float(d_nm.cpu().numpy()[1:].mean()) if match else 0.0
 
     # per-stage HIP-event timing on the extractor's stream (separate, untimed pass)
     ex.set_timing(True)
+    matcher.set_timing(True)
     reps = 5
     acc = {}
     for _ in range(reps):
         step()
         st = ex.stage_times()
+        if match:
+            st["match"] = matcher.last_ms()
         for k, v in st.items():
             acc[k] = acc.get(k, 0.0) + v
     sync()
     ex.set_timing(False)
+    matcher.set_timing(False)
     stage_ms = {k: v / reps for k, v in acc.items()}
     bytes_pf = stage_bytes(W, H, mean_kps)
     kernels = {k: v for k, v in stage_ms.items() if k != "total"}
     dom = max(kernels, key=kernels.get)
     achieved = bytes_pf[dom] * B / (stage_ms[dom] * 1e-3) / 1e9
-    pipeline_gbs = bytes_pf["total"] * B / (stage_ms["total"] * 1e-3) / 1e9
 
-    # bit-exact descriptor check of a few frames vs the oracle (outside the timed region)
     parity = None
-    if rank == 0 and args.parity_frames > 0:
-        from oracle import oracle as O
-        O.build()
-        p = O.params(1000, 1.2, 8, 20, 7)
-        kps_all = d_kps.cpu().numpy()
-        desc_all = d_desc.cpu().numpy()
-        ok = True
-        for b in range(min(args.parity_frames, B)):
-            kr, dr, _ = O.extract(frames_np[b], p)
-            n = int(n_host[b])
-            kg = kps_all[b, :n].view(np.uint8).reshape(n, 28)
-            kref = kr.view(np.uint8).reshape(len(kr), 28)
-            ok &= n == len(kr) and np.array_equal(kg, kref) and np.array_equal(desc_all[b, :n], dr)
-        parity = {"frames_checked": min(args.parity_frames, B), "bit_exact": bool(ok)}
+    if rank == 0 and args.parity_frames > 0 and match:
+        parity = check_parity(frames_np, T, d_kps.cpu().numpy(), d_desc.cpu().numpy(), n_host, d_mp.cpu().numpy(),
+                              d_nm.cpu().numpy(), max(2, args.parity_frames), sf)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         fps, nfr, el = cpu_baseline(frames_np[:32], args.cpu_seconds, threads)
         cpu = {"value": round(fps, 2), "unit": "frames/s", "cores": threads, "kind": "port",
-               "sample": f"{nfr} synthetic 640x480 frames (32 distinct) in {el:.1f}s, oracle C restatement "
-                         f"of ORBextractor::operator(), -O2 scalar, {threads} threads"}
+               "sample": f"{nfr} synthetic 640x480 frames (32 distinct) in {el:.1f}s: oracle C restatement of "
+                         f"ORBextractor::operator() (extraction only, matching not timed), -O2 scalar, "
+                         f"{threads} threads"}
 
     if rank == 0:
         out = {
@@ -225,17 +276,19 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": "configs[1]: batch of 256 synthetic 640x480 gray frames, nFeatures=1000, "
-                                   "scale 1.2, 8 levels, FAST 20/7, extract-only",
-                       "global_batch": B * world, "frames_per_gpu_step": B, "width": W, "height": H,
+            "config": {"workload": "configs[1]: 256 synthetic 640x480 gray frames per GPU (views of one textured canvas "
+                                   "along a random walk), nFeatures=1000, scale 1.2, 8 levels, FAST 20/7; step = "
+                                   "extract all frames + TrackWithMotionModel SearchByProjection of each frame "
+                                   "against its predecessor" + ("" if match else " (match disabled)"),
+                       "frames_per_gpu_step": B, "global_batch": B * world, "width": W, "height": H,
                        "parallelism": f"frame-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
-                         "pipeline_algorithmic_GBs": round(pipeline_gbs, 2)},
+                         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()}},
             "cpu_baseline": cpu,
             "parity": parity,
             "mean_keypoints_per_frame": round(mean_kps, 1),
+            "mean_matches_per_pair": round(mean_matches, 1),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

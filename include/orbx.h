@@ -220,6 +220,10 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
                                const float* scale_factors, int nlevels, float depth, float th,
                                int32_t* d_cur_mp, int32_t* d_nmatches, void* stream);
 
+/* HIP-event timing of orbx_match_sequence_device (milliseconds of the last call). */
+int orbx_matcher_set_timing(orbx_matcher* m, int enable);
+int orbx_matcher_last_ms(orbx_matcher* m, float* ms);
+
 /* SearchForTriangulation(KF1, KF2, F12, vMatchedPairs, bOnlyStereo)
  * ORBmatcher.cc:850-1056 (LocalMapping::CreateNewMapPoints, LocalMapping.cc:305).
  * DBoW2 FeatureVectors as CSR: node ids ascending (fv_node[k]), keypoints of node k

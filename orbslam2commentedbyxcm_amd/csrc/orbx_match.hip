@@ -138,67 +138,104 @@ __device__ __forceinline__ CellRange cell_range(const ProjProblem& pb, float x, 
     return c;
 }
 
+constexpr unsigned kNoKey32 = 0xffffffffu;
 constexpr unsigned long long kNoKey = ~0ull;
+constexpr int kNoCell = 0xfff;
+constexpr int kNumCells = kGridCols * kGridRows;
 
-// Top-2 (distance, candidate order) keys of query Q over the frame's keypoints, with the
-// candidate set of GetFeaturesInArea + the overload's filters.  Candidate order is
-// the reference's iteration order: grid column, grid row, keypoint index.
-__device__ void score_query(const ProjProblem& pb, const ProjParams& P, const ProjQuery& Q,
+// The frame's keypoints sorted by (grid cell, index) -- Frame::mGrid flattened: cell
+// c = ix*FRAME_GRID_ROWS + iy holds sorted positions [cstart[c], cstart[c+1]).  The
+// cells of one grid column are contiguous, so GetFeaturesInArea's walk (ix ascending,
+// iy ascending, index ascending) is a list of contiguous runs and a candidate's sorted
+// position is its rank in the reference's iteration order.
+struct SortedGrid {
+    const unsigned* skey;  // (cell << 13) | index, ascending
+    const int* cstart;
+    const float* sx;
+    const float* sy;
+    const int* soct;
+};
+
+// Top-2 keys (distance << 13 | sorted position) of query Q over the candidate set of
+// GetFeaturesInArea + the overload's filters, with the initial / current claims fmp.
+__device__ void score_query(const ProjProblem& pb, const ProjParams& P, const ProjQuery& Q, const SortedGrid& G,
                             const unsigned long long q0, const unsigned long long q1, const unsigned long long q2,
-                            const unsigned long long q3, const float* kx, const float* ky, const int* meta,
-                            const int* fmp, unsigned long long& k1, unsigned long long& k2) {
+                            const unsigned long long q3, const int* fmp, unsigned& k1, unsigned& k2) {
     const int lane = threadIdx.x & 63;
-    k1 = kNoKey;
-    k2 = kNoKey;
+    k1 = kNoKey32;
+    k2 = kNoKey32;
     const CellRange cr = cell_range(pb, Q.u, Q.v, Q.r);
     if (!cr.empty) {
         const bool check_levels = (Q.min_level > 0) || (Q.max_level >= 0);
-        for (int i = lane; i < pb.n; i += 64) {
-            const int m = meta[i];
-            const int cell = m >> 8;
-            if (cell == 0xfff) continue;
-            const int cx = cell / kGridRows, cy = cell - cx * kGridRows;
-            if (cx < cr.x0 || cx > cr.x1 || cy < cr.y0 || cy > cr.y1) continue;
-            const int oct = m & 0xff;
-            if (check_levels) {
-                if (oct < Q.min_level) continue;
-                if (Q.max_level >= 0 && oct > Q.max_level) continue;
+        for (int ix = cr.x0; ix <= cr.x1; ix++) {
+            const int beg = G.cstart[ix * kGridRows + cr.y0], end = G.cstart[ix * kGridRows + cr.y1 + 1];
+            for (int p = beg + lane; p < end; p += 64) {
+                const int oct = G.soct[p];
+                if (check_levels) {
+                    if (oct < Q.min_level) continue;
+                    if (Q.max_level >= 0 && oct > Q.max_level) continue;
+                }
+                const float distx = G.sx[p] - Q.u;
+                const float disty = G.sy[p] - Q.v;
+                if (!(fabsf(distx) < Q.r && fabsf(disty) < Q.r)) continue;
+                if (Q.post_min >= 0 && (oct < Q.post_min || oct > Q.post_max)) continue;
+                const int i = (int)(G.skey[p] & 0x1fffu);
+                if (kp_blocked(fmp[i], P)) continue;
+                if (Q.er_max >= 0.f && pb.u_right && pb.u_right[i] > 0) {
+                    const float er = fabsf(Q.ur - pb.u_right[i]);
+                    if (er > Q.er_max) continue;
+                }
+                const unsigned long long* t = (const unsigned long long*)(pb.desc + (size_t)i * 32);
+                const int d = __popcll(q0 ^ t[0]) + __popcll(q1 ^ t[1]) + __popcll(q2 ^ t[2]) + __popcll(q3 ^ t[3]);
+                const unsigned key = ((unsigned)d << 13) | (unsigned)p;
+                if (key < k1) { k2 = k1; k1 = key; }
+                else if (key < k2) { k2 = key; }
             }
-            const float distx = kx[i] - Q.u;
-            const float disty = ky[i] - Q.v;
-            if (!(fabsf(distx) < Q.r && fabsf(disty) < Q.r)) continue;
-            if (Q.post_min >= 0 && (oct < Q.post_min || oct > Q.post_max)) continue;
-            if (kp_blocked(fmp[i], P)) continue;
-            if (Q.er_max >= 0.f && pb.u_right && pb.u_right[i] > 0) {
-                const float er = fabsf(Q.ur - pb.u_right[i]);
-                if (er > Q.er_max) continue;
-            }
-            const unsigned long long* t = (const unsigned long long*)(pb.desc + (size_t)i * 32);
-            const int d = __popcll(q0 ^ t[0]) + __popcll(q1 ^ t[1]) + __popcll(q2 ^ t[2]) + __popcll(q3 ^ t[3]);
-            const unsigned long long key = ((unsigned long long)d << 25) | ((unsigned long long)cell << 13) | (unsigned)i;
-            if (key < k1) { k2 = k1; k1 = key; }
-            else if (key < k2) { k2 = key; }
         }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long o1 = __shfl_xor(k1, o), o2 = __shfl_xor(k2, o);
-        const unsigned long long hi = k1 < o1 ? o1 : k1;
-        const unsigned long long lo2 = k2 < o2 ? k2 : o2;
+        const unsigned o1 = __shfl_xor(k1, o), o2 = __shfl_xor(k2, o);
+        const unsigned hi = k1 < o1 ? o1 : k1;
+        const unsigned lo2 = k2 < o2 ? k2 : o2;
         k1 = k1 < o1 ? k1 : o1;
         k2 = hi < lo2 ? hi : lo2;
     }
 }
 
-__device__ __forceinline__ int key_idx(unsigned long long k) { return (int)(k & 0x1fffu); }
-__device__ __forceinline__ int key_dist(unsigned long long k) { return (int)(k >> 25); }
+__device__ __forceinline__ int key_dist(unsigned k) { return (int)(k >> 13); }
+__device__ __forceinline__ int key_pos(unsigned k) { return (int)(k & 0x1fffu); }
 
-// One workgroup per problem (one SearchByProjection call).  Waves score the queries in
-// parallel against the keypoints' initial mvpMapPoints state; wave 0 then replays the
-// reference's sequential loop: each query claims its best keypoint in order, and a
-// query whose best (or, with the ratio test, second) keypoint was claimed by an
-// earlier query is re-scored against the current state.  Finally the rotation
-// histogram (ORBmatcher.cc:1750-1786) un-matches bins outside the three maxima.
+// Ascending in-place bitonic sort of n2 (power of two) u32 keys by a 256-thread block.
+__device__ void block_bitonic_sort(unsigned* a, int n2) {
+    for (int k = 2; k <= n2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < n2; i += 256) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const unsigned x = a[i], y = a[l];
+                    const bool up = (i & k) == 0;
+                    if ((x > y) == up) {
+                        a[i] = y;
+                        a[l] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// One workgroup per problem (one SearchByProjection call).  The frame's keypoints are
+// sorted into grid order in LDS; waves score the queries in parallel against the
+// keypoints' initial mvpMapPoints state; wave 0 then replays the reference's
+// sequential loop: each query claims its best keypoint in order, and a query whose
+// best (or, with the ratio test, second) keypoint was claimed by an earlier query is
+// re-scored against the current state.  Finally the rotation histogram
+// (ORBmatcher.cc:1750-1786) un-matches bins outside the three maxima.
+// QLDS: per-query state in LDS (the serial replay then touches no global memory);
+// otherwise in the problem's global scratch (3 x u64 per query).
+template <bool QLDS>
 __global__ __launch_bounds__(256) void k_proj_search(const ProjProblem* __restrict__ probs, ProjParams P,
                                                      unsigned long long* __restrict__ scratch,
                                                      const long long* __restrict__ scratch_off) {
@@ -206,66 +243,108 @@ __global__ __launch_bounds__(256) void k_proj_search(const ProjProblem* __restri
     __shared__ int s_hist[kHistoLength];
     const ProjProblem pb = probs[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int n = pb.n;
-    float* kx = (float*)smem;
-    float* ky = kx + n;
-    int* meta = (int*)(ky + n);
-    int* fmp = meta + n;
-    int* mlist = fmp + n;                                                // matched kp per accepted query
-    int* mbin = mlist + pb.nq;                                           // its rotation bin
-    unsigned long long* keys2 = scratch + scratch_off[blockIdx.x];      // 2 per query
-    for (int i = tid; i < n; i += 256) {
-        const orbx_keypoint kp = pb.keys[i];
-        kx[i] = kp.x;
-        ky[i] = kp.y;
-        const int px = (int)roundf((kp.x - pb.min_x) * pb.inv_w);  // Frame::PosInGrid, Frame.cc:558-567
-        const int py = (int)roundf((kp.y - pb.min_y) * pb.inv_h);
-        const int cell = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? 0xfff : px * kGridRows + py;
-        meta[i] = (kp.octave & 0xff) | (cell << 8);
-        fmp[i] = pb.frame_mp[i];
+    const int n = pb.n, nq = pb.nq;
+    int n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    unsigned* skey = (unsigned*)smem;
+    int* cstart = (int*)(skey + n2);
+    float* sx = (float*)(cstart + kNumCells + 1);
+    float* sy = sx + n;
+    int* soct = (int*)(sy + n);
+    int* fmp = soct + n;
+    float* kang = (float*)(fmp + n);
+    unsigned* qk;
+    int *mlist, *mbin, *qmp;
+    float* qang;
+    if (QLDS) {
+        qk = (unsigned*)(kang + n);
+        mlist = (int*)(qk + 2 * nq);
+    } else {
+        unsigned long long* g = scratch + scratch_off[blockIdx.x];
+        qk = (unsigned*)g;
+        mlist = (int*)(g + nq);
+    }
+    mbin = mlist + nq;
+    qmp = mbin + nq;
+    qang = (float*)(qmp + nq);
+    for (int i = tid; i < n2; i += 256) {
+        unsigned key = 0xffffffffu;
+        if (i < n) {
+            const orbx_keypoint kp = pb.keys[i];
+            const int px = (int)roundf((kp.x - pb.min_x) * pb.inv_w);  // Frame::PosInGrid, Frame.cc:558-567
+            const int py = (int)roundf((kp.y - pb.min_y) * pb.inv_h);
+            const int cell = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? kNoCell : px * kGridRows + py;
+            key = ((unsigned)cell << 13) | (unsigned)i;
+            fmp[i] = pb.frame_mp[i];
+            kang[i] = kp.angle;
+        }
+        skey[i] = key;
     }
     if (tid < kHistoLength) s_hist[tid] = 0;
     __syncthreads();
-    for (int q = wave; q < pb.nq; q += 4) {
+    block_bitonic_sort(skey, n2);
+    for (int p = tid; p < n; p += 256) {
+        const orbx_keypoint kp = pb.keys[skey[p] & 0x1fffu];
+        sx[p] = kp.x;
+        sy[p] = kp.y;
+        soct[p] = kp.octave;
+    }
+    for (int c = tid; c <= kNumCells; c += 256) {  // lower_bound of (c << 13)
+        const unsigned target = (unsigned)c << 13;
+        int lo = 0, hi = n;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (skey[mid] < target) lo = mid + 1;
+            else hi = mid;
+        }
+        cstart[c] = lo;
+    }
+    __syncthreads();
+    SortedGrid G{skey, cstart, sx, sy, soct};
+    for (int q = wave; q < nq; q += 4) {
         const ProjQuery Q = pb.q[q];
-        unsigned long long k1 = kNoKey, k2 = kNoKey;
+        unsigned k1 = kNoKey32, k2 = kNoKey32;
         if (Q.mp >= 0) {
             const unsigned long long* qd = (const unsigned long long*)(pb.qdesc + (size_t)q * 32);
-            score_query(pb, P, Q, qd[0], qd[1], qd[2], qd[3], kx, ky, meta, fmp, k1, k2);
+            score_query(pb, P, Q, G, qd[0], qd[1], qd[2], qd[3], fmp, k1, k2);
         }
         if (lane == 0) {
-            keys2[2 * q] = k1;
-            keys2[2 * q + 1] = k2;
+            qk[2 * q] = k1;
+            qk[2 * q + 1] = k2;
+            qmp[q] = Q.mp;
+            qang[q] = Q.angle;
         }
     }
     __syncthreads();
     if (wave == 0) {
         int nmatch = 0, nrec = 0;
         const float factor = kHistoLength / 360.0f;
-        for (int q = 0; q < pb.nq; q++) {
-            const ProjQuery Q = pb.q[q];
-            if (Q.mp < 0) continue;
-            unsigned long long k1 = keys2[2 * q], k2 = keys2[2 * q + 1];
-            bool stale = (k1 != kNoKey && kp_blocked(fmp[key_idx(k1)], P)) ||
-                         (P.ratio_mode && k2 != kNoKey && kp_blocked(fmp[key_idx(k2)], P));
+        for (int q = 0; q < nq; q++) {
+            const int mp = qmp[q];
+            if (mp < 0) continue;
+            unsigned k1 = qk[2 * q], k2 = qk[2 * q + 1];
+            const bool stale =
+                (k1 != kNoKey32 && kp_blocked(fmp[skey[key_pos(k1)] & 0x1fffu], P)) ||
+                (P.ratio_mode && k2 != kNoKey32 && kp_blocked(fmp[skey[key_pos(k2)] & 0x1fffu], P));
             if (stale) {
+                const ProjQuery Q = pb.q[q];
                 const unsigned long long* qd = (const unsigned long long*)(pb.qdesc + (size_t)q * 32);
-                score_query(pb, P, Q, qd[0], qd[1], qd[2], qd[3], kx, ky, meta, fmp, k1, k2);
+                score_query(pb, P, Q, G, qd[0], qd[1], qd[2], qd[3], fmp, k1, k2);
             }
-            if (k1 == kNoKey) continue;
+            if (k1 == kNoKey32) continue;
             const int bestDist = key_dist(k1);
             if (bestDist > P.accept_th) continue;
-            const int idx1 = key_idx(k1);
+            const int idx1 = (int)(skey[key_pos(k1)] & 0x1fffu);
             if (P.ratio_mode) {
-                const int bestLevel = meta[idx1] & 0xff;
-                const int bestLevel2 = k2 == kNoKey ? -1 : (meta[key_idx(k2)] & 0xff);
-                const int bestDist2 = k2 == kNoKey ? 256 : key_dist(k2);
+                const int bestLevel = soct[key_pos(k1)];
+                const int bestLevel2 = k2 == kNoKey32 ? -1 : soct[key_pos(k2)];
+                const int bestDist2 = k2 == kNoKey32 ? 256 : key_dist(k2);
                 if (bestLevel == bestLevel2 && (float)bestDist > P.nnratio * (float)bestDist2) continue;
             }
-            if (lane == 0) fmp[idx1] = Q.mp;
+            if (lane == 0) fmp[idx1] = mp;
             nmatch++;
             if (P.check_ori) {
-                float rot = Q.angle - pb.keys[idx1].angle;
+                float rot = qang[q] - kang[idx1];
                 if (rot < 0.0f) rot += 360.0f;
                 int bin = (int)roundf(rot * factor);
                 if (bin == kHistoLength) bin = 0;
@@ -298,14 +377,13 @@ __global__ __launch_bounds__(256) void k_proj_search(const ProjProblem* __restri
             }
             if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
             else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
-            for (int m = lane; m < nrec; m += 64) {
-                const int b = mbin[m];
-                if (b != ind1 && b != ind2 && b != ind3) fmp[mlist[m]] = -1;
-            }
             int bad = 0;
             for (int m = lane; m < nrec; m += 64) {
                 const int b = mbin[m];
-                bad += (b != ind1 && b != ind2 && b != ind3);
+                if (b != ind1 && b != ind2 && b != ind3) {
+                    fmp[mlist[m]] = -1;
+                    bad++;
+                }
             }
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o);
@@ -344,7 +422,7 @@ __global__ __launch_bounds__(256) void k_seq_build(SeqArgs A, ProjQuery* __restr
         pb.inv_h = (float)kGridRows / (A.max_y - A.min_y);
         pb.nmatches = A.nmatches + p + 1;
         probs[p] = pb;
-        scratch_off[p] = (long long)p * 2 * A.cap;
+        scratch_off[p] = (long long)p * 3 * A.cap;
     }
     if (i >= A.cap) return;
     ProjQuery q{};
@@ -394,14 +472,25 @@ hipError_t launch_seq_build(const SeqArgs& A, int npairs, ProjQuery* queries, Pr
 hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned long long* scratch,
                               const long long* d_scratch_off, int max_n, int max_nq, hipStream_t stream) {
     if (nprob <= 0) return hipSuccess;
-    const size_t lds = (size_t)max_n * 16 + (size_t)max_nq * 8;
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (max_n >= 8192) return hipErrorInvalidValue;  // 13-bit keypoint positions
+    size_t n2 = 1;
+    while (n2 < (size_t)max_n) n2 <<= 1;
+    const size_t base = n2 * 4 + (size_t)(kNumCells + 1) * 4 + (size_t)max_n * 20;
+    const size_t with_q = base + (size_t)max_nq * 24;
+    const size_t limit = 160 * 1024;
+    if (base > limit) return hipErrorInvalidValue;
+    const bool qlds = with_q <= limit;
+    const size_t lds = qlds ? with_q : base;
+    const void* fn = qlds ? (const void*)k_proj_search<true> : (const void*)k_proj_search<false>;
     if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_proj_search, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)lds);
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_proj_search, dim3(nprob), dim3(256), lds, stream, d_probs, P, scratch, d_scratch_off);
+    if (qlds)
+        hipLaunchKernelGGL(k_proj_search<true>, dim3(nprob), dim3(256), lds, stream, d_probs, P, scratch, d_scratch_off);
+    else
+        hipLaunchKernelGGL(k_proj_search<false>, dim3(nprob), dim3(256), lds, stream, d_probs, P, scratch,
+                           d_scratch_off);
     return hipGetLastError();
 }
 

@@ -82,6 +82,9 @@ struct orbx_matcher {
     int check_ori = 1;
     hipStream_t stream = nullptr;
     Arena arena;
+    bool timing = false;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool have_time = false;
 };
 
 namespace {
@@ -99,7 +102,7 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
     const int nobs = mps->n;
     size_t need = pad(sizeof(orbx_keypoint) * n) + pad((size_t)n * 32) + pad(sizeof(float) * n) +
                   pad(sizeof(int32_t) * n) + pad(sizeof(ProjQuery) * nq) + pad((size_t)nq * 32) +
-                  pad(sizeof(int32_t) * (nobs ? nobs : 1)) + pad(sizeof(ProjProblem)) + pad(16 * (size_t)nq) +
+                  pad(sizeof(int32_t) * (nobs ? nobs : 1)) + pad(sizeof(ProjProblem)) + pad(24 * (size_t)nq) +
                   pad(sizeof(long long)) + pad(sizeof(int32_t));
     HIP_TRY(m->arena.reserve(need));
     m->arena.used = 0;
@@ -111,7 +114,7 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
     auto* d_qd = m->arena.take<uint8_t>((size_t)nq * 32);
     auto* d_obs = m->arena.take<int32_t>(nobs ? nobs : 1);
     auto* d_prob = m->arena.take<ProjProblem>(1);
-    auto* d_scr = m->arena.take<unsigned long long>(2 * (size_t)nq);
+    auto* d_scr = m->arena.take<unsigned long long>(3 * (size_t)nq);
     auto* d_off = m->arena.take<long long>(1);
     auto* d_nm = m->arena.take<int32_t>(1);
     hipStream_t s = m->stream;
@@ -179,6 +182,8 @@ void orbx_matcher_destroy(orbx_matcher* m) {
     (void)hipSetDevice(m->device);
     if (m->stream) (void)hipStreamSynchronize(m->stream);
     if (m->arena.base) (void)hipFree(m->arena.base);
+    for (auto& e : m->ev)
+        if (e) (void)hipEventDestroy(e);
     if (m->stream) (void)hipStreamDestroy(m->stream);
     delete m;
 }
@@ -301,7 +306,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     const size_t need = pad(sizeof(ProjQuery) * (size_t)(npairs > 0 ? npairs : 1) * cap) +
                         pad(sizeof(ProjProblem) * (size_t)(npairs > 0 ? npairs : 1)) +
                         pad(sizeof(long long) * (size_t)(npairs > 0 ? npairs : 1)) +
-                        pad(sizeof(unsigned long long) * 2 * (size_t)(npairs > 0 ? npairs : 1) * cap);
+                        pad(sizeof(unsigned long long) * 3 * (size_t)(npairs > 0 ? npairs : 1) * cap);
     if (m->arena.cap < need) {
         HIP_TRY(hipStreamSynchronize(s));
         HIP_TRY(m->arena.reserve(need));
@@ -310,7 +315,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     auto* d_q = m->arena.take<ProjQuery>((size_t)(npairs > 0 ? npairs : 1) * cap);
     auto* d_prob = m->arena.take<ProjProblem>(npairs > 0 ? npairs : 1);
     auto* d_off = m->arena.take<long long>(npairs > 0 ? npairs : 1);
-    auto* d_scr = m->arena.take<unsigned long long>(2 * (size_t)(npairs > 0 ? npairs : 1) * cap);
+    auto* d_scr = m->arena.take<unsigned long long>(3 * (size_t)(npairs > 0 ? npairs : 1) * cap);
     HIP_TRY(hipMemsetAsync(d_cur_mp, 0xff, sizeof(int32_t) * (size_t)batch * cap, s));
     HIP_TRY(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * (size_t)batch, s));
     if (npairs == 0) return ORBX_OK;
@@ -334,6 +339,11 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     for (int l = 0; l < nlevels; l++) A.scale[l] = scale_factors[l];
     A.cur_mp = d_cur_mp;
     A.nmatches = d_nmatches;
+    if (m->timing) {
+        for (auto& e : m->ev)
+            if (!e) HIP_TRY(hipEventCreate(&e));
+        HIP_TRY(hipEventRecord(m->ev[0], s));
+    }
     HIP_TRY(launch_seq_build(A, npairs, d_q, d_prob, d_off, s));
     ProjParams P{};
     P.mp_obs = nullptr;
@@ -342,6 +352,24 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     P.ratio_mode = 0;
     P.check_ori = m->check_ori;
     HIP_TRY(launch_proj_search(d_prob, npairs, P, d_scr, d_off, cap, cap, s));
+    if (m->timing) {
+        HIP_TRY(hipEventRecord(m->ev[1], s));
+        m->have_time = true;
+    }
+    return ORBX_OK;
+}
+
+int orbx_matcher_set_timing(orbx_matcher* m, int enable) {
+    if (!m) return fail(ORBX_ERR_ARG, "null matcher");
+    m->timing = enable != 0;
+    return ORBX_OK;
+}
+
+int orbx_matcher_last_ms(orbx_matcher* m, float* ms) {
+    if (!m || !ms) return fail(ORBX_ERR_ARG, "null argument");
+    if (!m->have_time) return fail(ORBX_ERR_STATE, "no timed call");
+    HIP_TRY(hipEventSynchronize(m->ev[1]));
+    HIP_TRY(hipEventElapsedTime(ms, m->ev[0], m->ev[1]));
     return ORBX_OK;
 }
 

@@ -239,6 +239,14 @@ class ORBmatcher:
             sf.ctypes.data_as(F32P), len(sf), depth, th, C.c_void_p(d_cur_mp.data_ptr()),
             C.c_void_p(d_nmatches.data_ptr()), s))
 
+    def set_timing(self, enable: bool = True) -> None:
+        L.check(L.lib().orbx_matcher_set_timing(self._h, 1 if enable else 0))
+
+    def last_ms(self) -> float:
+        t = C.c_float()
+        L.check(L.lib().orbx_matcher_last_ms(self._h, C.byref(t)))
+        return t.value
+
     def score_windows(self, qdesc, tdesc, tlevel, cand_off, cand, tie_last: bool = False) -> dict:
         """Batched candidate scoring (best / second-best Hamming) on the GPU."""
         q = np.ascontiguousarray(qdesc, dtype=np.uint8)
