@@ -147,70 +147,165 @@ constexpr int kNumCells = kGridCols * kGridRows;
 // c = ix*FRAME_GRID_ROWS + iy holds sorted positions [cstart[c], cstart[c+1]).  The
 // cells of one grid column are contiguous, so GetFeaturesInArea's walk (ix ascending,
 // iy ascending, index ascending) is a list of contiguous runs and a candidate's sorted
-// position is its rank in the reference's iteration order.
+// position is its rank in the reference's iteration order.  All per-keypoint state
+// (position, octave, angle, descriptor, mvpMapPoints claim) is kept in sorted order.
 struct SortedGrid {
-    const unsigned* skey;  // (cell << 13) | index, ascending
+    const unsigned* skey;   // (cell << 13) | index, ascending
     const int* cstart;
-    const float* sx;
-    const float* sy;
-    const int* soct;
+    const float4* skp;      // x, y, octave (int bits), angle
+    const uint4* sdesc;     // 2 x uint4 per keypoint, or null (descriptors read from global)
 };
 
-// Top-2 keys (distance << 13 | sorted position) of query Q over the candidate set of
-// GetFeaturesInArea + the overload's filters, with the initial / current claims fmp.
-__device__ void score_query(const ProjProblem& pb, const ProjParams& P, const ProjQuery& Q, const SortedGrid& G,
-                            const unsigned long long q0, const unsigned long long q1, const unsigned long long q2,
-                            const unsigned long long q3, const int* fmp, unsigned& k1, unsigned& k2) {
-    const int lane = threadIdx.x & 63;
-    k1 = kNoKey32;
-    k2 = kNoKey32;
-    const CellRange cr = cell_range(pb, Q.u, Q.v, Q.r);
-    if (!cr.empty) {
-        const bool check_levels = (Q.min_level > 0) || (Q.max_level >= 0);
-        for (int ix = cr.x0; ix <= cr.x1; ix++) {
-            const int beg = G.cstart[ix * kGridRows + cr.y0], end = G.cstart[ix * kGridRows + cr.y1 + 1];
-            for (int p = beg + lane; p < end; p += 64) {
-                const int oct = G.soct[p];
-                if (check_levels) {
-                    if (oct < Q.min_level) continue;
-                    if (Q.max_level >= 0 && oct > Q.max_level) continue;
+constexpr int kProjThreads = 1024;
+constexpr unsigned kNoEntry = 0xffffffffu;
+
+// Candidate-list entry: distance << 18 | octave << 13 | sorted position.  Entries of a
+// query are kept in the reference's (distance, iteration order) order.
+__device__ __forceinline__ int ent_dist(unsigned e) { return (int)(e >> 18); }
+__device__ __forceinline__ int ent_oct(unsigned e) { return (int)((e >> 13) & 31u); }
+__device__ __forceinline__ int ent_pos(unsigned e) { return (int)(e & 0x1fffu); }
+
+// Row minimum over the 16 lanes of each DPP row (quad_perm [1,0,3,2], [2,3,0,1],
+// row_half_mirror, row_mirror): every lane of the row ends with the row's minimum.
+// Must be called with the whole wave active.
+__device__ __forceinline__ unsigned umin_(unsigned a, unsigned b) { return a < b ? a : b; }
+__device__ __forceinline__ unsigned row_min_u32(unsigned v) {
+    v = umin_(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));
+    v = umin_(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));
+    v = umin_(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false));
+    v = umin_(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false));
+    return v;
+}
+
+// A query and its MapPoint descriptor held in registers (loaded ahead of use so the
+// global latency overlaps the LDS work of the previous query).
+struct QueryReg {
+    ProjQuery q;
+    uint4 d0, d1;
+};
+static_assert(sizeof(ProjQuery) == 48, "ProjQuery layout");
+
+__device__ __forceinline__ QueryReg load_query(const ProjProblem& pb, int q) {
+    QueryReg r;
+    r.q = pb.q[q];
+    const uint4* d = (const uint4*)(pb.qdesc + (size_t)q * 32);
+    r.d0 = d[0];
+    r.d1 = d[1];
+    return r;
+}
+
+// Lane `src`'s query, broadcast to the whole wave (v_readlane per word).
+__device__ __forceinline__ QueryReg bcast_query(const QueryReg& x, int src) {
+    constexpr int kW = (int)(sizeof(QueryReg) / 4);
+    static_assert(sizeof(QueryReg) % 4 == 0, "QueryReg words");
+    int w[kW];
+    __builtin_memcpy(w, &x, sizeof(QueryReg));
+#pragma unroll
+    for (int i = 0; i < kW; i++) w[i] = __builtin_amdgcn_readlane(w[i], src);
+    QueryReg r;
+    __builtin_memcpy(&r, w, sizeof(QueryReg));
+    return r;
+}
+
+// The four best candidates of a query (GetFeaturesInArea + the overload's filters)
+// against the current claims sfmp, as entries (kNoEntry = fewer candidates).  One
+// 16-lane row per query, four queries per wave: the row's lanes split the columns of
+// the query's cell window (and the sorted-position runs inside them), keep a local
+// top-4 of (distance << 13 | position) and merge it by DPP row minima.  The
+// candidate windows hold a few to a few tens of keypoints, so a row keeps its lanes
+// busy where a whole wave per query would mostly idle.  `valid` false: no query in
+// this row (out = kNoEntry).  Must be called with the whole wave active.
+__device__ void score_row4(const ProjProblem& pb, const ProjParams& P, const QueryReg& QR, bool valid,
+                           const SortedGrid& G, const int* sfmp, unsigned out[4]) {
+    const int r = threadIdx.x & 15;
+    const ProjQuery& Q = QR.q;
+    unsigned k[4] = {kNoEntry, kNoEntry, kNoEntry, kNoEntry};
+    if (valid) {
+        const CellRange cr = cell_range(pb, Q.u, Q.v, Q.r);
+        if (!cr.empty) {
+            const unsigned long long q0 = (unsigned long long)QR.d0.y << 32 | QR.d0.x;
+            const unsigned long long q1 = (unsigned long long)QR.d0.w << 32 | QR.d0.z;
+            const unsigned long long q2 = (unsigned long long)QR.d1.y << 32 | QR.d1.x;
+            const unsigned long long q3 = (unsigned long long)QR.d1.w << 32 | QR.d1.z;
+            const bool check_levels = (Q.min_level > 0) || (Q.max_level >= 0);
+            const int ncol = cr.x1 - cr.x0 + 1;
+            // 4, 2 or 1 lanes per column (ncol <= 4, <= 8, more): shifts, no division
+            const int sh = ncol <= 4 ? 2 : (ncol <= 8 ? 1 : 0);
+            const int lpc = 1 << sh, c0 = r >> sh, sub = r & (lpc - 1);
+            for (int c = c0; c < ncol; c += 16) {
+                const int cc = (cr.x0 + c) * kGridRows;
+                const int beg = G.cstart[cc + cr.y0], end = G.cstart[cc + cr.y1 + 1];
+                for (int p = beg + sub; p < end; p += lpc) {
+                    const float4 kp = G.skp[p];
+                    const int oct = __float_as_int(kp.z);
+                    if (check_levels) {
+                        if (oct < Q.min_level) continue;
+                        if (Q.max_level >= 0 && oct > Q.max_level) continue;
+                    }
+                    const float distx = kp.x - Q.u;
+                    const float disty = kp.y - Q.v;
+                    if (!(fabsf(distx) < Q.r && fabsf(disty) < Q.r)) continue;
+                    if (Q.post_min >= 0 && (oct < Q.post_min || oct > Q.post_max)) continue;
+                    if (kp_blocked(sfmp[p], P)) continue;
+                    int d;
+                    if (G.sdesc) {
+                        if (Q.er_max >= 0.f && pb.u_right) {
+                            const float ur = pb.u_right[G.skey[p] & 0x1fffu];
+                            if (ur > 0 && fabsf(Q.ur - ur) > Q.er_max) continue;
+                        }
+                        const uint4 a = G.sdesc[2 * p], b = G.sdesc[2 * p + 1];
+                        d = __popcll(q0 ^ ((unsigned long long)a.y << 32 | a.x)) +
+                            __popcll(q1 ^ ((unsigned long long)a.w << 32 | a.z)) +
+                            __popcll(q2 ^ ((unsigned long long)b.y << 32 | b.x)) +
+                            __popcll(q3 ^ ((unsigned long long)b.w << 32 | b.z));
+                    } else {
+                        const int i = (int)(G.skey[p] & 0x1fffu);
+                        if (Q.er_max >= 0.f && pb.u_right) {
+                            const float ur = pb.u_right[i];
+                            if (ur > 0 && fabsf(Q.ur - ur) > Q.er_max) continue;
+                        }
+                        const unsigned long long* tt = (const unsigned long long*)(pb.desc + (size_t)i * 32);
+                        d = __popcll(q0 ^ tt[0]) + __popcll(q1 ^ tt[1]) + __popcll(q2 ^ tt[2]) + __popcll(q3 ^ tt[3]);
+                    }
+                    const unsigned key = ((unsigned)d << 13) | (unsigned)p;
+                    if (key < k[3]) {
+                        if (key < k[2]) {
+                            k[3] = k[2];
+                            if (key < k[1]) {
+                                k[2] = k[1];
+                                if (key < k[0]) { k[1] = k[0]; k[0] = key; }
+                                else k[1] = key;
+                            } else k[2] = key;
+                        } else k[3] = key;
+                    }
                 }
-                const float distx = G.sx[p] - Q.u;
-                const float disty = G.sy[p] - Q.v;
-                if (!(fabsf(distx) < Q.r && fabsf(disty) < Q.r)) continue;
-                if (Q.post_min >= 0 && (oct < Q.post_min || oct > Q.post_max)) continue;
-                const int i = (int)(G.skey[p] & 0x1fffu);
-                if (kp_blocked(fmp[i], P)) continue;
-                if (Q.er_max >= 0.f && pb.u_right && pb.u_right[i] > 0) {
-                    const float er = fabsf(Q.ur - pb.u_right[i]);
-                    if (er > Q.er_max) continue;
-                }
-                const unsigned long long* t = (const unsigned long long*)(pb.desc + (size_t)i * 32);
-                const int d = __popcll(q0 ^ t[0]) + __popcll(q1 ^ t[1]) + __popcll(q2 ^ t[2]) + __popcll(q3 ^ t[3]);
-                const unsigned key = ((unsigned)d << 13) | (unsigned)p;
-                if (key < k1) { k2 = k1; k1 = key; }
-                else if (key < k2) { k2 = key; }
             }
         }
     }
+    // Row top-4: keys are unique (distinct positions), so one lane pops each minimum.
+    unsigned m[4];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned o1 = __shfl_xor(k1, o), o2 = __shfl_xor(k2, o);
-        const unsigned hi = k1 < o1 ? o1 : k1;
-        const unsigned lo2 = k2 < o2 ? k2 : o2;
-        k1 = k1 < o1 ? k1 : o1;
-        k2 = hi < lo2 ? hi : lo2;
+    for (int j = 0; j < 4; j++) {
+        m[j] = row_min_u32(k[0]);
+        if (k[0] == m[j] && m[j] != kNoEntry) {
+            k[0] = k[1];
+            k[1] = k[2];
+            k[2] = k[3];
+            k[3] = kNoEntry;
+        }
     }
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        out[j] = m[j] == kNoEntry ? kNoEntry
+                                  : ((m[j] >> 13) << 18) | ((unsigned)__float_as_int(G.skp[m[j] & 0x1fffu].z) << 13) |
+                                        (m[j] & 0x1fffu);
 }
 
-__device__ __forceinline__ int key_dist(unsigned k) { return (int)(k >> 13); }
-__device__ __forceinline__ int key_pos(unsigned k) { return (int)(k & 0x1fffu); }
-
-// Ascending in-place bitonic sort of n2 (power of two) u32 keys by a 256-thread block.
+// Ascending in-place bitonic sort of n2 (power of two) u32 keys by the workgroup.
 __device__ void block_bitonic_sort(unsigned* a, int n2) {
     for (int k = 2; k <= n2; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < n2; i += 256) {
+            for (int i = threadIdx.x; i < n2; i += kProjThreads) {
                 const int l = i ^ j;
                 if (l > i) {
                     const unsigned x = a[i], y = a[l];
@@ -226,139 +321,239 @@ __device__ void block_bitonic_sort(unsigned* a, int n2) {
     }
 }
 
-// One workgroup per problem (one SearchByProjection call).  The frame's keypoints are
-// sorted into grid order in LDS; waves score the queries in parallel against the
-// keypoints' initial mvpMapPoints state; wave 0 then replays the reference's
-// sequential loop: each query claims its best keypoint in order, and a query whose
-// best (or, with the ratio test, second) keypoint was claimed by an earlier query is
-// re-scored against the current state.  Finally the rotation histogram
-// (ORBmatcher.cc:1750-1786) un-matches bins outside the three maxima.
-// QLDS: per-query state in LDS (the serial replay then touches no global memory);
-// otherwise in the problem's global scratch (3 x u64 per query).
-template <bool QLDS>
-__global__ __launch_bounds__(256) void k_proj_search(const ProjProblem* __restrict__ probs, ProjParams P,
-                                                     unsigned long long* __restrict__ scratch,
-                                                     const long long* __restrict__ scratch_off) {
+__host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// LDS layout of k_proj_search (byte offsets), shared by the kernel and its launcher.
+struct ProjLds {
+    size_t skey, cstart, skp, sfmp, owner, sdesc, qk, qmp, qang, mlist, mbin, total;
+    __host__ __device__ ProjLds(int n, int n2, int nq, bool dlds, bool qlds) {
+        skey = 0;
+        cstart = align16((size_t)n2 * 4);
+        skp = align16(cstart + (size_t)(kNumCells + 1) * 4);
+        sfmp = skp + (size_t)n * 16;
+        owner = sfmp + (size_t)n * 4;
+        size_t o = align16(owner + (size_t)n * 4);
+        sdesc = o;
+        if (dlds) o += (size_t)n * 32;
+        qk = o;
+        qmp = qk + (size_t)nq * 16;
+        qang = qmp + (size_t)nq * 4;
+        mlist = qang + (size_t)nq * 4;
+        mbin = mlist + (size_t)nq * 4;
+        total = qlds ? mbin + (size_t)nq * 4 : o;
+    }
+};
+
+// One workgroup per problem (one SearchByProjection call).
+//  1. the frame's keypoints are sorted into grid order in LDS (with their descriptors
+//     when DLDS);
+//  2. all waves score the queries against the initial mvpMapPoints state, keeping each
+//     query's four best candidates;
+//  3. wave 0 replays the reference's sequential loop 64 queries at a time: every query
+//     takes the first candidates of its list that are still unclaimed; the queries of
+//     a chunk whose choice no earlier query of the chunk touches commit together, the
+//     first one that is touched resumes the replay after the others have committed, and
+//     a query whose list ran out is re-scored against the current claims;
+//  4. the rotation histogram (ORBmatcher.cc:1750-1786) un-matches bins outside the
+//     three maxima.
+// Claims only ever block more keypoints during the replay (a blocked keypoint is never
+// claimed again), so the first unblocked entries of a query's initial list are exactly
+// its best / second best against the current state while the list has them.
+// QLDS: per-query state in LDS; otherwise in the problem's global scratch.
+template <bool QLDS, bool DLDS>
+__global__ __launch_bounds__(kProjThreads) void k_proj_search(const ProjProblem* __restrict__ probs, ProjParams P,
+                                                              unsigned long long* __restrict__ scratch,
+                                                              const long long* __restrict__ scratch_off) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_hist[kHistoLength];
     const ProjProblem pb = probs[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int kWaves = kProjThreads / 64;
     const int n = pb.n, nq = pb.nq;
+    unsigned long long* st = P.stamps ? P.stamps + 8 * blockIdx.x : nullptr;
+    if (st && tid == 0) st[0] = wall_clock64();
     int n2 = 1;
     while (n2 < n) n2 <<= 1;
-    unsigned* skey = (unsigned*)smem;
-    int* cstart = (int*)(skey + n2);
-    float* sx = (float*)(cstart + kNumCells + 1);
-    float* sy = sx + n;
-    int* soct = (int*)(sy + n);
-    int* fmp = soct + n;
-    float* kang = (float*)(fmp + n);
-    unsigned* qk;
-    int *mlist, *mbin, *qmp;
+    const ProjLds L(n, n2, nq, DLDS, QLDS);
+    unsigned* skey = (unsigned*)(smem + L.skey);
+    int* cstart = (int*)(smem + L.cstart);
+    float4* skp = (float4*)(smem + L.skp);
+    int* sfmp = (int*)(smem + L.sfmp);
+    int* owner = (int*)(smem + L.owner);
+    uint4* sdesc = DLDS ? (uint4*)(smem + L.sdesc) : nullptr;
+    uint4* qk;
+    int *qmp, *mlist, *mbin;
     float* qang;
     if (QLDS) {
-        qk = (unsigned*)(kang + n);
-        mlist = (int*)(qk + 2 * nq);
+        qk = (uint4*)(smem + L.qk);
+        qmp = (int*)(smem + L.qmp);
+        qang = (float*)(smem + L.qang);
+        mlist = (int*)(smem + L.mlist);
+        mbin = (int*)(smem + L.mbin);
     } else {
         unsigned long long* g = scratch + scratch_off[blockIdx.x];
-        qk = (unsigned*)g;
-        mlist = (int*)(g + nq);
+        qk = (uint4*)g;
+        qmp = (int*)(g + 2 * (size_t)nq);
+        qang = (float*)(qmp + nq);
+        mlist = (int*)(qang + nq);
+        mbin = mlist + nq;
     }
-    mbin = mlist + nq;
-    qmp = mbin + nq;
-    qang = (float*)(qmp + nq);
-    for (int i = tid; i < n2; i += 256) {
+    for (int i = tid; i < n2; i += kProjThreads) {
         unsigned key = 0xffffffffu;
         if (i < n) {
-            const orbx_keypoint kp = pb.keys[i];
+            const orbx_keypoint& kp = pb.keys[i];
             const int px = (int)roundf((kp.x - pb.min_x) * pb.inv_w);  // Frame::PosInGrid, Frame.cc:558-567
             const int py = (int)roundf((kp.y - pb.min_y) * pb.inv_h);
             const int cell = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? kNoCell : px * kGridRows + py;
             key = ((unsigned)cell << 13) | (unsigned)i;
-            fmp[i] = pb.frame_mp[i];
-            kang[i] = kp.angle;
         }
         skey[i] = key;
     }
     if (tid < kHistoLength) s_hist[tid] = 0;
     __syncthreads();
     block_bitonic_sort(skey, n2);
-    for (int p = tid; p < n; p += 256) {
-        const orbx_keypoint kp = pb.keys[skey[p] & 0x1fffu];
-        sx[p] = kp.x;
-        sy[p] = kp.y;
-        soct[p] = kp.octave;
+    for (int p = tid; p < n; p += kProjThreads) {
+        const int i = (int)(skey[p] & 0x1fffu);
+        const orbx_keypoint& kp = pb.keys[i];
+        skp[p] = make_float4(kp.x, kp.y, __int_as_float(kp.octave), kp.angle);
+        sfmp[p] = pb.frame_mp[i];
+        owner[p] = 0x7fffffff;
     }
-    for (int c = tid; c <= kNumCells; c += 256) {  // lower_bound of (c << 13)
-        const unsigned target = (unsigned)c << 13;
-        int lo = 0, hi = n;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (skey[mid] < target) lo = mid + 1;
-            else hi = mid;
+    if (DLDS) {
+        for (int t = tid; t < 2 * n; t += kProjThreads) {
+            const int i = (int)(skey[t >> 1] & 0x1fffu);
+            sdesc[t] = ((const uint4*)(pb.desc + (size_t)i * 32))[t & 1];
         }
-        cstart[c] = lo;
     }
-    __syncthreads();
-    SortedGrid G{skey, cstart, sx, sy, soct};
-    for (int q = wave; q < nq; q += 4) {
-        const ProjQuery Q = pb.q[q];
-        unsigned k1 = kNoKey32, k2 = kNoKey32;
-        if (Q.mp >= 0) {
-            const unsigned long long* qd = (const unsigned long long*)(pb.qdesc + (size_t)q * 32);
-            score_query(pb, P, Q, G, qd[0], qd[1], qd[2], qd[3], fmp, k1, k2);
-        }
-        if (lane == 0) {
-            qk[2 * q] = k1;
-            qk[2 * q + 1] = k2;
-            qmp[q] = Q.mp;
-            qang[q] = Q.angle;
-        }
+    // cstart[c] = first sorted position whose cell >= c (each cell written once)
+    for (int p = tid; p <= n; p += kProjThreads) {
+        const int prev = p == 0 ? -1 : (int)(skey[p - 1] >> 13);
+        const int cur = p == n ? kNumCells : (int)(skey[p] >> 13);
+        const int hi = cur < kNumCells ? cur : kNumCells;
+        for (int c = prev + 1; c <= hi; c++) cstart[c] = p;
     }
     __syncthreads();
+    if (st && tid == 0) st[1] = wall_clock64();
+    const SortedGrid G{skey, cstart, skp, sdesc};
+    {
+        constexpr int kStep = kWaves * 4;
+        int qb = wave * 4;
+        QueryReg cur;
+        if (qb < nq) cur = load_query(pb, min(qb + (lane >> 4), nq - 1));
+        for (; qb < nq; qb += kStep) {
+            const int q = qb + (lane >> 4);
+            QueryReg nxt;
+            if (qb + kStep < nq) nxt = load_query(pb, min(q + kStep, nq - 1));  // prefetch
+            const int mp = q < nq ? cur.q.mp : -1;
+            unsigned e[4];
+            score_row4(pb, P, cur, mp >= 0, G, sfmp, e);
+            if ((lane & 15) == 0 && q < nq) {
+                qk[q] = make_uint4(e[0], e[1], e[2], e[3]);
+                qmp[q] = mp;
+                qang[q] = cur.q.angle;
+            }
+            cur = nxt;
+        }
+    }
+    __syncthreads();
+    if (st && tid == 0) st[2] = wall_clock64();
     if (wave == 0) {
-        int nmatch = 0, nrec = 0;
+        int nmatch = 0, nrec = 0, nrescore = 0, niter = 0;
         const float factor = kHistoLength / 360.0f;
-        for (int q = 0; q < nq; q++) {
-            const int mp = qmp[q];
-            if (mp < 0) continue;
-            unsigned k1 = qk[2 * q], k2 = qk[2 * q + 1];
-            const bool stale =
-                (k1 != kNoKey32 && kp_blocked(fmp[skey[key_pos(k1)] & 0x1fffu], P)) ||
-                (P.ratio_mode && k2 != kNoKey32 && kp_blocked(fmp[skey[key_pos(k2)] & 0x1fffu], P));
-            if (stale) {
-                const ProjQuery Q = pb.q[q];
-                const unsigned long long* qd = (const unsigned long long*)(pb.qdesc + (size_t)q * 32);
-                score_query(pb, P, Q, G, qd[0], qd[1], qd[2], qd[3], fmp, k1, k2);
+        const int need = P.ratio_mode ? 2 : 1;
+        const unsigned long long below = (1ull << lane) - 1;
+        for (int base = 0; base < nq; base += 64) {
+            const int q = base + lane;
+            int mp = -1;
+            float qa = 0.f;
+            unsigned e[4] = {kNoEntry, kNoEntry, kNoEntry, kNoEntry};
+            QueryReg mine;  // consumed only by a re-scoring (loads overlap the first round)
+            if (q < nq) mine = load_query(pb, q);
+            if (q < nq) {
+                mp = qmp[q];
+                const uint4 v = qk[q];
+                e[0] = v.x; e[1] = v.y; e[2] = v.z; e[3] = v.w;
+                qa = qang[q];
             }
-            if (k1 == kNoKey32) continue;
-            const int bestDist = key_dist(k1);
-            if (bestDist > P.accept_th) continue;
-            const int idx1 = (int)(skey[key_pos(k1)] & 0x1fffu);
-            if (P.ratio_mode) {
-                const int bestLevel = soct[key_pos(k1)];
-                const int bestLevel2 = k2 == kNoKey32 ? -1 : soct[key_pos(k2)];
-                const int bestDist2 = k2 == kNoKey32 ? 256 : key_dist(k2);
-                if (bestLevel == bestLevel2 && (float)bestDist > P.nnratio * (float)bestDist2) continue;
-            }
-            if (lane == 0) fmp[idx1] = mp;
-            nmatch++;
-            if (P.check_ori) {
-                float rot = qang[q] - kang[idx1];
-                if (rot < 0.0f) rot += 360.0f;
-                int bin = (int)roundf(rot * factor);
-                if (bin == kHistoLength) bin = 0;
-                if (lane == 0) {
-                    mlist[nrec] = idx1;
-                    mbin[nrec] = bin;
-                    s_hist[bin]++;
+            int start = 0;
+            while (true) {
+                niter++;
+                const bool act = lane >= start && mp >= 0;
+                unsigned c1 = kNoEntry, c2 = kNoEntry;
+                bool exhausted = false;
+                if (act) {
+                    int found = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        if (e[j] != kNoEntry && found < 2 && !kp_blocked(sfmp[ent_pos(e[j])], P)) {
+                            if (found == 0) c1 = e[j];
+                            else c2 = e[j];
+                            found++;
+                        }
+                    }
+                    exhausted = e[3] != kNoEntry && found < need;
                 }
-                nrec++;
+                bool acc = false;
+                if (act && !exhausted && c1 != kNoEntry && ent_dist(c1) <= P.accept_th) {
+                    acc = true;
+                    if (P.ratio_mode) {
+                        const int bestLevel2 = c2 == kNoEntry ? -1 : ent_oct(c2);
+                        const int bestDist2 = c2 == kNoEntry ? 256 : ent_dist(c2);
+                        if (ent_oct(c1) == bestLevel2 && (float)ent_dist(c1) > P.nnratio * (float)bestDist2)
+                            acc = false;
+                    }
+                }
+                const int tpos = acc ? ent_pos(c1) : -1;
+                // A query depends on an earlier one of the chunk if that one claims its best
+                // (or, with the ratio test, second best) keypoint.
+                // owner[p] = lowest lane of this round claiming p (LDS ops of a wave are
+                // executed in order: all atomics, then all reads, then the reset).
+                if (acc) atomicMin(&owner[tpos], lane);
+                bool conf = exhausted;
+                if (act && !exhausted) {
+                    if (c1 != kNoEntry && owner[ent_pos(c1)] < lane) conf = true;
+                    if (P.ratio_mode && c2 != kNoEntry && owner[ent_pos(c2)] < lane) conf = true;
+                }
+                if (acc) owner[tpos] = 0x7fffffff;
+                const unsigned long long cm = __ballot(conf);
+                const int f = cm ? __ffsll((long long)cm) - 1 : 64;
+                const bool com = acc && lane < f;
+                const unsigned long long comm = __ballot(com);
+                if (com) sfmp[tpos] = mp;
+                nmatch += __popcll(comm);
+                if (P.check_ori) {
+                    if (com) {
+                        float rot = qa - skp[tpos].w;
+                        if (rot < 0.0f) rot += 360.0f;
+                        int bin = (int)roundf(rot * factor);
+                        if (bin == kHistoLength) bin = 0;
+                        const int r = nrec + __popcll(comm & below);
+                        mlist[r] = tpos;
+                        mbin[r] = bin;
+                        atomicAdd(&s_hist[bin], 1);
+                    }
+                    nrec += __popcll(comm);
+                }
+                if (f >= 64) break;
+                if (__builtin_amdgcn_readlane((int)exhausted, f)) {
+                    nrescore++;
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                    __builtin_amdgcn_wave_barrier();
+                    unsigned ne[4];
+                    score_row4(pb, P, bcast_query(mine, f), lane < 16, G, sfmp, ne);
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const unsigned v = (unsigned)__builtin_amdgcn_readlane((int)ne[j], 0);
+                        if (lane == f) e[j] = v;
+                    }
+                }
+                start = f;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                __builtin_amdgcn_wave_barrier();
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
             __builtin_amdgcn_wave_barrier();
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         if (P.check_ori) {
             // ComputeThreeMaxima, ORBmatcher.cc:1935-1977
             int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
@@ -381,7 +576,7 @@ __global__ __launch_bounds__(256) void k_proj_search(const ProjProblem* __restri
             for (int m = lane; m < nrec; m += 64) {
                 const int b = mbin[m];
                 if (b != ind1 && b != ind2 && b != ind3) {
-                    fmp[mlist[m]] = -1;
+                    sfmp[mlist[m]] = -1;
                     bad++;
                 }
             }
@@ -390,9 +585,16 @@ __global__ __launch_bounds__(256) void k_proj_search(const ProjProblem* __restri
             nmatch -= bad;
         }
         if (lane == 0) *pb.nmatches = nmatch;
+        if (st && tid == 0) {
+            st[3] = wall_clock64();
+            st[5] = nrescore;
+            st[6] = nq;
+            st[7] = niter;
+        }
     }
     __syncthreads();
-    for (int i = tid; i < n; i += 256) pb.frame_mp[i] = fmp[i];
+    for (int p = tid; p < n; p += kProjThreads) pb.frame_mp[skey[p] & 0x1fffu] = sfmp[p];
+    if (st && tid == 0) st[4] = wall_clock64();
 }
 
 // Batched TrackWithMotionModel matching over a device-resident sequence: problem p
@@ -422,7 +624,7 @@ __global__ __launch_bounds__(256) void k_seq_build(SeqArgs A, ProjQuery* __restr
         pb.inv_h = (float)kGridRows / (A.max_y - A.min_y);
         pb.nmatches = A.nmatches + p + 1;
         probs[p] = pb;
-        scratch_off[p] = (long long)p * 3 * A.cap;
+        scratch_off[p] = (long long)p * kProjScratchWords * A.cap;
     }
     if (i >= A.cap) return;
     ProjQuery q{};
@@ -473,25 +675,28 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
                               const long long* d_scratch_off, int max_n, int max_nq, hipStream_t stream) {
     if (nprob <= 0) return hipSuccess;
     if (max_n >= 8192) return hipErrorInvalidValue;  // 13-bit keypoint positions
-    size_t n2 = 1;
-    while (n2 < (size_t)max_n) n2 <<= 1;
-    const size_t base = n2 * 4 + (size_t)(kNumCells + 1) * 4 + (size_t)max_n * 20;
-    const size_t with_q = base + (size_t)max_nq * 24;
-    const size_t limit = 160 * 1024;
-    if (base > limit) return hipErrorInvalidValue;
-    const bool qlds = with_q <= limit;
-    const size_t lds = qlds ? with_q : base;
-    const void* fn = qlds ? (const void*)k_proj_search<true> : (const void*)k_proj_search<false>;
+    int n2 = 1;
+    while (n2 < max_n) n2 <<= 1;
+    const size_t limit = 160 * 1024 - 256;  // minus the static histogram
+    // Prefer LDS-resident descriptors (the scoring loads), then LDS-resident query state.
+    bool dlds = true, qlds = true;
+    if (ProjLds(max_n, n2, max_nq, true, true).total > limit) {
+        qlds = false;
+        if (ProjLds(max_n, n2, max_nq, true, false).total > limit) {
+            dlds = false;
+            qlds = ProjLds(max_n, n2, max_nq, false, true).total <= limit;
+        }
+    }
+    const size_t lds = ProjLds(max_n, n2, max_nq, dlds, qlds).total;
+    if (lds > limit) return hipErrorInvalidValue;
+    const void* fn = qlds ? (dlds ? (const void*)k_proj_search<true, true> : (const void*)k_proj_search<true, false>)
+                          : (dlds ? (const void*)k_proj_search<false, true> : (const void*)k_proj_search<false, false>);
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    if (qlds)
-        hipLaunchKernelGGL(k_proj_search<true>, dim3(nprob), dim3(256), lds, stream, d_probs, P, scratch, d_scratch_off);
-    else
-        hipLaunchKernelGGL(k_proj_search<false>, dim3(nprob), dim3(256), lds, stream, d_probs, P, scratch,
-                           d_scratch_off);
-    return hipGetLastError();
+    void* args[] = {(void*)&d_probs, (void*)&P, (void*)&scratch, (void*)&d_scratch_off};
+    return hipLaunchKernel(fn, dim3(nprob), dim3(kProjThreads), args, lds, stream);
 }
 
 // ------------------------------------------------------------------ triangulation

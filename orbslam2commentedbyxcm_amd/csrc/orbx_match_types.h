@@ -25,7 +25,7 @@ struct ProjQuery {
     int post_min, post_max;    // extra candidate level filter [post_min, post_max] (-1 = none)
     int mp;               // MapPoint id written to mvpMapPoints on a match; < 0 = skip query
     float angle;          // keypoint angle of the query (rotation histogram)
-    int pad[2];
+    int pad;              // 48-byte record
 };
 
 struct ProjProblem {
@@ -41,6 +41,9 @@ struct ProjProblem {
     int32_t* nmatches;          // out
 };
 
+// Global scratch per query (u64 words) when the per-query state does not fit in LDS.
+constexpr int kProjScratchWords = 4;
+
 // Call-level semantics of the SearchByProjection overload being executed.
 struct ProjParams {
     const int32_t* mp_obs;  // Observations() per MapPoint id (blocked_mode 0)
@@ -50,6 +53,7 @@ struct ProjParams {
     int ratio_mode;         // 1: reject if bestLevel==bestLevel2 && best > nnratio*second (a11)
     float nnratio;
     int check_ori;          // rotation-consistency histogram (a12, a13)
+    unsigned long long* stamps;  // optional: per-problem wall_clock64 phase stamps (diagnostics)
 };
 
 // Batched frame-to-frame matching over an extracted device sequence.

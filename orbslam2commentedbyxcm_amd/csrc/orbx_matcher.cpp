@@ -5,6 +5,8 @@
 // hands the dense part -- candidate windows, Hamming scoring, the ordered commit --
 // to one kernel launch on the matcher's stream.  MapPoint* pointers are represented
 // by integer ids; mvpMapPoints arrays hold ids (-1 = NULL).
+#include <cstdio>
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -102,7 +104,7 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
     const int nobs = mps->n;
     size_t need = pad(sizeof(orbx_keypoint) * n) + pad((size_t)n * 32) + pad(sizeof(float) * n) +
                   pad(sizeof(int32_t) * n) + pad(sizeof(ProjQuery) * nq) + pad((size_t)nq * 32) +
-                  pad(sizeof(int32_t) * (nobs ? nobs : 1)) + pad(sizeof(ProjProblem)) + pad(24 * (size_t)nq) +
+                  pad(sizeof(int32_t) * (nobs ? nobs : 1)) + pad(sizeof(ProjProblem)) + pad(8 * kProjScratchWords * (size_t)nq) +
                   pad(sizeof(long long)) + pad(sizeof(int32_t));
     HIP_TRY(m->arena.reserve(need));
     m->arena.used = 0;
@@ -114,7 +116,7 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
     auto* d_qd = m->arena.take<uint8_t>((size_t)nq * 32);
     auto* d_obs = m->arena.take<int32_t>(nobs ? nobs : 1);
     auto* d_prob = m->arena.take<ProjProblem>(1);
-    auto* d_scr = m->arena.take<unsigned long long>(3 * (size_t)nq);
+    auto* d_scr = m->arena.take<unsigned long long>(kProjScratchWords * (size_t)nq);
     auto* d_off = m->arena.take<long long>(1);
     auto* d_nm = m->arena.take<int32_t>(1);
     hipStream_t s = m->stream;
@@ -306,7 +308,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     const size_t need = pad(sizeof(ProjQuery) * (size_t)(npairs > 0 ? npairs : 1) * cap) +
                         pad(sizeof(ProjProblem) * (size_t)(npairs > 0 ? npairs : 1)) +
                         pad(sizeof(long long) * (size_t)(npairs > 0 ? npairs : 1)) +
-                        pad(sizeof(unsigned long long) * 3 * (size_t)(npairs > 0 ? npairs : 1) * cap);
+                        pad(sizeof(unsigned long long) * kProjScratchWords * (size_t)(npairs > 0 ? npairs : 1) * cap);
     if (m->arena.cap < need) {
         HIP_TRY(hipStreamSynchronize(s));
         HIP_TRY(m->arena.reserve(need));
@@ -315,7 +317,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     auto* d_q = m->arena.take<ProjQuery>((size_t)(npairs > 0 ? npairs : 1) * cap);
     auto* d_prob = m->arena.take<ProjProblem>(npairs > 0 ? npairs : 1);
     auto* d_off = m->arena.take<long long>(npairs > 0 ? npairs : 1);
-    auto* d_scr = m->arena.take<unsigned long long>(3 * (size_t)(npairs > 0 ? npairs : 1) * cap);
+    auto* d_scr = m->arena.take<unsigned long long>(kProjScratchWords * (size_t)(npairs > 0 ? npairs : 1) * cap);
     HIP_TRY(hipMemsetAsync(d_cur_mp, 0xff, sizeof(int32_t) * (size_t)batch * cap, s));
     HIP_TRY(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * (size_t)batch, s));
     if (npairs == 0) return ORBX_OK;
@@ -351,10 +353,44 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     P.accept_th = TH_HIGH;
     P.ratio_mode = 0;
     P.check_ori = m->check_ori;
+    // ORBX_MATCH_STAMPS=1: per-phase wall-clock breakdown of the search kernel to stderr
+    // (diagnostics only; synchronises the stream).
+    static const bool stamps = getenv("ORBX_MATCH_STAMPS") != nullptr;
+    unsigned long long* d_st = nullptr;
+    if (stamps) {
+        HIP_TRY(hipMalloc(&d_st, sizeof(unsigned long long) * 8 * npairs));
+        P.stamps = d_st;
+    }
     HIP_TRY(launch_proj_search(d_prob, npairs, P, d_scr, d_off, cap, cap, s));
     if (m->timing) {
         HIP_TRY(hipEventRecord(m->ev[1], s));
         m->have_time = true;
+    }
+    if (stamps) {
+        std::vector<unsigned long long> h((size_t)8 * npairs);
+        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(hipMemcpy(h.data(), d_st, h.size() * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipFree(d_st));
+        double ph[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0}, resc = 0, nq = 0, nit = 0;
+        unsigned long long t0 = ~0ull, t1 = 0;
+        for (int p = 0; p < npairs; p++) {
+            const unsigned long long* r = &h[(size_t)8 * p];
+            for (int k = 0; k < 4; k++) {
+                const double d = (double)(r[k + 1] - r[k]) * 0.01;  // 100 MHz -> us
+                ph[k] += d;
+                if (d > mx[k]) mx[k] = d;
+            }
+            resc += (double)r[5];
+            nq += (double)r[6];
+            nit += (double)r[7];
+            if (r[0] < t0) t0 = r[0];
+            if (r[4] > t1) t1 = r[4];
+        }
+        fprintf(stderr,
+                "[orbx stamps] pairs=%d span=%.1fus | mean/max us: sort %.1f/%.1f score %.1f/%.1f commit %.1f/%.1f "
+                "store %.1f/%.1f | rescored %.1f of %.1f queries, %.1f replay rounds\n",
+                npairs, (double)(t1 - t0) * 0.01, ph[0] / npairs, mx[0], ph[1] / npairs, mx[1], ph[2] / npairs, mx[2],
+                ph[3] / npairs, mx[3], resc / npairs, nq / npairs, nit / npairs);
     }
     return ORBX_OK;
 }
