@@ -207,6 +207,10 @@ def main():
     for _ in range(args.warmup):
         step()
     sync()
+    # Per-stage HIP events on the extractor's stream, recorded inside the timed loop
+    # (a ring of event sets; read back after the loop, no synchronisation inside it).
+    ex.set_timing(True)
+    matcher.set_timing(True)
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -227,22 +231,11 @@ def main():
     mean_kps = float(n_host.mean())
     mean_matches = float(d_nm.cpu().numpy()[1:].mean()) if match else 0.0
 
-    # per-stage HIP-event timing on the extractor's stream (separate, untimed pass)
-    ex.set_timing(True)
-    matcher.set_timing(True)
-    reps = 5
-    acc = {}
-    for _ in range(reps):
-        step()
-        st = ex.stage_times()
-        if match:
-            st["match"] = matcher.last_ms()
-        for k, v in st.items():
-            acc[k] = acc.get(k, 0.0) + v
-    sync()
+    stage_ms = ex.stage_times()
+    if match:
+        stage_ms["match"] = matcher.last_ms()
     ex.set_timing(False)
     matcher.set_timing(False)
-    stage_ms = {k: v / reps for k, v in acc.items()}
     bytes_pf = stage_bytes(W, H, mean_kps)
     kernels = {k: v for k, v in stage_ms.items() if k != "total"}
     dom = max(kernels, key=kernels.get)

@@ -107,8 +107,10 @@ int orbx_extract_batch_device(orbx_extractor* ex, int batch, const uint8_t* d_im
 /* The extractor's hipStream_t (as void*). */
 void* orbx_extractor_stream(orbx_extractor* ex);
 
-/* Per-stage timing of the last orbx_extract_batch_device call (requires
- * orbx_extractor_set_timing(ex, 1) beforehand).  Names are static strings. */
+/* Per-stage HIP-event timing (ms) of extraction calls, averaged over the (up to 64)
+ * most recent calls made since orbx_extractor_set_timing(ex, 1), which also resets the
+ * average.  Events are recorded on the launch stream between the stages, so a timed
+ * loop is measured without synchronising inside it.  Names are static strings. */
 int orbx_extractor_set_timing(orbx_extractor* ex, int enable);
 int orbx_extractor_stage_times(orbx_extractor* ex, int max_stages, const char** names, float* ms,
                                int* n_stages);
@@ -220,7 +222,8 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
                                const float* scale_factors, int nlevels, float depth, float th,
                                int32_t* d_cur_mp, int32_t* d_nmatches, void* stream);
 
-/* HIP-event timing of orbx_match_sequence_device (milliseconds of the last call). */
+/* HIP-event timing of orbx_match_sequence_device: milliseconds averaged over the (up
+ * to 64) most recent calls since orbx_matcher_set_timing(m, 1). */
 int orbx_matcher_set_timing(orbx_matcher* m, int enable);
 int orbx_matcher_last_ms(orbx_matcher* m, float* ms);
 

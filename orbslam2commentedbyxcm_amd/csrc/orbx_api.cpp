@@ -59,10 +59,12 @@ struct orbx_extractor {
     hipStream_t stream = nullptr;
     Plan plan;
     DeviceBuffers db;
+    // Stage timing: a ring of event sets, one per timed call, so a whole timed loop is
+    // measured without synchronising inside it; stage_times averages the ring.
+    static constexpr int kRing = 64;
     bool timing = false;
-    hipEvent_t ev[kStages + 1] = {};
-    float stage_ms[kStages] = {};
-    bool have_times = false;
+    hipEvent_t ev[kRing][kStages + 1] = {};
+    long long ncalls = 0;
     // host-API staging
     uint8_t* d_in = nullptr;
     size_t d_in_bytes = 0;
@@ -139,14 +141,15 @@ int run_device(orbx_extractor* ex, int batch, const uint8_t* d_imgs, size_t fram
     if (rc != ORBX_OK) return rc;
     hipEvent_t* ev = nullptr;
     if (ex->timing) {
+        hipEvent_t* slot = ex->ev[ex->ncalls % orbx_extractor::kRing];
         for (int i = 0; i <= kStages; i++)
-            if (!ex->ev[i]) HIP_TRY(hipEventCreate(&ex->ev[i]));
-        ev = ex->ev;
+            if (!slot[i]) HIP_TRY(hipEventCreate(&slot[i]));
+        ev = slot;
     }
     hipError_t e = launch_extract(ex->plan, ex->db, batch, d_imgs, frame_pitch, stride, d_kps, d_desc, cap, d_n,
                                   stream, ev);
     if (e != hipSuccess) return hip_fail(e, "launch_extract");
-    ex->have_times = ex->timing;
+    if (ex->timing) ex->ncalls++;
     ex->last_batch = batch;
     ex->have_pyramid = true;
     return ORBX_OK;
@@ -232,8 +235,9 @@ void orbx_extractor_destroy(orbx_extractor* ex) {
     if (ex->d_kps) (void)hipFree(ex->d_kps);
     if (ex->d_desc) (void)hipFree(ex->d_desc);
     if (ex->d_n) (void)hipFree(ex->d_n);
-    for (auto& e : ex->ev)
-        if (e) (void)hipEventDestroy(e);
+    for (auto& slot : ex->ev)
+        for (auto& e : slot)
+            if (e) (void)hipEventDestroy(e);
     if (ex->stream) (void)hipStreamDestroy(ex->stream);
     delete ex;
 }
@@ -269,22 +273,30 @@ void* orbx_extractor_stream(orbx_extractor* ex) { return ex ? (void*)ex->stream 
 int orbx_extractor_set_timing(orbx_extractor* ex, int enable) {
     if (!ex) return fail(ORBX_ERR_ARG, "null extractor");
     ex->timing = enable != 0;
+    ex->ncalls = 0;
     return ORBX_OK;
 }
 
 int orbx_extractor_stage_times(orbx_extractor* ex, int max_stages, const char** names, float* ms, int* n_stages) {
     if (!ex) return fail(ORBX_ERR_ARG, "null extractor");
-    if (!ex->have_times) return fail(ORBX_ERR_STATE, "no timed extraction yet");
-    HIP_TRY(hipEventSynchronize(ex->ev[kStages - 1]));
+    if (ex->ncalls == 0) return fail(ORBX_ERR_STATE, "no timed extraction yet");
+    const long long last = ex->ncalls - 1;
+    const int nslots = ex->ncalls < orbx_extractor::kRing ? (int)ex->ncalls : orbx_extractor::kRing;
+    HIP_TRY(hipEventSynchronize(ex->ev[last % orbx_extractor::kRing][kStages - 1]));
     int n = kStages < max_stages ? kStages : max_stages;
     for (int i = 0; i < n; i++) {
-        float t = 0.f;
-        if (i < kStages - 1)
-            HIP_TRY(hipEventElapsedTime(&t, ex->ev[i], ex->ev[i + 1]));
-        else
-            HIP_TRY(hipEventElapsedTime(&t, ex->ev[0], ex->ev[kStages - 1]));
+        double sum = 0.0;
+        for (int k = 0; k < nslots; k++) {
+            hipEvent_t* e = ex->ev[(last - k) % orbx_extractor::kRing];
+            float t = 0.f;
+            if (i < kStages - 1)
+                HIP_TRY(hipEventElapsedTime(&t, e[i], e[i + 1]));
+            else
+                HIP_TRY(hipEventElapsedTime(&t, e[0], e[kStages - 1]));
+            sum += t;
+        }
         if (names) names[i] = kStageNames[i];
-        if (ms) ms[i] = t;
+        if (ms) ms[i] = (float)(sum / nslots);
     }
     if (n_stages) *n_stages = n;
     return ORBX_OK;

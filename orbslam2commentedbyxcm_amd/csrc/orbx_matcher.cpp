@@ -84,9 +84,12 @@ struct orbx_matcher {
     int check_ori = 1;
     hipStream_t stream = nullptr;
     Arena arena;
+    // orbx_match_sequence_device timing: a ring of (start, end) events, one per timed
+    // call, averaged by orbx_matcher_last_ms.
+    static constexpr int kRing = 64;
     bool timing = false;
-    hipEvent_t ev[2] = {nullptr, nullptr};
-    bool have_time = false;
+    hipEvent_t ev[kRing][2] = {};
+    long long ncalls = 0;
 };
 
 namespace {
@@ -184,8 +187,9 @@ void orbx_matcher_destroy(orbx_matcher* m) {
     (void)hipSetDevice(m->device);
     if (m->stream) (void)hipStreamSynchronize(m->stream);
     if (m->arena.base) (void)hipFree(m->arena.base);
-    for (auto& e : m->ev)
-        if (e) (void)hipEventDestroy(e);
+    for (auto& slot : m->ev)
+        for (auto& e : slot)
+            if (e) (void)hipEventDestroy(e);
     if (m->stream) (void)hipStreamDestroy(m->stream);
     delete m;
 }
@@ -341,10 +345,11 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     for (int l = 0; l < nlevels; l++) A.scale[l] = scale_factors[l];
     A.cur_mp = d_cur_mp;
     A.nmatches = d_nmatches;
+    hipEvent_t* ev = m->ev[m->ncalls % orbx_matcher::kRing];
     if (m->timing) {
-        for (auto& e : m->ev)
-            if (!e) HIP_TRY(hipEventCreate(&e));
-        HIP_TRY(hipEventRecord(m->ev[0], s));
+        for (int i = 0; i < 2; i++)
+            if (!ev[i]) HIP_TRY(hipEventCreate(&ev[i]));
+        HIP_TRY(hipEventRecord(ev[0], s));
     }
     HIP_TRY(launch_seq_build(A, npairs, d_q, d_prob, d_off, s));
     ProjParams P{};
@@ -363,8 +368,8 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     }
     HIP_TRY(launch_proj_search(d_prob, npairs, P, d_scr, d_off, cap, cap, s));
     if (m->timing) {
-        HIP_TRY(hipEventRecord(m->ev[1], s));
-        m->have_time = true;
+        HIP_TRY(hipEventRecord(ev[1], s));
+        m->ncalls++;
     }
     if (stamps) {
         std::vector<unsigned long long> h((size_t)8 * npairs);
@@ -398,14 +403,24 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
 int orbx_matcher_set_timing(orbx_matcher* m, int enable) {
     if (!m) return fail(ORBX_ERR_ARG, "null matcher");
     m->timing = enable != 0;
+    m->ncalls = 0;
     return ORBX_OK;
 }
 
 int orbx_matcher_last_ms(orbx_matcher* m, float* ms) {
     if (!m || !ms) return fail(ORBX_ERR_ARG, "null argument");
-    if (!m->have_time) return fail(ORBX_ERR_STATE, "no timed call");
-    HIP_TRY(hipEventSynchronize(m->ev[1]));
-    HIP_TRY(hipEventElapsedTime(ms, m->ev[0], m->ev[1]));
+    if (m->ncalls == 0) return fail(ORBX_ERR_STATE, "no timed call");
+    const long long last = m->ncalls - 1;
+    const int nslots = m->ncalls < orbx_matcher::kRing ? (int)m->ncalls : orbx_matcher::kRing;
+    HIP_TRY(hipEventSynchronize(m->ev[last % orbx_matcher::kRing][1]));
+    double sum = 0.0;
+    for (int k = 0; k < nslots; k++) {
+        hipEvent_t* e = m->ev[(last - k) % orbx_matcher::kRing];
+        float t = 0.f;
+        HIP_TRY(hipEventElapsedTime(&t, e[0], e[1]));
+        sum += t;
+    }
+    *ms = (float)(sum / nslots);
     return ORBX_OK;
 }
 
