@@ -159,22 +159,64 @@ __device__ __forceinline__ int reflect101(int i, int n) {
     return i >= n ? 2 * n - 2 - i : i;
 }
 
+// XCD-aware workgroup -> (frame, block) map for 1-D grids of nframes * per_frame
+// workgroups.  The dispatcher hands consecutive workgroup ids to the 8 XCDs round robin
+// and each XCD has its own L2; with nframes % 8 == 0, XCD x runs whole frames x, x+8,
+// ... in block order, so the halos / patches that neighbouring blocks of a frame share
+// are fetched into one L2 once, and every kernel of the pipeline keeps frame f on the
+// same XCD (its L2 may still hold what the previous kernel wrote).
+constexpr int kXcds = 8;
+__device__ __forceinline__ void xcd_frame_block(int per_frame, int nframes, int& f, int& blk) {
+    const int lin = blockIdx.x;
+    if (nframes % kXcds != 0) {
+        f = lin / per_frame;
+        blk = lin - f * per_frame;
+        return;
+    }
+    const int x = lin % kXcds, k = lin / kXcds;
+    const int fl = k / per_frame;
+    blk = k - fl * per_frame;
+    f = fl * kXcds + x;
+}
+
 constexpr int kTW = 64, kTH = 32;  // level tile (outputs) of k_level_tiles
+constexpr int kSW = kTW + 8;       // staged row: image columns X0-4 .. X0+67
+
+typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+
+// Bytes [c+dx, c+dx+3] of a row from its aligned dwords at c-4 (lo), c (mid), c+4 (hi).
+__device__ __forceinline__ uint32_t row_bytes(uint32_t lo, uint32_t mid, uint32_t hi, int dx) {
+    return dx < 0 ? __builtin_amdgcn_alignbyte(mid, lo, 4 + dx) : (dx == 0 ? mid : __builtin_amdgcn_alignbyte(hi, mid, dx));
+}
+// bytes 0,1 / 2,3 of a dword zero-extended into the two 16-bit halves
+__device__ __forceinline__ uint32_t lo_pair(uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c010c00u); }
+__device__ __forceinline__ uint32_t hi_pair(uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c030c02u); }
 
 // One 64x32 tile of one pyramid level per workgroup, all levels and frames in one
-// launch.  The tile plus a 3-pixel REFLECT_101 margin is staged in LDS once and
-// feeds both per-pixel products of the level:
-//  * the FAST strength map M (pixels of the FAST detection area [19, w-19) x [19, h-19)),
+// launch (XCD-aware frame placement).  The tile plus a 3-pixel REFLECT_101 margin is
+// staged in LDS once and feeds both per-pixel products of the level:
 //  * GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of the level ROI clone
 //    (ORBextractor.cc:1587-1595), OpenCV 3.3.1 8U fixed point: taps
-//    {18,34,49,55,49,34,18}, exact integer rows, column (sum + 2^15) >> 16, saturate.
+//    {18,34,49,55,49,34,18}, exact integer rows (<= 257*255, fits u16, packed
+//    v_pk_mad_u16 on 4 pixels per lane), column (sum + 2^15) >> 16, saturate;
+//  * the FAST strength map M on the FAST detection area [19, w-19) x [19, h-19).
+//    Only M > t_q (t_q = min(iniThFAST, minThFAST)) can ever make a keypoint or a
+//    non-zero NMS neighbour in k_fast_cells, and M > t requires two adjacent compass
+//    points (ring 0/4/8/12) beyond t on the same side (every 9-arc holds two).  So
+//    a cheap 4-pixels-per-lane compass test rejects most pixels (M := 0), the
+//    survivors are compacted and only they run the full 16-arc strength.
 __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                      uint8_t* __restrict__ score, long long fb,
-                                                     const LevelGeom* __restrict__ lv, int L) {
-    __shared__ uint8_t s_in[kTH + 6][kTW + 8];
-    __shared__ uint16_t s_row[kTH + 6][kTW];
-    const int tile = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
+                                                     const LevelGeom* __restrict__ lv, int L, int tiles_pf,
+                                                     int nframes, int tq) {
+    __shared__ __align__(16) uint8_t s_in[kTH + 6][kSW];
+    __shared__ __align__(16) uint16_t s_row[kTH + 6][kTW];
+    __shared__ __align__(16) uint8_t s_m[kTH][kTW];
+    __shared__ uint16_t s_list[kTH * kTW];
+    __shared__ int s_n;
+    int f, tile;
+    xcd_frame_block(tiles_pf, nframes, f, tile);
+    const int tid = threadIdx.x, lane = tid & 63;
     int l = 0;
     while (l + 1 < L && tile >= lv[l + 1].tile_first) l++;
     const LevelGeom& g = lv[l];
@@ -182,36 +224,136 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
     const int ty = t / g.tiles_x;
     const int X0 = (t - ty * g.tiles_x) * kTW, Y0 = ty * kTH;
     const uint8_t* img = pyr + (size_t)f * fb + g.off;
-    const int gx0 = reflect101(X0 + lane - 3, g.w);
-    const int gx1 = reflect101(X0 + 64 + (lane < 6 ? lane : 0) - 3, g.w);
-    for (int r = wave; r < kTH + 6; r += 4) {
-        const uint8_t* row = img + (size_t)reflect101(Y0 + r - 3, g.h) * g.pitch;
-        s_in[r][lane] = row[gx0];
-        if (lane < 6) s_in[r][64 + lane] = row[gx1];
-    }
-    __syncthreads();
-    for (int i = tid; i < (kTH + 6) * kTW; i += 256) {
-        const int r = i >> 6, c = i & 63;
-        const uint8_t* p = &s_in[r][c];
-        s_row[r][c] = (uint16_t)(18 * (p[0] + p[6]) + 34 * (p[1] + p[5]) + 49 * (p[2] + p[4]) + 55 * p[3]);
-    }
-    __syncthreads();
-    uint8_t* bout = blur + (size_t)f * fb + g.off;
-    uint8_t* mout = score + (size_t)f * fb + g.off;
-    const int x = X0 + lane;
-    const bool xin = x < g.w;
-    const bool xdet = x >= kEdge && x < g.w - kEdge;
-    for (int r = wave; r < kTH; r += 4) {
-        const int y = Y0 + r;
-        if (y < g.h && xin) {
-            const int s = 18 * ((int)s_row[r][lane] + s_row[r + 6][lane]) + 34 * ((int)s_row[r + 1][lane] + s_row[r + 5][lane]) +
-                          49 * ((int)s_row[r + 2][lane] + s_row[r + 4][lane]) + 55 * (int)s_row[r + 3][lane];
-            const int v = (s + (1 << 15)) >> 16;
-            bout[(size_t)y * g.pitch + x] = (uint8_t)(v > 255 ? 255 : v);
-            int m = 0;
-            if (xdet && y >= kEdge && y < g.h - kEdge) m = fast_strength(&s_in[r + 3][lane + 3], kTW + 8);
-            mout[(size_t)y * g.pitch + x] = (uint8_t)m;
+    // ---- stage rows Y0-3 .. Y0+34, columns X0-4 .. X0+67 (REFLECT_101 at the ROI edges)
+    if (X0 >= 4 && X0 + kTW + 4 <= g.w) {
+        for (int i = tid; i < (kTH + 6) * (kSW / 4); i += 256) {
+            const int r = i / (kSW / 4), c4 = i - r * (kSW / 4);
+            const uint8_t* row = img + (size_t)reflect101(Y0 + r - 3, g.h) * g.pitch;
+            *(uint32_t*)&s_in[r][4 * c4] = *(const uint32_t*)(row + X0 - 4 + 4 * c4);
         }
+    } else {
+        for (int i = tid; i < (kTH + 6) * kSW; i += 256) {
+            const int r = i / kSW, c = i - r * kSW;
+            const uint8_t* row = img + (size_t)reflect101(Y0 + r - 3, g.h) * g.pitch;
+            s_in[r][c] = row[reflect101(min(X0 - 4 + c, 2 * g.w - 2), g.w)];
+        }
+    }
+    if (tid == 0) s_n = 0;
+    for (int i = tid; i < kTH * kTW / 4; i += 256) ((uint32_t*)s_m)[i] = 0u;
+    __syncthreads();
+    // ---- blur rows: 4 outputs per task, packed u16 multiply-add
+    for (int i = tid; i < (kTH + 6) * (kTW / 4); i += 256) {
+        const int r = i >> 4, c0 = 4 + 4 * (i & 15);
+        const uint32_t* rp = (const uint32_t*)&s_in[r][c0];
+        const uint32_t dlo = rp[-1], dmid = rp[0], dhi = rp[1];
+        ushort2_t a = {0, 0}, b = {0, 0};
+        constexpr unsigned short w7[7] = {18, 34, 49, 55, 49, 34, 18};
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            const uint32_t s = row_bytes(dlo, dmid, dhi, k - 3);
+            const ushort2_t wk = {w7[k], w7[k]};
+            a += __builtin_bit_cast(ushort2_t, lo_pair(s)) * wk;
+            b += __builtin_bit_cast(ushort2_t, hi_pair(s)) * wk;
+        }
+        *(uint2*)&s_row[r][c0 - 4] = make_uint2(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b));
+    }
+    // ---- FAST compass test on the detection area, compaction of the survivors
+    for (int i = tid; i < kTH * (kTW / 4); i += 256) {
+        const int r = i >> 4, j = i & 15, c0 = 4 + 4 * j;
+        const int y = Y0 + r, x0 = X0 + 4 * j;
+        unsigned pass = 0;
+        if (y >= kEdge && y < g.h - kEdge && x0 + 3 >= kEdge && x0 < g.w - kEdge) {
+            const uint32_t* rc = (const uint32_t*)&s_in[r + 3][c0];
+            const uint32_t V = rc[0];
+            const uint32_t C0 = *(const uint32_t*)&s_in[r + 6][c0];  // ring 0  (0, +3)
+            const uint32_t C8 = *(const uint32_t*)&s_in[r][c0];      // ring 8  (0, -3)
+            const uint32_t C4 = row_bytes(rc[-1], rc[0], rc[1], 3);   // ring 4  (+3, 0)
+            const uint32_t C12 = row_bytes(rc[-1], rc[0], rc[1], -3); // ring 12 (-3, 0)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const short2_t v = __builtin_bit_cast(short2_t, h ? hi_pair(V) : lo_pair(V));
+                const short2_t a0 = __builtin_bit_cast(short2_t, h ? hi_pair(C0) : lo_pair(C0)) - v;
+                const short2_t a4 = __builtin_bit_cast(short2_t, h ? hi_pair(C4) : lo_pair(C4)) - v;
+                const short2_t a8 = __builtin_bit_cast(short2_t, h ? hi_pair(C8) : lo_pair(C8)) - v;
+                const short2_t a12 = __builtin_bit_cast(short2_t, h ? hi_pair(C12) : lo_pair(C12)) - v;
+                // bright: min of an adjacent pair of (x - v); dark: min of (v - x) = -max(x - v)
+                const short2_t br = __builtin_elementwise_max(
+                    __builtin_elementwise_max(__builtin_elementwise_min(a0, a4), __builtin_elementwise_min(a4, a8)),
+                    __builtin_elementwise_max(__builtin_elementwise_min(a8, a12), __builtin_elementwise_min(a12, a0)));
+                const short2_t dk = __builtin_elementwise_min(
+                    __builtin_elementwise_min(__builtin_elementwise_max(a0, a4), __builtin_elementwise_max(a4, a8)),
+                    __builtin_elementwise_min(__builtin_elementwise_max(a8, a12), __builtin_elementwise_max(a12, a0)));
+                if (br.x > tq || -dk.x > tq) pass |= 1u << (2 * h);
+                if (br.y > tq || -dk.y > tq) pass |= 2u << (2 * h);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int x = x0 + k;
+                if (x < kEdge || x >= g.w - kEdge) pass &= ~(1u << k);
+            }
+        }
+        // wave-level append: offsets from the per-bit ballots, one LDS atomic per wave
+        const unsigned long long below = (1ull << lane) - 1;
+        int off = 0, tot = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const unsigned long long m = __ballot((pass >> k) & 1u);
+            off += __popcll(m & below);
+            tot += __popcll(m);
+        }
+        int base = 0;
+        if (lane == 0 && tot) base = atomicAdd(&s_n, tot);
+        base = __shfl(base, 0);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if ((pass >> k) & 1u) s_list[base + off++] = (uint16_t)((r << 8) | (4 * j + k));
+        }
+    }
+    __syncthreads();
+    // ---- blur columns (4 outputs per task) -> global; exact strength of the survivors
+    uint8_t* bout = blur + (size_t)f * fb + g.off;
+    for (int i = tid; i < kTH * (kTW / 4); i += 256) {
+        const int r = i >> 4, c = 4 * (i & 15);
+        const int y = Y0 + r, x = X0 + c;
+        if (y >= g.h || x >= g.w) continue;
+        unsigned s[4] = {0, 0, 0, 0};
+        constexpr unsigned w7[7] = {18, 34, 49, 55, 49, 34, 18};
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            const uint2 q = *(const uint2*)&s_row[r + k][c];
+            s[0] += w7[k] * (q.x & 0xffffu);
+            s[1] += w7[k] * (q.x >> 16);
+            s[2] += w7[k] * (q.y & 0xffffu);
+            s[3] += w7[k] * (q.y >> 16);
+        }
+        uint32_t packed = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const unsigned v = (s[k] + (1u << 15)) >> 16;
+            packed |= (v > 255 ? 255u : v) << (8 * k);
+        }
+        uint8_t* o = bout + (size_t)y * g.pitch + x;
+        if (x + 4 <= g.w) *(uint32_t*)o = packed;
+        else
+            for (int k = 0; x + k < g.w; k++) o[k] = (uint8_t)(packed >> (8 * k));
+    }
+    const int n = s_n;
+    for (int i = tid; i < n; i += 256) {
+        const int rc = s_list[i];
+        const int r = rc >> 8, c = rc & 255;
+        s_m[r][c] = (uint8_t)fast_strength(&s_in[r + 3][c + 4], kSW);
+    }
+    __syncthreads();
+    uint8_t* mout = score + (size_t)f * fb + g.off;
+    for (int i = tid; i < kTH * (kTW / 4); i += 256) {
+        const int r = i >> 4, c = 4 * (i & 15);
+        const int y = Y0 + r, x = X0 + c;
+        if (y >= g.h || x >= g.w) continue;
+        const uint32_t packed = *(const uint32_t*)&s_m[r][c];
+        uint8_t* o = mout + (size_t)y * g.pitch + x;
+        if (x + 4 <= g.w) *(uint32_t*)o = packed;
+        else
+            for (int k = 0; x + k < g.w; k++) o[k] = (uint8_t)(packed >> (8 * k));
     }
 }
 
@@ -226,12 +368,13 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
                                                     const LevelGeom* __restrict__ lv,
                                                     const CellGeom* __restrict__ cells, int ncells,
                                                     int ini_th, int min_th, uint32_t* __restrict__ slots,
-                                                    int slots_pf, int* __restrict__ cell_count) {
+                                                    int slots_pf, int* __restrict__ cell_count, int nframes) {
     __shared__ uint8_t s_m[4][kCellMax + 2][kCellMax + 2];
     __shared__ unsigned long long s_mask[4][kCellMax];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int ci = blockIdx.x * 4 + wave;
-    const int f = blockIdx.y;
+    int f, cb;
+    xcd_frame_block((ncells + 3) / 4, nframes, f, cb);
+    const int ci = cb * 4 + wave;
     if (ci >= ncells) return;  // whole wave exits; no block barriers below
     const CellGeom c = cells[ci];
     const LevelGeom& g = lv[c.level];
@@ -373,7 +516,7 @@ __global__ __launch_bounds__(256) void k_octree(const LevelGeom* __restrict__ lv
                                                 uint32_t* __restrict__ keys, int* __restrict__ key_node,
                                                 int keys_pf, uint32_t* __restrict__ kept, int kept_pf,
                                                 int* __restrict__ kept_count, int* __restrict__ status,
-                                                int NC) {
+                                                int NC, int nframes) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_tmp[8];
     __shared__ int s_scal[16];
@@ -381,7 +524,9 @@ __global__ __launch_bounds__(256) void k_octree(const LevelGeom* __restrict__ lv
     __shared__ int s_map[kMaxIni];
     __shared__ int s_icnt[kMaxIni];
 
-    const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    int f, l;
+    xcd_frame_block(L, nframes, f, l);
+    const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const LevelGeom& g = lv[l];
     const int N = g.N;
@@ -744,10 +889,11 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
                                                   const uint32_t* __restrict__ kept, int kept_pf,
                                                   const int* __restrict__ kept_count,
                                                   orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
-                                                  int cap, int* __restrict__ n_out) {
+                                                  int cap, int* __restrict__ n_out, int nframes) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int slot = blockIdx.x * 4 + wave;
-    const int f = blockIdx.y;
+    int f, sb;
+    xcd_frame_block((kept_pf + 3) / 4, nframes, f, sb);
+    const int slot = sb * 4 + wave;
     if (slot >= kept_pf) return;
     int l = 0;
     while (l + 1 < L && slot >= lv[l + 1].out_off) l++;
@@ -854,29 +1000,32 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     }
     if (ev) (void)hipEventRecord(ev[1], stream);
     {
-        dim3 grid(plan.tiles_total, batch);
-        hipLaunchKernelGGL(k_level_tiles, grid, dim3(256), 0, stream, db.pyr, db.blur, db.score, fb, db.lv, L);
+        dim3 grid(plan.tiles_total * batch);
+        int tq = plan.prm.ini_th < plan.prm.min_th ? plan.prm.ini_th : plan.prm.min_th;
+        tq = tq < 0 ? 0 : (tq > 255 ? 255 : tq);
+        hipLaunchKernelGGL(k_level_tiles, grid, dim3(256), 0, stream, db.pyr, db.blur, db.score, fb, db.lv, L,
+                           plan.tiles_total, batch, tq);
     }
     if (ev) (void)hipEventRecord(ev[2], stream);
     {
-        dim3 grid((ncells + 3) / 4, batch);
+        dim3 grid(((ncells + 3) / 4) * batch);
         hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), 0, stream, db.score, fb, db.lv, db.cells, ncells,
-                           plan.prm.ini_th, plan.prm.min_th, db.slots, plan.slots_per_frame, db.cell_count);
+                           plan.prm.ini_th, plan.prm.min_th, db.slots, plan.slots_per_frame, db.cell_count, batch);
     }
     if (ev) (void)hipEventRecord(ev[3], stream);
     {
         const int NC = (plan.max_ncap + 63) & ~63;
         const size_t lds = (size_t)NC * (8 + 16 + 12 + 8 + 8 + 16 + 2);
-        dim3 grid(L, batch);
+        dim3 grid(L * batch);
         hipLaunchKernelGGL(k_octree, grid, dim3(256), lds, stream, db.lv, L, db.slots, plan.slots_per_frame,
                            db.cells, db.cell_count, ncells, db.keys, db.key_node, plan.keys_per_frame,
-                           db.kept, plan.kept_per_frame, db.kept_count, db.status, NC);
+                           db.kept, plan.kept_per_frame, db.kept_count, db.status, NC, batch);
     }
     if (ev) (void)hipEventRecord(ev[4], stream);
     {
-        dim3 grid((plan.kept_per_frame + 3) / 4, batch);
+        dim3 grid(((plan.kept_per_frame + 3) / 4) * batch);
         hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, stream, db.pyr, db.blur, fb, db.lv, L, db.kept,
-                           plan.kept_per_frame, db.kept_count, (orbx_keypoint*)kps, desc, cap, n_per_frame);
+                           plan.kept_per_frame, db.kept_count, (orbx_keypoint*)kps, desc, cap, n_per_frame, batch);
     }
     if (ev) (void)hipEventRecord(ev[5], stream);
     return hipGetLastError();
