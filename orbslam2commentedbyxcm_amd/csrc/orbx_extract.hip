@@ -37,6 +37,26 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// XCD-aware workgroup -> (frame, block) map for 1-D grids of nframes * per_frame
+// workgroups.  The dispatcher hands consecutive workgroup ids to the 8 XCDs round robin
+// and each XCD has its own L2; with nframes % 8 == 0, XCD x runs whole frames x, x+8,
+// ... in block order, so the halos / patches that neighbouring blocks of a frame share
+// are fetched into one L2 once, and every kernel of the pipeline keeps frame f on the
+// same XCD (its L2 may still hold what the previous kernel wrote).
+constexpr int kXcds = 8;
+__device__ __forceinline__ void xcd_frame_block(int per_frame, int nframes, int& f, int& blk) {
+    const int lin = blockIdx.x;
+    if (nframes % kXcds != 0) {
+        f = lin / per_frame;
+        blk = lin - f * per_frame;
+        return;
+    }
+    const int x = lin % kXcds, k = lin / kXcds;
+    const int fl = k / per_frame;
+    blk = k - fl * per_frame;
+    f = fl * kXcds + x;
+}
+
 // ------------------------------------------------------------------ pyramid
 
 // Level 0 = the input frame copied into the pyramid block (ORBextractor.cc:1688-1690;
@@ -64,56 +84,71 @@ __global__ __launch_bounds__(256) void k_copy_level0(const uint8_t* __restrict__
     }
 }
 
-constexpr int kRszTW = 64, kRszTH = 16;           // resize output tile
-constexpr int kRszSW = 192, kRszSH = 48;          // max staged source region
-
 // cv::resize(level l-1 ROI, level l, INTER_LINEAR), OpenCV 3.3.1 fixed point:
 // h = S[sx0]*a0 + S[sx1]*a1 (exact), dst = ((b0*(h0>>4))>>16 + (b1*(h1>>4))>>16 + 2)>>2.
-// One 64x16 output tile per workgroup; its source rows/columns are staged in LDS.
+// One kRzTW x kRzTH (256 x 32) output tile per workgroup (XCD-aware frame placement).
+// The tile's source region is staged in LDS with dword loads (columns aligned down to
+// 4 bytes; sw x sh bytes of dynamic LDS sized by the plan); each lane keeps the
+// horizontal taps of its 4 output columns in registers and the waves walk the rows,
+// whose vertical taps are wave-uniform.  Output rows are written as dwords.
 __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, long long fb,
                                                 const LevelGeom* __restrict__ lv, int l,
-                                                const int16_t* __restrict__ rtab) {
-    __shared__ uint8_t s_src[kRszSH][kRszSW];
+                                                const int16_t* __restrict__ rtab, int nframes, int sw) {
+    extern __shared__ __align__(16) uint8_t s_src[];
     const LevelGeom& g = lv[l];
     const LevelGeom& p = lv[l - 1];
-    const int f = blockIdx.z, X0 = blockIdx.x * kRszTW, Y0 = blockIdx.y * kRszTH;
+    const int tx = (g.w + kRzTW - 1) / kRzTW, tyn = (g.h + kRzTH - 1) / kRzTH;
+    int f, b;
+    xcd_frame_block(tx * tyn, nframes, f, b);
+    const int by = b / tx;
+    const int X0 = (b - by * tx) * kRzTW, Y0 = by * kRzTH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int16_t* xt = rtab + g.xtab_off;
     const int16_t* yt = rtab + g.ytab_off;
-    const int xe = min(X0 + kRszTW, g.w) - 1, ye = min(Y0 + kRszTH, g.h) - 1;
-    const int sx_lo = xt[4 * X0], sx_hi = xt[4 * xe + 1];
+    const int xe = min(X0 + kRzTW, g.w) - 1, ye = min(Y0 + kRzTH, g.h) - 1;
+    const int a_lo = xt[4 * X0] & ~3, sx_hi = xt[4 * xe + 1];
     const int sy_lo = yt[4 * Y0], sy_hi = yt[4 * ye + 1];
-    const int ncols = sx_hi - sx_lo + 1, nrows = sy_hi - sy_lo + 1;
-    const uint8_t* base = pyr + (size_t)f * fb + p.off + (size_t)sy_lo * p.pitch + sx_lo;
-    for (int r = wave; r < nrows; r += 4)
-        for (int c = lane; c < ncols; c += 64) s_src[r][c] = base[(size_t)r * p.pitch + c];
-    __syncthreads();
-    const int ry = tid >> 4, cx = (tid & 15) * 4;
-    const int dy = Y0 + ry;
-    if (dy >= g.h) return;
-    const int r0 = yt[4 * dy] - sy_lo, r1 = yt[4 * dy + 1] - sy_lo;
-    const int b0 = yt[4 * dy + 2], b1 = yt[4 * dy + 3];
-    uint32_t packed = 0;
-    const int nvalid = min(4, g.w - (X0 + cx));
+    const int ncols4 = ((sx_hi - a_lo) >> 2) + 1, nrows = sy_hi - sy_lo + 1;
+    const uint8_t* base = pyr + (size_t)f * fb + p.off + (size_t)sy_lo * p.pitch + a_lo;
+    for (int i = tid; i < nrows * ncols4; i += 256) {
+        const int r = i / ncols4, c = i - r * ncols4;
+        *(uint32_t*)&s_src[r * sw + 4 * c] = *(const uint32_t*)(base + (size_t)r * p.pitch + 4 * c);
+    }
+    // horizontal taps of this lane's 4 columns
+    const int cx = X0 + 4 * lane;
+    const int nvalid = min(4, g.w - cx);
+    int sx0[4], sx1[4], a0[4], a1[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        if (k < nvalid) {
-            const int dx = X0 + cx + k;
-            const int2 t = *(const int2*)(xt + 4 * dx);  // sx0, sx1, a0, a1 as 4 x int16
-            const int sx0 = (int16_t)(t.x & 0xffff) - sx_lo, sx1 = (int16_t)(t.x >> 16) - sx_lo;
-            const int a0 = (int16_t)(t.y & 0xffff), a1 = (int16_t)(t.y >> 16);
-            const int h0 = s_src[r0][sx0] * a0 + s_src[r0][sx1] * a1;
-            const int h1 = s_src[r1][sx0] * a0 + s_src[r1][sx1] * a1;
+        const int dx = k < nvalid ? cx + k : X0;
+        const int2 t = *(const int2*)(xt + 4 * dx);  // sx0, sx1, a0, a1 as 4 x int16
+        sx0[k] = (int16_t)(t.x & 0xffff) - a_lo;
+        sx1[k] = (int16_t)(t.x >> 16) - a_lo;
+        a0[k] = (int16_t)(t.y & 0xffff);
+        a1[k] = (int16_t)(t.y >> 16);
+    }
+    __syncthreads();
+    if (nvalid <= 0) return;
+    uint8_t* out = pyr + (size_t)f * fb + g.off + cx;
+    for (int r = wave; Y0 + r <= ye; r += 4) {
+        const int dy = Y0 + r;
+        const int2 t = *(const int2*)(yt + 4 * dy);  // wave-uniform: r0, r1, b0, b1
+        const uint8_t* s0 = s_src + ((int16_t)(t.x & 0xffff) - sy_lo) * sw;
+        const uint8_t* s1 = s_src + ((int16_t)(t.x >> 16) - sy_lo) * sw;
+        const int b0 = (int16_t)(t.y & 0xffff), b1 = (int16_t)(t.y >> 16);
+        uint32_t packed = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int h0 = s0[sx0[k]] * a0[k] + s0[sx1[k]] * a1[k];
+            const int h1 = s1[sx0[k]] * a0[k] + s1[sx1[k]] * a1[k];
             int v = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
             v = v < 0 ? 0 : (v > 255 ? 255 : v);
             packed |= (uint32_t)v << (8 * k);
         }
-    }
-    uint8_t* out = pyr + (size_t)f * fb + g.off + (size_t)dy * g.pitch + X0 + cx;
-    if (nvalid == 4) {
-        *(uint32_t*)out = packed;
-    } else {
-        for (int k = 0; k < nvalid; k++) out[k] = (uint8_t)(packed >> (8 * k));
+        uint8_t* o = out + (size_t)dy * g.pitch;
+        if (nvalid == 4) *(uint32_t*)o = packed;
+        else
+            for (int k = 0; k < nvalid; k++) o[k] = (uint8_t)(packed >> (8 * k));
     }
 }
 
@@ -157,26 +192,6 @@ __device__ __forceinline__ int fast_strength(const uint8_t* c, int pitch) {
 __device__ __forceinline__ int reflect101(int i, int n) {
     i = i < 0 ? -i : i;
     return i >= n ? 2 * n - 2 - i : i;
-}
-
-// XCD-aware workgroup -> (frame, block) map for 1-D grids of nframes * per_frame
-// workgroups.  The dispatcher hands consecutive workgroup ids to the 8 XCDs round robin
-// and each XCD has its own L2; with nframes % 8 == 0, XCD x runs whole frames x, x+8,
-// ... in block order, so the halos / patches that neighbouring blocks of a frame share
-// are fetched into one L2 once, and every kernel of the pipeline keeps frame f on the
-// same XCD (its L2 may still hold what the previous kernel wrote).
-constexpr int kXcds = 8;
-__device__ __forceinline__ void xcd_frame_block(int per_frame, int nframes, int& f, int& blk) {
-    const int lin = blockIdx.x;
-    if (nframes % kXcds != 0) {
-        f = lin / per_frame;
-        blk = lin - f * per_frame;
-        return;
-    }
-    const int x = lin % kXcds, k = lin / kXcds;
-    const int fl = k / per_frame;
-    blk = k - fl * per_frame;
-    f = fl * kXcds + x;
 }
 
 constexpr int kTW = 64, kTH = 32;  // level tile (outputs) of k_level_tiles
@@ -992,10 +1007,17 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
         dim3 grid(64, batch);
         hipLaunchKernelGGL(k_copy_level0, grid, dim3(256), 0, stream, d_imgs, frame_pitch, stride, g0.w, g0.h,
                            db.pyr, fb, g0.pitch, vec16);
+        const size_t rz_lds = (size_t)plan.rz_sw * plan.rz_sh;
+        if (rz_lds > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void*)k_resize, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)rz_lds);
+            if (e != hipSuccess) return e;
+        }
         for (int l = 1; l < L; l++) {
             const LevelGeom& g = plan.lv[l];
-            dim3 gr((g.w + kRszTW - 1) / kRszTW, (g.h + kRszTH - 1) / kRszTH, batch);
-            hipLaunchKernelGGL(k_resize, gr, dim3(256), 0, stream, db.pyr, fb, db.lv, l, db.rtab);
+            dim3 gr(((g.w + kRzTW - 1) / kRzTW) * ((g.h + kRzTH - 1) / kRzTH) * batch);
+            hipLaunchKernelGGL(k_resize, gr, dim3(256), rz_lds, stream, db.pyr, fb, db.lv, l, db.rtab, batch,
+                               plan.rz_sw);
         }
     }
     if (ev) (void)hipEventRecord(ev[1], stream);

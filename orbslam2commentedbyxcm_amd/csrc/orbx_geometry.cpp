@@ -196,17 +196,22 @@ bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
             g.ytab_off = (int)plan.rtab.size();
             plan.rtab.resize(plan.rtab.size() + 4 * (size_t)g.h);
             resize_tables(prev_w, prev_h, g.w, g.h, plan.rtab.data() + g.xtab_off, plan.rtab.data() + g.ytab_off);
-            // the resize kernel stages each 64x16 output tile's source region in LDS
+            // the resize kernel stages each kRzTW x kRzTH output tile's source region
+            // (dword-aligned columns) in LDS; record the largest region
             const int16_t* xt = plan.rtab.data() + g.xtab_off;
             const int16_t* yt = plan.rtab.data() + g.ytab_off;
-            for (int x0 = 0; x0 < g.w; x0 += 64) {
-                const int xe = (x0 + 64 < g.w ? x0 + 64 : g.w) - 1;
-                if (xt[4 * xe + 1] - xt[4 * x0] + 1 > 192) { plan.why = "scale factor too large"; return false; }
+            for (int x0 = 0; x0 < g.w; x0 += kRzTW) {
+                const int xe = (x0 + kRzTW < g.w ? x0 + kRzTW : g.w) - 1;
+                const int a_lo = xt[4 * x0] & ~3;
+                const int bytes = 4 * (((xt[4 * xe + 1] - a_lo) >> 2) + 1);
+                if (bytes > plan.rz_sw) plan.rz_sw = bytes;
             }
-            for (int y0 = 0; y0 < g.h; y0 += 16) {
-                const int ye = (y0 + 16 < g.h ? y0 + 16 : g.h) - 1;
-                if (yt[4 * ye + 1] - yt[4 * y0] + 1 > 48) { plan.why = "scale factor too large"; return false; }
+            for (int y0 = 0; y0 < g.h; y0 += kRzTH) {
+                const int ye = (y0 + kRzTH < g.h ? y0 + kRzTH : g.h) - 1;
+                const int rows = yt[4 * ye + 1] - yt[4 * y0] + 1;
+                if (rows > plan.rz_sh) plan.rz_sh = rows;
             }
+            if ((long long)plan.rz_sw * plan.rz_sh > kRzMaxLds) { plan.why = "scale factor too large"; return false; }
         }
         prev_w = g.w;
         prev_h = g.h;

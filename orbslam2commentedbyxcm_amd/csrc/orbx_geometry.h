@@ -68,6 +68,10 @@ struct CellGeom {
     int pad;
 };
 
+// k_resize output tile and its LDS budget for the staged source region
+constexpr int kRzTW = 256, kRzTH = 32;
+constexpr int kRzMaxLds = 144 * 1024;
+
 struct Plan {
     int W = 0, H = 0, L = 0;
     OrbParams prm;
@@ -79,6 +83,7 @@ struct Plan {
     int keys_per_frame = 0;         // candidate key capacity per frame
     int kept_per_frame = 0;         // sum of ncap
     int tiles_total = 0;            // blur tiles per frame
+    int rz_sw = 0, rz_sh = 0;       // largest staged resize source region (bytes x rows)
     int max_ncap = 0;
     int max_key_cap = 0;
     bool ok = false;
