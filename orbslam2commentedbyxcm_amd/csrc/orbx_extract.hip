@@ -18,7 +18,7 @@ namespace orbx {
 
 const char* const kStageNames[kStages] = {"pyramid", "score_blur", "fast_cells", "octree", "describe", "total"};
 
-__constant__ int8_t c_pattern[1024];
+__constant__ __align__(16) int8_t c_pattern[1024];
 __constant__ int c_umax[16];
 
 static const int8_t kPatternHost[1024] = {
@@ -110,9 +110,23 @@ __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, long 
     const int sy_lo = yt[4 * Y0], sy_hi = yt[4 * ye + 1];
     const int ncols4 = ((sx_hi - a_lo) >> 2) + 1, nrows = sy_hi - sy_lo + 1;
     const uint8_t* base = pyr + (size_t)f * fb + p.off + (size_t)sy_lo * p.pitch + a_lo;
-    for (int i = tid; i < nrows * ncols4; i += 256) {
-        const int r = i / ncols4, c = i - r * ncols4;
-        *(uint32_t*)&s_src[r * sw + 4 * c] = *(const uint32_t*)(base + (size_t)r * p.pitch + 4 * c);
+    const int nld = nrows * ncols4;
+    for (int i0 = 0; i0 < nld; i0 += 256 * 8) {  // 8 loads in flight per thread
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int i = min(i0 + tid + 256 * k, nld - 1);
+            const int r = i / ncols4, c = i - r * ncols4;
+            v[k] = *(const uint32_t*)(base + (size_t)r * p.pitch + 4 * c);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int i = i0 + tid + 256 * k;
+            if (i < nld) {
+                const int r = i / ncols4, c = i - r * ncols4;
+                *(uint32_t*)&s_src[r * sw + 4 * c] = v[k];
+            }
+        }
     }
     // horizontal taps of this lane's 4 columns
     const int cx = X0 + 4 * lane;
@@ -240,17 +254,34 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
     const int X0 = (t - ty * g.tiles_x) * kTW, Y0 = ty * kTH;
     const uint8_t* img = pyr + (size_t)f * fb + g.off;
     // ---- stage rows Y0-3 .. Y0+34, columns X0-4 .. X0+67 (REFLECT_101 at the ROI edges)
+    // (all loads of a thread are issued before the LDS stores: no per-load round trip)
     if (X0 >= 4 && X0 + kTW + 4 <= g.w) {
-        for (int i = tid; i < (kTH + 6) * (kSW / 4); i += 256) {
+        constexpr int kN = (kTH + 6) * (kSW / 4), kPer = (kN + 255) / 256;
+        uint32_t v[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int i = min(tid + 256 * k, kN - 1);
             const int r = i / (kSW / 4), c4 = i - r * (kSW / 4);
-            const uint8_t* row = img + (size_t)reflect101(Y0 + r - 3, g.h) * g.pitch;
-            *(uint32_t*)&s_in[r][4 * c4] = *(const uint32_t*)(row + X0 - 4 + 4 * c4);
+            v[k] = *(const uint32_t*)(img + (size_t)reflect101(Y0 + r - 3, g.h) * g.pitch + X0 - 4 + 4 * c4);
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int i = tid + 256 * k;
+            if (i < kN) ((uint32_t*)s_in)[i] = v[k];
         }
     } else {
-        for (int i = tid; i < (kTH + 6) * kSW; i += 256) {
+        constexpr int kN = (kTH + 6) * kSW, kPer = (kN + 255) / 256;
+        uint8_t v[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int i = min(tid + 256 * k, kN - 1);
             const int r = i / kSW, c = i - r * kSW;
-            const uint8_t* row = img + (size_t)reflect101(Y0 + r - 3, g.h) * g.pitch;
-            s_in[r][c] = row[reflect101(min(X0 - 4 + c, 2 * g.w - 2), g.w)];
+            v[k] = img[(size_t)reflect101(Y0 + r - 3, g.h) * g.pitch + reflect101(min(X0 - 4 + c, 2 * g.w - 2), g.w)];
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int i = tid + 256 * k;
+            if (i < kN) ((uint8_t*)s_in)[i] = v[k];
         }
     }
     if (tid == 0) s_n = 0;
@@ -376,16 +407,28 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
 
 // One wave per cell.  Reproduces cv::FAST(cell, kps, t, true) for t = iniThFAST and,
 // if that leaves the cell empty, t = minThFAST (ORBextractor.cc:1091-1104), from the
-// strength map M: corner iff M > t, score M - 1, FAST_t's non-max suppression over the
-// 8-neighbourhood where neighbours outside the cell's detection window or below the
-// threshold score 0.  Writes the cell's keypoints in raster order.
+// strength map M (corner iff M > t, score M - 1).  FAST_t's non-max suppression over
+// the 8-neighbourhood, where neighbours outside the cell's detection window or below
+// the threshold score 0, keeps a corner p iff M_p > t, M_p >= 2 and M_p exceeds every
+// in-window neighbour's M (a neighbour with M_n >= M_p > t always suppresses; one
+// below M_p never does) -- threshold-independent apart from M_p > t.  So one sweep
+// over the window rows (lane = column, horizontal neighbours by DPP lane shifts,
+// vertical ones rolled in registers) yields the keep masks of both thresholds; each
+// row's two ballots are parked in lane `row` of four VGPRs.  Survivors are written in
+// raster order.
+__device__ __forceinline__ int lane_from_left(int v) {   // v of lane-1 (0 at lane 0)
+    return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, false);  // wave_shr:1
+}
+__device__ __forceinline__ int lane_from_right(int v) {  // v of lane+1 (0 at lane 63)
+    return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xF, 0xF, false);  // wave_shl:1
+}
+
 __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ score, long long fb,
                                                     const LevelGeom* __restrict__ lv,
                                                     const CellGeom* __restrict__ cells, int ncells,
                                                     int ini_th, int min_th, uint32_t* __restrict__ slots,
                                                     int slots_pf, int* __restrict__ cell_count, int nframes) {
-    __shared__ uint8_t s_m[4][kCellMax + 2][kCellMax + 2];
-    __shared__ unsigned long long s_mask[4][kCellMax];
+    __shared__ uint8_t s_m[4][kCellMax][64];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int f, cb;
     xcd_frame_block((ncells + 3) / 4, nframes, f, cb);
@@ -397,56 +440,78 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
     int count = 0;
     if (wr > 0 && wc > 0) {
         const uint8_t* src = score + (size_t)f * fb + g.off + (size_t)(c.y0 + 3) * g.pitch + c.x0 + 3;
-        uint8_t(*m)[kCellMax + 2] = s_m[wave];
-        // window M with a zero frame: m[r+1][c+1] = M(r, c)
-        for (int r = 0; r < wr + 2; r++)
-            for (int col = lane; col < wc + 2; col += 64) m[r][col] = 0;
-        wave_lds_fence();
-        for (int r = 0; r < wr; r++)
-            if (lane < wc) m[r + 1][lane + 1] = src[(size_t)r * g.pitch + lane];
-        wave_lds_fence();
-        for (int pass = 0; pass < 2; pass++) {
-            int t = pass == 0 ? ini_th : min_th;
-            t = t < 0 ? 0 : (t > 255 ? 255 : t);
-            count = 0;
-            for (int r = 0; r < wr; r++) {
-                bool keep = false;
-                if (lane < wc) {
-                    const int mc = m[r + 1][lane + 1];
-                    if (mc > t) {
-                        int nb = 0;
+        uint8_t(*m)[64] = s_m[wave];
+        const bool act = lane < wc;
+        // 16 rows of loads in flight at a time (unconditional loads from clamped
+        // addresses, so the compiler does not serialise load -> LDS store per row)
+        for (int r0 = 0; r0 < wr; r0 += 16) {
+            int v[16];
 #pragma unroll
-                        for (int dy = 0; dy < 3; dy++)
-#pragma unroll
-                            for (int dx = 0; dx < 3; dx++) {
-                                if (dx == 1 && dy == 1) continue;
-                                const int mn = m[r + dy][lane + dx];
-                                const int sn = mn > t ? mn - 1 : 0;
-                                nb = sn > nb ? sn : nb;
-                            }
-                        keep = mc - 1 > nb;
-                    }
-                }
-                const unsigned long long mask = __ballot(keep);
-                if (lane == 0) s_mask[wave][r] = mask;
-                count += __popcll(mask);
+            for (int k = 0; k < 16; k++) {
+                const bool ok = act && r0 + k < wr;
+                v[k] = src[ok ? (size_t)(r0 + k) * g.pitch + lane : 0];
+                v[k] = ok ? v[k] : 0;
             }
-            if (count > 0) break;
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                if (r0 + k < wr) m[r0 + k][lane] = (uint8_t)v[k];
         }
         wave_lds_fence();
-        uint32_t* out = slots + (size_t)f * slots_pf + c.slot_off;
-        int running = 0;
-        const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+        const int ti = ini_th < 0 ? 0 : (ini_th > 255 ? 255 : ini_th);
+        const int tm = min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th);
+        int vc = m[0][lane];
+        int vn = wr > 1 ? m[1][lane] : 0;
+        int hp = 0;                                                    // row r-1: max of c-1, c, c+1
+        int hc = max(max(lane_from_left(vc), lane_from_right(vc)), vc);  // row r
+        unsigned ki_lo = 0, ki_hi = 0, km_lo = 0, km_hi = 0;           // lane r: row r's keep masks
+        int cnt_i = 0, cnt_m = 0;
         for (int r = 0; r < wr; r++) {
-            const unsigned long long mask = s_mask[wave][r];
-            if ((mask >> lane) & 1ull) {
-                const int idx = running + __popcll(mask & below);
-                const int xr = c.x0 + 3 + lane - kMinBorder;  // relative to minBorderX
-                const int yr = c.y0 + 3 + r - kMinBorder;
-                const int resp = m[r + 1][lane + 1] - 1;
-                out[idx] = (uint32_t)xr | ((uint32_t)yr << 12) | ((uint32_t)resp << 24);
+            const int vnn = r + 2 < wr ? m[r + 2][lane] : 0;
+            const int ln = lane_from_left(vn), rn = lane_from_right(vn);
+            const int hn = max(max(ln, rn), vn);
+            const int nb = max(max(hp, hn), max(lane_from_left(vc), lane_from_right(vc)));
+            const bool lm = act && vc >= 2 && vc > nb;
+            const unsigned long long bi = __ballot(lm && vc > ti);
+            const unsigned long long bm = __ballot(lm && vc > tm);
+            cnt_i += __popcll(bi);
+            cnt_m += __popcll(bm);
+            if (lane == r) {
+                ki_lo = (unsigned)bi;
+                ki_hi = (unsigned)(bi >> 32);
+                km_lo = (unsigned)bm;
+                km_hi = (unsigned)(bm >> 32);
             }
-            running += __popcll(mask);
+            hp = hc;
+            hc = hn;
+            vc = vn;
+            vn = vnn;
+        }
+        const bool use_ini = cnt_i > 0;
+        count = use_ini ? cnt_i : cnt_m;
+        if (count > 0) {
+            const unsigned klo = use_ini ? ki_lo : km_lo, khi = use_ini ? ki_hi : km_hi;
+            const int pc = lane < wr ? __popc(klo) + __popc(khi) : 0;
+            int incl = pc;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(incl, o);
+                if (lane >= o) incl += y;
+            }
+            const int excl = incl - pc;
+            uint32_t* out = slots + (size_t)f * slots_pf + c.slot_off;
+            const unsigned long long below = (1ull << lane) - 1;
+            const int xr = c.x0 + 3 + lane - kMinBorder;  // relative to minBorderX
+            for (int r = 0; r < wr; r++) {
+                const unsigned long long mask = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)khi, r) << 32) |
+                                                (unsigned)__builtin_amdgcn_readlane((int)klo, r);
+                if (!mask) continue;
+                if ((mask >> lane) & 1ull) {
+                    const int idx = __builtin_amdgcn_readlane(excl, r) + __popcll(mask & below);
+                    const int yr = c.y0 + 3 + r - kMinBorder;
+                    const int resp = m[r][lane] - 1;
+                    out[idx] = (uint32_t)xr | ((uint32_t)yr << 12) | ((uint32_t)resp << 24);
+                }
+            }
         }
     }
     if (lane == 0) cell_count[(size_t)f * ncells + ci] = count;
@@ -928,20 +993,38 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     const uint32_t key = kept[(size_t)f * kept_pf + slot];
     const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
     const int resp = key_resp(key);
+    // loads that do not depend on the patch, issued up front (the empty asm keeps the
+    // compiler from sinking them behind the IC-angle latency)
+    int pat[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        pat[k] = ((const int*)c_pattern)[k * 64 + lane];  // x0, y0, x1, y1 of pair k*64+lane
+        asm volatile("" : "+v"(pat[k]));
+    }
+    float lv_scale = g.scale, lv_size = g.kp_size;
+    asm volatile("" : "+v"(lv_scale), "+v"(lv_size));
 
-    // IC angle: lanes 0..30 own columns u = -15..15 of the circular patch
+    // IC angle (cc:59-106): lane u+15 (u = -15..15) sums column u over rows v = 0..15,
+    // lane 32+u+15 over rows v = -1..-15; all 16 loads of a lane are issued before any
+    // is consumed (unconditional loads from in-patch addresses, masked afterwards).
     int m10 = 0, m01 = 0;
-    if (lane < 31) {
-        const int u = lane - 15;
+    {
+        const int half = lane >> 5, u = (lane & 31) - 15;
         const int au = u < 0 ? -u : u;
-        const uint8_t* col = pyr + (size_t)f * fb + g.off + (size_t)y * g.pitch + x + u;
-        m10 = u * (int)col[0];
-        for (int v = 1; v <= 15; v++) {
-            if (au <= c_umax[v]) {
-                const int plus = col[(size_t)v * g.pitch];
-                const int minus = col[-(long)v * g.pitch];
-                m10 += u * (plus + minus);
-                m01 += v * (plus - minus);
+        const bool col_ok = (lane & 31) < 31;
+        const uint8_t* ctr = pyr + (size_t)f * fb + g.off + (size_t)y * g.pitch + x + (col_ok ? u : 0);
+        const long sgn = half ? -(long)g.pitch : (long)g.pitch;
+        int px[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) px[k] = ctr[(long)k * sgn];
+        if (col_ok) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                if (k == 0 && half) continue;  // row 0 counted once (by the v >= 0 half)
+                if (k > 0 && au > c_umax[k]) continue;
+                const int v = half ? -k : k;
+                m10 += u * px[k];
+                m01 += v * px[k];
             }
         }
     }
@@ -952,22 +1035,23 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     }
     const float angle = fast_atan2((float)m01, (float)m10);
 
-    // steered BRIEF on the blurred level
+    // steered BRIEF on the blurred level: all 8 samples of a lane in flight at once
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float rad = angle * factorPI;
     const float a = (float)cos((double)rad), b = (float)sin((double)rad);
     const uint8_t* center = blur + (size_t)f * fb + g.off + (size_t)y * g.pitch + x;
     const int step = g.pitch;
-    unsigned long long words[4];
+    int t0[4], t1[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const int p = k * 64 + lane;
-        const float x0 = (float)c_pattern[4 * p], y0 = (float)c_pattern[4 * p + 1];
-        const float x1 = (float)c_pattern[4 * p + 2], y1 = (float)c_pattern[4 * p + 3];
-        const int t0 = center[cv_round(x0 * b + y0 * a) * step + cv_round(x0 * a - y0 * b)];
-        const int t1 = center[cv_round(x1 * b + y1 * a) * step + cv_round(x1 * a - y1 * b)];
-        words[k] = __ballot(t0 < t1);
+        const float x0 = (float)(int8_t)(pat[k] & 0xff), y0 = (float)(int8_t)((pat[k] >> 8) & 0xff);
+        const float x1 = (float)(int8_t)((pat[k] >> 16) & 0xff), y1 = (float)(int8_t)(pat[k] >> 24);
+        t0[k] = center[cv_round(x0 * b + y0 * a) * step + cv_round(x0 * a - y0 * b)];
+        t1[k] = center[cv_round(x1 * b + y1 * a) * step + cv_round(x1 * a - y1 * b)];
     }
+    unsigned long long words[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) words[k] = __ballot(t0[k] < t1[k]);
     if (lane < 4) {
         unsigned long long* d = (unsigned long long*)(desc + ((size_t)f * cap + o) * 32);
         d[lane] = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
@@ -975,13 +1059,13 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     if (lane == 0) {
         float fx = (float)x, fy = (float)y;
         if (l != 0) {
-            fx = fx * g.scale;
-            fy = fy * g.scale;
+            fx = fx * lv_scale;
+            fy = fy * lv_scale;
         }
         orbx_keypoint kp;
         kp.x = fx;
         kp.y = fy;
-        kp.size = g.kp_size;
+        kp.size = lv_size;
         kp.angle = angle;
         kp.response = (float)resp;
         kp.octave = l;
