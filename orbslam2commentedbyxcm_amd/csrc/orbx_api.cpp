@@ -81,7 +81,7 @@ namespace {
 
 void free_buffers(DeviceBuffers& db) {
     void* ptrs[] = {db.lv, db.cells, db.rtab, db.pyr, db.blur, db.score, db.slots, db.cell_count,
-                    db.keys, db.key_node, db.kept, db.kept_count, db.status};
+                    db.keys, db.key_node, db.kept, db.kept_count, db.status, db.oct_stamps};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     db = DeviceBuffers();
@@ -117,6 +117,7 @@ int prepare(orbx_extractor* ex, int W, int H, int batch) {
     HIP_TRY(dalloc(&db.kept, B * (size_t)p.kept_per_frame));
     HIP_TRY(dalloc(&db.kept_count, B * (size_t)p.L));
     HIP_TRY(dalloc(&db.status, B));
+    if (getenv("ORBX_OCT_STAMPS")) HIP_TRY(dalloc(&db.oct_stamps, B * (size_t)p.L * 8));
     HIP_TRY(hipMemcpyAsync(db.lv, p.lv, sizeof(LevelGeom) * kMaxLevels, hipMemcpyHostToDevice, ex->stream));
     HIP_TRY(hipMemcpyAsync(db.cells, p.cells.data(), sizeof(CellGeom) * p.cells.size(), hipMemcpyHostToDevice,
                            ex->stream));
@@ -149,6 +150,27 @@ int run_device(orbx_extractor* ex, int batch, const uint8_t* d_imgs, size_t fram
     hipError_t e = launch_extract(ex->plan, ex->db, batch, d_imgs, frame_pitch, stride, d_kps, d_desc, cap, d_n,
                                   stream, ev);
     if (e != hipSuccess) return hip_fail(e, "launch_extract");
+    if (ex->db.oct_stamps) {  // diagnostics: per-level k_octree phase times (us) to stderr
+        const int L = ex->plan.L;
+        std::vector<unsigned long long> h((size_t)batch * L * 8);
+        HIP_TRY(hipStreamSynchronize(stream));
+        HIP_TRY(hipMemcpy(h.data(), ex->db.oct_stamps, h.size() * 8, hipMemcpyDeviceToHost));
+        for (int l = 0; l < L; l++) {
+            double ph[4] = {0, 0, 0, 0}, mx = 0, n = 0, g1 = 0, g2 = 0;
+            for (int f = 0; f < batch; f++) {
+                const unsigned long long* r = &h[((size_t)f * L + l) * 8];
+                for (int k = 0; k < 4; k++) ph[k] += (double)(r[k + 1] - r[k]) * 0.01;
+                const double tot = (double)(r[4] - r[0]) * 0.01;
+                mx = tot > mx ? tot : mx;
+                n += (double)r[6];
+                g1 += (double)r[7];
+                g2 += (double)r[5];
+            }
+            fprintf(stderr, "[orbx oct] L%d keys %.0f | gather %.1f passes %.1f (%.1f it) final %.1f (%.1f it) out %.1f | max %.1f us\n",
+                    l, n / batch, ph[0] / batch, ph[1] / batch, g1 / batch, ph[2] / batch, (g2 - g1) / batch,
+                    ph[3] / batch, mx);
+        }
+    }
     if (ex->timing) ex->ncalls++;
     ex->last_batch = batch;
     ex->have_pyramid = true;

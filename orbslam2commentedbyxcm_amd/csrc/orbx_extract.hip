@@ -12,6 +12,8 @@
 // which follow the reference's float expression order (built -ffp-contract=off).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "orbx_kernels.h"
 
 namespace orbx {
@@ -570,6 +572,22 @@ __device__ __forceinline__ void child_box(int q, int x0, int y0, int x1, int y1,
 // ------------------------------------------------------------------ octree
 
 // Node list, stored in list order (front first).  Two buffers, swapped every step.
+constexpr int kOctKeysReg = 24 * 256;  // keys per level held in registers by k_octree
+
+// atomicAdd(&a[idx], 1) for the active lanes, one atomic per distinct idx of the wave
+// (the early octree passes send thousands of keys to a handful of counters).
+__device__ __forceinline__ void wave_count(int* a, int idx) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long act = __ballot(1);
+    while (act) {
+        const int leader = __ffsll((long long)act) - 1;
+        const int t = __builtin_amdgcn_readlane(idx, leader);
+        const unsigned long long m = __ballot(idx == t);
+        if (lane == leader) atomicAdd(&a[t], __popcll(m));
+        act &= ~m;
+    }
+}
+
 struct NodeBuf {
     int16_t *x0, *y0, *x1, *y1;
     int* cnt;
@@ -596,17 +614,20 @@ __global__ __launch_bounds__(256) void k_octree(const LevelGeom* __restrict__ lv
                                                 uint32_t* __restrict__ keys, int* __restrict__ key_node,
                                                 int keys_pf, uint32_t* __restrict__ kept, int kept_pf,
                                                 int* __restrict__ kept_count, int* __restrict__ status,
-                                                int NC, int nframes) {
+                                                int NC, int nframes, unsigned long long* __restrict__ stamps) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_tmp[8];
     __shared__ int s_scal[16];
     __shared__ int s_off[256];
+    __shared__ int s_src[256];
     __shared__ int s_map[kMaxIni];
     __shared__ int s_icnt[kMaxIni];
 
     int f, l;
     xcd_frame_block(L, nframes, f, l);
     const int tid = threadIdx.x;
+    unsigned long long* st = stamps ? stamps + 8 * ((size_t)f * L + l) : nullptr;
+    if (st && tid == 0) st[0] = wall_clock64();
     const int lane = tid & 63, wave = tid >> 6;
     const LevelGeom& g = lv[l];
     const int N = g.N;
@@ -621,59 +642,125 @@ __global__ __launch_bounds__(256) void k_octree(const LevelGeom* __restrict__ lv
     int* crkb = cntb + 2 * NC;                                          // 2*NC
     int16_t* boxb = (int16_t*)(crkb + 2 * NC);                          // 8*NC
     uint8_t* inVb = (uint8_t*)(boxb + 8 * NC);                          // 2*NC
-    NodeBuf nb[2];
-    for (int b = 0; b < 2; b++) {
-        nb[b].x0 = boxb + (4 * b + 0) * NC;
-        nb[b].y0 = boxb + (4 * b + 1) * NC;
-        nb[b].x1 = boxb + (4 * b + 2) * NC;
-        nb[b].y1 = boxb + (4 * b + 3) * NC;
-        nb[b].cnt = cntb + b * NC;
-        nb[b].crank = crkb + b * NC;
-        nb[b].inV = inVb + b * NC;
-    }
+    NodeBuf nb0, nb1;
+    nb0.x0 = boxb;
+    nb0.y0 = boxb + NC;
+    nb0.x1 = boxb + 2 * NC;
+    nb0.y1 = boxb + 3 * NC;
+    nb0.cnt = cntb;
+    nb0.crank = crkb;
+    nb0.inV = inVb;
+    nb1.x0 = boxb + 4 * NC;
+    nb1.y0 = boxb + 5 * NC;
+    nb1.x1 = boxb + 6 * NC;
+    nb1.y1 = boxb + 7 * NC;
+    nb1.cnt = cntb + NC;
+    nb1.crank = crkb + NC;
+    nb1.inV = inVb + NC;
 
     uint32_t* K = keys + (size_t)f * keys_pf + g.key_off;
     int* KN = key_node + (size_t)f * keys_pf + g.key_off;
 
     // ---- 1. gather candidates in cell order (vToDistributeKeys, cc:1054-1122)
+    // 256 cells at a time: offsets by a block scan, then the chunk's keys are copied
+    // flat (key t of the chunk finds its cell by binary search over the offsets), so
+    // every thread has several independent loads in flight.
     int n = 0;
+    const uint32_t* fslots = slots + (size_t)f * slots_pf;
     for (int cb = 0; cb < g.ncells; cb += 256) {
         const int nc = g.ncells - cb < 256 ? g.ncells - cb : 256;
-        if (tid < nc) s_off[tid] = cell_count[(size_t)f * ncells_total + g.cell_first + cb + tid];
+        if (tid < nc) {
+            s_off[tid] = cell_count[(size_t)f * ncells_total + g.cell_first + cb + tid];
+            s_src[tid] = cells[g.cell_first + cb + tid].slot_off;
+        }
         __syncthreads();
         const int tot = block_exscan(s_off, nc, s_tmp);
-        for (int k = wave; k < nc; k += 4) {
-            const CellGeom& c = cells[g.cell_first + cb + k];
-            const uint32_t* src = slots + (size_t)f * slots_pf + c.slot_off;
-            const int cnt = (k + 1 < nc ? s_off[k + 1] : tot) - s_off[k];
-            for (int i = lane; i < cnt; i += 64) K[n + s_off[k] + i] = src[i];
+        for (int t0 = 0; t0 < tot; t0 += 4 * 256) {
+            uint32_t v[4];
+            int dst[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int t = t0 + u * 256 + tid;
+                int lo = 0, hi = nc - 1;  // last cell with s_off <= t
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (s_off[mid] <= t) lo = mid;
+                    else hi = mid - 1;
+                }
+                const int tc = t < tot ? t : tot - 1;
+                dst[u] = t < tot ? n + t : -1;
+                v[u] = fslots[s_src[lo] + (tc - s_off[lo])];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (dst[u] >= 0) K[dst[u]] = v[u];
         }
         n += tot;
         __syncthreads();
     }
     __threadfence_block();
+    __syncthreads();
+    if (st && tid == 0) {
+        st[1] = wall_clock64();
+        st[6] = n;
+    }
+
+    // The per-key state (packed key, node) of key k lives with thread k % 256 for the
+    // whole distribution: in registers when the level has at most kOctKeysReg keys
+    // (REG), otherwise in global memory.
+    auto tail = [&](auto reg_tag) {
+    constexpr bool REG = decltype(reg_tag)::value;
+    constexpr int KPT = REG ? kOctKeysReg / 256 : 1;
+    uint32_t kr[KPT];
+    int nr[KPT];
+    if (REG) {
+#pragma unroll
+        for (int i = 0; i < KPT; i++) {
+            const int k = min(tid + 256 * i, n - 1);
+            kr[i] = n > 0 ? K[k] : 0u;
+            nr[i] = 0;
+        }
+    }
+#define FOR_KEYS(BODY)                                                      \
+    if (REG) {                                                              \
+        _Pragma("unroll") for (int i_ = 0; i_ < KPT; i_++) {                \
+            const int k = tid + 256 * i_;                                   \
+            if (k < n) {                                                    \
+                const uint32_t KK = kr[i_];                                 \
+                int& NN = nr[i_];                                           \
+                BODY                                                        \
+            }                                                               \
+        }                                                                   \
+    } else {                                                                \
+        for (int k = tid; k < n; k += 256) {                                \
+            const uint32_t KK = K[k];                                       \
+            int NN = KN[k];                                                 \
+            BODY                                                            \
+            KN[k] = NN;                                                     \
+        }                                                                   \
+    }
 
     // ---- 2. root nodes (cc:674-742)
     if (tid < g.nIni) s_icnt[tid] = 0;
     __syncthreads();
-    for (int k = tid; k < n; k += 256) {
-        const int idx = (int)((float)key_x(K[k]) / g.hX);
-        atomicAdd(&s_icnt[idx], 1);
-        KN[k] = idx;
-    }
+    FOR_KEYS({
+        const int idx = (int)((float)key_x(KK) / g.hX);
+        wave_count(s_icnt, idx);
+        NN = idx;
+    })
     __syncthreads();
     if (tid == 0) {
         int j = 0;
         for (int i = 0; i < g.nIni; i++) {
             if (s_icnt[i] > 0) {
                 s_map[i] = j;
-                nb[0].x0[j] = (int16_t)g.ini_x0[i];
-                nb[0].x1[j] = (int16_t)g.ini_x0[i + 1];
-                nb[0].y0[j] = 0;
-                nb[0].y1[j] = (int16_t)g.height_rel;
-                nb[0].cnt[j] = s_icnt[i];
-                nb[0].crank[j] = i;
-                nb[0].inV[j] = 0;
+                nb0.x0[j] = (int16_t)g.ini_x0[i];
+                nb0.x1[j] = (int16_t)g.ini_x0[i + 1];
+                nb0.y0[j] = 0;
+                nb0.y1[j] = (int16_t)g.height_rel;
+                nb0.cnt[j] = s_icnt[i];
+                nb0.crank[j] = i;
+                nb0.inV[j] = 0;
                 j++;
             } else {
                 s_map[i] = -1;
@@ -682,7 +769,7 @@ __global__ __launch_bounds__(256) void k_octree(const LevelGeom* __restrict__ lv
         s_scal[0] = j;  // size
     }
     __syncthreads();
-    for (int k = tid; k < n; k += 256) KN[k] = s_map[KN[k]];
+    FOR_KEYS({ NN = s_map[NN]; })
     __syncthreads();
 
     int cur = 0;
@@ -694,22 +781,23 @@ __global__ __launch_bounds__(256) void k_octree(const LevelGeom* __restrict__ lv
     // ---- 3. full passes (cc:758-873)
     while (!finish && !final_phase) {
         if (++guard > 64) { if (tid == 0) atomicOr(&status[f], kStatusIterations); break; }
-        const NodeBuf& A = nb[cur];
-        const NodeBuf& B = nb[cur ^ 1];
+        const NodeBuf& A = cur ? nb1 : nb0;
+        const NodeBuf& B = cur ? nb0 : nb1;
         const int prev = size;
         for (int j = tid; j < size; j += 256) {
             ccnt[4 * j] = ccnt[4 * j + 1] = ccnt[4 * j + 2] = ccnt[4 * j + 3] = 0;
         }
         if (tid == 0) s_scal[1] = 0;
         __syncthreads();
-        for (int k = tid; k < n; k += 256) {
-            const int nd = KN[k];
+        const bool few = size <= 64;
+        FOR_KEYS({
+            const int nd = NN;
             if (A.cnt[nd] >= 2) {
-                const uint32_t kk = K[k];
-                const int q = quadrant(key_x(kk), key_y(kk), A.x0[nd], A.y0[nd], A.x1[nd], A.y1[nd]);
-                atomicAdd(&ccnt[4 * nd + q], 1);
+                const int q = quadrant(key_x(KK), key_y(KK), A.x0[nd], A.y0[nd], A.x1[nd], A.y1[nd]);
+                if (few) wave_count(ccnt, 4 * nd + q);
+                else atomicAdd(&ccnt[4 * nd + q], 1);
             }
-        }
+        })
         __syncthreads();
         int g2 = 0;
         for (int j = tid; j < size; j += 256) {
@@ -766,16 +854,15 @@ __global__ __launch_bounds__(256) void k_octree(const LevelGeom* __restrict__ lv
             }
         }
         __syncthreads();
-        for (int k = tid; k < n; k += 256) {
-            const int nd = KN[k];
+        FOR_KEYS({
+            const int nd = NN;
             if (A.cnt[nd] >= 2) {
-                const uint32_t kk = K[k];
-                const int q = quadrant(key_x(kk), key_y(kk), A.x0[nd], A.y0[nd], A.x1[nd], A.y1[nd]);
-                KN[k] = ccnt[4 * nd + q];
+                const int q = quadrant(key_x(KK), key_y(KK), A.x0[nd], A.y0[nd], A.x1[nd], A.y1[nd]);
+                NN = ccnt[4 * nd + q];
             } else {
-                KN[k] = sb[nd];
+                NN = sb[nd];
             }
-        }
+        })
         __syncthreads();
         cur ^= 1;
         size = nsize;
@@ -785,42 +872,50 @@ __global__ __launch_bounds__(256) void k_octree(const LevelGeom* __restrict__ lv
             final_phase = true;
     }
 
+    if (st && tid == 0) {
+        st[2] = wall_clock64();
+        st[7] = guard;
+    }
     // ---- 4. final phase (cc:888-971)
     while (!finish && final_phase) {
         if (++guard > 4096) { if (tid == 0) atomicOr(&status[f], kStatusIterations); break; }
-        const NodeBuf& A = nb[cur];
-        const NodeBuf& B = nb[cur ^ 1];
+        const NodeBuf& A = cur ? nb1 : nb0;
+        const NodeBuf& B = cur ? nb0 : nb1;
         const int prev = size;
         // processing order: vPrev sorted ascending by (size, address), walked from the back
         if (tid == 0) s_scal[2] = 0;
         __syncthreads();
         int nvloc = 0;
+        // order key of vPrev members: (size, creation rank) + 1, 0 for the others
+        // (`best` is free until phase 5)
+        for (int j = tid; j < size; j += 256)
+            best[j] = A.inV[j] ? (((unsigned long long)A.cnt[j] << 32) | (unsigned)A.crank[j]) + 1 : 0ull;
+        __syncthreads();
         for (int j = tid; j < size; j += 256) {
             sc[j] = -1;  // rank of node j in processing order, -1 if not in vPrev
-            if (A.inV[j]) {
+            const unsigned long long kj = best[j];
+            if (kj) {
                 nvloc++;
-                const int cj = A.cnt[j], rj = A.crank[j];
                 int r = 0;
-                for (int i = 0; i < size; i++)
-                    if (A.inV[i] && (A.cnt[i] > cj || (A.cnt[i] == cj && A.crank[i] > rj))) r++;
+                for (int i = 0; i < size; i++) r += best[i] > kj;
                 sc[j] = r;
             }
             ccnt[4 * j] = ccnt[4 * j + 1] = ccnt[4 * j + 2] = ccnt[4 * j + 3] = 0;
         }
+        __syncthreads();
         if (nvloc) atomicAdd(&s_scal[2], nvloc);
         __syncthreads();
         const int nv = s_scal[2];
         if (nv == 0) { finish = true; break; }
         for (int j = tid; j < size; j += 256)
             if (sc[j] >= 0) sa[sc[j]] = j;  // sa[r] = node processed r-th
-        for (int k = tid; k < n; k += 256) {
-            const int nd = KN[k];
+        FOR_KEYS({
+            const int nd = NN;
             if (A.inV[nd]) {
-                const uint32_t kk = K[k];
-                const int q = quadrant(key_x(kk), key_y(kk), A.x0[nd], A.y0[nd], A.x1[nd], A.y1[nd]);
+                const int q = quadrant(key_x(KK), key_y(KK), A.x0[nd], A.y0[nd], A.x1[nd], A.y1[nd]);
                 atomicAdd(&ccnt[4 * nd + q], 1);
             }
-        }
+        })
         __syncthreads();
         // sb[r] = ne of the r-th processed node
         for (int r = tid; r < nv; r += 256) {
@@ -896,29 +991,30 @@ __global__ __launch_bounds__(256) void k_octree(const LevelGeom* __restrict__ lv
             }
         }
         __syncthreads();
-        for (int k = tid; k < n; k += 256) {
-            const int nd = KN[k];
+        FOR_KEYS({
+            const int nd = NN;
             if (sc[nd] >= 0) {
-                const uint32_t kk = K[k];
-                const int q = quadrant(key_x(kk), key_y(kk), A.x0[nd], A.y0[nd], A.x1[nd], A.y1[nd]);
-                KN[k] = ccnt[4 * nd + q];
+                const int q = quadrant(key_x(KK), key_y(KK), A.x0[nd], A.y0[nd], A.x1[nd], A.y1[nd]);
+                NN = ccnt[4 * nd + q];
             } else {
-                KN[k] = sa[nd];
+                NN = sa[nd];
             }
-        }
+        })
         __syncthreads();
         cur ^= 1;
         size = nsize;
         if (size >= N || size == prev) finish = true;
     }
 
+    if (st && tid == 0) st[3] = wall_clock64();
     // ---- 5. best key per node (cc:984-1009)
     for (int j = tid; j < size; j += 256) best[j] = 0ull;
     __syncthreads();
-    for (int k = tid; k < n; k += 256) {
-        const unsigned long long v = ((unsigned long long)key_resp(K[k]) << 32) | (0xffffffffu - (unsigned)k);
-        atomicMax(&best[KN[k]], v);
-    }
+    FOR_KEYS({
+        const unsigned long long v = ((unsigned long long)key_resp(KK) << 32) | (0xffffffffu - (unsigned)k);
+        atomicMax(&best[NN], v);
+    })
+#undef FOR_KEYS
     __syncthreads();
     const int outn = size < g.ncap ? size : g.ncap;
     uint32_t* out = kept + (size_t)f * kept_pf + g.out_off;
@@ -929,7 +1025,14 @@ __global__ __launch_bounds__(256) void k_octree(const LevelGeom* __restrict__ lv
     if (tid == 0) {
         kept_count[(size_t)f * L + l] = outn;
         if (size > g.ncap) atomicOr(&status[f], kStatusNodeOverflow);
+        if (st) {
+            st[4] = wall_clock64();
+            st[5] = guard;
+        }
     }
+    };
+    if (n <= kOctKeysReg) tail(std::true_type{});
+    else tail(std::false_type{});
 }
 
 // ------------------------------------------------------------------ angle + descriptor
@@ -1125,7 +1228,7 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
         dim3 grid(L * batch);
         hipLaunchKernelGGL(k_octree, grid, dim3(256), lds, stream, db.lv, L, db.slots, plan.slots_per_frame,
                            db.cells, db.cell_count, ncells, db.keys, db.key_node, plan.keys_per_frame,
-                           db.kept, plan.kept_per_frame, db.kept_count, db.status, NC, batch);
+                           db.kept, plan.kept_per_frame, db.kept_count, db.status, NC, batch, db.oct_stamps);
     }
     if (ev) (void)hipEventRecord(ev[4], stream);
     {

@@ -25,6 +25,7 @@ struct DeviceBuffers {
     uint32_t* kept = nullptr;        // [B][kept_per_frame] kept keypoints (octree list order)
     int* kept_count = nullptr;       // [B][L]
     int* status = nullptr;           // [B] error flags
+    unsigned long long* oct_stamps = nullptr;  // [B][L][8] k_octree phase stamps (ORBX_OCT_STAMPS)
 };
 
 // Kernel status bits (DeviceBuffers::status)
