@@ -12,6 +12,7 @@
 // which follow the reference's float expression order (built -ffp-contract=off).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "orbx_kernels.h"
@@ -412,107 +413,115 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
 // strength map M (corner iff M > t, score M - 1).  FAST_t's non-max suppression over
 // the 8-neighbourhood, where neighbours outside the cell's detection window or below
 // the threshold score 0, keeps a corner p iff M_p > t, M_p >= 2 and M_p exceeds every
-// in-window neighbour's M (a neighbour with M_n >= M_p > t always suppresses; one
-// below M_p never does) -- threshold-independent apart from M_p > t.  So one sweep
-// over the window rows (lane = column, horizontal neighbours by DPP lane shifts,
-// vertical ones rolled in registers) yields the keep masks of both thresholds; each
-// row's two ballots are parked in lane `row` of four VGPRs.  Survivors are written in
-// raster order.
-__device__ __forceinline__ int lane_from_left(int v) {   // v of lane-1 (0 at lane 0)
-    return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, false);  // wave_shr:1
-}
-__device__ __forceinline__ int lane_from_right(int v) {  // v of lane+1 (0 at lane 63)
-    return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xF, 0xF, false);  // wave_shl:1
-}
-
+// in-window neighbour's M (a neighbour with M_n >= M_p > t always suppresses; one below
+// M_p never does) -- threshold-independent apart from M_p > t.  M is sparse (k_level_tiles
+// zeroes M <= min(iniTh, minTh)), so the wave lists the window's non-zero pixels in
+// raster order (one ballot per row), tests only those against their neighbours, and
+// writes the survivors of the chosen threshold in the same order.
 __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ score, long long fb,
-                                                    const LevelGeom* __restrict__ lv,
                                                     const CellGeom* __restrict__ cells, int ncells,
                                                     int ini_th, int min_th, uint32_t* __restrict__ slots,
-                                                    int slots_pf, int* __restrict__ cell_count, int nframes) {
-    __shared__ uint8_t s_m[4][kCellMax][64];
+                                                    int slots_pf, int* __restrict__ cell_count, int nframes,
+                                                    int max_wr, int max_wc) {
+    // per wave: max_wr rows x 64 bytes of M, then a candidate list of max_wr*max_wc u16
+    extern __shared__ __align__(16) uint8_t s_dyn[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int per_wave = ((max_wr * 64 + 2 * max_wr * max_wc) + 15) & ~15;
     int f, cb;
     xcd_frame_block((ncells + 3) / 4, nframes, f, cb);
     const int ci = cb * 4 + wave;
     if (ci >= ncells) return;  // whole wave exits; no block barriers below
     const CellGeom c = cells[ci];
-    const LevelGeom& g = lv[c.level];
     const int wr = c.rows - 6, wc = c.cols - 6;  // detection window [3,rows-3) x [3,cols-3)
     int count = 0;
     if (wr > 0 && wc > 0) {
-        const uint8_t* src = score + (size_t)f * fb + g.off + (size_t)(c.y0 + 3) * g.pitch + c.x0 + 3;
-        uint8_t(*m)[64] = s_m[wave];
+        const int ti = ini_th < 0 ? 0 : (ini_th > 255 ? 255 : ini_th);
+        const int tm = min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th);
+        const int tc = max(min(ti, tm), 1);  // candidates: M > tc
+        const uint8_t* src = score + (size_t)f * fb + c.src_off;
+        uint8_t(*m)[64] = (uint8_t(*)[64])(s_dyn + wave * per_wave);
+        uint16_t* list = (uint16_t*)(s_dyn + wave * per_wave + max_wr * 64);
         const bool act = lane < wc;
-        // 16 rows of loads in flight at a time (unconditional loads from clamped
-        // addresses, so the compiler does not serialise load -> LDS store per row)
+        const unsigned long long below = (1ull << lane) - 1;
+        int n = 0;
+        // 16 rows of loads in flight at a time (unconditional loads from clamped addresses)
         for (int r0 = 0; r0 < wr; r0 += 16) {
             int v[16];
 #pragma unroll
             for (int k = 0; k < 16; k++) {
                 const bool ok = act && r0 + k < wr;
-                v[k] = src[ok ? (size_t)(r0 + k) * g.pitch + lane : 0];
+                v[k] = src[ok ? (size_t)(r0 + k) * c.pitch + lane : 0];
                 v[k] = ok ? v[k] : 0;
             }
 #pragma unroll
-            for (int k = 0; k < 16; k++)
-                if (r0 + k < wr) m[r0 + k][lane] = (uint8_t)v[k];
+            for (int k = 0; k < 16; k++) {
+                const int r = r0 + k;
+                if (r < wr) {
+                    m[r][lane] = (uint8_t)v[k];
+                    const unsigned long long b = __ballot(v[k] > tc);
+                    if ((b >> lane) & 1ull) list[n + __popcll(b & below)] = (uint16_t)((r << 8) | lane);
+                    n += __popcll(b);
+                }
+            }
         }
         wave_lds_fence();
-        const int ti = ini_th < 0 ? 0 : (ini_th > 255 ? 255 : ini_th);
-        const int tm = min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th);
-        int vc = m[0][lane];
-        int vn = wr > 1 ? m[1][lane] : 0;
-        int hp = 0;                                                    // row r-1: max of c-1, c, c+1
-        int hc = max(max(lane_from_left(vc), lane_from_right(vc)), vc);  // row r
-        unsigned ki_lo = 0, ki_hi = 0, km_lo = 0, km_hi = 0;           // lane r: row r's keep masks
+        // neighbour test of the candidates, counts at both thresholds
         int cnt_i = 0, cnt_m = 0;
-        for (int r = 0; r < wr; r++) {
-            const int vnn = r + 2 < wr ? m[r + 2][lane] : 0;
-            const int ln = lane_from_left(vn), rn = lane_from_right(vn);
-            const int hn = max(max(ln, rn), vn);
-            const int nb = max(max(hp, hn), max(lane_from_left(vc), lane_from_right(vc)));
-            const bool lm = act && vc >= 2 && vc > nb;
-            const unsigned long long bi = __ballot(lm && vc > ti);
-            const unsigned long long bm = __ballot(lm && vc > tm);
-            cnt_i += __popcll(bi);
-            cnt_m += __popcll(bm);
-            if (lane == r) {
-                ki_lo = (unsigned)bi;
-                ki_hi = (unsigned)(bi >> 32);
-                km_lo = (unsigned)bm;
-                km_hi = (unsigned)(bm >> 32);
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            bool ki = false, km = false;
+            const int i = i0 + lane;
+            if (i < n) {
+                const int rc = list[i], r = rc >> 8, col = rc & 255;
+                const int M = m[r][col];
+                int nb = 0;
+#pragma unroll
+                for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+                    for (int dx = -1; dx <= 1; dx++) {
+                        if (dx == 0 && dy == 0) continue;
+                        const int rr = r + dy, cc = col + dx;
+                        if (rr >= 0 && rr < wr && cc >= 0 && cc < wc) nb = max(nb, (int)m[rr][cc]);
+                    }
+                const bool lm = M > nb;  // M > tc >= 1, so M >= 2
+                ki = lm && M > ti;
+                km = lm && M > tm;
             }
-            hp = hc;
-            hc = hn;
-            vc = vn;
-            vn = vnn;
+            cnt_i += __popcll(__ballot(ki));
+            cnt_m += __popcll(__ballot(km));
         }
         const bool use_ini = cnt_i > 0;
         count = use_ini ? cnt_i : cnt_m;
+        const int t = use_ini ? ti : tm;
         if (count > 0) {
-            const unsigned klo = use_ini ? ki_lo : km_lo, khi = use_ini ? ki_hi : km_hi;
-            const int pc = lane < wr ? __popc(klo) + __popc(khi) : 0;
-            int incl = pc;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int y = __shfl_up(incl, o);
-                if (lane >= o) incl += y;
-            }
-            const int excl = incl - pc;
             uint32_t* out = slots + (size_t)f * slots_pf + c.slot_off;
-            const unsigned long long below = (1ull << lane) - 1;
-            const int xr = c.x0 + 3 + lane - kMinBorder;  // relative to minBorderX
-            for (int r = 0; r < wr; r++) {
-                const unsigned long long mask = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)khi, r) << 32) |
-                                                (unsigned)__builtin_amdgcn_readlane((int)klo, r);
-                if (!mask) continue;
-                if ((mask >> lane) & 1ull) {
-                    const int idx = __builtin_amdgcn_readlane(excl, r) + __popcll(mask & below);
-                    const int yr = c.y0 + 3 + r - kMinBorder;
-                    const int resp = m[r][lane] - 1;
-                    out[idx] = (uint32_t)xr | ((uint32_t)yr << 12) | ((uint32_t)resp << 24);
+            int base = 0;
+            for (int i0 = 0; i0 < n; i0 += 64) {
+                const int i = i0 + lane;
+                bool keep = false;
+                int r = 0, col = 0, M = 0;
+                if (i < n) {
+                    const int rc = list[i];
+                    r = rc >> 8;
+                    col = rc & 255;
+                    M = m[r][col];
+                    int nb = 0;
+#pragma unroll
+                    for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+                        for (int dx = -1; dx <= 1; dx++) {
+                            if (dx == 0 && dy == 0) continue;
+                            const int rr = r + dy, cc = col + dx;
+                            if (rr >= 0 && rr < wr && cc >= 0 && cc < wc) nb = max(nb, (int)m[rr][cc]);
+                        }
+                    keep = M > nb && M > t;
                 }
+                const unsigned long long b = __ballot(keep);
+                if (keep) {
+                    const int xr = c.x0 + 3 + col - kMinBorder;  // relative to minBorderX
+                    const int yr = c.y0 + 3 + r - kMinBorder;
+                    out[base + __popcll(b & below)] = (uint32_t)xr | ((uint32_t)yr << 12) | ((uint32_t)(M - 1) << 24);
+                }
+                base += __popcll(b);
             }
         }
     }
@@ -1218,8 +1227,10 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     if (ev) (void)hipEventRecord(ev[2], stream);
     {
         dim3 grid(((ncells + 3) / 4) * batch);
-        hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), 0, stream, db.score, fb, db.lv, db.cells, ncells,
-                           plan.prm.ini_th, plan.prm.min_th, db.slots, plan.slots_per_frame, db.cell_count, batch);
+        const size_t fc_lds = 4 * (size_t)(((plan.fc_wr * 64 + 2 * plan.fc_wr * plan.fc_wc) + 15) & ~15);
+        hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), fc_lds, stream, db.score, fb, db.cells, ncells,
+                           plan.prm.ini_th, plan.prm.min_th, db.slots, plan.slots_per_frame, db.cell_count, batch,
+                           plan.fc_wr, plan.fc_wc);
     }
     if (ev) (void)hipEventRecord(ev[3], stream);
     {

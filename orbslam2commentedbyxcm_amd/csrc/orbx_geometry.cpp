@@ -1,6 +1,7 @@
 // orbx_geometry.cpp -- host-side extraction plan (see orbx_geometry.h).
 // Compiled with -ffp-contract=off: every float expression below restates a
 // reference expression operation by operation.
+#include <algorithm>
 #include "orbx_geometry.h"
 
 #include <cmath>
@@ -158,6 +159,10 @@ bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
                 if (wc > kCellMax || wr > kCellMax) { plan.why = "FAST cell wider than 64 px"; return false; }
                 c.slot_off = slot_off;
                 c.slot_cap = ((wc + 1) / 2) * ((wr + 1) / 2);
+                c.pitch = g.pitch;
+                plan.fc_wr = std::max(plan.fc_wr, wr);
+                plan.fc_wc = std::max(plan.fc_wc, wc);
+                c.src_off = (int)(g.off + (long long)(c.y0 + 3) * g.pitch + c.x0 + 3);
                 slot_off += c.slot_cap;
                 level_cap += c.slot_cap;
                 plan.cells.push_back(c);

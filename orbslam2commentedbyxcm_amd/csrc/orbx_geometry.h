@@ -65,7 +65,8 @@ struct CellGeom {
     int x0, y0, cols, rows;
     int slot_off;          // offset of this cell's candidate slots in the frame's slot array
     int slot_cap;
-    int pad;
+    int src_off;           // level.off + (y0 + 3) * pitch + x0 + 3: detection window origin in a frame block
+    int pitch;             // level row pitch
 };
 
 // k_resize output tile and its LDS budget for the staged source region
@@ -84,6 +85,7 @@ struct Plan {
     int kept_per_frame = 0;         // sum of ncap
     int tiles_total = 0;            // blur tiles per frame
     int rz_sw = 0, rz_sh = 0;       // largest staged resize source region (bytes x rows)
+    int fc_wr = 0, fc_wc = 0;       // largest FAST detection window (rows, cols)
     int max_ncap = 0;
     int max_key_cap = 0;
     bool ok = false;
