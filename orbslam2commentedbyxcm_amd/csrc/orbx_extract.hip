@@ -191,16 +191,21 @@ __device__ __forceinline__ int fast_strength(const uint8_t* c, int pitch) {
         const int x = c[off[k]];
         d[k] = V - __builtin_bit_cast(short2_t, (int)(x - (x << 16)));       // (v - x, x - v)
     }
-    short2_t m2[16], m4[16];
+    // For odd j, m8[j] = min(d[j..j+7]) serves two arcs: [j-1, j+7] and [j, j+8]
+    // (55 packed min/max instead of 79 for all 16 arcs independently).
+    short2_t m2[8], m4[8], m8[8];
 #pragma unroll
-    for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(d[k], d[(k + 1) & 15]);
+    for (int i = 0; i < 8; i++) m2[i] = __builtin_elementwise_min(d[2 * i + 1], d[(2 * i + 2) & 15]);
 #pragma unroll
-    for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
-    short2_t best = __builtin_elementwise_min(__builtin_elementwise_min(m4[0], m4[4]), d[8]);
+    for (int i = 0; i < 8; i++) m4[i] = __builtin_elementwise_min(m2[i], m2[(i + 1) & 7]);
 #pragma unroll
-    for (int k = 1; k < 16; k++) {
-        const short2_t m9 = __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]), d[(k + 8) & 15]);
-        best = __builtin_elementwise_max(best, m9);
+    for (int i = 0; i < 8; i++) m8[i] = __builtin_elementwise_min(m4[i], m4[(i + 2) & 7]);
+    short2_t best = __builtin_elementwise_min(m8[0], d[0]);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int j = 2 * i + 1;
+        if (i > 0) best = __builtin_elementwise_max(best, __builtin_elementwise_min(m8[i], d[j - 1]));
+        best = __builtin_elementwise_max(best, __builtin_elementwise_min(m8[i], d[(j + 8) & 15]));
     }
     const int M = best.x > best.y ? best.x : best.y;
     return M > 0 ? M : 0;
@@ -216,9 +221,23 @@ constexpr int kSW = kTW + 8;       // staged row: image columns X0-4 .. X0+67
 
 typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
 
-// Bytes [c+dx, c+dx+3] of a row from its aligned dwords at c-4 (lo), c (mid), c+4 (hi).
+// Bytes [c+dx, c+dx+3] of a row from its aligned dwords at c-4 (lo), c (mid), c+4 (hi),
+// dx in [-4, 4].
 __device__ __forceinline__ uint32_t row_bytes(uint32_t lo, uint32_t mid, uint32_t hi, int dx) {
-    return dx < 0 ? __builtin_amdgcn_alignbyte(mid, lo, 4 + dx) : (dx == 0 ? mid : __builtin_amdgcn_alignbyte(hi, mid, dx));
+    return dx == -4 ? lo
+                    : dx < 0 ? __builtin_amdgcn_alignbyte(mid, lo, 4 + dx)
+                             : (dx == 0 ? mid : (dx == 4 ? hi : __builtin_amdgcn_alignbyte(hi, mid, dx)));
+}
+
+// Horizontal 7-tap blur sums (exact, <= 257 * 255) of 4 consecutive pixels as two
+// v_dot4_u32_u8 per pixel: taps 18,34,49,55 on bytes x-3..x, taps 49,34,18 on x+1..x+3.
+__device__ __forceinline__ void blur_row4(uint32_t lo, uint32_t mid, uint32_t hi, uint32_t out[4]) {
+    constexpr uint32_t kW1 = 18u | (34u << 8) | (49u << 16) | (55u << 24);
+    constexpr uint32_t kW2 = 49u | (34u << 8) | (18u << 16);
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        out[j] = __builtin_amdgcn_udot4(row_bytes(lo, mid, hi, j - 3), kW1,
+                                        __builtin_amdgcn_udot4(row_bytes(lo, mid, hi, j + 1), kW2, 0u, false), false);
 }
 // bytes 0,1 / 2,3 of a dword zero-extended into the two 16-bit halves
 __device__ __forceinline__ uint32_t lo_pair(uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c010c00u); }
@@ -242,7 +261,7 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
                                                      const LevelGeom* __restrict__ lv, int L, int tiles_pf,
                                                      int nframes, int tq) {
     __shared__ __align__(16) uint8_t s_in[kTH + 6][kSW];
-    __shared__ __align__(16) uint16_t s_row[kTH + 6][kTW];
+    __shared__ __align__(16) uint32_t s_rowp[(kTH + 6) / 2][kTW];  // (row 2p, row 2p+1) u16 pairs
     __shared__ __align__(16) uint8_t s_m[kTH][kTW];
     __shared__ uint16_t s_list[kTH * kTW];
     __shared__ int s_n;
@@ -290,21 +309,16 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
     if (tid == 0) s_n = 0;
     for (int i = tid; i < kTH * kTW / 4; i += 256) ((uint32_t*)s_m)[i] = 0u;
     __syncthreads();
-    // ---- blur rows: 4 outputs per task, packed u16 multiply-add
-    for (int i = tid; i < (kTH + 6) * (kTW / 4); i += 256) {
-        const int r = i >> 4, c0 = 4 + 4 * (i & 15);
-        const uint32_t* rp = (const uint32_t*)&s_in[r][c0];
-        const uint32_t dlo = rp[-1], dmid = rp[0], dhi = rp[1];
-        ushort2_t a = {0, 0}, b = {0, 0};
-        constexpr unsigned short w7[7] = {18, 34, 49, 55, 49, 34, 18};
-#pragma unroll
-        for (int k = 0; k < 7; k++) {
-            const uint32_t s = row_bytes(dlo, dmid, dhi, k - 3);
-            const ushort2_t wk = {w7[k], w7[k]};
-            a += __builtin_bit_cast(ushort2_t, lo_pair(s)) * wk;
-            b += __builtin_bit_cast(ushort2_t, hi_pair(s)) * wk;
-        }
-        *(uint2*)&s_row[r][c0 - 4] = make_uint2(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b));
+    // ---- blur rows: 2 rows x 4 columns per task (dot4), stored as row-pair u16 dwords
+    for (int i = tid; i < ((kTH + 6) / 2) * (kTW / 4); i += 256) {
+        const int pr = i >> 4, c0 = 4 + 4 * (i & 15);
+        const uint32_t* ra = (const uint32_t*)&s_in[2 * pr][c0];
+        const uint32_t* rb = (const uint32_t*)&s_in[2 * pr + 1][c0];
+        uint32_t a[4], b[4];
+        blur_row4(ra[-1], ra[0], ra[1], a);
+        blur_row4(rb[-1], rb[0], rb[1], b);
+        *(uint4*)&s_rowp[pr][c0 - 4] = make_uint4(a[0] | (b[0] << 16), a[1] | (b[1] << 16), a[2] | (b[2] << 16),
+                                                  a[3] | (b[3] << 16));
     }
     // ---- FAST compass test on the detection area, compaction of the survivors
     for (int i = tid; i < kTH * (kTW / 4); i += 256) {
@@ -365,15 +379,23 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
         const int r = i >> 4, c = 4 * (i & 15);
         const int y = Y0 + r, x = X0 + c;
         if (y >= g.h || x >= g.w) continue;
+        // staged rows r..r+6, as 4 row pairs starting at r (even r) or r-1 (odd r),
+        // one v_dot2_u32_u16 per pair and column
         unsigned s[4] = {0, 0, 0, 0};
-        constexpr unsigned w7[7] = {18, 34, 49, 55, 49, 34, 18};
+        const int p0 = r >> 1;
+        const bool odd = r & 1;
+        const ushort2_t w0 = odd ? ushort2_t{0, 18} : ushort2_t{18, 34};
+        const ushort2_t w1 = odd ? ushort2_t{34, 49} : ushort2_t{49, 55};
+        const ushort2_t w2 = odd ? ushort2_t{55, 49} : ushort2_t{49, 34};
+        const ushort2_t w3 = odd ? ushort2_t{34, 18} : ushort2_t{18, 0};
+        const ushort2_t wk[4] = {w0, w1, w2, w3};
 #pragma unroll
-        for (int k = 0; k < 7; k++) {
-            const uint2 q = *(const uint2*)&s_row[r + k][c];
-            s[0] += w7[k] * (q.x & 0xffffu);
-            s[1] += w7[k] * (q.x >> 16);
-            s[2] += w7[k] * (q.y & 0xffffu);
-            s[3] += w7[k] * (q.y >> 16);
+        for (int k = 0; k < 4; k++) {
+            const uint4 q = *(const uint4*)&s_rowp[p0 + k][c];
+            s[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, q.x), wk[k], s[0], false);
+            s[1] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, q.y), wk[k], s[1], false);
+            s[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, q.z), wk[k], s[2], false);
+            s[3] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, q.w), wk[k], s[3], false);
         }
         uint32_t packed = 0;
 #pragma unroll
