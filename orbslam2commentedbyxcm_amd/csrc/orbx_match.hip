@@ -157,7 +157,9 @@ struct SortedGrid {
 };
 
 constexpr int kProjThreads = 1024;
-constexpr unsigned kNoEntry = 0xffffffffu;
+constexpr int kTopK = 8;                   // candidate-list length per query
+constexpr unsigned kNoEntry = 0xffffffffu;  // no further candidate
+constexpr unsigned kTrunc = 0xfffffffeu;    // further candidates exist but are not listed
 
 // Candidate-list entry: distance << 18 | octave << 13 | sorted position.  Entries of a
 // query are kept in the reference's (distance, iteration order) order.
@@ -207,19 +209,22 @@ __device__ __forceinline__ QueryReg bcast_query(const QueryReg& x, int src) {
     return r;
 }
 
-// The four best candidates of a query (GetFeaturesInArea + the overload's filters)
-// against the current claims sfmp, as entries (kNoEntry = fewer candidates).  One
-// 16-lane row per query, four queries per wave: the row's lanes split the columns of
-// the query's cell window (and the sorted-position runs inside them), keep a local
-// top-4 of (distance << 13 | position) and merge it by DPP row minima.  The
-// candidate windows hold a few to a few tens of keypoints, so a row keeps its lanes
-// busy where a whole wave per query would mostly idle.  `valid` false: no query in
-// this row (out = kNoEntry).  Must be called with the whole wave active.
-__device__ void score_row4(const ProjProblem& pb, const ProjParams& P, const QueryReg& QR, bool valid,
-                           const SortedGrid& G, const int* sfmp, unsigned out[4]) {
+// The kTopK best candidates of a query (GetFeaturesInArea + the overload's filters)
+// against the current claims sfmp, as entries (kNoEntry = no more candidates, kTrunc =
+// more candidates exist than listed).  One 16-lane row per query, four queries per wave:
+// the row's lanes split the columns of the query's cell window (and the sorted-position
+// runs inside them), keep a local top-4 of (distance << 13 | position) and merge them by
+// DPP row minima.  A lane that saw more than 4 candidates only knows its 4 best, so the
+// merged list is exact up to the point where such a lane runs dry; the rest is kTrunc.
+// The candidate windows hold a few to a few tens of keypoints, so a row keeps its lanes
+// busy where a whole wave per query would mostly idle.  `valid` false: no query in this
+// row (out = kNoEntry).  Must be called with the whole wave active.
+__device__ void score_rowk(const ProjProblem& pb, const ProjParams& P, const QueryReg& QR, bool valid,
+                           const SortedGrid& G, const int* sfmp, unsigned out[kTopK]) {
     const int r = threadIdx.x & 15;
     const ProjQuery& Q = QR.q;
     unsigned k[4] = {kNoEntry, kNoEntry, kNoEntry, kNoEntry};
+    int seen = 0;
     if (valid) {
         const CellRange cr = cell_range(pb, Q.u, Q.v, Q.r);
         if (!cr.empty) {
@@ -268,6 +273,7 @@ __device__ void score_row4(const ProjProblem& pb, const ProjParams& P, const Que
                         d = __popcll(q0 ^ tt[0]) + __popcll(q1 ^ tt[1]) + __popcll(q2 ^ tt[2]) + __popcll(q3 ^ tt[3]);
                     }
                     const unsigned key = ((unsigned)d << 13) | (unsigned)p;
+                    seen++;
                     if (key < k[3]) {
                         if (key < k[2]) {
                             k[3] = k[2];
@@ -282,10 +288,16 @@ __device__ void score_row4(const ProjProblem& pb, const ProjParams& P, const Que
             }
         }
     }
-    // Row top-4: keys are unique (distinct positions), so one lane pops each minimum.
-    unsigned m[4];
+    // Row top-kTopK: keys are unique (distinct positions), so one lane pops each minimum.
+    const int rsh = threadIdx.x & 48;  // first lane of this row
+    bool over = seen > 4;
+    bool trunc = false;
+    unsigned m[kTopK];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
+    for (int j = 0; j < kTopK; j++) {
+        // a lane whose listed candidates are used up but that saw more makes the rest unknown
+        const unsigned long long dry = __ballot(over && k[0] == kNoEntry);
+        trunc = trunc || ((dry >> rsh) & 0xffffull) != 0;
         m[j] = row_min_u32(k[0]);
         if (k[0] == m[j] && m[j] != kNoEntry) {
             k[0] = k[1];
@@ -293,12 +305,13 @@ __device__ void score_row4(const ProjProblem& pb, const ProjParams& P, const Que
             k[2] = k[3];
             k[3] = kNoEntry;
         }
+        if (trunc) m[j] = kTrunc;
     }
 #pragma unroll
-    for (int j = 0; j < 4; j++)
-        out[j] = m[j] == kNoEntry ? kNoEntry
-                                  : ((m[j] >> 13) << 18) | ((unsigned)__float_as_int(G.skp[m[j] & 0x1fffu].z) << 13) |
-                                        (m[j] & 0x1fffu);
+    for (int j = 0; j < kTopK; j++)
+        out[j] = m[j] >= kTrunc ? m[j]
+                                : ((m[j] >> 13) << 18) | ((unsigned)__float_as_int(G.skp[m[j] & 0x1fffu].z) << 13) |
+                                      (m[j] & 0x1fffu);
 }
 
 // Ascending in-place bitonic sort of n2 (power of two) u32 keys by the workgroup.
@@ -336,7 +349,7 @@ struct ProjLds {
         sdesc = o;
         if (dlds) o += (size_t)n * 32;
         qk = o;
-        qmp = qk + (size_t)nq * 16;
+        qmp = qk + (size_t)nq * 4 * kTopK;
         qang = qmp + (size_t)nq * 4;
         mlist = qang + (size_t)nq * 4;
         mbin = mlist + (size_t)nq * 4;
@@ -393,7 +406,7 @@ __global__ __launch_bounds__(kProjThreads) void k_proj_search(const ProjProblem*
     } else {
         unsigned long long* g = scratch + scratch_off[blockIdx.x];
         qk = (uint4*)g;
-        qmp = (int*)(g + 2 * (size_t)nq);
+        qmp = (int*)(g + 4 * (size_t)nq);
         qang = (float*)(qmp + nq);
         mlist = (int*)(qang + nq);
         mbin = mlist + nq;
@@ -445,10 +458,11 @@ __global__ __launch_bounds__(kProjThreads) void k_proj_search(const ProjProblem*
             QueryReg nxt;
             if (qb + kStep < nq) nxt = load_query(pb, min(q + kStep, nq - 1));  // prefetch
             const int mp = q < nq ? cur.q.mp : -1;
-            unsigned e[4];
-            score_row4(pb, P, cur, mp >= 0, G, sfmp, e);
+            unsigned e[kTopK];
+            score_rowk(pb, P, cur, mp >= 0, G, sfmp, e);
             if ((lane & 15) == 0 && q < nq) {
-                qk[q] = make_uint4(e[0], e[1], e[2], e[3]);
+                qk[2 * q] = make_uint4(e[0], e[1], e[2], e[3]);
+                qk[2 * q + 1] = make_uint4(e[4], e[5], e[6], e[7]);
                 qmp[q] = mp;
                 qang[q] = cur.q.angle;
             }
@@ -466,13 +480,16 @@ __global__ __launch_bounds__(kProjThreads) void k_proj_search(const ProjProblem*
             const int q = base + lane;
             int mp = -1;
             float qa = 0.f;
-            unsigned e[4] = {kNoEntry, kNoEntry, kNoEntry, kNoEntry};
+            unsigned e[kTopK];
+#pragma unroll
+            for (int j = 0; j < kTopK; j++) e[j] = kNoEntry;
             QueryReg mine;  // consumed only by a re-scoring (loads overlap the first round)
             if (q < nq) mine = load_query(pb, q);
             if (q < nq) {
                 mp = qmp[q];
-                const uint4 v = qk[q];
+                const uint4 v = qk[2 * q], w = qk[2 * q + 1];
                 e[0] = v.x; e[1] = v.y; e[2] = v.z; e[3] = v.w;
+                e[4] = w.x; e[5] = w.y; e[6] = w.z; e[7] = w.w;
                 qa = qang[q];
             }
             int start = 0;
@@ -484,14 +501,15 @@ __global__ __launch_bounds__(kProjThreads) void k_proj_search(const ProjProblem*
                 if (act) {
                     int found = 0;
 #pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        if (e[j] != kNoEntry && found < 2 && !kp_blocked(sfmp[ent_pos(e[j])], P)) {
+                    for (int j = 0; j < kTopK; j++) {
+                        if (e[j] < kTrunc && found < 2 && !kp_blocked(sfmp[ent_pos(e[j])], P)) {
                             if (found == 0) c1 = e[j];
                             else c2 = e[j];
                             found++;
                         }
                     }
-                    exhausted = e[3] != kNoEntry && found < need;
+                    // a full (or truncated) list may hide unlisted candidates
+                    exhausted = e[kTopK - 1] != kNoEntry && found < need;
                 }
                 bool acc = false;
                 if (act && !exhausted && c1 != kNoEntry && ent_dist(c1) <= P.accept_th) {
@@ -539,10 +557,10 @@ __global__ __launch_bounds__(kProjThreads) void k_proj_search(const ProjProblem*
                     nrescore++;
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                     __builtin_amdgcn_wave_barrier();
-                    unsigned ne[4];
-                    score_row4(pb, P, bcast_query(mine, f), lane < 16, G, sfmp, ne);
+                    unsigned ne[kTopK];
+                    score_rowk(pb, P, bcast_query(mine, f), lane < 16, G, sfmp, ne);
 #pragma unroll
-                    for (int j = 0; j < 4; j++) {
+                    for (int j = 0; j < kTopK; j++) {
                         const unsigned v = (unsigned)__builtin_amdgcn_readlane((int)ne[j], 0);
                         if (lane == f) e[j] = v;
                     }

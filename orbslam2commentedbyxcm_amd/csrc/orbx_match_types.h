@@ -42,7 +42,7 @@ struct ProjProblem {
 };
 
 // Global scratch per query (u64 words) when the per-query state does not fit in LDS.
-constexpr int kProjScratchWords = 4;
+constexpr int kProjScratchWords = 6;  // 8-entry candidate list (32 B) + mp, angle, match list, bin
 
 // Call-level semantics of the SearchByProjection overload being executed.
 struct ProjParams {
