@@ -76,6 +76,33 @@ def stage_bytes(W, H, n_kps, nlevels=8, scale=1.2):
     }
 
 
+# stage -> kernels of one launch of that stage (rocprofv3 kernel names)
+STAGE_KERNELS = {"pyramid": ["orbx::k_copy_level0", "orbx::k_resize"], "score_blur": ["orbx::k_level_tiles"],
+                 "fast_cells": ["orbx::k_fast_cells"], "octree": ["orbx::k_octree"],
+                 "describe": ["orbx::k_describe"], "match": ["orbx::k_seq_build", "orbx::k_proj_search<true, true>"]}
+
+
+def pmc_traffic(stage: str):
+    """HBM bytes per launch of `stage` from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate FETCH_SIZE /
+    WRITE_SIZE rocprofv3 passes of this bench), or (None, None)."""
+    files = sorted((ROOT / "profiles").glob("*_pmc_traffic.json"))
+    if not files:
+        return None, None
+    ks = json.loads(files[-1].read_text())["kernels"]
+    names = STAGE_KERNELS.get(stage, [])
+    if not names or any(k not in ks for k in names):
+        return None, files[-1].name
+    # k_resize runs once per level: its per-dispatch mean times its dispatches per step
+    tot = 0
+    for k in names:
+        v = ks[k]
+        per_step = v["traffic_bytes"] * (v["dispatches"] // ks["orbx::k_level_tiles"]["dispatches"]
+                                         if k == "orbx::k_resize" else 1)
+        tot += per_step
+    return int(tot), files[-1].name
+
+
 def cpu_baseline(frames_np, seconds: float, threads: int):
     """Oracle (TEST INFRASTRUCTURE) on host cores: extracted frames/s over a bounded sample."""
     from concurrent.futures import ThreadPoolExecutor
@@ -240,6 +267,7 @@ def main():
     kernels = {k: v for k, v in stage_ms.items() if k != "total"}
     dom = max(kernels, key=kernels.get)
     achieved = bytes_pf[dom] * B / (stage_ms[dom] * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(dom)
 
     parity = None
     if rank == 0 and args.parity_frames > 0 and match:
@@ -276,7 +304,9 @@ def main():
                        "frames_per_gpu_step": B, "global_batch": B * world, "width": W, "height": H,
                        "parallelism": f"frame-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "traffic_unit": "bytes per launch (PMC FETCH_SIZEx2 + WRITE_SIZE)",
+                         "traffic_source": traffic_src, "algorithmic_bytes_per_launch": int(bytes_pf[dom] * B),
                          "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()}},
             "cpu_baseline": cpu,
             "parity": parity,
