@@ -182,6 +182,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, available cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--parity-frames", type=int, default=2)
+    ap.add_argument("--lanes", type=int, default=2,
+                    help="split the batch into this many contiguous chunks, each on its own extractor/matcher "
+                         "stream, so one chunk's latency-bound kernels overlap another's")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -204,8 +207,11 @@ def main():
 
     from orbslam2commentedbyxcm_amd import ORBextractor
     from orbslam2commentedbyxcm_amd.matcher import ORBmatcher
-    ex = ORBextractor(1000, 1.2, 8, 20, 7, device=local_rank)
-    matcher = ORBmatcher(0.9, True, device=local_rank)  # TrackWithMotionModel, Tracking.cc:968
+    S = max(1, min(args.lanes, B // 2))
+    exs = [ORBextractor(1000, 1.2, 8, 20, 7, device=local_rank) for _ in range(S)]
+    # TrackWithMotionModel, Tracking.cc:968
+    matchers = [ORBmatcher(0.9, True, device=local_rank) for _ in range(S)]
+    ex, matcher = exs[0], matchers[0]
     sf = ex.GetScaleFactors()
     cap = ex.max_keypoints(W, H)
     d_frames = torch.from_numpy(frames_np).to(dev)
@@ -216,13 +222,32 @@ def main():
     d_mp = torch.empty((B, cap), dtype=torch.int32, device=dev)
     d_nm = torch.empty((B,), dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)  # uploads on torch's stream finish before the extractor's stream reads them
-    stream = ex.stream_handle()
+    # lane c extracts frames [b0, b1) on its extractor's stream and matches pairs (b-1 -> b)
+    # for b in [max(b0,1), b1); its first pair needs lane c-1's last frame (event).
+    bounds = [(B * c // S, B * (c + 1) // S) for c in range(S)]
+    streams = [torch.cuda.ExternalStream(e.stream_handle(), device=dev) for e in exs]
+    done = [torch.cuda.Event() for _ in range(S)]
+    # matches of lane c > 0 go to their own buffers (frame b0-1 is the first frame of its range)
+    lane_mp = [d_mp] + [torch.empty((b1 - b0 + 1, cap), dtype=torch.int32, device=dev) for (b0, b1) in bounds[1:]]
+    lane_nm = [d_nm] + [torch.empty((b1 - b0 + 1,), dtype=torch.int32, device=dev) for (b0, b1) in bounds[1:]]
 
     def step():
-        ex.extract_batch_device(d_frames, d_kps, d_desc, d_n)
+        for c in range(S):
+            b0, b1 = bounds[c]
+            exs[c].extract_batch_device(d_frames[b0:b1], d_kps[b0:b1], d_desc[b0:b1], d_n[b0:b1])
+            if S > 1:
+                done[c].record(streams[c])
         if match:
-            matcher.match_sequence_device(d_kps, d_desc, d_n, d_T, d_mp, d_nm, sf, FX, FY, CX, CY, W, H,
-                                          depth=DEPTH, th=TH, stream=stream)
+            for c in range(S):
+                b0, b1 = bounds[c]
+                lo = b0 if c == 0 else b0 - 1
+                if c > 0:
+                    streams[c].wait_event(done[c - 1])
+                out_mp = d_mp[0:b1] if c == 0 else lane_mp[c]
+                out_nm = d_nm[0:b1] if c == 0 else lane_nm[c]
+                matchers[c].match_sequence_device(d_kps[lo:b1], d_desc[lo:b1], d_n[lo:b1], d_T[lo:b1], out_mp,
+                                                  out_nm, sf, FX, FY, CX, CY, W, H, depth=DEPTH, th=TH,
+                                                  stream=exs[c].stream_handle())
 
     def sync():
         torch.cuda.synchronize(dev)
@@ -256,7 +281,10 @@ def main():
 
     n_host = d_n.cpu().numpy()
     mean_kps = float(n_host.mean())
-    mean_matches = float(d_nm.cpu().numpy()[1:].mean()) if match else 0.0
+    mean_matches = 0.0
+    if match:
+        nm_all = [d_nm[1:bounds[0][1]].cpu().numpy()] + [lane_nm[c][1:].cpu().numpy() for c in range(1, S)]
+        mean_matches = float(np.concatenate(nm_all).mean())
 
     stage_ms = ex.stage_times()
     if match:
@@ -266,7 +294,8 @@ def main():
     bytes_pf = stage_bytes(W, H, mean_kps)
     kernels = {k: v for k, v in stage_ms.items() if k != "total"}
     dom = max(kernels, key=kernels.get)
-    achieved = bytes_pf[dom] * B / (stage_ms[dom] * 1e-3) / 1e9
+    Bc = bounds[0][1] - bounds[0][0]  # frames of lane 0, whose events time the stages
+    achieved = bytes_pf[dom] * Bc / (stage_ms[dom] * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(dom)
 
     parity = None
@@ -302,11 +331,11 @@ def main():
                                    "extract all frames + TrackWithMotionModel SearchByProjection of each frame "
                                    "against its predecessor" + ("" if match else " (match disabled)"),
                        "frames_per_gpu_step": B, "global_batch": B * world, "width": W, "height": H,
-                       "parallelism": f"frame-sharded x{world}"},
+                       "parallelism": f"frame-sharded x{world}", "lanes_per_gpu": S},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_unit": "bytes per launch (PMC FETCH_SIZEx2 + WRITE_SIZE)",
-                         "traffic_source": traffic_src, "algorithmic_bytes_per_launch": int(bytes_pf[dom] * B),
+                         "traffic_source": traffic_src, "algorithmic_bytes_per_launch": int(bytes_pf[dom] * Bc),
                          "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()}},
             "cpu_baseline": cpu,
             "parity": parity,
