@@ -168,13 +168,18 @@ typedef struct {
     float Tcw[12];               /* mTcw rows 0..2, row-major */
 } orbx_frame_view;
 
-/* MapPoint fields, indexed by MapPoint id (the ids stand in for MapPoint*). */
+/* MapPoint fields, indexed by MapPoint id (the ids stand in for MapPoint*).  Fields a
+ * call does not read may be NULL: max/min_distance and normal are read only by the
+ * KeyFrame / Sim3 projections (a13, a14). */
 typedef struct {
     int n;
     const float* pos;            /* GetWorldPos(), n x 3 (may be NULL where unused) */
     const uint8_t* desc;         /* GetDescriptor(), n x 32 */
     const int32_t* observations; /* Observations() */
     const uint8_t* bad;          /* isBad() or NULL */
+    const float* max_distance;   /* mfMaxDistance (GetMaxDistanceInvariance() = 1.2f * it) */
+    const float* min_distance;   /* mfMinDistance (GetMinDistanceInvariance() = 0.8f * it) */
+    const float* normal;         /* GetNormal(), n x 3 */
 } orbx_mappoints;
 
 /* Frame::IsInFrustum outputs per MapPoint id (Frame.cc:412-477), read by
@@ -208,6 +213,26 @@ int orbx_search_by_projection_frame(orbx_matcher* m, const orbx_frame_view* cur,
                                     const orbx_frame_view* last, const int32_t* last_mp,
                                     const uint8_t* last_outlier, const orbx_mappoints* mps, float th,
                                     int mono, int* nmatches);
+
+/* SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>& sAlreadyFound,
+ * th, ORBdist) ORBmatcher.cc:1792-1924 (relocalisation, Tracking.cc:1629-1653).  kf: the
+ * KeyFrame's keypoints (angles for the rotation check), kf_mp: GetMapPointMatches() as ids
+ * (-1 = NULL), already_found: per MapPoint id (sAlreadyFound) or NULL.  cur_mp
+ * (CurrentFrame.mvpMapPoints as ids) is updated in place.  Reads mps pos, desc, bad,
+ * max_distance, min_distance. */
+int orbx_search_by_projection_keyframe(orbx_matcher* m, const orbx_frame_view* cur, int32_t* cur_mp,
+                                       const orbx_frame_view* kf, const int32_t* kf_mp,
+                                       const uint8_t* already_found, const orbx_mappoints* mps, float th,
+                                       int orb_dist, int* nmatches);
+
+/* SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const vector<MapPoint*>& vpPoints,
+ * vector<MapPoint*>& vpMatched, int th) ORBmatcher.cc:398-520 (LoopClosing::ComputeSim3,
+ * LoopClosing.cc:417).  Scw: 3x4 row-major [sR | st].  points: vpPoints as ids; matched:
+ * vpMatched as ids (kf->n entries, -1 = NULL), updated in place.  Reads mps pos, desc,
+ * bad, max_distance, min_distance, normal. */
+int orbx_search_by_projection_sim3(orbx_matcher* m, const orbx_frame_view* kf, const float* Scw,
+                                   const int32_t* points, int npoints, int32_t* matched,
+                                   const orbx_mappoints* mps, int th, int* nmatches);
 
 /* Batched TrackWithMotionModel matching (Tracking.cc:966-994) over a device-resident
  * sequence produced by orbx_extract_batch_device: for b >= 1, frame b (CurrentFrame)

@@ -114,6 +114,25 @@ public:
         return n;
     }
 
+    // SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>& sAlreadyFound, th, ORBdist)
+    int SearchByProjection(const orbx_frame_view& CurrentFrame, int32_t* curMapPoints, const orbx_frame_view& KF,
+                           const int32_t* kfMapPoints, const uint8_t* alreadyFound, const orbx_mappoints& mps,
+                           float th, int ORBdist) {
+        int n = 0;
+        check(orbx_search_by_projection_keyframe(h_, &CurrentFrame, curMapPoints, &KF, kfMapPoints, alreadyFound, &mps,
+                                                 th, ORBdist, &n));
+        return n;
+    }
+
+    // SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const vector<MapPoint*>& vpPoints, vector<MapPoint*>& vpMatched, th)
+    int SearchByProjection(const orbx_frame_view& KF, const float Scw[12], const std::vector<int32_t>& vpPoints,
+                           int32_t* vpMatched, const orbx_mappoints& mps, int th) {
+        int n = 0;
+        check(orbx_search_by_projection_sim3(h_, &KF, Scw, vpPoints.data(), (int)vpPoints.size(), vpMatched, &mps, th,
+                                             &n));
+        return n;
+    }
+
     // SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
     struct FeatureVector {
         std::vector<int32_t> node, off, idx;  // CSR of DBoW2::FeatureVector

@@ -200,7 +200,8 @@ class OraFrame(C.Structure):
 
 
 class OraMapPoints(C.Structure):
-    _fields_ = [("n", C.c_int), ("pos", F32P), ("desc", U8P), ("observations", I32P), ("bad", U8P)]
+    _fields_ = [("n", C.c_int), ("pos", F32P), ("desc", U8P), ("observations", I32P), ("bad", U8P),
+                ("max_distance", F32P), ("min_distance", F32P), ("normal", F32P)]
 
 
 class OraTrack(C.Structure):
@@ -237,13 +238,18 @@ def _mappoints(mps, keep):
     o = np.ascontiguousarray(mps.observations, dtype=np.int32)
     p = None if mps.pos is None else np.ascontiguousarray(mps.pos, dtype=np.float32)
     b = None if mps.bad is None else np.ascontiguousarray(mps.bad, dtype=np.uint8)
-    keep += [d, o, p, b]
+    f32 = lambda a: None if a is None else np.ascontiguousarray(a, dtype=np.float32)  # noqa: E731
+    mx, mn, nr = (f32(getattr(mps, k, None)) for k in ("max_distance", "min_distance", "normal"))
+    keep += [d, o, p, b, mx, mn, nr]
     m = OraMapPoints()
     m.n = len(d)
     m.pos = p.ctypes.data_as(F32P) if p is not None else None
     m.desc = d.ctypes.data_as(U8P)
     m.observations = o.ctypes.data_as(I32P)
     m.bad = b.ctypes.data_as(U8P) if b is not None else None
+    m.max_distance = mx.ctypes.data_as(F32P) if mx is not None else None
+    m.min_distance = mn.ctypes.data_as(F32P) if mn is not None else None
+    m.normal = nr.ctypes.data_as(F32P) if nr is not None else None
     keep.append(m)
     return m
 
@@ -277,6 +283,36 @@ def sbp_frame(cur, cur_mp, last, last_mp, mps, th, mono, check_ori, last_outlier
     return L.ora_sbp_frame(C.addressof(fc), cur_mp.ctypes.data_as(I32P), C.addressof(fl), lm.ctypes.data_as(I32P),
                            lo.ctypes.data_as(U8P) if lo is not None else None, C.addressof(m), th,
                            1 if mono else 0, 1 if check_ori else 0)
+
+
+def sbp_keyframe(cur, cur_mp, kf, kf_mp, mps, th, orb_dist, check_ori, already_found=None):
+    """ORBmatcher::SearchByProjection(Frame&, KeyFrame*, set, th, ORBdist) restated;
+    cur_mp updated in place, returns nmatches."""
+    keep = []
+    fc = _frame(cur, keep)
+    fk = _frame(kf, keep)
+    m = _mappoints(mps, keep)
+    km = np.ascontiguousarray(kf_mp, dtype=np.int32)
+    af = None if already_found is None else np.ascontiguousarray(already_found, dtype=np.uint8)
+    L = lib()
+    L.ora_sbp_keyframe.argtypes = [C.c_void_p, I32P, C.c_void_p, I32P, U8P, C.c_void_p, C.c_float, C.c_int, C.c_int]
+    return L.ora_sbp_keyframe(C.addressof(fc), cur_mp.ctypes.data_as(I32P), C.addressof(fk), km.ctypes.data_as(I32P),
+                              af.ctypes.data_as(U8P) if af is not None else None, C.addressof(m), th, int(orb_dist),
+                              1 if check_ori else 0)
+
+
+def sbp_sim3(kf, Scw, points, matched, mps, th):
+    """ORBmatcher::SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th) restated;
+    matched updated in place, returns nmatches."""
+    keep = []
+    fk = _frame(kf, keep)
+    m = _mappoints(mps, keep)
+    S = np.ascontiguousarray(np.asarray(Scw, np.float32)[:3, :4])
+    pts = np.ascontiguousarray(points, dtype=np.int32)
+    L = lib()
+    L.ora_sbp_sim3.argtypes = [C.c_void_p, F32P, I32P, C.c_int, I32P, C.c_void_p, C.c_int]
+    return L.ora_sbp_sim3(C.addressof(fk), S.ctypes.data_as(F32P), pts.ctypes.data_as(I32P), len(pts),
+                          matched.ctypes.data_as(I32P), C.addressof(m), int(th))
 
 
 def search_for_triangulation(kf1, has1, fv1, kf2, has2, fv2, F12, only_stereo, check_ori):

@@ -310,6 +310,180 @@ int ora_sbp_frame(const ora_frame* cur, int32_t* cur_mp, const ora_frame* last, 
     return nmatches;
 }
 
+/* MapPoint::PredictScale (MapPoint.cc:469-509).  MapPoint.cc has no `using namespace
+ * std`, so `log(ratio)` is C's log(double) of the float ratio; the quotient is double and
+ * ceil(double).  mfLogScaleFactor = log(mfScaleFactor) (Frame.cc:116, KeyFrame copy),
+ * again the double log, stored as float. */
+static int predict_scale(float max_distance, float current_dist, const ora_frame* f) {
+    const float ratio = max_distance / current_dist;
+    const float log_scale = (float)log((double)f->scale_factors[1]);
+    int n = (int)ceil(log((double)ratio) / (double)log_scale);
+    if (n < 0) n = 0;
+    else if (n >= f->nlevels) n = f->nlevels - 1;
+    return n;
+}
+
+/* cv::norm of a 3x1 CV_32F Mat (NORM_L2): squares accumulated in double, sqrt, to float */
+static float norm3(const float* p) {
+    double s = 0.0;
+    for (int k = 0; k < 3; k++) s += (double)p[k] * p[k];
+    return (float)sqrt(s);
+}
+
+/* ---------------------------------------------------------------- a13 */
+
+/* ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>&
+ * sAlreadyFound, th, ORBdist), ORBmatcher.cc:1792-1924.  kf_mp: pKF->GetMapPointMatches()
+ * as ids; already_found[id] or NULL.  Claims: any assigned keypoint is skipped
+ * (cc:1865-1866). */
+int ora_sbp_keyframe(const ora_frame* cur, int32_t* cur_mp, const ora_frame* kf, const int32_t* kf_mp,
+                     const uint8_t* already_found, const ora_mappoints* mps, float th, int orb_dist, int check_ori) {
+    ora_grid g;
+    ora_grid_build(cur, &g);
+    int* cand = (int*)malloc(sizeof(int) * (size_t)(cur->n + 1));
+    rot_hist hist;
+    hist_init(&hist, cur->n);
+    int nmatches = 0;
+    const float* T = cur->Tcw;
+    float Ow[3];  /* -Rcw^T tcw (cc:1796-1798) */
+    for (int c = 0; c < 3; c++) Ow[c] = -(T[c] * T[3] + T[4 + c] * T[7] + T[8 + c] * T[11]);
+    for (int i = 0; i < kf->n; i++) {
+        const int mp = kf_mp[i];
+        if (mp < 0) continue;
+        if (mps->bad && mps->bad[mp]) continue;
+        if (already_found && already_found[mp]) continue;
+        const float* x3Dw = mps->pos + 3 * (size_t)mp;
+        float x3Dc[3];
+        project(cur->Tcw, x3Dw, x3Dc);
+        const float xc = x3Dc[0], yc = x3Dc[1];
+        const float invzc = (float)(1.0 / x3Dc[2]);
+        const float u = cur->fx * xc * invzc + cur->cx;
+        const float v = cur->fy * yc * invzc + cur->cy;
+        if (u < cur->min_x || u > cur->max_x) continue;
+        if (v < cur->min_y || v > cur->max_y) continue;
+        float PO[3];
+        for (int c = 0; c < 3; c++) PO[c] = x3Dw[c] - Ow[c];
+        const float dist3D = norm3(PO);
+        const float maxDistance = 1.2f * mps->max_distance[mp];
+        const float minDistance = 0.8f * mps->min_distance[mp];
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const int nPredictedLevel = predict_scale(mps->max_distance[mp], dist3D, cur);
+        const float radius = th * cur->scale_factors[nPredictedLevel];
+        const int nc = ora_features_in_area(cur, &g, u, v, radius, nPredictedLevel - 1, nPredictedLevel + 1, cand,
+                                            cur->n + 1);
+        if (nc == 0) continue;
+        const uint8_t* dMP = mps->desc + (size_t)mp * 32;
+        int bestDist = 256, bestIdx2 = -1;
+        for (int c = 0; c < nc; c++) {
+            const int i2 = cand[c];
+            if (cur_mp[i2] >= 0) continue;
+            const int dist = hamming(dMP, cur->desc + (size_t)i2 * 32);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx2 = i2;
+            }
+        }
+        if (bestDist <= orb_dist) {
+            cur_mp[bestIdx2] = mp;
+            nmatches++;
+            if (check_ori) hist_push(&hist, kf->keys[i].angle, cur->keys[bestIdx2].angle, bestIdx2);
+        }
+    }
+    if (check_ori) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        ora_compute_three_maxima(hist.size, HISTO_LENGTH, &ind1, &ind2, &ind3);
+        for (int b = 0; b < HISTO_LENGTH; b++) {
+            if (b != ind1 && b != ind2 && b != ind3) {
+                for (int j = 0; j < hist.size[b]; j++) {
+                    cur_mp[hist.items[b][j]] = -1;
+                    nmatches--;
+                }
+            }
+        }
+    }
+    hist_free(&hist);
+    free(cand);
+    ora_grid_free(&g);
+    return nmatches;
+}
+
+/* ---------------------------------------------------------------- a14 */
+
+/* ORBmatcher::SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const vector<MapPoint*>&
+ * vpPoints, vector<MapPoint*>& vpMatched, int th), ORBmatcher.cc:398-520.  Scw 3x4
+ * row-major.  OpenCV arithmetic as restated: Mat::dot accumulates in
+ * double; Mat / scalar multiplies by (float)(1/s); Mat products sum float products left
+ * to right. */
+int ora_sbp_sim3(const ora_frame* kf, const float* Scw, const int32_t* points, int npoints, int32_t* matched,
+                 const ora_mappoints* mps, int th) {
+    ora_grid g;
+    ora_grid_build(kf, &g);
+    int* cand = (int*)malloc(sizeof(int) * (size_t)(kf->n + 1));
+    double d0 = 0.0;
+    for (int c = 0; c < 3; c++) d0 += (double)Scw[c] * Scw[c];
+    const float scw = (float)sqrt(d0);
+    const float alpha = (float)(1.0 / scw);
+    float T[12];  /* [Rcw | tcw] */
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 4; c++) T[4 * r + c] = Scw[4 * r + c] * alpha;
+    float Ow[3];
+    for (int c = 0; c < 3; c++) Ow[c] = -(T[c] * T[3] + T[4 + c] * T[7] + T[8 + c] * T[11]);
+    /* spAlreadyFound: the MapPoints of vpMatched before the loop */
+    uint8_t* found = (uint8_t*)calloc((size_t)(mps->n > 0 ? mps->n : 1), 1);
+    for (int i = 0; i < kf->n; i++)
+        if (matched[i] >= 0) found[matched[i]] = 1;
+    int nmatches = 0;
+    for (int k = 0; k < npoints; k++) {
+        const int mp = points[k];
+        if ((mps->bad && mps->bad[mp]) || found[mp]) continue;
+        const float* p3Dw = mps->pos + 3 * (size_t)mp;
+        float p3Dc[3];
+        project(T, p3Dw, p3Dc);
+        if (p3Dc[2] < 0.0) continue;
+        const float invz = 1 / p3Dc[2];
+        const float x = p3Dc[0] * invz;
+        const float y = p3Dc[1] * invz;
+        const float u = kf->fx * x + kf->cx;
+        const float v = kf->fy * y + kf->cy;
+        if (!(u >= kf->min_x && u < kf->max_x && v >= kf->min_y && v < kf->max_y)) continue;  /* IsInImage */
+        const float maxDistance = 1.2f * mps->max_distance[mp];
+        const float minDistance = 0.8f * mps->min_distance[mp];
+        float PO[3];
+        for (int c = 0; c < 3; c++) PO[c] = p3Dw[c] - Ow[c];
+        const float dist = norm3(PO);
+        if (dist < minDistance || dist > maxDistance) continue;
+        const float* Pn = mps->normal + 3 * (size_t)mp;
+        double dot = 0.0;
+        for (int c = 0; c < 3; c++) dot += (double)PO[c] * Pn[c];
+        if (dot < 0.5 * dist) continue;
+        const int nPredictedLevel = predict_scale(mps->max_distance[mp], dist, kf);
+        const float radius = th * kf->scale_factors[nPredictedLevel];
+        const int nc = ora_features_in_area(kf, &g, u, v, radius, -1, -1, cand, kf->n + 1);
+        if (nc == 0) continue;
+        const uint8_t* dMP = mps->desc + (size_t)mp * 32;
+        int bestDist = 256, bestIdx = -1;
+        for (int c = 0; c < nc; c++) {
+            const int idx = cand[c];
+            if (matched[idx] >= 0) continue;
+            const int kpLevel = kf->keys[idx].octave;
+            if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+            const int d = hamming(dMP, kf->desc + (size_t)idx * 32);
+            if (d < bestDist) {
+                bestDist = d;
+                bestIdx = idx;
+            }
+        }
+        if (bestDist <= TH_LOW) {
+            matched[bestIdx] = mp;
+            nmatches++;
+        }
+    }
+    free(found);
+    free(cand);
+    ora_grid_free(&g);
+    return nmatches;
+}
+
 /* ---------------------------------------------------------------- a15 */
 
 /* ORBmatcher::CheckDistEpipolarLine, ORBmatcher.cc:186-213 */

@@ -41,6 +41,9 @@ typedef struct {
     const uint8_t* desc;         /* GetDescriptor(), n x 32 */
     const int32_t* observations; /* Observations() */
     const uint8_t* bad;          /* isBad() or NULL */
+    const float* max_distance;   /* mfMaxDistance */
+    const float* min_distance;   /* mfMinDistance */
+    const float* normal;         /* GetNormal(), n x 3 */
 } ora_mappoints;
 
 /* Frame::IsInFrustum outputs per MapPoint (Frame.cc:412-477) */
@@ -62,6 +65,10 @@ int ora_sbp_local(const ora_frame* f, int32_t* frame_mp, const int32_t* queries,
                   const ora_track* trk, float th, float nnratio);
 int ora_sbp_frame(const ora_frame* cur, int32_t* cur_mp, const ora_frame* last, const int32_t* last_mp,
                   const uint8_t* last_outlier, const ora_mappoints* mps, float th, int bMono, int check_ori);
+int ora_sbp_keyframe(const ora_frame* cur, int32_t* cur_mp, const ora_frame* kf, const int32_t* kf_mp,
+                     const uint8_t* already_found, const ora_mappoints* mps, float th, int orb_dist, int check_ori);
+int ora_sbp_sim3(const ora_frame* kf, const float* Scw, const int32_t* points, int npoints, int32_t* matched,
+                 const ora_mappoints* mps, int th);
 int ora_search_for_triangulation(const ora_frame* kf1, const uint8_t* kf1_has_mp, const int32_t* fv1_node,
                                  const int32_t* fv1_off, const int32_t* fv1_idx, int fv1_n, const ora_frame* kf2,
                                  const uint8_t* kf2_has_mp, const int32_t* fv2_node, const int32_t* fv2_off,

@@ -250,7 +250,7 @@ __device__ void score_rowk(const ProjProblem& pb, const ProjParams& P, const Que
                     const float distx = kp.x - Q.u;
                     const float disty = kp.y - Q.v;
                     if (!(fabsf(distx) < Q.r && fabsf(disty) < Q.r)) continue;
-                    if (Q.post_min >= 0 && (oct < Q.post_min || oct > Q.post_max)) continue;
+                    if (Q.post_max >= 0 && (oct < Q.post_min || oct > Q.post_max)) continue;
                     if (kp_blocked(sfmp[p], P)) continue;
                     int d;
                     if (G.sdesc) {

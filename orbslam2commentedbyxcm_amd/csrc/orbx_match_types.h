@@ -22,7 +22,7 @@ struct ProjQuery {
     float r;              // GetFeaturesInArea radius
     float er_max;         // reject if |ur - mvuRight| > er_max where mvuRight > 0; < 0 = no check
     int min_level, max_level;  // GetFeaturesInArea level arguments
-    int post_min, post_max;    // extra candidate level filter [post_min, post_max] (-1 = none)
+    int post_min, post_max;    // extra candidate level filter [post_min, post_max] (post_max < 0 = none)
     int mp;               // MapPoint id written to mvpMapPoints on a match; < 0 = skip query
     float angle;          // keypoint angle of the query (rotation histogram)
     int pad;              // 48-byte record

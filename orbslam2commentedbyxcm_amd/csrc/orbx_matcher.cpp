@@ -76,6 +76,24 @@ void centre(const float* Tcw, float* c) {
     for (int k = 0; k < 3; k++) c[k] = -(Tcw[k] * Tcw[3] + Tcw[4 + k] * Tcw[7] + Tcw[8 + k] * Tcw[11]);
 }
 
+// cv::norm of a 3x1 CV_32F Mat: squares accumulated in double, sqrt, stored as float
+float norm3(const float* p) {
+    double s = 0.0;
+    for (int k = 0; k < 3; k++) s += (double)p[k] * p[k];
+    return (float)std::sqrt(s);
+}
+
+// MapPoint::PredictScale (MapPoint.cc:469-509): C log(double) of the float ratio (no
+// `using namespace std` there), double quotient, ceil; mfLogScaleFactor = (float)log(sf).
+int predict_scale(float max_distance, float current_dist, const orbx_frame_view* f) {
+    const float ratio = max_distance / current_dist;
+    const float log_scale = (float)std::log((double)f->scale_factors[1]);
+    int n = (int)std::ceil(std::log((double)ratio) / (double)log_scale);
+    if (n < 0) n = 0;
+    else if (n >= f->nlevels) n = f->nlevels - 1;
+    return n;
+}
+
 }  // namespace
 
 struct orbx_matcher {
@@ -294,6 +312,129 @@ int orbx_search_by_projection_frame(orbx_matcher* m, const orbx_frame_view* cur,
     P.ratio_mode = 0;
     P.check_ori = m->check_ori;
     return run_proj(m, cur, cur_mp, qs, qd, mps, P, nmatches);
+}
+
+// ORBmatcher::SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist),
+// ORBmatcher.cc:1792-1924: queries in KeyFrame keypoint order; any assigned keypoint of
+// the current frame is skipped (cc:1865-1866); best <= ORBdist; rotation check.
+int orbx_search_by_projection_keyframe(orbx_matcher* m, const orbx_frame_view* cur, int32_t* cur_mp,
+                                       const orbx_frame_view* kf, const int32_t* kf_mp,
+                                       const uint8_t* already_found, const orbx_mappoints* mps, float th,
+                                       int orb_dist, int* nmatches) {
+    if (!m || !cur || !cur_mp || !kf || !kf_mp || !mps || !mps->pos || !mps->max_distance || !mps->min_distance)
+        return fail(ORBX_ERR_ARG, "null argument");
+    if (cur->nlevels < 2) return fail(ORBX_ERR_ARG, "need >= 2 pyramid levels");
+    float Ow[3];
+    centre(cur->Tcw, Ow);  // cc:1796-1798
+    std::vector<ProjQuery> qs;
+    std::vector<uint8_t> qd;
+    for (int i = 0; i < kf->n; i++) {
+        const int mp = kf_mp[i];
+        if (mp < 0) continue;
+        if (mp >= mps->n) return fail(ORBX_ERR_ARG, "MapPoint id out of range");
+        if (mps->bad && mps->bad[mp]) continue;
+        if (already_found && already_found[mp]) continue;
+        const float* x3Dw = mps->pos + 3 * (size_t)mp;
+        float x3Dc[3];
+        project(cur->Tcw, x3Dw, x3Dc);
+        const float invzc = (float)(1.0 / x3Dc[2]);
+        const float u = cur->fx * x3Dc[0] * invzc + cur->cx;
+        const float v = cur->fy * x3Dc[1] * invzc + cur->cy;
+        if (u < cur->min_x || u > cur->max_x) continue;
+        if (v < cur->min_y || v > cur->max_y) continue;
+        float PO[3];
+        for (int c = 0; c < 3; c++) PO[c] = x3Dw[c] - Ow[c];
+        const float dist3D = norm3(PO);
+        if (dist3D < 0.8f * mps->min_distance[mp] || dist3D > 1.2f * mps->max_distance[mp]) continue;
+        const int pred = predict_scale(mps->max_distance[mp], dist3D, cur);
+        ProjQuery q{};
+        q.u = u;
+        q.v = v;
+        q.r = th * cur->scale_factors[pred];
+        q.er_max = -1.f;
+        q.min_level = pred - 1;  // GetFeaturesInArea(u, v, radius, pred-1, pred+1)
+        q.max_level = pred + 1;
+        q.post_min = -1;
+        q.post_max = -1;
+        q.mp = mp;
+        q.angle = kf->keys[i].angle;
+        qs.push_back(q);
+        qd.insert(qd.end(), mps->desc + (size_t)mp * 32, mps->desc + (size_t)mp * 32 + 32);
+    }
+    ProjParams P{};
+    P.blocked_mode = 1;
+    P.accept_th = orb_dist;
+    P.ratio_mode = 0;
+    P.check_ori = m->check_ori;
+    return run_proj(m, cur, cur_mp, qs, qd, mps, P, nmatches);
+}
+
+// ORBmatcher::SearchByProjection(KeyFrame*, cv::Mat Scw, const vector<MapPoint*>&,
+// vector<MapPoint*>&, int th), ORBmatcher.cc:398-520.  OpenCV arithmetic as restated in
+// DESIGN.md §2 (Mat::dot in double, Mat / s as a float multiply by (float)(1/s)).
+int orbx_search_by_projection_sim3(orbx_matcher* m, const orbx_frame_view* kf, const float* Scw,
+                                   const int32_t* points, int npoints, int32_t* matched,
+                                   const orbx_mappoints* mps, int th, int* nmatches) {
+    if (!m || !kf || !Scw || !matched || !mps || !mps->pos || !mps->max_distance || !mps->min_distance ||
+        !mps->normal || (npoints && !points))
+        return fail(ORBX_ERR_ARG, "null argument");
+    if (kf->nlevels < 2) return fail(ORBX_ERR_ARG, "need >= 2 pyramid levels");
+    double d0 = 0.0;
+    for (int c = 0; c < 3; c++) d0 += (double)Scw[c] * Scw[c];
+    const float scw = (float)std::sqrt(d0);                 // cc:408
+    const float alpha = (float)(1.0 / scw);
+    float T[12];                                            // Rcw = sRcw / scw, tcw = st / scw (cc:409-410)
+    for (int k = 0; k < 12; k++) T[k] = Scw[k] * alpha;
+    float Ow[3];
+    centre(T, Ow);                                          // cc:411
+    std::vector<uint8_t> found((size_t)(mps->n > 0 ? mps->n : 1), 0);  // spAlreadyFound (cc:414-415)
+    for (int i = 0; i < kf->n; i++) {
+        if (matched[i] >= mps->n) return fail(ORBX_ERR_ARG, "MapPoint id out of range");
+        if (matched[i] >= 0) found[matched[i]] = 1;
+    }
+    std::vector<ProjQuery> qs;
+    std::vector<uint8_t> qd;
+    for (int k = 0; k < npoints; k++) {
+        const int mp = points[k];
+        if (mp < 0 || mp >= mps->n) return fail(ORBX_ERR_ARG, "MapPoint id out of range");
+        if ((mps->bad && mps->bad[mp]) || found[mp]) continue;
+        const float* p3Dw = mps->pos + 3 * (size_t)mp;
+        float p3Dc[3];
+        project(T, p3Dw, p3Dc);
+        if (p3Dc[2] < 0.0) continue;
+        const float invz = 1 / p3Dc[2];
+        const float u = kf->fx * (p3Dc[0] * invz) + kf->cx;
+        const float v = kf->fy * (p3Dc[1] * invz) + kf->cy;
+        if (!(u >= kf->min_x && u < kf->max_x && v >= kf->min_y && v < kf->max_y)) continue;  // IsInImage
+        float PO[3];
+        for (int c = 0; c < 3; c++) PO[c] = p3Dw[c] - Ow[c];
+        const float dist = norm3(PO);
+        if (dist < 0.8f * mps->min_distance[mp] || dist > 1.2f * mps->max_distance[mp]) continue;
+        const float* Pn = mps->normal + 3 * (size_t)mp;
+        double dot = 0.0;
+        for (int c = 0; c < 3; c++) dot += (double)PO[c] * Pn[c];
+        if (dot < 0.5 * dist) continue;
+        const int pred = predict_scale(mps->max_distance[mp], dist, kf);
+        ProjQuery q{};
+        q.u = u;
+        q.v = v;
+        q.r = (float)th * kf->scale_factors[pred];
+        q.er_max = -1.f;
+        q.min_level = -1;  // KeyFrame::GetFeaturesInArea has no level arguments
+        q.max_level = -1;
+        q.post_min = pred - 1;  // kpLevel in [pred-1, pred] (cc:480-483)
+        q.post_max = pred;
+        q.mp = mp;
+        q.angle = 0.f;
+        qs.push_back(q);
+        qd.insert(qd.end(), mps->desc + (size_t)mp * 32, mps->desc + (size_t)mp * 32 + 32);
+    }
+    ProjParams P{};
+    P.blocked_mode = 1;
+    P.accept_th = TH_LOW;
+    P.ratio_mode = 0;
+    P.check_ori = 0;
+    return run_proj(m, kf, matched, qs, qd, mps, P, nmatches);
 }
 
 // Batched SearchByProjection(CurrentFrame, LastFrame, th, bMono=true) over a device

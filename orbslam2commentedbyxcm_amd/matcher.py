@@ -29,7 +29,8 @@ class _FrameViewC(C.Structure):
 
 
 class _MapPointsC(C.Structure):
-    _fields_ = [("n", C.c_int), ("pos", F32P), ("desc", U8P), ("observations", I32P), ("bad", U8P)]
+    _fields_ = [("n", C.c_int), ("pos", F32P), ("desc", U8P), ("observations", I32P), ("bad", U8P),
+                ("max_distance", F32P), ("min_distance", F32P), ("normal", F32P)]
 
 
 class _TrackC(C.Structure):
@@ -90,6 +91,9 @@ class MapPoints:
     observations: np.ndarray               # Observations() (m,)
     pos: np.ndarray | None = None          # GetWorldPos() (m, 3)
     bad: np.ndarray | None = None          # isBad() (m,)
+    max_distance: np.ndarray | None = None  # mfMaxDistance (m,)
+    min_distance: np.ndarray | None = None  # mfMinDistance (m,)
+    normal: np.ndarray | None = None        # GetNormal() (m, 3)
     _keep: list = field(default_factory=list, repr=False)
 
     def c(self) -> _MapPointsC:
@@ -97,13 +101,17 @@ class MapPoints:
         o = np.ascontiguousarray(self.observations, dtype=np.int32)
         p = None if self.pos is None else _f32(self.pos)
         b = None if self.bad is None else np.ascontiguousarray(self.bad, dtype=np.uint8)
-        self._keep = [d, o, p, b]
+        mx, mn, nr = (None if a is None else _f32(a) for a in (self.max_distance, self.min_distance, self.normal))
+        self._keep = [d, o, p, b, mx, mn, nr]
         v = _MapPointsC()
         v.n = len(d)
         v.pos = p.ctypes.data_as(F32P) if p is not None else None
         v.desc = d.ctypes.data_as(U8P)
         v.observations = o.ctypes.data_as(I32P)
         v.bad = b.ctypes.data_as(U8P) if b is not None else None
+        v.max_distance = mx.ctypes.data_as(F32P) if mx is not None else None
+        v.min_distance = mn.ctypes.data_as(F32P) if mn is not None else None
+        v.normal = nr.ctypes.data_as(F32P) if nr is not None else None
         return v
 
 
@@ -191,6 +199,33 @@ class ORBmatcher:
                                                         C.addressof(lv), lm.ctypes.data_as(I32P),
                                                         lo.ctypes.data_as(U8P) if lo is not None else None,
                                                         C.addressof(mv), float(th), 1 if bMono else 0, C.byref(n)))
+        return n.value
+
+    # SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist)  ORBmatcher.cc:1792-1924
+    def SearchByProjectionKeyFrame(self, cur: FrameView, cur_mp: np.ndarray, kf: FrameView, kf_mp: np.ndarray,
+                                   mps: MapPoints, th: float, ORBdist: int, already_found=None) -> int:
+        assert cur_mp.dtype == np.int32 and cur_mp.flags.c_contiguous
+        km = np.ascontiguousarray(kf_mp, dtype=np.int32)
+        af = None if already_found is None else np.ascontiguousarray(already_found, dtype=np.uint8)
+        cv_, kv, mv = cur.c(), kf.c(), mps.c()
+        n = C.c_int()
+        L.check(L.lib().orbx_search_by_projection_keyframe(
+            self._h, C.addressof(cv_), cur_mp.ctypes.data_as(I32P), C.addressof(kv), km.ctypes.data_as(I32P),
+            af.ctypes.data_as(U8P) if af is not None else None, C.addressof(mv), float(th), int(ORBdist),
+            C.byref(n)))
+        return n.value
+
+    # SearchByProjection(KeyFrame*, cv::Mat Scw, vpPoints, vpMatched, th)  ORBmatcher.cc:398-520
+    def SearchByProjectionSim3(self, kf: FrameView, Scw, points, matched: np.ndarray, mps: MapPoints, th: int) -> int:
+        assert matched.dtype == np.int32 and matched.flags.c_contiguous and len(matched) == len(kf.keys)
+        S = np.ascontiguousarray(np.asarray(Scw, dtype=np.float32)[:3, :4])
+        pts = np.ascontiguousarray(points, dtype=np.int32)
+        kv, mv = kf.c(), mps.c()
+        n = C.c_int()
+        L.check(L.lib().orbx_search_by_projection_sim3(self._h, C.addressof(kv), S.ctypes.data_as(F32P),
+                                                       pts.ctypes.data_as(I32P), len(pts),
+                                                       matched.ctypes.data_as(I32P), C.addressof(mv), int(th),
+                                                       C.byref(n)))
         return n.value
 
     # SearchForTriangulation(KF1, KF2, F12, vMatchedPairs, bOnlyStereo)  ORBmatcher.cc:850-1056

@@ -54,6 +54,24 @@ def mappoints_from(A, seed=0, obs_zero_frac=0.1):
     return MapPoints(desc=A.desc.copy(), observations=obs, pos=pos, bad=(rng.random(n) < 0.03).astype(np.uint8))
 
 
+def with_depth_info(mps, A, seed=0, flip_frac=0.05):
+    """MapPoint::UpdateNormalAndDepth (MapPoint.cc) for points first seen by view A:
+    mfMaxDistance = dist * scale[octave], mfMinDistance = mfMaxDistance / scale[L-1],
+    normal = unit viewing direction (a few flipped to exercise the normal test)."""
+    rng = np.random.default_rng(seed + 17)
+    T = np.asarray(A.Tcw, np.float32)
+    Ow = -(T[:3, :3].T @ T[:3, 3])
+    PO = mps.pos - Ow[None, :]
+    dist = np.linalg.norm(PO.astype(np.float64), axis=1).astype(np.float32)
+    sf = np.asarray(A.scale_factors, np.float32)
+    mx = (dist * sf[A.keys["octave"]]).astype(np.float32)
+    mn = (mx / sf[-1]).astype(np.float32)
+    nrm = (PO / dist[:, None]).astype(np.float32)
+    nrm[rng.random(len(nrm)) < flip_frac] *= -1
+    mps.max_distance, mps.min_distance, mps.normal = mx, mn, nrm
+    return mps
+
+
 def local_track(A, B, mps, seed=0):
     """IsInFrustum outputs for projecting A's MapPoints into B."""
     rng = np.random.default_rng(seed + 5)

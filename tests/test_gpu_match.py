@@ -38,6 +38,51 @@ def test_search_by_projection_frame(oracle, orbx_built, seed, stereo, th, preass
         assert n_ref > 50  # the scene really matches
 
 
+@pytest.mark.parametrize("seed,th,orb_dist,check_ori", [(0, 10.0, 100, True), (1, 3.0, 64, True),
+                                                        (2, 10.0, 100, False)])
+def test_search_by_projection_keyframe(oracle, orbx_built, seed, th, orb_dist, check_ori):
+    """a13: relocalisation SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist)."""
+    A, B = S.two_views(oracle, seed)
+    mps = S.with_depth_info(S.mappoints_from(A, seed), A, seed)
+    rng = np.random.default_rng(seed)
+    kf_mp = np.arange(len(A.keys), dtype=np.int32)
+    kf_mp[rng.random(len(A.keys)) < 0.1] = -1
+    already = (rng.random(len(A.keys)) < 0.1).astype(np.uint8)
+    cur0 = np.full(len(B.keys), -1, np.int32)
+    sel = rng.random(len(B.keys)) < 0.05
+    cur0[sel] = rng.integers(0, len(A.keys), sel.sum())
+    m = ORBmatcher(0.9, check_ori)
+    cur_gpu = cur0.copy()
+    n_gpu = m.SearchByProjectionKeyFrame(B, cur_gpu, A, kf_mp, mps, th, orb_dist, already_found=already)
+    cur_ref = cur0.copy()
+    n_ref = oracle.sbp_keyframe(B, cur_ref, A, kf_mp, mps, th, orb_dist, check_ori, already_found=already)
+    assert n_gpu == n_ref
+    assert np.array_equal(cur_gpu, cur_ref), np.nonzero(cur_gpu != cur_ref)[0][:10]
+    assert n_ref > 50
+
+
+@pytest.mark.parametrize("seed,scale,th", [(0, 1.0, 10), (1, 1.7, 10), (2, 0.6, 5)])
+def test_search_by_projection_sim3(oracle, orbx_built, seed, scale, th):
+    """a14: loop-closing SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th)."""
+    A, B = S.two_views(oracle, seed)
+    mps = S.with_depth_info(S.mappoints_from(A, seed), A, seed)
+    rng = np.random.default_rng(seed + 1)
+    n = len(A.keys)
+    Scw = (np.float32(scale) * np.asarray(B.Tcw, np.float32)[:3, :4]).astype(np.float32)
+    points = rng.permutation(n)[: int(0.9 * n)].astype(np.int32)
+    matched0 = np.full(len(B.keys), -1, np.int32)
+    sel = rng.random(len(B.keys)) < 0.05
+    matched0[sel] = rng.integers(0, n, sel.sum())
+    m = ORBmatcher(0.75, False)
+    got = matched0.copy()
+    n_gpu = m.SearchByProjectionSim3(B, Scw, points, got, mps, th)
+    ref = matched0.copy()
+    n_ref = oracle.sbp_sim3(B, Scw, points, ref, mps, th)
+    assert n_gpu == n_ref
+    assert np.array_equal(got, ref), np.nonzero(got != ref)[0][:10]
+    assert n_ref > 50
+
+
 @pytest.mark.parametrize("seed,th,nnratio", [(0, 1.0, 0.8), (1, 3.0, 0.8), (2, 5.0, 0.6)])
 def test_search_by_projection_local(oracle, orbx_built, seed, th, nnratio):
     A, B = S.two_views(oracle, seed, stereo=seed == 2)
