@@ -654,8 +654,21 @@ __global__ __launch_bounds__(256) void k_octree(const LevelGeom* __restrict__ lv
     __shared__ int s_map[kMaxIni];
     __shared__ int s_icnt[kMaxIni];
 
+    // Level-major order (all frames' level 0 first, then level 1, ...): the long level-0
+    // distributions start first and the short ones fill in behind them; frames keep their
+    // XCD (frame f on XCD f % 8) when nframes % 8 == 0.
     int f, l;
-    xcd_frame_block(L, nframes, f, l);
+    {
+        const int lin = blockIdx.x;
+        if (nframes % kXcds == 0) {
+            const int per = nframes / kXcds, x = lin % kXcds, k = lin / kXcds;
+            l = k / per;
+            f = (k - l * per) * kXcds + x;
+        } else {
+            l = lin / nframes;
+            f = lin - l * nframes;
+        }
+    }
     const int tid = threadIdx.x;
     unsigned long long* st = stamps ? stamps + 8 * ((size_t)f * L + l) : nullptr;
     if (st && tid == 0) st[0] = wall_clock64();
