@@ -437,18 +437,21 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
 // the threshold score 0, keeps a corner p iff M_p > t, M_p >= 2 and M_p exceeds every
 // in-window neighbour's M (a neighbour with M_n >= M_p > t always suppresses; one below
 // M_p never does) -- threshold-independent apart from M_p > t.  M is sparse (k_level_tiles
-// zeroes M <= min(iniTh, minTh)), so the wave lists the window's non-zero pixels in
-// raster order (one ballot per row), tests only those against their neighbours, and
-// writes the survivors of the chosen threshold in the same order.
+// zeroes M <= min(iniTh, minTh)), so the wave stages the window with a zero frame, lists
+// the non-zero pixels in raster order (one ballot per row -- per row pair when the window
+// is at most 32 wide), tests only those against their neighbours, and writes the
+// survivors of the chosen threshold in the same order.
+constexpr int kFcStride = 68;  // staged window row pitch (64 + zero frame, bank spread)
+
 __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ score, long long fb,
                                                     const CellGeom* __restrict__ cells, int ncells,
                                                     int ini_th, int min_th, uint32_t* __restrict__ slots,
                                                     int slots_pf, int* __restrict__ cell_count, int nframes,
                                                     int max_wr, int max_wc) {
-    // per wave: max_wr rows x 64 bytes of M, then a candidate list of max_wr*max_wc u16
+    // per wave: (max_wr + 2) framed rows of M, then a candidate list of max_wr*max_wc u16
     extern __shared__ __align__(16) uint8_t s_dyn[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int per_wave = ((max_wr * 64 + 2 * max_wr * max_wc) + 15) & ~15;
+    const int per_wave = (((max_wr + 2) * kFcStride + 2 * max_wr * max_wc) + 15) & ~15;
     int f, cb;
     xcd_frame_block((ncells + 3) / 4, nframes, f, cb);
     const int ci = cb * 4 + wave;
@@ -461,50 +464,66 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
         const int tm = min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th);
         const int tc = max(min(ti, tm), 1);  // candidates: M > tc
         const uint8_t* src = score + (size_t)f * fb + c.src_off;
-        uint8_t(*m)[64] = (uint8_t(*)[64])(s_dyn + wave * per_wave);
-        uint16_t* list = (uint16_t*)(s_dyn + wave * per_wave + max_wr * 64);
-        const bool act = lane < wc;
+        uint8_t* m = s_dyn + wave * per_wave;  // m[(r + 1) * kFcStride + c + 1] = M(r, c)
+        uint16_t* list = (uint16_t*)(s_dyn + wave * per_wave + (max_wr + 2) * kFcStride);
         const unsigned long long below = (1ull << lane) - 1;
+        // zero frame: rows -1 and wr, column -1 (columns >= wc are written as 0 below)
+        m[lane] = 0;
+        m[(wr + 1) * kFcStride + lane] = 0;
+        if (lane < 4) {
+            m[64 + lane] = 0;
+            m[(wr + 1) * kFcStride + 64 + lane] = 0;
+        }
+        for (int r = lane; r < wr + 2; r += 64) {  // columns -1 and wc
+            m[r * kFcStride] = 0;
+            m[r * kFcStride + wc + 1] = 0;
+        }
         int n = 0;
-        // 16 rows of loads in flight at a time (unconditional loads from clamped addresses)
-        for (int r0 = 0; r0 < wr; r0 += 16) {
-            int v[16];
+        const bool pairs = wc <= 32;
+        const int col = pairs ? (lane & 31) : lane;
+        const int half = pairs ? (lane >> 5) : 0;
+        const int rstep = pairs ? 2 : 1;
+        const bool act = col < wc;
+        // 8 row steps of loads in flight at a time (unconditional loads, clamped addresses)
+        for (int r0 = 0; r0 < wr; r0 += 8 * rstep) {
+            int v[8];
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const bool ok = act && r0 + k < wr;
-                v[k] = src[ok ? (size_t)(r0 + k) * c.pitch + lane : 0];
+            for (int k = 0; k < 8; k++) {
+                const int r = r0 + k * rstep + half;
+                const bool ok = act && r < wr;
+                v[k] = src[ok ? (size_t)r * c.pitch + col : 0];
                 v[k] = ok ? v[k] : 0;
             }
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const int r = r0 + k;
-                if (r < wr) {
-                    m[r][lane] = (uint8_t)v[k];
-                    const unsigned long long b = __ballot(v[k] > tc);
-                    if ((b >> lane) & 1ull) list[n + __popcll(b & below)] = (uint16_t)((r << 8) | lane);
+            for (int k = 0; k < 8; k++) {
+                const int rb = r0 + k * rstep;  // first row of this step (wave-uniform)
+                if (rb < wr) {
+                    const int r = rb + half;
+                    if (r < wr) m[(r + 1) * kFcStride + col + 1] = (uint8_t)v[k];
+                    const unsigned long long b = __ballot(v[k] > tc);  // raster order: row rb, then rb+1
+                    if ((b >> lane) & 1ull) list[n + __popcll(b & below)] = (uint16_t)((r << 8) | col);
                     n += __popcll(b);
                 }
             }
         }
         wave_lds_fence();
-        // neighbour test of the candidates, counts at both thresholds
+        // neighbour test of the candidates (zero frame: no bounds checks), both thresholds
+        auto keep_of = [&](int i, int& r, int& cc, int& M) -> bool {
+            const int rc = list[i];
+            r = rc >> 8;
+            cc = rc & 255;
+            const uint8_t* p = m + (r + 1) * kFcStride + cc + 1;
+            M = p[0];
+            const int nb = max(max(max(p[-kFcStride - 1], p[-kFcStride]), max(p[-kFcStride + 1], p[-1])),
+                               max(max(p[1], p[kFcStride - 1]), max(p[kFcStride], p[kFcStride + 1])));
+            return M > nb;  // M > tc >= 1, so M >= 2
+        };
         int cnt_i = 0, cnt_m = 0;
         for (int i0 = 0; i0 < n; i0 += 64) {
             bool ki = false, km = false;
-            const int i = i0 + lane;
-            if (i < n) {
-                const int rc = list[i], r = rc >> 8, col = rc & 255;
-                const int M = m[r][col];
-                int nb = 0;
-#pragma unroll
-                for (int dy = -1; dy <= 1; dy++)
-#pragma unroll
-                    for (int dx = -1; dx <= 1; dx++) {
-                        if (dx == 0 && dy == 0) continue;
-                        const int rr = r + dy, cc = col + dx;
-                        if (rr >= 0 && rr < wr && cc >= 0 && cc < wc) nb = max(nb, (int)m[rr][cc]);
-                    }
-                const bool lm = M > nb;  // M > tc >= 1, so M >= 2
+            if (i0 + lane < n) {
+                int r, cc, M;
+                const bool lm = keep_of(i0 + lane, r, cc, M);
                 ki = lm && M > ti;
                 km = lm && M > tm;
             }
@@ -518,28 +537,12 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
             uint32_t* out = slots + (size_t)f * slots_pf + c.slot_off;
             int base = 0;
             for (int i0 = 0; i0 < n; i0 += 64) {
-                const int i = i0 + lane;
                 bool keep = false;
-                int r = 0, col = 0, M = 0;
-                if (i < n) {
-                    const int rc = list[i];
-                    r = rc >> 8;
-                    col = rc & 255;
-                    M = m[r][col];
-                    int nb = 0;
-#pragma unroll
-                    for (int dy = -1; dy <= 1; dy++)
-#pragma unroll
-                        for (int dx = -1; dx <= 1; dx++) {
-                            if (dx == 0 && dy == 0) continue;
-                            const int rr = r + dy, cc = col + dx;
-                            if (rr >= 0 && rr < wr && cc >= 0 && cc < wc) nb = max(nb, (int)m[rr][cc]);
-                        }
-                    keep = M > nb && M > t;
-                }
+                int r = 0, cc = 0, M = 0;
+                if (i0 + lane < n) keep = keep_of(i0 + lane, r, cc, M) && M > t;
                 const unsigned long long b = __ballot(keep);
                 if (keep) {
-                    const int xr = c.x0 + 3 + col - kMinBorder;  // relative to minBorderX
+                    const int xr = c.x0 + 3 + cc - kMinBorder;  // relative to minBorderX
                     const int yr = c.y0 + 3 + r - kMinBorder;
                     out[base + __popcll(b & below)] = (uint32_t)xr | ((uint32_t)yr << 12) | ((uint32_t)(M - 1) << 24);
                 }
@@ -1262,7 +1265,7 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     if (ev) (void)hipEventRecord(ev[2], stream);
     {
         dim3 grid(((ncells + 3) / 4) * batch);
-        const size_t fc_lds = 4 * (size_t)(((plan.fc_wr * 64 + 2 * plan.fc_wr * plan.fc_wc) + 15) & ~15);
+        const size_t fc_lds = 4 * (size_t)((((plan.fc_wr + 2) * kFcStride + 2 * plan.fc_wr * plan.fc_wc) + 15) & ~15);
         hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), fc_lds, stream, db.score, fb, db.cells, ncells,
                            plan.prm.ini_th, plan.prm.min_th, db.slots, plan.slots_per_frame, db.cell_count, batch,
                            plan.fc_wr, plan.fc_wc);
