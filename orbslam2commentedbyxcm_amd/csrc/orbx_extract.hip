@@ -1110,9 +1110,11 @@ __device__ float fast_atan2(float y, float x) {
 
 __device__ __forceinline__ int cv_round(float v) { return (int)rintf(v); }
 
-// One wave per kept keypoint slot: IC_Angle on the level (cc:59-106), rBRIEF on the
-// blurred level (cc:118-172), coordinate scaling (cc:1613-1622), output in the
-// reference's level-major order.
+// Two kept keypoint slots per wave (one per 32-lane half): IC_Angle on the level
+// (cc:59-106), rBRIEF on the blurred level (cc:118-172), coordinate scaling
+// (cc:1613-1622), output in the reference's level-major order.  Halving the waves halves
+// the per-keypoint cost of everything evaluated once per wave (fastAtan2, the double
+// cos/sin, addressing) while each lane keeps 31 + 16 independent loads in flight.
 __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ pyr,
                                                   const uint8_t* __restrict__ blur, long long fb,
                                                   const LevelGeom* __restrict__ lv, int L,
@@ -1121,92 +1123,99 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
                                                   orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                   int cap, int* __restrict__ n_out, int nframes) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int half = lane >> 5, hl = lane & 31;
     int f, sb;
-    xcd_frame_block((kept_pf + 3) / 4, nframes, f, sb);
-    const int slot = sb * 4 + wave;
-    if (slot >= kept_pf) return;
+    xcd_frame_block((kept_pf + 7) / 8, nframes, f, sb);
+    const int slot0 = sb * 8 + wave * 2;
+    if (slot0 >= kept_pf) return;  // whole wave
+    const int slot = slot0 + half;
+    const int* kc = kept_count + (size_t)f * L;
+    // level of this half's slot, its output base and the frame total
     int l = 0;
     while (l + 1 < L && slot >= lv[l + 1].out_off) l++;
-    const LevelGeom& g = lv[l];
-    const int i = slot - g.out_off;
-    const int* kc = kept_count + (size_t)f * L;
     int base = 0, total = 0;
     for (int l2 = 0; l2 < L; l2++) {
         const int c = kc[l2];
         if (l2 < l) base += c;
         total += c;
     }
-    if (slot == 0 && lane == 0) n_out[f] = total;
-    if (i >= kc[l]) return;
+    if (slot0 == 0 && lane == 0) n_out[f] = total;
+    const LevelGeom& g = lv[l];
+    const int i = slot - g.out_off;
     const int o = base + i;
-    if (o >= cap) return;
-    const uint32_t key = kept[(size_t)f * kept_pf + slot];
-    const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
+    const bool valid = slot < kept_pf && i < kc[l] && o < cap;
+    if (__ballot(valid) == 0) return;  // both halves empty
+    const uint32_t key = valid ? kept[(size_t)f * kept_pf + slot] : 0u;
+    // an empty half samples the middle of its level (>= 23 px from every edge) and is masked
+    const int x = valid ? key_x(key) + kMinBorder : g.w / 2;
+    const int y = valid ? key_y(key) + kMinBorder : g.h / 2;
     const int resp = key_resp(key);
-    // loads that do not depend on the patch, issued up front (the empty asm keeps the
-    // compiler from sinking them behind the IC-angle latency)
-    int pat[4];
+    const size_t goff = (size_t)f * fb + g.off;
+    const int pitch = g.pitch;
+    // pattern pairs hl, 32+hl, ..., 224+hl (x0, y0, x1, y1 as int8), issued up front
+    int pat[8];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        pat[k] = ((const int*)c_pattern)[k * 64 + lane];  // x0, y0, x1, y1 of pair k*64+lane
+    for (int k = 0; k < 8; k++) {
+        pat[k] = ((const int*)c_pattern)[k * 32 + hl];
         asm volatile("" : "+v"(pat[k]));
     }
     float lv_scale = g.scale, lv_size = g.kp_size;
     asm volatile("" : "+v"(lv_scale), "+v"(lv_size));
 
-    // IC angle (cc:59-106): lane u+15 (u = -15..15) sums column u over rows v = 0..15,
-    // lane 32+u+15 over rows v = -1..-15; all 16 loads of a lane are issued before any
-    // is consumed (unconditional loads from in-patch addresses, masked afterwards).
+    // IC angle: lane hl (u = hl - 15, hl < 31) sums its column over rows v = -15..15 with
+    // the circular mask |u| <= umax[|v|]; all 31 loads are issued before any is consumed.
     int m10 = 0, m01 = 0;
     {
-        const int half = lane >> 5, u = (lane & 31) - 15;
+        const int u = hl - 15;
         const int au = u < 0 ? -u : u;
-        const bool col_ok = (lane & 31) < 31;
-        const uint8_t* ctr = pyr + (size_t)f * fb + g.off + (size_t)y * g.pitch + x + (col_ok ? u : 0);
-        const long sgn = half ? -(long)g.pitch : (long)g.pitch;
-        int px[16];
+        const bool col_ok = hl < 31;
+        const uint8_t* ctr = pyr + goff + (size_t)y * pitch + x + (col_ok ? u : 0);
+        int px[31];
 #pragma unroll
-        for (int k = 0; k < 16; k++) px[k] = ctr[(long)k * sgn];
+        for (int k = 0; k < 31; k++) px[k] = ctr[(long)(k - 15) * pitch];
         if (col_ok) {
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                if (k == 0 && half) continue;  // row 0 counted once (by the v >= 0 half)
-                if (k > 0 && au > c_umax[k]) continue;
-                const int v = half ? -k : k;
+            for (int k = 0; k < 31; k++) {
+                const int v = k - 15;
+                const int av = v < 0 ? -v : v;
+                if (v != 0 && au > c_umax[av]) continue;
                 m10 += u * px[k];
                 m01 += v * px[k];
             }
         }
     }
 #pragma unroll
-    for (int o2 = 32; o2 > 0; o2 >>= 1) {
+    for (int o2 = 16; o2 > 0; o2 >>= 1) {  // within the 32-lane half
         m10 += __shfl_xor(m10, o2);
         m01 += __shfl_xor(m01, o2);
     }
     const float angle = fast_atan2((float)m01, (float)m10);
 
-    // steered BRIEF on the blurred level: all 8 samples of a lane in flight at once
+    // steered BRIEF on the blurred level: 16 samples per lane in flight
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float rad = angle * factorPI;
     const float a = (float)cos((double)rad), b = (float)sin((double)rad);
-    const uint8_t* center = blur + (size_t)f * fb + g.off + (size_t)y * g.pitch + x;
-    const int step = g.pitch;
-    int t0[4], t1[4];
+    const uint8_t* center = blur + goff + (size_t)y * pitch + x;
+    int t0[8], t1[8];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < 8; k++) {
         const float x0 = (float)(int8_t)(pat[k] & 0xff), y0 = (float)(int8_t)((pat[k] >> 8) & 0xff);
         const float x1 = (float)(int8_t)((pat[k] >> 16) & 0xff), y1 = (float)(int8_t)(pat[k] >> 24);
-        t0[k] = center[cv_round(x0 * b + y0 * a) * step + cv_round(x0 * a - y0 * b)];
-        t1[k] = center[cv_round(x1 * b + y1 * a) * step + cv_round(x1 * a - y1 * b)];
+        t0[k] = center[cv_round(x0 * b + y0 * a) * pitch + cv_round(x0 * a - y0 * b)];
+        t1[k] = center[cv_round(x1 * b + y1 * a) * pitch + cv_round(x1 * a - y1 * b)];
     }
-    unsigned long long words[4];
+    uint32_t words[8];
 #pragma unroll
-    for (int k = 0; k < 4; k++) words[k] = __ballot(t0[k] < t1[k]);
-    if (lane < 4) {
-        unsigned long long* d = (unsigned long long*)(desc + ((size_t)f * cap + o) * 32);
-        d[lane] = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+    for (int k = 0; k < 8; k++) {
+        const unsigned long long bits = __ballot(t0[k] < t1[k]);
+        words[k] = half ? (uint32_t)(bits >> 32) : (uint32_t)bits;  // descriptor bytes 4k..4k+3
     }
-    if (lane == 0) {
+    if (valid && hl < 2) {
+        uint4* d = (uint4*)(desc + ((size_t)f * cap + o) * 32);
+        d[hl] = hl == 0 ? make_uint4(words[0], words[1], words[2], words[3])
+                        : make_uint4(words[4], words[5], words[6], words[7]);
+    }
+    if (valid && hl == 0) {
         float fx = (float)x, fy = (float)y;
         if (l != 0) {
             fx = fx * lv_scale;
@@ -1281,7 +1290,7 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     }
     if (ev) (void)hipEventRecord(ev[4], stream);
     {
-        dim3 grid(((plan.kept_per_frame + 3) / 4) * batch);
+        dim3 grid(((plan.kept_per_frame + 7) / 8) * batch);
         hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, stream, db.pyr, db.blur, fb, db.lv, L, db.kept,
                            plan.kept_per_frame, db.kept_count, (orbx_keypoint*)kps, desc, cap, n_per_frame, batch);
     }
