@@ -263,6 +263,7 @@ def main():
         mp2 = [d_mp, torch.empty_like(d_mp)]
         nm2 = [d_nm, torch.empty_like(d_nm)]
         ms = torch.cuda.Stream(device=dev)
+        matcher.set_footprint(True)  # leave wave slots / LDS to the concurrent extraction
         ev_ex = [[torch.cuda.Event() for _ in range(S)] for _ in range(2)]  # [buffer][lane]
         ev_m = [torch.cuda.Event(), torch.cuda.Event()]
         used = [False, False]

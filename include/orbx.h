@@ -247,6 +247,12 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
                                const float* scale_factors, int nlevels, float depth, float th,
                                int32_t* d_cur_mp, int32_t* d_nmatches, void* stream);
 
+/* Footprint of orbx_match_sequence_device's search kernel: 0 (default) = 1024 threads
+ * per problem with keypoint descriptors and query state in LDS (fastest alone); 1 =
+ * 256 threads and global-memory query state, for running concurrently with extraction
+ * on another stream (leaves wave slots and LDS to the other kernels).  Same results. */
+int orbx_matcher_set_footprint(orbx_matcher* m, int small);
+
 /* HIP-event timing of orbx_match_sequence_device: milliseconds averaged over the (up
  * to 64) most recent calls since orbx_matcher_set_timing(m, 1). */
 int orbx_matcher_set_timing(orbx_matcher* m, int enable);

@@ -34,7 +34,7 @@ EXPORTED = [
     "orbx_last_error", "orbx_matcher_create", "orbx_matcher_destroy", "orbx_search_by_projection_local",
     "orbx_search_by_projection_frame", "orbx_search_for_triangulation", "orbx_compute_stereo_matches",
     "orbx_match_sequence_device", "orbx_matcher_set_timing", "orbx_matcher_last_ms",
-    "orbx_search_by_projection_keyframe", "orbx_search_by_projection_sim3",
+    "orbx_search_by_projection_keyframe", "orbx_search_by_projection_sim3", "orbx_matcher_set_footprint",
 ]
 
 
@@ -107,6 +107,7 @@ def lib() -> C.CDLL:
     L.orbx_search_by_projection_keyframe.argtypes = [vp, vp, i32p, vp, i32p, u8p, vp, C.c_float, C.c_int, ip]
     L.orbx_search_by_projection_sim3.argtypes = [vp, vp, fp, i32p, C.c_int, i32p, vp, C.c_int, ip]
     L.orbx_matcher_set_timing.argtypes = [vp, C.c_int]
+    L.orbx_matcher_set_footprint.argtypes = [vp, C.c_int]
     L.orbx_matcher_last_ms.argtypes = [vp, fp]
     L.orbx_version.restype = C.c_char_p
     L.orbx_device_count.argtypes = [ip]

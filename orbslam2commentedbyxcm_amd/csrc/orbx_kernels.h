@@ -49,7 +49,8 @@ hipError_t launch_hamming_matrix(const uint8_t* a, int na, const uint8_t* b, int
                                  hipStream_t stream);
 
 hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned long long* scratch,
-                              const long long* d_scratch_off, int max_n, int max_nq, hipStream_t stream);
+                              const long long* d_scratch_off, int max_n, int max_nq, hipStream_t stream,
+                              bool small = false);
 
 hipError_t launch_seq_build(const SeqArgs& A, int npairs, ProjQuery* queries, ProjProblem* probs,
                             long long* scratch_off, hipStream_t stream);

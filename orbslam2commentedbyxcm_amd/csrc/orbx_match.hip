@@ -156,7 +156,8 @@ struct SortedGrid {
     const uint4* sdesc;     // 2 x uint4 per keypoint, or null (descriptors read from global)
 };
 
-constexpr int kProjThreads = 1024;
+constexpr int kProjThreads = 1024;      // default workgroup size of k_proj_search
+constexpr int kProjThreadsSmall = 256;  // small-footprint variant (overlapped with other work)
 constexpr int kTopK = 8;                   // candidate-list length per query
 constexpr unsigned kNoEntry = 0xffffffffu;  // no further candidate
 constexpr unsigned kTrunc = 0xfffffffeu;    // further candidates exist but are not listed
@@ -315,10 +316,11 @@ __device__ void score_rowk(const ProjProblem& pb, const ProjParams& P, const Que
 }
 
 // Ascending in-place bitonic sort of n2 (power of two) u32 keys by the workgroup.
+template <int NT>
 __device__ void block_bitonic_sort(unsigned* a, int n2) {
     for (int k = 2; k <= n2; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < n2; i += kProjThreads) {
+            for (int i = threadIdx.x; i < n2; i += NT) {
                 const int l = i ^ j;
                 if (l > i) {
                     const unsigned x = a[i], y = a[l];
@@ -373,15 +375,15 @@ struct ProjLds {
 // claimed again), so the first unblocked entries of a query's initial list are exactly
 // its best / second best against the current state while the list has them.
 // QLDS: per-query state in LDS; otherwise in the problem's global scratch.
-template <bool QLDS, bool DLDS>
-__global__ __launch_bounds__(kProjThreads) void k_proj_search(const ProjProblem* __restrict__ probs, ProjParams P,
+template <bool QLDS, bool DLDS, int NT>
+__global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restrict__ probs, ProjParams P,
                                                               unsigned long long* __restrict__ scratch,
                                                               const long long* __restrict__ scratch_off) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_hist[kHistoLength];
     const ProjProblem pb = probs[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr int kWaves = kProjThreads / 64;
+    constexpr int kWaves = NT / 64;
     const int n = pb.n, nq = pb.nq;
     unsigned long long* st = P.stamps ? P.stamps + 8 * blockIdx.x : nullptr;
     if (st && tid == 0) st[0] = wall_clock64();
@@ -411,7 +413,7 @@ __global__ __launch_bounds__(kProjThreads) void k_proj_search(const ProjProblem*
         mlist = (int*)(qang + nq);
         mbin = mlist + nq;
     }
-    for (int i = tid; i < n2; i += kProjThreads) {
+    for (int i = tid; i < n2; i += NT) {
         unsigned key = 0xffffffffu;
         if (i < n) {
             const orbx_keypoint& kp = pb.keys[i];
@@ -424,8 +426,8 @@ __global__ __launch_bounds__(kProjThreads) void k_proj_search(const ProjProblem*
     }
     if (tid < kHistoLength) s_hist[tid] = 0;
     __syncthreads();
-    block_bitonic_sort(skey, n2);
-    for (int p = tid; p < n; p += kProjThreads) {
+    block_bitonic_sort<NT>(skey, n2);
+    for (int p = tid; p < n; p += NT) {
         const int i = (int)(skey[p] & 0x1fffu);
         const orbx_keypoint& kp = pb.keys[i];
         skp[p] = make_float4(kp.x, kp.y, __int_as_float(kp.octave), kp.angle);
@@ -433,13 +435,13 @@ __global__ __launch_bounds__(kProjThreads) void k_proj_search(const ProjProblem*
         owner[p] = 0x7fffffff;
     }
     if (DLDS) {
-        for (int t = tid; t < 2 * n; t += kProjThreads) {
+        for (int t = tid; t < 2 * n; t += NT) {
             const int i = (int)(skey[t >> 1] & 0x1fffu);
             sdesc[t] = ((const uint4*)(pb.desc + (size_t)i * 32))[t & 1];
         }
     }
     // cstart[c] = first sorted position whose cell >= c (each cell written once)
-    for (int p = tid; p <= n; p += kProjThreads) {
+    for (int p = tid; p <= n; p += NT) {
         const int prev = p == 0 ? -1 : (int)(skey[p - 1] >> 13);
         const int cur = p == n ? kNumCells : (int)(skey[p] >> 13);
         const int hi = cur < kNumCells ? cur : kNumCells;
@@ -611,7 +613,7 @@ __global__ __launch_bounds__(kProjThreads) void k_proj_search(const ProjProblem*
         }
     }
     __syncthreads();
-    for (int p = tid; p < n; p += kProjThreads) pb.frame_mp[skey[p] & 0x1fffu] = sfmp[p];
+    for (int p = tid; p < n; p += NT) pb.frame_mp[skey[p] & 0x1fffu] = sfmp[p];
     if (st && tid == 0) st[4] = wall_clock64();
 }
 
@@ -690,15 +692,16 @@ hipError_t launch_seq_build(const SeqArgs& A, int npairs, ProjQuery* queries, Pr
 }
 
 hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned long long* scratch,
-                              const long long* d_scratch_off, int max_n, int max_nq, hipStream_t stream) {
+                              const long long* d_scratch_off, int max_n, int max_nq, hipStream_t stream, bool small) {
     if (nprob <= 0) return hipSuccess;
     if (max_n >= 8192) return hipErrorInvalidValue;  // 13-bit keypoint positions
     int n2 = 1;
     while (n2 < max_n) n2 <<= 1;
     const size_t limit = 160 * 1024 - 256;  // minus the static histogram
-    // Prefer LDS-resident descriptors (the scoring loads), then LDS-resident query state.
-    bool dlds = true, qlds = true;
-    if (ProjLds(max_n, n2, max_nq, true, true).total > limit) {
+    // Fast: LDS-resident descriptors (the scoring loads), then LDS-resident query state,
+    // 1024 threads.  Small (meant to run beside other kernels): neither, 256 threads.
+    bool dlds = !small, qlds = !small;
+    if (!small && ProjLds(max_n, n2, max_nq, true, true).total > limit) {
         qlds = false;
         if (ProjLds(max_n, n2, max_nq, true, false).total > limit) {
             dlds = false;
@@ -707,14 +710,20 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
     }
     const size_t lds = ProjLds(max_n, n2, max_nq, dlds, qlds).total;
     if (lds > limit) return hipErrorInvalidValue;
-    const void* fn = qlds ? (dlds ? (const void*)k_proj_search<true, true> : (const void*)k_proj_search<true, false>)
-                          : (dlds ? (const void*)k_proj_search<false, true> : (const void*)k_proj_search<false, false>);
+    const void* fn;
+    if (small)
+        fn = (const void*)k_proj_search<false, false, kProjThreadsSmall>;
+    else
+        fn = qlds ? (dlds ? (const void*)k_proj_search<true, true, kProjThreads>
+                          : (const void*)k_proj_search<true, false, kProjThreads>)
+                  : (dlds ? (const void*)k_proj_search<false, true, kProjThreads>
+                          : (const void*)k_proj_search<false, false, kProjThreads>);
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
     void* args[] = {(void*)&d_probs, (void*)&P, (void*)&scratch, (void*)&d_scratch_off};
-    return hipLaunchKernel(fn, dim3(nprob), dim3(kProjThreads), args, lds, stream);
+    return hipLaunchKernel(fn, dim3(nprob), dim3(small ? kProjThreadsSmall : kProjThreads), args, lds, stream);
 }
 
 // ------------------------------------------------------------------ triangulation

@@ -108,6 +108,7 @@ struct orbx_matcher {
     bool timing = false;
     hipEvent_t ev[kRing][2] = {};
     long long ncalls = 0;
+    bool small = false;  // orbx_matcher_set_footprint
 };
 
 namespace {
@@ -507,7 +508,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
         HIP_TRY(hipMalloc(&d_st, sizeof(unsigned long long) * 8 * npairs));
         P.stamps = d_st;
     }
-    HIP_TRY(launch_proj_search(d_prob, npairs, P, d_scr, d_off, cap, cap, s));
+    HIP_TRY(launch_proj_search(d_prob, npairs, P, d_scr, d_off, cap, cap, s, m->small));
     if (m->timing) {
         HIP_TRY(hipEventRecord(ev[1], s));
         m->ncalls++;
@@ -538,6 +539,12 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
                 npairs, (double)(t1 - t0) * 0.01, ph[0] / npairs, mx[0], ph[1] / npairs, mx[1], ph[2] / npairs, mx[2],
                 ph[3] / npairs, mx[3], resc / npairs, nq / npairs, nit / npairs);
     }
+    return ORBX_OK;
+}
+
+int orbx_matcher_set_footprint(orbx_matcher* m, int small) {
+    if (!m) return fail(ORBX_ERR_ARG, "null matcher");
+    m->small = small != 0;
     return ORBX_OK;
 }
 

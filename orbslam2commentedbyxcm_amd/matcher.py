@@ -277,6 +277,11 @@ class ORBmatcher:
     def set_timing(self, enable: bool = True) -> None:
         L.check(L.lib().orbx_matcher_set_timing(self._h, 1 if enable else 0))
 
+    def set_footprint(self, small: bool) -> None:
+        """small=True: the batched sequence search uses 256 threads and global query
+        state, to run beside extraction on another stream (orbx_matcher_set_footprint)."""
+        L.check(L.lib().orbx_matcher_set_footprint(self._h, 1 if small else 0))
+
     def last_ms(self) -> float:
         t = C.c_float()
         L.check(L.lib().orbx_matcher_last_ms(self._h, C.byref(t)))

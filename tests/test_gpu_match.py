@@ -164,8 +164,10 @@ def test_descriptor_distance_and_windows(oracle, orbx_built):
                 assert res["second_dist"][i] == d[order[1]] and res["second_level"][i] == lv[c[order[1]]]
 
 
-def test_match_sequence_device(oracle, orbx_built):
-    """Batched frame-to-frame matching on device-resident frames == per-pair oracle."""
+@pytest.mark.parametrize("small", [False, True])
+def test_match_sequence_device(oracle, orbx_built, small):
+    """Batched frame-to-frame matching on device-resident frames == per-pair oracle
+    (both kernel footprints: 1024 threads + LDS state, 256 threads + global state)."""
     import torch
 
     from orbslam2commentedbyxcm_amd.matcher import MapPoints
@@ -191,6 +193,7 @@ def test_match_sequence_device(oracle, orbx_built):
     d_nm = torch.empty((B,), dtype=torch.int32, device=dev)
     sf = ex.GetScaleFactors()
     m = ORBmatcher(0.9, True)
+    m.set_footprint(small)
     m.match_sequence_device(d_kps, d_desc, d_n, d_T, d_mp, d_nm, sf, fx, fy, cx, cy, 640, 480, depth=z, th=15.0,
                             stream=ex.stream_handle())
     torch.cuda.synchronize()
