@@ -10,7 +10,10 @@ from pathlib import Path
 
 import numpy as np
 
-LIB_PATH = Path(__file__).resolve().parent / "liborbx.so"
+import os
+
+# ORBX_LIB: alternative build of the library (A/B measurements of kernel variants)
+LIB_PATH = Path(os.environ.get("ORBX_LIB", str(Path(__file__).resolve().parent / "liborbx.so")))
 
 ORBX_OK = 0
 ORBX_EMPTY = 1
