@@ -279,6 +279,63 @@ int orbx_compute_stereo_matches(orbx_matcher* m, orbx_extractor* ex, int left_fr
                                 const uint8_t* desc_r, int n_right, float max_disparity, float* u_right,
                                 float* depth);
 
+/* ---- DBoW2 vocabulary (TemplatedVocabulary<FORB::TDescriptor, FORB>, §8(f) rank 1) ----
+ * The tree lives in HBM as its CSR edge list.  Scoring / weighting
+ * codes are DBoW2's enums (BowVector.h:29-56): scoring L1_NORM 0, L2_NORM 1,
+ * CHI_SQUARE 2, KL 3, BHATTACHARYYA 4, DOT_PRODUCT 5; weighting TF_IDF 0, TF 1, IDF 2,
+ * BINARY 3. */
+typedef struct orbx_vocabulary orbx_vocabulary;
+
+/* TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1338-1424; called by
+ * System.cc:67): header "k L scoring weighting", then one node per line "parent
+ * isLeaf d0..d31 weight".  Same header range checks; empty lines are skipped (the
+ * reference turns a trailing one into a root child with an uninitialised descriptor);
+ * a malformed node line or a parent id that does not precede the node is ORBX_ERR_ARG. */
+int orbx_vocabulary_load_text_file(const char* path, int device, orbx_vocabulary** out);
+/* Same from an in-memory text of `len` bytes. */
+int orbx_vocabulary_load_text(const char* text, size_t len, int device, orbx_vocabulary** out);
+void orbx_vocabulary_destroy(orbx_vocabulary* voc);
+/* m_k, m_L, m_scoring, m_weighting, node count (incl. root), size() (words). */
+int orbx_vocabulary_info(const orbx_vocabulary* voc, int* k, int* L, int* scoring, int* weighting, int* nnodes,
+                         int* nwords);
+/* The vocabulary's hipStream_t (as void*). */
+void* orbx_vocabulary_stream(orbx_vocabulary* voc);
+
+/* TemplatedVocabulary::transform(feature, word_id, weight, nid, levelsup)
+ * (TemplatedVocabulary.h:1220-1259) for n descriptors (host buffers, n x 32 B).
+ * node may be NULL.  A leaf reached above level L - levelsup reports the deepest
+ * node (the reference leaves nid unset there). */
+int orbx_vocabulary_transform_features(orbx_vocabulary* voc, const uint8_t* desc, int n, int levelsup,
+                                       int32_t* word, double* weight, int32_t* node);
+
+/* TemplatedVocabulary::transform(features, BowVector&, FeatureVector&, levelsup)
+ * (TemplatedVocabulary.h:1127-1186) for one frame of n <= 8192 descriptors (host
+ * buffers), as called by Frame::ComputeBoW / KeyFrame::ComputeBoW with levelsup 4
+ * (Frame.cc:573-583, KeyFrame.cc:66-74).  BowVector: (bow_word[j], bow_value[j]),
+ * j < *nbow, ascending words.  FeatureVector: node fv_node[j] (ascending) holds the
+ * features fv_idx[fv_off[j] .. fv_off[j+1]) (ascending), j < *nfv.  Capacities: n
+ * entries, fv_off n + 1. */
+int orbx_vocabulary_transform(orbx_vocabulary* voc, const uint8_t* desc, int n, int levelsup, int32_t* bow_word,
+                              double* bow_value, int* nbow, int32_t* fv_node, int32_t* fv_off, int32_t* fv_idx,
+                              int* nfv);
+
+/* Batched device path over the orbx_extract_batch_device layout: frame b's
+ * descriptors at d_desc + b*cap*32, min(d_n[b], cap) of them, cap <= 8192.  Outputs
+ * (device) per frame: d_bow_word / d_bow_value / d_fv_node / d_fv_idx [B][cap],
+ * d_fv_off [B][cap+1], d_nbow / d_nfv [B]; optional d_feat_word / d_feat_node [B][cap]
+ * (the word and level-(L - levelsup) node of every feature; NULL = not wanted).
+ * Asynchronous on `stream` (or the vocabulary's stream). */
+int orbx_vocabulary_transform_batch_device(orbx_vocabulary* voc, int batch, const uint8_t* d_desc,
+                                           const int32_t* d_n, int cap, int levelsup, int32_t* d_feat_word,
+                                           int32_t* d_feat_node, int32_t* d_bow_word, double* d_bow_value,
+                                           int32_t* d_nbow, int32_t* d_fv_node, int32_t* d_fv_off,
+                                           int32_t* d_fv_idx, int32_t* d_nfv, void* stream);
+
+/* HIP-event timing of transform calls (events on the launch stream), averaged over
+ * the (up to 64) most recent calls: the tree walk and the per-frame vector build. */
+int orbx_vocabulary_set_timing(orbx_vocabulary* voc, int enable);
+int orbx_vocabulary_stage_times(orbx_vocabulary* voc, float* walk_ms, float* frame_ms);
+
 /* Library / device info. */
 const char* orbx_version(void);
 int orbx_device_count(int* n);

@@ -360,3 +360,50 @@ def compute_stereo_matches(left, keys_r, desc_r, levels_l, levels_r, maxD):
                                  w.ctypes.data_as(I32P), h.ctypes.data_as(I32P), inv.ctypes.data_as(F32P), maxD,
                                  ur.ctypes.data_as(F32P), dp.ctypes.data_as(F32P))
     return ur[:n].copy(), dp[:n].copy()
+
+
+# ---- DBoW2 vocabulary transform (orbx_oracle_vocab.c) --------------------------------
+class OraVocab(C.Structure):
+    _fields_ = [("k", C.c_int), ("L", C.c_int), ("scoring", C.c_int), ("weighting", C.c_int),
+                ("nnodes", C.c_int), ("nwords", C.c_int), ("desc", C.c_void_p), ("parent", C.c_void_p),
+                ("child_off", C.c_void_p), ("child", C.c_void_p), ("word_id", C.c_void_p),
+                ("weight", C.c_void_p)]
+
+
+class Vocab:
+    """CPU restatement of TemplatedVocabulary::loadFromTextFile + transform."""
+
+    def __init__(self, text: str | bytes):
+        b = text.encode() if isinstance(text, str) else bytes(text)
+        L = lib()
+        L.ora_vocab_load_text.argtypes = [C.POINTER(OraVocab), C.c_char_p, C.c_size_t]
+        L.ora_vocab_free.argtypes = [C.POINTER(OraVocab)]
+        L.ora_vocab_free.restype = None
+        self.v = OraVocab()
+        self.ok = L.ora_vocab_load_text(C.byref(self.v), b, len(b)) == 0
+
+    def __del__(self):
+        if getattr(self, "ok", False):
+            lib().ora_vocab_free(C.byref(self.v))
+            self.ok = False
+
+    def transform(self, desc: np.ndarray, levelsup: int = 4):
+        """-> (bow_word, bow_value, fv_node, fv_off, fv_idx) arrays."""
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(d)
+        cap = max(n, 1)
+        bw = np.zeros(cap, np.int32)
+        bv = np.zeros(cap, np.float64)
+        fn = np.zeros(cap, np.int32)
+        fo = np.zeros(cap + 1, np.int32)
+        fi = np.zeros(cap, np.int32)
+        nb, nf = C.c_int(), C.c_int()
+        L = lib()
+        DP = C.POINTER(C.c_double)
+        L.ora_vocab_transform.argtypes = [C.POINTER(OraVocab), U8P, C.c_int, C.c_int, I32P, DP, C.POINTER(C.c_int),
+                                          I32P, I32P, I32P, C.POINTER(C.c_int)]
+        L.ora_vocab_transform(C.byref(self.v), d.ctypes.data_as(U8P), n, int(levelsup), bw.ctypes.data_as(I32P),
+                              bv.ctypes.data_as(DP), C.byref(nb), fn.ctypes.data_as(I32P), fo.ctypes.data_as(I32P),
+                              fi.ctypes.data_as(I32P), C.byref(nf))
+        nb, nf = nb.value, nf.value
+        return bw[:nb].copy(), bv[:nb].copy(), fn[:nf].copy(), fo[:nf + 1].copy(), fi[:fo[nf]].copy()

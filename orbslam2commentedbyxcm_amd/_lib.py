@@ -38,6 +38,10 @@ EXPORTED = [
     "orbx_search_by_projection_frame", "orbx_search_for_triangulation", "orbx_compute_stereo_matches",
     "orbx_match_sequence_device", "orbx_matcher_set_timing", "orbx_matcher_last_ms",
     "orbx_search_by_projection_keyframe", "orbx_search_by_projection_sim3", "orbx_matcher_set_footprint",
+    "orbx_vocabulary_load_text_file", "orbx_vocabulary_load_text", "orbx_vocabulary_destroy",
+    "orbx_vocabulary_info", "orbx_vocabulary_stream", "orbx_vocabulary_transform_features",
+    "orbx_vocabulary_transform", "orbx_vocabulary_transform_batch_device", "orbx_vocabulary_set_timing",
+    "orbx_vocabulary_stage_times",
 ]
 
 
@@ -112,6 +116,19 @@ def lib() -> C.CDLL:
     L.orbx_matcher_set_timing.argtypes = [vp, C.c_int]
     L.orbx_matcher_set_footprint.argtypes = [vp, C.c_int]
     L.orbx_matcher_last_ms.argtypes = [vp, fp]
+    dp = C.POINTER(C.c_double)
+    L.orbx_vocabulary_load_text_file.argtypes = [C.c_char_p, C.c_int, C.POINTER(vp)]
+    L.orbx_vocabulary_load_text.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.POINTER(vp)]
+    L.orbx_vocabulary_destroy.argtypes = [vp]
+    L.orbx_vocabulary_destroy.restype = None
+    L.orbx_vocabulary_info.argtypes = [vp, ip, ip, ip, ip, ip, ip]
+    L.orbx_vocabulary_stream.argtypes = [vp]
+    L.orbx_vocabulary_stream.restype = vp
+    L.orbx_vocabulary_transform_features.argtypes = [vp, u8p, C.c_int, C.c_int, i32p, dp, i32p]
+    L.orbx_vocabulary_transform.argtypes = [vp, u8p, C.c_int, C.c_int, i32p, dp, ip, i32p, i32p, i32p, ip]
+    L.orbx_vocabulary_transform_batch_device.argtypes = [vp, C.c_int, vp, vp, C.c_int, C.c_int] + [vp] * 9 + [vp]
+    L.orbx_vocabulary_set_timing.argtypes = [vp, C.c_int]
+    L.orbx_vocabulary_stage_times.argtypes = [vp, fp, fp]
     L.orbx_version.restype = C.c_char_p
     L.orbx_device_count.argtypes = [ip]
     L.orbx_last_error.restype = C.c_char_p

@@ -1,0 +1,180 @@
+"""Synthetic DBoW2 vocabularies and query descriptors (no ORBvoc.txt ships with the
+reference), plus a pure-Python restatement of TemplatedVocabulary::transform used to
+cross-check the C oracle on small cases."""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from orbslam2commentedbyxcm_amd.vocabulary import save_text
+
+
+class Tree:
+    def __init__(self, k, L, scoring, weighting):
+        self.k, self.L, self.scoring, self.weighting = k, L, scoring, weighting
+        self.parent, self.leaf, self.desc, self.weight = [], [], [], []  # non-root nodes in file order
+
+    def text(self) -> str:
+        return save_text(self.k, self.L, self.scoring, self.weighting, self.parent, self.leaf, self.desc,
+                         self.weight)
+
+
+def _flip(rng, d, nbits):
+    bits = np.unpackbits(d)
+    idx = rng.choice(256, size=nbits, replace=False)
+    bits[idx] ^= 1
+    return np.packbits(bits)
+
+
+def make_vocab(seed: int, k: int = 10, L: int = 3, scoring: int = 0, weighting: int = 0, irregular: bool = False,
+               tie_frac: float = 0.0, stop_frac: float = 0.05, shuffle: bool = False) -> Tree:
+    """k-ary tree of depth L: child descriptors are bit-flipped copies of the parent's
+    (fewer flips deeper), so nearby queries descend to nearby leaves.  irregular:
+    1..k children per node and early leaves; tie_frac: siblings duplicating an
+    earlier sibling's descriptor (first one must win); stop_frac: leaves with weight 0
+    (stopped words); shuffle: parents still precede children but siblings are
+    interleaved in the file."""
+    rng = np.random.default_rng(seed)
+    t = Tree(k, L, scoring, weighting)
+    # build nodes: (id, parent, depth, desc)
+    root_desc = rng.integers(0, 256, 32, dtype=np.uint8)
+    nodes = [(0, -1, 0, root_desc)]
+    children = {0: []}
+    frontier = [0]
+    for depth in range(1, L + 1):
+        nxt = []
+        for p in frontier:
+            pdesc = nodes[p][3]
+            if irregular and depth > 1 and rng.random() < 0.15:
+                continue  # p stays a leaf above level L
+            nk = int(rng.integers(1, k + 1)) if irregular else k
+            flips = max(2, 96 >> (depth - 1))
+            sib = []
+            for _ in range(nk):
+                if sib and rng.random() < tie_frac:
+                    d = sib[int(rng.integers(0, len(sib)))].copy()
+                else:
+                    d = _flip(rng, pdesc, flips)
+                sib.append(d)
+                cid = len(nodes)
+                nodes.append((cid, p, depth, d))
+                children.setdefault(p, []).append(cid)
+                children[cid] = []
+                nxt.append(cid)
+        frontier = nxt
+    # file order: BFS (as the reference's creation order keeps siblings together) or an
+    # interleaved topological order
+    order = [n[0] for n in nodes[1:]]
+    if shuffle:
+        order = []
+        ready = list(children[0])
+        while ready:  # any node whose parent is out; the file order then defines sibling order
+            c = ready.pop(int(rng.integers(0, len(ready))))
+            order.append(c)
+            ready.extend(children[c])
+    newid = {0: 0}
+    for i, c in enumerate(order):
+        newid[c] = i + 1
+    for c in order:
+        _, p, depth, d = nodes[c]
+        is_leaf = len(children[c]) == 0
+        t.parent.append(newid[p])
+        t.leaf.append(1 if is_leaf else 0)
+        t.desc.append(d)
+        if is_leaf:
+            # as written by saveToTextFile (precision 6) and read back
+            w = 0.0 if rng.random() < stop_frac else float(f"{rng.uniform(0.05, 6.0):g}")
+        else:
+            w = 0.0
+        t.weight.append(w)
+    return t
+
+
+def queries(seed: int, tree: Tree, n: int, dup_frac: float = 0.2) -> np.ndarray:
+    """Descriptors near random leaves (a few bits flipped), some exact repeats (same
+    word several times in a frame), some uniformly random."""
+    rng = np.random.default_rng(seed)
+    leaves = [i for i, lf in enumerate(tree.leaf) if lf]
+    out = np.zeros((n, 32), np.uint8)
+    for i in range(n):
+        r = rng.random()
+        if i > 0 and r < dup_frac:
+            out[i] = out[int(rng.integers(0, i))]
+        elif r < 0.9 and leaves:
+            out[i] = _flip(rng, tree.desc[leaves[int(rng.integers(0, len(leaves)))]], int(rng.integers(0, 24)))
+        else:
+            out[i] = rng.integers(0, 256, 32, dtype=np.uint8)
+    return out
+
+
+# ---- pure-Python restatement (small cases) -------------------------------------------
+def _popcount(a: np.ndarray, b: np.ndarray) -> int:
+    return int(np.unpackbits(np.bitwise_xor(a, b)).sum())
+
+
+def py_transform(tree: Tree, desc: np.ndarray, levelsup: int):
+    """TemplatedVocabulary.h:1127-1259 + BowVector.cpp + FeatureVector.cpp in plain
+    Python (std::map -> dict sorted at the end)."""
+    n_nodes = len(tree.parent) + 1
+    kids = {i: [] for i in range(n_nodes)}
+    for i, p in enumerate(tree.parent):
+        kids[p].append(i + 1)
+    word_of, wid = {}, 0
+    for i, lf in enumerate(tree.leaf):
+        if lf:
+            word_of[i + 1] = wid
+            wid += 1
+    if wid == 0:
+        return {}, {}
+    nid_level = tree.L - levelsup
+    bow, fv = {}, {}
+    for f, q in enumerate(desc):
+        node, level, nid = 0, 0, 0
+        while True:
+            level += 1
+            cs = kids[node]
+            best, bd = cs[0], _popcount(q, tree.desc[cs[0] - 1])
+            for c in cs[1:]:
+                d = _popcount(q, tree.desc[c - 1])
+                if d < bd:
+                    best, bd = c, d
+            node = best
+            if level <= nid_level:
+                nid = node
+            if not kids[node]:
+                break
+        if nid_level <= 0:
+            nid = 0
+        w = tree.weight[node - 1]
+        word = word_of.get(node, 0)
+        if w > 0:
+            if tree.weighting in (0, 1):
+                bow[word] = bow[word] + w if word in bow else w
+            else:
+                bow.setdefault(word, w)
+            fv.setdefault(nid, []).append(f)
+    words = sorted(bow)
+    must = tree.scoring != 5
+    if must:
+        if tree.scoring == 1:
+            s = 0.0
+            for w in words:
+                s += bow[w] * bow[w]
+            s = math.sqrt(s)
+        else:
+            s = 0.0
+            for w in words:
+                s += abs(bow[w])
+        if s > 0:
+            bow = {w: bow[w] / s for w in words}
+    elif tree.weighting in (0, 1) and words:
+        nd = float(len(words))
+        bow = {w: bow[w] / nd for w in words}
+    return {w: bow[w] for w in sorted(bow)}, {k2: fv[k2] for k2 in sorted(fv)}
+
+
+def arrays_to_maps(bw, bv, fn, fo, fi):
+    bow = {int(w): float(v) for w, v in zip(bw, bv)}
+    fv = {int(nd): [int(x) for x in fi[fo[j]:fo[j + 1]]] for j, nd in enumerate(fn)}
+    return bow, fv
