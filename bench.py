@@ -86,7 +86,7 @@ def pmc_traffic(stage: str):
     """HBM bytes per launch of `stage` from the newest committed PMC summary
     (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate FETCH_SIZE /
     WRITE_SIZE rocprofv3 passes of this bench), or (None, None)."""
-    files = sorted((ROOT / "profiles").glob("*_pmc_traffic.json"))
+    files = sorted(f for f in (ROOT / "profiles").glob("*_pmc_traffic.json") if "vocab" not in f.name)
     if not files:
         return None, None
     ks = json.loads(files[-1].read_text())["kernels"]

@@ -380,11 +380,12 @@ class Vocab:
         L.ora_vocab_free.argtypes = [C.POINTER(OraVocab)]
         L.ora_vocab_free.restype = None
         self.v = OraVocab()
+        self._free = L.ora_vocab_free
         self.ok = L.ora_vocab_load_text(C.byref(self.v), b, len(b)) == 0
 
     def __del__(self):
         if getattr(self, "ok", False):
-            lib().ora_vocab_free(C.byref(self.v))
+            self._free(C.byref(self.v))
             self.ok = False
 
     def transform(self, desc: np.ndarray, levelsup: int = 4):

@@ -5,14 +5,17 @@
 // the children of node p occupy edge slots [off(p), off(p) + cnt(p)) in file order, so
 // one node's k child descriptors are one contiguous 32*k-byte run.  Per edge slot:
 //   edesc  2 x uint4   the child's 256-bit descriptor
-//   enext  int2        (off, cnt) of the child's own children; cnt == 0 -> leaf
-//   enode  int         the child's node id
-// plus per node word id (int) and weight (double).  ORBvoc.txt (k=10, L=6, ~1.1M nodes)
-// is ~50 MB in this form: the upper levels stay in L2, the rest in the Infinity Cache.
+//   einfo  int4        (off, cnt) of the child's own children (cnt == 0 -> leaf), the
+//                      child's node id and word id
+//   eweight double     the child's weight
+// ORBvoc.txt (k=10, L=6, ~1.1M nodes) is ~62 MB in this form: the upper levels stay in
+// L2, the rest in the Infinity Cache.
 //
 // k_vocab_walk: one 16-lane row per descriptor (four per wave), one lane per child.
 //   Each level is a 16-wide Hamming + DPP row minimum of (distance << 16 | child),
 //   so ties resolve to the first child in file order like the reference's strict '<'.
+//   Every lane loads its child's einfo together with the descriptor and the winner's
+//   is taken by lane shuffle, so a level costs one dependent global load, not two.
 // k_vocab_frame: one workgroup per frame builds the BowVector (word -> value map,
 //   BowVector.cpp) and FeatureVector (node -> ascending feature indices,
 //   FeatureVector.cpp:31-45) from the per-feature words: LDS bitonic sort of
@@ -35,6 +38,7 @@
 
 using namespace orbx;
 
+namespace orbx {
 namespace {
 
 constexpr int kVocMaxCap = 8192;   // features per frame in one transform (LDS sort size)
@@ -42,6 +46,8 @@ constexpr int kFrameThreads = 1024;
 constexpr int kWalkThreads = 256;  // 16 descriptors per block
 
 __device__ __forceinline__ unsigned umin_(unsigned a, unsigned b) { return a < b ? a : b; }
+
+}  // namespace
 
 // Minimum over each 16-lane DPP row, broadcast to the row (quad_perm x2, half mirror,
 // mirror).
@@ -55,10 +61,8 @@ __device__ __forceinline__ unsigned row_min16(unsigned v) {
 
 struct VocDev {
     const uint4* edesc;
-    const int2* enext;
-    const int* enode;
-    const int* word;
-    const double* weight;
+    const int4* einfo;
+    const double* eweight;
     int root_cnt;
     int max_depth;
 };
@@ -80,33 +84,41 @@ __global__ __launch_bounds__(kWalkThreads) void k_vocab_walk(VocDev V, const uin
     const size_t slot = (size_t)b * cap + (live ? i : 0);
     const uint4* q = (const uint4*)(desc + slot * 32);
     const uint4 q0 = q[0], q1 = q[1];
-    int off = 0, cnt = V.root_cnt, node = 0, nid = 0;
+    int off = 0, cnt = V.root_cnt, node = 0, nid = 0, word = 0, e = -1;
+    const int rowbase = threadIdx.x & ~15;
     // Each row leaves at its leaf; off/cnt are row-uniform, so a row's 16 lanes stay
-    // converged for the DPP minimum.  max_depth bounds the walk.
+    // converged for the DPP minimum and the shuffles.  max_depth bounds the walk.
     for (int level = 1; level <= V.max_depth && cnt > 0; level++) {
         unsigned best = 0xffffffffu;
+        int4 mine = make_int4(0, 0, 0, 0);  // einfo of this lane's best child
         for (int c0 = 0; c0 < cnt; c0 += 16) {
             const int j = c0 + sub;
             if (j < cnt) {
-                const uint4* e = V.edesc + 2 * (size_t)(off + j);
-                const uint4 a = e[0], c = e[1];
+                const uint4* ed = V.edesc + 2 * (size_t)(off + j);
+                const uint4 a = ed[0], c = ed[1];
+                const int4 inf = V.einfo[off + j];
                 const unsigned d = __popc(a.x ^ q0.x) + __popc(a.y ^ q0.y) + __popc(a.z ^ q0.z) +
                                    __popc(a.w ^ q0.w) + __popc(c.x ^ q1.x) + __popc(c.y ^ q1.y) +
                                    __popc(c.z ^ q1.z) + __popc(c.w ^ q1.w);
-                best = umin_(best, d << 16 | (unsigned)j);
+                const unsigned key = d << 16 | (unsigned)j;
+                if (key < best) {
+                    best = key;
+                    mine = inf;
+                }
             }
         }
         best = row_min16(best);
-        const int e = off + (int)(best & 0xffffu);
-        const int2 nx = V.enext[e];
-        node = V.enode[e];
+        const int src = rowbase | (int)(best & 15u);  // the lane that scored the winner
+        e = off + (int)(best & 0xffffu);
+        off = __shfl(mine.x, src, 64);
+        cnt = __shfl(mine.y, src, 64);
+        node = __shfl(mine.z, src, 64);
+        word = __shfl(mine.w, src, 64);
         if (level <= nid_level) nid = node;  // leaf above nid_level: deepest node
-        off = nx.x;
-        cnt = nx.y;
     }
     if (live && sub == 0) {
-        feat_word[slot] = V.word[node];
-        feat_weight[slot] = V.weight[node];
+        feat_word[slot] = word;
+        feat_weight[slot] = e >= 0 ? V.eweight[e] : 0.0;
         if (feat_node) feat_node[slot] = nid_level <= 0 ? 0 : nid;
     }
 }
@@ -138,21 +150,65 @@ __device__ int block_scan(int v, int* s_wave, int& excl) {
     return total;
 }
 
-__device__ void bitonic_sort(unsigned long long* s, int np) {
-    for (int k = 2; k <= np; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < np; i += kFrameThreads) {
-                const int ij = i ^ j;
-                if (ij > i) {
-                    const unsigned long long a = s[i], c = s[ij];
-                    if ((a > c) == ((i & k) == 0)) {
-                        s[i] = c;
-                        s[ij] = a;
-                    }
+__device__ __forceinline__ unsigned long long shfl_xor64(unsigned long long v, int j) {
+    const int lo = __shfl_xor((int)(unsigned)v, j, 64), hi = __shfl_xor((int)(unsigned)(v >> 32), j, 64);
+    return (unsigned long long)(unsigned)hi << 32 | (unsigned)lo;
+}
+
+// Register stages of a bitonic merge: partner distances j < 64 live in the same wave
+// (element e*1024 + t sits in lane t & 63), so they run as lane shuffles with no
+// barrier.  New value of element i: min of (i, i^j) when "i is the lower index" agrees
+// with "block k ascending", else max.
+__device__ __forceinline__ void reg_stages(unsigned long long (&r)[kVocMaxCap / kFrameThreads], int ne, int k,
+                                           int jtop) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int j = 32; j > 0; j >>= 1) {
+        if (j > jtop) continue;
+#pragma unroll
+        for (int e = 0; e < kVocMaxCap / kFrameThreads; e++) {
+            if (e < ne) {
+                const unsigned long long v = r[e], p = shfl_xor64(v, j);
+                const int i = e * kFrameThreads + t;
+                const bool lower = (t & j) == 0, asc = (i & k) == 0;
+                r[e] = (lower == asc) ? (v < p ? v : p) : (v < p ? p : v);
+            }
+        }
+    }
+}
+
+// Bitonic sort of m = ne * 1024 keys (ne = 1..8; r[e] holds element e*1024 + t) into
+// s[0, m): merge distances >= 64 in place in LDS (one barrier each), the rest in
+// registers.  Ends with the sorted keys in s and a barrier.
+__device__ void bitonic_sort(unsigned long long (&r)[kVocMaxCap / kFrameThreads], int ne,
+                             unsigned long long* s) {
+    const int t = threadIdx.x, m = ne * kFrameThreads;
+    for (int k = 2; k <= 64; k <<= 1) reg_stages(r, ne, k, k >> 1);
+#pragma unroll
+    for (int e = 0; e < kVocMaxCap / kFrameThreads; e++)
+        if (e < ne) s[e * kFrameThreads + t] = r[e];
+    __syncthreads();
+    for (int k = 128; k <= m; k <<= 1) {
+        for (int j = k >> 1; j >= 64; j >>= 1) {
+            for (int q = t; q < m / 2; q += kFrameThreads) {
+                const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1));
+                const unsigned long long a = s[i], c = s[i + j];
+                if ((a > c) == ((i & k) == 0)) {
+                    s[i] = c;
+                    s[i + j] = a;
                 }
             }
             __syncthreads();
         }
+#pragma unroll
+        for (int e = 0; e < kVocMaxCap / kFrameThreads; e++)
+            if (e < ne) r[e] = s[e * kFrameThreads + t];
+        reg_stages(r, ne, k, 32);
+#pragma unroll
+        for (int e = 0; e < kVocMaxCap / kFrameThreads; e++)
+            if (e < ne) s[e * kFrameThreads + t] = r[e];
+        __syncthreads();
+    }
 }
 
 // Run heads of the sorted keys s[0, nw): each thread owns `per` consecutive entries.
@@ -196,18 +252,25 @@ __global__ __launch_bounds__(kFrameThreads) void k_vocab_frame(const int32_t* __
     const int b = blockIdx.x;
     const int n = min(nper[b], cap);
     const size_t base = (size_t)b * cap;
-    const int per = (np + kFrameThreads - 1) / kFrameThreads;
+    // this frame's sort size: the next power of two >= n, at least 1024 (one key per thread)
+    int ne = 1;
+    while (ne * kFrameThreads < n) ne <<= 1;
+    const int m = ne * kFrameThreads;
+    const int per = ne;
+    unsigned long long r[kVocMaxCap / kFrameThreads];
 
     // ---- BowVector: sort (word, feature) over non-stopped features
-    for (int i = threadIdx.x; i < np; i += kFrameThreads)
-        s_key[i] = (i < n && feat_weight[base + i] > 0)
-                       ? ((unsigned long long)(unsigned)feat_word[base + i] << 32 | (unsigned)i)
-                       : ~0ull;
+#pragma unroll
+    for (int e = 0; e < kVocMaxCap / kFrameThreads; e++) {
+        const int i = e * kFrameThreads + threadIdx.x;
+        r[e] = (e < ne && i < n && feat_weight[base + i] > 0)
+                   ? ((unsigned long long)(unsigned)feat_word[base + i] << 32 | (unsigned)i)
+                   : ~0ull;
+    }
     if (threadIdx.x == 0) s_nw = 0;
-    __syncthreads();
-    bitonic_sort(s_key, np);
-    for (int i = threadIdx.x; i < np; i += kFrameThreads)
-        if (s_key[i] != ~0ull && (i + 1 == np || s_key[i + 1] == ~0ull)) s_nw = i + 1;
+    bitonic_sort(r, ne, s_key);
+    for (int i = threadIdx.x; i < m; i += kFrameThreads)
+        if (s_key[i] != ~0ull && (i + 1 == m || s_key[i + 1] == ~0ull)) s_nw = i + 1;
     __syncthreads();
     const int nw = s_nw;
     // s_val[p] = value of run p; runs summed in feature order (addWeight) or first (addIfNotExist)
@@ -241,15 +304,17 @@ __global__ __launch_bounds__(kFrameThreads) void k_vocab_frame(const int32_t* __
     __syncthreads();
 
     // ---- FeatureVector: sort (node, feature) over the same features
-    for (int i = threadIdx.x; i < np; i += kFrameThreads)
-        s_key[i] = (i < n && feat_weight[base + i] > 0)
-                       ? ((unsigned long long)(unsigned)feat_node[base + i] << 32 | (unsigned)i)
-                       : ~0ull;
-    __syncthreads();
-    bitonic_sort(s_key, np);
+#pragma unroll
+    for (int e = 0; e < kVocMaxCap / kFrameThreads; e++) {
+        const int i = e * kFrameThreads + threadIdx.x;
+        r[e] = (e < ne && i < n && feat_weight[base + i] > 0)
+                   ? ((unsigned long long)(unsigned)feat_node[base + i] << 32 | (unsigned)i)
+                   : ~0ull;
+    }
+    bitonic_sort(r, ne, s_key);
     for (int i = threadIdx.x; i < nw; i += kFrameThreads) O.fv_idx[base + i] = (int32_t)(unsigned)s_key[i];
     const int nf = scan_heads(s_key, nw, per, s_wave, [&](int p, int i) {
-        O.fv_node[b * (size_t)(cap + 1) + p] = (int32_t)(s_key[i] >> 32);
+        O.fv_node[base + p] = (int32_t)(s_key[i] >> 32);
         O.fv_off[b * (size_t)(cap + 1) + p] = i;
     });
     if (threadIdx.x == 0) {
@@ -258,7 +323,7 @@ __global__ __launch_bounds__(kFrameThreads) void k_vocab_frame(const int32_t* __
     }
 }
 
-}  // namespace
+}  // namespace orbx
 
 // ---------------------------------------------------------------------------------------
 // Host side
@@ -269,10 +334,8 @@ struct orbx_vocabulary {
     int nnodes = 0, nwords = 0, max_depth = 0, root_cnt = 0;
     hipStream_t stream = nullptr;
     uint4* edesc = nullptr;
-    int2* enext = nullptr;
-    int* enode = nullptr;
-    int* word = nullptr;
-    double* weight = nullptr;
+    int4* einfo = nullptr;
+    double* eweight = nullptr;
     // grow-only work buffers: per-feature words/weights/nodes, host-API staging
     char* work = nullptr;
     size_t work_cap = 0;
@@ -381,14 +444,14 @@ int upload(orbx_vocabulary* v, const HostTree& t) {
     }
     std::vector<int> fill(off.begin(), off.end() - 1);
     std::vector<uint8_t> edesc((size_t)(E > 0 ? E : 1) * 32);
-    std::vector<int2> enext(E > 0 ? E : 1);
-    std::vector<int> enode(E > 0 ? E : 1);
+    std::vector<int4> einfo(E > 0 ? E : 1);
+    std::vector<double> eweight(E > 0 ? E : 1);
     int max_depth = 0;
     for (int i = 1; i < n; i++) {
         const int e = fill[t.parent[i]]++;
         std::memcpy(&edesc[(size_t)e * 32], &t.desc[(size_t)i * 32], 32);
-        enext[e] = make_int2(off[i], off[i + 1] - off[i]);
-        enode[e] = i;
+        einfo[e] = make_int4(off[i], off[i + 1] - off[i], i, t.word[i]);
+        eweight[e] = t.weight[i];
         depth[i] = depth[t.parent[i]] + 1;
         if (depth[i] > max_depth) max_depth = depth[i];
     }
@@ -400,20 +463,16 @@ int upload(orbx_vocabulary* v, const HostTree& t) {
     v->root_cnt = off[1] - off[0];
     v->max_depth = max_depth;
     HIP_TRY(hipMalloc((void**)&v->edesc, edesc.size()));
-    HIP_TRY(hipMalloc((void**)&v->enext, sizeof(int2) * enext.size()));
-    HIP_TRY(hipMalloc((void**)&v->enode, sizeof(int) * enode.size()));
-    HIP_TRY(hipMalloc((void**)&v->word, sizeof(int) * (size_t)n));
-    HIP_TRY(hipMalloc((void**)&v->weight, sizeof(double) * (size_t)n));
+    HIP_TRY(hipMalloc((void**)&v->einfo, sizeof(int4) * einfo.size()));
+    HIP_TRY(hipMalloc((void**)&v->eweight, sizeof(double) * eweight.size()));
     HIP_TRY(hipMemcpy(v->edesc, edesc.data(), edesc.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(v->enext, enext.data(), sizeof(int2) * enext.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(v->enode, enode.data(), sizeof(int) * enode.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(v->word, t.word.data(), sizeof(int) * (size_t)n, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(v->weight, t.weight.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(v->einfo, einfo.data(), sizeof(int4) * einfo.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(v->eweight, eweight.data(), sizeof(double) * eweight.size(), hipMemcpyHostToDevice));
     return ORBX_OK;
 }
 
 void free_vocab(orbx_vocabulary* v) {
-    void* ptrs[] = {v->edesc, v->enext, v->enode, v->word, v->weight, v->work};
+    void* ptrs[] = {v->edesc, v->einfo, v->eweight, v->work};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& slot : v->ev)
@@ -447,7 +506,7 @@ int norm_kind(int scoring) { return scoring == 1 ? 2 : (scoring == 5 ? 0 : 1); }
 int launch(orbx_vocabulary* v, int batch, const uint8_t* d_desc, const int32_t* d_n, int cap, int levelsup,
            int32_t* feat_word, double* feat_weight, int32_t* feat_node, const FrameOut& O, hipStream_t s,
            bool need_frame) {
-    VocDev V{v->edesc, v->enext, v->enode, v->word, v->weight, v->root_cnt, v->max_depth};
+    VocDev V{v->edesc, v->einfo, v->eweight, v->root_cnt, v->max_depth};
     hipEvent_t* ev = nullptr;
     if (v->timing) {
         ev = v->ev[v->ncalls % orbx_vocabulary::kRing];
@@ -461,7 +520,7 @@ int launch(orbx_vocabulary* v, int batch, const uint8_t* d_desc, const int32_t* 
     HIP_TRY(hipGetLastError());
     if (ev) HIP_TRY(hipEventRecord(ev[1], s));
     if (need_frame) {
-        const int np = next_pow2(cap < 2 ? 2 : cap);
+        const int np = next_pow2(cap < kFrameThreads ? kFrameThreads : cap);
         const size_t lds = (size_t)np * 16;
         static thread_local bool attr = false;
         if (!attr) {

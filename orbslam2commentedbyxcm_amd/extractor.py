@@ -25,6 +25,7 @@ class ORBextractor:
         prm = L.ExtractorParams(int(nfeatures), float(scaleFactor), int(nlevels), int(iniThFAST), int(minThFAST))
         h = C.c_void_p()
         L.check(L.lib().orbx_extractor_create(C.byref(prm), int(device), C.byref(h)))
+        self._destroy = L.lib().orbx_extractor_destroy  # held: module globals may be gone at exit
         self._h = h
         self.nfeatures = int(nfeatures)
         self.scaleFactor = float(scaleFactor)
@@ -37,7 +38,7 @@ class ORBextractor:
 
     def __del__(self):
         if getattr(self, "_h", None):
-            L.lib().orbx_extractor_destroy(self._h)
+            self._destroy(self._h)
             self._h = None
 
     # ---- getters (ORBextractor.h:119-159)

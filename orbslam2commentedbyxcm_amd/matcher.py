@@ -161,11 +161,12 @@ class ORBmatcher:
         self._h = None
         h = C.c_void_p()
         L.check(L.lib().orbx_matcher_create(self.device, self.mfNNratio, 1 if checkOri else 0, C.byref(h)))
+        self._destroy = L.lib().orbx_matcher_destroy  # held: module globals may be gone at exit
         self._h = h
 
     def __del__(self):
         if getattr(self, "_h", None):
-            L.lib().orbx_matcher_destroy(self._h)
+            self._destroy(self._h)
             self._h = None
 
     @staticmethod

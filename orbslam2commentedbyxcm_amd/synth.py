@@ -116,3 +116,60 @@ def stereo_pair(seed: int, width: int = 1241, height: int = 376, max_disp: int =
     xs = np.minimum(np.arange(width)[None, :] + disp, width - 1)
     right = np.take_along_axis(left, xs, axis=1)
     return left, np.ascontiguousarray(right), disp.astype(np.int32)
+
+
+def vocabulary_text(seed: int, k: int = 10, L: int = 6, scoring: int = 0, weighting: int = 0,
+                    centres: np.ndarray | None = None) -> bytes:
+    """A complete k-ary, depth-L vocabulary in loadFromTextFile format (TemplatedVocabulary.h:
+    1338-1424), nodes in level order (siblings contiguous, like the reference's creation
+    order).  Stands in for ORBvoc.txt (k=10, L=6, ~1.1M nodes), which the reference does
+    not ship.  Child descriptors are bit-flipped copies of their parent's (fewer flips
+    deeper).  If `centres` (M x 32 uint8, e.g. extracted ORB descriptors) is given, the
+    level-1 nodes start from them, so real descriptors spread over the whole tree.
+    Columns are fixed-width (whitespace-separated like the reference's own files)."""
+    rng = _rng(seed)
+    levels_desc, levels_parent = [], []
+    if centres is not None and len(centres):
+        d1 = np.asarray(centres, np.uint8)[rng.integers(0, len(centres), k)]
+    else:
+        d1 = rng.integers(0, 256, (k, 32), dtype=np.uint8)
+    levels_desc.append(d1)
+    levels_parent.append(np.zeros(k, np.int64))
+    first_id = 1
+    for depth in range(2, L + 1):
+        prev = levels_desc[-1]
+        n_prev = len(prev)
+        d = np.repeat(prev, k, axis=0)
+        q = 24.0 / 256.0 / (depth - 1)  # per-bit flip probability: ~24 bits at level 2, fewer deeper
+        flips = np.concatenate([np.packbits(rng.random((min(1 << 16, len(d) - i), 256), np.float32) < q, axis=1)
+                                for i in range(0, len(d), 1 << 16)])
+        levels_desc.append(d ^ flips)
+        levels_parent.append(np.repeat(np.arange(first_id, first_id + n_prev, dtype=np.int64), k))
+        first_id += n_prev
+    desc = np.concatenate(levels_desc)
+    parent = np.concatenate(levels_parent)
+    n = len(desc)
+    leaf = np.zeros(n, np.int64)
+    leaf[n - len(levels_desc[-1]):] = 1
+    # weights: 5-decimal values in [0.05, 9.99999] on leaves (IDF-like), a few stopped
+    # (0) words, 0 on inner nodes
+    wq = rng.integers(5000, 1000000, n)
+    wq[rng.random(n) < 0.02] = 0
+    wq[leaf == 0] = 0
+
+    def digits(v: np.ndarray, width: int) -> np.ndarray:
+        out = np.empty((len(v), width), np.uint8)
+        x = v.copy()
+        for c in range(width - 1, -1, -1):
+            out[:, c] = ord("0") + x % 10
+            x //= 10
+        return out
+
+    sp = np.full((n, 1), ord(" "), np.uint8)
+    cols = [digits(parent, 7), sp, (ord("0") + leaf).astype(np.uint8)[:, None], sp]
+    table = np.array([[ord(c) for c in f"{i:3d} "] for i in range(256)], np.uint8)
+    cols.append(table[desc].reshape(n, 128))
+    w = digits(wq, 6)
+    cols += [sp, w[:, :1], np.full((n, 1), ord("."), np.uint8), w[:, 1:], np.full((n, 1), ord("\n"), np.uint8)]
+    body = np.concatenate(cols, axis=1).tobytes()
+    return f"{k} {L}  {scoring} {weighting}\n".encode() + body

@@ -29,13 +29,14 @@ class ORBVocabulary:
     def __init__(self, device: int = 0):
         self.device = int(device)
         self._h = None
+        self._destroy = L.lib().orbx_vocabulary_destroy  # held: module globals may be gone at exit
 
     def __del__(self):
         self._release()
 
     def _release(self):
         if getattr(self, "_h", None):
-            L.lib().orbx_vocabulary_destroy(self._h)
+            self._destroy(self._h)
             self._h = None
 
     # -- loading ------------------------------------------------------------------

@@ -103,7 +103,8 @@ def test_rejected_files(orbx_built, tmp_path):
     assert V.loadFromTextFile(str(p)) and V.size() == sum(t.leaf)
 
 
-def test_batch_device_ragged(oracle, orbx_built):
+@pytest.mark.parametrize("levelsup", [4, 2, 0])
+def test_batch_device_ragged(oracle, orbx_built, levelsup):
     import torch
 
     from orbslam2commentedbyxcm_amd.vocabulary import ORBVocabulary
@@ -119,9 +120,11 @@ def test_batch_device_ragged(oracle, orbx_built):
     d_desc = torch.from_numpy(q).cuda()
     d_n = torch.tensor(counts, dtype=torch.int32, device="cuda")
     out = ORBVocabulary.alloc_batch_outputs(B, cap)
+    for v in out.values():
+        v.fill_(-3)  # no output may rely on fresh memory
     fw = torch.full((B, cap), -7, dtype=torch.int32, device="cuda")
     fnode = torch.full((B, cap), -7, dtype=torch.int32, device="cuda")
-    V.transform_batch_device(d_desc, d_n, cap, 4, out, stream=torch.cuda.current_stream().cuda_stream,
+    V.transform_batch_device(d_desc, d_n, cap, levelsup, out, stream=torch.cuda.current_stream().cuda_stream,
                              feat_word=fw, feat_node=fnode)
     torch.cuda.synchronize()
     h = {k2: v.cpu().numpy() for k2, v in out.items()}
@@ -131,7 +134,7 @@ def test_batch_device_ragged(oracle, orbx_built):
         nb, nf = int(h["nbow"][b]), int(h["nfv"][b])
         got = (h["bow_word"][b, :nb], h["bow_value"][b, :nb], h["fv_node"][b, :nf], h["fv_off"][b, :nf + 1],
                h["fv_idx"][b, :h["fv_off"][b, nf]])
-        _same(got, O.transform(q[b, :n], 4))
-        w, _, nd = V.transform_features(q[b, :n], 4)
+        _same(got, O.transform(q[b, :n], levelsup))
+        w, _, nd = V.transform_features(q[b, :n], levelsup)
         assert np.array_equal(fw[b, :n], w) and np.array_equal(fnode[b, :n], nd)
         assert (fw[b, n:] == -7).all()
