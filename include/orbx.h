@@ -247,6 +247,35 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
                                const float* scale_factors, int nlevels, float depth, float th,
                                int32_t* d_cur_mp, int32_t* d_nmatches, void* stream);
 
+/* ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches)
+ * (ORBmatcher.cc:228-392; Tracking::TrackReferenceKeyFrame / Relocalization).
+ * kf_mp[i]: MapPoint id of KF keypoint i, -1 for NULL or isBad().  FeatureVectors as
+ * CSR (nodes ascending, indices ascending within a node).  matches [f->n] out: the KF
+ * MapPoint id matched to each frame keypoint, -1 = none.  Uses the matcher's nnratio
+ * and checkOri. */
+int orbx_search_by_bow_frame(orbx_matcher* m, const orbx_frame_view* kf, const int32_t* kf_mp,
+                             const int32_t* kf_fv_node, const int32_t* kf_fv_off, const int32_t* kf_fv_idx,
+                             int kf_fv_n, const orbx_frame_view* f, const int32_t* f_fv_node, const int32_t* f_fv_off,
+                             const int32_t* f_fv_idx, int f_fv_n, int32_t* matches, int* nmatches);
+
+/* ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12)
+ * (ORBmatcher.cc:696-839; LoopClosing::ComputeSim3).  mp1 / mp2: MapPoint ids, -1 for
+ * NULL or isBad().  matches12 [kf1->n] out: KF2's MapPoint id matched to each KF1
+ * keypoint, -1 = none. */
+int orbx_search_by_bow_keyframes(orbx_matcher* m, const orbx_frame_view* kf1, const int32_t* mp1,
+                                 const int32_t* fv1_node, const int32_t* fv1_off, const int32_t* fv1_idx, int fv1_n,
+                                 const orbx_frame_view* kf2, const int32_t* mp2, const int32_t* fv2_node,
+                                 const int32_t* fv2_off, const int32_t* fv2_idx, int fv2_n, int32_t* matches12,
+                                 int* nmatches);
+
+/* ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, vector<cv::Point2f>& vbPrevMatched,
+ * vector<int>& vnMatches12, int windowSize) (ORBmatcher.cc:539-683;
+ * Tracking::MonocularInitialization).  prev_matched [f1->n][2] in/out; matches12
+ * [f1->n] out (F2 index or -1).  Frames of up to 2^20 keypoints whose working set
+ * fits one workgroup's LDS (16 B per keypoint: n1, n2 <= ~8k). */
+int orbx_search_for_initialization(orbx_matcher* m, const orbx_frame_view* f1, const orbx_frame_view* f2,
+                                   float* prev_matched, int32_t* matches12, int window_size, int* nmatches);
+
 /* Footprint of orbx_match_sequence_device's search kernel: 0 (default) = 1024 threads
  * per problem with keypoint descriptors and query state in LDS (fastest alone); 1 =
  * 256 threads and global-memory query state, for running concurrently with extraction

@@ -152,6 +152,39 @@ public:
         return np;
     }
 
+    // SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches); kfMapPoints: id or -1
+    int SearchByBoW(const orbx_frame_view& KF, const int32_t* kfMapPoints, const FeatureVector& kfFeatVec,
+                    const orbx_frame_view& F, const FeatureVector& fFeatVec, std::vector<int32_t>& vpMapPointMatches) {
+        vpMapPointMatches.assign((size_t)F.n, -1);
+        int n = 0;
+        check(orbx_search_by_bow_frame(h_, &KF, kfMapPoints, kfFeatVec.node.data(), kfFeatVec.off.data(),
+                                       kfFeatVec.idx.data(), (int)kfFeatVec.node.size(), &F, fFeatVec.node.data(),
+                                       fFeatVec.off.data(), fFeatVec.idx.data(), (int)fFeatVec.node.size(),
+                                       vpMapPointMatches.data(), &n));
+        return n;
+    }
+
+    // SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12)
+    int SearchByBoW(const orbx_frame_view& KF1, const int32_t* mapPoints1, const FeatureVector& fv1,
+                    const orbx_frame_view& KF2, const int32_t* mapPoints2, const FeatureVector& fv2,
+                    std::vector<int32_t>& vpMatches12) {
+        vpMatches12.assign((size_t)KF1.n, -1);
+        int n = 0;
+        check(orbx_search_by_bow_keyframes(h_, &KF1, mapPoints1, fv1.node.data(), fv1.off.data(), fv1.idx.data(),
+                                           (int)fv1.node.size(), &KF2, mapPoints2, fv2.node.data(), fv2.off.data(),
+                                           fv2.idx.data(), (int)fv2.node.size(), vpMatches12.data(), &n));
+        return n;
+    }
+
+    // SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize); vbPrevMatched as x,y pairs
+    int SearchForInitialization(const orbx_frame_view& F1, const orbx_frame_view& F2, std::vector<float>& vbPrevMatched,
+                                std::vector<int>& vnMatches12, int windowSize = 10) {
+        vnMatches12.assign((size_t)F1.n, -1);
+        int n = 0;
+        check(orbx_search_for_initialization(h_, &F1, &F2, vbPrevMatched.data(), vnMatches12.data(), windowSize, &n));
+        return n;
+    }
+
     orbx_matcher* handle() { return h_; }
 
 private:

@@ -336,6 +336,55 @@ def search_for_triangulation(kf1, has1, fv1, kf2, has2, fv2, F12, only_stereo, c
     return pairs[:n].copy()
 
 
+def search_by_bow_frame(kf, kf_mp, fv1, f, fv2, nnratio, check_ori):
+    keep = []
+    a, b = _frame(kf, keep), _frame(f, keep)
+    mp = np.ascontiguousarray(kf_mp, np.int32)
+    n1, o1, i1 = (np.ascontiguousarray(x, np.int32) for x in fv1)
+    n2, o2, i2 = (np.ascontiguousarray(x, np.int32) for x in fv2)
+    out = np.full(max(len(f.keys), 1), -1, np.int32)
+    L = lib()
+    L.ora_search_by_bow_kf_frame.argtypes = [C.c_void_p, I32P, I32P, I32P, I32P, C.c_int, C.c_void_p, I32P, I32P, I32P,
+                                             C.c_int, C.c_float, C.c_int, I32P]
+    n = L.ora_search_by_bow_kf_frame(C.addressof(a), mp.ctypes.data_as(I32P), n1.ctypes.data_as(I32P),
+                                     o1.ctypes.data_as(I32P), i1.ctypes.data_as(I32P), len(n1), C.addressof(b),
+                                     n2.ctypes.data_as(I32P), o2.ctypes.data_as(I32P), i2.ctypes.data_as(I32P), len(n2),
+                                     float(nnratio), 1 if check_ori else 0, out.ctypes.data_as(I32P))
+    return n, out[:len(f.keys)].copy()
+
+
+def search_by_bow_keyframes(kf1, mp1, fv1, kf2, mp2, fv2, nnratio, check_ori):
+    keep = []
+    a, b = _frame(kf1, keep), _frame(kf2, keep)
+    m1 = np.ascontiguousarray(mp1, np.int32)
+    m2 = np.ascontiguousarray(mp2, np.int32)
+    n1, o1, i1 = (np.ascontiguousarray(x, np.int32) for x in fv1)
+    n2, o2, i2 = (np.ascontiguousarray(x, np.int32) for x in fv2)
+    out = np.full(max(len(kf1.keys), 1), -1, np.int32)
+    L = lib()
+    L.ora_search_by_bow_kf_kf.argtypes = [C.c_void_p, I32P, I32P, I32P, I32P, C.c_int, C.c_void_p, I32P, I32P, I32P,
+                                          I32P, C.c_int, C.c_float, C.c_int, I32P]
+    n = L.ora_search_by_bow_kf_kf(C.addressof(a), m1.ctypes.data_as(I32P), n1.ctypes.data_as(I32P),
+                                  o1.ctypes.data_as(I32P), i1.ctypes.data_as(I32P), len(n1), C.addressof(b),
+                                  m2.ctypes.data_as(I32P), n2.ctypes.data_as(I32P), o2.ctypes.data_as(I32P),
+                                  i2.ctypes.data_as(I32P), len(n2), float(nnratio), 1 if check_ori else 0,
+                                  out.ctypes.data_as(I32P))
+    return n, out[:len(kf1.keys)].copy()
+
+
+def search_for_initialization(f1, f2, prev_matched, window, nnratio, check_ori):
+    """-> (nmatches, vnMatches12, updated vbPrevMatched copy)."""
+    keep = []
+    a, b = _frame(f1, keep), _frame(f2, keep)
+    prev = np.ascontiguousarray(prev_matched, np.float32).copy()
+    out = np.full(max(len(f1.keys), 1), -1, np.int32)
+    L = lib()
+    L.ora_search_for_initialization.argtypes = [C.c_void_p, C.c_void_p, F32P, I32P, C.c_int, C.c_float, C.c_int]
+    n = L.ora_search_for_initialization(C.addressof(a), C.addressof(b), prev.ctypes.data_as(F32P),
+                                        out.ctypes.data_as(I32P), int(window), float(nnratio), 1 if check_ori else 0)
+    return n, out[:len(f1.keys)].copy(), prev
+
+
 def compute_stereo_matches(left, keys_r, desc_r, levels_l, levels_r, maxD):
     keep = []
     f = _frame(left, keep)

@@ -744,3 +744,214 @@ void ora_compute_stereo_matches(const ora_frame* left, const ora_keypoint* keys_
     free(fill);
     free(rcnt);
 }
+
+/* ---------------------------------------------------------------- f2 */
+
+/* ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&), ORBmatcher.cc:228-392.
+ * kf_mp[i]: MapPoint id of KF keypoint i, -1 when NULL or isBad().  FeatureVectors as
+ * CSR (see ora_search_for_triangulation).  matches[f->n] out: the KF MapPoint id matched
+ * to each frame keypoint or -1.  The histogram uses the frame keypoint's angle from
+ * mvKeys (== mvKeysUn's angle). */
+int ora_search_by_bow_kf_frame(const ora_frame* kf, const int32_t* kf_mp, const int32_t* fv1_node,
+                               const int32_t* fv1_off, const int32_t* fv1_idx, int fv1_n, const ora_frame* f,
+                               const int32_t* fv2_node, const int32_t* fv2_off, const int32_t* fv2_idx, int fv2_n,
+                               float nnratio, int check_ori, int32_t* matches) {
+    for (int i = 0; i < f->n; i++) matches[i] = -1;
+    rot_hist hist;
+    hist_init(&hist, f->n);
+    int nmatches = 0;
+    int f1 = 0, f2 = 0;
+    while (f1 < fv1_n && f2 < fv2_n) {
+        if (fv1_node[f1] == fv2_node[f2]) {
+            for (int i1 = fv1_off[f1]; i1 < fv1_off[f1 + 1]; i1++) {
+                const int realIdxKF = fv1_idx[i1];
+                const int pMP = kf_mp[realIdxKF];
+                if (pMP < 0) continue;
+                const uint8_t* dKF = kf->desc + (size_t)realIdxKF * 32;
+                int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+                for (int i2 = fv2_off[f2]; i2 < fv2_off[f2 + 1]; i2++) {
+                    const int realIdxF = fv2_idx[i2];
+                    if (matches[realIdxF] >= 0) continue;
+                    const int dist = hamming(dKF, f->desc + (size_t)realIdxF * 32);
+                    if (dist < bestDist1) {
+                        bestDist2 = bestDist1;
+                        bestDist1 = dist;
+                        bestIdxF = realIdxF;
+                    } else if (dist < bestDist2) {
+                        bestDist2 = dist;
+                    }
+                }
+                if (bestDist1 <= TH_LOW) {
+                    if ((float)bestDist1 < nnratio * (float)bestDist2) {
+                        matches[bestIdxF] = pMP;
+                        if (check_ori) hist_push(&hist, kf->keys[realIdxKF].angle, f->keys[bestIdxF].angle, bestIdxF);
+                        nmatches++;
+                    }
+                }
+            }
+            f1++;
+            f2++;
+        } else if (fv1_node[f1] < fv2_node[f2]) {
+            while (f1 < fv1_n && fv1_node[f1] < fv2_node[f2]) f1++;
+        } else {
+            while (f2 < fv2_n && fv2_node[f2] < fv1_node[f1]) f2++;
+        }
+    }
+    if (check_ori) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        ora_compute_three_maxima(hist.size, HISTO_LENGTH, &ind1, &ind2, &ind3);
+        for (int b = 0; b < HISTO_LENGTH; b++) {
+            if (b == ind1 || b == ind2 || b == ind3) continue;
+            for (int j = 0; j < hist.size[b]; j++) {
+                matches[hist.items[b][j]] = -1;
+                nmatches--;
+            }
+        }
+    }
+    hist_free(&hist);
+    return nmatches;
+}
+
+/* ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&), ORBmatcher.cc:696-839.
+ * mp1 / mp2: MapPoint ids (-1 = NULL or bad).  matches12[kf1->n] out: KF2's MapPoint
+ * id matched to each KF1 keypoint or -1. */
+int ora_search_by_bow_kf_kf(const ora_frame* kf1, const int32_t* mp1, const int32_t* fv1_node, const int32_t* fv1_off,
+                            const int32_t* fv1_idx, int fv1_n, const ora_frame* kf2, const int32_t* mp2,
+                            const int32_t* fv2_node, const int32_t* fv2_off, const int32_t* fv2_idx, int fv2_n,
+                            float nnratio, int check_ori, int32_t* matches12) {
+    for (int i = 0; i < kf1->n; i++) matches12[i] = -1;
+    uint8_t* vbMatched2 = (uint8_t*)calloc((size_t)kf2->n + 1, 1);
+    rot_hist hist;
+    hist_init(&hist, kf1->n);
+    int nmatches = 0;
+    int f1 = 0, f2 = 0;
+    while (f1 < fv1_n && f2 < fv2_n) {
+        if (fv1_node[f1] == fv2_node[f2]) {
+            for (int i1 = fv1_off[f1]; i1 < fv1_off[f1 + 1]; i1++) {
+                const int idx1 = fv1_idx[i1];
+                if (mp1[idx1] < 0) continue;
+                const uint8_t* d1 = kf1->desc + (size_t)idx1 * 32;
+                int bestDist1 = 256, bestIdx2 = -1, bestDist2 = 256;
+                for (int i2 = fv2_off[f2]; i2 < fv2_off[f2 + 1]; i2++) {
+                    const int idx2 = fv2_idx[i2];
+                    if (vbMatched2[idx2] || mp2[idx2] < 0) continue;
+                    const int dist = hamming(d1, kf2->desc + (size_t)idx2 * 32);
+                    if (dist < bestDist1) {
+                        bestDist2 = bestDist1;
+                        bestDist1 = dist;
+                        bestIdx2 = idx2;
+                    } else if (dist < bestDist2) {
+                        bestDist2 = dist;
+                    }
+                }
+                if (bestDist1 < TH_LOW) {
+                    if ((float)bestDist1 < nnratio * (float)bestDist2) {
+                        matches12[idx1] = mp2[bestIdx2];
+                        vbMatched2[bestIdx2] = 1;
+                        if (check_ori) hist_push(&hist, kf1->keys[idx1].angle, kf2->keys[bestIdx2].angle, idx1);
+                        nmatches++;
+                    }
+                }
+            }
+            f1++;
+            f2++;
+        } else if (fv1_node[f1] < fv2_node[f2]) {
+            while (f1 < fv1_n && fv1_node[f1] < fv2_node[f2]) f1++;
+        } else {
+            while (f2 < fv2_n && fv2_node[f2] < fv1_node[f1]) f2++;
+        }
+    }
+    if (check_ori) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        ora_compute_three_maxima(hist.size, HISTO_LENGTH, &ind1, &ind2, &ind3);
+        for (int b = 0; b < HISTO_LENGTH; b++) {
+            if (b == ind1 || b == ind2 || b == ind3) continue;
+            for (int j = 0; j < hist.size[b]; j++) {
+                matches12[hist.items[b][j]] = -1;
+                nmatches--;
+            }
+        }
+    }
+    hist_free(&hist);
+    free(vbMatched2);
+    return nmatches;
+}
+
+/* ORBmatcher::SearchForInitialization, ORBmatcher.cc:539-683.  prev_matched[2*n1]
+ * (vbPrevMatched) in/out; matches12[f1->n] out (vnMatches12). */
+int ora_search_for_initialization(const ora_frame* f1, const ora_frame* f2, float* prev_matched, int32_t* matches12,
+                                  int windowSize, float nnratio, int check_ori) {
+    int nmatches = 0;
+    for (int i = 0; i < f1->n; i++) matches12[i] = -1;
+    rot_hist hist;
+    hist_init(&hist, f1->n);
+    ora_grid g;
+    ora_grid_build(f2, &g);
+    int* vMatchedDistance = (int*)malloc(sizeof(int) * (size_t)(f2->n + 1));
+    int* vnMatches21 = (int*)malloc(sizeof(int) * (size_t)(f2->n + 1));
+    int* cand = (int*)malloc(sizeof(int) * (size_t)(f2->n + 1));
+    for (int i = 0; i < f2->n; i++) {
+        vMatchedDistance[i] = 0x7fffffff;
+        vnMatches21[i] = -1;
+    }
+    for (int i1 = 0; i1 < f1->n; i1++) {
+        const ora_keypoint* kp1 = &f1->keys[i1];
+        const int level1 = kp1->octave;
+        if (level1 > 0) continue;
+        const int nc = ora_features_in_area(f2, &g, prev_matched[2 * i1], prev_matched[2 * i1 + 1], (float)windowSize,
+                                            level1, level1, cand, f2->n + 1);
+        if (nc == 0) continue;
+        const uint8_t* d1 = f1->desc + (size_t)i1 * 32;
+        int bestDist = 0x7fffffff, bestDist2 = 0x7fffffff, bestIdx2 = -1;
+        for (int c = 0; c < nc; c++) {
+            const int i2 = cand[c];
+            const int dist = hamming(d1, f2->desc + (size_t)i2 * 32);
+            if (vMatchedDistance[i2] <= dist) continue;
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestIdx2 = i2;
+            } else if (dist < bestDist2) {
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= TH_LOW) {
+            if (bestDist < (float)bestDist2 * nnratio) {
+                if (vnMatches21[bestIdx2] >= 0) {
+                    matches12[vnMatches21[bestIdx2]] = -1;
+                    nmatches--;
+                }
+                matches12[i1] = bestIdx2;
+                vnMatches21[bestIdx2] = i1;
+                vMatchedDistance[bestIdx2] = bestDist;
+                nmatches++;
+                if (check_ori) hist_push(&hist, f1->keys[i1].angle, f2->keys[bestIdx2].angle, i1);
+            }
+        }
+    }
+    if (check_ori) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        ora_compute_three_maxima(hist.size, HISTO_LENGTH, &ind1, &ind2, &ind3);
+        for (int b = 0; b < HISTO_LENGTH; b++) {
+            if (b == ind1 || b == ind2 || b == ind3) continue;
+            for (int j = 0; j < hist.size[b]; j++) {
+                const int idx1 = hist.items[b][j];
+                if (matches12[idx1] >= 0) {
+                    matches12[idx1] = -1;
+                    nmatches--;
+                }
+            }
+        }
+    }
+    for (int i1 = 0; i1 < f1->n; i1++)
+        if (matches12[i1] >= 0) {
+            prev_matched[2 * i1] = f2->keys[matches12[i1]].x;
+            prev_matched[2 * i1 + 1] = f2->keys[matches12[i1]].y;
+        }
+    free(cand);
+    free(vnMatches21);
+    free(vMatchedDistance);
+    ora_grid_free(&g);
+    hist_free(&hist);
+    return nmatches;
+}

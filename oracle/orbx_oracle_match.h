@@ -74,6 +74,16 @@ int ora_search_for_triangulation(const ora_frame* kf1, const uint8_t* kf1_has_mp
                                  const uint8_t* kf2_has_mp, const int32_t* fv2_node, const int32_t* fv2_off,
                                  const int32_t* fv2_idx, int fv2_n, const float* F12, int bOnlyStereo, int check_ori,
                                  int32_t* pairs);
+int ora_search_by_bow_kf_frame(const ora_frame* kf, const int32_t* kf_mp, const int32_t* fv1_node,
+                               const int32_t* fv1_off, const int32_t* fv1_idx, int fv1_n, const ora_frame* f,
+                               const int32_t* fv2_node, const int32_t* fv2_off, const int32_t* fv2_idx, int fv2_n,
+                               float nnratio, int check_ori, int32_t* matches);
+int ora_search_by_bow_kf_kf(const ora_frame* kf1, const int32_t* mp1, const int32_t* fv1_node, const int32_t* fv1_off,
+                            const int32_t* fv1_idx, int fv1_n, const ora_frame* kf2, const int32_t* mp2,
+                            const int32_t* fv2_node, const int32_t* fv2_off, const int32_t* fv2_idx, int fv2_n,
+                            float nnratio, int check_ori, int32_t* matches12);
+int ora_search_for_initialization(const ora_frame* f1, const ora_frame* f2, float* prev_matched, int32_t* matches12,
+                                  int windowSize, float nnratio, int check_ori);
 void ora_compute_stereo_matches(const ora_frame* left, const ora_keypoint* keys_r, const uint8_t* desc_r, int nr,
                                 const uint8_t* const* levels_l, const uint8_t* const* levels_r, const int* level_w,
                                 const int* level_h, const float* inv_scale, float maxD, float* u_right, float* depth);

@@ -41,7 +41,8 @@ EXPORTED = [
     "orbx_vocabulary_load_text_file", "orbx_vocabulary_load_text", "orbx_vocabulary_destroy",
     "orbx_vocabulary_info", "orbx_vocabulary_stream", "orbx_vocabulary_transform_features",
     "orbx_vocabulary_transform", "orbx_vocabulary_transform_batch_device", "orbx_vocabulary_set_timing",
-    "orbx_vocabulary_stage_times",
+    "orbx_vocabulary_stage_times", "orbx_search_by_bow_frame", "orbx_search_by_bow_keyframes",
+    "orbx_search_for_initialization",
 ]
 
 
@@ -113,6 +114,11 @@ def lib() -> C.CDLL:
                                              C.c_float, C.c_float, vp, vp, vp]
     L.orbx_search_by_projection_keyframe.argtypes = [vp, vp, i32p, vp, i32p, u8p, vp, C.c_float, C.c_int, ip]
     L.orbx_search_by_projection_sim3.argtypes = [vp, vp, fp, i32p, C.c_int, i32p, vp, C.c_int, ip]
+    L.orbx_search_by_bow_frame.argtypes = [vp, vp, i32p, i32p, i32p, i32p, C.c_int, vp, i32p, i32p, i32p, C.c_int,
+                                           i32p, ip]
+    L.orbx_search_by_bow_keyframes.argtypes = [vp, vp, i32p, i32p, i32p, i32p, C.c_int, vp, i32p, i32p, i32p, i32p,
+                                               C.c_int, i32p, ip]
+    L.orbx_search_for_initialization.argtypes = [vp, vp, vp, fp, i32p, C.c_int, ip]
     L.orbx_matcher_set_timing.argtypes = [vp, C.c_int]
     L.orbx_matcher_set_footprint.argtypes = [vp, C.c_int]
     L.orbx_matcher_last_ms.argtypes = [vp, fp]

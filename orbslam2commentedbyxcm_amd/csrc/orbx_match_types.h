@@ -100,6 +100,53 @@ struct TriProblem {
     long long scratch_off;
 };
 
+// SearchByBoW (KF->F and KF->KF): one shared vocabulary node.  Its queries (side-1
+// keypoints with a valid MapPoint, node-list order) are q_idx1[q_beg..q_end); its
+// side-2 candidates are fv2_idx[c_beg..c_end) (ascending index, the node list).
+struct BowNode {
+    int q_beg, q_end;
+    int c_beg, c_end;
+};
+
+struct BowProblem {
+    const uint8_t* desc1;
+    const orbx_keypoint* keys1;
+    const uint8_t* desc2;
+    const orbx_keypoint* keys2;
+    const int32_t* q_idx1;      // queries (side-1 keypoint indices), node by node
+    const int32_t* fv2_idx;     // side-2 FeatureVector indices
+    const uint8_t* avail2;      // side-2 keypoint may be matched (KF->KF: has a good MapPoint)
+    const int32_t* mp1;         // side-1 MapPoint ids (KF->F: written to the frame)
+    const int32_t* mp2;         // side-2 MapPoint ids (KF->KF: written to matches12)
+    const BowNode* nodes;
+    int nnodes;
+    int n1, n2;
+    int kf_kf;                  // 0: SearchByBoW(KF, F) (accept <= TH_LOW); 1: (KF, KF) (accept < TH_LOW)
+    float nnratio;
+    int check_ori;
+    int32_t* matches;           // KF->F: [n2] frame matches; KF->KF: [n1] matches12 (pre-filled -1)
+};
+
+// SearchForInitialization: F2's grid (Frame::mGrid as CSR) and the level-0 queries of F1.
+struct InitProblem {
+    const orbx_keypoint* keys1;
+    const uint8_t* desc1;
+    const orbx_keypoint* keys2;
+    const uint8_t* desc2;
+    const int32_t* cell_start;  // [kNumCells + 1], cell c = ix * FRAME_GRID_ROWS + iy
+    const int32_t* cell_idx;    // keypoint indices, ascending within a cell
+    const int32_t* q_idx1;      // F1 keypoints with octave 0, ascending
+    const float* prev;          // vbPrevMatched [n1][2]
+    int nq, n1, n2;
+    float min_x, min_y, inv_w, inv_h;
+    float r;                    // windowSize
+    float nnratio;
+    int check_ori;
+    int32_t* matches12;         // out [n1] (vnMatches12)
+    unsigned long long* lists;  // scratch [nq][8]
+    int* trunc;                 // scratch [nq]
+};
+
 struct StereoProblem {
     const orbx_keypoint* keys_l;
     const uint8_t* desc_l;

@@ -38,6 +38,7 @@ int fail(int code, const char* what) {
         }                                                                           \
     } while (0)
 
+constexpr int kNumCellsHost = kGridCols * kGridRows;
 constexpr int TH_HIGH = 100;  // ORBmatcher.cc:38
 constexpr int TH_LOW = 50;    // ORBmatcher.cc:39
 
@@ -682,6 +683,248 @@ int orbx_search_for_triangulation(orbx_matcher* m, const orbx_frame_view* kf1, c
         np++;
     }
     *npairs = np;
+    return ORBX_OK;
+}
+
+namespace {
+
+// Shared vocabulary nodes in the reference's visiting order (ascending node id, the
+// lower_bound walk of ORBmatcher.cc:254-358 / 721-814) with each node's side-1 queries.
+int bow_nodes(const int32_t* fv1_node, const int32_t* fv1_off, const int32_t* fv1_idx, int fv1_n, int n1,
+              const int32_t* fv2_node, const int32_t* fv2_off, int fv2_n, const int32_t* mp1,
+              std::vector<BowNode>& nodes, std::vector<int32_t>& qidx) {
+    int f1 = 0, f2 = 0;
+    while (f1 < fv1_n && f2 < fv2_n) {
+        if (fv1_node[f1] == fv2_node[f2]) {
+            BowNode nd;
+            nd.q_beg = (int)qidx.size();
+            for (int i = fv1_off[f1]; i < fv1_off[f1 + 1]; i++) {
+                const int idx1 = fv1_idx[i];
+                if (idx1 < 0 || idx1 >= n1) return fail(ORBX_ERR_ARG, "feature index out of range");
+                if (mp1[idx1] < 0) continue;  // !pMP || pMP->isBad()
+                qidx.push_back(idx1);
+            }
+            nd.q_end = (int)qidx.size();
+            nd.c_beg = fv2_off[f2];
+            nd.c_end = fv2_off[f2 + 1];
+            if (nd.c_end - nd.c_beg > 65535) return fail(ORBX_ERR_UNSUPPORTED, "vocabulary node with > 65535 features");
+            if (nd.q_end > nd.q_beg && nd.c_end > nd.c_beg) nodes.push_back(nd);
+            f1++;
+            f2++;
+        } else if (fv1_node[f1] < fv2_node[f2]) {
+            f1 = (int)(std::lower_bound(fv1_node + f1, fv1_node + fv1_n, fv2_node[f2]) - fv1_node);
+        } else {
+            f2 = (int)(std::lower_bound(fv2_node + f2, fv2_node + fv2_n, fv1_node[f1]) - fv2_node);
+        }
+    }
+    return ORBX_OK;
+}
+
+int run_bow(orbx_matcher* m, const orbx_frame_view* v1, const int32_t* mp1, const int32_t* fv1_node,
+            const int32_t* fv1_off, const int32_t* fv1_idx, int fv1_n, const orbx_frame_view* v2, const int32_t* mp2,
+            const int32_t* fv2_node, const int32_t* fv2_off, const int32_t* fv2_idx, int fv2_n, bool kf_kf,
+            int32_t* matches, int* nmatches) {
+    const int n1 = v1->n, n2 = v2->n, nout = kf_kf ? n1 : n2;
+    for (int i = 0; i < nout; i++) matches[i] = -1;
+    *nmatches = 0;
+    std::vector<BowNode> nodes;
+    std::vector<int32_t> qidx;
+    int rc = bow_nodes(fv1_node, fv1_off, fv1_idx, fv1_n, n1, fv2_node, fv2_off, fv2_n, mp1, nodes, qidx);
+    if (rc != ORBX_OK) return rc;
+    if (nodes.empty()) return ORBX_OK;
+    const int nfv2 = fv2_off[fv2_n];  // fv2_n > 0 here (a node is shared)
+    for (int i = 0; i < nfv2; i++)
+        if (fv2_idx[i] < 0 || fv2_idx[i] >= n2) return fail(ORBX_ERR_ARG, "feature index out of range");
+    std::vector<uint8_t> avail;
+    if (kf_kf) {  // vbMatched2 starts false; !pMP2 || pMP2->isBad() never match
+        avail.resize((size_t)n2);
+        for (int i = 0; i < n2; i++) avail[(size_t)i] = mp2[i] >= 0;
+    }
+    HIP_TRY(hipSetDevice(m->device));
+    const int nq = (int)qidx.size(), nn = (int)nodes.size();
+    const size_t need = pad(sizeof(orbx_keypoint) * n1) + pad((size_t)n1 * 32) + pad(sizeof(orbx_keypoint) * n2) +
+                        pad((size_t)n2 * 32) + pad(sizeof(int32_t) * nq) + pad(sizeof(int32_t) * nfv2) + pad(n2) +
+                        pad(sizeof(int32_t) * n1) + pad(sizeof(int32_t) * n2) + pad(sizeof(BowNode) * nn) +
+                        pad(sizeof(int32_t) * nout) + pad(sizeof(BowProblem));
+    HIP_TRY(m->arena.reserve(need));
+    m->arena.used = 0;
+    auto* d_k1 = m->arena.take<orbx_keypoint>(n1);
+    auto* d_d1 = m->arena.take<uint8_t>((size_t)n1 * 32);
+    auto* d_k2 = m->arena.take<orbx_keypoint>(n2);
+    auto* d_d2 = m->arena.take<uint8_t>((size_t)n2 * 32);
+    auto* d_q = m->arena.take<int32_t>(nq);
+    auto* d_fv2 = m->arena.take<int32_t>(nfv2);
+    auto* d_av = m->arena.take<uint8_t>(n2);
+    auto* d_mp1 = m->arena.take<int32_t>(n1);
+    auto* d_mp2 = m->arena.take<int32_t>(n2);
+    auto* d_nodes = m->arena.take<BowNode>(nn);
+    auto* d_out = m->arena.take<int32_t>(nout);
+    auto* d_prob = m->arena.take<BowProblem>(1);
+    hipStream_t s = m->stream;
+    HIP_TRY(hipMemcpyAsync(d_k1, v1->keys, sizeof(orbx_keypoint) * n1, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_d1, v1->desc, (size_t)n1 * 32, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_k2, v2->keys, sizeof(orbx_keypoint) * n2, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_d2, v2->desc, (size_t)n2 * 32, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_q, qidx.data(), sizeof(int32_t) * nq, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_fv2, fv2_idx, sizeof(int32_t) * nfv2, hipMemcpyHostToDevice, s));
+    if (kf_kf) {
+        HIP_TRY(hipMemcpyAsync(d_av, avail.data(), n2, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(d_mp2, mp2, sizeof(int32_t) * n2, hipMemcpyHostToDevice, s));
+    } else {
+        HIP_TRY(hipMemcpyAsync(d_mp1, mp1, sizeof(int32_t) * n1, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(hipMemcpyAsync(d_nodes, nodes.data(), sizeof(BowNode) * nn, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(d_out, 0xff, sizeof(int32_t) * nout, s));
+    BowProblem pb{};
+    pb.desc1 = d_d1;
+    pb.keys1 = d_k1;
+    pb.desc2 = d_d2;
+    pb.keys2 = d_k2;
+    pb.q_idx1 = d_q;
+    pb.fv2_idx = d_fv2;
+    pb.avail2 = kf_kf ? d_av : nullptr;
+    pb.mp1 = d_mp1;
+    pb.mp2 = d_mp2;
+    pb.nodes = d_nodes;
+    pb.nnodes = nn;
+    pb.n1 = n1;
+    pb.n2 = n2;
+    pb.kf_kf = kf_kf ? 1 : 0;
+    pb.nnratio = m->nnratio;
+    pb.check_ori = m->check_ori;
+    pb.matches = d_out;
+    HIP_TRY(hipMemcpyAsync(d_prob, &pb, sizeof(pb), hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_bow(d_prob, n2, nout, s));
+    HIP_TRY(hipMemcpyAsync(matches, d_out, sizeof(int32_t) * nout, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    int nm = 0;
+    for (int i = 0; i < nout; i++) nm += matches[i] >= 0;
+    *nmatches = nm;
+    return ORBX_OK;
+}
+
+}  // namespace
+
+// ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&), ORBmatcher.cc:228-392
+int orbx_search_by_bow_frame(orbx_matcher* m, const orbx_frame_view* kf, const int32_t* kf_mp,
+                             const int32_t* kf_fv_node, const int32_t* kf_fv_off, const int32_t* kf_fv_idx,
+                             int kf_fv_n, const orbx_frame_view* f, const int32_t* f_fv_node, const int32_t* f_fv_off,
+                             const int32_t* f_fv_idx, int f_fv_n, int32_t* matches, int* nmatches) {
+    if (!m || !kf || !f || !kf_mp || !matches || !nmatches || (kf_fv_n && (!kf_fv_node || !kf_fv_off || !kf_fv_idx)) ||
+        (f_fv_n && (!f_fv_node || !f_fv_off || !f_fv_idx)) || kf_fv_n < 0 || f_fv_n < 0)
+        return fail(ORBX_ERR_ARG, "null argument");
+    return run_bow(m, kf, kf_mp, kf_fv_node, kf_fv_off, kf_fv_idx, kf_fv_n, f, nullptr, f_fv_node, f_fv_off, f_fv_idx,
+                   f_fv_n, false, matches, nmatches);
+}
+
+// ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&), ORBmatcher.cc:696-839
+int orbx_search_by_bow_keyframes(orbx_matcher* m, const orbx_frame_view* kf1, const int32_t* mp1,
+                                 const int32_t* fv1_node, const int32_t* fv1_off, const int32_t* fv1_idx, int fv1_n,
+                                 const orbx_frame_view* kf2, const int32_t* mp2, const int32_t* fv2_node,
+                                 const int32_t* fv2_off, const int32_t* fv2_idx, int fv2_n, int32_t* matches12,
+                                 int* nmatches) {
+    if (!m || !kf1 || !kf2 || !mp1 || !mp2 || !matches12 || !nmatches || (fv1_n && (!fv1_node || !fv1_off || !fv1_idx)) ||
+        (fv2_n && (!fv2_node || !fv2_off || !fv2_idx)) || fv1_n < 0 || fv2_n < 0)
+        return fail(ORBX_ERR_ARG, "null argument");
+    return run_bow(m, kf1, mp1, fv1_node, fv1_off, fv1_idx, fv1_n, kf2, mp2, fv2_node, fv2_off, fv2_idx, fv2_n, true,
+                   matches12, nmatches);
+}
+
+// ORBmatcher::SearchForInitialization, ORBmatcher.cc:539-683
+int orbx_search_for_initialization(orbx_matcher* m, const orbx_frame_view* f1, const orbx_frame_view* f2,
+                                   float* prev_matched, int32_t* matches12, int window_size, int* nmatches) {
+    if (!m || !f1 || !f2 || !prev_matched || !matches12 || !nmatches) return fail(ORBX_ERR_ARG, "null argument");
+    const int n1 = f1->n, n2 = f2->n;
+    if (n1 >= (1 << 20) || n2 >= (1 << 20)) return fail(ORBX_ERR_UNSUPPORTED, "more than 2^20 keypoints");
+    for (int i = 0; i < n1; i++) matches12[i] = -1;
+    *nmatches = 0;
+    std::vector<int32_t> qidx;
+    for (int i = 0; i < n1; i++)
+        if (f1->keys[i].octave <= 0) qidx.push_back(i);  // level1 > 0 skipped (cc:562-564)
+    // Frame::AssignFeaturesToGrid (Frame.cc:351-370) of F2 as CSR
+    const float inv_w = (float)kGridCols / (f2->max_x - f2->min_x);
+    const float inv_h = (float)kGridRows / (f2->max_y - f2->min_y);
+    std::vector<int32_t> cstart(kNumCellsHost + 1, 0), cell((size_t)n2), cidx;
+    for (int i = 0; i < n2; i++) {
+        const int px = (int)roundf((f2->keys[i].x - f2->min_x) * inv_w);  // PosInGrid, Frame.cc:558-567
+        const int py = (int)roundf((f2->keys[i].y - f2->min_y) * inv_h);
+        cell[(size_t)i] = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? -1 : px * kGridRows + py;
+        if (cell[(size_t)i] >= 0) cstart[cell[(size_t)i] + 1]++;
+    }
+    for (int c = 0; c < kNumCellsHost; c++) cstart[c + 1] += cstart[c];
+    cidx.resize((size_t)cstart[kNumCellsHost] + 1);
+    {
+        std::vector<int32_t> fill(cstart.begin(), cstart.end() - 1);
+        for (int i = 0; i < n2; i++)
+            if (cell[(size_t)i] >= 0) cidx[(size_t)fill[cell[(size_t)i]]++] = i;
+    }
+    const int nq = (int)qidx.size();
+    if (nq == 0 || n2 == 0) return ORBX_OK;
+    const size_t lds = (size_t)4 * (2 * n2 + n1 + nq) + (size_t)nq + 16;
+    if (lds > 160 * 1024) return fail(ORBX_ERR_UNSUPPORTED, "frames too large for one workgroup");
+    HIP_TRY(hipSetDevice(m->device));
+    const size_t need = pad(sizeof(orbx_keypoint) * n1) + pad((size_t)n1 * 32) + pad(sizeof(orbx_keypoint) * n2) +
+                        pad((size_t)n2 * 32) + pad(sizeof(int32_t) * (kNumCellsHost + 1)) + pad(sizeof(int32_t) * cidx.size()) +
+                        pad(sizeof(int32_t) * nq) + pad(sizeof(float) * 2 * n1) + pad(sizeof(int32_t) * n1) +
+                        pad(8 * (size_t)nq * 8) + pad(sizeof(int) * nq) + pad(sizeof(InitProblem));
+    HIP_TRY(m->arena.reserve(need));
+    m->arena.used = 0;
+    auto* d_k1 = m->arena.take<orbx_keypoint>(n1);
+    auto* d_d1 = m->arena.take<uint8_t>((size_t)n1 * 32);
+    auto* d_k2 = m->arena.take<orbx_keypoint>(n2);
+    auto* d_d2 = m->arena.take<uint8_t>((size_t)n2 * 32);
+    auto* d_cs = m->arena.take<int32_t>(kNumCellsHost + 1);
+    auto* d_ci = m->arena.take<int32_t>(cidx.size());
+    auto* d_q = m->arena.take<int32_t>(nq);
+    auto* d_prev = m->arena.take<float>(2 * (size_t)n1);
+    auto* d_m12 = m->arena.take<int32_t>(n1);
+    auto* d_lists = m->arena.take<unsigned long long>((size_t)nq * 8);
+    auto* d_tr = m->arena.take<int>(nq);
+    auto* d_prob = m->arena.take<InitProblem>(1);
+    hipStream_t s = m->stream;
+    HIP_TRY(hipMemcpyAsync(d_k1, f1->keys, sizeof(orbx_keypoint) * n1, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_d1, f1->desc, (size_t)n1 * 32, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_k2, f2->keys, sizeof(orbx_keypoint) * n2, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_d2, f2->desc, (size_t)n2 * 32, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_cs, cstart.data(), sizeof(int32_t) * cstart.size(), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_ci, cidx.data(), sizeof(int32_t) * cidx.size(), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_q, qidx.data(), sizeof(int32_t) * nq, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_prev, prev_matched, sizeof(float) * 2 * n1, hipMemcpyHostToDevice, s));
+    InitProblem pb{};
+    pb.keys1 = d_k1;
+    pb.desc1 = d_d1;
+    pb.keys2 = d_k2;
+    pb.desc2 = d_d2;
+    pb.cell_start = d_cs;
+    pb.cell_idx = d_ci;
+    pb.q_idx1 = d_q;
+    pb.prev = d_prev;
+    pb.nq = nq;
+    pb.n1 = n1;
+    pb.n2 = n2;
+    pb.min_x = f2->min_x;
+    pb.min_y = f2->min_y;
+    pb.inv_w = inv_w;
+    pb.inv_h = inv_h;
+    pb.r = (float)window_size;
+    pb.nnratio = m->nnratio;
+    pb.check_ori = m->check_ori;
+    pb.matches12 = d_m12;
+    pb.lists = d_lists;
+    pb.trunc = d_tr;
+    HIP_TRY(hipMemcpyAsync(d_prob, &pb, sizeof(pb), hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_init(d_prob, n1, n2, nq, s));
+    HIP_TRY(hipMemcpyAsync(matches12, d_m12, sizeof(int32_t) * n1, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    int nm = 0;
+    for (int i = 0; i < n1; i++) {
+        const int j = matches12[i];
+        if (j < 0) continue;
+        nm++;
+        prev_matched[2 * i] = f2->keys[j].x;  // vbPrevMatched[i1] = F2.mvKeysUn[..].pt (cc:676-678)
+        prev_matched[2 * i + 1] = f2->keys[j].y;
+    }
+    *nmatches = nm;
     return ORBX_OK;
 }
 

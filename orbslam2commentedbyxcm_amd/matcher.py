@@ -247,6 +247,50 @@ class ORBmatcher:
             1 if bOnlyStereo else 0, pairs.ctypes.data_as(I32P), C.byref(npairs)))
         return pairs[: npairs.value].copy()
 
+    # SearchByBoW(KeyFrame* pKF, Frame& F, vpMapPointMatches)  ORBmatcher.cc:228-392
+    def SearchByBoWFrame(self, kf: FrameView, kf_mp, kf_fv, f: FrameView, f_fv):
+        """-> (nmatches, matches[f.n]: KF MapPoint id per frame keypoint or -1).  kf_mp:
+        MapPoint id per KF keypoint, -1 for NULL / isBad().  FeatureVectors as CSR."""
+        mp = np.ascontiguousarray(kf_mp, dtype=np.int32)
+        n1, o1, i1 = (np.ascontiguousarray(x, dtype=np.int32) for x in kf_fv)
+        n2, o2, i2 = (np.ascontiguousarray(x, dtype=np.int32) for x in f_fv)
+        v1, v2 = kf.c(), f.c()
+        out = np.full(max(len(f.keys), 1), -1, dtype=np.int32)
+        nm = C.c_int()
+        L.check(L.lib().orbx_search_by_bow_frame(
+            self._h, C.addressof(v1), mp.ctypes.data_as(I32P), n1.ctypes.data_as(I32P), o1.ctypes.data_as(I32P),
+            i1.ctypes.data_as(I32P), len(n1), C.addressof(v2), n2.ctypes.data_as(I32P), o2.ctypes.data_as(I32P),
+            i2.ctypes.data_as(I32P), len(n2), out.ctypes.data_as(I32P), C.byref(nm)))
+        return nm.value, out[:len(f.keys)].copy()
+
+    # SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vpMatches12)  ORBmatcher.cc:696-839
+    def SearchByBoWKeyFrames(self, kf1: FrameView, mp1, fv1, kf2: FrameView, mp2, fv2):
+        """-> (nmatches, matches12[kf1.n]: KF2 MapPoint id per KF1 keypoint or -1)."""
+        a1 = np.ascontiguousarray(mp1, dtype=np.int32)
+        a2 = np.ascontiguousarray(mp2, dtype=np.int32)
+        n1, o1, i1 = (np.ascontiguousarray(x, dtype=np.int32) for x in fv1)
+        n2, o2, i2 = (np.ascontiguousarray(x, dtype=np.int32) for x in fv2)
+        v1, v2 = kf1.c(), kf2.c()
+        out = np.full(max(len(kf1.keys), 1), -1, dtype=np.int32)
+        nm = C.c_int()
+        L.check(L.lib().orbx_search_by_bow_keyframes(
+            self._h, C.addressof(v1), a1.ctypes.data_as(I32P), n1.ctypes.data_as(I32P), o1.ctypes.data_as(I32P),
+            i1.ctypes.data_as(I32P), len(n1), C.addressof(v2), a2.ctypes.data_as(I32P), n2.ctypes.data_as(I32P),
+            o2.ctypes.data_as(I32P), i2.ctypes.data_as(I32P), len(n2), out.ctypes.data_as(I32P), C.byref(nm)))
+        return nm.value, out[:len(kf1.keys)].copy()
+
+    # SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)  ORBmatcher.cc:539-683
+    def SearchForInitialization(self, f1: FrameView, f2: FrameView, prev_matched: np.ndarray, windowSize: int = 10):
+        """prev_matched: float32 [f1.n, 2], updated in place.  -> (nmatches, vnMatches12)."""
+        assert prev_matched.dtype == np.float32 and prev_matched.flags.c_contiguous
+        v1, v2 = f1.c(), f2.c()
+        out = np.full(max(len(f1.keys), 1), -1, dtype=np.int32)
+        nm = C.c_int()
+        L.check(L.lib().orbx_search_for_initialization(self._h, C.addressof(v1), C.addressof(v2),
+                                                       prev_matched.ctypes.data_as(F32P), out.ctypes.data_as(I32P),
+                                                       int(windowSize), C.byref(nm)))
+        return nm.value, out[:len(f1.keys)].copy()
+
     # Frame::ComputeStereoMatches  Frame.cc:673-885
     def ComputeStereoMatches(self, extractor, left_frame: int, right_frame: int, left: FrameView, keys_r, desc_r,
                              maxD: float):
