@@ -308,6 +308,35 @@ int orbx_compute_stereo_matches(orbx_matcher* m, orbx_extractor* ex, int left_fr
                                 const uint8_t* desc_r, int n_right, float max_disparity, float* u_right,
                                 float* depth);
 
+/* ---- Frame: undistortion and grid (§8(f) rank 3) ----
+ * Camera intrinsics and distortion: Frame::mK and Frame::mDistCoef [k1 k2 p1 p2 (k3)]
+ * (Tracking.cc:60-92; k3 = 0 when the settings have four coefficients). */
+typedef struct {
+    float fx, fy, cx, cy;
+    float k1, k2, p1, p2, k3;
+} orbx_camera;
+
+/* Frame::UndistortKeyPoints (Frame.cc:586-628): cv::undistortPoints(mvKeys, K, D,
+ * noArray(), K) on every keypoint; mvKeysUn = mvKeys when k1 == 0.  Host buffers of n
+ * keypoints (keys_un may equal keys). */
+int orbx_undistort_keypoints(int device, const orbx_camera* cam, const orbx_keypoint* keys, int n,
+                             orbx_keypoint* keys_un);
+/* Same over the orbx_extract_batch_device layout (frame b at d_keys + b*cap, min(d_n[b], cap)
+ * keypoints) into d_keys_un [B][cap].  Asynchronous on `stream`. */
+int orbx_undistort_keypoints_device(const orbx_camera* cam, int batch, const orbx_keypoint* d_keys,
+                                    const int32_t* d_n, int cap, orbx_keypoint* d_keys_un, void* stream);
+/* Frame::ComputeImageBounds (Frame.cc:636-665): bounds = {mnMinX, mnMaxX, mnMinY, mnMaxY}. */
+int orbx_compute_image_bounds(int device, const orbx_camera* cam, int cols, int rows, float* bounds);
+/* Frame::AssignFeaturesToGrid (Frame.cc:351-370, PosInGrid 558-567) as CSR: cell
+ * c = ix * FRAME_GRID_ROWS + iy (64 x 48) holds cell_idx[cell_start[c] .. cell_start[c+1]),
+ * ascending; keypoints outside the grid are left out.  n <= 8192. */
+int orbx_assign_features_to_grid(int device, const orbx_keypoint* keys_un, int n, const float* bounds,
+                                 int32_t* cell_start, int32_t* cell_idx);
+/* Batched: d_cell_start [B][3073], d_cell_idx [B][cap], cap <= 8192.  Asynchronous. */
+int orbx_assign_features_to_grid_device(int batch, const orbx_keypoint* d_keys_un, const int32_t* d_n, int cap,
+                                        const float* bounds, int32_t* d_cell_start, int32_t* d_cell_idx,
+                                        void* stream);
+
 /* ---- DBoW2 vocabulary (TemplatedVocabulary<FORB::TDescriptor, FORB>, §8(f) rank 1) ----
  * The tree lives in HBM as its CSR edge list.  Scoring / weighting
  * codes are DBoW2's enums (BowVector.h:29-56): scoring L1_NORM 0, L2_NORM 1,

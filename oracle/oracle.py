@@ -385,6 +385,61 @@ def search_for_initialization(f1, f2, prev_matched, window, nnratio, check_ori):
     return n, out[:len(f1.keys)].copy(), prev
 
 
+def undistort_points(K, D, pts):
+    """cv::undistortPoints(pts, K, D, noArray(), K) restated (float32 (n, 2) -> (n, 2))."""
+    Kf = np.ascontiguousarray(K, np.float32).reshape(4)
+    Df = np.zeros(5, np.float32)
+    Df[:len(D)] = D
+    p = np.ascontiguousarray(pts, np.float32).reshape(-1, 2)
+    out = np.zeros_like(p)
+    L = lib()
+    L.ora_undistort_points.argtypes = [F32P, F32P, F32P, C.c_int, F32P]
+    L.ora_undistort_points.restype = None
+    L.ora_undistort_points(Kf.ctypes.data_as(F32P), Df.ctypes.data_as(F32P), p.ctypes.data_as(F32P), len(p),
+                           out.ctypes.data_as(F32P))
+    return out
+
+
+def undistort_keypoints(K, D, keys):
+    """Frame::UndistortKeyPoints (Frame.cc:586-628): copy when k1 == 0."""
+    out = np.array(keys, copy=True)
+    if np.float32(D[0]) == 0.0:
+        return out
+    u = undistort_points(K, D, np.stack([keys["x"], keys["y"]], 1))
+    out["x"], out["y"] = u[:, 0], u[:, 1]
+    return out
+
+
+def compute_image_bounds(K, D, cols, rows):
+    """Frame::ComputeImageBounds (Frame.cc:636-665) -> (min_x, max_x, min_y, max_y)."""
+    if np.float32(D[0]) == 0.0:
+        return np.array([0.0, cols, 0.0, rows], np.float32)
+    c = undistort_points(K, D, np.array([[0, 0], [cols, 0], [0, rows], [cols, rows]], np.float32))
+    return np.array([min(c[0, 0], c[2, 0]), max(c[1, 0], c[3, 0]), min(c[0, 1], c[1, 1]), max(c[2, 1], c[3, 1])],
+                    np.float32)
+
+
+def assign_features_to_grid(keys_un, bounds):
+    """Frame::AssignFeaturesToGrid (Frame.cc:351-370) as CSR (cell_start[3073], cell_idx)."""
+    inv_w = np.float32(64) / np.float32(bounds[1] - bounds[0])
+    inv_h = np.float32(48) / np.float32(bounds[3] - bounds[2])
+    import math
+
+    def cround(v):  # C round(): half away from zero (float32 v + 0.5 is exact in double)
+        return int(math.copysign(math.floor(abs(float(v)) + 0.5), float(v)))
+
+    cells = [[] for _ in range(64 * 48)]
+    for i, kp in enumerate(keys_un):
+        px = cround(np.float32(np.float32(kp["x"]) - np.float32(bounds[0])) * inv_w)
+        py = cround(np.float32(np.float32(kp["y"]) - np.float32(bounds[2])) * inv_h)
+        if 0 <= px < 64 and 0 <= py < 48:
+            cells[px * 48 + py].append(i)
+    start = np.zeros(64 * 48 + 1, np.int32)
+    start[1:] = np.cumsum([len(c) for c in cells])
+    idx = np.array([i for c in cells for i in c], np.int32)
+    return start, idx
+
+
 def compute_stereo_matches(left, keys_r, desc_r, levels_l, levels_r, maxD):
     keep = []
     f = _frame(left, keep)

@@ -955,3 +955,37 @@ int ora_search_for_initialization(const ora_frame* f1, const ora_frame* f2, floa
     hist_free(&hist);
     return nmatches;
 }
+
+/* ---------------------------------------------------------------- f3 */
+
+/* cv::undistortPoints(src, dst, K, D, noArray(), K) for CV_32FC2 points, OpenCV 3.3.1
+ * cvUndistortPoints (imgproc/src/undistort.cpp, not vendored: parity unpinned), as
+ * called by Frame::UndistortKeyPoints (Frame.cc:586-628) and ComputeImageBounds
+ * (Frame.cc:636-665).  K = (fx, fy, cx, cy), D = (k1, k2, p1, p2, k3), all converted to
+ * double; 5 fixed-point iterations; R = I and P = K make the final projection
+ * fx*x + cx exactly; the result is rounded to float. */
+void ora_undistort_points(const float* K, const float* D, const float* pts, int n, float* out) {
+    const double fx = K[0], fy = K[1], cx = K[2], cy = K[3];
+    const double ifx = 1. / fx, ify = 1. / fy;
+    double k[14] = {0};
+    for (int i = 0; i < 5; i++) k[i] = D[i];
+    for (int i = 0; i < n; i++) {
+        double x = pts[2 * i], y = pts[2 * i + 1];
+        x = (x - cx) * ifx;
+        y = (y - cy) * ify;
+        const double x0 = x, y0 = y;
+        for (int j = 0; j < 5; j++) {
+            const double r2 = x * x + y * y;
+            const double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+            const double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x) + k[8] * r2 + k[9] * r2 * r2;
+            const double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y + k[10] * r2 + k[11] * r2 * r2;
+            x = (x0 - deltaX) * icdist;
+            y = (y0 - deltaY) * icdist;
+        }
+        const double xx = fx * x + 0. * y + cx;
+        const double yy = 0. * x + fy * y + cy;
+        const double ww = 1. / (0. * x + 0. * y + 1.);
+        out[2 * i] = (float)(xx * ww);
+        out[2 * i + 1] = (float)(yy * ww);
+    }
+}

@@ -84,6 +84,7 @@ int ora_search_by_bow_kf_kf(const ora_frame* kf1, const int32_t* mp1, const int3
                             float nnratio, int check_ori, int32_t* matches12);
 int ora_search_for_initialization(const ora_frame* f1, const ora_frame* f2, float* prev_matched, int32_t* matches12,
                                   int windowSize, float nnratio, int check_ori);
+void ora_undistort_points(const float* K, const float* D, const float* pts, int n, float* out);
 void ora_compute_stereo_matches(const ora_frame* left, const ora_keypoint* keys_r, const uint8_t* desc_r, int nr,
                                 const uint8_t* const* levels_l, const uint8_t* const* levels_r, const int* level_w,
                                 const int* level_h, const float* inv_scale, float maxD, float* u_right, float* depth);

@@ -42,8 +42,14 @@ EXPORTED = [
     "orbx_vocabulary_info", "orbx_vocabulary_stream", "orbx_vocabulary_transform_features",
     "orbx_vocabulary_transform", "orbx_vocabulary_transform_batch_device", "orbx_vocabulary_set_timing",
     "orbx_vocabulary_stage_times", "orbx_search_by_bow_frame", "orbx_search_by_bow_keyframes",
-    "orbx_search_for_initialization",
+    "orbx_search_for_initialization", "orbx_undistort_keypoints", "orbx_undistort_keypoints_device",
+    "orbx_compute_image_bounds", "orbx_assign_features_to_grid", "orbx_assign_features_to_grid_device",
 ]
+
+
+class Camera(C.Structure):
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("k1", C.c_float),
+                ("k2", C.c_float), ("p1", C.c_float), ("p2", C.c_float), ("k3", C.c_float)]
 
 
 class ExtractorParams(C.Structure):
@@ -119,6 +125,12 @@ def lib() -> C.CDLL:
     L.orbx_search_by_bow_keyframes.argtypes = [vp, vp, i32p, i32p, i32p, i32p, C.c_int, vp, i32p, i32p, i32p, i32p,
                                                C.c_int, i32p, ip]
     L.orbx_search_for_initialization.argtypes = [vp, vp, vp, fp, i32p, C.c_int, ip]
+    cp = C.POINTER(Camera)
+    L.orbx_undistort_keypoints.argtypes = [C.c_int, cp, vp, C.c_int, vp]
+    L.orbx_undistort_keypoints_device.argtypes = [cp, C.c_int, vp, vp, C.c_int, vp, vp]
+    L.orbx_compute_image_bounds.argtypes = [C.c_int, cp, C.c_int, C.c_int, fp]
+    L.orbx_assign_features_to_grid.argtypes = [C.c_int, vp, C.c_int, fp, i32p, i32p]
+    L.orbx_assign_features_to_grid_device.argtypes = [C.c_int, vp, vp, C.c_int, fp, vp, vp, vp]
     L.orbx_matcher_set_timing.argtypes = [vp, C.c_int]
     L.orbx_matcher_set_footprint.argtypes = [vp, C.c_int]
     L.orbx_matcher_last_ms.argtypes = [vp, fp]

@@ -1,0 +1,301 @@
+// orbx_frame.hip -- the per-frame steps between extraction and matching on the device
+// (SURVEY.md §8(f) rank 3):
+//   Frame::UndistortKeyPoints   Frame.cc:586-628  (cv::undistortPoints, OpenCV 3.3.1)
+//   Frame::ComputeImageBounds   Frame.cc:636-665
+//   Frame::AssignFeaturesToGrid Frame.cc:351-370  (+ PosInGrid 558-567)
+// so a batch extracted by orbx_extract_batch_device gets mvKeysUn and mGrid without a
+// host round trip.  Undistortion is one thread per keypoint in double precision (the
+// 5-iteration fixed point of cvUndistortPoints, same operation order as the oracle,
+// no contraction).  The grid is one 1024-thread workgroup per frame: keys
+// (cell << 32 | index) are block-sorted (orbx_block_sort.h), so each cell's list is in
+// ascending index order like the reference's push_back loop, and written as CSR.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "orbx.h"
+#include "orbx_block_sort.h"
+#include "orbx_error.h"
+#include "orbx_match_types.h"
+
+using namespace orbx;
+
+namespace orbx {
+
+struct CamDev {
+    double fx, fy, cx, cy, ifx, ify;
+    double k[5];
+    int enabled;  // mDistCoef.at<float>(0) != 0
+};
+
+// cvUndistortPoints for one point (see oracle/orbx_oracle_match.c ora_undistort_points)
+__device__ __forceinline__ void undistort_point(const CamDev& C, float u, float v, float& ou, float& ov) {
+    double x = u, y = v;
+    x = __dmul_rn(__dsub_rn(x, C.cx), C.ifx);
+    y = __dmul_rn(__dsub_rn(y, C.cy), C.ify);
+    const double x0 = x, y0 = y;
+    const double* k = C.k;
+    for (int j = 0; j < 5; j++) {
+        const double r2 = __dadd_rn(__dmul_rn(x, x), __dmul_rn(y, y));
+        // (1 + ((k7*r2 + k6)*r2 + k5)*r2) with k5..k7 = 0 is exactly 1
+        const double num = __dadd_rn(1.0, __dmul_rn(__dadd_rn(__dmul_rn(__dadd_rn(__dmul_rn(0.0, r2), 0.0), r2), 0.0), r2));
+        const double den = __dadd_rn(1.0, __dmul_rn(__dadd_rn(__dmul_rn(__dadd_rn(__dmul_rn(k[4], r2), k[1]), r2), k[0]), r2));
+        const double icdist = num / den;
+        // 2*k2*x*y + k3*(r2 + 2*x*x) + k8*r2 + k9*r2*r2
+        const double dX = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(__dmul_rn(__dmul_rn(2.0, k[2]), x), y),
+                                                        __dmul_rn(k[3], __dadd_rn(r2, __dmul_rn(__dmul_rn(2.0, x), x)))),
+                                              __dmul_rn(0.0, r2)),
+                                    __dmul_rn(__dmul_rn(0.0, r2), r2));
+        // k2*(r2 + 2*y*y) + 2*k3*x*y + k10*r2 + k11*r2*r2
+        const double dY = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(k[2], __dadd_rn(r2, __dmul_rn(__dmul_rn(2.0, y), y))),
+                                                        __dmul_rn(__dmul_rn(__dmul_rn(2.0, k[3]), x), y)),
+                                              __dmul_rn(0.0, r2)),
+                                    __dmul_rn(__dmul_rn(0.0, r2), r2));
+        x = __dmul_rn(__dsub_rn(x0, dX), icdist);
+        y = __dmul_rn(__dsub_rn(y0, dY), icdist);
+    }
+    const double xx = __dadd_rn(__dadd_rn(__dmul_rn(C.fx, x), __dmul_rn(0.0, y)), C.cx);
+    const double yy = __dadd_rn(__dadd_rn(__dmul_rn(0.0, x), __dmul_rn(C.fy, y)), C.cy);
+    const double ww = 1.0 / __dadd_rn(__dadd_rn(__dmul_rn(0.0, x), __dmul_rn(0.0, y)), 1.0);
+    ou = (float)__dmul_rn(xx, ww);
+    ov = (float)__dmul_rn(yy, ww);
+}
+
+__global__ __launch_bounds__(256) void k_undistort(CamDev C, const orbx_keypoint* __restrict__ kin,
+                                                   const int32_t* __restrict__ nper, int cap,
+                                                   orbx_keypoint* __restrict__ kout) {
+    const int b = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int n = min(nper[b], cap);
+    if (i >= n) return;
+    const size_t s = (size_t)b * cap + i;
+    orbx_keypoint kp = kin[s];
+    if (C.enabled) undistort_point(C, kp.x, kp.y, kp.x, kp.y);
+    kout[s] = kp;
+}
+
+// Image corners for ComputeImageBounds (4 points)
+__global__ void k_undistort_points(CamDev C, const float* __restrict__ pts, int n, float* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) undistort_point(C, pts[2 * i], pts[2 * i + 1], out[2 * i], out[2 * i + 1]);
+}
+
+struct GridArgs {
+    float min_x, min_y, inv_w, inv_h;
+};
+
+// Frame::AssignFeaturesToGrid for frame blockIdx.x: cell_start [kGridCols*kGridRows + 1],
+// cell_idx [cap] (the first cell_start[last] entries are valid).
+__global__ __launch_bounds__(kSortThreads) void k_grid(GridArgs G, const orbx_keypoint* __restrict__ keys,
+                                                       const int32_t* __restrict__ nper, int cap,
+                                                       int32_t* __restrict__ cell_start, int32_t* __restrict__ cell_idx) {
+    extern __shared__ unsigned long long s_key[];
+    constexpr int kCells = kGridCols * kGridRows;
+    const int b = blockIdx.x;
+    const int n = min(nper[b], cap);
+    int ne = 1;
+    while (ne * kSortThreads < n) ne <<= 1;
+    const int m = ne * kSortThreads;
+    unsigned long long r[kSortPer];
+#pragma unroll
+    for (int e = 0; e < kSortPer; e++) {
+        const int i = e * kSortThreads + threadIdx.x;
+        unsigned long long key = ~0ull;
+        if (e < ne && i < n) {
+            const orbx_keypoint kp = keys[(size_t)b * cap + i];
+            const int px = (int)roundf(__fmul_rn(__fsub_rn(kp.x, G.min_x), G.inv_w));  // PosInGrid
+            const int py = (int)roundf(__fmul_rn(__fsub_rn(kp.y, G.min_y), G.inv_h));
+            if (!(px < 0 || px >= kGridCols || py < 0 || py >= kGridRows))
+                key = (unsigned long long)(unsigned)(px * kGridRows + py) << 32 | (unsigned)i;
+        }
+        r[e] = key;
+    }
+    block_bitonic_sort64(r, ne, s_key);
+    int32_t* cs = cell_start + (size_t)b * (kCells + 1);
+    int32_t* ci = cell_idx + (size_t)b * cap;
+    // cell_start[c] = first sorted position with cell >= c
+    for (int p = threadIdx.x; p < m; p += kSortThreads) {
+        const unsigned long long k = s_key[p];
+        const int c = k == ~0ull ? kCells : (int)(k >> 32);
+        const int cprev = p == 0 ? -1 : (s_key[p - 1] == ~0ull ? kCells : (int)(s_key[p - 1] >> 32));
+        for (int q = cprev + 1; q <= c; q++) cs[q] = p;
+        if (c < kCells) ci[p] = (int32_t)(unsigned)k;
+        if (p == m - 1)
+            for (int q = c + 1; q <= kCells; q++) cs[q] = m;  // every key valid: tail cells start at m
+    }
+}
+
+}  // namespace orbx
+
+namespace {
+
+int fail(int code, const char* what) {
+    set_last_error(what);
+    return code;
+}
+
+#define HIP_TRY(expr)                                                               \
+    do {                                                                            \
+        hipError_t _e = (expr);                                                     \
+        if (_e != hipSuccess) {                                                     \
+            set_last_error(std::string(#expr) + ": " + hipGetErrorString(_e));      \
+            return ORBX_ERR_HIP;                                                    \
+        }                                                                           \
+    } while (0)
+
+CamDev cam_dev(const orbx_camera* c) {
+    CamDev C;
+    C.fx = c->fx;
+    C.fy = c->fy;
+    C.cx = c->cx;
+    C.cy = c->cy;
+    C.ifx = 1.0 / C.fx;
+    C.ify = 1.0 / C.fy;
+    C.k[0] = c->k1;
+    C.k[1] = c->k2;
+    C.k[2] = c->p1;
+    C.k[3] = c->p2;
+    C.k[4] = c->k3;
+    C.enabled = c->k1 != 0.0f;
+    return C;
+}
+
+bool bounds_ok(const float* bd) { return bd && bd[1] > bd[0] && bd[3] > bd[2]; }
+
+GridArgs grid_args(const float* bd) {
+    GridArgs G;
+    G.min_x = bd[0];
+    G.min_y = bd[2];
+    G.inv_w = (float)kGridCols / (bd[1] - bd[0]);  // Frame.cc:157-159
+    G.inv_h = (float)kGridRows / (bd[3] - bd[2]);
+    return G;
+}
+
+hipError_t launch_grid(const GridArgs& G, int batch, const orbx_keypoint* keys, const int32_t* n, int cap,
+                       int32_t* cell_start, int32_t* cell_idx, hipStream_t s) {
+    int np = kSortThreads;
+    while (np < cap) np <<= 1;
+    const size_t lds = (size_t)np * 8;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_grid, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_grid, dim3(batch), dim3(kSortThreads), lds, s, G, keys, n, cap, cell_start, cell_idx);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+int orbx_undistort_keypoints_device(const orbx_camera* cam, int batch, const orbx_keypoint* d_keys, const int32_t* d_n,
+                                    int cap, orbx_keypoint* d_keys_un, void* stream) {
+    if (!cam || batch < 0 || cap < 0 || (batch && cap && (!d_keys || !d_n || !d_keys_un)))
+        return fail(ORBX_ERR_ARG, "bad argument");
+    if (!batch || !cap) return ORBX_OK;
+    const dim3 g((cap + 255) / 256, batch);
+    hipLaunchKernelGGL(k_undistort, g, dim3(256), 0, (hipStream_t)stream, cam_dev(cam), d_keys, d_n, cap, d_keys_un);
+    HIP_TRY(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbx_undistort_keypoints(int device, const orbx_camera* cam, const orbx_keypoint* keys, int n,
+                             orbx_keypoint* keys_un) {
+    if (!cam || n < 0 || (n && (!keys || !keys_un))) return fail(ORBX_ERR_ARG, "bad argument");
+    if (n == 0) return ORBX_OK;
+    if (cam->k1 == 0.0f) {  // mvKeysUn = mvKeys (Frame.cc:587-590)
+        if (keys_un != keys) std::memcpy(keys_un, keys, sizeof(orbx_keypoint) * (size_t)n);
+        return ORBX_OK;
+    }
+    HIP_TRY(hipSetDevice(device));
+    orbx_keypoint* d = nullptr;
+    int32_t* d_n = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, sizeof(orbx_keypoint) * (size_t)n * 2));
+    hipError_t e = hipMalloc((void**)&d_n, sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemcpy(d, keys, sizeof(orbx_keypoint) * (size_t)n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_n, &n, sizeof(int32_t), hipMemcpyHostToDevice);
+    int rc = ORBX_OK;
+    if (e == hipSuccess) rc = orbx_undistort_keypoints_device(cam, 1, d, d_n, n, d + n, nullptr);
+    if (e == hipSuccess && rc == ORBX_OK)
+        e = hipMemcpy(keys_un, d + n, sizeof(orbx_keypoint) * (size_t)n, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (d_n) (void)hipFree(d_n);
+    if (rc != ORBX_OK) return rc;
+    HIP_TRY(e);
+    return ORBX_OK;
+}
+
+int orbx_compute_image_bounds(int device, const orbx_camera* cam, int cols, int rows, float* bounds) {
+    if (!cam || !bounds || cols <= 0 || rows <= 0) return fail(ORBX_ERR_ARG, "bad argument");
+    if (cam->k1 == 0.0f) {
+        bounds[0] = 0.0f;
+        bounds[1] = (float)cols;
+        bounds[2] = 0.0f;
+        bounds[3] = (float)rows;
+        return ORBX_OK;
+    }
+    const float c[8] = {0.0f, 0.0f, (float)cols, 0.0f, 0.0f, (float)rows, (float)cols, (float)rows};
+    float u[8];
+    HIP_TRY(hipSetDevice(device));
+    float* d = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, sizeof(c) * 2));
+    hipError_t e = hipMemcpy(d, c, sizeof(c), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_undistort_points, dim3(1), dim3(64), 0, nullptr, cam_dev(cam), d, 4, d + 8);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(u, d + 8, sizeof(u), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    HIP_TRY(e);
+    bounds[0] = u[0] < u[4] ? u[0] : u[4];  // min(top-left x, bottom-left x)
+    bounds[1] = u[2] > u[6] ? u[2] : u[6];  // max(top-right x, bottom-right x)
+    bounds[2] = u[1] < u[3] ? u[1] : u[3];  // min(top-left y, top-right y)
+    bounds[3] = u[5] > u[7] ? u[5] : u[7];  // max(bottom-left y, bottom-right y)
+    return ORBX_OK;
+}
+
+int orbx_assign_features_to_grid_device(int batch, const orbx_keypoint* d_keys_un, const int32_t* d_n, int cap,
+                                        const float* bounds, int32_t* d_cell_start, int32_t* d_cell_idx,
+                                        void* stream) {
+    if (batch < 0 || cap < 0 || !bounds_ok(bounds) || (batch && (!d_keys_un || !d_n || !d_cell_start || !d_cell_idx)))
+        return fail(ORBX_ERR_ARG, "bad argument");
+    if (cap > kSortMaxKeys) return fail(ORBX_ERR_UNSUPPORTED, "more than 8192 keypoints per frame");
+    if (!batch) return ORBX_OK;
+    HIP_TRY(launch_grid(grid_args(bounds), batch, d_keys_un, d_n, cap < 1 ? 1 : cap, d_cell_start, d_cell_idx,
+                        (hipStream_t)stream));
+    return ORBX_OK;
+}
+
+int orbx_assign_features_to_grid(int device, const orbx_keypoint* keys_un, int n, const float* bounds,
+                                 int32_t* cell_start, int32_t* cell_idx) {
+    if (n < 0 || !bounds_ok(bounds) || !cell_start || (n && (!keys_un || !cell_idx)))
+        return fail(ORBX_ERR_ARG, "bad argument");
+    if (n > kSortMaxKeys) return fail(ORBX_ERR_UNSUPPORTED, "more than 8192 keypoints per frame");
+    constexpr int kCells = kGridCols * kGridRows;
+    if (n == 0) {
+        for (int c = 0; c <= kCells; c++) cell_start[c] = 0;
+        return ORBX_OK;
+    }
+    HIP_TRY(hipSetDevice(device));
+    char* d = nullptr;
+    const size_t bk = sizeof(orbx_keypoint) * (size_t)n, bs = sizeof(int32_t) * (kCells + 1),
+                 bi = sizeof(int32_t) * (size_t)n;
+    HIP_TRY(hipMalloc((void**)&d, bk + bs + bi + 256));
+    orbx_keypoint* d_k = (orbx_keypoint*)d;
+    int32_t* d_s = (int32_t*)(d + bk);
+    int32_t* d_i = (int32_t*)(d + bk + bs);
+    int32_t* d_n = (int32_t*)(d + bk + bs + bi);
+    hipError_t e = hipMemcpy(d_k, keys_un, bk, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_n, &n, sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_grid(grid_args(bounds), 1, d_k, d_n, n, d_s, d_i, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(cell_start, d_s, bs, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && cell_start[kCells] > 0)
+        e = hipMemcpy(cell_idx, d_i, sizeof(int32_t) * (size_t)cell_start[kCells], hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    HIP_TRY(e);
+    return ORBX_OK;
+}
+
+}  // extern "C"

@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "orbx.h"
+#include "orbx_block_sort.h"
 #include "orbx_error.h"
 
 using namespace orbx;
@@ -44,6 +45,7 @@ namespace {
 constexpr int kVocMaxCap = 8192;   // features per frame in one transform (LDS sort size)
 constexpr int kFrameThreads = 1024;
 constexpr int kWalkThreads = 256;  // 16 descriptors per block
+static_assert(kFrameThreads == kSortThreads && kVocMaxCap == kSortMaxKeys, "orbx_block_sort.h geometry");
 
 __device__ __forceinline__ unsigned umin_(unsigned a, unsigned b) { return a < b ? a : b; }
 
@@ -150,67 +152,6 @@ __device__ int block_scan(int v, int* s_wave, int& excl) {
     return total;
 }
 
-__device__ __forceinline__ unsigned long long shfl_xor64(unsigned long long v, int j) {
-    const int lo = __shfl_xor((int)(unsigned)v, j, 64), hi = __shfl_xor((int)(unsigned)(v >> 32), j, 64);
-    return (unsigned long long)(unsigned)hi << 32 | (unsigned)lo;
-}
-
-// Register stages of a bitonic merge: partner distances j < 64 live in the same wave
-// (element e*1024 + t sits in lane t & 63), so they run as lane shuffles with no
-// barrier.  New value of element i: min of (i, i^j) when "i is the lower index" agrees
-// with "block k ascending", else max.
-__device__ __forceinline__ void reg_stages(unsigned long long (&r)[kVocMaxCap / kFrameThreads], int ne, int k,
-                                           int jtop) {
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int j = 32; j > 0; j >>= 1) {
-        if (j > jtop) continue;
-#pragma unroll
-        for (int e = 0; e < kVocMaxCap / kFrameThreads; e++) {
-            if (e < ne) {
-                const unsigned long long v = r[e], p = shfl_xor64(v, j);
-                const int i = e * kFrameThreads + t;
-                const bool lower = (t & j) == 0, asc = (i & k) == 0;
-                r[e] = (lower == asc) ? (v < p ? v : p) : (v < p ? p : v);
-            }
-        }
-    }
-}
-
-// Bitonic sort of m = ne * 1024 keys (ne = 1..8; r[e] holds element e*1024 + t) into
-// s[0, m): merge distances >= 64 in place in LDS (one barrier each), the rest in
-// registers.  Ends with the sorted keys in s and a barrier.
-__device__ void bitonic_sort(unsigned long long (&r)[kVocMaxCap / kFrameThreads], int ne,
-                             unsigned long long* s) {
-    const int t = threadIdx.x, m = ne * kFrameThreads;
-    for (int k = 2; k <= 64; k <<= 1) reg_stages(r, ne, k, k >> 1);
-#pragma unroll
-    for (int e = 0; e < kVocMaxCap / kFrameThreads; e++)
-        if (e < ne) s[e * kFrameThreads + t] = r[e];
-    __syncthreads();
-    for (int k = 128; k <= m; k <<= 1) {
-        for (int j = k >> 1; j >= 64; j >>= 1) {
-            for (int q = t; q < m / 2; q += kFrameThreads) {
-                const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1));
-                const unsigned long long a = s[i], c = s[i + j];
-                if ((a > c) == ((i & k) == 0)) {
-                    s[i] = c;
-                    s[i + j] = a;
-                }
-            }
-            __syncthreads();
-        }
-#pragma unroll
-        for (int e = 0; e < kVocMaxCap / kFrameThreads; e++)
-            if (e < ne) r[e] = s[e * kFrameThreads + t];
-        reg_stages(r, ne, k, 32);
-#pragma unroll
-        for (int e = 0; e < kVocMaxCap / kFrameThreads; e++)
-            if (e < ne) s[e * kFrameThreads + t] = r[e];
-        __syncthreads();
-    }
-}
-
 // Run heads of the sorted keys s[0, nw): each thread owns `per` consecutive entries.
 // Writes head positions via `emit(pos, i)`; returns the number of runs.
 template <typename Emit>
@@ -257,18 +198,18 @@ __global__ __launch_bounds__(kFrameThreads) void k_vocab_frame(const int32_t* __
     while (ne * kFrameThreads < n) ne <<= 1;
     const int m = ne * kFrameThreads;
     const int per = ne;
-    unsigned long long r[kVocMaxCap / kFrameThreads];
+    unsigned long long r[kSortPer];
 
     // ---- BowVector: sort (word, feature) over non-stopped features
 #pragma unroll
-    for (int e = 0; e < kVocMaxCap / kFrameThreads; e++) {
+    for (int e = 0; e < kSortPer; e++) {
         const int i = e * kFrameThreads + threadIdx.x;
         r[e] = (e < ne && i < n && feat_weight[base + i] > 0)
                    ? ((unsigned long long)(unsigned)feat_word[base + i] << 32 | (unsigned)i)
                    : ~0ull;
     }
     if (threadIdx.x == 0) s_nw = 0;
-    bitonic_sort(r, ne, s_key);
+    block_bitonic_sort64(r, ne, s_key);
     for (int i = threadIdx.x; i < m; i += kFrameThreads)
         if (s_key[i] != ~0ull && (i + 1 == m || s_key[i + 1] == ~0ull)) s_nw = i + 1;
     __syncthreads();
@@ -305,13 +246,13 @@ __global__ __launch_bounds__(kFrameThreads) void k_vocab_frame(const int32_t* __
 
     // ---- FeatureVector: sort (node, feature) over the same features
 #pragma unroll
-    for (int e = 0; e < kVocMaxCap / kFrameThreads; e++) {
+    for (int e = 0; e < kSortPer; e++) {
         const int i = e * kFrameThreads + threadIdx.x;
         r[e] = (e < ne && i < n && feat_weight[base + i] > 0)
                    ? ((unsigned long long)(unsigned)feat_node[base + i] << 32 | (unsigned)i)
                    : ~0ull;
     }
-    bitonic_sort(r, ne, s_key);
+    block_bitonic_sort64(r, ne, s_key);
     for (int i = threadIdx.x; i < nw; i += kFrameThreads) O.fv_idx[base + i] = (int32_t)(unsigned)s_key[i];
     const int nf = scan_heads(s_key, nw, per, s_wave, [&](int p, int i) {
         O.fv_node[base + p] = (int32_t)(s_key[i] >> 32);
