@@ -276,6 +276,44 @@ int orbx_search_by_bow_keyframes(orbx_matcher* m, const orbx_frame_view* kf1, co
 int orbx_search_for_initialization(orbx_matcher* m, const orbx_frame_view* f1, const orbx_frame_view* f2,
                                    float* prev_matched, int32_t* matches12, int window_size, int* nmatches);
 
+/* ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, float th)
+ * (ORBmatcher.cc:1067-1221; LocalMapping::SearchInNeighbors): the search part.  For
+ * each points[k] (MapPoint id, -1 = NULL) not flagged in skip[id] (isBad() ||
+ * IsInKeyFrame(pKF)), best[k] receives the KF keypoint it fuses with (distance <=
+ * TH_LOW, Fuse's chi-square gate on mvuRight) or -1.  No MapPoint's search depends on
+ * another's, so all run at once; the caller then runs the reference's Replace /
+ * AddObservation loop in order over best[], re-checking isBad() / IsInKeyFrame(). */
+int orbx_fuse(orbx_matcher* m, const orbx_frame_view* kf, const int32_t* points, int npoints, const uint8_t* skip,
+              const orbx_mappoints* mps, float th, int32_t* best);
+
+/* ORBmatcher::Fuse(KeyFrame* pKF, cv::Mat Scw, const vector<MapPoint*>& vpPoints, float th,
+ * vector<MapPoint*>& vpReplacePoint) (ORBmatcher.cc:1226-1352; LoopClosing::SearchAndFuse):
+ * the search part; skip[id] = isBad() || pKF->GetMapPoints().count(pMP).  Scw: 3 x 4
+ * row-major [sR | st]. */
+int orbx_fuse_sim3(orbx_matcher* m, const orbx_frame_view* kf, const float* Scw, const int32_t* points, int npoints,
+                   const uint8_t* skip, const orbx_mappoints* mps, float th, int32_t* best);
+
+/* ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
+ * (ORBmatcher.cc:1361-1602; LoopClosing::ComputeSim3).  mp1 / mp2: GetMapPointMatches()
+ * as ids (-1 = NULL); already1 / already2: vbAlreadyMatched1/2 from the incoming
+ * vpMatches12 (may be NULL = none); R12 row-major 3 x 3, t12 3.  matches12 [kf1->n]
+ * in/out (KF2 MapPoint ids): mutual matches are written, other entries are left as
+ * they are.  *nfound = number written. */
+int orbx_search_by_sim3(orbx_matcher* m, const orbx_frame_view* kf1, const int32_t* mp1, const uint8_t* already1,
+                        const orbx_frame_view* kf2, const int32_t* mp2, const uint8_t* already2,
+                        const orbx_mappoints* mps, float s12, const float* R12, const float* t12, float th,
+                        int32_t* matches12, int* nfound);
+
+/* MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:295-360) for nmp MapPoints at once:
+ * MapPoint k's descriptors (good observations, observation-map order) are
+ * desc[off[k] .. off[k+1]) (32 B each).  best[k] = index within that list of the
+ * descriptor with the smallest median distance (-1 when empty); out_desc [nmp][32]
+ * (optional) receives it. */
+int orbx_compute_distinctive_descriptors(int device, int nmp, const int32_t* off, const uint8_t* desc, int32_t* best,
+                                         uint8_t* out_desc);
+int orbx_compute_distinctive_descriptors_device(int nmp, const int32_t* d_off, const uint8_t* d_desc, int32_t* d_best,
+                                                uint8_t* d_out_desc, void* stream);
+
 /* Footprint of orbx_match_sequence_device's search kernel: 0 (default) = 1024 threads
  * per problem with keypoint descriptors and query state in LDS (fastest alone); 1 =
  * 256 threads and global-memory query state, for running concurrently with extraction

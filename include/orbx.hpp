@@ -185,6 +185,31 @@ public:
         return n;
     }
 
+    // Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, th): search part, best[k] = KF keypoint or -1
+    void Fuse(const orbx_frame_view& KF, const std::vector<int32_t>& vpMapPoints, const uint8_t* skip,
+              const orbx_mappoints& mps, std::vector<int32_t>& best, float th = 3.0f) {
+        best.assign(vpMapPoints.size(), -1);
+        check(orbx_fuse(h_, &KF, vpMapPoints.data(), (int)vpMapPoints.size(), skip, &mps, th, best.data()));
+    }
+
+    // Fuse(KeyFrame* pKF, cv::Mat Scw, vpPoints, th, vpReplacePoint): search part
+    void Fuse(const orbx_frame_view& KF, const float Scw[12], const std::vector<int32_t>& vpPoints, const uint8_t* skip,
+              const orbx_mappoints& mps, std::vector<int32_t>& best, float th = 4.0f) {
+        best.assign(vpPoints.size(), -1);
+        check(orbx_fuse_sim3(h_, &KF, Scw, vpPoints.data(), (int)vpPoints.size(), skip, &mps, th, best.data()));
+    }
+
+    // SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
+    int SearchBySim3(const orbx_frame_view& KF1, const int32_t* mapPoints1, const uint8_t* alreadyMatched1,
+                     const orbx_frame_view& KF2, const int32_t* mapPoints2, const uint8_t* alreadyMatched2,
+                     const orbx_mappoints& mps, float s12, const float R12[9], const float t12[3], float th,
+                     int32_t* vpMatches12) {
+        int n = 0;
+        check(orbx_search_by_sim3(h_, &KF1, mapPoints1, alreadyMatched1, &KF2, mapPoints2, alreadyMatched2, &mps, s12,
+                                  R12, t12, th, vpMatches12, &n));
+        return n;
+    }
+
     orbx_matcher* handle() { return h_; }
 
 private:

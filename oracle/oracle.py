@@ -315,6 +315,65 @@ def sbp_sim3(kf, Scw, points, matched, mps, th):
                           matched.ctypes.data_as(I32P), C.addressof(m), int(th))
 
 
+def fuse(kf, points, skip, mps, th):
+    keep = []
+    fk, m = _frame(kf, keep), _mappoints(mps, keep)
+    pts = np.ascontiguousarray(points, np.int32)
+    sk = np.ascontiguousarray(skip, np.uint8)
+    best = np.full(max(len(pts), 1), -1, np.int32)
+    L = lib()
+    L.ora_fuse.argtypes = [C.c_void_p, I32P, C.c_int, U8P, C.c_void_p, C.c_float, I32P]
+    L.ora_fuse.restype = None
+    L.ora_fuse(C.addressof(fk), pts.ctypes.data_as(I32P), len(pts), sk.ctypes.data_as(U8P), C.addressof(m), float(th),
+               best.ctypes.data_as(I32P))
+    return best[:len(pts)].copy()
+
+
+def fuse_sim3(kf, Scw, points, skip, mps, th):
+    keep = []
+    fk, m = _frame(kf, keep), _mappoints(mps, keep)
+    S = np.ascontiguousarray(np.asarray(Scw, np.float32)[:3, :4])
+    pts = np.ascontiguousarray(points, np.int32)
+    sk = np.ascontiguousarray(skip, np.uint8)
+    best = np.full(max(len(pts), 1), -1, np.int32)
+    L = lib()
+    L.ora_fuse_sim3.argtypes = [C.c_void_p, F32P, I32P, C.c_int, U8P, C.c_void_p, C.c_float, I32P]
+    L.ora_fuse_sim3.restype = None
+    L.ora_fuse_sim3(C.addressof(fk), S.ctypes.data_as(F32P), pts.ctypes.data_as(I32P), len(pts),
+                    sk.ctypes.data_as(U8P), C.addressof(m), float(th), best.ctypes.data_as(I32P))
+    return best[:len(pts)].copy()
+
+
+def search_by_sim3(kf1, mp1, already1, kf2, mp2, already2, mps, s12, R12, t12, th, matches12):
+    """matches12 updated in place; returns nFound."""
+    keep = []
+    f1, f2, m = _frame(kf1, keep), _frame(kf2, keep), _mappoints(mps, keep)
+    a1, a2 = np.ascontiguousarray(mp1, np.int32), np.ascontiguousarray(mp2, np.int32)
+    al1 = np.zeros(len(a1), np.uint8) if already1 is None else np.ascontiguousarray(already1, np.uint8)
+    al2 = np.zeros(len(a2), np.uint8) if already2 is None else np.ascontiguousarray(already2, np.uint8)
+    R = np.ascontiguousarray(R12, np.float32).reshape(9)
+    t = np.ascontiguousarray(t12, np.float32).reshape(3)
+    L = lib()
+    L.ora_search_by_sim3.argtypes = [C.c_void_p, I32P, U8P, C.c_void_p, I32P, U8P, C.c_void_p, C.c_float, F32P, F32P,
+                                     C.c_float, I32P]
+    return L.ora_search_by_sim3(C.addressof(f1), a1.ctypes.data_as(I32P), al1.ctypes.data_as(U8P), C.addressof(f2),
+                                a2.ctypes.data_as(I32P), al2.ctypes.data_as(U8P), C.addressof(m), float(s12),
+                                R.ctypes.data_as(F32P), t.ctypes.data_as(F32P), float(th),
+                                matches12.ctypes.data_as(I32P))
+
+
+def distinctive_descriptors(off, desc):
+    o = np.ascontiguousarray(off, np.int32)
+    d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    nmp = len(o) - 1
+    best = np.full(max(nmp, 1), -1, np.int32)
+    L = lib()
+    L.ora_distinctive_descriptors.argtypes = [C.c_int, I32P, U8P, I32P]
+    L.ora_distinctive_descriptors.restype = None
+    L.ora_distinctive_descriptors(nmp, o.ctypes.data_as(I32P), d.ctypes.data_as(U8P), best.ctypes.data_as(I32P))
+    return best[:nmp].copy()
+
+
 def search_for_triangulation(kf1, has1, fv1, kf2, has2, fv2, F12, only_stereo, check_ori):
     keep = []
     f1 = _frame(kf1, keep)

@@ -989,3 +989,224 @@ void ora_undistort_points(const float* K, const float* D, const float* pts, int 
         out[2 * i + 1] = (float)(yy * ww);
     }
 }
+
+/* ---------------------------------------------------------------- f4 */
+
+/* Window search shared by Fuse / SearchBySim3: the first keypoint (GetFeaturesInArea
+ * order) with the smallest distance among those with octave in [pred-1, pred] (and,
+ * when gate, inside Fuse's chi-square gate); returns it when its distance <= accept. */
+static int window_best(const ora_frame* kf, const ora_grid* g, int* cand, const uint8_t* dMP, float u, float v,
+                       float ur, float radius, int pred, int gate, const float* inv_sigma2, int accept) {
+    const int nc = ora_features_in_area(kf, g, u, v, radius, -1, -1, cand, kf->n + 1);
+    if (nc == 0) return -1;
+    int bestDist = 256, bestIdx = -1;
+    for (int c = 0; c < nc; c++) {
+        const int idx = cand[c];
+        const ora_keypoint* kp = &kf->keys[idx];
+        const int kpLevel = kp->octave;
+        if (kpLevel < pred - 1 || kpLevel > pred) continue;
+        if (gate) {
+            if (kf->u_right && kf->u_right[idx] >= 0) { /* cc:1137-1150 */
+                const float ex = u - kp->x, ey = v - kp->y, er = ur - kf->u_right[idx];
+                const float e2 = ex * ex + ey * ey + er * er;
+                if ((double)(e2 * inv_sigma2[kpLevel]) > 7.8) continue;
+            } else {
+                const float ex = u - kp->x, ey = v - kp->y;
+                const float e2 = ex * ex + ey * ey;
+                if ((double)(e2 * inv_sigma2[kpLevel]) > 5.99) continue;
+            }
+        }
+        const int d = hamming(dMP, kf->desc + (size_t)idx * 32);
+        if (d < bestDist) {
+            bestDist = d;
+            bestIdx = idx;
+        }
+    }
+    return bestDist <= accept ? bestIdx : -1;
+}
+
+/* ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, th),
+ * ORBmatcher.cc:1067-1221: the search part.  points[k]: MapPoint id or -1; skip[id]:
+ * isBad() || IsInKeyFrame(pKF) when the loop reaches it.  best[k] out: the fused KF
+ * keypoint or -1.  (Replace / AddObservation stay with the caller, in order.) */
+void ora_fuse(const ora_frame* kf, const int32_t* points, int npoints, const uint8_t* skip, const ora_mappoints* mps,
+              float th, int32_t* best) {
+    ora_grid g;
+    ora_grid_build(kf, &g);
+    int* cand = (int*)malloc(sizeof(int) * (size_t)(kf->n + 1));
+    float inv_sigma2[32];
+    for (int l = 0; l < kf->nlevels; l++) inv_sigma2[l] = 1.0f / kf->level_sigma2[l];
+    float Ow[3];
+    for (int c = 0; c < 3; c++) Ow[c] = -(kf->Tcw[c] * kf->Tcw[3] + kf->Tcw[4 + c] * kf->Tcw[7] + kf->Tcw[8 + c] * kf->Tcw[11]);
+    for (int k = 0; k < npoints; k++) {
+        best[k] = -1;
+        const int mp = points[k];
+        if (mp < 0 || skip[mp]) continue;
+        const float* p3Dw = mps->pos + 3 * (size_t)mp;
+        float p3Dc[3];
+        project(kf->Tcw, p3Dw, p3Dc);
+        if (p3Dc[2] < 0.0f) continue;
+        const float invz = 1 / p3Dc[2];
+        const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
+        const float u = kf->fx * x + kf->cx, v = kf->fy * y + kf->cy;
+        if (!(u >= kf->min_x && u < kf->max_x && v >= kf->min_y && v < kf->max_y)) continue;
+        const float ur = u - kf->bf * invz;
+        const float maxDistance = 1.2f * mps->max_distance[mp], minDistance = 0.8f * mps->min_distance[mp];
+        float PO[3];
+        for (int c = 0; c < 3; c++) PO[c] = p3Dw[c] - Ow[c];
+        const float dist3D = norm3(PO);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const float* Pn = mps->normal + 3 * (size_t)mp;
+        double dot = 0.0;
+        for (int c = 0; c < 3; c++) dot += (double)PO[c] * Pn[c];
+        if (dot < 0.5 * dist3D) continue;
+        const int pred = predict_scale(mps->max_distance[mp], dist3D, kf);
+        const float radius = th * kf->scale_factors[pred];
+        best[k] = window_best(kf, &g, cand, mps->desc + (size_t)mp * 32, u, v, ur, radius, pred, 1, inv_sigma2, TH_LOW);
+    }
+    free(cand);
+    ora_grid_free(&g);
+}
+
+/* ORBmatcher::Fuse(KeyFrame* pKF, cv::Mat Scw, const vector<MapPoint*>& vpPoints, th,
+ * vector<MapPoint*>& vpReplacePoint), ORBmatcher.cc:1226-1352: the search part.
+ * skip[id]: isBad() || in pKF->GetMapPoints(). */
+void ora_fuse_sim3(const ora_frame* kf, const float* Scw, const int32_t* points, int npoints, const uint8_t* skip,
+                   const ora_mappoints* mps, float th, int32_t* best) {
+    ora_grid g;
+    ora_grid_build(kf, &g);
+    int* cand = (int*)malloc(sizeof(int) * (size_t)(kf->n + 1));
+    double d0 = 0.0;
+    for (int c = 0; c < 3; c++) d0 += (double)Scw[c] * Scw[c];
+    const float scw = (float)sqrt(d0);
+    const float alpha = (float)(1.0 / scw);
+    float T[12];
+    for (int k = 0; k < 12; k++) T[k] = Scw[k] * alpha;
+    float Ow[3];
+    for (int c = 0; c < 3; c++) Ow[c] = -(T[c] * T[3] + T[4 + c] * T[7] + T[8 + c] * T[11]);
+    for (int k = 0; k < npoints; k++) {
+        best[k] = -1;
+        const int mp = points[k];
+        if (mp < 0 || skip[mp]) continue;
+        const float* p3Dw = mps->pos + 3 * (size_t)mp;
+        float p3Dc[3];
+        project(T, p3Dw, p3Dc);
+        if (p3Dc[2] < 0.0f) continue;
+        const float invz = (float)(1.0 / p3Dc[2]);
+        const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
+        const float u = kf->fx * x + kf->cx, v = kf->fy * y + kf->cy;
+        if (!(u >= kf->min_x && u < kf->max_x && v >= kf->min_y && v < kf->max_y)) continue;
+        const float maxDistance = 1.2f * mps->max_distance[mp], minDistance = 0.8f * mps->min_distance[mp];
+        float PO[3];
+        for (int c = 0; c < 3; c++) PO[c] = p3Dw[c] - Ow[c];
+        const float dist3D = norm3(PO);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const float* Pn = mps->normal + 3 * (size_t)mp;
+        double dot = 0.0;
+        for (int c = 0; c < 3; c++) dot += (double)PO[c] * Pn[c];
+        if (dot < 0.5 * dist3D) continue;
+        const int pred = predict_scale(mps->max_distance[mp], dist3D, kf);
+        const float radius = th * kf->scale_factors[pred];
+        best[k] = window_best(kf, &g, cand, mps->desc + (size_t)mp * 32, u, v, 0.f, radius, pred, 0, NULL, TH_LOW);
+    }
+    free(cand);
+    ora_grid_free(&g);
+}
+
+/* One direction of SearchBySim3: MapPoints of `src` (ids src_mp, -1 = NULL) mapped
+ * into `dst` by x_dst = sR * (R_src x + t_src) + t, window-searched in dst. */
+static void sim3_direction(const ora_frame* src, const int32_t* src_mp, const uint8_t* already, const ora_frame* dst,
+                           const ora_mappoints* mps, const float* sR, const float* t, float th, int* vnMatch) {
+    ora_grid g;
+    ora_grid_build(dst, &g);
+    int* cand = (int*)malloc(sizeof(int) * (size_t)(dst->n + 1));
+    for (int i = 0; i < src->n; i++) {
+        vnMatch[i] = -1;
+        const int mp = src_mp[i];
+        if (mp < 0 || already[i]) continue;
+        if (mps->bad && mps->bad[mp]) continue;
+        const float* p3Dw = mps->pos + 3 * (size_t)mp;
+        float pc[3], pd[3];
+        project(src->Tcw, p3Dw, pc);
+        for (int r = 0; r < 3; r++) pd[r] = sR[3 * r] * pc[0] + sR[3 * r + 1] * pc[1] + sR[3 * r + 2] * pc[2] + t[r];
+        if (pd[2] < 0.0) continue;
+        const float invz = (float)(1.0 / pd[2]);
+        const float x = pd[0] * invz, y = pd[1] * invz;
+        const float u = dst->fx * x + dst->cx, v = dst->fy * y + dst->cy;
+        if (!(u >= dst->min_x && u < dst->max_x && v >= dst->min_y && v < dst->max_y)) continue;
+        const float maxDistance = 1.2f * mps->max_distance[mp], minDistance = 0.8f * mps->min_distance[mp];
+        const float dist3D = norm3(pd);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const int pred = predict_scale(mps->max_distance[mp], dist3D, dst);
+        const float radius = th * dst->scale_factors[pred];
+        vnMatch[i] = window_best(dst, &g, cand, mps->desc + (size_t)mp * 32, u, v, 0.f, radius, pred, 0, NULL, TH_HIGH);
+    }
+    free(cand);
+    ora_grid_free(&g);
+}
+
+/* ORBmatcher::SearchBySim3, ORBmatcher.cc:1361-1602.  kf*_mp: GetMapPointMatches() as
+ * ids; already1/2: vbAlreadyMatched1/2 (from the incoming vpMatches12); matches12 in/out
+ * (KF2 MapPoint ids).  sR12 = s12*R12; sR21 = R12^T * (float)(1/s12); t21 = -sR21*t12.
+ * Returns nFound. */
+int ora_search_by_sim3(const ora_frame* kf1, const int32_t* mp1, const uint8_t* already1, const ora_frame* kf2,
+                       const int32_t* mp2, const uint8_t* already2, const ora_mappoints* mps, float s12,
+                       const float* R12, const float* t12, float th, int32_t* matches12) {
+    float sR12[9], sR21[9], t21[3];
+    const float inv = (float)(1.0 / s12);
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+            sR12[3 * r + c] = s12 * R12[3 * r + c];
+            sR21[3 * r + c] = R12[3 * c + r] * inv;
+        }
+    for (int r = 0; r < 3; r++) t21[r] = -(sR21[3 * r] * t12[0] + sR21[3 * r + 1] * t12[1] + sR21[3 * r + 2] * t12[2]);
+    int* vnMatch1 = (int*)malloc(sizeof(int) * (size_t)(kf1->n + 1));
+    int* vnMatch2 = (int*)malloc(sizeof(int) * (size_t)(kf2->n + 1));
+    sim3_direction(kf1, mp1, already1, kf2, mps, sR21, t21, th, vnMatch1);
+    sim3_direction(kf2, mp2, already2, kf1, mps, sR12, t12, th, vnMatch2);
+    int nFound = 0;
+    for (int i1 = 0; i1 < kf1->n; i1++) {
+        const int idx2 = vnMatch1[i1];
+        if (idx2 >= 0 && vnMatch2[idx2] == i1) {
+            matches12[i1] = mp2[idx2];
+            nFound++;
+        }
+    }
+    free(vnMatch1);
+    free(vnMatch2);
+    return nFound;
+}
+
+/* MapPoint::ComputeDistinctiveDescriptors, MapPoint.cc:295-360: descriptors of the
+ * good observations in observation-map order; the one with the smallest median
+ * distance (vDists[0.5*(N-1)], first on ties).  best[m] = index in the MapPoint's list
+ * or -1 when it has none. */
+void ora_distinctive_descriptors(int nmp, const int32_t* off, const uint8_t* desc, int32_t* best) {
+    for (int m = 0; m < nmp; m++) {
+        const int N = off[m + 1] - off[m];
+        best[m] = -1;
+        if (N <= 0) continue;
+        const uint8_t* D = desc + (size_t)off[m] * 32;
+        int* row = (int*)malloc(sizeof(int) * (size_t)N);
+        int BestMedian = 0x7fffffff, BestIdx = 0;
+        for (int i = 0; i < N; i++) {
+            for (int j = 0; j < N; j++) row[j] = i == j ? 0 : hamming(D + (size_t)i * 32, D + (size_t)j * 32);
+            for (int a = 1; a < N; a++) { /* insertion sort */
+                const int x = row[a];
+                int b = a - 1;
+                while (b >= 0 && row[b] > x) {
+                    row[b + 1] = row[b];
+                    b--;
+                }
+                row[b + 1] = x;
+            }
+            const int median = row[(size_t)(0.5 * (N - 1))];
+            if (median < BestMedian) {
+                BestMedian = median;
+                BestIdx = i;
+            }
+        }
+        best[m] = BestIdx;
+        free(row);
+    }
+}

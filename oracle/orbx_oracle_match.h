@@ -84,6 +84,14 @@ int ora_search_by_bow_kf_kf(const ora_frame* kf1, const int32_t* mp1, const int3
                             float nnratio, int check_ori, int32_t* matches12);
 int ora_search_for_initialization(const ora_frame* f1, const ora_frame* f2, float* prev_matched, int32_t* matches12,
                                   int windowSize, float nnratio, int check_ori);
+void ora_fuse(const ora_frame* kf, const int32_t* points, int npoints, const uint8_t* skip, const ora_mappoints* mps,
+              float th, int32_t* best);
+void ora_fuse_sim3(const ora_frame* kf, const float* Scw, const int32_t* points, int npoints, const uint8_t* skip,
+                   const ora_mappoints* mps, float th, int32_t* best);
+int ora_search_by_sim3(const ora_frame* kf1, const int32_t* mp1, const uint8_t* already1, const ora_frame* kf2,
+                       const int32_t* mp2, const uint8_t* already2, const ora_mappoints* mps, float s12,
+                       const float* R12, const float* t12, float th, int32_t* matches12);
+void ora_distinctive_descriptors(int nmp, const int32_t* off, const uint8_t* desc, int32_t* best);
 void ora_undistort_points(const float* K, const float* D, const float* pts, int n, float* out);
 void ora_compute_stereo_matches(const ora_frame* left, const ora_keypoint* keys_r, const uint8_t* desc_r, int nr,
                                 const uint8_t* const* levels_l, const uint8_t* const* levels_r, const int* level_w,

@@ -44,6 +44,8 @@ EXPORTED = [
     "orbx_vocabulary_stage_times", "orbx_search_by_bow_frame", "orbx_search_by_bow_keyframes",
     "orbx_search_for_initialization", "orbx_undistort_keypoints", "orbx_undistort_keypoints_device",
     "orbx_compute_image_bounds", "orbx_assign_features_to_grid", "orbx_assign_features_to_grid_device",
+    "orbx_fuse", "orbx_fuse_sim3", "orbx_search_by_sim3", "orbx_compute_distinctive_descriptors",
+    "orbx_compute_distinctive_descriptors_device",
 ]
 
 
@@ -131,6 +133,11 @@ def lib() -> C.CDLL:
     L.orbx_compute_image_bounds.argtypes = [C.c_int, cp, C.c_int, C.c_int, fp]
     L.orbx_assign_features_to_grid.argtypes = [C.c_int, vp, C.c_int, fp, i32p, i32p]
     L.orbx_assign_features_to_grid_device.argtypes = [C.c_int, vp, vp, C.c_int, fp, vp, vp, vp]
+    L.orbx_fuse.argtypes = [vp, vp, i32p, C.c_int, u8p, vp, C.c_float, i32p]
+    L.orbx_fuse_sim3.argtypes = [vp, vp, fp, i32p, C.c_int, u8p, vp, C.c_float, i32p]
+    L.orbx_search_by_sim3.argtypes = [vp, vp, i32p, u8p, vp, i32p, u8p, vp, C.c_float, fp, fp, C.c_float, i32p, ip]
+    L.orbx_compute_distinctive_descriptors.argtypes = [C.c_int, C.c_int, i32p, u8p, i32p, u8p]
+    L.orbx_compute_distinctive_descriptors_device.argtypes = [C.c_int, vp, vp, vp, vp, vp]
     L.orbx_matcher_set_timing.argtypes = [vp, C.c_int]
     L.orbx_matcher_set_footprint.argtypes = [vp, C.c_int]
     L.orbx_matcher_last_ms.argtypes = [vp, fp]

@@ -61,6 +61,9 @@ hipError_t launch_triangulation(const TriProblem* d_probs, int nprob, unsigned l
 hipError_t launch_stereo(const StereoProblem& pb, StereoResult* out, hipStream_t stream);
 hipError_t launch_bow(const BowProblem* d_prob, int n2, int nitems, hipStream_t stream);
 hipError_t launch_init(const InitProblem* d_prob, int n1, int n2, int nq, hipStream_t stream);
+hipError_t launch_window_best(const BestProblem* d_prob, int nq, hipStream_t stream);
+hipError_t launch_distinctive(int nmp, const int32_t* off, const uint8_t* desc, int32_t* best, uint8_t* out_desc,
+                              hipStream_t stream);
 
 hipError_t launch_window_match(const uint8_t* qdesc, int nq, const uint8_t* tdesc, const int32_t* tlevel,
                                const int32_t* cand_off, const int32_t* cand, int tie_last,

@@ -147,6 +147,30 @@ struct InitProblem {
     int* trunc;                 // scratch [nq]
 };
 
+// Fuse / SearchBySim3: one projected MapPoint searched in a keyframe's grid window
+// for the first keypoint with the smallest distance (no claims).
+struct BestQuery {
+    float u, v, ur, r;  // projection, right-image u (Fuse gate), GetFeaturesInArea radius
+    int pred;           // predicted level: candidates with octave in [pred-1, pred]
+    int pad[3];         // 32-byte record
+};
+
+struct BestProblem {
+    const orbx_keypoint* keys;  // searched keyframe (mvKeysUn)
+    const uint8_t* desc;
+    const float* u_right;       // mvuRight or null (gate only)
+    const int32_t* cell_start;  // mGrid as CSR, cell c = ix * FRAME_GRID_ROWS + iy
+    const int32_t* cell_idx;
+    float inv_sigma2[32];       // mvInvLevelSigma2 (gate only)
+    float min_x, min_y, inv_w, inv_h;
+    const BestQuery* q;
+    const uint8_t* qdesc;       // nq x 32
+    int nq;
+    int gate;                   // 1: Fuse(KF, vpMapPoints) chi-square gate (5.99 mono / 7.8 stereo)
+    int accept;                 // best distance threshold (<=)
+    int32_t* best;              // out [nq]: keypoint index or -1
+};
+
 struct StereoProblem {
     const orbx_keypoint* keys_l;
     const uint8_t* desc_l;

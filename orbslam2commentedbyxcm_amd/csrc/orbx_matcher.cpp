@@ -928,6 +928,316 @@ int orbx_search_for_initialization(orbx_matcher* m, const orbx_frame_view* f1, c
     return ORBX_OK;
 }
 
+namespace {
+
+// Frame::AssignFeaturesToGrid (Frame.cc:351-370) of a view, as CSR (cell c = ix*ROWS + iy).
+void host_grid(const orbx_frame_view* f, std::vector<int32_t>& cstart, std::vector<int32_t>& cidx, float& inv_w,
+               float& inv_h) {
+    inv_w = (float)kGridCols / (f->max_x - f->min_x);
+    inv_h = (float)kGridRows / (f->max_y - f->min_y);
+    cstart.assign(kNumCellsHost + 1, 0);
+    std::vector<int32_t> cell((size_t)f->n);
+    for (int i = 0; i < f->n; i++) {
+        const int px = (int)roundf((f->keys[i].x - f->min_x) * inv_w);  // PosInGrid, Frame.cc:558-567
+        const int py = (int)roundf((f->keys[i].y - f->min_y) * inv_h);
+        cell[(size_t)i] = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? -1 : px * kGridRows + py;
+        if (cell[(size_t)i] >= 0) cstart[cell[(size_t)i] + 1]++;
+    }
+    for (int c = 0; c < kNumCellsHost; c++) cstart[c + 1] += cstart[c];
+    cidx.assign((size_t)cstart[kNumCellsHost] + 1, 0);
+    std::vector<int32_t> fill(cstart.begin(), cstart.end() - 1);
+    for (int i = 0; i < f->n; i++)
+        if (cell[(size_t)i] >= 0) cidx[(size_t)fill[cell[(size_t)i]]++] = i;
+}
+
+// Window-best search of `qs` in keyframe `f` (one k_window_best launch); best[k] out.
+int run_best(orbx_matcher* m, const orbx_frame_view* f, const std::vector<BestQuery>& qs,
+             const std::vector<uint8_t>& qd, int gate, int accept, int32_t* best) {
+    const int nq = (int)qs.size(), n = f->n;
+    if (nq == 0) return ORBX_OK;
+    if (n == 0) {
+        for (int k = 0; k < nq; k++) best[k] = -1;
+        return ORBX_OK;
+    }
+    std::vector<int32_t> cstart, cidx;
+    float inv_w, inv_h;
+    host_grid(f, cstart, cidx, inv_w, inv_h);
+    HIP_TRY(hipSetDevice(m->device));
+    const size_t need = pad(sizeof(orbx_keypoint) * n) + pad((size_t)n * 32) + pad(sizeof(float) * n) +
+                        pad(sizeof(int32_t) * cstart.size()) + pad(sizeof(int32_t) * cidx.size()) +
+                        pad(sizeof(BestQuery) * nq) + pad((size_t)nq * 32) + pad(sizeof(int32_t) * nq) +
+                        pad(sizeof(BestProblem));
+    HIP_TRY(m->arena.reserve(need));
+    m->arena.used = 0;
+    auto* d_k = m->arena.take<orbx_keypoint>(n);
+    auto* d_d = m->arena.take<uint8_t>((size_t)n * 32);
+    auto* d_ur = m->arena.take<float>(n);
+    auto* d_cs = m->arena.take<int32_t>(cstart.size());
+    auto* d_ci = m->arena.take<int32_t>(cidx.size());
+    auto* d_q = m->arena.take<BestQuery>(nq);
+    auto* d_qd = m->arena.take<uint8_t>((size_t)nq * 32);
+    auto* d_best = m->arena.take<int32_t>(nq);
+    auto* d_prob = m->arena.take<BestProblem>(1);
+    hipStream_t s = m->stream;
+    HIP_TRY(hipMemcpyAsync(d_k, f->keys, sizeof(orbx_keypoint) * n, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_d, f->desc, (size_t)n * 32, hipMemcpyHostToDevice, s));
+    if (gate && f->u_right) HIP_TRY(hipMemcpyAsync(d_ur, f->u_right, sizeof(float) * n, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_cs, cstart.data(), sizeof(int32_t) * cstart.size(), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_ci, cidx.data(), sizeof(int32_t) * cidx.size(), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_q, qs.data(), sizeof(BestQuery) * nq, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_qd, qd.data(), (size_t)nq * 32, hipMemcpyHostToDevice, s));
+    BestProblem pb{};
+    pb.keys = d_k;
+    pb.desc = d_d;
+    pb.u_right = (gate && f->u_right) ? d_ur : nullptr;
+    pb.cell_start = d_cs;
+    pb.cell_idx = d_ci;
+    for (int l = 0; l < f->nlevels && l < 32; l++) pb.inv_sigma2[l] = 1.0f / f->level_sigma2[l];  // mvInvLevelSigma2
+    pb.min_x = f->min_x;
+    pb.min_y = f->min_y;
+    pb.inv_w = inv_w;
+    pb.inv_h = inv_h;
+    pb.q = d_q;
+    pb.qdesc = d_qd;
+    pb.nq = nq;
+    pb.gate = gate;
+    pb.accept = accept;
+    pb.best = d_best;
+    HIP_TRY(hipMemcpyAsync(d_prob, &pb, sizeof(pb), hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_window_best(d_prob, nq, s));
+    HIP_TRY(hipMemcpyAsync(best, d_best, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return ORBX_OK;
+}
+
+bool in_image(const orbx_frame_view* f, float u, float v) {  // KeyFrame::IsInImage, KeyFrame.cc:661-663
+    return u >= f->min_x && u < f->max_x && v >= f->min_y && v < f->max_y;
+}
+
+// Shared tail of both Fuse overloads: distance / viewing-angle checks, PredictScale,
+// query record.  Returns false when the MapPoint is rejected before the window search.
+bool fuse_query(const orbx_frame_view* kf, const orbx_mappoints* mps, int mp, const float* Ow, float u, float v,
+                float ur, float th, BestQuery& q) {
+    const float* p3Dw = mps->pos + 3 * (size_t)mp;
+    float PO[3];
+    for (int c = 0; c < 3; c++) PO[c] = p3Dw[c] - Ow[c];
+    const float dist3D = norm3(PO);
+    if (dist3D < 0.8f * mps->min_distance[mp] || dist3D > 1.2f * mps->max_distance[mp]) return false;
+    const float* Pn = mps->normal + 3 * (size_t)mp;
+    double dot = 0.0;  // Mat::dot accumulates in double
+    for (int c = 0; c < 3; c++) dot += (double)PO[c] * Pn[c];
+    if (dot < 0.5 * dist3D) return false;
+    const int pred = predict_scale(mps->max_distance[mp], dist3D, kf);
+    q = BestQuery{};
+    q.u = u;
+    q.v = v;
+    q.ur = ur;
+    q.r = th * kf->scale_factors[pred];
+    q.pred = pred;
+    return true;
+}
+
+bool mps_ok(const orbx_mappoints* mps, bool need_normal) {
+    return mps && mps->pos && mps->desc && mps->max_distance && mps->min_distance && (!need_normal || mps->normal);
+}
+
+}  // namespace
+
+// ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, th), ORBmatcher.cc:1067-1221
+int orbx_fuse(orbx_matcher* m, const orbx_frame_view* kf, const int32_t* points, int npoints, const uint8_t* skip,
+              const orbx_mappoints* mps, float th, int32_t* best) {
+    if (!m || !kf || !skip || !best || !mps_ok(mps, true) || npoints < 0 || (npoints && !points))
+        return fail(ORBX_ERR_ARG, "null argument");
+    if (kf->nlevels < 2) return fail(ORBX_ERR_ARG, "need >= 2 pyramid levels");
+    float Ow[3];
+    centre(kf->Tcw, Ow);
+    std::vector<BestQuery> qs;
+    std::vector<uint8_t> qd;
+    std::vector<int> slot;
+    for (int k = 0; k < npoints; k++) {
+        best[k] = -1;
+        const int mp = points[k];
+        if (mp < 0) continue;
+        if (mp >= mps->n) return fail(ORBX_ERR_ARG, "MapPoint id out of range");
+        if (skip[mp]) continue;  // isBad() || IsInKeyFrame(pKF)
+        float p3Dc[3];
+        project(kf->Tcw, mps->pos + 3 * (size_t)mp, p3Dc);
+        if (p3Dc[2] < 0.0f) continue;
+        const float invz = 1 / p3Dc[2];
+        const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
+        const float u = kf->fx * x + kf->cx, v = kf->fy * y + kf->cy;
+        if (!in_image(kf, u, v)) continue;
+        const float ur = u - kf->bf * invz;
+        BestQuery q;
+        if (!fuse_query(kf, mps, mp, Ow, u, v, ur, th, q)) continue;
+        qs.push_back(q);
+        qd.insert(qd.end(), mps->desc + (size_t)mp * 32, mps->desc + (size_t)mp * 32 + 32);
+        slot.push_back(k);
+    }
+    std::vector<int32_t> out(qs.size());
+    const int rc = run_best(m, kf, qs, qd, 1, TH_LOW, out.data());
+    if (rc != ORBX_OK) return rc;
+    for (size_t j = 0; j < slot.size(); j++) best[slot[j]] = out[j];
+    return ORBX_OK;
+}
+
+// ORBmatcher::Fuse(KeyFrame* pKF, cv::Mat Scw, const vector<MapPoint*>& vpPoints, th,
+// vector<MapPoint*>& vpReplacePoint), ORBmatcher.cc:1226-1352
+int orbx_fuse_sim3(orbx_matcher* m, const orbx_frame_view* kf, const float* Scw, const int32_t* points, int npoints,
+                   const uint8_t* skip, const orbx_mappoints* mps, float th, int32_t* best) {
+    if (!m || !kf || !Scw || !skip || !best || !mps_ok(mps, true) || npoints < 0 || (npoints && !points))
+        return fail(ORBX_ERR_ARG, "null argument");
+    if (kf->nlevels < 2) return fail(ORBX_ERR_ARG, "need >= 2 pyramid levels");
+    double d0 = 0.0;
+    for (int c = 0; c < 3; c++) d0 += (double)Scw[c] * Scw[c];
+    const float scw = (float)std::sqrt(d0);  // cc:1234
+    const float alpha = (float)(1.0 / scw);
+    float T[12];
+    for (int k = 0; k < 12; k++) T[k] = Scw[k] * alpha;
+    float Ow[3];
+    centre(T, Ow);
+    std::vector<BestQuery> qs;
+    std::vector<uint8_t> qd;
+    std::vector<int> slot;
+    for (int k = 0; k < npoints; k++) {
+        best[k] = -1;
+        const int mp = points[k];
+        if (mp < 0 || mp >= mps->n) return fail(ORBX_ERR_ARG, "MapPoint id out of range");
+        if (skip[mp]) continue;  // isBad() || spAlreadyFound.count(pMP)
+        float p3Dc[3];
+        project(T, mps->pos + 3 * (size_t)mp, p3Dc);
+        if (p3Dc[2] < 0.0f) continue;
+        const float invz = (float)(1.0 / p3Dc[2]);
+        const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
+        const float u = kf->fx * x + kf->cx, v = kf->fy * y + kf->cy;
+        if (!in_image(kf, u, v)) continue;
+        BestQuery q;
+        if (!fuse_query(kf, mps, mp, Ow, u, v, 0.f, th, q)) continue;
+        qs.push_back(q);
+        qd.insert(qd.end(), mps->desc + (size_t)mp * 32, mps->desc + (size_t)mp * 32 + 32);
+        slot.push_back(k);
+    }
+    std::vector<int32_t> out(qs.size());
+    const int rc = run_best(m, kf, qs, qd, 0, TH_LOW, out.data());
+    if (rc != ORBX_OK) return rc;
+    for (size_t j = 0; j < slot.size(); j++) best[slot[j]] = out[j];
+    return ORBX_OK;
+}
+
+namespace {
+
+// One direction of SearchBySim3 (cc:1408-1475 / 1477-1545): MapPoints of `src` mapped by
+// x_dst = sR (R_src x + t_src) + t into `dst`, window-searched there (accept <= TH_HIGH).
+int sim3_direction(orbx_matcher* m, const orbx_frame_view* src, const int32_t* src_mp, const uint8_t* already,
+                   const orbx_frame_view* dst, const orbx_mappoints* mps, const float* sR, const float* t, float th,
+                   std::vector<int32_t>& vnMatch) {
+    vnMatch.assign((size_t)src->n, -1);
+    std::vector<BestQuery> qs;
+    std::vector<uint8_t> qd;
+    std::vector<int> slot;
+    for (int i = 0; i < src->n; i++) {
+        const int mp = src_mp[i];
+        if (mp < 0 || (already && already[i])) continue;
+        if (mp >= mps->n) return fail(ORBX_ERR_ARG, "MapPoint id out of range");
+        if (mps->bad && mps->bad[mp]) continue;
+        float pc[3], pd[3];
+        project(src->Tcw, mps->pos + 3 * (size_t)mp, pc);
+        for (int r = 0; r < 3; r++) pd[r] = sR[3 * r] * pc[0] + sR[3 * r + 1] * pc[1] + sR[3 * r + 2] * pc[2] + t[r];
+        if (pd[2] < 0.0) continue;
+        const float invz = (float)(1.0 / pd[2]);
+        const float x = pd[0] * invz, y = pd[1] * invz;
+        const float u = dst->fx * x + dst->cx, v = dst->fy * y + dst->cy;
+        if (!in_image(dst, u, v)) continue;
+        const float dist3D = norm3(pd);
+        if (dist3D < 0.8f * mps->min_distance[mp] || dist3D > 1.2f * mps->max_distance[mp]) continue;
+        const int pred = predict_scale(mps->max_distance[mp], dist3D, dst);
+        BestQuery q{};
+        q.u = u;
+        q.v = v;
+        q.r = th * dst->scale_factors[pred];
+        q.pred = pred;
+        qs.push_back(q);
+        qd.insert(qd.end(), mps->desc + (size_t)mp * 32, mps->desc + (size_t)mp * 32 + 32);
+        slot.push_back(i);
+    }
+    std::vector<int32_t> out(qs.size());
+    const int rc = run_best(m, dst, qs, qd, 0, TH_HIGH, out.data());
+    if (rc != ORBX_OK) return rc;
+    for (size_t j = 0; j < slot.size(); j++) vnMatch[(size_t)slot[j]] = out[j];
+    return ORBX_OK;
+}
+
+}  // namespace
+
+// ORBmatcher::SearchBySim3, ORBmatcher.cc:1361-1602
+int orbx_search_by_sim3(orbx_matcher* m, const orbx_frame_view* kf1, const int32_t* mp1, const uint8_t* already1,
+                        const orbx_frame_view* kf2, const int32_t* mp2, const uint8_t* already2,
+                        const orbx_mappoints* mps, float s12, const float* R12, const float* t12, float th,
+                        int32_t* matches12, int* nfound) {
+    if (!m || !kf1 || !kf2 || !mp1 || !mp2 || !R12 || !t12 || !matches12 || !nfound || !mps_ok(mps, false))
+        return fail(ORBX_ERR_ARG, "null argument");
+    if (kf1->nlevels < 2 || kf2->nlevels < 2) return fail(ORBX_ERR_ARG, "need >= 2 pyramid levels");
+    // sR12 = s12*R12; sR21 = (1.0/s12)*R12^T (a float Mat scaled by (float)(1/s12)); t21 = -sR21*t12
+    float sR12[9], sR21[9], t21[3];
+    const float inv = (float)(1.0 / s12);
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+            sR12[3 * r + c] = s12 * R12[3 * r + c];
+            sR21[3 * r + c] = R12[3 * c + r] * inv;
+        }
+    for (int r = 0; r < 3; r++) t21[r] = -(sR21[3 * r] * t12[0] + sR21[3 * r + 1] * t12[1] + sR21[3 * r + 2] * t12[2]);
+    std::vector<int32_t> vnMatch1, vnMatch2;
+    int rc = sim3_direction(m, kf1, mp1, already1, kf2, mps, sR21, t21, th, vnMatch1);
+    if (rc != ORBX_OK) return rc;
+    rc = sim3_direction(m, kf2, mp2, already2, kf1, mps, sR12, t12, th, vnMatch2);
+    if (rc != ORBX_OK) return rc;
+    int n = 0;
+    for (int i1 = 0; i1 < kf1->n; i1++) {  // mutual check (cc:1547-1560)
+        const int idx2 = vnMatch1[(size_t)i1];
+        if (idx2 >= 0 && vnMatch2[(size_t)idx2] == i1) {
+            matches12[i1] = mp2[idx2];
+            n++;
+        }
+    }
+    *nfound = n;
+    return ORBX_OK;
+}
+
+// MapPoint::ComputeDistinctiveDescriptors, MapPoint.cc:295-360, batched over MapPoints
+int orbx_compute_distinctive_descriptors_device(int nmp, const int32_t* d_off, const uint8_t* d_desc, int32_t* d_best,
+                                                uint8_t* d_out_desc, void* stream) {
+    if (nmp < 0 || (nmp && (!d_off || !d_desc || !d_best))) return fail(ORBX_ERR_ARG, "null argument");
+    HIP_TRY(launch_distinctive(nmp, d_off, d_desc, d_best, d_out_desc, (hipStream_t)stream));
+    return ORBX_OK;
+}
+
+int orbx_compute_distinctive_descriptors(int device, int nmp, const int32_t* off, const uint8_t* desc, int32_t* best,
+                                         uint8_t* out_desc) {
+    if (nmp < 0 || (nmp && (!off || !best))) return fail(ORBX_ERR_ARG, "null argument");
+    if (nmp == 0) return ORBX_OK;
+    const int total = off[nmp];
+    if (total < 0 || (total && !desc)) return fail(ORBX_ERR_ARG, "bad observation offsets");
+    for (int k = 0; k < nmp; k++)
+        if (off[k + 1] < off[k] || off[k] < 0) return fail(ORBX_ERR_ARG, "bad observation offsets");
+    HIP_TRY(hipSetDevice(device));
+    char* d = nullptr;
+    const size_t bo = pad(sizeof(int32_t) * (nmp + 1)), bd = pad((size_t)total * 32), bb = pad(sizeof(int32_t) * nmp),
+                 bx = pad((size_t)nmp * 32);
+    HIP_TRY(hipMalloc((void**)&d, bo + bd + bb + bx));
+    int32_t* d_off = (int32_t*)d;
+    uint8_t* d_desc = (uint8_t*)(d + bo);
+    int32_t* d_best = (int32_t*)(d + bo + bd);
+    uint8_t* d_out = (uint8_t*)(d + bo + bd + bb);
+    hipError_t e = hipMemcpy(d_off, off, sizeof(int32_t) * (nmp + 1), hipMemcpyHostToDevice);
+    if (e == hipSuccess && total) e = hipMemcpy(d_desc, desc, (size_t)total * 32, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_distinctive(nmp, d_off, d_desc, d_best, d_out, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(best, d_best, sizeof(int32_t) * nmp, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && out_desc) e = hipMemcpy(out_desc, d_out, (size_t)nmp * 32, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    HIP_TRY(e);
+    return ORBX_OK;
+}
+
 // Frame::ComputeStereoMatches, Frame.cc:673-885
 int orbx_compute_stereo_matches(orbx_matcher* m, orbx_extractor* ex, int left_frame, int right_frame,
                                 const orbx_frame_view* left, const orbx_keypoint* keys_r, const uint8_t* desc_r,

@@ -229,6 +229,49 @@ class ORBmatcher:
                                                        C.byref(n)))
         return n.value
 
+    # Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, th)  ORBmatcher.cc:1067-1221 (search part)
+    def Fuse(self, kf: FrameView, points, skip, mps: MapPoints, th: float = 3.0) -> np.ndarray:
+        """-> best[k]: the KF keypoint MapPoint points[k] fuses with, or -1."""
+        pts = np.ascontiguousarray(points, dtype=np.int32)
+        sk = np.ascontiguousarray(skip, dtype=np.uint8)
+        best = np.full(max(len(pts), 1), -1, np.int32)
+        kv, mv = kf.c(), mps.c()
+        L.check(L.lib().orbx_fuse(self._h, C.addressof(kv), pts.ctypes.data_as(I32P), len(pts), sk.ctypes.data_as(U8P),
+                                  C.addressof(mv), float(th), best.ctypes.data_as(I32P)))
+        return best[:len(pts)].copy()
+
+    # Fuse(KeyFrame* pKF, cv::Mat Scw, vpPoints, th, vpReplacePoint)  ORBmatcher.cc:1226-1352 (search part)
+    def FuseSim3(self, kf: FrameView, Scw, points, skip, mps: MapPoints, th: float = 4.0) -> np.ndarray:
+        S = np.ascontiguousarray(np.asarray(Scw, dtype=np.float32)[:3, :4])
+        pts = np.ascontiguousarray(points, dtype=np.int32)
+        sk = np.ascontiguousarray(skip, dtype=np.uint8)
+        best = np.full(max(len(pts), 1), -1, np.int32)
+        kv, mv = kf.c(), mps.c()
+        L.check(L.lib().orbx_fuse_sim3(self._h, C.addressof(kv), S.ctypes.data_as(F32P), pts.ctypes.data_as(I32P),
+                                       len(pts), sk.ctypes.data_as(U8P), C.addressof(mv), float(th),
+                                       best.ctypes.data_as(I32P)))
+        return best[:len(pts)].copy()
+
+    # SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)  ORBmatcher.cc:1361-1602
+    def SearchBySim3(self, kf1: FrameView, mp1, kf2: FrameView, mp2, matches12: np.ndarray, mps: MapPoints,
+                     s12: float, R12, t12, th: float = 7.5, already1=None, already2=None) -> int:
+        """matches12 (int32, KF2 MapPoint ids) updated in place; returns nFound."""
+        assert matches12.dtype == np.int32 and matches12.flags.c_contiguous and len(matches12) == len(kf1.keys)
+        a1 = np.ascontiguousarray(mp1, dtype=np.int32)
+        a2 = np.ascontiguousarray(mp2, dtype=np.int32)
+        al1 = None if already1 is None else np.ascontiguousarray(already1, dtype=np.uint8)
+        al2 = None if already2 is None else np.ascontiguousarray(already2, dtype=np.uint8)
+        R = _f32(R12).reshape(9)
+        t = _f32(t12).reshape(3)
+        k1, k2, mv = kf1.c(), kf2.c(), mps.c()
+        n = C.c_int()
+        L.check(L.lib().orbx_search_by_sim3(
+            self._h, C.addressof(k1), a1.ctypes.data_as(I32P), None if al1 is None else al1.ctypes.data_as(U8P),
+            C.addressof(k2), a2.ctypes.data_as(I32P), None if al2 is None else al2.ctypes.data_as(U8P),
+            C.addressof(mv), float(s12), R.ctypes.data_as(F32P), t.ctypes.data_as(F32P), float(th),
+            matches12.ctypes.data_as(I32P), C.byref(n)))
+        return n.value
+
     # SearchForTriangulation(KF1, KF2, F12, vMatchedPairs, bOnlyStereo)  ORBmatcher.cc:850-1056
     def SearchForTriangulation(self, kf1: FrameView, kf1_has_mp, fv1, kf2: FrameView, kf2_has_mp, fv2, F12,
                                bOnlyStereo: bool = False):
@@ -347,3 +390,17 @@ class ORBmatcher:
                                           *(L.i32ptr(out[k]) for k in ("best_idx", "best_dist", "best_level",
                                                                        "second_dist", "second_level"))))
         return out
+
+
+def ComputeDistinctiveDescriptors(off, desc, device: int = 0):
+    """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:295-360) for many MapPoints:
+    MapPoint k's observation descriptors are desc[off[k]:off[k+1]].  -> (best index per
+    MapPoint or -1, chosen descriptors (nmp, 32))."""
+    o = np.ascontiguousarray(off, dtype=np.int32)
+    d = np.ascontiguousarray(desc, dtype=np.uint8).reshape(-1, 32)
+    nmp = len(o) - 1
+    best = np.full(max(nmp, 1), -1, np.int32)
+    out = np.zeros((max(nmp, 1), 32), np.uint8)
+    L.check(L.lib().orbx_compute_distinctive_descriptors(device, nmp, o.ctypes.data_as(I32P), d.ctypes.data_as(U8P),
+                                                         best.ctypes.data_as(I32P), out.ctypes.data_as(U8P)))
+    return best[:nmp].copy(), out[:nmp].copy()
