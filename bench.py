@@ -77,7 +77,7 @@ def stage_bytes(W, H, n_kps, nlevels=8, scale=1.2):
 
 
 # stage -> kernels of one launch of that stage (rocprofv3 kernel names)
-STAGE_KERNELS = {"pyramid": ["orbx::k_copy_level0", "orbx::k_resize"], "score_blur": ["orbx::k_level_tiles"],
+STAGE_KERNELS = {"pyramid": ["orbx::k_pyramid"], "score_blur": ["orbx::k_level_tiles"],
                  "fast_cells": ["orbx::k_fast_cells"], "octree": ["orbx::k_octree"],
                  "describe": ["orbx::k_describe"], "match": ["orbx::k_seq_build", "orbx::k_proj_search<true, true>"]}
 
@@ -93,13 +93,7 @@ def pmc_traffic(stage: str):
     names = STAGE_KERNELS.get(stage, [])
     if not names or any(k not in ks for k in names):
         return None, files[-1].name
-    # k_resize runs once per level: its per-dispatch mean times its dispatches per step
-    tot = 0
-    for k in names:
-        v = ks[k]
-        per_step = v["traffic_bytes"] * (v["dispatches"] // ks["orbx::k_level_tiles"]["dispatches"]
-                                         if k == "orbx::k_resize" else 1)
-        tot += per_step
+    tot = sum(ks[k]["traffic_bytes"] for k in names)
     return int(tot), files[-1].name
 
 

@@ -1,13 +1,14 @@
 // orbx_extract.hip -- MI355X (gfx950) kernels for ORB-SLAM2's ORBextractor::operator().
 //
-// Pipeline for a batch of B frames of one size (one launch per stage, every stage
-// covers all frames and, except the pyramid, all levels at once):
-//   1. k_copy_level0 + k_resize (x L-1) : image pyramid, ORBextractor.cc:1635-1694
-//   2. k_fast_cells   : per 30-px cell FAST-9 score, window-local NMS, iniTh -> minTh
-//                       fallback, ordered compaction            cc:1025-1122
-//   3. k_octree       : DistributeOctTree, one workgroup per (frame, level)  cc:667-1013
-//   4. k_blur         : GaussianBlur 7x7 sigma 2 REFLECT_101 per level       cc:1587-1595
-//   5. k_describe     : IC angle + steered BRIEF + level scaling + output    cc:59-172,1597-1627
+// Pipeline for a batch of B frames of one size (one launch per stage; every stage
+// covers all frames and all levels at once):
+//   1. k_pyramid     : image pyramid, one tile of every level per workgroup   cc:1635-1694
+//   2. k_level_tiles : GaussianBlur 7x7 sigma 2 REFLECT_101 + FAST strength map
+//                                                                 cc:1587-1595, 1091-1104
+//   3. k_fast_cells  : per 30-px cell FAST-9 threshold, window-local NMS, iniTh -> minTh
+//                      fallback, ordered compaction                   cc:1025-1122
+//   4. k_octree      : DistributeOctTree, one workgroup per (frame, level)  cc:667-1013
+//   5. k_describe    : IC angle + steered BRIEF + level scaling + output   cc:59-172, 1597-1627
 // Bit-exactness: integer arithmetic everywhere except fastAtan2/cos/sin/cvRound,
 // which follow the reference's float expression order (built -ffp-contract=off).
 #include <hip/hip_runtime.h>
@@ -62,110 +63,196 @@ __device__ __forceinline__ void xcd_frame_block(int per_frame, int nframes, int&
 
 // ------------------------------------------------------------------ pyramid
 
-// Level 0 = the input frame copied into the pyramid block (ORBextractor.cc:1688-1690;
-// the REFLECT_101 border is never read by extraction).  16 bytes per lane when the
-// rows are 16-byte aligned.
-__global__ __launch_bounds__(256) void k_copy_level0(const uint8_t* __restrict__ src, size_t frame_pitch,
-                                                     size_t stride, int w, int h, uint8_t* __restrict__ pyr,
-                                                     long long fb, int pitch, int vec16) {
-    const int f = blockIdx.y;
-    const uint8_t* s = src + (size_t)f * frame_pitch;
-    uint8_t* d = pyr + (size_t)f * fb;
-    if (vec16) {
-        const int per_row = w >> 4;
-        const int total = per_row * h;
-        for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
-            const int y = i / per_row, x = (i - y * per_row) << 4;
-            *(uint4*)(d + (size_t)y * pitch + x) = *(const uint4*)(s + (size_t)y * stride + x);
-        }
+// 24 x 24 -> high 32 bits of the 48-bit product (v_mul_hi_u32_u24)
+__device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
+    return (uint32_t)(((unsigned long long)(a & 0xffffff) * (b & 0xffffff)) >> 32);
+}
+
+// The whole pyramid of one tile per workgroup (ORBextractor::ComputePyramid,
+// ORBextractor.cc:1635-1694): level 0 is the input frame (cc:1688-1690; the
+// REFLECT_101 border is never read by extraction), level l is
+// cv::resize(level l-1 ROI, INTER_LINEAR) (cc:1656-1661), OpenCV 3.3.1 fixed point:
+// h = S[sx0]*a0 + S[sx1]*a1 (exact), dst = ((b0*(h0>>4))>>16 + (b1*(h1>>4))>>16 + 2)>>2.
+// The tile's needed rectangle of every level (its own pixels plus the source footprint
+// of the next level, orbx_geometry.h) lives in LDS, ping-ponging between two buffers,
+// so the L-level cascade is one launch: only level 0 is read from HBM, and every
+// pixel a tile owns is written once.  Threads own a column quad and a run of rows;
+// each source row's horizontal sums are computed once and reused by the (one or two)
+// output rows that read it.  (b*(h>>4))>>16 is one v_mul_hi_u32_u24 on (b<<8, (h>>4)<<8).
+// Write the bytes of quad [x, x+4) that fall in the owned columns [ox0, ox1).
+__device__ __forceinline__ void store_owned_quad(uint8_t* o, int x, int ox0, int ox1, uint32_t packed) {
+    if (x >= ox0 && x + 4 <= ox1) {
+        *(uint32_t*)o = packed;
     } else {
-        const int total = w * h;
-        for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
-            const int y = i / w, x = i - y * w;
-            d[(size_t)y * pitch + x] = s[(size_t)y * stride + x];
-        }
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+            if (x + b >= ox0 && x + b < ox1) o[b] = (uint8_t)(packed >> (8 * b));
     }
 }
 
-// cv::resize(level l-1 ROI, level l, INTER_LINEAR), OpenCV 3.3.1 fixed point:
-// h = S[sx0]*a0 + S[sx1]*a1 (exact), dst = ((b0*(h0>>4))>>16 + (b1*(h1>>4))>>16 + 2)>>2.
-// One kRzTW x kRzTH (256 x 32) output tile per workgroup (XCD-aware frame placement).
-// The tile's source region is staged in LDS with dword loads (columns aligned down to
-// 4 bytes; sw x sh bytes of dynamic LDS sized by the plan); each lane keeps the
-// horizontal taps of its 4 output columns in registers and the waves walk the rows,
-// whose vertical taps are wave-uniform.  Output rows are written as dwords.
-__global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, long long fb,
-                                                const LevelGeom* __restrict__ lv, int l,
-                                                const int16_t* __restrict__ rtab, int nframes, int sw) {
-    extern __shared__ __align__(16) uint8_t s_src[];
-    const LevelGeom& g = lv[l];
-    const LevelGeom& p = lv[l - 1];
-    const int tx = (g.w + kRzTW - 1) / kRzTW, tyn = (g.h + kRzTH - 1) / kRzTH;
-    int f, b;
-    xcd_frame_block(tx * tyn, nframes, f, b);
-    const int by = b / tx;
-    const int X0 = (b - by * tx) * kRzTW, Y0 = by * kRzTH;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int16_t* xt = rtab + g.xtab_off;
-    const int16_t* yt = rtab + g.ytab_off;
-    const int xe = min(X0 + kRzTW, g.w) - 1, ye = min(Y0 + kRzTH, g.h) - 1;
-    const int a_lo = xt[4 * X0] & ~3, sx_hi = xt[4 * xe + 1];
-    const int sy_lo = yt[4 * Y0], sy_hi = yt[4 * ye + 1];
-    const int ncols4 = ((sx_hi - a_lo) >> 2) + 1, nrows = sy_hi - sy_lo + 1;
-    const uint8_t* base = pyr + (size_t)f * fb + p.off + (size_t)sy_lo * p.pitch + a_lo;
-    const int nld = nrows * ncols4;
-    for (int i0 = 0; i0 < nld; i0 += 256 * 8) {  // 8 loads in flight per thread
-        uint32_t v[8];
+// Thread -> (column quad, row group) split of a level rectangle nq quads wide: G groups
+// of nqp lanes; the quotient comes from a float reciprocal (exact for tid < 256).
+struct QuadSplit {
+    int nqp, G, q, gr;
+};
+__device__ __forceinline__ QuadSplit quad_split(int nq, int tid) {
+    QuadSplit s;
+    s.nqp = min(nq, 256);
+    s.G = 256 / s.nqp;
+    s.gr = (int)(((float)tid + 0.5f) * (1.0f / (float)s.nqp));
+    s.q = tid - s.gr * s.nqp;
+    return s;
+}
+
+__global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ src, size_t frame_pitch, size_t stride,
+                                                 int vec4, uint8_t* __restrict__ pyr, long long fb,
+                                                 const LevelGeom* __restrict__ lv, int L,
+                                                 const int16_t* __restrict__ rtab, int pz_off, int tiles_pf,
+                                                 int nframes, int lds_a) {
+    extern __shared__ __align__(16) uint8_t s_pz[];
+    int f, tile;
+    xcd_frame_block(tiles_pf, nframes, f, tile);
+    const int tid = threadIdx.x;
+    const int16_t* R = rtab + pz_off + (size_t)tile * L * 8;
+    uint8_t* const frame = pyr + (size_t)f * fb;
+    // LDS rows of a level hold its needed columns widened to whole quads, [x0 & ~3, ...)
+    // ---- level 0: load the needed rectangle into buffer A, write the owned part
+    {
+        const int x0 = R[0], y0 = R[1], x1 = R[2], y1 = R[3];
+        const int ox0 = R[4], oy0 = R[5], ox1 = R[6], oy1 = R[7];
+        const LevelGeom& g = lv[0];
+        if (x1 > x0 && y1 > y0) {
+            const int xa = x0 & ~3;
+            const int nq = (x1 - xa + 3) >> 2, hn = y1 - y0, ostride = 4 * nq;
+            const QuadSplit sp = quad_split(nq, tid);
+            const uint8_t* in = src + (size_t)f * frame_pitch;
+            if (sp.gr < sp.G) {
+                for (int qq = sp.q; qq < nq; qq += sp.nqp) {
+                    const int x = xa + 4 * qq;
+                    const bool full = x + 4 <= g.w;
+                    const bool own_x = x + 4 > ox0 && x < ox1;
+                    for (int r0 = sp.gr; r0 < hn; r0 += 8 * sp.G) {  // 8 rows in flight
+                        uint32_t v[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const int i = min(i0 + tid + 256 * k, nld - 1);
-            const int r = i / ncols4, c = i - r * ncols4;
-            v[k] = *(const uint32_t*)(base + (size_t)r * p.pitch + 4 * c);
-        }
+                        for (int k = 0; k < 8; k++) {
+                            const int y = y0 + min(r0 + k * sp.G, hn - 1);
+                            const uint8_t* p = in + (size_t)y * stride + x;
+                            if (vec4 && full) {
+                                v[k] = *(const uint32_t*)p;
+                            } else {
+                                uint32_t w = 0;
+                                for (int b = 0; b < 4 && x + b < g.w; b++) w |= (uint32_t)p[b] << (8 * b);
+                                v[k] = w;
+                            }
+                        }
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const int i = i0 + tid + 256 * k;
-            if (i < nld) {
-                const int r = i / ncols4, c = i - r * ncols4;
-                *(uint32_t*)&s_src[r * sw + 4 * c] = v[k];
+                        for (int k = 0; k < 8; k++) {
+                            const int r = r0 + k * sp.G;
+                            if (r < hn) {
+                                *(uint32_t*)&s_pz[r * ostride + 4 * qq] = v[k];
+                                const int y = y0 + r;
+                                if (own_x && y >= oy0 && y < oy1)
+                                    store_owned_quad(frame + g.off + (size_t)y * g.pitch + x, x, ox0, ox1, v[k]);
+                            }
+                        }
+                    }
+                }
             }
         }
     }
-    // horizontal taps of this lane's 4 columns
-    const int cx = X0 + 4 * lane;
-    const int nvalid = min(4, g.w - cx);
-    int sx0[4], sx1[4], a0[4], a1[4];
+    // ---- levels 1..L-1 from the previous level's rectangle in LDS.
+    // h = S[sx0]*a0 + S[sx1]*a1 is kept as hm = h & ~15 and the vertical step
+    // (b*(h>>4))>>16 = (b*hm)>>20 is one v_mul_hi_u32_u24 of (b << 12, hm).  The result
+    // needs no saturation: a0 + a1 <= 2049 and b0 + b1 <= 2049 bound it by 255.
+    for (int l = 1; l < L; l++) {
+        __syncthreads();
+        const int16_t* Rp = R + 8 * (l - 1);
+        const int16_t* Rl = R + 8 * l;
+        const int sxa = Rp[0] & ~3, sy0 = Rp[1], sstride = 4 * ((Rp[2] - sxa + 3) >> 2);
+        const int x0 = Rl[0], y0 = Rl[1], x1 = Rl[2], y1 = Rl[3];
+        const int ox0 = Rl[4], oy0 = Rl[5], ox1 = Rl[6], oy1 = Rl[7];
+        if (!(x1 > x0 && y1 > y0)) continue;  // block-uniform
+        const uint8_t* sb = s_pz + ((l & 1) ? 0 : lds_a);
+        uint8_t* ob = s_pz + ((l & 1) ? lds_a : 0);
+        const LevelGeom& g = lv[l];
+        const int16_t* xt = rtab + g.xtab_off;
+        const int xa = x0 & ~3;
+        const int nq = (x1 - xa + 3) >> 2, hn = y1 - y0, ostride = 4 * nq;
+        const QuadSplit sp = quad_split(nq, tid);
+        if (sp.gr >= sp.G) continue;
+        const int rc = (hn + sp.G - 1) / sp.G;
+        const int ra = sp.gr * rc, rb = min(hn, ra + rc);
+        if (ra >= rb) continue;
+        // owned rows of this thread's run, relative to the rectangle
+        const int wlo = max(ra, oy0 - y0), whi = min(rb, oy1 - y0);
+        for (int qq = sp.q; qq < nq; qq += sp.nqp) {
+            const int x = xa + 4 * qq;
+            // 0: not owned, 1: whole quad owned, 2: partly owned
+            const int own = (x + 4 <= ox0 || x >= ox1) ? 0 : ((x >= ox0 && x + 4 <= ox1) ? 1 : 2);
+            int c0[4], c1[4];
+            uint32_t a0[4], a1[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int dx = k < nvalid ? cx + k : X0;
-        const int2 t = *(const int2*)(xt + 4 * dx);  // sx0, sx1, a0, a1 as 4 x int16
-        sx0[k] = (int16_t)(t.x & 0xffff) - a_lo;
-        sx1[k] = (int16_t)(t.x >> 16) - a_lo;
-        a0[k] = (int16_t)(t.y & 0xffff);
-        a1[k] = (int16_t)(t.y >> 16);
-    }
-    __syncthreads();
-    if (nvalid <= 0) return;
-    uint8_t* out = pyr + (size_t)f * fb + g.off + cx;
-    for (int r = wave; Y0 + r <= ye; r += 4) {
-        const int dy = Y0 + r;
-        const int2 t = *(const int2*)(yt + 4 * dy);  // wave-uniform: r0, r1, b0, b1
-        const uint8_t* s0 = s_src + ((int16_t)(t.x & 0xffff) - sy_lo) * sw;
-        const uint8_t* s1 = s_src + ((int16_t)(t.x >> 16) - sy_lo) * sw;
-        const int b0 = (int16_t)(t.y & 0xffff), b1 = (int16_t)(t.y >> 16);
-        uint32_t packed = 0;
+            for (int k = 0; k < 4; k++) {
+                // columns outside [x0, x1) (quad widening) borrow x0's taps: their bytes
+                // are computed but never read by the next level and never owned
+                const int dx = x + k >= x0 && x + k < x1 ? x + k : x0;
+                const int2 t = *(const int2*)(xt + 4 * dx);  // sx0, sx1, a0, a1 as 4 x int16
+                c0[k] = (int16_t)(t.x & 0xffff) - sxa;
+                c1[k] = (int16_t)(t.x >> 16) - sxa;
+                a0[k] = (uint32_t)(t.y & 0xffff);
+                a1[k] = (uint32_t)t.y >> 16;
+            }
+            const int16_t* yp = rtab + g.ytab_off + 4 * (y0 + ra);
+            uint8_t* lp = ob + ra * ostride + 4 * qq;
+            uint8_t* gp = frame + g.off + (size_t)(y0 + ra) * g.pitch + x;
+            int s_cur = -1;
+            const uint8_t* srow = sb;
+            uint32_t hc[4] = {0, 0, 0, 0}, hp[4] = {0, 0, 0, 0};
+            for (int rr = ra; rr < rb; rr += 8) {
+                int2 yv[8];  // 8 rows' taps r0, r1, b0, b1 in flight (rtab is padded at the end)
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int h0 = s0[sx0[k]] * a0[k] + s0[sx1[k]] * a1[k];
-            const int h1 = s1[sx0[k]] * a0[k] + s1[sx1[k]] * a1[k];
-            int v = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
-            v = v < 0 ? 0 : (v > 255 ? 255 : v);
-            packed |= (uint32_t)v << (8 * k);
+                for (int k = 0; k < 8; k++) yv[k] = *(const int2*)(yp + 4 * k);
+                yp += 32;
+#pragma unroll
+                for (int kb = 0; kb < 8; kb++) {
+                    const int r = rr + kb;
+                    if (r >= rb) break;
+                    const int2 t = yv[kb];
+                    const int r0 = (int16_t)(t.x & 0xffff), r1 = (int16_t)(t.x >> 16);
+                    while (s_cur < r1) {  // the source rows are monotone; each is summed once
+                        if (s_cur < 0) {
+                            s_cur = r0;
+                            srow = sb + (r0 - sy0) * sstride;
+                        } else {
+                            s_cur++;
+                            srow += sstride;
+                        }
+#pragma unroll
+                        for (int k = 0; k < 4; k++) {
+                            hp[k] = hc[k];
+                            // two byte reads (a merged u16 read would be unaligned)
+                            hc[k] = (srow[c0[k]] * a0[k] + srow[c1[k]] * a1[k]) & ~15u;
+                        }
+                    }
+                    const uint32_t b0 = ((uint32_t)t.y & 0xffffu) << 12, b1 = ((uint32_t)t.y >> 16) << 12;
+                    const bool same = r0 == s_cur;
+                    uint32_t packed = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t v = (mulhi24(b0, same ? hc[k] : hp[k]) + mulhi24(b1, hc[k]) + 2) >> 2;
+                        packed |= v << (8 * k);
+                    }
+                    *(uint32_t*)lp = packed;
+                    if (own != 0 && r >= wlo && r < whi) {
+                        if (own == 1) *(uint32_t*)gp = packed;
+                        else
+                            store_owned_quad(gp, x, ox0, ox1, packed);
+                    }
+                    lp += ostride;
+                    gp += g.pitch;
+                }
+            }
         }
-        uint8_t* o = out + (size_t)dy * g.pitch;
-        if (nvalid == 4) *(uint32_t*)o = packed;
-        else
-            for (int k = 0; k < nvalid; k++) o[k] = (uint8_t)(packed >> (8 * k));
     }
 }
 
@@ -177,22 +264,21 @@ typedef short short2_t __attribute__((ext_vector_type(2)));
 // max(min(v - ring), min(ring - v)).  At threshold t the pixel is a corner iff
 // M > t, and cornerScore<16> then returns max(t, M) - 1 = M - 1, independent of t
 // (features2d/fast.cpp FAST_t / fast_score.cpp cornerScore<16>).  Both signs are
-// evaluated at once in packed int16 lanes: (v - x, x - v).
+// evaluated at once in packed int16 lanes on (x, 255 - x): per arc,
+// min(x - v) = min(x) - v and min(v - x) = min(255 - x) - (255 - v), so the arc
+// minima of the pairs are taken first and (v, 255 - v) is subtracted once.  The pair
+// is one v_mad_i32_i24: x * (1 - 2^16) + 255 * 2^16.
 __device__ __forceinline__ int fast_strength(const uint8_t* c, int pitch) {
     const int off[16] = {0 + 3 * pitch,  1 + 3 * pitch,  2 + 2 * pitch,  3 + 1 * pitch,
                          3,              3 - 1 * pitch,  2 - 2 * pitch,  1 - 3 * pitch,
                          0 - 3 * pitch, -1 - 3 * pitch, -2 - 2 * pitch, -3 - 1 * pitch,
                          -3,            -3 + 1 * pitch, -2 + 2 * pitch, -1 + 3 * pitch};
     const int v = c[0];
-    const short2_t V = __builtin_bit_cast(short2_t, (int)(v - (v << 16)));   // (v, -v)
     short2_t d[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int x = c[off[k]];
-        d[k] = V - __builtin_bit_cast(short2_t, (int)(x - (x << 16)));       // (v - x, x - v)
-    }
+    for (int k = 0; k < 16; k++) d[k] = __builtin_bit_cast(short2_t, (int)c[off[k]] * -65535 + 0xff0000);
     // For odd j, m8[j] = min(d[j..j+7]) serves two arcs: [j-1, j+7] and [j, j+8]
-    // (55 packed min/max instead of 79 for all 16 arcs independently).
+    // (47 packed min/max instead of 79 for all 16 arcs independently).
     short2_t m2[8], m4[8], m8[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) m2[i] = __builtin_elementwise_min(d[2 * i + 1], d[(2 * i + 2) & 15]);
@@ -200,13 +286,15 @@ __device__ __forceinline__ int fast_strength(const uint8_t* c, int pitch) {
     for (int i = 0; i < 8; i++) m4[i] = __builtin_elementwise_min(m2[i], m2[(i + 1) & 7]);
 #pragma unroll
     for (int i = 0; i < 8; i++) m8[i] = __builtin_elementwise_min(m4[i], m4[(i + 2) & 7]);
-    short2_t best = __builtin_elementwise_min(m8[0], d[0]);
+    // the two arcs of m8[j] give max(min(m8, d[j-1]), min(m8, d[j+8])) = min(m8, max(d[j-1], d[j+8]))
+    short2_t best = __builtin_elementwise_min(m8[0], __builtin_elementwise_max(d[0], d[9]));
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
+    for (int i = 1; i < 8; i++) {
         const int j = 2 * i + 1;
-        if (i > 0) best = __builtin_elementwise_max(best, __builtin_elementwise_min(m8[i], d[j - 1]));
-        best = __builtin_elementwise_max(best, __builtin_elementwise_min(m8[i], d[(j + 8) & 15]));
+        best = __builtin_elementwise_max(
+            best, __builtin_elementwise_min(m8[i], __builtin_elementwise_max(d[j - 1], d[(j + 8) & 15])));
     }
+    best = best - __builtin_bit_cast(short2_t, v * -65535 + 0xff0000);  // (min x - v, v - max x)
     const int M = best.x > best.y ? best.x : best.y;
     return M > 0 ? M : 0;
 }
@@ -263,7 +351,7 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
     __shared__ __align__(16) uint8_t s_in[kTH + 6][kSW];
     __shared__ __align__(16) uint32_t s_rowp[(kTH + 6) / 2][kTW];  // (row 2p, row 2p+1) u16 pairs
     __shared__ __align__(16) uint8_t s_m[kTH][kTW];
-    __shared__ uint16_t s_list[kTH * kTW];
+    __shared__ uint16_t s_list[kTH * kTW + 1];  // + a dump slot for branch-free appends
     __shared__ int s_n;
     int f, tile;
     xcd_frame_block(tiles_pf, nframes, f, tile);
@@ -292,18 +380,30 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
             if (i < kN) ((uint32_t*)s_in)[i] = v[k];
         }
     } else {
-        constexpr int kN = (kTH + 6) * kSW, kPer = (kN + 255) / 256;
-        uint8_t v[kPer];
+        // edge tile: the same dword loads with the start column clamped into the row
+        // (an in-range column's dword never clamps: pitch >= w rounded up to 4), then
+        // the only reflected columns anything reads, -3..-1 and w..w+2 (the blur's
+        // reach; FAST stays inside [16, w - 16)), are rewritten from the staged row.
+        constexpr int kN = (kTH + 6) * (kSW / 4), kPer = (kN + 255) / 256;
+        uint32_t v[kPer];
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             const int i = min(tid + 256 * k, kN - 1);
-            const int r = i / kSW, c = i - r * kSW;
-            v[k] = img[(size_t)reflect101(Y0 + r - 3, g.h) * g.pitch + reflect101(min(X0 - 4 + c, 2 * g.w - 2), g.w)];
+            const int r = i / (kSW / 4), c4 = i - r * (kSW / 4);
+            const int col = min(max(X0 - 4 + 4 * c4, 0), g.pitch - 4);
+            v[k] = *(const uint32_t*)(img + (size_t)reflect101(Y0 + r - 3, g.h) * g.pitch + col);
         }
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             const int i = tid + 256 * k;
-            if (i < kN) ((uint8_t*)s_in)[i] = v[k];
+            if (i < kN) ((uint32_t*)s_in)[i] = v[k];
+        }
+        __syncthreads();
+        if (tid < (kTH + 6) * 6) {
+            const int r = tid / 6, k = tid - 6 * r;
+            const int col = k < 3 ? -1 - k : g.w + k - 3;  // REFLECT_101 source: -col or 2w - 2 - col
+            const int sc = col - X0 + 4, ss = (k < 3 ? -col : 2 * g.w - 2 - col) - X0 + 4;
+            if (sc >= 0 && sc < kSW) s_in[r][sc] = s_in[r][ss];
         }
     }
     if (tid == 0) s_n = 0;
@@ -320,56 +420,69 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
         *(uint4*)&s_rowp[pr][c0 - 4] = make_uint4(a[0] | (b[0] << 16), a[1] | (b[1] << 16), a[2] | (b[2] << 16),
                                                   a[3] | (b[3] << 16));
     }
-    // ---- FAST compass test on the detection area, compaction of the survivors
-    for (int i = tid; i < kTH * (kTW / 4); i += 256) {
-        const int r = i >> 4, j = i & 15, c0 = 4 + 4 * j;
-        const int y = Y0 + r, x0 = X0 + 4 * j;
-        unsigned pass = 0;
-        if (y >= kEdge && y < g.h - kEdge && x0 + 3 >= kEdge && x0 < g.w - kEdge) {
-            const uint32_t* rc = (const uint32_t*)&s_in[r + 3][c0];
-            const uint32_t V = rc[0];
-            const uint32_t C0 = *(const uint32_t*)&s_in[r + 6][c0];  // ring 0  (0, +3)
-            const uint32_t C8 = *(const uint32_t*)&s_in[r][c0];      // ring 8  (0, -3)
-            const uint32_t C4 = row_bytes(rc[-1], rc[0], rc[1], 3);   // ring 4  (+3, 0)
-            const uint32_t C12 = row_bytes(rc[-1], rc[0], rc[1], -3); // ring 12 (-3, 0)
+    // ---- FAST compass test on the detection area, compaction of the survivors.
+    // A thread always owns columns 4j..4j+3 (j = tid & 15) of rows tid/16 and
+    // tid/16 + 16, so its detection-area column mask is computed once.
+    {
+        const int j = tid & 15, c0 = 4 + 4 * j, x0 = X0 + 4 * j;
+        unsigned colmask = 0;
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const short2_t v = __builtin_bit_cast(short2_t, h ? hi_pair(V) : lo_pair(V));
-                const short2_t a0 = __builtin_bit_cast(short2_t, h ? hi_pair(C0) : lo_pair(C0)) - v;
-                const short2_t a4 = __builtin_bit_cast(short2_t, h ? hi_pair(C4) : lo_pair(C4)) - v;
-                const short2_t a8 = __builtin_bit_cast(short2_t, h ? hi_pair(C8) : lo_pair(C8)) - v;
-                const short2_t a12 = __builtin_bit_cast(short2_t, h ? hi_pair(C12) : lo_pair(C12)) - v;
-                // bright: min of an adjacent pair of (x - v); dark: min of (v - x) = -max(x - v)
-                const short2_t br = __builtin_elementwise_max(
-                    __builtin_elementwise_max(__builtin_elementwise_min(a0, a4), __builtin_elementwise_min(a4, a8)),
-                    __builtin_elementwise_max(__builtin_elementwise_min(a8, a12), __builtin_elementwise_min(a12, a0)));
-                const short2_t dk = __builtin_elementwise_min(
-                    __builtin_elementwise_min(__builtin_elementwise_max(a0, a4), __builtin_elementwise_max(a4, a8)),
-                    __builtin_elementwise_min(__builtin_elementwise_max(a8, a12), __builtin_elementwise_max(a12, a0)));
-                if (br.x > tq || -dk.x > tq) pass |= 1u << (2 * h);
-                if (br.y > tq || -dk.y > tq) pass |= 2u << (2 * h);
+        for (int k = 0; k < 4; k++) colmask |= (x0 + k >= kEdge && x0 + k < g.w - kEdge) ? 1u << k : 0u;
+        const short2_t tq1 = {(short)(tq + 1), (short)(tq + 1)};
+#pragma unroll
+        for (int it = 0; it < 2; it++) {
+            const int r = (tid >> 4) + 16 * it;
+            const int y = Y0 + r;
+            unsigned pass = 0;
+            if (colmask != 0 && y >= kEdge && y < g.h - kEdge) {
+                const uint32_t* rc = (const uint32_t*)&s_in[r + 3][c0];
+                const uint32_t V = rc[0];
+                const uint32_t C0 = *(const uint32_t*)&s_in[r + 6][c0];  // ring 0  (0, +3)
+                const uint32_t C8 = *(const uint32_t*)&s_in[r][c0];      // ring 8  (0, -3)
+                const uint32_t C4 = row_bytes(rc[-1], rc[0], rc[1], 3);   // ring 4  (+3, 0)
+                const uint32_t C12 = row_bytes(rc[-1], rc[0], rc[1], -3); // ring 12 (-3, 0)
+                uint32_t q[2];
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const short2_t v = __builtin_bit_cast(short2_t, h ? hi_pair(V) : lo_pair(V));
+                    const short2_t a0 = __builtin_bit_cast(short2_t, h ? hi_pair(C0) : lo_pair(C0)) - v;
+                    const short2_t a4 = __builtin_bit_cast(short2_t, h ? hi_pair(C4) : lo_pair(C4)) - v;
+                    const short2_t a8 = __builtin_bit_cast(short2_t, h ? hi_pair(C8) : lo_pair(C8)) - v;
+                    const short2_t a12 = __builtin_bit_cast(short2_t, h ? hi_pair(C12) : lo_pair(C12)) - v;
+                    // bright: min of an adjacent pair of (x - v); dark: min of (v - x) = -max(x - v)
+                    const short2_t br = __builtin_elementwise_max(
+                        __builtin_elementwise_max(__builtin_elementwise_min(a0, a4), __builtin_elementwise_min(a4, a8)),
+                        __builtin_elementwise_max(__builtin_elementwise_min(a8, a12), __builtin_elementwise_min(a12, a0)));
+                    const short2_t dk = __builtin_elementwise_min(
+                        __builtin_elementwise_min(__builtin_elementwise_max(a0, a4), __builtin_elementwise_max(a4, a8)),
+                        __builtin_elementwise_min(__builtin_elementwise_max(a8, a12), __builtin_elementwise_max(a12, a0)));
+                    // max(br, -dk) - (tq + 1) >= 0 <=> the pixel passes; sign in bits 15 / 31
+                    q[h] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(br, short2_t{0, 0} - dk) - tq1);
+                }
+                // sign bytes of the 4 pixels -> bit k of pass (clear sign = pass)
+                const uint32_t sb = ~__builtin_amdgcn_perm(q[1], q[0], 0x07050301u) & 0x80808080u;
+                pass = (((sb >> 7) * 0x01020408u) >> 24) & colmask;
             }
+            // wave-level append: offsets from the per-bit ballots, one LDS atomic per wave;
+            // list order is irrelevant (each entry names its own pixel)
+            unsigned off = 0;
+            int tot = 0;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const int x = x0 + k;
-                if (x < kEdge || x >= g.w - kEdge) pass &= ~(1u << k);
+                const unsigned long long m = __ballot((pass >> k) & 1u);
+                off = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, off));
+                tot += __popcll(m);
             }
-        }
-        // wave-level append: offsets from the per-bit ballots, one LDS atomic per wave
-        const unsigned long long below = (1ull << lane) - 1;
-        int off = 0, tot = 0;
+            int base = 0;
+            if (lane == 0 && tot) base = atomicAdd(&s_n, tot);
+            base = __shfl(base, 0) + off;
+            const int rowc = (r << 8) | (4 * j);
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const unsigned long long m = __ballot((pass >> k) & 1u);
-            off += __popcll(m & below);
-            tot += __popcll(m);
-        }
-        int base = 0;
-        if (lane == 0 && tot) base = atomicAdd(&s_n, tot);
-        base = __shfl(base, 0);
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            if ((pass >> k) & 1u) s_list[base + off++] = (uint16_t)((r << 8) | (4 * j + k));
+            for (int k = 0; k < 4; k++) {
+                const bool p = (pass >> k) & 1u;
+                s_list[p ? base : kTH * kTW] = (uint16_t)(rowc + k);
+                base += p;
+            }
         }
     }
     __syncthreads();
@@ -1244,24 +1357,16 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     if (ev) (void)hipEventRecord(ev[0], stream);
     (void)hipMemsetAsync(db.status, 0, sizeof(int) * (size_t)batch, stream);
     {
-        const LevelGeom& g0 = plan.lv[0];
-        const int vec16 = ((uintptr_t)d_imgs % 16 == 0) && (stride % 16 == 0) && (frame_pitch % 16 == 0) &&
-                          (g0.w % 16 == 0);
-        dim3 grid(64, batch);
-        hipLaunchKernelGGL(k_copy_level0, grid, dim3(256), 0, stream, d_imgs, frame_pitch, stride, g0.w, g0.h,
-                           db.pyr, fb, g0.pitch, vec16);
-        const size_t rz_lds = (size_t)plan.rz_sw * plan.rz_sh;
-        if (rz_lds > 64 * 1024) {
-            hipError_t e = hipFuncSetAttribute((const void*)k_resize, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)rz_lds);
+        const int vec4 = ((uintptr_t)d_imgs % 4 == 0) && (stride % 4 == 0) && (frame_pitch % 4 == 0);
+        const size_t lds = (size_t)plan.pz_lds_a + plan.pz_lds_b;
+        if (lds > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void*)k_pyramid, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)lds);
             if (e != hipSuccess) return e;
         }
-        for (int l = 1; l < L; l++) {
-            const LevelGeom& g = plan.lv[l];
-            dim3 gr(((g.w + kRzTW - 1) / kRzTW) * ((g.h + kRzTH - 1) / kRzTH) * batch);
-            hipLaunchKernelGGL(k_resize, gr, dim3(256), rz_lds, stream, db.pyr, fb, db.lv, l, db.rtab, batch,
-                               plan.rz_sw);
-        }
+        hipLaunchKernelGGL(k_pyramid, dim3(plan.pz_tiles * batch), dim3(256), lds, stream, d_imgs, frame_pitch,
+                           stride, vec4, db.pyr, fb, db.lv, L, db.rtab, plan.pz_off, plan.pz_tiles, batch,
+                           plan.pz_lds_a);
     }
     if (ev) (void)hipEventRecord(ev[1], stream);
     {

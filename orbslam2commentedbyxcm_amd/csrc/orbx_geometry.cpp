@@ -5,6 +5,8 @@
 #include "orbx_geometry.h"
 
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 namespace orbx {
@@ -98,6 +100,85 @@ static void resize_tables(int sw, int sh, int dw, int dh, int16_t* xtab, int16_t
         t[2] = (int16_t)cv_roundf((1.f - fy) * 2048);
         t[3] = (int16_t)cv_roundf(fy * 2048);
     }
+}
+
+// k_pyramid tile rectangles (orbx_geometry.h).  Ownership: level 0 is split into an
+// nx x ny grid; a boundary b at level l - 1 moves to the first level-l column (row)
+// whose resize source starts at or after b, so a tile's owned pixels at level l read
+// only its own pixels at level l - 1 apart from the one-pixel right / bottom reach of
+// the interpolation.  Needed rectangles are then grown from the top level down by the
+// resize tables' source footprints (the tables are monotone, so a range of columns
+// maps to [t(first).s0, t(last).s1]): the halo is 0 on the left / top and about
+// 1 + 1.2 * (halo of the level above) on the right / bottom.
+static bool pyramid_tiles(Plan& plan) {
+    const int L = plan.L;
+    // ORBX_PZ_TILE=WxH overrides the level-0 tile size (tuning; the output is the same)
+    int tw = kPzTW, th = kPzTH;
+    if (const char* e = std::getenv("ORBX_PZ_TILE")) {
+        int a = 0, b = 0;
+        if (std::sscanf(e, "%dx%d", &a, &b) == 2 && a >= 16 && b >= 16) { tw = a; th = b; }
+    }
+    const int nx = (plan.W + tw - 1) / tw, ny = (plan.H + th - 1) / th;
+    plan.pz_nx = nx;
+    plan.pz_ny = ny;
+    plan.pz_tiles = nx * ny;
+    plan.pz_off = (int)plan.rtab.size();
+    plan.rtab.resize(plan.rtab.size() + (size_t)nx * ny * L * 8);
+    // owned boundaries per level: bx[l][0..nx], by[l][0..ny]
+    std::vector<std::vector<int>> bx(L, std::vector<int>(nx + 1)), by(L, std::vector<int>(ny + 1));
+    for (int j = 0; j <= nx; j++) bx[0][j] = (int)(((long long)j * plan.W) / nx);
+    for (int i = 0; i <= ny; i++) by[0][i] = (int)(((long long)i * plan.H) / ny);
+    for (int l = 1; l < L; l++) {
+        const LevelGeom& g = plan.lv[l];
+        const int16_t* xt = plan.rtab.data() + g.xtab_off;
+        const int16_t* yt = plan.rtab.data() + g.ytab_off;
+        for (int j = 0; j <= nx; j++) {
+            int c = j == 0 ? 0 : bx[l][j - 1];
+            while (c < g.w && (j == nx || xt[4 * c] < bx[l - 1][j])) c++;
+            bx[l][j] = c;
+        }
+        for (int i = 0; i <= ny; i++) {
+            int r = i == 0 ? 0 : by[l][i - 1];
+            while (r < g.h && (i == ny || yt[4 * r] < by[l - 1][i])) r++;
+            by[l][i] = r;
+        }
+    }
+    for (int ty = 0; ty < ny; ty++)
+        for (int tx = 0; tx < nx; tx++) {
+            int16_t* R = plan.rtab.data() + plan.pz_off + (size_t)(ty * nx + tx) * L * 8;
+            int nx0 = 0, ny0 = 0, nx1 = 0, ny1 = 0;  // needed rectangle of level l + 1
+            for (int l = L - 1; l >= 0; l--) {
+                const LevelGeom& g = plan.lv[l];
+                const int ox0 = bx[l][tx], ox1 = bx[l][tx + 1], oy0 = by[l][ty], oy1 = by[l][ty + 1];
+                int x0 = ox0, x1 = ox1, y0 = oy0, y1 = oy1;
+                bool any = ox1 > ox0 && oy1 > oy0;
+                if (l + 1 < L && nx1 > nx0 && ny1 > ny0) {
+                    const LevelGeom& u = plan.lv[l + 1];
+                    const int16_t* xt = plan.rtab.data() + u.xtab_off;
+                    const int16_t* yt = plan.rtab.data() + u.ytab_off;
+                    const int sx0 = xt[4 * nx0], sx1 = xt[4 * (nx1 - 1) + 1] + 1;
+                    const int sy0 = yt[4 * ny0], sy1 = yt[4 * (ny1 - 1) + 1] + 1;
+                    if (any) {
+                        x0 = std::min(x0, sx0); x1 = std::max(x1, sx1);
+                        y0 = std::min(y0, sy0); y1 = std::max(y1, sy1);
+                    } else {
+                        x0 = sx0; x1 = sx1; y0 = sy0; y1 = sy1;
+                    }
+                    any = true;
+                }
+                if (!any) x0 = x1 = y0 = y1 = 0;
+                const int16_t r[8] = {(int16_t)x0, (int16_t)y0, (int16_t)x1, (int16_t)y1,
+                                      (int16_t)ox0, (int16_t)oy0, (int16_t)ox1, (int16_t)oy1};
+                std::memcpy(R + 8 * l, r, sizeof(r));
+                // LDS holds the needed columns widened to whole 4-byte quads
+                const int bytes = any ? 4 * ((x1 - (x0 & ~3) + 3) / 4) * (y1 - y0) : 0;
+                int& buf = (l & 1) ? plan.pz_lds_b : plan.pz_lds_a;
+                buf = std::max(buf, (bytes + 15) & ~15);
+                nx0 = x0; nx1 = x1; ny0 = y0; ny1 = y1;
+            }
+        }
+    if (plan.pz_lds_a + plan.pz_lds_b > kPzMaxLds) { plan.why = "pyramid tile exceeds LDS (scale factor too large)"; return false; }
+    return true;
 }
 
 bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
@@ -201,32 +282,17 @@ bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
             g.ytab_off = (int)plan.rtab.size();
             plan.rtab.resize(plan.rtab.size() + 4 * (size_t)g.h);
             resize_tables(prev_w, prev_h, g.w, g.h, plan.rtab.data() + g.xtab_off, plan.rtab.data() + g.ytab_off);
-            // the resize kernel stages each kRzTW x kRzTH output tile's source region
-            // (dword-aligned columns) in LDS; record the largest region
-            const int16_t* xt = plan.rtab.data() + g.xtab_off;
-            const int16_t* yt = plan.rtab.data() + g.ytab_off;
-            for (int x0 = 0; x0 < g.w; x0 += kRzTW) {
-                const int xe = (x0 + kRzTW < g.w ? x0 + kRzTW : g.w) - 1;
-                const int a_lo = xt[4 * x0] & ~3;
-                const int bytes = 4 * (((xt[4 * xe + 1] - a_lo) >> 2) + 1);
-                if (bytes > plan.rz_sw) plan.rz_sw = bytes;
-            }
-            for (int y0 = 0; y0 < g.h; y0 += kRzTH) {
-                const int ye = (y0 + kRzTH < g.h ? y0 + kRzTH : g.h) - 1;
-                const int rows = yt[4 * ye + 1] - yt[4 * y0] + 1;
-                if (rows > plan.rz_sh) plan.rz_sh = rows;
-            }
-            if ((long long)plan.rz_sw * plan.rz_sh > kRzMaxLds) { plan.why = "scale factor too large"; return false; }
         }
         prev_w = g.w;
         prev_h = g.h;
     }
+    if (!pyramid_tiles(plan)) return false;
     plan.pyr_frame_bytes = off;
     plan.slots_per_frame = slot_off;
     plan.keys_per_frame = key_off;
     plan.kept_per_frame = out_off;
     plan.tiles_total = tile_first;
-    if (plan.rtab.empty()) plan.rtab.push_back(0);
+    plan.rtab.resize(plan.rtab.size() + 64, 0);  // k_pyramid reads row taps in batches of 8 rows
     plan.ok = true;
     return true;
 }

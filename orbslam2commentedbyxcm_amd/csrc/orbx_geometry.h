@@ -69,9 +69,14 @@ struct CellGeom {
     int pitch;             // level row pitch
 };
 
-// k_resize output tile and its LDS budget for the staged source region
-constexpr int kRzTW = 256, kRzTH = 32;
-constexpr int kRzMaxLds = 144 * 1024;
+// k_pyramid: one workgroup per (frame, tile) computes every level of its tile.  A
+// tile owns a rectangle of every level (kPzTW x kPzTH at level 0, boundaries carried up
+// the cascade by the resize tables); its "needed" rectangle at level l is what it owns
+// plus the source footprint of its needed rectangle at level l + 1, so levels chain
+// inside LDS with a small recomputed right / bottom halo.  Per (tile, level) the table
+// holds 8 int16: needed x0, y0, x1, y1 and owned x0, y0, x1, y1 (ends exclusive).
+constexpr int kPzTW = 128, kPzTH = 96;
+constexpr int kPzMaxLds = 150 * 1024;
 
 struct Plan {
     int W = 0, H = 0, L = 0;
@@ -84,7 +89,10 @@ struct Plan {
     int keys_per_frame = 0;         // candidate key capacity per frame
     int kept_per_frame = 0;         // sum of ncap
     int tiles_total = 0;            // blur tiles per frame
-    int rz_sw = 0, rz_sh = 0;       // largest staged resize source region (bytes x rows)
+    int pz_tiles = 0;               // k_pyramid tiles per frame (pz_nx x pz_ny)
+    int pz_nx = 0, pz_ny = 0;
+    int pz_off = 0;                 // offset (int16 units) of the tile rectangles in rtab
+    int pz_lds_a = 0, pz_lds_b = 0; // LDS ping / pong buffers (even / odd levels), bytes
     int fc_wr = 0, fc_wc = 0;       // largest FAST detection window (rows, cols)
     int max_ncap = 0;
     int max_key_cap = 0;
