@@ -35,6 +35,7 @@ sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+VALU_PEAK_GIPS = 1024 * 2.4 / 2  # wave64 VALU issue: 1024 SIMDs, 2.4 GHz, 2 cycles each (same guide)
 FX = FY = 500.0
 CX, CY = 320.0, 240.0
 DEPTH = 5.0
@@ -82,11 +83,32 @@ STAGE_KERNELS = {"pyramid": ["orbx::k_pyramid"], "score_blur": ["orbx::k_level_t
                  "describe": ["orbx::k_describe"], "match": ["orbx::k_seq_build", "orbx::k_proj_search<true, true>"]}
 
 
+def newest_profiles(pattern: str):
+    """profiles/ files matching `pattern` (vocabulary runs excluded), oldest first by the
+    numbers in their tags (r01v9 < r01v10)."""
+    import re
+    files = [f for f in (ROOT / "profiles").glob(pattern) if "vocab" not in f.name]
+    return sorted(files, key=lambda f: [int(x) for x in re.findall(r"\d+", f.name)])
+
+
+def pmc_valu(stage: str):
+    """VALU wave-instructions per launch of `stage` from the newest profiles/*_pmc_valu.json
+    (tools/pmc_valu.sh + tools/pmc_valu.py), or (None, None)."""
+    files = newest_profiles("*_pmc_valu.json")
+    if not files:
+        return None, None
+    ks = json.loads(files[-1].read_text())["kernels"]
+    names = STAGE_KERNELS.get(stage, [])
+    if not names or any(k not in ks for k in names):
+        return None, files[-1].name
+    return sum(ks[k]["sq_insts_valu"] for k in names), files[-1].name
+
+
 def pmc_traffic(stage: str):
     """HBM bytes per launch of `stage` from the newest committed PMC summary
     (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate FETCH_SIZE /
     WRITE_SIZE rocprofv3 passes of this bench), or (None, None)."""
-    files = sorted(f for f in (ROOT / "profiles").glob("*_pmc_traffic.json") if "vocab" not in f.name)
+    files = newest_profiles("*_pmc_traffic.json")
     if not files:
         return None, None
     ks = json.loads(files[-1].read_text())["kernels"]
@@ -341,11 +363,21 @@ def main():
     ex.set_timing(False)
     matcher.set_timing(False)
     bytes_pf = stage_bytes(W, H, mean_kps)
-    kernels = {k: v for k, v in stage_ms.items() if k != "total"}
+    # Dominant kernel: the longest stage on the critical path.  Pipelined, the matcher
+    # runs beside the next batch's extraction on its own stream (its event time includes
+    # that contention), so the extraction stages are the critical path.
+    kernels = {k: v for k, v in stage_ms.items() if k != "total" and not (pipeline and k == "match")}
     dom = max(kernels, key=kernels.get)
     Bc = bounds[0][1] - bounds[0][0]  # frames of lane 0, whose events time the stages
     achieved = bytes_pf[dom] * Bc / (stage_ms[dom] * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(dom)
+    valu, valu_src = pmc_valu(dom)
+    issue = None
+    if valu:
+        rate = valu / (stage_ms[dom] * 1e-3) / 1e9
+        issue = {"bound": "valu", "achieved": round(rate, 1), "peak": VALU_PEAK_GIPS, "unit": "G wave-instr/s",
+                 "frac": round(rate / VALU_PEAK_GIPS, 4), "valu_per_launch": valu, "source": valu_src,
+                 "note": "SQ_INSTS_VALU per launch / stage time; peak = 1024 SIMDs x 2.4 GHz / 2 cycles"}
 
     parity = None
     if rank == 0 and args.parity_frames > 0 and match:
@@ -386,7 +418,7 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_unit": "bytes per launch (PMC FETCH_SIZEx2 + WRITE_SIZE)",
                          "traffic_source": traffic_src, "algorithmic_bytes_per_launch": int(bytes_pf[dom] * Bc),
-                         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()}},
+                         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()}, "issue": issue},
             "cpu_baseline": cpu,
             "parity": parity,
             "mean_keypoints_per_frame": round(mean_kps, 1),
