@@ -17,6 +17,7 @@
 #include <type_traits>
 
 #include "orbx_kernels.h"
+#include "orbx_sincos.h"
 
 namespace orbx {
 
@@ -1307,15 +1308,22 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     // steered BRIEF on the blurred level: 16 samples per lane in flight
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float rad = angle * factorPI;
-    const float a = (float)cos((double)rad), b = (float)sin((double)rad);
+    double cd, sd;
+    sincos_0_2pi((double)rad, cd, sd);  // == (float)cos/sin((double)rad) (orbx_sincos.h)
+    const float a = (float)cd, b = (float)sd;
     const uint8_t* center = blur + goff + (size_t)y * pitch + x;
+    // cvRound(v) for |v| < 2^22 is the low bits of v + 1.5 * 2^23 (round to nearest
+    // even, like rint): 0x4B400000 + cvRound(v).  The row offset is one v_mul_u32_u24,
+    // which reads only the low 24 bits (0x400000 + cvRound(y)); kRoundK takes the
+    // constants off again.
+    const uint32_t kRoundK = 0x400000u * (uint32_t)pitch + 0x4B400000u;
     int t0[8], t1[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
         const float x0 = (float)(int8_t)(pat[k] & 0xff), y0 = (float)(int8_t)((pat[k] >> 8) & 0xff);
         const float x1 = (float)(int8_t)((pat[k] >> 16) & 0xff), y1 = (float)(int8_t)(pat[k] >> 24);
-        t0[k] = center[cv_round(x0 * b + y0 * a) * pitch + cv_round(x0 * a - y0 * b)];
-        t1[k] = center[cv_round(x1 * b + y1 * a) * pitch + cv_round(x1 * a - y1 * b)];
+        t0[k] = center[(int)(__umul24(__float_as_uint((x0 * b + y0 * a) + 12582912.0f), (uint32_t)pitch) + __float_as_uint((x0 * a - y0 * b) + 12582912.0f) - kRoundK)];
+        t1[k] = center[(int)(__umul24(__float_as_uint((x1 * b + y1 * a) + 12582912.0f), (uint32_t)pitch) + __float_as_uint((x1 * a - y1 * b) + 12582912.0f) - kRoundK)];
     }
     uint32_t words[8];
 #pragma unroll
