@@ -564,7 +564,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
                                                     int max_wr, int max_wc) {
     // per wave: (max_wr + 2) framed rows of M, then a candidate list of max_wr*max_wc u16
     extern __shared__ __align__(16) uint8_t s_dyn[];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int per_wave = (((max_wr + 2) * kFcStride + 2 * max_wr * max_wc) + 15) & ~15;
     int f, cb;
     xcd_frame_block((ncells + 3) / 4, nframes, f, cb);
@@ -598,16 +598,18 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
         const int half = pairs ? (lane >> 5) : 0;
         const int rstep = pairs ? 2 : 1;
         const bool act = col < wc;
-        // 8 row steps of loads in flight at a time (unconditional loads, clamped addresses)
+        // 8 row steps of loads in flight at a time.  The loads are unconditional: the
+        // window ends >= 19 rows above the level's bottom and rows are >= 64 wide, so up
+        // to 15 rows / 63 columns past it stay inside the frame's block (and the buffer
+        // has slack); the values are masked.  The row part of each offset is wave-uniform
+        // (scalar adds to the base), the lane part a 32-bit vector offset.
+        const uint32_t loff = (uint32_t)(half * c.pitch + col);
         for (int r0 = 0; r0 < wr; r0 += 8 * rstep) {
             int v[8];
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const int r = r0 + k * rstep + half;
-                const bool ok = act && r < wr;
-                v[k] = src[ok ? (size_t)r * c.pitch + col : 0];
-                v[k] = ok ? v[k] : 0;
-            }
+            for (int k = 0; k < 8; k++) v[k] = src[(uint32_t)((r0 + k * rstep) * c.pitch) + loff];
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[k] = (act && r0 + k * rstep + half < wr) ? v[k] : 0;
 #pragma unroll
             for (int k = 0; k < 8; k++) {
                 const int rb = r0 + k * rstep;  // first row of this step (wave-uniform)
@@ -1236,7 +1238,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
                                                   const int* __restrict__ kept_count,
                                                   orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                   int cap, int* __restrict__ n_out, int nframes) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int half = lane >> 5, hl = lane & 31;
     int f, sb;
     xcd_frame_block((kept_pf + 7) / 8, nframes, f, sb);
