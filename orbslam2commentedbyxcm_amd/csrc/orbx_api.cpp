@@ -107,8 +107,9 @@ int prepare(orbx_extractor* ex, int W, int H, int batch) {
     HIP_TRY(dalloc(&db.lv, kMaxLevels));
     HIP_TRY(dalloc(&db.cells, p.cells.size()));
     HIP_TRY(dalloc(&db.rtab, p.rtab.size()));
-    HIP_TRY(dalloc(&db.pyr, B * (size_t)p.pyr_frame_bytes));
-    HIP_TRY(dalloc(&db.blur, B * (size_t)p.pyr_frame_bytes));
+    // slack: k_describe's dword patch loads may reach a few bytes past a level's last row
+    HIP_TRY(dalloc(&db.pyr, B * (size_t)p.pyr_frame_bytes + 65536));
+    HIP_TRY(dalloc(&db.blur, B * (size_t)p.pyr_frame_bytes + 65536));
     HIP_TRY(dalloc(&db.score, B * (size_t)p.pyr_frame_bytes + 65536));  // k_fast_cells reads past windows
     HIP_TRY(dalloc(&db.slots, B * (size_t)p.slots_per_frame));
     HIP_TRY(dalloc(&db.cell_count, B * p.cells.size()));

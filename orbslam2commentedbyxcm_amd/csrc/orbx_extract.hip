@@ -25,6 +25,11 @@ const char* const kStageNames[kStages] = {"pyramid", "score_blur", "fast_cells",
 
 __constant__ __align__(16) int8_t c_pattern[1024];
 __constant__ int c_umax[16];
+// IC_Angle by rows: for a patch row v and the patch's start alignment d0 = (x-15) & 3,
+// c_icm[d0][|v|] holds 9 dwords of byte masks (1 where |u| <= umax[|v|]) and c_icw the
+// same bytes weighted by u + 15, laid over the 36 bytes staged from (x-15) & ~3.
+__constant__ __align__(16) uint32_t c_icm[4][16][12];
+__constant__ __align__(16) uint32_t c_icw[4][16][12];
 
 static const int8_t kPatternHost[1024] = {
 #include "orb_pattern.inc"
@@ -32,6 +37,20 @@ static const int8_t kPatternHost[1024] = {
 
 hipError_t upload_constants(const OrbParams& prm) {
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), kPatternHost, sizeof(kPatternHost));
+    if (e != hipSuccess) return e;
+    uint32_t icm[4][16][12] = {}, icw[4][16][12] = {};
+    for (int d0 = 0; d0 < 4; d0++)
+        for (int av = 0; av < 16; av++)
+            for (int u = -15; u <= 15; u++) {
+                const int au = u < 0 ? -u : u;
+                if (av != 0 && au > prm.umax[av]) continue;  // IC_Angle's circular patch, cc:70-102
+                const int byte = d0 + u + 15;
+                icm[d0][av][byte >> 2] |= 1u << (8 * (byte & 3));
+                icw[d0][av][byte >> 2] |= (uint32_t)(u + 15) << (8 * (byte & 3));
+            }
+    e = hipMemcpyToSymbol(HIP_SYMBOL(c_icm), icm, sizeof(icm));
+    if (e != hipSuccess) return e;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(c_icw), icw, sizeof(icw));
     if (e != hipSuccess) return e;
     return hipMemcpyToSymbol(HIP_SYMBOL(c_umax), prm.umax, sizeof(prm.umax));
 }
@@ -1224,13 +1243,12 @@ __device__ float fast_atan2(float y, float x) {
     return a;
 }
 
-__device__ __forceinline__ int cv_round(float v) { return (int)rintf(v); }
-
 // Two kept keypoint slots per wave (one per 32-lane half): IC_Angle on the level
 // (cc:59-106), rBRIEF on the blurred level (cc:118-172), coordinate scaling
 // (cc:1613-1622), output in the reference's level-major order.  Halving the waves halves
-// the per-keypoint cost of everything evaluated once per wave (fastAtan2, the double
-// cos/sin, addressing) while each lane keeps 31 + 16 independent loads in flight.
+// the per-keypoint cost of everything evaluated once per wave (fastAtan2, the sincos,
+// addressing); a lane's global loads (its IC row, its BRIEF patch rows) are issued
+// together, and the BRIEF gathers then read the LDS-staged patch.
 __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ pyr,
                                                   const uint8_t* __restrict__ blur, long long fb,
                                                   const LevelGeom* __restrict__ lv, int L,
@@ -1238,6 +1256,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
                                                   const int* __restrict__ kept_count,
                                                   orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                   int cap, int* __restrict__ n_out, int nframes) {
+    __shared__ __align__(16) uint32_t s_bpatch[8][37 * 12];  // BRIEF patches, 48-byte rows
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int half = lane >> 5, hl = lane & 31;
     int f, sb;
@@ -1266,40 +1285,64 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     const int x = valid ? key_x(key) + kMinBorder : g.w / 2;
     const int y = valid ? key_y(key) + kMinBorder : g.h / 2;
     const int resp = key_resp(key);
-    const size_t goff = (size_t)f * fb + g.off;
     const int pitch = g.pitch;
-    // pattern pairs hl, 32+hl, ..., 224+hl (x0, y0, x1, y1 as int8), issued up front
-    int pat[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        pat[k] = ((const int*)c_pattern)[k * 32 + hl];
-        asm volatile("" : "+v"(pat[k]));
-    }
     float lv_scale = g.scale, lv_size = g.kp_size;
     asm volatile("" : "+v"(lv_scale), "+v"(lv_size));
-
-    // IC angle: lane hl (u = hl - 15, hl < 31) sums its column over rows v = -15..15 with
-    // the circular mask |u| <= umax[|v|]; all 31 loads are issued before any is consumed.
-    int m10 = 0, m01 = 0;
+    // IC_Angle (cc:59-106) by rows: lane hl < 31 loads patch row v = hl - 15 of the level,
+    // 36 bytes from (x-15) & ~3, and two v_dot4_u32_u8 per dword against the circular
+    // mask and the (u + 15)-weighted mask give sum(I) and sum((u+15) I) over the row:
+    // m10 += sum((u+15) I) - 15 sum(I), m01 += v sum(I).  The steered-BRIEF patch of the
+    // blurred level, rows y-18..y+18 (|rotated pattern point| <= 13*sqrt(2) < 18.5), 44
+    // bytes from (x-18) & ~3, is staged in LDS (48-byte rows, lanes 0..31 rows 0..31,
+    // lanes 0..4 rows 32..36); all loads are issued together, one round of latency.
+    // Keypoints lie in [19, w-20] x [19, h-20] of their level, so every row exists; a
+    // row's last dword may reach 6 bytes past the level width (inside the pitch, or the
+    // buffers' slack for the very last row).
+    const int kp = wave * 2 + half;
+    uint8_t* const bp = (uint8_t*)s_bpatch[kp];
+    const int xs = (x - 15) & ~3, xb = (x - 18) & ~3;
+    int m10, m01;
     {
-        const int u = hl - 15;
-        const int au = u < 0 ? -u : u;
-        const bool col_ok = hl < 31;
-        const uint8_t* ctr = pyr + goff + (size_t)y * pitch + x + (col_ok ? u : 0);
-        int px[31];
-#pragma unroll
-        for (int k = 0; k < 31; k++) px[k] = ctr[(long)(k - 15) * pitch];
-        if (col_ok) {
-#pragma unroll
-            for (int k = 0; k < 31; k++) {
-                const int v = k - 15;
-                const int av = v < 0 ? -v : v;
-                if (v != 0 && au > c_umax[av]) continue;
-                m10 += u * px[k];
-                m01 += v * px[k];
-            }
+        const uint8_t* pframe = pyr + (size_t)f * fb;   // wave-uniform bases,
+        const uint8_t* bframe = blur + (size_t)f * fb;  // 32-bit offsets
+        const int v = min(hl, 30) - 15;
+        const int av = v < 0 ? -v : v;
+        const int d0 = (x - 15) & 3;
+        const uint8_t* prow = pframe + (uint32_t)(g.off + (long long)(y + v) * pitch + xs);
+        const uint4 p0 = *(const uint4*)prow, p1 = *(const uint4*)(prow + 16);
+        const uint32_t p2 = *(const uint32_t*)(prow + 32);
+        const uint8_t* brow0 = bframe + (uint32_t)(g.off + (long long)(y - 18 + hl) * pitch + xb);
+        const uint8_t* brow1 = bframe + (uint32_t)(g.off + (long long)(y + 14 + min(hl, 4)) * pitch + xb);
+        const uint4 b00 = *(const uint4*)brow0, b01 = *(const uint4*)(brow0 + 16), b02 = *(const uint4*)(brow0 + 32);
+        const uint4 b10 = *(const uint4*)brow1, b11 = *(const uint4*)(brow1 + 16), b12 = *(const uint4*)(brow1 + 32);
+        const uint4* cm = (const uint4*)c_icm[d0][av];
+        const uint4* cw = (const uint4*)c_icw[d0][av];
+        const uint4 m0 = cm[0], m1 = cm[1], m2 = cm[2], w0 = cw[0], w1 = cw[1], w2 = cw[2];
+        uint32_t cs = 0, ws = 0;
+        cs = __builtin_amdgcn_udot4(p0.x, m0.x, cs, false); ws = __builtin_amdgcn_udot4(p0.x, w0.x, ws, false);
+        cs = __builtin_amdgcn_udot4(p0.y, m0.y, cs, false); ws = __builtin_amdgcn_udot4(p0.y, w0.y, ws, false);
+        cs = __builtin_amdgcn_udot4(p0.z, m0.z, cs, false); ws = __builtin_amdgcn_udot4(p0.z, w0.z, ws, false);
+        cs = __builtin_amdgcn_udot4(p0.w, m0.w, cs, false); ws = __builtin_amdgcn_udot4(p0.w, w0.w, ws, false);
+        cs = __builtin_amdgcn_udot4(p1.x, m1.x, cs, false); ws = __builtin_amdgcn_udot4(p1.x, w1.x, ws, false);
+        cs = __builtin_amdgcn_udot4(p1.y, m1.y, cs, false); ws = __builtin_amdgcn_udot4(p1.y, w1.y, ws, false);
+        cs = __builtin_amdgcn_udot4(p1.z, m1.z, cs, false); ws = __builtin_amdgcn_udot4(p1.z, w1.z, ws, false);
+        cs = __builtin_amdgcn_udot4(p1.w, m1.w, cs, false); ws = __builtin_amdgcn_udot4(p1.w, w1.w, ws, false);
+        cs = __builtin_amdgcn_udot4(p2, m2.x, cs, false); ws = __builtin_amdgcn_udot4(p2, w2.x, ws, false);
+        const bool row_ok = hl < 31;
+        m10 = row_ok ? (int)ws - 15 * (int)cs : 0;
+        m01 = row_ok ? v * (int)cs : 0;
+        uint4* bd = (uint4*)(bp + hl * 48);
+        bd[0] = b00;
+        bd[1] = b01;
+        bd[2] = b02;
+        if (hl < 5) {
+            uint4* bd1 = (uint4*)(bp + (32 + hl) * 48);
+            bd1[0] = b10;
+            bd1[1] = b11;
+            bd1[2] = b12;
         }
     }
+    wave_lds_fence();
 #pragma unroll
     for (int o2 = 16; o2 > 0; o2 >>= 1) {  // within the 32-lane half
         m10 += __shfl_xor(m10, o2);
@@ -1307,25 +1350,32 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     }
     const float angle = fast_atan2((float)m01, (float)m10);
 
-    // steered BRIEF on the blurred level: 16 samples per lane in flight
+    // steered BRIEF on the staged blurred patch: pairs hl, 32 + hl, ..., 224 + hl
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float rad = angle * factorPI;
     double cd, sd;
     sincos_0_2pi((double)rad, cd, sd);  // == (float)cos/sin((double)rad) (orbx_sincos.h)
     const float a = (float)cd, b = (float)sd;
-    const uint8_t* center = blur + goff + (size_t)y * pitch + x;
     // cvRound(v) for |v| < 2^22 is the low bits of v + 1.5 * 2^23 (round to nearest
     // even, like rint): 0x4B400000 + cvRound(v).  The row offset is one v_mul_u32_u24,
-    // which reads only the low 24 bits (0x400000 + cvRound(y)); kRoundK takes the
-    // constants off again.
-    const uint32_t kRoundK = 0x400000u * (uint32_t)pitch + 0x4B400000u;
+    // which reads only the low 24 bits (0x400000 + cvRound(y)); the constants come off
+    // the patch centre once.
+    const uint32_t center = (uint32_t)(18 * 48 + 18 + (x - 18 - xb)) - (0x400000u * 48u + 0x4B400000u);
+    const float kRound = 12582912.0f;  // 1.5 * 2^23
+    auto sample = [&](float px, float py) -> int {
+        const uint32_t ry = __float_as_uint((px * b + py * a) + kRound);
+        const uint32_t rx = __float_as_uint((px * a - py * b) + kRound);
+        return bp[center + __umul24(ry, 48u) + rx];
+    };
+    const int* pat = (const int*)c_pattern + hl;
     int t0[8], t1[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        const float x0 = (float)(int8_t)(pat[k] & 0xff), y0 = (float)(int8_t)((pat[k] >> 8) & 0xff);
-        const float x1 = (float)(int8_t)((pat[k] >> 16) & 0xff), y1 = (float)(int8_t)(pat[k] >> 24);
-        t0[k] = center[(int)(__umul24(__float_as_uint((x0 * b + y0 * a) + 12582912.0f), (uint32_t)pitch) + __float_as_uint((x0 * a - y0 * b) + 12582912.0f) - kRoundK)];
-        t1[k] = center[(int)(__umul24(__float_as_uint((x1 * b + y1 * a) + 12582912.0f), (uint32_t)pitch) + __float_as_uint((x1 * a - y1 * b) + 12582912.0f) - kRoundK)];
+        const int q = pat[32 * k];
+        const float x0 = (float)(int8_t)(q & 0xff), y0 = (float)(int8_t)((q >> 8) & 0xff);
+        const float x1 = (float)(int8_t)((q >> 16) & 0xff), y1 = (float)(int8_t)(q >> 24);
+        t0[k] = sample(x0, y0);
+        t1[k] = sample(x1, y1);
     }
     uint32_t words[8];
 #pragma unroll
