@@ -324,7 +324,8 @@ __device__ __forceinline__ int reflect101(int i, int n) {
     return i >= n ? 2 * n - 2 - i : i;
 }
 
-constexpr int kTW = 64, kTH = 32;  // level tile (outputs) of k_level_tiles
+constexpr int kTW = kLtTW, kTH = kLtTH;  // level tile (outputs) of k_level_tiles
+static_assert(kTW == 64 && kTH % 16 == 0, "k_level_tiles maps 16 column quads x kTH rows");
 constexpr int kSW = kTW + 8;       // staged row: image columns X0-4 .. X0+67
 
 typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
@@ -351,7 +352,7 @@ __device__ __forceinline__ void blur_row4(uint32_t lo, uint32_t mid, uint32_t hi
 __device__ __forceinline__ uint32_t lo_pair(uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c010c00u); }
 __device__ __forceinline__ uint32_t hi_pair(uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c030c02u); }
 
-// One 64x32 tile of one pyramid level per workgroup, all levels and frames in one
+// One 64x48 tile of one pyramid level per workgroup, all levels and frames in one
 // launch (XCD-aware frame placement).  The tile plus a 3-pixel REFLECT_101 margin is
 // staged in LDS once and feeds both per-pixel products of the level:
 //  * GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of the level ROI clone
@@ -419,8 +420,8 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
             if (i < kN) ((uint32_t*)s_in)[i] = v[k];
         }
         __syncthreads();
-        if (tid < (kTH + 6) * 6) {
-            const int r = tid / 6, k = tid - 6 * r;
+        for (int i = tid; i < (kTH + 6) * 6; i += 256) {
+            const int r = i / 6, k = i - 6 * r;
             const int col = k < 3 ? -1 - k : g.w + k - 3;  // REFLECT_101 source: -col or 2w - 2 - col
             const int sc = col - X0 + 4, ss = (k < 3 ? -col : 2 * g.w - 2 - col) - X0 + 4;
             if (sc >= 0 && sc < kSW) s_in[r][sc] = s_in[r][ss];
@@ -441,8 +442,8 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
                                                   a[3] | (b[3] << 16));
     }
     // ---- FAST compass test on the detection area, compaction of the survivors.
-    // A thread always owns columns 4j..4j+3 (j = tid & 15) of rows tid/16 and
-    // tid/16 + 16, so its detection-area column mask is computed once.
+    // A thread always owns columns 4j..4j+3 (j = tid & 15) of rows tid/16 + 16 i, so
+    // its detection-area column mask is computed once.
     {
         const int j = tid & 15, c0 = 4 + 4 * j, x0 = X0 + 4 * j;
         unsigned colmask = 0;
@@ -450,7 +451,7 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
         for (int k = 0; k < 4; k++) colmask |= (x0 + k >= kEdge && x0 + k < g.w - kEdge) ? 1u << k : 0u;
         const short2_t tq1 = {(short)(tq + 1), (short)(tq + 1)};
 #pragma unroll
-        for (int it = 0; it < 2; it++) {
+        for (int it = 0; it < kTH / 16; it++) {
             const int r = (tid >> 4) + 16 * it;
             const int y = Y0 + r;
             unsigned pass = 0;

@@ -269,9 +269,9 @@ bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
         out_off += ncap;
         if (ncap > plan.max_ncap) plan.max_ncap = ncap;
 
-        // score/blur tiles (64 x 32 outputs)
-        g.tiles_x = (g.w + 63) / 64;
-        g.tiles_y = (g.h + 31) / 32;
+        // score/blur tiles (kLtTW x kLtTH outputs)
+        g.tiles_x = (g.w + kLtTW - 1) / kLtTW;
+        g.tiles_y = (g.h + kLtTH - 1) / kLtTH;
         g.tile_first = tile_first;
         tile_first += g.tiles_x * g.tiles_y;
 
