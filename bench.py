@@ -186,6 +186,17 @@ def check_parity(frames_np, T, kps_all, desc_all, n_host, mp_all, nm_all, nframe
 
 
 def main():
+    # Secondary measurements (their implementations live under tests/: they run the
+    # oracle as parity check and CPU baseline): the DBoW2 transform and the per-row table.
+    if "--vocab" in sys.argv[1:] or "--rows" in sys.argv[1:]:
+        sys.path.insert(0, str(ROOT / "tests"))
+        mode = "--vocab" if "--vocab" in sys.argv[1:] else "--rows"
+        rest = [a for a in sys.argv[1:] if a != mode]
+        if mode == "--vocab":
+            import vocab_bench
+            return vocab_bench.main(rest)
+        import row_bench
+        return row_bench.main(rest)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)

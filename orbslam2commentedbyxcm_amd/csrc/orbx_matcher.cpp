@@ -45,13 +45,17 @@ constexpr int TH_LOW = 50;    // ORBmatcher.cc:39
 // Grow-only device arena, reset per call.
 struct Arena {
     char* base = nullptr;
-    size_t cap = 0, used = 0;
+    char* host = nullptr;  // pinned mirror: a call's inputs are staged here and uploaded in one copy
+    size_t cap = 0, used = 0, dirty = 0;
     hipError_t reserve(size_t bytes) {
+        dirty = 0;
         if (bytes <= cap) return hipSuccess;
         if (base) (void)hipFree(base);
-        base = nullptr;
+        if (host) (void)hipHostFree(host);
+        base = host = nullptr;
         cap = 0;
         hipError_t e = hipMalloc((void**)&base, bytes);
+        if (e == hipSuccess) e = hipHostMalloc((void**)&host, bytes, hipHostMallocDefault);
         if (e == hipSuccess) cap = bytes;
         return e;
     }
@@ -61,6 +65,47 @@ struct Arena {
         T* p = (T*)(base + used);
         used += sizeof(T) * (n ? n : 1);
         return p;
+    }
+    // stage `bytes` of host data for device address d (inside the arena)
+    void up(void* d, const void* h, size_t bytes) {
+        const size_t o = (size_t)((char*)d - base);
+        std::memcpy(host + o, h, bytes);
+        if (o + bytes > dirty) dirty = o + bytes;
+    }
+    // fill `bytes` at device address d with byte v, staged like up() (a device memset
+    // before flush() would be overwritten by the prefix copy)
+    void fill(void* d, int v, size_t bytes) {
+        const size_t o = (size_t)((char*)d - base);
+        std::memset(host + o, v, bytes);
+        if (o + bytes > dirty) dirty = o + bytes;
+    }
+    // one H2D copy of everything staged since the last flush (the prefix [0, dirty))
+    hipError_t flush(hipStream_t s) {
+        if (!dirty) return hipSuccess;
+        const hipError_t e = hipMemcpyAsync(base, host, dirty, hipMemcpyHostToDevice, s);
+        dirty = 0;
+        return e;
+    }
+    // D2H of `bytes` at device address d into the pinned mirror; sync() copies it to h
+    struct Pending { void* h; size_t o, bytes; };
+    std::vector<Pending> pending;
+    hipError_t down(void* h, const void* d, size_t bytes, hipStream_t s) {
+        const size_t o = (size_t)((const char*)d - base);
+        pending.push_back({h, o, bytes});
+        return hipMemcpyAsync(host + o, d, bytes, hipMemcpyDeviceToHost, s);
+    }
+    hipError_t sync(hipStream_t s) {
+        const hipError_t e = hipStreamSynchronize(s);
+        if (e == hipSuccess)
+            for (const Pending& p : pending) std::memcpy(p.h, host + p.o, p.bytes);
+        pending.clear();
+        return e;
+    }
+    void release() {
+        if (base) (void)hipFree(base);
+        if (host) (void)hipHostFree(host);
+        base = host = nullptr;
+        cap = used = dirty = 0;
     }
 };
 
@@ -143,14 +188,14 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
     auto* d_off = m->arena.take<long long>(1);
     auto* d_nm = m->arena.take<int32_t>(1);
     hipStream_t s = m->stream;
-    HIP_TRY(hipMemcpyAsync(d_keys, f->keys, sizeof(orbx_keypoint) * n, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_desc, f->desc, (size_t)n * 32, hipMemcpyHostToDevice, s));
-    if (f->u_right) HIP_TRY(hipMemcpyAsync(d_ur, f->u_right, sizeof(float) * n, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_fmp, frame_mp, sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_q, qs.data(), sizeof(ProjQuery) * nq, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_qd, qdesc.data(), (size_t)nq * 32, hipMemcpyHostToDevice, s));
+    m->arena.up(d_keys, f->keys, sizeof(orbx_keypoint) * n);
+    m->arena.up(d_desc, f->desc, (size_t)n * 32);
+    if (f->u_right) m->arena.up(d_ur, f->u_right, sizeof(float) * n);
+    m->arena.up(d_fmp, frame_mp, sizeof(int32_t) * n);
+    m->arena.up(d_q, qs.data(), sizeof(ProjQuery) * nq);
+    m->arena.up(d_qd, qdesc.data(), (size_t)nq * 32);
     if (nobs && mps->observations)
-        HIP_TRY(hipMemcpyAsync(d_obs, mps->observations, sizeof(int32_t) * nobs, hipMemcpyHostToDevice, s));
+        m->arena.up(d_obs, mps->observations, sizeof(int32_t) * nobs);
     ProjProblem pb{};
     pb.keys = d_keys;
     pb.desc = d_desc;
@@ -166,15 +211,16 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
     pb.inv_h = (float)kGridRows / (f->max_y - f->min_y);
     pb.nmatches = d_nm;
     const long long zero = 0;
-    HIP_TRY(hipMemcpyAsync(d_prob, &pb, sizeof(pb), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_off, &zero, sizeof(zero), hipMemcpyHostToDevice, s));
+    m->arena.up(d_prob, &pb, sizeof(pb));
+    m->arena.up(d_off, &zero, sizeof(zero));
     ProjParams P = base_params;
     P.mp_obs = d_obs;
+    HIP_TRY(m->arena.flush(s));
     HIP_TRY(launch_proj_search(d_prob, 1, P, d_scr, d_off, n, nq, s));
     int nm = 0;
-    HIP_TRY(hipMemcpyAsync(frame_mp, d_fmp, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(&nm, d_nm, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(m->arena.down(frame_mp, d_fmp, sizeof(int32_t) * n, s));
+    HIP_TRY(m->arena.down(&nm, d_nm, sizeof(int32_t), s));
+    HIP_TRY(m->arena.sync(s));
     if (nmatches) *nmatches = nm;
     return ORBX_OK;
 }
@@ -206,7 +252,7 @@ void orbx_matcher_destroy(orbx_matcher* m) {
     if (!m) return;
     (void)hipSetDevice(m->device);
     if (m->stream) (void)hipStreamSynchronize(m->stream);
-    if (m->arena.base) (void)hipFree(m->arena.base);
+    m->arena.release();
     for (auto& slot : m->ev)
         for (auto& e : slot)
             if (e) (void)hipEventDestroy(e);
@@ -639,17 +685,17 @@ int orbx_search_for_triangulation(orbx_matcher* m, const orbx_frame_view* kf1, c
     auto* d_prob = m->arena.take<TriProblem>(1);
     auto* d_scr = m->arena.take<unsigned long long>(nq);
     hipStream_t s = m->stream;
-    HIP_TRY(hipMemcpyAsync(d_k1, kf1->keys, sizeof(orbx_keypoint) * n1, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_d1, kf1->desc, (size_t)n1 * 32, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_k2, kf2->keys, sizeof(orbx_keypoint) * n2, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_d2, kf2->desc, (size_t)n2 * 32, hipMemcpyHostToDevice, s));
-    if (kf2->u_right) HIP_TRY(hipMemcpyAsync(d_ur2, kf2->u_right, sizeof(float) * n2, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_mp2, kf2_has_mp, n2, hipMemcpyHostToDevice, s));
-    if (nfv2) HIP_TRY(hipMemcpyAsync(d_fv2, fv2_idx, sizeof(int32_t) * nfv2, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_sc2, kf2->scale_factors, sizeof(float) * kf2->nlevels, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_sg2, kf2->level_sigma2, sizeof(float) * kf2->nlevels, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_q, qs.data(), sizeof(TriQuery) * nq, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(d_m12, 0xff, sizeof(int32_t) * n1, s));
+    m->arena.up(d_k1, kf1->keys, sizeof(orbx_keypoint) * n1);
+    m->arena.up(d_d1, kf1->desc, (size_t)n1 * 32);
+    m->arena.up(d_k2, kf2->keys, sizeof(orbx_keypoint) * n2);
+    m->arena.up(d_d2, kf2->desc, (size_t)n2 * 32);
+    if (kf2->u_right) m->arena.up(d_ur2, kf2->u_right, sizeof(float) * n2);
+    m->arena.up(d_mp2, kf2_has_mp, n2);
+    if (nfv2) m->arena.up(d_fv2, fv2_idx, sizeof(int32_t) * nfv2);
+    m->arena.up(d_sc2, kf2->scale_factors, sizeof(float) * kf2->nlevels);
+    m->arena.up(d_sg2, kf2->level_sigma2, sizeof(float) * kf2->nlevels);
+    m->arena.up(d_q, qs.data(), sizeof(TriQuery) * nq);
+    m->arena.fill(d_m12, 0xff, sizeof(int32_t) * n1);
     TriProblem pb{};
     pb.keys1 = d_k1;
     pb.desc1 = d_d1;
@@ -670,11 +716,12 @@ int orbx_search_for_triangulation(orbx_matcher* m, const orbx_frame_view* kf1, c
     pb.nq = nq;
     pb.matches12 = d_m12;
     pb.scratch_off = 0;
-    HIP_TRY(hipMemcpyAsync(d_prob, &pb, sizeof(pb), hipMemcpyHostToDevice, s));
+    m->arena.up(d_prob, &pb, sizeof(pb));
+    HIP_TRY(m->arena.flush(s));
     HIP_TRY(launch_triangulation(d_prob, 1, d_scr, n2, nq, s));
     std::vector<int32_t> m12((size_t)n1);
-    HIP_TRY(hipMemcpyAsync(m12.data(), d_m12, sizeof(int32_t) * n1, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(m->arena.down(m12.data(), d_m12, sizeof(int32_t) * n1, s));
+    HIP_TRY(m->arena.sync(s));
     int np = 0;
     for (int i = 0; i < n1; i++) {  // vMatchedPairs in idx1 order (cc:1045-1053)
         if (m12[(size_t)i] < 0) continue;
@@ -761,20 +808,20 @@ int run_bow(orbx_matcher* m, const orbx_frame_view* v1, const int32_t* mp1, cons
     auto* d_out = m->arena.take<int32_t>(nout);
     auto* d_prob = m->arena.take<BowProblem>(1);
     hipStream_t s = m->stream;
-    HIP_TRY(hipMemcpyAsync(d_k1, v1->keys, sizeof(orbx_keypoint) * n1, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_d1, v1->desc, (size_t)n1 * 32, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_k2, v2->keys, sizeof(orbx_keypoint) * n2, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_d2, v2->desc, (size_t)n2 * 32, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_q, qidx.data(), sizeof(int32_t) * nq, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_fv2, fv2_idx, sizeof(int32_t) * nfv2, hipMemcpyHostToDevice, s));
+    m->arena.up(d_k1, v1->keys, sizeof(orbx_keypoint) * n1);
+    m->arena.up(d_d1, v1->desc, (size_t)n1 * 32);
+    m->arena.up(d_k2, v2->keys, sizeof(orbx_keypoint) * n2);
+    m->arena.up(d_d2, v2->desc, (size_t)n2 * 32);
+    m->arena.up(d_q, qidx.data(), sizeof(int32_t) * nq);
+    m->arena.up(d_fv2, fv2_idx, sizeof(int32_t) * nfv2);
     if (kf_kf) {
-        HIP_TRY(hipMemcpyAsync(d_av, avail.data(), n2, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(d_mp2, mp2, sizeof(int32_t) * n2, hipMemcpyHostToDevice, s));
+        m->arena.up(d_av, avail.data(), n2);
+        m->arena.up(d_mp2, mp2, sizeof(int32_t) * n2);
     } else {
-        HIP_TRY(hipMemcpyAsync(d_mp1, mp1, sizeof(int32_t) * n1, hipMemcpyHostToDevice, s));
+        m->arena.up(d_mp1, mp1, sizeof(int32_t) * n1);
     }
-    HIP_TRY(hipMemcpyAsync(d_nodes, nodes.data(), sizeof(BowNode) * nn, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(d_out, 0xff, sizeof(int32_t) * nout, s));
+    m->arena.up(d_nodes, nodes.data(), sizeof(BowNode) * nn);
+    m->arena.fill(d_out, 0xff, sizeof(int32_t) * nout);
     BowProblem pb{};
     pb.desc1 = d_d1;
     pb.keys1 = d_k1;
@@ -793,10 +840,11 @@ int run_bow(orbx_matcher* m, const orbx_frame_view* v1, const int32_t* mp1, cons
     pb.nnratio = m->nnratio;
     pb.check_ori = m->check_ori;
     pb.matches = d_out;
-    HIP_TRY(hipMemcpyAsync(d_prob, &pb, sizeof(pb), hipMemcpyHostToDevice, s));
+    m->arena.up(d_prob, &pb, sizeof(pb));
+    HIP_TRY(m->arena.flush(s));
     HIP_TRY(launch_bow(d_prob, n2, nout, s));
-    HIP_TRY(hipMemcpyAsync(matches, d_out, sizeof(int32_t) * nout, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(m->arena.down(matches, d_out, sizeof(int32_t) * nout, s));
+    HIP_TRY(m->arena.sync(s));
     int nm = 0;
     for (int i = 0; i < nout; i++) nm += matches[i] >= 0;
     *nmatches = nm;
@@ -882,14 +930,14 @@ int orbx_search_for_initialization(orbx_matcher* m, const orbx_frame_view* f1, c
     auto* d_tr = m->arena.take<int>(nq);
     auto* d_prob = m->arena.take<InitProblem>(1);
     hipStream_t s = m->stream;
-    HIP_TRY(hipMemcpyAsync(d_k1, f1->keys, sizeof(orbx_keypoint) * n1, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_d1, f1->desc, (size_t)n1 * 32, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_k2, f2->keys, sizeof(orbx_keypoint) * n2, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_d2, f2->desc, (size_t)n2 * 32, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_cs, cstart.data(), sizeof(int32_t) * cstart.size(), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_ci, cidx.data(), sizeof(int32_t) * cidx.size(), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_q, qidx.data(), sizeof(int32_t) * nq, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_prev, prev_matched, sizeof(float) * 2 * n1, hipMemcpyHostToDevice, s));
+    m->arena.up(d_k1, f1->keys, sizeof(orbx_keypoint) * n1);
+    m->arena.up(d_d1, f1->desc, (size_t)n1 * 32);
+    m->arena.up(d_k2, f2->keys, sizeof(orbx_keypoint) * n2);
+    m->arena.up(d_d2, f2->desc, (size_t)n2 * 32);
+    m->arena.up(d_cs, cstart.data(), sizeof(int32_t) * cstart.size());
+    m->arena.up(d_ci, cidx.data(), sizeof(int32_t) * cidx.size());
+    m->arena.up(d_q, qidx.data(), sizeof(int32_t) * nq);
+    m->arena.up(d_prev, prev_matched, sizeof(float) * 2 * n1);
     InitProblem pb{};
     pb.keys1 = d_k1;
     pb.desc1 = d_d1;
@@ -912,10 +960,11 @@ int orbx_search_for_initialization(orbx_matcher* m, const orbx_frame_view* f1, c
     pb.matches12 = d_m12;
     pb.lists = d_lists;
     pb.trunc = d_tr;
-    HIP_TRY(hipMemcpyAsync(d_prob, &pb, sizeof(pb), hipMemcpyHostToDevice, s));
+    m->arena.up(d_prob, &pb, sizeof(pb));
+    HIP_TRY(m->arena.flush(s));
     HIP_TRY(launch_init(d_prob, n1, n2, nq, s));
-    HIP_TRY(hipMemcpyAsync(matches12, d_m12, sizeof(int32_t) * n1, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(m->arena.down(matches12, d_m12, sizeof(int32_t) * n1, s));
+    HIP_TRY(m->arena.sync(s));
     int nm = 0;
     for (int i = 0; i < n1; i++) {
         const int j = matches12[i];
@@ -979,13 +1028,13 @@ int run_best(orbx_matcher* m, const orbx_frame_view* f, const std::vector<BestQu
     auto* d_best = m->arena.take<int32_t>(nq);
     auto* d_prob = m->arena.take<BestProblem>(1);
     hipStream_t s = m->stream;
-    HIP_TRY(hipMemcpyAsync(d_k, f->keys, sizeof(orbx_keypoint) * n, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_d, f->desc, (size_t)n * 32, hipMemcpyHostToDevice, s));
-    if (gate && f->u_right) HIP_TRY(hipMemcpyAsync(d_ur, f->u_right, sizeof(float) * n, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_cs, cstart.data(), sizeof(int32_t) * cstart.size(), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_ci, cidx.data(), sizeof(int32_t) * cidx.size(), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_q, qs.data(), sizeof(BestQuery) * nq, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_qd, qd.data(), (size_t)nq * 32, hipMemcpyHostToDevice, s));
+    m->arena.up(d_k, f->keys, sizeof(orbx_keypoint) * n);
+    m->arena.up(d_d, f->desc, (size_t)n * 32);
+    if (gate && f->u_right) m->arena.up(d_ur, f->u_right, sizeof(float) * n);
+    m->arena.up(d_cs, cstart.data(), sizeof(int32_t) * cstart.size());
+    m->arena.up(d_ci, cidx.data(), sizeof(int32_t) * cidx.size());
+    m->arena.up(d_q, qs.data(), sizeof(BestQuery) * nq);
+    m->arena.up(d_qd, qd.data(), (size_t)nq * 32);
     BestProblem pb{};
     pb.keys = d_k;
     pb.desc = d_d;
@@ -1003,10 +1052,11 @@ int run_best(orbx_matcher* m, const orbx_frame_view* f, const std::vector<BestQu
     pb.gate = gate;
     pb.accept = accept;
     pb.best = d_best;
-    HIP_TRY(hipMemcpyAsync(d_prob, &pb, sizeof(pb), hipMemcpyHostToDevice, s));
+    m->arena.up(d_prob, &pb, sizeof(pb));
+    HIP_TRY(m->arena.flush(s));
     HIP_TRY(launch_window_best(d_prob, nq, s));
-    HIP_TRY(hipMemcpyAsync(best, d_best, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(m->arena.down(best, d_best, sizeof(int32_t) * nq, s));
+    HIP_TRY(m->arena.sync(s));
     return ORBX_OK;
 }
 
@@ -1310,14 +1360,14 @@ int orbx_compute_stereo_matches(orbx_matcher* m, orbx_extractor* ex, int left_fr
     // the extractor's stream produced the pyramids: order this stream after it
     hipStream_t s = m->stream;
     HIP_TRY(hipStreamSynchronize((hipStream_t)orbx_extractor_stream(ex)));
-    HIP_TRY(hipMemcpyAsync(d_kl, left->keys, sizeof(orbx_keypoint) * N, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_dl, left->desc, (size_t)N * 32, hipMemcpyHostToDevice, s));
+    m->arena.up(d_kl, left->keys, sizeof(orbx_keypoint) * N);
+    m->arena.up(d_dl, left->desc, (size_t)N * 32);
     if (n_right) {
-        HIP_TRY(hipMemcpyAsync(d_kr, keys_r, sizeof(orbx_keypoint) * n_right, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(d_dr, desc_r, (size_t)n_right * 32, hipMemcpyHostToDevice, s));
+        m->arena.up(d_kr, keys_r, sizeof(orbx_keypoint) * n_right);
+        m->arena.up(d_dr, desc_r, (size_t)n_right * 32);
     }
-    HIP_TRY(hipMemcpyAsync(d_off, off.data(), sizeof(int32_t) * (nRows + 1), hipMemcpyHostToDevice, s));
-    if (nidx) HIP_TRY(hipMemcpyAsync(d_idx, idx.data(), sizeof(int32_t) * nidx, hipMemcpyHostToDevice, s));
+    m->arena.up(d_off, off.data(), sizeof(int32_t) * (nRows + 1));
+    if (nidx) m->arena.up(d_idx, idx.data(), sizeof(int32_t) * nidx);
     pb.keys_l = d_kl;
     pb.desc_l = d_dl;
     pb.nl = N;
@@ -1327,10 +1377,11 @@ int orbx_compute_stereo_matches(orbx_matcher* m, orbx_extractor* ex, int left_fr
     pb.row_idx = d_idx;
     pb.bf = left->bf;
     pb.max_d = max_disparity;
+    HIP_TRY(m->arena.flush(s));
     HIP_TRY(launch_stereo(pb, d_res, s));
     std::vector<StereoResult> res((size_t)N);
-    HIP_TRY(hipMemcpyAsync(res.data(), d_res, sizeof(StereoResult) * N, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(m->arena.down(res.data(), d_res, sizeof(StereoResult) * N, s));
+    HIP_TRY(m->arena.sync(s));
     // Sequential outlier pass of this fork (Frame.cc:868-884): after every left keypoint
     // that reaches it, vDistIdx (sorted by (dist, iL)) is re-scanned from the back and
     // entries with dist >= 1.5f*1.4f*median are invalidated.  An empty vDistIdx is

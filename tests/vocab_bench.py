@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """DBoW2 vocabulary transform throughput on one MI355X.
 
-    python tools/bench_vocab.py [--steps K] [--warmup W] [--batch B] [--k 10] [--L 6]
+    python bench.py --vocab [--steps K] [--warmup W] [--batch B] [--k 10] [--L 6]
+
+(Lives under tests/ because it runs the oracle as its parity check and CPU baseline;
+bench.py --vocab is the entry point.)
 
 Workload: B=256 synthetic 640x480 frames are extracted on the GPU (ORBextractor,
 nFeatures=1000; not timed) and their descriptors stay in HBM.  A synthetic vocabulary
@@ -26,7 +29,8 @@ import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-sys.path.insert(0, str(ROOT))
+if str(ROOT) not in sys.path:
+    sys.path.insert(0, str(ROOT))
 
 import numpy as np  # noqa: E402
 
@@ -35,7 +39,7 @@ HBM_PEAK_GBS = 8000.0
 
 def pmc_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the newest profiles/*vocab*_pmc_traffic.json
-    (tools/pmc_traffic.sh TAG tools/bench_vocab.py + tools/pmc_traffic.py TAG)."""
+    (tools/pmc_traffic.sh TAG "bench.py --vocab" + tools/pmc_traffic.py TAG)."""
     files = sorted((ROOT / "profiles").glob("*vocab*_pmc_traffic.json"))
     if not files:
         return None, None
@@ -43,8 +47,8 @@ def pmc_traffic(kernel: str):
     return (int(ks[kernel]["traffic_bytes"]) if kernel in ks else None), files[-1].name
 
 
-def main():
-    ap = argparse.ArgumentParser()
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="bench.py --vocab")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256)
@@ -55,7 +59,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--parity-frames", type=int, default=4)
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     B = args.batch
 
     import torch
