@@ -32,6 +32,13 @@ constexpr int kThLow = 50;          // ORBmatcher::TH_LOW, ORBmatcher.cc:39
 constexpr int kInitList = 8;        // listed candidates per initialisation query
 constexpr unsigned long long kNone = ~0ull;
 
+// v of lane `src` (wave-uniform src) in every lane
+__device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int src) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, src);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), src);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int o) {
     const int lo = __shfl_xor((int)(unsigned)v, o, 64), hi = __shfl_xor((int)(unsigned)(v >> 32), o, 64);
     return (unsigned long long)(unsigned)hi << 32 | (unsigned)lo;
@@ -269,23 +276,35 @@ __device__ void init_scan(const InitProblem& pb, int i1, const int* md, unsigned
 
 }  // namespace
 
-__global__ __launch_bounds__(kBowThreads) void k_init(const InitProblem* __restrict__ probs) {
+__global__ __launch_bounds__(kBowThreads) void k_init(const InitProblem* __restrict__ probs, int lists_lds) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_hist[kHistoLength];
     __shared__ int s_ind[3];
     __shared__ int s_nrec;
     const InitProblem pb = probs[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    int* md = (int*)smem;          // vMatchedDistance [n2]
+    // LDS: the candidate lists first (8-byte aligned; in the problem's global buffer
+    // when they do not fit), then 4-byte arrays, then the bins
+    unsigned long long* lists = lists_lds ? (unsigned long long*)smem : pb.lists;  // [nq * kInitList]
+    int* md = (int*)(smem + (lists_lds ? (size_t)8 * kInitList * pb.nq : 0));      // vMatchedDistance [n2]
     int* m21 = md + pb.n2;         // vnMatches21 [n2]
     int* m12 = m21 + pb.n2;        // vnMatches12 [n1]
     int* items = m12 + pb.n1;      // rotHist entries (F1 index) [nq]
-    uint8_t* bins = (uint8_t*)(items + pb.nq);
+    int* trunc = items + pb.nq;    // listed count | truncated << 8 [nq]
+    int* qi1 = trunc + pb.nq;      // the queries' F1 keypoints [nq]
+    float* ang1 = (float*)(qi1 + pb.nq);  // keypoint angles of F1 [n1] and F2 [n2]
+    float* ang2 = ang1 + pb.n1;
+    uint8_t* bins = (uint8_t*)(ang2 + pb.n2);
     for (int i = tid; i < pb.n2; i += kBowThreads) {
         md[i] = INT_MAX;
         m21[i] = -1;
+        ang2[i] = pb.keys2[i].angle;
     }
-    for (int i = tid; i < pb.n1; i += kBowThreads) m12[i] = -1;
+    for (int i = tid; i < pb.n1; i += kBowThreads) {
+        m12[i] = -1;
+        ang1[i] = pb.keys1[i].angle;
+    }
+    for (int i = tid; i < pb.nq; i += kBowThreads) qi1[i] = pb.q_idx1[i];
     if (tid < kHistoLength) s_hist[tid] = 0;
     if (tid == 0) s_nrec = 0;
 
@@ -299,7 +318,7 @@ __global__ __launch_bounds__(kBowThreads) void k_init(const InitProblem* __restr
         for (; cnt < kInitList; cnt++) {
             const unsigned long long m = wave_min_u64(l[0]);
             if (m == kNone) break;
-            if (lane == 0) pb.lists[(size_t)q * kInitList + cnt] = m;
+            if (lane == 0) lists[(size_t)q * kInitList + cnt] = m;
             if (l[0] == m) {  // the owner pops its head
                 l[0] = l[1];
                 l[1] = l[2];
@@ -316,28 +335,29 @@ __global__ __launch_bounds__(kBowThreads) void k_init(const InitProblem* __restr
             }
         }
         if (cnt == kInitList && __any(l[0] != kNone || (seen > used && used == 4))) tr = 1;
-        if (lane == 0) pb.trunc[q] = cnt | tr << 8;
+        if (lane == 0) trunc[q] = cnt | tr << 8;
     }
     __syncthreads();
 
     // phase 2: the reference's sequential loop over F1's level-0 keypoints (wave 0)
     if (wave == 0) {
         for (int q = 0; q < pb.nq; q++) {
-            const int i1 = pb.q_idx1[q];
-            const int t = pb.trunc[q];
+            const int i1 = qi1[q];
+            const int t = trunc[q];
             const int cnt = t & 0xff, tr = t >> 8;
-            unsigned long long best = kNone, second = kNone;
-            int found = 0;
-            for (int j = 0; j < cnt && found < 2; j++) {
-                const unsigned long long e = pb.lists[(size_t)q * kInitList + j];
-                if (md[e_idx(e)] > e_dist(e)) {
-                    if (found == 0)
-                        best = e;
-                    else
-                        second = e;
-                    found++;
-                }
+            // the first two listed entries still available, in list order: lane k checks
+            // entry k against vMatchedDistance, the two lowest set ballot bits win
+            unsigned long long e = kNone;
+            bool avail = false;
+            if (lane < cnt) {
+                e = lists[(size_t)q * kInitList + lane];
+                avail = md[e_idx(e)] > e_dist(e);
             }
+            const unsigned long long bal = __ballot(avail);
+            const int found = __popcll(bal) < 2 ? __popcll(bal) : 2;
+            unsigned long long best = kNone, second = kNone;
+            if (found >= 1) best = shfl_u64(e, __ffsll((long long)bal) - 1);
+            if (found >= 2) second = shfl_u64(e, __ffsll((long long)(bal & (bal - 1))) - 1);
             if (found < 2 && tr) {  // the list ran out: rescan the window against vMatchedDistance
                 unsigned long long l[2];
                 int seen;
@@ -356,7 +376,7 @@ __global__ __launch_bounds__(kBowThreads) void k_init(const InitProblem* __restr
                     m21[i2] = i1;
                     md[i2] = bestDist;
                     if (pb.check_ori) {
-                        const int bin = rot_bin(pb.keys1[i1].angle, pb.keys2[i2].angle);
+                        const int bin = rot_bin(ang1[i1], ang2[i2]);
                         items[s_nrec] = i1;
                         bins[s_nrec] = (uint8_t)bin;
                         s_nrec++;
@@ -382,13 +402,15 @@ __global__ __launch_bounds__(kBowThreads) void k_init(const InitProblem* __restr
 }
 
 hipError_t launch_init(const InitProblem* d_prob, int n1, int n2, int nq, hipStream_t stream) {
-    const size_t lds = (size_t)4 * (2 * n2 + n1 + nq) + (size_t)nq + 16;
+    const size_t base = (size_t)4 * (3 * n2 + 2 * n1 + 3 * nq) + (size_t)nq + 16;
+    const int lists_lds = base + (size_t)8 * kInitList * nq <= 160 * 1024;
+    const size_t lds = base + (lists_lds ? (size_t)8 * kInitList * nq : 0);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)k_init, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_init, dim3(1), dim3(kBowThreads), lds, stream, d_prob);
+    hipLaunchKernelGGL(k_init, dim3(1), dim3(kBowThreads), lds, stream, d_prob, lists_lds);
     return hipGetLastError();
 }
 

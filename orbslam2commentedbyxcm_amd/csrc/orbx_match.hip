@@ -772,7 +772,11 @@ __device__ void score_tri(const TriProblem& pb, const TriQuery& Q, const uint8_t
     }
 }
 
-__global__ __launch_bounds__(256) void k_triangulation(const TriProblem* __restrict__ probs,
+// 16 waves score the queries (each scan is a chain of dependent gathers); wave 0 then
+// replays the greedy commit.
+constexpr int kTriThreads = 1024;
+
+__global__ __launch_bounds__(kTriThreads) void k_triangulation(const TriProblem* __restrict__ probs,
                                                        unsigned long long* __restrict__ scratch) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_hist[kHistoLength];
@@ -781,45 +785,71 @@ __global__ __launch_bounds__(256) void k_triangulation(const TriProblem* __restr
     uint8_t* matched2 = smem;  // vbMatched2, n2 bytes
     int* mlist = (int*)(smem + ((pb.n2 + 15) & ~15));
     int* mbin = mlist + pb.nq;
-    for (int i = tid; i < pb.n2; i += 256) matched2[i] = 0;
+    for (int i = tid; i < pb.n2; i += kTriThreads) matched2[i] = 0;
     if (tid < kHistoLength) s_hist[tid] = 0;
     __syncthreads();
     unsigned long long* keys = scratch + pb.scratch_off;
-    for (int q = wave; q < pb.nq; q += 4) {
+    for (int q = wave; q < pb.nq; q += kTriThreads / 64) {  // candidate scans: all waves
         unsigned long long best;
         score_tri(pb, pb.q[q], matched2, best);
         if (lane == 0) keys[q] = best;
     }
     __syncthreads();
     if (wave == 0) {
+        // The greedy commit (cc:985-990) in query order, 64 queries per chunk: lane i
+        // prefetches query q0+i's record, pre-scored best, candidate and angles, and the
+        // sequential walk reads them back by v_readlane, so only a claimed best (a
+        // re-score against the current vbMatched2) touches global memory.
         int nrec = 0;
         const float factor = kHistoLength / 360.0f;
-        for (int q = 0; q < pb.nq; q++) {
-            const TriQuery Q = pb.q[q];
-            unsigned long long best = keys[q];
-            if (best != kNoKey) {
-                const int idx2 = pb.fv2_idx[Q.beg + (int)(0xffffffffu - (unsigned)(best & 0xffffffffu))];
-                if (matched2[idx2]) score_tri(pb, Q, matched2, best);
-            }
-            int idx2 = -1;
-            if (best != kNoKey) idx2 = pb.fv2_idx[Q.beg + (int)(0xffffffffu - (unsigned)(best & 0xffffffffu))];
-            if (lane == 0) pb.matches12[Q.idx1] = idx2;
-            if (idx2 < 0) continue;
-            if (lane == 0) matched2[idx2] = 1;
-            if (pb.check_ori) {
-                float rot = pb.keys1[Q.idx1].angle - pb.keys2[idx2].angle;
-                if (rot < 0.0f) rot += 360.0f;
-                int bin = (int)roundf(rot * factor);
-                if (bin == kHistoLength) bin = 0;
-                if (lane == 0) {
-                    mlist[nrec] = Q.idx1;
-                    mbin[nrec] = bin;
-                    s_hist[bin]++;
+        for (int q0 = 0; q0 < pb.nq; q0 += 64) {
+            const int ql = q0 + lane;
+            int l_idx1 = 0, l_idx2 = -1;
+            unsigned long long l_best = kNoKey;
+            float l_a1 = 0.f, l_a2 = 0.f;
+            if (ql < pb.nq) {
+                const TriQuery Q = pb.q[ql];
+                l_idx1 = Q.idx1;
+                l_best = keys[ql];
+                if (l_best != kNoKey) {
+                    l_idx2 = pb.fv2_idx[Q.beg + (int)(0xffffffffu - (unsigned)(l_best & 0xffffffffu))];
+                    l_a2 = pb.keys2[l_idx2].angle;
                 }
-                nrec++;
+                l_a1 = pb.keys1[Q.idx1].angle;
             }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-            __builtin_amdgcn_wave_barrier();
+            const int cnt = pb.nq - q0 < 64 ? pb.nq - q0 : 64;
+            for (int j = 0; j < cnt; j++) {
+                const int idx1 = __builtin_amdgcn_readlane(l_idx1, j);
+                unsigned long long best = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(l_best >> 32), j) << 32) |
+                                          (unsigned)__builtin_amdgcn_readlane((int)(unsigned)l_best, j);
+                int idx2 = __builtin_amdgcn_readlane(l_idx2, j);
+                float a2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l_a2), j));
+                if (best != kNoKey && matched2[idx2]) {  // taken by an earlier query: re-score
+                    const TriQuery Q = pb.q[q0 + j];
+                    score_tri(pb, Q, matched2, best);
+                    idx2 = best != kNoKey
+                               ? pb.fv2_idx[Q.beg + (int)(0xffffffffu - (unsigned)(best & 0xffffffffu))]
+                               : -1;
+                    if (idx2 >= 0) a2 = pb.keys2[idx2].angle;
+                }
+                if (lane == 0) pb.matches12[idx1] = idx2;
+                if (idx2 < 0) continue;
+                if (lane == 0) matched2[idx2] = 1;
+                if (pb.check_ori) {
+                    float rot = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l_a1), j)) - a2;
+                    if (rot < 0.0f) rot += 360.0f;
+                    int bin = (int)roundf(rot * factor);
+                    if (bin == kHistoLength) bin = 0;
+                    if (lane == 0) {
+                        mlist[nrec] = idx1;
+                        mbin[nrec] = bin;
+                        s_hist[bin]++;
+                    }
+                    nrec++;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         if (pb.check_ori) {
@@ -857,7 +887,7 @@ hipError_t launch_triangulation(const TriProblem* d_probs, int nprob, unsigned l
                                            (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_triangulation, dim3(nprob), dim3(256), lds, stream, d_probs, scratch);
+    hipLaunchKernelGGL(k_triangulation, dim3(nprob), dim3(kTriThreads), lds, stream, d_probs, scratch);
     return hipGetLastError();
 }
 
