@@ -68,6 +68,13 @@ struct orbx_extractor {
     // host-API staging
     uint8_t* d_in = nullptr;
     size_t d_in_bytes = 0;
+    // pinned mirrors of d_in / d_kps / d_desc / d_n: host frames are packed here and
+    // uploaded in one copy (a 2-D copy of an odd-width frame goes row by row), results
+    // come back through them
+    uint8_t* h_in = nullptr;
+    orbx_keypoint* h_kps = nullptr;
+    uint8_t* h_desc = nullptr;
+    int* h_n = nullptr;
     orbx_keypoint* d_kps = nullptr;
     uint8_t* d_desc = nullptr;
     int* d_n = nullptr;
@@ -186,26 +193,69 @@ int check_status(orbx_extractor* ex, int batch) {
     return ORBX_OK;
 }
 
+template <typename T>
+hipError_t halloc(T** p, size_t n) {  // pinned host memory
+    if (n == 0) n = 1;
+    return hipHostMalloc((void**)p, sizeof(T) * n, hipHostMallocDefault);
+}
+
+void free_host_staging(orbx_extractor* ex) {
+    if (ex->d_in) (void)hipFree(ex->d_in);
+    if (ex->d_kps) (void)hipFree(ex->d_kps);
+    if (ex->d_desc) (void)hipFree(ex->d_desc);
+    if (ex->d_n) (void)hipFree(ex->d_n);
+    if (ex->h_in) (void)hipHostFree(ex->h_in);
+    if (ex->h_kps) (void)hipHostFree(ex->h_kps);
+    if (ex->h_desc) (void)hipHostFree(ex->h_desc);
+    if (ex->h_n) (void)hipHostFree(ex->h_n);
+    ex->d_in = nullptr;
+    ex->d_kps = nullptr;
+    ex->d_desc = nullptr;
+    ex->d_n = nullptr;
+    ex->h_in = nullptr;
+    ex->h_kps = nullptr;
+    ex->h_desc = nullptr;
+    ex->h_n = nullptr;
+    ex->d_in_bytes = 0;
+    ex->d_out_cap = 0;
+    ex->d_n_cap = 0;
+}
+
 int ensure_host_staging(orbx_extractor* ex, size_t in_bytes, size_t out_slots, int nframes) {
     if (ex->d_in_bytes < in_bytes) {
         if (ex->d_in) (void)hipFree(ex->d_in);
+        if (ex->h_in) (void)hipHostFree(ex->h_in);
         ex->d_in = nullptr;
+        ex->h_in = nullptr;
+        ex->d_in_bytes = 0;
         HIP_TRY(dalloc(&ex->d_in, in_bytes));
+        HIP_TRY(halloc(&ex->h_in, in_bytes));
         ex->d_in_bytes = in_bytes;
     }
     if (ex->d_out_cap < out_slots) {
         if (ex->d_kps) (void)hipFree(ex->d_kps);
         if (ex->d_desc) (void)hipFree(ex->d_desc);
+        if (ex->h_kps) (void)hipHostFree(ex->h_kps);
+        if (ex->h_desc) (void)hipHostFree(ex->h_desc);
         ex->d_kps = nullptr;
         ex->d_desc = nullptr;
+        ex->h_kps = nullptr;
+        ex->h_desc = nullptr;
+        ex->d_out_cap = 0;
         HIP_TRY(dalloc(&ex->d_kps, out_slots));
         HIP_TRY(dalloc(&ex->d_desc, out_slots * 32));
+        HIP_TRY(halloc(&ex->h_kps, out_slots));
+        HIP_TRY(halloc(&ex->h_desc, out_slots * 32));
         ex->d_out_cap = out_slots;
     }
     if (ex->d_n_cap < nframes) {
         if (ex->d_n) (void)hipFree(ex->d_n);
+        if (ex->h_n) (void)hipHostFree(ex->h_n);
         ex->d_n = nullptr;
+        ex->h_n = nullptr;
+        ex->d_n_cap = 0;
         HIP_TRY(dalloc(&ex->d_n, (size_t)nframes));
+        HIP_TRY(halloc(&ex->h_n, (size_t)nframes));
         ex->d_n_cap = nframes;
     }
     return ORBX_OK;
@@ -254,10 +304,7 @@ void orbx_extractor_destroy(orbx_extractor* ex) {
     (void)hipSetDevice(ex->device);
     if (ex->stream) (void)hipStreamSynchronize(ex->stream);
     free_buffers(ex->db);
-    if (ex->d_in) (void)hipFree(ex->d_in);
-    if (ex->d_kps) (void)hipFree(ex->d_kps);
-    if (ex->d_desc) (void)hipFree(ex->d_desc);
-    if (ex->d_n) (void)hipFree(ex->d_n);
+    free_host_staging(ex);
     for (auto& slot : ex->ev)
         for (auto& e : slot)
             if (e) (void)hipEventDestroy(e);
@@ -346,14 +393,22 @@ int orbx_extract_batch(orbx_extractor* ex, int batch, const uint8_t* const* imgs
     const size_t fbytes = (size_t)width * height;
     int rc = ensure_host_staging(ex, fbytes * batch, (size_t)batch * (cap > 0 ? cap : 1), batch);
     if (rc != ORBX_OK) return rc;
-    for (int b = 0; b < batch; b++)
-        HIP_TRY(hipMemcpy2DAsync(ex->d_in + fbytes * b, width, imgs[b], stride, width, height, hipMemcpyHostToDevice,
-                                 ex->stream));
+    // the previous call's downloads into the pinned mirrors completed at its final sync
+    for (int b = 0; b < batch; b++) {
+        uint8_t* dst = ex->h_in + fbytes * b;
+        if (stride == (size_t)width) {
+            std::memcpy(dst, imgs[b], fbytes);
+        } else {
+            for (int y = 0; y < height; y++) std::memcpy(dst + (size_t)y * width, imgs[b] + (size_t)y * stride, width);
+        }
+    }
+    HIP_TRY(hipMemcpyAsync(ex->d_in, ex->h_in, fbytes * batch, hipMemcpyHostToDevice, ex->stream));
     rc = run_device(ex, batch, ex->d_in, fbytes, width, height, (size_t)width, ex->d_kps, ex->d_desc,
                     cap > 0 ? cap : 1, ex->d_n, ex->stream);
     if (rc != ORBX_OK) return rc;
-    HIP_TRY(hipMemcpyAsync(n_per_frame, ex->d_n, sizeof(int) * batch, hipMemcpyDeviceToHost, ex->stream));
+    HIP_TRY(hipMemcpyAsync(ex->h_n, ex->d_n, sizeof(int) * batch, hipMemcpyDeviceToHost, ex->stream));
     HIP_TRY(hipStreamSynchronize(ex->stream));
+    std::memcpy(n_per_frame, ex->h_n, sizeof(int) * batch);
     rc = check_status(ex, batch);
     if (rc != ORBX_OK) return rc;
     int overflow = 0;
@@ -362,14 +417,20 @@ int orbx_extract_batch(orbx_extractor* ex, int batch, const uint8_t* const* imgs
         if (n_per_frame[b] > cap) overflow = 1;
         if (n > 0) {
             if (kps)
-                HIP_TRY(hipMemcpyAsync(kps + (size_t)b * cap, ex->d_kps + (size_t)b * cap, sizeof(orbx_keypoint) * n,
-                                       hipMemcpyDeviceToHost, ex->stream));
+                HIP_TRY(hipMemcpyAsync(ex->h_kps + (size_t)b * cap, ex->d_kps + (size_t)b * cap,
+                                       sizeof(orbx_keypoint) * n, hipMemcpyDeviceToHost, ex->stream));
             if (desc)
-                HIP_TRY(hipMemcpyAsync(desc + (size_t)b * cap * 32, ex->d_desc + (size_t)b * cap * 32, (size_t)n * 32,
-                                       hipMemcpyDeviceToHost, ex->stream));
+                HIP_TRY(hipMemcpyAsync(ex->h_desc + (size_t)b * cap * 32, ex->d_desc + (size_t)b * cap * 32,
+                                       (size_t)n * 32, hipMemcpyDeviceToHost, ex->stream));
         }
     }
     HIP_TRY(hipStreamSynchronize(ex->stream));
+    for (int b = 0; b < batch; b++) {
+        const int n = n_per_frame[b] < cap ? n_per_frame[b] : cap;
+        if (n <= 0) continue;
+        if (kps) std::memcpy(kps + (size_t)b * cap, ex->h_kps + (size_t)b * cap, sizeof(orbx_keypoint) * n);
+        if (desc) std::memcpy(desc + (size_t)b * cap * 32, ex->h_desc + (size_t)b * cap * 32, (size_t)n * 32);
+    }
     return overflow ? fail(ORBX_ERR_CAPACITY, "more keypoints than cap") : ORBX_OK;
 }
 

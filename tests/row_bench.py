@@ -62,6 +62,23 @@ def rows(O, reps: int):
         out.append({"row": row, "reference": ref, "size": size, "gpu_ms": round(g_ms, 4), "cpu_ms": round(c_ms, 4),
                     "speedup": round(c_ms / g_ms, 2) if g_ms > 0 else None, "bit_exact": bool(_eq(g, c))})
 
+    # a1-a8 ORBextractor::operator(): one frame per call (host image in, keypoints and
+    # descriptors out), the BASELINE configs C1, C3 (KITTI), C5 (5000 features, 12 levels)
+    for (W, H, nf, L, tag) in ((640, 480, 1000, 8, "C1"), (1241, 376, 2000, 8, "C3"), (640, 480, 5000, 12, "C5")):
+        img = synth.frame(11, W, H)
+        ex = ORBextractor(nf, 1.2, L, 20, 7)
+        p = O.params(nf, 1.2, L, 20, 7)
+
+        def ex_g(ex=ex, img=img):
+            k, d = ex(img)
+            return k.view(np.uint8).copy(), d.copy()
+
+        def ex_c(p=p, img=img):
+            k, d, _ = O.extract(img, p)
+            return k.view(np.uint8).copy(), d.copy()
+        add("a2", "ORBextractor::operator() ORBextractor.cc:1513-1629 (a1-a8)",
+            f"{tag}: {W}x{H}, {nf} features, {L} levels, one frame", ex_g, ex_c)
+
     A, B = S.two_views(O, 0)
     As, Bs = S.two_views(O, 2, stereo=True)
     nA, nB = len(A.keys), len(B.keys)
