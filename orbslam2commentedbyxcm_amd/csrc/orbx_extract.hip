@@ -280,43 +280,47 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ src
 
 typedef short short2_t __attribute__((ext_vector_type(2)));
 
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+
 // FAST-9/16 corner strength M = max over the 16 contiguous 9-arcs of
 // max(min(v - ring), min(ring - v)).  At threshold t the pixel is a corner iff
 // M > t, and cornerScore<16> then returns max(t, M) - 1 = M - 1, independent of t
 // (features2d/fast.cpp FAST_t / fast_score.cpp cornerScore<16>).  Both signs are
-// evaluated at once in packed int16 lanes on (x, 255 - x): per arc,
-// min(x - v) = min(x) - v and min(v - x) = min(255 - x) - (255 - v), so the arc
-// minima of the pairs are taken first and (v, 255 - v) is subtracted once.  The pair
-// is one v_mad_i32_i24: x * (1 - 2^16) + 255 * 2^16.
+// evaluated at once in packed pairs (x, 255 - x): per arc, min(x - v) = min(x) - v and
+// min(v - x) = min(255 - x) - (255 - v), so the arc minima of the pairs are taken first
+// and (v, 255 - v) is subtracted once.  The pairs are f16 1024 + (x, 255 - x): f16 bits
+// 0x6400 + n for n < 1024, i.e. one v_mad_i32_i24 per ring pixel, x * (1 - 2^16) +
+// 0x64FF6400, and every value stays an exact small integer.  That admits gfx950's
+// 3-input v_pk_minimum3_f16 / v_pk_maximum3_f16: windows of 3 (16), arcs of 9 as
+// three windows of 3 (16), the maximum over the arcs (8) -- 40 packed operations.
 __device__ __forceinline__ int fast_strength(const uint8_t* c, int pitch) {
     const int off[16] = {0 + 3 * pitch,  1 + 3 * pitch,  2 + 2 * pitch,  3 + 1 * pitch,
                          3,              3 - 1 * pitch,  2 - 2 * pitch,  1 - 3 * pitch,
                          0 - 3 * pitch, -1 - 3 * pitch, -2 - 2 * pitch, -3 - 1 * pitch,
                          -3,            -3 + 1 * pitch, -2 + 2 * pitch, -1 + 3 * pitch};
     const int v = c[0];
-    short2_t d[16];
+    half2_t d[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = __builtin_bit_cast(short2_t, (int)c[off[k]] * -65535 + 0xff0000);
-    // For odd j, m8[j] = min(d[j..j+7]) serves two arcs: [j-1, j+7] and [j, j+8]
-    // (47 packed min/max instead of 79 for all 16 arcs independently).
-    short2_t m2[8], m4[8], m8[8];
+    for (int k = 0; k < 16; k++) d[k] = __builtin_bit_cast(half2_t, (int)c[off[k]] * -65535 + 0x64ff6400);
+    auto mn3 = [](half2_t a, half2_t b, half2_t e) {
+        return __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), e);
+    };
+    auto mx3 = [](half2_t a, half2_t b, half2_t e) {
+        return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), e);
+    };
+    half2_t t3[16], arc[16];
 #pragma unroll
-    for (int i = 0; i < 8; i++) m2[i] = __builtin_elementwise_min(d[2 * i + 1], d[(2 * i + 2) & 15]);
+    for (int j = 0; j < 16; j++) t3[j] = mn3(d[j], d[(j + 1) & 15], d[(j + 2) & 15]);
 #pragma unroll
-    for (int i = 0; i < 8; i++) m4[i] = __builtin_elementwise_min(m2[i], m2[(i + 1) & 7]);
-#pragma unroll
-    for (int i = 0; i < 8; i++) m8[i] = __builtin_elementwise_min(m4[i], m4[(i + 2) & 7]);
-    // the two arcs of m8[j] give max(min(m8, d[j-1]), min(m8, d[j+8])) = min(m8, max(d[j-1], d[j+8]))
-    short2_t best = __builtin_elementwise_min(m8[0], __builtin_elementwise_max(d[0], d[9]));
-#pragma unroll
-    for (int i = 1; i < 8; i++) {
-        const int j = 2 * i + 1;
-        best = __builtin_elementwise_max(
-            best, __builtin_elementwise_min(m8[i], __builtin_elementwise_max(d[j - 1], d[(j + 8) & 15])));
-    }
-    best = best - __builtin_bit_cast(short2_t, v * -65535 + 0xff0000);  // (min x - v, v - max x)
-    const int M = best.x > best.y ? best.x : best.y;
-    return M > 0 ? M : 0;
+    for (int j = 0; j < 16; j++) arc[j] = mn3(t3[j], t3[(j + 3) & 15], t3[(j + 6) & 15]);
+    const half2_t b0 = mx3(arc[0], arc[1], arc[2]), b1 = mx3(arc[3], arc[4], arc[5]);
+    const half2_t b2 = mx3(arc[6], arc[7], arc[8]), b3 = mx3(arc[9], arc[10], arc[11]);
+    const half2_t b4 = mx3(arc[12], arc[13], arc[14]);
+    const half2_t best = __builtin_elementwise_maximum(mx3(b0, b1, b2), mx3(b3, b4, arc[15]));
+    // (min x - v, v - max x), exact in f16
+    const half2_t r = best - __builtin_bit_cast(half2_t, v * -65535 + 0x64ff6400);
+    const _Float16 M = r.x > r.y ? r.x : r.y;
+    return M > (_Float16)0 ? (int)M : 0;
 }
 
 __device__ __forceinline__ int reflect101(int i, int n) {
