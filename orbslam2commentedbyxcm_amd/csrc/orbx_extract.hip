@@ -746,7 +746,7 @@ __device__ __forceinline__ void child_box(int q, int x0, int y0, int x1, int y1,
 // ------------------------------------------------------------------ octree
 
 // Node list, stored in list order (front first).  Two buffers, swapped every step.
-constexpr int kOctKeysReg = 24 * 256;  // keys per level held in registers by k_octree
+constexpr int kOctKeysReg = 16 * 256;  // keys per level held in registers by k_octree
 
 // atomicAdd(&a[idx], 1) for the active lanes, one atomic per distinct idx of the wave
 // (the early octree passes send thousands of keys to a handful of counters).
