@@ -781,7 +781,7 @@ struct NodeBuf {
 //    node first;
 //  * each surviving node keeps its max-response key, first (lowest index) on ties
 //    (cc:984-1009).
-__global__ __launch_bounds__(256) void k_octree(const LevelGeom* __restrict__ lv, int L,
+__global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__ lv, int L,
                                                 const uint32_t* __restrict__ slots, int slots_pf,
                                                 const CellGeom* __restrict__ cells,
                                                 const int* __restrict__ cell_count, int ncells_total,
@@ -899,14 +899,15 @@ __global__ __launch_bounds__(256) void k_octree(const LevelGeom* __restrict__ lv
     constexpr bool REG = decltype(reg_tag)::value;
     constexpr int KPT = REG ? kOctKeysReg / 256 : 1;
     uint32_t kr[KPT];
-    int nr[KPT];
+    uint32_t nr[(KPT + 1) / 2];  // node ids (< NC <= 2^15), two per register
     if (REG) {
 #pragma unroll
         for (int i = 0; i < KPT; i++) {
             const int k = min(tid + 256 * i, n - 1);
             kr[i] = n > 0 ? K[k] : 0u;
-            nr[i] = 0;
         }
+#pragma unroll
+        for (int i = 0; i < (KPT + 1) / 2; i++) nr[i] = 0u;
     }
 #define FOR_KEYS(BODY)                                                      \
     if (REG) {                                                              \
@@ -914,8 +915,11 @@ __global__ __launch_bounds__(256) void k_octree(const LevelGeom* __restrict__ lv
             const int k = tid + 256 * i_;                                   \
             if (k < n) {                                                    \
                 const uint32_t KK = kr[i_];                                 \
-                int& NN = nr[i_];                                           \
+                const int sh_ = 16 * (i_ & 1);                              \
+                int NN = (int)((nr[i_ >> 1] >> sh_) & 0xffffu);             \
                 BODY                                                        \
+                nr[i_ >> 1] = (nr[i_ >> 1] & ~(0xffffu << sh_)) |           \
+                              ((uint32_t)NN & 0xffffu) << sh_;             \
             }                                                               \
         }                                                                   \
     } else {                                                                \
