@@ -319,8 +319,8 @@ __device__ __forceinline__ int fast_strength(const uint8_t* c, int pitch) {
     const half2_t best = __builtin_elementwise_maximum(mx3(b0, b1, b2), mx3(b3, b4, arc[15]));
     // (min x - v, v - max x), exact in f16
     const half2_t r = best - __builtin_bit_cast(half2_t, v * -65535 + 0x64ff6400);
-    const _Float16 M = r.x > r.y ? r.x : r.y;
-    return M > (_Float16)0 ? (int)M : 0;
+    const _Float16 M = __builtin_elementwise_maximum(__builtin_elementwise_maximum(r.x, r.y), (_Float16)0);
+    return (unsigned short)M;  // v_max3_f16 + v_cvt_u16_f16
 }
 
 __device__ __forceinline__ int reflect101(int i, int n) {
@@ -454,11 +454,11 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
 #pragma unroll
         for (int k = 0; k < 4; k++) colmask |= (x0 + k >= kEdge && x0 + k < g.w - kEdge) ? 1u << k : 0u;
         const short2_t tq1 = {(short)(tq + 1), (short)(tq + 1)};
+        unsigned pass = 0;  // bit 4 it + k: pixel (row tid/16 + 16 it, column 4j + k) passes
 #pragma unroll
         for (int it = 0; it < kTH / 16; it++) {
             const int r = (tid >> 4) + 16 * it;
             const int y = Y0 + r;
-            unsigned pass = 0;
             if (colmask != 0 && y >= kEdge && y < g.h - kEdge) {
                 const uint32_t* rc = (const uint32_t*)&s_in[r + 3][c0];
                 const uint32_t V = rc[0];
@@ -484,27 +484,33 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
                     // max(br, -dk) - (tq + 1) >= 0 <=> the pixel passes; sign in bits 15 / 31
                     q[h] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(br, short2_t{0, 0} - dk) - tq1);
                 }
-                // sign bytes of the 4 pixels -> bit k of pass (clear sign = pass)
+                // sign bytes of the 4 pixels -> bit k (clear sign = pass)
                 const uint32_t sb = ~__builtin_amdgcn_perm(q[1], q[0], 0x07050301u) & 0x80808080u;
-                pass = (((sb >> 7) * 0x01020408u) >> 24) & colmask;
+                pass |= ((((sb >> 7) * 0x01020408u) >> 24) & colmask) << (4 * it);
             }
-            // wave-level append: offsets from the per-bit ballots, one LDS atomic per wave;
-            // list order is irrelevant (each entry names its own pixel)
-            unsigned off = 0;
-            int tot = 0;
+        }
+        // one wave-level append for the thread's kTH/16 x 4 pixels: the exclusive prefix
+        // of the per-thread counts (<= 12) from one ballot per count bit, one LDS atomic
+        // per wave; list order is irrelevant (each entry names its own pixel)
+        static_assert(kTH / 16 * 4 < 16, "4 count bits");
+        const unsigned cnt = __popc(pass);
+        unsigned off = 0;
+        int tot = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const unsigned long long m = __ballot((cnt >> b) & 1u);
+            off += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
+            tot += __popcll(m) << b;
+        }
+        int base = 0;
+        if (lane == 0 && tot) base = atomicAdd(&s_n, tot);
+        base = __builtin_amdgcn_readfirstlane(base) + off;
+#pragma unroll
+        for (int it = 0; it < kTH / 16; it++) {
+            const int rowc = (((tid >> 4) + 16 * it) << 8) | (4 * j);
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const unsigned long long m = __ballot((pass >> k) & 1u);
-                off = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, off));
-                tot += __popcll(m);
-            }
-            int base = 0;
-            if (lane == 0 && tot) base = atomicAdd(&s_n, tot);
-            base = __shfl(base, 0) + off;
-            const int rowc = (r << 8) | (4 * j);
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const bool p = (pass >> k) & 1u;
+                const unsigned p = (pass >> (4 * it + k)) & 1u;
                 s_list[p ? base : kTH * kTW] = (uint16_t)(rowc + k);
                 base += p;
             }
@@ -519,7 +525,7 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
         if (y >= g.h || x >= g.w) continue;
         // staged rows r..r+6, as 4 row pairs starting at r (even r) or r-1 (odd r),
         // one v_dot2_u32_u16 per pair and column
-        unsigned s[4] = {0, 0, 0, 0};
+        unsigned s[4] = {1u << 15, 1u << 15, 1u << 15, 1u << 15};  // + the rounding half
         const int p0 = r >> 1;
         const bool odd = r & 1;
         const ushort2_t w0 = odd ? ushort2_t{0, 18} : ushort2_t{18, 34};
@@ -538,7 +544,7 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
         uint32_t packed = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const unsigned v = (s[k] + (1u << 15)) >> 16;
+            const unsigned v = s[k] >> 16;
             packed |= (v > 255 ? 255u : v) << (8 * k);
         }
         uint8_t* o = bout + (size_t)y * g.pitch + x;
