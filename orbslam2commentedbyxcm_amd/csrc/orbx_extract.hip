@@ -356,6 +356,18 @@ __device__ __forceinline__ void blur_row4(uint32_t lo, uint32_t mid, uint32_t hi
 __device__ __forceinline__ uint32_t lo_pair(uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c010c00u); }
 __device__ __forceinline__ uint32_t hi_pair(uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c030c02u); }
 
+// Inclusive prefix sum over the 64 lanes of a wave (all lanes active): DPP row_shr
+// 1/2/4/8 inside each 16-lane row, then row_bcast:15 and row_bcast:31 across rows.
+__device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+    return v;
+}
+
 // One 64x48 tile of one pyramid level per workgroup, all levels and frames in one
 // launch (XCD-aware frame placement).  The tile plus a 3-pixel REFLECT_101 margin is
 // staged in LDS once and feeds both per-pixel products of the level:
@@ -376,7 +388,7 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
     __shared__ __align__(16) uint8_t s_in[kTH + 6][kSW];
     __shared__ __align__(16) uint32_t s_rowp[(kTH + 6) / 2][kTW];  // (row 2p, row 2p+1) u16 pairs
     __shared__ __align__(16) uint8_t s_m[kTH][kTW];
-    __shared__ uint16_t s_list[kTH * kTW + 1];  // + a dump slot for branch-free appends
+    __shared__ uint16_t s_list[kTH * kTW + 128];  // + per-lane dump slots for branch-free appends
     __shared__ int s_n;
     int f, tile;
     xcd_frame_block(tiles_pf, nframes, f, tile);
@@ -489,30 +501,35 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
                 pass |= ((((sb >> 7) * 0x01020408u) >> 24) & colmask) << (4 * it);
             }
         }
-        // one wave-level append for the thread's kTH/16 x 4 pixels: the exclusive prefix
-        // of the per-thread counts (<= 12) from one ballot per count bit, one LDS atomic
-        // per wave; list order is irrelevant (each entry names its own pixel)
-        static_assert(kTH / 16 * 4 < 16, "4 count bits");
-        const unsigned cnt = __popc(pass);
-        unsigned off = 0;
+        // one wave-level append for the thread's kTH/16 x 4 pixels, one LDS atomic per
+        // wave.  Inside the wave's block the entries go iteration-major (all row-group-0
+        // pixels of the wave, then row group 1, ...): 32 consecutive entries then come
+        // from adjacent rows, whose ring bytes the strength loop reads from distinct LDS
+        // banks (thread-major order put rows r, r + 16, r + 32 -- one bank -- together).
+        // Per-iteration counts in 10-bit fields, exclusive offsets from one DPP wave scan.
+        static_assert(kTH / 16 <= 3, "three 10-bit count fields");
+        uint32_t C = 0;
+#pragma unroll
+        for (int it = 0; it < kTH / 16; it++) C |= (uint32_t)__popc((pass >> (4 * it)) & 15u) << (10 * it);
+        const uint32_t S = wave_inclusive_sum(C);
+        const uint32_t T = __builtin_amdgcn_readlane(S, 63), E = S - C;
         int tot = 0;
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const unsigned long long m = __ballot((cnt >> b) & 1u);
-            off += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
-            tot += __popcll(m) << b;
-        }
+        for (int it = 0; it < kTH / 16; it++) tot += (T >> (10 * it)) & 1023u;
         int base = 0;
         if (lane == 0 && tot) base = atomicAdd(&s_n, tot);
-        base = __builtin_amdgcn_readfirstlane(base) + off;
+        base = __builtin_amdgcn_readfirstlane(base);
+        const int dump = kTH * kTW + 2 * lane;  // per-lane dump slots: no shared address
 #pragma unroll
         for (int it = 0; it < kTH / 16; it++) {
+            int o = base + ((E >> (10 * it)) & 1023u);
+            base += (T >> (10 * it)) & 1023u;
             const int rowc = (((tid >> 4) + 16 * it) << 8) | (4 * j);
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const unsigned p = (pass >> (4 * it + k)) & 1u;
-                s_list[p ? base : kTH * kTW] = (uint16_t)(rowc + k);
-                base += p;
+                s_list[p ? o : dump] = (uint16_t)(rowc + k);
+                o += p;
             }
         }
     }
