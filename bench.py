@@ -185,6 +185,27 @@ def check_parity(frames_np, T, kps_all, desc_all, n_host, mp_all, nm_all, nframe
     return {"frames_checked": nframes, "pairs_checked": 1, "bit_exact": bool(ok), "matches_pair0": int(nr)}
 
 
+
+def _match_stream(dev):
+    """The matcher's stream.  ORBX_MATCH_CUSTRIDE=k (tuning knob) restricts it to every
+    k-th compute unit (hipExtStreamCreateWithCUMask), so the concurrent extraction keeps
+    the other CUs' LDS and wave slots to itself."""
+    import torch
+    k = int(os.environ.get("ORBX_MATCH_CUSTRIDE", "0"))
+    if k <= 1:
+        return torch.cuda.Stream(device=dev)
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    words = (ctypes.c_uint32 * ((ncu + 31) // 32))()
+    for i in range(0, ncu, k):
+        words[i // 32] |= 1 << (i % 32)
+    h = ctypes.c_void_p()
+    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(words)), words)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {rc}")
+    return torch.cuda.ExternalStream(h.value, device=dev)
+
 def main():
     # Secondary measurements (their implementations live under tests/: they run the
     # oracle as parity check and CPU baseline): the DBoW2 transform and the per-row table.
@@ -289,7 +310,7 @@ def main():
         n2 = [d_n, torch.empty_like(d_n)]
         mp2 = [d_mp, torch.empty_like(d_mp)]
         nm2 = [d_nm, torch.empty_like(d_nm)]
-        ms = torch.cuda.Stream(device=dev)
+        ms = _match_stream(dev)
         matcher.set_footprint(True)  # leave wave slots / LDS to the concurrent extraction
         ev_ex = [[torch.cuda.Event() for _ in range(S)] for _ in range(2)]  # [buffer][lane]
         ev_m = [torch.cuda.Event(), torch.cuda.Event()]

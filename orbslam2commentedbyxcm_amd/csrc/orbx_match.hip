@@ -647,6 +647,12 @@ __global__ __launch_bounds__(256) void k_seq_build(SeqArgs A, ProjQuery* __restr
         scratch_off[p] = (long long)p * kProjScratchWords * A.cap;
     }
     if (i >= A.cap) return;
+    // the outputs' initial state (no match), here rather than in two memsets: fewer
+    // launches on a stream that runs beside the extraction
+    A.cur_mp[(size_t)(p + 1) * A.cap + i] = -1;
+    if (p == 0) A.cur_mp[i] = -1;
+    if (i == 0) A.nmatches[p + 1] = 0;
+    if (p == 0 && i == 0) A.nmatches[0] = 0;
     ProjQuery q{};
     q.mp = -1;
     if (i < nlast) {

@@ -511,9 +511,11 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     auto* d_prob = m->arena.take<ProjProblem>(npairs > 0 ? npairs : 1);
     auto* d_off = m->arena.take<long long>(npairs > 0 ? npairs : 1);
     auto* d_scr = m->arena.take<unsigned long long>(kProjScratchWords * (size_t)(npairs > 0 ? npairs : 1) * cap);
-    HIP_TRY(hipMemsetAsync(d_cur_mp, 0xff, sizeof(int32_t) * (size_t)batch * cap, s));
-    HIP_TRY(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * (size_t)batch, s));
-    if (npairs == 0) return ORBX_OK;
+    if (npairs == 0) {  // otherwise k_seq_build initialises both outputs
+        HIP_TRY(hipMemsetAsync(d_cur_mp, 0xff, sizeof(int32_t) * (size_t)batch * cap, s));
+        HIP_TRY(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * (size_t)batch, s));
+        return ORBX_OK;
+    }
     SeqArgs A{};
     A.kps = d_kps;
     A.desc = d_desc;
