@@ -199,8 +199,8 @@ def _match_stream(dev):
     the other CUs' LDS and wave slots to itself."""
     import torch
     k = int(os.environ.get("ORBX_MATCH_CUSTRIDE", "0"))
-    if k <= 1:
-        return torch.cuda.Stream(device=dev)
+    if k <= 1:  # ORBX_MATCH_PRIO=-1: high-priority matcher stream (tuning knob)
+        return torch.cuda.Stream(device=dev, priority=int(os.environ.get("ORBX_MATCH_PRIO", "0")))
     import ctypes
     hip = ctypes.CDLL("libamdhip64.so")
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -318,7 +318,8 @@ def main():
         mp2 = [d_mp, torch.empty_like(d_mp)]
         nm2 = [d_nm, torch.empty_like(d_nm)]
         ms = _match_stream(dev)
-        matcher.set_footprint(True)  # leave wave slots / LDS to the concurrent extraction
+        # leave wave slots / LDS to the concurrent extraction (ORBX_MATCH_BIG=1: tuning knob)
+        matcher.set_footprint(os.environ.get("ORBX_MATCH_BIG", "0") != "1")
         ev_ex = [[torch.cuda.Event() for _ in range(S)] for _ in range(2)]  # [buffer][lane]
         ev_m = [torch.cuda.Event(), torch.cuda.Event()]
         used = [False, False]
