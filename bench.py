@@ -87,7 +87,19 @@ def stage_bytes(W, H, n_kps, nlevels=8, scale=1.2):
 # stage -> kernels of one launch of that stage (rocprofv3 kernel names)
 STAGE_KERNELS = {"pyramid": ["orbx::k_pyramid"], "score_blur": ["orbx::k_level_tiles"],
                  "fast_cells": ["orbx::k_fast_cells"], "octree": ["orbx::k_octree"],
-                 "describe": ["orbx::k_describe"], "match": ["orbx::k_seq_build", "orbx::k_proj_search<true, true>"]}
+                 "describe": ["orbx::k_describe"], "match": ["orbx::k_seq_build", "orbx::k_proj_search"]}
+
+
+def _stage_sum(ks: dict, stage: str, field: str):
+    """Sum of `field` over the kernels of `stage` (a name matches its STAGE_KERNELS entry
+    or that entry plus template arguments); None unless every entry matches one."""
+    tot = 0
+    for name in STAGE_KERNELS.get(stage, []):
+        hits = [k for k in ks if k == name or k.startswith(name + "<")]
+        if not hits:
+            return None
+        tot += sum(ks[k][field] for k in hits)
+    return tot if STAGE_KERNELS.get(stage) else None
 
 
 def newest_profiles(pattern: str):
@@ -105,10 +117,8 @@ def pmc_valu(stage: str):
     if not files:
         return None, None
     ks = json.loads(files[-1].read_text())["kernels"]
-    names = STAGE_KERNELS.get(stage, [])
-    if not names or any(k not in ks for k in names):
-        return None, files[-1].name
-    return sum(ks[k]["sq_insts_valu"] for k in names), files[-1].name
+    tot = _stage_sum(ks, stage, "sq_insts_valu")
+    return (None if tot is None else int(tot)), files[-1].name
 
 
 def pmc_traffic(stage: str):
@@ -119,11 +129,8 @@ def pmc_traffic(stage: str):
     if not files:
         return None, None
     ks = json.loads(files[-1].read_text())["kernels"]
-    names = STAGE_KERNELS.get(stage, [])
-    if not names or any(k not in ks for k in names):
-        return None, files[-1].name
-    tot = sum(ks[k]["traffic_bytes"] for k in names)
-    return int(tot), files[-1].name
+    tot = _stage_sum(ks, stage, "traffic_bytes")
+    return (None if tot is None else int(tot)), files[-1].name
 
 
 def cpu_baseline(frames_np, seconds: float, threads: int):

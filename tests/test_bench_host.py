@@ -1,0 +1,52 @@
+"""Host-side measurement logic of bench.py (no GPU): the algorithmic bytes per frame are
+SURVEY.md §8(d)'s canonical figures, level sizes follow ORBextractor.cc:1641-1643, and
+the PMC summaries under profiles/ resolve to every extraction stage's kernels."""
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+import bench  # noqa: E402
+
+
+def test_level_sizes_c1():
+    # SURVEY.md §8 table, C1
+    assert bench.level_areas(640, 480) == [(640, 480), (533, 400), (444, 333), (370, 278), (309, 231),
+                                           (257, 193), (214, 161), (179, 134)]
+
+
+def test_b_frame_matches_survey():
+    # C1, C3 (per image), C5
+    assert bench.stage_bytes(640, 480, 1000)["total"] == 3_862_128
+    assert bench.stage_bytes(1241, 376, 2000)["total"] == 5_896_388
+    assert bench.stage_bytes(640, 480, 5000, nlevels=12)["total"] == 4_269_504
+
+
+def test_score_blur_bytes_are_three_passes():
+    P = sum(w * h for w, h in bench.level_areas(640, 480))
+    assert P == 950_532
+    assert bench.stage_bytes(640, 480, 1000)["score_blur"] == 3 * P
+
+
+def test_pmc_summaries_cover_the_stages():
+    for stage in ("pyramid", "score_blur", "fast_cells", "octree", "describe", "match"):
+        t, src = bench.pmc_traffic(stage)
+        v, vsrc = bench.pmc_valu(stage)
+        assert t is not None and t > 0, (stage, src)
+        assert v is not None and v > 0, (stage, vsrc)
+
+
+def test_stage_sum_prefix_and_missing():
+    ks = {"orbx::k_seq_build": {"x": 1}, "orbx::k_proj_search<false, false, 256>": {"x": 2}}
+    assert bench._stage_sum(ks, "match", "x") == 3
+    assert bench._stage_sum(ks, "pyramid", "x") is None
+    assert bench._stage_sum({}, "no-such-stage", "x") is None
+
+
+def test_newest_profile_is_highest_tag():
+    files = bench.newest_profiles("*_pmc_traffic.json")
+    assert files, "no PMC traffic summary under profiles/"
+    data = json.loads(files[-1].read_text())
+    assert "orbx::k_level_tiles" in data["kernels"]
