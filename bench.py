@@ -1,24 +1,28 @@
 #!/usr/bin/env python3
 """bench.py -- ORB extract + match throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload tum|kitti|euroc]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Workload (BASELINE.json configs[1], 640x480, nFeatures=1000, scale 1.2, 8 levels,
 FAST 20/7): each rank holds a batch of B=256 synthetic grayscale frames in HBM -- 256
 views of one textured canvas along a random camera walk (data: synthetic).  One step =
-  1. ORBextractor::operator() on all 256 frames (orbx_extract_batch_device), and
+  1. ORBextractor::operator() on all 256 frames (orbx_extract_batch_device, two
+     128-frame lanes on two extractor streams), and
   2. TrackWithMotionModel matching of every frame against its predecessor
      (SearchByProjection(CurrentFrame, LastFrame, th=15, bMono) semantics, batched:
-     orbx_match_sequence_device),
-both enqueued on the extractor's HIP stream; inputs and outputs stay in HBM.  N>1: one
-process per GPU over RCCL, each rank its own batch (frames are independent: no
-data-path collective), "scaling": "weak".
+     orbx_match_sequence_device) on a third stream, overlapped with the next batch's
+     extraction (orbslam2commentedbyxcm_amd/pipeline.py); inputs and outputs stay in HBM.
+N>1: one process per GPU over RCCL (`--gpus N` starts the N ranks itself when no
+launcher did), each rank its own batch (frames are independent: no data-path
+collective), "scaling": "weak".  --workload kitti / euroc: configs[2] / configs[3]
+(tests/stereo_bench.py, tests/euroc_bench.py).
 
 Prints ONE JSON line on rank 0: value = frames/s of the whole job; roofline for the
 dominant kernel (HIP events on the extractor's stream; algorithmic bytes in
-DESIGN.md §Roofline); cpu_baseline = the oracle (C restatement) on this host's cores;
-parity = bit-exact check of a few frames and one matched pair against the oracle.
+DESIGN.md §5); cpu_baseline = the oracle (C restatement, -O3 -march=native) doing the
+same extract + match work on this host's cores; parity = every frame and every matched
+pair of the last batch against the oracle, plus the octree status words.
 """
 from __future__ import annotations
 
@@ -133,72 +137,99 @@ def pmc_traffic(stage: str):
     return (None if tot is None else int(tot)), files[-1].name
 
 
-def cpu_baseline(frames_np, seconds: float, threads: int):
-    """Oracle (TEST INFRASTRUCTURE) on host cores: extracted frames/s over a bounded sample."""
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(frames_np, T, sf, seconds: float, threads: int, W=640, H=480):
+    """The oracle (C restatement, TEST INFRASTRUCTURE) on this host's cores doing the same
+    work as one step's unit: extract frame i and match it against frame i-1
+    (SearchByProjection(CurrentFrame, LastFrame, th=15, bMono), ORBmatcher.cc:1620-1789),
+    built with the reference's -O3 -march=native (CMakeLists.txt:10-19).  Bounded sample:
+    a contiguous run of the bench's frames, ~seconds/3 on one thread (latency) then
+    ~seconds on `threads` threads (throughput, one chain of consecutive frames each)."""
     from concurrent.futures import ThreadPoolExecutor
 
-    from oracle import oracle as O
-    O.build()
-    p = O.params(1000, 1.2, 8, 20, 7)
-    n = len(frames_np)
-    done = [0] * threads
-    stop = time.perf_counter() + seconds
-
-    def worker(t):
-        i = t
-        while time.perf_counter() < stop:
-            O.extract(frames_np[i % n], p)
-            done[t] += 1
-            i += threads
-
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(threads) as ex:
-        list(ex.map(worker, range(threads)))
-    el = time.perf_counter() - t0
-    return sum(done) / el, sum(done), el
-
-
-def poses(off):
-    """mTcw (rows 0..2) of each view: pure translation making pixel shifts consistent at DEPTH."""
-    T = np.zeros((len(off), 12), np.float32)
-    for b in range(len(off)):
-        T[b] = [1, 0, 0, -off[b, 0] * DEPTH / FX, 0, 1, 0, -off[b, 1] * DEPTH / FY, 0, 0, 1, 0]
-    return T
-
-
-def check_parity(frames_np, T, kps_all, desc_all, n_host, mp_all, nm_all, nframes, sf):
-    """Bit-exact check of the first frames' extraction and of pair (0 -> 1)'s matches."""
+    from oracle import checks
     from oracle import oracle as O
     from orbslam2commentedbyxcm_amd.matcher import FrameView, MapPoints
-    O.build()
-    p = O.params(1000, 1.2, 8, 20, 7)
-    ok = True
-    ref = []
-    for b in range(nframes):
-        kr, dr, _ = O.extract(frames_np[b], p)
-        n = int(n_host[b])
-        kg = kps_all[b, :n].view(np.uint8).reshape(n, 28)
-        ok &= n == len(kr) and np.array_equal(kg, kr.view(np.uint8).reshape(len(kr), 28)) \
-            and np.array_equal(desc_all[b, :n], dr)
-        ref.append((kr, dr))
-    F32 = np.float32
-    (lk, ld), (ck, cd) = ref[0], ref[1]
-    Tl = T[0]
-    xc0 = (lk["x"] - F32(CX)) / F32(FX) * F32(DEPTH)
-    xc1 = (lk["y"] - F32(CY)) / F32(FY) * F32(DEPTH)
-    xc2 = np.full(len(lk), F32(DEPTH), np.float32)
-    Xw = np.stack([Tl[c] * (xc0 - Tl[3]) + Tl[4 + c] * (xc1 - Tl[7]) + Tl[8 + c] * (xc2 - Tl[11])
-                   for c in range(3)], 1).astype(np.float32)
-    mps = MapPoints(desc=ld, observations=np.ones(len(lk), np.int32), pos=Xw)
-    mk = lambda k, d, t: FrameView(keys=k, desc=d, fx=FX, fy=FY, cx=CX, cy=CY, max_x=640.0, max_y=480.0,  # noqa
-                                   scale_factors=sf, Tcw=np.vstack([t.reshape(3, 4), [0, 0, 0, 1]]).astype(np.float32))
-    cur_ref = np.full(len(ck), -1, np.int32)
-    nr = O.sbp_frame(mk(ck, cd, T[1]), cur_ref, mk(lk, ld, T[0]), np.arange(len(lk), dtype=np.int32), mps, TH,
-                     True, True)
-    ok &= int(nm_all[1]) == nr and np.array_equal(mp_all[1, :len(ck)], cur_ref)
-    return {"frames_checked": nframes, "pairs_checked": 1, "bit_exact": bool(ok), "matches_pair0": int(nr)}
 
+    flags = O.select("native")
+    try:
+        n = len(frames_np)
+        p = O.params(1000, 1.2, 8, 20, 7)
+        F32 = np.float32
 
+        def view(k, d, t):
+            return FrameView(keys=k, desc=d, fx=FX, fy=FY, cx=CX, cy=CY, max_x=float(W), max_y=float(H),
+                             scale_factors=sf, Tcw=np.vstack([t.reshape(3, 4), [0, 0, 0, 1]]).astype(np.float32))
+
+        def match(prev, cur, i):
+            (lk, ld), (ck, cd) = prev, cur
+            Tl = T[i - 1]
+            xc0 = (lk["x"] - F32(CX)) / F32(FX) * F32(DEPTH)
+            xc1 = (lk["y"] - F32(CY)) / F32(FY) * F32(DEPTH)
+            xc2 = np.full(len(lk), F32(DEPTH), np.float32)
+            Xw = np.stack([Tl[c] * (xc0 - Tl[3]) + Tl[4 + c] * (xc1 - Tl[7]) + Tl[8 + c] * (xc2 - Tl[11])
+                           for c in range(3)], 1).astype(np.float32)
+            mps = MapPoints(desc=ld, observations=np.ones(len(lk), np.int32), pos=Xw)
+            out = np.full(len(ck), -1, np.int32)
+            return O.sbp_frame(view(ck, cd, T[i]), out, view(lk, ld, Tl), np.arange(len(lk), dtype=np.int32), mps,
+                               TH, True, True)
+
+        # same sources, other flags: the baseline build must reproduce the checker exactly
+        k0, d0, _ = O.extract(frames_np[0], p)
+        k1, d1, _ = O.extract(frames_np[1], p)
+        nm_native = match((k0, d0), (k1, d1), 1)
+        O.select("parity")
+        ref = checks.extract_all(frames_np[:2], threads=1)
+        same = all(np.array_equal(a[0].view(np.uint8), b[0].view(np.uint8)) and np.array_equal(a[1], b[1])
+                   for a, b in zip(ref, [(k0, d0), (k1, d1)]))
+        same = same and nm_native == match(ref[0], ref[1], 1)
+        O.select("native")
+
+        def chain(start, stop_at, counter, idx):
+            i = start % n
+            prev = O.extract(frames_np[i], p)[:2]
+            while time.perf_counter() < stop_at:
+                i += 1
+                if i == n:  # wrap: frame 0 does not follow frame n-1, re-seed the chain
+                    i = 0
+                    prev = O.extract(frames_np[0], p)[:2]
+                    continue
+                cur = O.extract(frames_np[i], p)[:2]
+                match(prev, cur, i)
+                prev = cur
+                counter[idx] += 1
+
+        one = [0]
+        t0 = time.perf_counter()
+        chain(0, t0 + seconds / 3, one, 0)
+        el1 = time.perf_counter() - t0
+        done = [0] * threads
+        stop = time.perf_counter() + seconds
+        t1 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(lambda t: chain(t * max(1, n // threads), stop, done, t), range(threads)))
+        el = time.perf_counter() - t1
+    finally:
+        O.select("parity")
+    return {"value": round(sum(done) / el, 2), "unit": "frames/s", "cores": threads, "kind": "port",
+            "single_thread_ms_per_frame": round(el1 * 1e3 / max(one[0], 1), 3),
+            "single_thread_frames_per_s": round(one[0] / el1, 2),
+            "cpu_model": cpu_model(), "host_cpus_visible": len(os.sched_getaffinity(0)), "flags": flags,
+            "baseline_build_matches_checker": bool(same),
+            "sample": f"{sum(done)} frames in {el:.1f}s on {threads} threads (+{one[0]} in {el1:.1f}s on 1 thread), "
+                      f"each = oracle C restatement of ORBextractor::operator() + SearchByProjection(CurrentFrame, "
+                      f"LastFrame, th={TH:g}, mono) against the previous frame, over {n} consecutive bench frames; "
+                      f"scalar port built {flags} (no OpenCV / IPP SIMD)"}
 
 def _match_stream(dev):
     """The matcher's stream.  ORBX_MATCH_CUSTRIDE=k (tuning knob) restricts it to every
@@ -220,18 +251,53 @@ def _match_stream(dev):
         raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {rc}")
     return torch.cuda.ExternalStream(h.value, device=dev)
 
+
+def launch_ranks(n: int, argv) -> int:
+    """bench.py --gpus N without a launcher: start N ranks of this script as child processes
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, 127.0.0.1 rendezvous) before this
+    process touches the GPU, wait for all, return the worst exit code.  Rank 0 prints the
+    JSON line."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+def selftest_launch(args, rank, world, local_rank):
+    """--selftest-launch: the launcher path on CPU (gloo): every rank joins the group, the
+    world size is checked against --gpus, rank 0 prints one JSON line."""
+    import torch
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    try:
+        t = torch.tensor([rank + 1], dtype=torch.int64)
+        dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"selftest_launch": True, "world": dist.get_world_size(), "gpus": args.gpus,
+                              "rank_sum": int(t.item()), "local_rank0": local_rank}), flush=True)
+    finally:
+        dist.destroy_process_group()
+
+
 def main():
-    # Secondary measurements (their implementations live under tests/: they run the
-    # oracle as parity check and CPU baseline): the DBoW2 transform and the per-row table.
-    if "--vocab" in sys.argv[1:] or "--rows" in sys.argv[1:]:
-        sys.path.insert(0, str(ROOT / "tests"))
-        mode = "--vocab" if "--vocab" in sys.argv[1:] else "--rows"
-        rest = [a for a in sys.argv[1:] if a != mode]
-        if mode == "--vocab":
-            import vocab_bench
-            return vocab_bench.main(rest)
-        import row_bench
-        return row_bench.main(rest)
+    # Secondary workloads and measurements (their implementations live under tests/: they
+    # run the oracle as parity check and CPU baseline).
+    for flag, mod in (("--vocab", "vocab_bench"), ("--rows", "row_bench")):
+        if flag in sys.argv[1:]:
+            sys.path.insert(0, str(ROOT / "tests"))
+            return __import__(mod).main([a for a in sys.argv[1:] if a != flag])
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -239,27 +305,41 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--workload", default="tum", choices=["tum", "kitti", "euroc"],
+                    help="tum: configs[1] (default, the headline); kitti: configs[2] stereo; euroc: configs[3]")
     ap.add_argument("--no-match", action="store_true", help="extraction only")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, available cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--parity-frames", type=int, default=2)
+    ap.add_argument("--parity-frames", type=int, default=-1, help="-1 = every frame and pair of the last batch")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="do not overlap batch i's matching with batch i+1's extraction")
     ap.add_argument("--lanes", type=int, default=2,
-                    help="split the batch into this many contiguous chunks, each on its own extractor/matcher "
-                         "stream, so one chunk's latency-bound kernels overlap another's")
-    args = ap.parse_args()
+                    help="split the batch into this many contiguous chunks, each on its own extractor stream, so "
+                         "one chunk's latency-bound kernels overlap another's")
+    ap.add_argument("--selftest-launch", action="store_true", help=argparse.SUPPRESS)
+    args, _ = ap.parse_known_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])  # nothing here has touched the GPU
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
+    if args.selftest_launch:
+        return selftest_launch(args, rank, world, local_rank)
+    if args.workload != "tum":
+        sys.path.insert(0, str(ROOT / "tests"))
+        mod = {"kitti": "stereo_bench", "euroc": "euroc_bench"}[args.workload]
+        return __import__(mod).main([a for a in sys.argv[1:]])
+
     B, W, H = args.batch, args.width, args.height
     match = not args.no_match
-
     from orbslam2commentedbyxcm_amd import synth
+    from orbslam2commentedbyxcm_amd.pipeline import SequencePipeline, sequence_poses
     frames_np, off = synth.sequence(1000 + rank, B, W, H)
-    T = poses(off)
+    T = sequence_poses(off, FX, FY, DEPTH)
 
     import torch
     import torch.distributed as dist
@@ -269,94 +349,15 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
-    from orbslam2commentedbyxcm_amd import ORBextractor
-    from orbslam2commentedbyxcm_amd.matcher import ORBmatcher
-    S = max(1, min(args.lanes, B // 2))
-    exs = [ORBextractor(1000, 1.2, 8, 20, 7, device=local_rank) for _ in range(S)]
-    # TrackWithMotionModel, Tracking.cc:968
-    matchers = [ORBmatcher(0.9, True, device=local_rank) for _ in range(S)]
-    ex, matcher = exs[0], matchers[0]
-    sf = ex.GetScaleFactors()
-    cap = ex.max_keypoints(W, H)
+    pipeline = match and not args.no_pipeline
+    pl = SequencePipeline(B, W, H, lanes=args.lanes, pipelined=pipeline, match=match, device=local_rank,
+                          fx=FX, fy=FY, cx=CX, cy=CY, depth=DEPTH, th=TH,
+                          small_matcher=os.environ.get("ORBX_MATCH_BIG", "0") != "1",
+                          match_stream=_match_stream(dev) if match else None)
+    S = pl.S
     d_frames = torch.from_numpy(frames_np).to(dev)
     d_T = torch.from_numpy(T).to(dev)
-    d_kps = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)
-    d_desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
-    d_n = torch.empty((B,), dtype=torch.int32, device=dev)
-    d_mp = torch.empty((B, cap), dtype=torch.int32, device=dev)
-    d_nm = torch.empty((B,), dtype=torch.int32, device=dev)
-    torch.cuda.synchronize(dev)  # uploads on torch's stream finish before the extractor's stream reads them
-    # lane c extracts frames [b0, b1) on its extractor's stream and matches pairs (b-1 -> b)
-    # for b in [max(b0,1), b1); its first pair needs lane c-1's last frame (event).
-    bounds = [(B * c // S, B * (c + 1) // S) for c in range(S)]
-    streams = [torch.cuda.ExternalStream(e.stream_handle(), device=dev) for e in exs]
-    done = [torch.cuda.Event() for _ in range(S)]
-    # matches of lane c > 0 go to their own buffers (frame b0-1 is the first frame of its range)
-    lane_mp = [d_mp] + [torch.empty((b1 - b0 + 1, cap), dtype=torch.int32, device=dev) for (b0, b1) in bounds[1:]]
-    lane_nm = [d_nm] + [torch.empty((b1 - b0 + 1,), dtype=torch.int32, device=dev) for (b0, b1) in bounds[1:]]
-
-    def step():
-        for c in range(S):
-            b0, b1 = bounds[c]
-            exs[c].extract_batch_device(d_frames[b0:b1], d_kps[b0:b1], d_desc[b0:b1], d_n[b0:b1])
-            if S > 1:
-                done[c].record(streams[c])
-        if match:
-            for c in range(S):
-                b0, b1 = bounds[c]
-                lo = b0 if c == 0 else b0 - 1
-                if c > 0:
-                    streams[c].wait_event(done[c - 1])
-                out_mp = d_mp[0:b1] if c == 0 else lane_mp[c]
-                out_nm = d_nm[0:b1] if c == 0 else lane_nm[c]
-                matchers[c].match_sequence_device(d_kps[lo:b1], d_desc[lo:b1], d_n[lo:b1], d_T[lo:b1], out_mp,
-                                                  out_nm, sf, FX, FY, CX, CY, W, H, depth=DEPTH, th=TH,
-                                                  stream=exs[c].stream_handle())
-
-    # Pipelined mode (default): batch j is extracted on the extractor's stream while batch
-    # j-1 is matched on a second stream (double-buffered keypoints/descriptors), so the
-    # matcher's latency-bound replay overlaps the next extraction.  A timed run of K steps
-    # does K extractions and K matchings, pipeline fill and drain included.
-    pipeline = match and not args.no_pipeline
-    if pipeline:
-        kps2 = [d_kps, torch.empty_like(d_kps)]
-        desc2 = [d_desc, torch.empty_like(d_desc)]
-        n2 = [d_n, torch.empty_like(d_n)]
-        mp2 = [d_mp, torch.empty_like(d_mp)]
-        nm2 = [d_nm, torch.empty_like(d_nm)]
-        ms = _match_stream(dev)
-        # leave wave slots / LDS to the concurrent extraction (ORBX_MATCH_BIG=1: tuning knob)
-        matcher.set_footprint(os.environ.get("ORBX_MATCH_BIG", "0") != "1")
-        ev_ex = [[torch.cuda.Event() for _ in range(S)] for _ in range(2)]  # [buffer][lane]
-        ev_m = [torch.cuda.Event(), torch.cuda.Event()]
-        used = [False, False]
-        state = {"it": 0}
-
-        def p_extract():
-            b = state["it"] % 2
-            for c in range(S):
-                b0, b1 = bounds[c]
-                if used[b]:
-                    streams[c].wait_event(ev_m[b])  # matching of the batch that last used buffer b is done
-                exs[c].extract_batch_device(d_frames[b0:b1], kps2[b][b0:b1], desc2[b][b0:b1], n2[b][b0:b1])
-                ev_ex[b][c].record(streams[c])
-            used[b] = True
-            state["it"] += 1
-
-        def p_match(b):
-            for c in range(S):
-                ms.wait_event(ev_ex[b][c])
-            matcher.match_sequence_device(kps2[b], desc2[b], n2[b], d_T, mp2[b], nm2[b], sf, FX, FY, CX, CY, W, H,
-                                          depth=DEPTH, th=TH, stream=ms.cuda_stream)
-            ev_m[b].record(ms)
-
-        def run(k):
-            for j in range(k):
-                b_prev = (state["it"] - 1) % 2
-                p_extract()          # batch j on the extractor stream(s)
-                if j > 0:
-                    p_match(b_prev)  # batch j-1 on the matcher stream
-            p_match((state["it"] - 1) % 2)  # drain: the last batch
+    torch.cuda.synchronize(dev)  # uploads on torch's stream finish before the extractor streams read them
 
     def sync():
         torch.cuda.synchronize(dev)
@@ -365,24 +366,15 @@ def main():
         if world > 1:
             dist.barrier()
 
-    if pipeline:
-        run(max(args.warmup, 1))
-    else:
-        for _ in range(args.warmup):
-            step()
+    pl.run(d_frames, d_T, max(args.warmup, 1))
     sync()
     # Per-stage HIP events on the extractor's stream, recorded inside the timed loop
     # (a ring of event sets; read back after the loop, no synchronisation inside it).
-    ex.set_timing(True)
-    matcher.set_timing(True)
+    pl.set_timing(True)
     barrier()
     sync()
     t0 = time.perf_counter()
-    if pipeline:
-        run(args.steps)
-    else:
-        for _ in range(args.steps):
-            step()
+    pl.run(d_frames, d_T, args.steps)
     sync()
     barrier()
     sync()
@@ -394,28 +386,23 @@ def main():
     value = B * args.steps * world / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
-    if pipeline:  # results of the last batch
-        b = (state["it"] - 1) % 2
-        d_kps, d_desc, d_n, d_mp, d_nm = kps2[b], desc2[b], n2[b], mp2[b], nm2[b]
-    n_host = d_n.cpu().numpy()
+    res = pl.host_results()
+    status = pl.status()
+    n_host = res["n"]
     mean_kps = float(n_host.mean())
-    mean_matches = 0.0
-    if match:
-        nm_all = [d_nm[1:bounds[0][1]].cpu().numpy()] + [lane_nm[c][1:].cpu().numpy() for c in range(1, S)]
-        mean_matches = float(np.concatenate(nm_all).mean())
+    mean_matches = float(res["nm"][1:].mean()) if match and B > 1 else 0.0
 
-    stage_ms = ex.stage_times()
+    stage_ms = pl.exs[0].stage_times()
     if match:
-        stage_ms["match"] = matcher.last_ms()
-    ex.set_timing(False)
-    matcher.set_timing(False)
+        stage_ms["match"] = pl.matcher.last_ms()
+    pl.set_timing(False)
     bytes_pf = stage_bytes(W, H, mean_kps)
     # Dominant kernel: the longest stage on the critical path.  Pipelined, the matcher
     # runs beside the next batch's extraction on its own stream (its event time includes
     # that contention), so the extraction stages are the critical path.
     kernels = {k: v for k, v in stage_ms.items() if k != "total" and not (pipeline and k == "match")}
     dom = max(kernels, key=kernels.get)
-    Bc = bounds[0][1] - bounds[0][0]  # frames of lane 0, whose events time the stages
+    Bc = pl.bounds[0][1] - pl.bounds[0][0]  # frames of lane 0, whose events time the stages
     achieved = bytes_pf[dom] * Bc / (stage_ms[dom] * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(dom)
     valu, valu_src = pmc_valu(dom)
@@ -427,19 +414,21 @@ def main():
                  "note": "SQ_INSTS_VALU per launch / stage time; peak = 1024 SIMDs x 2.4 GHz / 2 cycles",
                  "frac_all_lanes": round(rate * S / VALU_PEAK_GIPS, 4)}
 
-    parity = None
-    if rank == 0 and args.parity_frames > 0 and match:
-        parity = check_parity(frames_np, T, d_kps.cpu().numpy(), d_desc.cpu().numpy(), n_host, d_mp.cpu().numpy(),
-                              d_nm.cpu().numpy(), max(2, args.parity_frames), sf)
+    parity = {"octree_status_clean": not bool(status.any())}
+    if rank == 0 and args.parity_frames != 0:
+        from oracle import checks
+        nchk = B if args.parity_frames < 0 else min(B, max(2, args.parity_frames))
+        sub = {k: v[:nchk] for k, v in res.items()}
+        if not match:
+            sub.pop("mp"), sub.pop("nm")
+        parity.update(checks.check_sequence(frames_np[:nchk], T[:nchk], sub, pl.sf, fx=FX, fy=FY, cx=CX, cy=CY,
+                                            W=W, H=H, depth=DEPTH, th=TH))
+        parity["bit_exact"] = parity["bit_exact"] and parity["octree_status_clean"]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        fps, nfr, el = cpu_baseline(frames_np[:32], args.cpu_seconds, threads)
-        cpu = {"value": round(fps, 2), "unit": "frames/s", "cores": threads, "kind": "port",
-               "sample": f"{nfr} synthetic 640x480 frames (32 distinct) in {el:.1f}s: oracle C restatement of "
-                         f"ORBextractor::operator() (extraction only, matching not timed), -O2 scalar, "
-                         f"{threads} threads"}
+        cpu = cpu_baseline(frames_np[:32], T[:32], pl.sf, args.cpu_seconds, threads, W, H)
 
     if rank == 0:
         out = {
@@ -484,4 +473,5 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)
+

@@ -107,6 +107,26 @@ int orbx_extract_batch_device(orbx_extractor* ex, int batch, const uint8_t* d_im
 /* The extractor's hipStream_t (as void*). */
 void* orbx_extractor_stream(orbx_extractor* ex);
 
+/* Kernel status of the last extraction (any path), per frame: 0 = complete; bit 0
+ * (ORBX_STATUS_NODE_OVERFLOW) = an octree level needed more nodes than its capacity,
+ * bit 1 (ORBX_STATUS_ITERATIONS) = an octree loop hit its iteration guard; either way
+ * that frame's keypoints are truncated and differ from the reference's DistributeOctTree
+ * (ORBextractor.cc:667-1013).  The host paths (orbx_extract, orbx_extract_batch) turn a
+ * non-zero status into ORBX_ERR_STATE; orbx_extract_batch_device returns before the
+ * kernels run, so its callers read the status here.  Synchronises with the last
+ * extraction's stream; flags (nullable) receives `batch` ints, *any their OR. */
+#define ORBX_STATUS_NODE_OVERFLOW 1
+#define ORBX_STATUS_ITERATIONS 2
+int orbx_extractor_status(orbx_extractor* ex, int batch, int* flags, int* any);
+/* The same without synchronising: the device array of per-frame status words (int32
+ * [last batch]), valid after the last extraction's stream reaches that point and until
+ * the next extraction. */
+int orbx_extractor_status_device(orbx_extractor* ex, const int32_t** d_status);
+/* Test hook: cap every level's octree node capacity at `cap` (0 = the bound the
+ * reference's algorithm guarantees, max(N+4, 4*nIni+4) per level), so that the overflow
+ * status can be exercised.  Takes effect at the next extraction. */
+int orbx_extractor_set_node_capacity(orbx_extractor* ex, int cap);
+
 /* Per-stage HIP-event timing (ms) of extraction calls, averaged over the (up to 64)
  * most recent calls made since orbx_extractor_set_timing(ex, 1), which also resets the
  * average.  Events are recorded on the launch stream between the stages, so a timed

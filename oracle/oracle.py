@@ -34,7 +34,48 @@ def build() -> Path:
     return LIB
 
 
+def build_baseline() -> Path:
+    """The portable CPU-baseline build (-O3 -march=x86-64-v3); see select("native")."""
+    subprocess.run(["make", "-s", "-C", str(HERE), "portable"], check=True)
+    return HERE / "_native" / "liborbx_oracle_v3.so"
+
+
 _lib = None
+_variant = "parity"
+
+
+def _cpu_tag() -> str:
+    """Short hash of this host's CPU model + feature flags (-march=native builds are per CPU)."""
+    import hashlib
+    try:
+        info = [ln for ln in open("/proc/cpuinfo") if ln.startswith(("model name", "flags"))][:2]
+    except OSError:
+        info = []
+    return hashlib.sha1("".join(info).encode()).hexdigest()[:12]
+
+
+def select(kind: str = "parity") -> str:
+    """Switch every oracle call of this process to a build variant of the same sources:
+    "parity" (liborbx_oracle.so, -O2, the checker) or "native" (-O3 -march=native, built
+    here on first use, falling back to the prebuilt -march=x86-64-v3 copy): the CPU
+    baseline's flags (the reference's CMakeLists.txt:10-19).  Returns the flags used."""
+    global _lib, _variant
+    if kind == "parity":
+        _lib, _variant = _load(LIB if LIB.exists() else build()), "parity"
+        return "-O2 -ffp-contract=off"
+    if kind != "native":
+        raise ValueError(kind)
+    tag = _cpu_tag()
+    native = HERE / "_native" / tag / "liborbx_oracle_native.so"
+    portable = HERE / "_native" / "liborbx_oracle_v3.so"
+    r = subprocess.run(["make", "-s", "-C", str(HERE), "native", f"NATIVE_TAG={tag}"], capture_output=True)
+    if r.returncode == 0 and native.exists():
+        _lib, _variant = _load(native), "native"
+        return "-O3 -march=native -ffp-contract=off"
+    if not portable.exists():
+        subprocess.run(["make", "-s", "-C", str(HERE), "portable"], check=True)
+    _lib, _variant = _load(portable), "native"
+    return "-O3 -march=x86-64-v3 -ffp-contract=off"
 
 
 def lib() -> C.CDLL:
@@ -42,29 +83,36 @@ def lib() -> C.CDLL:
     if _lib is None:
         if not LIB.exists():
             build()
-        _lib = C.CDLL(str(LIB))
-        u8p = C.POINTER(C.c_uint8)
-        _lib.ora_params_init.argtypes = [C.POINTER(Params), C.c_int, C.c_float, C.c_int, C.c_int, C.c_int]
-        _lib.ora_extract.argtypes = [C.POINTER(Params), u8p, C.c_int, C.c_int, C.c_size_t,
-                                     C.c_void_p, u8p, C.c_int, C.POINTER(C.c_int)]
-        _lib.ora_fast_atan2.argtypes = [C.c_float, C.c_float]
-        _lib.ora_fast_atan2.restype = C.c_float
-        _lib.ora_descriptor_distance.argtypes = [u8p, u8p]
-        _lib.ora_resize_linear_u8.argtypes = [u8p, C.c_int, C.c_int, C.c_size_t, u8p, C.c_int, C.c_int, C.c_size_t]
-        _lib.ora_gaussian_blur7_u8.argtypes = [u8p, C.c_int, C.c_int, C.c_size_t, u8p, C.c_size_t]
-        _lib.ora_fast_corner_score.argtypes = [u8p, C.c_int, C.c_int]
-        _lib.ora_fast_detect.argtypes = [u8p, C.c_int, C.c_int, C.c_size_t, C.c_int, C.c_void_p, C.c_int]
-        _lib.ora_ic_angle.argtypes = [u8p, C.c_size_t, C.c_float, C.c_float, C.POINTER(C.c_int)]
-        _lib.ora_ic_angle.restype = C.c_float
-        _lib.ora_cos_sin.argtypes = [C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
-        _lib.ora_orb_descriptor.argtypes = [u8p, C.c_size_t, C.c_float, C.c_float, C.c_float, u8p]
-        _lib.ora_distribute_octree.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
-                                               C.c_int, C.c_void_p, C.c_int]
-        _lib.ora_pyramid.argtypes = [C.POINTER(Params), u8p, C.c_int, C.c_int, C.c_size_t, C.POINTER(u8p)]
-        _lib.ora_level_candidates.argtypes = [C.POINTER(Params), u8p, C.c_int, C.c_int, C.c_void_p, C.c_int]
-        _lib.ora_level_size.argtypes = [C.POINTER(Params), C.c_int, C.c_int, C.c_int,
-                                        C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        _lib = _load(LIB)
     return _lib
+
+
+def _load(path) -> C.CDLL:
+    L = C.CDLL(str(path))
+    u8p = C.POINTER(C.c_uint8)
+    L.ora_params_init.argtypes = [C.POINTER(Params), C.c_int, C.c_float, C.c_int, C.c_int, C.c_int]
+    L.ora_extract.argtypes = [C.POINTER(Params), u8p, C.c_int, C.c_int, C.c_size_t,
+                                 C.c_void_p, u8p, C.c_int, C.POINTER(C.c_int)]
+    L.ora_fast_atan2.argtypes = [C.c_float, C.c_float]
+    L.ora_fast_atan2.restype = C.c_float
+    L.ora_descriptor_distance.argtypes = [u8p, u8p]
+    L.ora_resize_linear_u8.argtypes = [u8p, C.c_int, C.c_int, C.c_size_t, u8p, C.c_int, C.c_int, C.c_size_t]
+    L.ora_gaussian_blur7_u8.argtypes = [u8p, C.c_int, C.c_int, C.c_size_t, u8p, C.c_size_t]
+    L.ora_fast_corner_score.argtypes = [u8p, C.c_int, C.c_int]
+    L.ora_fast_detect.argtypes = [u8p, C.c_int, C.c_int, C.c_size_t, C.c_int, C.c_void_p, C.c_int]
+    L.ora_ic_angle.argtypes = [u8p, C.c_size_t, C.c_float, C.c_float, C.POINTER(C.c_int)]
+    L.ora_ic_angle.restype = C.c_float
+    L.ora_cos_sin.argtypes = [C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+    L.ora_orb_descriptor.argtypes = [u8p, C.c_size_t, C.c_float, C.c_float, C.c_float, u8p]
+    L.ora_distribute_octree.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                           C.c_int, C.c_void_p, C.c_int]
+    L.ora_pyramid.argtypes = [C.POINTER(Params), u8p, C.c_int, C.c_int, C.c_size_t, C.POINTER(u8p)]
+    L.ora_level_candidates.argtypes = [C.POINTER(Params), u8p, C.c_int, C.c_int, C.c_void_p, C.c_int]
+    L.ora_level_size.argtypes = [C.POINTER(Params), C.c_int, C.c_int, C.c_int,
+                                    C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.ora_set_trig_mode.argtypes = [C.c_int]
+    L.ora_set_trig_mode.restype = None
+    return L
 
 
 def _u8(a: np.ndarray):
@@ -88,15 +136,24 @@ def level_sizes(p: Params, width: int, height: int):
     return out
 
 
-def extract(img: np.ndarray, p: Params | None = None, cap: int = 1 << 16):
-    """ORBextractor::operator() on one u8 image -> (keypoints[n], descriptors[n,32], level_counts)."""
+def extract(img: np.ndarray, p: Params | None = None, cap: int = 1 << 16, trig_mode: int = 0):
+    """ORBextractor::operator() on one u8 image -> (keypoints[n], descriptors[n,32], level_counts).
+    trig_mode 1: rBRIEF rotation by glibc cosf / sinf (the reference's literal arithmetic,
+    hazard H3) instead of the shipped correctly rounded values."""
     p = p or params()
     img = np.ascontiguousarray(img, dtype=np.uint8)
     kps = np.zeros(cap, dtype=KEYPOINT_DTYPE)
     desc = np.zeros((cap, 32), dtype=np.uint8)
     counts = (C.c_int * MAX_LEVELS)()
-    n = lib().ora_extract(C.byref(p), _u8(img), img.shape[1], img.shape[0], img.strides[0],
+    L = lib()
+    if trig_mode:
+        L.ora_set_trig_mode(int(trig_mode))  # thread-local: this thread's next calls only
+    try:
+        n = L.ora_extract(C.byref(p), _u8(img), img.shape[1], img.shape[0], img.strides[0],
                           kps.ctypes.data, _u8(desc), cap, counts)
+    finally:
+        if trig_mode:
+            L.ora_set_trig_mode(0)
     if n < 0:
         raise RuntimeError("oracle capacity exceeded")
     return kps[:n].copy(), desc[:n].copy(), np.array(counts[:p.nlevels], dtype=np.int32)

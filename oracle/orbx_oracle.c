@@ -401,10 +401,24 @@ float ora_ic_angle(const uint8_t* img, size_t stride, float x, float y, const in
  * The reference calls std::cos(float) (glibc cosf); this restatement fixes the
  * result to the correctly rounded float value, (float)cos((double)r).  glibc 2.35's
  * cosf/sinf differ from it by one ulp on 0.26 % / 0.55 % of [0,360) degrees
- * (measured). */
+ * (measured).
+ *
+ * ora_set_trig_mode(1) switches the calling thread to the reference's literal
+ * arithmetic, cosf / sinf of the float radian (ORBextractor.cc:123-125 under `using
+ * namespace std`), so the descriptor-level effect of H3 can be counted
+ * (tests/h3_flip_count.py).  Mode 0 (default) is the shipped restatement. */
+static _Thread_local int g_trig_mode = 0;
+
+void ora_set_trig_mode(int mode) { g_trig_mode = mode; }
+
 void ora_cos_sin(float angle_deg, float* c, float* s) {
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     float r = angle_deg * factorPI;
+    if (g_trig_mode == 1) {
+        *c = cosf(r);
+        *s = sinf(r);
+        return;
+    }
     *c = (float)cos((double)r);
     *s = (float)sin((double)r);
 }

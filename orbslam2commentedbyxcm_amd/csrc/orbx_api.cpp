@@ -82,6 +82,7 @@ struct orbx_extractor {
     int d_n_cap = 0;
     int last_batch = 0;
     bool have_pyramid = false;
+    hipStream_t last_stream = nullptr;  // stream of the last extraction (status reads order after it)
 };
 
 namespace {
@@ -182,6 +183,7 @@ int run_device(orbx_extractor* ex, int batch, const uint8_t* d_imgs, size_t fram
     if (ex->timing) ex->ncalls++;
     ex->last_batch = batch;
     ex->have_pyramid = true;
+    ex->last_stream = stream;
     return ORBX_OK;
 }
 
@@ -189,7 +191,13 @@ int check_status(orbx_extractor* ex, int batch) {
     std::vector<int> st((size_t)batch);
     HIP_TRY(hipMemcpy(st.data(), ex->db.status, sizeof(int) * (size_t)batch, hipMemcpyDeviceToHost));
     for (int b = 0; b < batch; b++)
-        if (st[(size_t)b]) return fail(ORBX_ERR_STATE, "octree kernel reported an internal overflow");
+        if (st[(size_t)b]) {
+            char msg[160];
+            snprintf(msg, sizeof(msg), "octree kernel reported %s%s (frame %d): keypoints truncated",
+                     (st[(size_t)b] & kStatusNodeOverflow) ? "a node-capacity overflow" : "",
+                     (st[(size_t)b] & kStatusIterations) ? " an iteration-guard stop" : "", b);
+            return fail(ORBX_ERR_STATE, msg);
+        }
     return ORBX_OK;
 }
 
@@ -339,6 +347,41 @@ int orbx_extractor_max_keypoints(orbx_extractor* ex, int width, int height, int*
 }
 
 void* orbx_extractor_stream(orbx_extractor* ex) { return ex ? (void*)ex->stream : nullptr; }
+
+int orbx_extractor_status(orbx_extractor* ex, int batch, int* flags, int* any) {
+    if (!ex || batch < 0) return fail(ORBX_ERR_ARG, "bad argument");
+    if (!ex->have_pyramid) return fail(ORBX_ERR_STATE, "no extraction yet");
+    if (batch > ex->last_batch) return fail(ORBX_ERR_ARG, "batch exceeds the last extraction");
+    HIP_TRY(hipSetDevice(ex->device));
+    HIP_TRY(hipStreamSynchronize(ex->last_stream));
+    std::vector<int> st((size_t)(batch > 0 ? batch : 1));
+    if (batch > 0)
+        HIP_TRY(hipMemcpy(st.data(), ex->db.status, sizeof(int) * (size_t)batch, hipMemcpyDeviceToHost));
+    int a = 0;
+    for (int b = 0; b < batch; b++) a |= st[(size_t)b];
+    if (flags) std::memcpy(flags, st.data(), sizeof(int) * (size_t)batch);
+    if (any) *any = a;
+    return ORBX_OK;
+}
+
+int orbx_extractor_status_device(orbx_extractor* ex, const int32_t** d_status) {
+    if (!ex || !d_status) return fail(ORBX_ERR_ARG, "null argument");
+    if (!ex->have_pyramid) return fail(ORBX_ERR_STATE, "no extraction yet");
+    *d_status = ex->db.status;
+    return ORBX_OK;
+}
+
+int orbx_extractor_set_node_capacity(orbx_extractor* ex, int cap) {
+    if (!ex || cap < 0) return fail(ORBX_ERR_ARG, "bad argument");
+    HIP_TRY(hipSetDevice(ex->device));
+    HIP_TRY(hipStreamSynchronize(ex->stream));
+    if (ex->last_stream) HIP_TRY(hipStreamSynchronize(ex->last_stream));
+    ex->prm.node_cap_limit = cap;
+    free_buffers(ex->db);  // replanned (and reallocated) by the next extraction
+    ex->plan = Plan();
+    ex->have_pyramid = false;
+    return ORBX_OK;
+}
 
 int orbx_extractor_set_timing(orbx_extractor* ex, int enable) {
     if (!ex) return fail(ORBX_ERR_ARG, "null extractor");

@@ -264,6 +264,7 @@ bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
         g.height_rel = maxY - minY;
         int ncap = g.N + 4;
         if (4 * g.nIni + 4 > ncap) ncap = 4 * g.nIni + 4;
+        if (prm.node_cap_limit > 0 && prm.node_cap_limit < ncap) ncap = prm.node_cap_limit;
         g.ncap = ncap;
         g.out_off = out_off;
         out_off += ncap;

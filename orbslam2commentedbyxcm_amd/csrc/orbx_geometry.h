@@ -30,6 +30,10 @@ struct OrbParams {
     float scale[kMaxLevels], inv_scale[kMaxLevels], sigma2[kMaxLevels], inv_sigma2[kMaxLevels];
     int features[kMaxLevels];
     int umax[16];
+    // orbx_extractor_set_node_capacity: > 0 lowers every level's octree node capacity
+    // below the bound the reference's algorithm guarantees (max(N+4, 4 nIni+4)), which
+    // makes the kernels' overflow status observable in tests.  0 = the guaranteed bound.
+    int node_cap_limit = 0;
 };
 bool init_params(OrbParams& p, int nfeatures, float scale_factor, int nlevels, int ini, int min);
 

@@ -29,7 +29,7 @@ struct DeviceBuffers {
 };
 
 // Kernel status bits (DeviceBuffers::status)
-enum : int { kStatusNodeOverflow = 1, kStatusIterations = 2 };
+enum : int { kStatusNodeOverflow = ORBX_STATUS_NODE_OVERFLOW, kStatusIterations = ORBX_STATUS_ITERATIONS };
 
 constexpr int kStages = 6;
 extern const char* const kStageNames[kStages];

@@ -147,14 +147,18 @@ constexpr int kNumCells = kGridCols * kGridRows;
 // c = ix*FRAME_GRID_ROWS + iy holds sorted positions [cstart[c], cstart[c+1]).  The
 // cells of one grid column are contiguous, so GetFeaturesInArea's walk (ix ascending,
 // iy ascending, index ascending) is a list of contiguous runs and a candidate's sorted
-// position is its rank in the reference's iteration order.  All per-keypoint state
-// (position, octave, angle, descriptor, mvpMapPoints claim) is kept in sorted order.
+// position is its rank in the reference's iteration order.  The per-keypoint state the
+// scans read (position, octave, mvpMapPoints claim) is kept in sorted order in LDS, 20
+// bytes per keypoint plus a u16 cell table; descriptors stay in global memory unless
+// they fit too, angles are read from global memory at commit time.
 struct SortedGrid {
-    const unsigned* skey;   // (cell << 13) | index, ascending
-    const int* cstart;
-    const float4* skp;      // x, y, octave (int bits), angle
-    const uint4* sdesc;     // 2 x uint4 per keypoint, or null (descriptors read from global)
+    const unsigned* skey;     // (cell << 18) | (index << 5) | octave, ascending
+    const uint16_t* cstart;
+    const float2* sxy;        // x, y
+    const uint4* sdesc;       // 2 x uint4 per keypoint, or null (descriptors read from global)
 };
+__device__ __forceinline__ int sk_idx(unsigned k) { return (int)((k >> 5) & 0x1fffu); }
+__device__ __forceinline__ int sk_oct(unsigned k) { return (int)(k & 31u); }
 
 constexpr int kProjThreads = 1024;      // default workgroup size of k_proj_search
 constexpr int kProjThreadsSmall = 256;  // small-footprint variant (overlapped with other work)
@@ -242,8 +246,9 @@ __device__ void score_rowk(const ProjProblem& pb, const ProjParams& P, const Que
                 const int cc = (cr.x0 + c) * kGridRows;
                 const int beg = G.cstart[cc + cr.y0], end = G.cstart[cc + cr.y1 + 1];
                 for (int p = beg + sub; p < end; p += lpc) {
-                    const float4 kp = G.skp[p];
-                    const int oct = __float_as_int(kp.z);
+                    const float2 kp = G.sxy[p];
+                    const unsigned sk = G.skey[p];
+                    const int oct = sk_oct(sk);
                     if (check_levels) {
                         if (oct < Q.min_level) continue;
                         if (Q.max_level >= 0 && oct > Q.max_level) continue;
@@ -256,7 +261,7 @@ __device__ void score_rowk(const ProjProblem& pb, const ProjParams& P, const Que
                     int d;
                     if (G.sdesc) {
                         if (Q.er_max >= 0.f && pb.u_right) {
-                            const float ur = pb.u_right[G.skey[p] & 0x1fffu];
+                            const float ur = pb.u_right[sk_idx(sk)];
                             if (ur > 0 && fabsf(Q.ur - ur) > Q.er_max) continue;
                         }
                         const uint4 a = G.sdesc[2 * p], b = G.sdesc[2 * p + 1];
@@ -265,7 +270,7 @@ __device__ void score_rowk(const ProjProblem& pb, const ProjParams& P, const Que
                             __popcll(q2 ^ ((unsigned long long)b.y << 32 | b.x)) +
                             __popcll(q3 ^ ((unsigned long long)b.w << 32 | b.z));
                     } else {
-                        const int i = (int)(G.skey[p] & 0x1fffu);
+                        const int i = sk_idx(sk);
                         if (Q.er_max >= 0.f && pb.u_right) {
                             const float ur = pb.u_right[i];
                             if (ur > 0 && fabsf(Q.ur - ur) > Q.er_max) continue;
@@ -311,7 +316,7 @@ __device__ void score_rowk(const ProjProblem& pb, const ProjParams& P, const Que
 #pragma unroll
     for (int j = 0; j < kTopK; j++)
         out[j] = m[j] >= kTrunc ? m[j]
-                                : ((m[j] >> 13) << 18) | ((unsigned)__float_as_int(G.skp[m[j] & 0x1fffu].z) << 13) |
+                                : ((m[j] >> 13) << 18) | ((unsigned)sk_oct(G.skey[m[j] & 0x1fffu]) << 13) |
                                       (m[j] & 0x1fffu);
 }
 
@@ -340,12 +345,12 @@ __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~(siz
 
 // LDS layout of k_proj_search (byte offsets), shared by the kernel and its launcher.
 struct ProjLds {
-    size_t skey, cstart, skp, sfmp, owner, sdesc, qk, qmp, qang, mlist, mbin, total;
+    size_t skey, cstart, sxy, sfmp, owner, sdesc, qk, qmp, qang, mlist, mbin, total;
     __host__ __device__ ProjLds(int n, int n2, int nq, bool dlds, bool qlds) {
         skey = 0;
         cstart = align16((size_t)n2 * 4);
-        skp = align16(cstart + (size_t)(kNumCells + 1) * 4);
-        sfmp = skp + (size_t)n * 16;
+        sxy = align16(cstart + (size_t)(kNumCells + 1) * 2);
+        sfmp = sxy + (size_t)n * 8;
         owner = sfmp + (size_t)n * 4;
         size_t o = align16(owner + (size_t)n * 4);
         sdesc = o;
@@ -391,8 +396,8 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     while (n2 < n) n2 <<= 1;
     const ProjLds L(n, n2, nq, DLDS, QLDS);
     unsigned* skey = (unsigned*)(smem + L.skey);
-    int* cstart = (int*)(smem + L.cstart);
-    float4* skp = (float4*)(smem + L.skp);
+    uint16_t* cstart = (uint16_t*)(smem + L.cstart);
+    float2* sxy = (float2*)(smem + L.sxy);
     int* sfmp = (int*)(smem + L.sfmp);
     int* owner = (int*)(smem + L.owner);
     uint4* sdesc = DLDS ? (uint4*)(smem + L.sdesc) : nullptr;
@@ -420,7 +425,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
             const int px = (int)roundf((kp.x - pb.min_x) * pb.inv_w);  // Frame::PosInGrid, Frame.cc:558-567
             const int py = (int)roundf((kp.y - pb.min_y) * pb.inv_h);
             const int cell = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? kNoCell : px * kGridRows + py;
-            key = ((unsigned)cell << 13) | (unsigned)i;
+            key = ((unsigned)cell << 18) | ((unsigned)i << 5) | ((unsigned)kp.octave & 31u);
         }
         skey[i] = key;
     }
@@ -428,28 +433,28 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     __syncthreads();
     block_bitonic_sort<NT>(skey, n2);
     for (int p = tid; p < n; p += NT) {
-        const int i = (int)(skey[p] & 0x1fffu);
+        const int i = sk_idx(skey[p]);
         const orbx_keypoint& kp = pb.keys[i];
-        skp[p] = make_float4(kp.x, kp.y, __int_as_float(kp.octave), kp.angle);
+        sxy[p] = make_float2(kp.x, kp.y);
         sfmp[p] = pb.frame_mp[i];
         owner[p] = 0x7fffffff;
     }
     if (DLDS) {
         for (int t = tid; t < 2 * n; t += NT) {
-            const int i = (int)(skey[t >> 1] & 0x1fffu);
+            const int i = sk_idx(skey[t >> 1]);
             sdesc[t] = ((const uint4*)(pb.desc + (size_t)i * 32))[t & 1];
         }
     }
     // cstart[c] = first sorted position whose cell >= c (each cell written once)
     for (int p = tid; p <= n; p += NT) {
-        const int prev = p == 0 ? -1 : (int)(skey[p - 1] >> 13);
-        const int cur = p == n ? kNumCells : (int)(skey[p] >> 13);
+        const int prev = p == 0 ? -1 : (int)(skey[p - 1] >> 18);
+        const int cur = p == n ? kNumCells : (int)(skey[p] >> 18);
         const int hi = cur < kNumCells ? cur : kNumCells;
-        for (int c = prev + 1; c <= hi; c++) cstart[c] = p;
+        for (int c = prev + 1; c <= hi; c++) cstart[c] = (uint16_t)p;
     }
     __syncthreads();
     if (st && tid == 0) st[1] = wall_clock64();
-    const SortedGrid G{skey, cstart, skp, sdesc};
+    const SortedGrid G{skey, cstart, sxy, sdesc};
     {
         constexpr int kStep = kWaves * 4;
         int qb = wave * 4;
@@ -543,7 +548,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
                 nmatch += __popcll(comm);
                 if (P.check_ori) {
                     if (com) {
-                        float rot = qa - skp[tpos].w;
+                        float rot = qa - pb.keys[sk_idx(skey[tpos])].angle;
                         if (rot < 0.0f) rot += 360.0f;
                         int bin = (int)roundf(rot * factor);
                         if (bin == kHistoLength) bin = 0;
@@ -613,7 +618,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
         }
     }
     __syncthreads();
-    for (int p = tid; p < n; p += NT) pb.frame_mp[skey[p] & 0x1fffu] = sfmp[p];
+    for (int p = tid; p < n; p += NT) pb.frame_mp[sk_idx(skey[p])] = sfmp[p];
     if (st && tid == 0) st[4] = wall_clock64();
 }
 

@@ -127,6 +127,29 @@ class ORBextractor:
     def stream_handle(self) -> int:
         return L.lib().orbx_extractor_stream(self._h) or 0
 
+    # ---- kernel status of the last extraction (orbx_extractor_status)
+    STATUS_NODE_OVERFLOW = 1
+    STATUS_ITERATIONS = 2
+
+    def status(self, batch: int | None = None) -> np.ndarray:
+        """Per-frame octree status words of the last extraction (0 = complete; see
+        include/orbx.h).  Synchronises with that extraction's stream."""
+        b = self._last_batch if batch is None else int(batch)
+        flags = np.zeros(max(b, 1), dtype=np.int32)
+        anyf = C.c_int()
+        L.check(L.lib().orbx_extractor_status(self._h, b, flags.ctypes.data_as(C.POINTER(C.c_int)), C.byref(anyf)))
+        return flags[:b]
+
+    def status_device_ptr(self) -> int:
+        """Device address of the per-frame status words (int32[last batch]), no sync."""
+        p = C.c_void_p()
+        L.check(L.lib().orbx_extractor_status_device(self._h, C.byref(p)))
+        return p.value or 0
+
+    def set_node_capacity(self, cap: int) -> None:
+        """Test hook: cap the octree node capacity per level (0 = the guaranteed bound)."""
+        L.check(L.lib().orbx_extractor_set_node_capacity(self._h, int(cap)))
+
     def set_timing(self, enable: bool = True) -> None:
         L.check(L.lib().orbx_extractor_set_timing(self._h, 1 if enable else 0))
 

@@ -1,0 +1,144 @@
+"""Batched monocular front end over a device-resident frame sequence: the headline path.
+
+One step = ORBextractor::operator() on B frames (ORBextractor.cc:1513-1629) plus
+TrackWithMotionModel's SearchByProjection(CurrentFrame, LastFrame, th, bMono)
+(Tracking.cc:966-994, ORBmatcher.cc:1620-1789) of every frame against its predecessor,
+all in HBM:
+
+* the batch is split into `lanes` contiguous chunks, each extracted by its own
+  ORBextractor on its own HIP stream, so one chunk's latency-bound kernels (octree,
+  describe) overlap another's;
+* one ORBmatcher matches all B-1 pairs on a third stream once every lane is done;
+* pipelined (default): keypoint / descriptor / match buffers are double-buffered, so
+  batch j is extracted while batch j-1 is matched; the next use of a buffer waits for
+  the matching that last read it (events in both directions).  Not pipelined: the same
+  launches with a single buffer set, each step waiting for the previous step's match.
+
+bench.py times this object; tests/test_gpu_pipeline.py checks every frame and every
+pair of its output against the CPU parity oracle.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .extractor import ORBextractor
+from .matcher import ORBmatcher
+
+
+class SequencePipeline:
+    def __init__(self, batch: int, width: int, height: int, lanes: int = 2, pipelined: bool = True,
+                 match: bool = True, device: int = 0, params=(1000, 1.2, 8, 20, 7), fx: float = 500.0,
+                 fy: float = 500.0, cx: float = 320.0, cy: float = 240.0, depth: float = 5.0, th: float = 15.0,
+                 nnratio: float = 0.9, check_ori: bool = True, small_matcher: bool = True, match_stream=None):
+        import torch
+
+        self.B, self.W, self.H = int(batch), int(width), int(height)
+        self.S = max(1, min(int(lanes), self.B))
+        self.match = bool(match)
+        self.pipelined = bool(pipelined) and self.match
+        self.dev = torch.device("cuda", device)
+        self.fx, self.fy, self.cx, self.cy, self.depth, self.th = fx, fy, cx, cy, depth, th
+        self.exs = [ORBextractor(*params, device=device) for _ in range(self.S)]
+        self.matcher = ORBmatcher(nnratio, check_ori, device=device)
+        self.matcher.set_footprint(small_matcher and self.pipelined)
+        self.sf = self.exs[0].GetScaleFactors()
+        self.cap = self.exs[0].max_keypoints(self.W, self.H)
+        self.bounds = [(self.B * c // self.S, self.B * (c + 1) // self.S) for c in range(self.S)]
+        self.streams = [torch.cuda.ExternalStream(e.stream_handle(), device=self.dev) for e in self.exs]
+        self.ms = match_stream if match_stream is not None else torch.cuda.Stream(device=self.dev)
+        nbuf = 2 if self.pipelined else 1
+        B, cap = self.B, self.cap
+        i32 = dict(dtype=torch.int32, device=self.dev)
+        self.kps = [torch.empty((B, cap, 7), **i32) for _ in range(nbuf)]
+        self.desc = [torch.empty((B, cap, 32), dtype=torch.uint8, device=self.dev) for _ in range(nbuf)]
+        self.n = [torch.empty((B,), **i32) for _ in range(nbuf)]
+        self.mp = [torch.empty((B, cap), **i32) for _ in range(nbuf)]
+        self.nm = [torch.empty((B,), **i32) for _ in range(nbuf)]
+        self.ev_ex = [[torch.cuda.Event() for _ in range(self.S)] for _ in range(nbuf)]  # [buffer][lane]
+        self.ev_m = [torch.cuda.Event() for _ in range(nbuf)]
+        self.used = [False] * nbuf
+        self.it = 0            # extractions issued
+        self.pending = None    # buffer extracted but not yet matched (pipelined)
+        self.last = None       # buffer holding the newest complete result
+
+    # -- launches -----------------------------------------------------------------
+    def _extract(self, frames, b):
+        for c in range(self.S):
+            b0, b1 = self.bounds[c]
+            if self.used[b] and self.match:
+                self.streams[c].wait_event(self.ev_m[b])  # the matching that last read buffer b is done
+            self.exs[c].extract_batch_device(frames[b0:b1], self.kps[b][b0:b1], self.desc[b][b0:b1],
+                                             self.n[b][b0:b1])
+            self.ev_ex[b][c].record(self.streams[c])
+        self.used[b] = True
+
+    def _match(self, b, Tcw):
+        for c in range(self.S):
+            self.ms.wait_event(self.ev_ex[b][c])
+        self.matcher.match_sequence_device(self.kps[b], self.desc[b], self.n[b], Tcw, self.mp[b], self.nm[b],
+                                           self.sf, self.fx, self.fy, self.cx, self.cy, self.W, self.H,
+                                           depth=self.depth, th=self.th, stream=self.ms.cuda_stream)
+        self.ev_m[b].record(self.ms)
+
+    def step(self, frames, Tcw):
+        """Issue one step (asynchronous).  Pipelined: extracts this batch and matches the
+        previous one; call drain() after the last step."""
+        nbuf = len(self.kps)
+        b = self.it % nbuf
+        self._extract(frames, b)
+        self.it += 1
+        if not self.match:
+            self.last = b
+            return
+        if self.pipelined:
+            if self.pending is not None:
+                self._match(self.pending, Tcw)
+                self.last = self.pending
+            self.pending = b
+        else:
+            self._match(b, Tcw)
+            self.last = b
+
+    def drain(self, Tcw):
+        if self.pipelined and self.pending is not None:
+            self._match(self.pending, Tcw)
+            self.last = self.pending
+            self.pending = None
+
+    def run(self, frames, Tcw, k: int):
+        """k steps, pipeline fill and drain included (K extractions and K matchings)."""
+        for _ in range(k):
+            self.step(frames, Tcw)
+        self.drain(Tcw)
+
+    # -- results ------------------------------------------------------------------
+    def results(self) -> dict:
+        """Device tensors of the newest complete batch (call after synchronising)."""
+        b = self.last
+        return {"kps": self.kps[b], "desc": self.desc[b], "n": self.n[b], "mp": self.mp[b], "nm": self.nm[b]}
+
+    def host_results(self) -> dict:
+        r = self.results()
+        B, cap = self.B, self.cap
+        from . import _lib as L
+        return {"kps": r["kps"].cpu().numpy().view(np.uint8).reshape(B, cap, 28).view(L.KEYPOINT_DTYPE).reshape(B, cap),
+                "desc": r["desc"].cpu().numpy(), "n": r["n"].cpu().numpy(), "mp": r["mp"].cpu().numpy(),
+                "nm": r["nm"].cpu().numpy()}
+
+    def status(self) -> np.ndarray:
+        """Octree status words of every frame of the newest extraction (0 = complete)."""
+        return np.concatenate([e.status(b1 - b0) for e, (b0, b1) in zip(self.exs, self.bounds)])
+
+    def set_timing(self, enable: bool):
+        self.exs[0].set_timing(enable)
+        if self.match:
+            self.matcher.set_timing(enable)
+
+
+def sequence_poses(off: np.ndarray, fx: float = 500.0, fy: float = 500.0, depth: float = 5.0) -> np.ndarray:
+    """mTcw rows 0..2 of each view of synth.sequence: a pure translation that makes the
+    canvas shift `off` pixels at depth `depth`."""
+    T = np.zeros((len(off), 12), np.float32)
+    for b in range(len(off)):
+        T[b] = [1, 0, 0, -off[b, 0] * depth / fx, 0, 1, 0, -off[b, 1] * depth / fy, 0, 0, 1, 0]
+    return T

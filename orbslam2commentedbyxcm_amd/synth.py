@@ -72,9 +72,15 @@ def frames(n: int, width: int = 640, height: int = 480, first_seed: int = 0, wor
     args = [(first_seed + i, width, height) for i in range(n)]
     if workers > 1 and n > 1:
         import multiprocessing as mp
-        with mp.get_context("fork").Pool(min(workers, n)) as pool:
+        # close + join (not the context manager's terminate): workers exit on their own, so
+        # a profiler's signal handlers inherited by the fork never log a SIGTERM abort
+        pool = mp.get_context("fork").Pool(min(workers, n))
+        try:
             for i, f in enumerate(pool.imap(_frame_args, args, chunksize=4)):
                 out[i] = f
+        finally:
+            pool.close()
+            pool.join()
     else:
         for i, a in enumerate(args):
             out[i] = frame(*a)

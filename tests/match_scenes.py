@@ -13,17 +13,21 @@ CX, CY = 320.0, 240.0
 Z0 = 5.0
 
 
-def _view(O, img, T, u_right=None, bf=0.0, b=0.0):
-    p = O.params(1000, 1.2, 8, 20, 7)
+C1 = (1000, 1.2, 8, 20, 7)   # TUM-like
+C5 = (5000, 1.2, 12, 20, 7)   # configs[4]: 5000 features x 12 levels
+
+
+def _view(O, img, T, u_right=None, bf=0.0, b=0.0, prm=C1):
+    p = O.params(*prm)
     kps, desc, _ = O.extract(img, p)
-    sf = np.array(p.scale[:8], np.float32)
-    sg = np.array(p.sigma2[:8], np.float32)
+    sf = np.array(p.scale[:p.nlevels], np.float32)
+    sg = np.array(p.sigma2[:p.nlevels], np.float32)
     h, w = img.shape
     return FrameView(keys=kps, desc=desc, fx=FX, fy=FY, cx=CX, cy=CY, bf=bf, b=b, min_x=0.0, max_x=float(w),
                      min_y=0.0, max_y=float(h), scale_factors=sf, level_sigma2=sg, Tcw=T, u_right=u_right)
 
 
-def two_views(O, seed=0, dx=7, dy=-4, stereo=False):
+def two_views(O, seed=0, dx=7, dy=-4, stereo=False, prm=C1):
     a, bimg = synth.shifted_pair(seed, 640, 480, dx, dy)
     TA = np.eye(4, dtype=np.float32)
     TB = np.eye(4, dtype=np.float32)
@@ -31,8 +35,8 @@ def two_views(O, seed=0, dx=7, dy=-4, stereo=False):
     TB[1, 3] = -dy * Z0 / FY
     bf = 0.54 * FX if stereo else 0.0
     b = bf / FX if stereo else 0.0
-    A = _view(O, a, TA, bf=bf, b=b)
-    B = _view(O, bimg, TB, bf=bf, b=b)
+    A = _view(O, a, TA, bf=bf, b=b, prm=prm)
+    B = _view(O, bimg, TB, bf=bf, b=b, prm=prm)
     if stereo:
         rng = np.random.default_rng(seed + 11)
         for V in (A, B):
@@ -85,7 +89,8 @@ def local_track(A, B, mps, seed=0):
     v = (FY * yc / z + CY + rng.normal(0, 0.7, n)).astype(np.float32)
     return Track(in_view=(rng.random(n) < 0.92).astype(np.uint8), proj_x=u, proj_y=v,
                  proj_xr=(u - (B.bf / z if B.bf else 0)).astype(np.float32),
-                 scale_level=np.clip(A.keys["octave"] + rng.integers(-1, 2, n), 0, 7).astype(np.int32),
+                 scale_level=np.clip(A.keys["octave"] + rng.integers(-1, 2, n), 0,
+                                     len(A.scale_factors) - 1).astype(np.int32),
                  view_cos=rng.uniform(0.995, 1.0, n).astype(np.float32))
 
 

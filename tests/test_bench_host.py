@@ -50,3 +50,54 @@ def test_newest_profile_is_highest_tag():
     assert files, "no PMC traffic summary under profiles/"
     data = json.loads(files[-1].read_text())
     assert "orbx::k_level_tiles" in data["kernels"]
+
+
+def test_gpus_flag_launches_that_many_ranks():
+    """bench.py --gpus 2 with no launcher starts two ranks itself (the path the driver's
+    N>1 runs take when WORLD_SIZE is unset); each joins the group (gloo here)."""
+    import subprocess
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--selftest-launch"],
+                       capture_output=True, text=True, timeout=240, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, r.stdout
+    out = json.loads(line[0])
+    assert out["world"] == 2 and out["gpus"] == 2 and out["rank_sum"] == 3
+
+
+def test_gpus_flag_must_match_world_size():
+    import os
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--selftest-launch"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd="/tmp")
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_cpu_baseline_build_matches_checker(oracle):
+    """The -O3 -march=native baseline build reproduces the -O2 checker bit for bit."""
+    import numpy as np
+    from orbslam2commentedbyxcm_amd import synth
+    frames = synth.frames(2, first_seed=40)
+    p = oracle.params()
+    ref = [oracle.extract(f, p) for f in frames]
+    flags = oracle.select("native")
+    try:
+        nat = [oracle.extract(f, p) for f in frames]
+    finally:
+        oracle.select("parity")
+    assert "-O3" in flags
+    for (k0, d0, _), (k1, d1, _) in zip(ref, nat):
+        assert np.array_equal(k0.view(np.uint8), k1.view(np.uint8)) and np.array_equal(d0, d1)
+
+
+def test_h3_flip_count_runs(oracle):
+    """cosf/sinf (the reference's literal H3 arithmetic) vs the shipped correctly rounded
+    cos/sin: same keypoints; the descriptor difference is counted (profiles/r02_h3_flips.json
+    holds the 256-frame figure)."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import h3_flip_count
+    from orbslam2commentedbyxcm_amd import synth
+    r = h3_flip_count.count_flips(synth.frames(3, first_seed=90), threads=3)
+    assert r["keypoints_identical_all_frames"] and r["keypoints"] > 2000
+    assert r["descriptors_differing"] <= r["keypoints"] // 100

@@ -164,18 +164,71 @@ def test_descriptor_distance_and_windows(oracle, orbx_built):
                 assert res["second_dist"][i] == d[order[1]] and res["second_level"][i] == lv[c[order[1]]]
 
 
-@pytest.mark.parametrize("small", [False, True])
-def test_match_sequence_device(oracle, orbx_built, small):
+# ---- configs[4] sizes: 5000 features x 12 levels (k_proj_search's LDS layout at n ~ 5000)
+
+def test_c5_search_by_projection_frame(oracle, orbx_built):
+    A, B = S.two_views(oracle, 5, prm=S.C5)
+    assert len(A.keys) > 4000 and len(A.scale_factors) == 12
+    mps = S.mappoints_from(A, 5)
+    rng = np.random.default_rng(5)
+    last_mp = np.arange(len(A.keys), dtype=np.int32)
+    last_mp[rng.random(len(A.keys)) < 0.1] = -1
+    for check_ori in (True, False):
+        m = ORBmatcher(0.9, check_ori)
+        cur_gpu = np.full(len(B.keys), -1, np.int32)
+        n_gpu = m.SearchByProjectionFrame(B, cur_gpu, A, last_mp, mps, 15.0, True)
+        cur_ref = np.full(len(B.keys), -1, np.int32)
+        n_ref = oracle.sbp_frame(B, cur_ref, A, last_mp, mps, 15.0, True, check_ori)
+        assert n_gpu == n_ref and n_ref > 1000
+        assert np.array_equal(cur_gpu, cur_ref), np.nonzero(cur_gpu != cur_ref)[0][:10]
+
+
+@pytest.mark.parametrize("th,nnratio", [(1.0, 0.8), (5.0, 0.6)])
+def test_c5_search_by_projection_local(oracle, orbx_built, th, nnratio):
+    A, B = S.two_views(oracle, 6, prm=S.C5)
+    mps = S.mappoints_from(A, 6)
+    trk = S.local_track(A, B, mps, 6)
+    rng = np.random.default_rng(7)
+    queries = rng.permutation(len(A.keys)).astype(np.int32)
+    f0 = np.full(len(B.keys), -1, np.int32)
+    sel = rng.random(len(B.keys)) < 0.15
+    f0[sel] = rng.integers(0, len(A.keys), sel.sum())
+    m = ORBmatcher(nnratio, False)
+    fg = f0.copy()
+    ng = m.SearchByProjectionLocal(B, fg, queries, mps, trk, th)
+    fr = f0.copy()
+    nr = oracle.sbp_local(B, fr, queries, mps, trk, th, nnratio)
+    assert ng == nr and nr > 500
+    assert np.array_equal(fg, fr), np.nonzero(fg != fr)[0][:10]
+
+
+@pytest.mark.parametrize("stereo", [False, True])
+def test_c5_search_for_triangulation(oracle, orbx_built, stereo):
+    A, B = S.two_views(oracle, 7, stereo=stereo, prm=S.C5)
+    rng = np.random.default_rng(8)
+    has1 = (rng.random(len(A.keys)) < 0.2).astype(np.uint8)
+    has2 = (rng.random(len(B.keys)) < 0.2).astype(np.uint8)
+    fv1, fv2 = S.fv(A, nnodes=160), S.fv(B, nnodes=160)
+    F12 = S.fundamental(A, B)
+    m = ORBmatcher(0.6, False)
+    pg = m.SearchForTriangulation(A, has1, fv1, B, has2, fv2, F12, False)
+    pr = oracle.search_for_triangulation(A, has1, fv1, B, has2, fv2, F12, False, False)
+    assert np.array_equal(pg, pr), (len(pg), len(pr))
+    assert len(pr) > 100
+
+
+@pytest.mark.parametrize("small,prm", [(False, S.C1), (True, S.C1), (False, S.C5), (True, S.C5)])
+def test_match_sequence_device(oracle, orbx_built, small, prm):
     """Batched frame-to-frame matching on device-resident frames == per-pair oracle
-    (both kernel footprints: 1024 threads + LDS state, 256 threads + global state)."""
+    (both kernel footprints: 1024 threads, 256 threads; C1 and configs[4]'s 5000 x 12)."""
     import torch
 
     from orbslam2commentedbyxcm_amd.matcher import MapPoints
 
-    B = 6
+    B = 6 if prm == S.C1 else 4
     frames, off = synth.sequence(3, B)
     dev = torch.device("cuda", 0)
-    ex = ORBextractor(1000, 1.2, 8, 20, 7)
+    ex = ORBextractor(*prm)
     cap = ex.max_keypoints(640, 480)
     d_frames = torch.from_numpy(frames).to(dev)
     d_kps = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)
@@ -220,6 +273,9 @@ def test_match_sequence_device(oracle, orbx_built, small):
                         Tcw=np.vstack([T[p + 1].reshape(3, 4), [0, 0, 0, 1]]).astype(np.float32))
         ref = np.full(len(ck), -1, np.int32)
         nr = oracle.sbp_frame(cur, ref, last, np.arange(len(lk), dtype=np.int32), mps, 15.0, True, True)
+        if p == 0:
+            kr, dr, _ = oracle.extract(frames[p], oracle.params(*prm))
+            assert np.array_equal(lk.view(np.uint8), kr.view(np.uint8)) and np.array_equal(ld, dr)
         assert nm[p + 1] == nr
         assert np.array_equal(mp[p + 1][: n[p + 1]], ref)
         assert nr > 200

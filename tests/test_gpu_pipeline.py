@@ -1,0 +1,79 @@
+"""GPU parity of the headline path itself: SequencePipeline (what bench.py times) over
+device-resident batches, every frame's extraction and every pair's TrackWithMotionModel
+matches against the oracle.
+
+Covers the configurations the bench runs and their neighbours: B = 256 in two 128-frame
+lanes (nframes % 8 == 0: the XCD-swizzled grids of orbx_extract.hip's xcd_frame_block),
+pipelined (double-buffered, matching of batch j-1 beside extraction of batch j) and not;
+B = 16 in one lane; B = 8 and 12 with lanes and pipelining; plus the octree status words
+(orbx_extractor_status) on the device path, clean and forced to overflow.
+"""
+import numpy as np
+import pytest
+
+from oracle import checks
+from orbslam2commentedbyxcm_amd import OrbxError, ORBextractor, synth
+from orbslam2commentedbyxcm_amd.pipeline import SequencePipeline, sequence_poses
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(B, lanes, pipelined, steps, seed=1000):
+    import torch
+
+    frames, off = synth.sequence(seed, B)
+    T = sequence_poses(off)
+    pl = SequencePipeline(B, 640, 480, lanes=lanes, pipelined=pipelined)
+    d_frames = torch.from_numpy(frames).to(pl.dev)
+    d_T = torch.from_numpy(T).to(pl.dev)
+    torch.cuda.synchronize()
+    pl.run(d_frames, d_T, steps)
+    torch.cuda.synchronize()
+    return frames, T, pl
+
+
+@pytest.mark.parametrize("B,lanes,pipelined,steps", [(256, 2, True, 2), (16, 1, False, 1), (8, 2, True, 3),
+                                                     (12, 2, False, 2), (256, 2, False, 1)])
+def test_sequence_pipeline_matches_oracle(oracle, orbx_built, B, lanes, pipelined, steps):
+    frames, T, pl = _run(B, lanes, pipelined, steps)
+    res = pl.host_results()
+    assert not pl.status().any()
+    r = checks.check_sequence(frames, T, res, pl.sf)
+    assert r["frames_mismatched"] == 0, r
+    assert r["pairs_mismatched"] == 0, r
+    assert r["mean_matches_per_pair_ref"] > 200
+    # the lane boundary pair (last frame of lane 0 -> first frame of lane 1) is matched
+    b1 = pl.bounds[0][1]
+    if lanes > 1 and b1 < B:
+        assert res["nm"][b1] > 200
+
+
+def test_device_status_reports_forced_overflow(oracle, orbx_built):
+    """A node capacity below the algorithm's bound truncates the octree: the device path
+    returns normally but orbx_extractor_status flags every frame; the host path fails
+    with ORBX_ERR_STATE; restoring the capacity restores bit-exact output."""
+    import torch
+
+    frames, _ = synth.sequence(7, 8)
+    ex = ORBextractor(1000, 1.2, 8, 20, 7)
+    cap = ex.max_keypoints(640, 480)
+    dev = torch.device("cuda", 0)
+    d_frames = torch.from_numpy(frames).to(dev)
+    kps = torch.empty((8, cap, 7), dtype=torch.int32, device=dev)
+    desc = torch.empty((8, cap, 32), dtype=torch.uint8, device=dev)
+    n = torch.empty((8,), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    ex.extract_batch_device(d_frames, kps, desc, n)
+    assert not ex.status().any()
+    ex.set_node_capacity(40)  # below level 0's 217 + 4
+    ex.extract_batch_device(d_frames, kps, desc, n)
+    st = ex.status()
+    assert len(st) == 8 and (st & ORBextractor.STATUS_NODE_OVERFLOW).all(), st
+    with pytest.raises(OrbxError) as e:
+        ex(frames[0])
+    assert e.value.code == -5 and "overflow" in str(e.value)
+    ex.set_node_capacity(0)
+    kp, ds = ex(frames[0])
+    kr, dr, _ = oracle.extract(frames[0], oracle.params(1000, 1.2, 8, 20, 7))
+    assert np.array_equal(kp.view(np.uint8), kr.view(np.uint8)) and np.array_equal(ds, dr)
+    assert not ex.status().any()
