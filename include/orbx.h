@@ -340,8 +340,9 @@ int orbx_compute_distinctive_descriptors_device(int nmp, const int32_t* d_off, c
  * on another stream (leaves wave slots and LDS to the other kernels).  Same results. */
 int orbx_matcher_set_footprint(orbx_matcher* m, int small);
 
-/* HIP-event timing of orbx_match_sequence_device: milliseconds averaged over the (up
- * to 64) most recent calls since orbx_matcher_set_timing(m, 1). */
+/* HIP-event timing of orbx_match_sequence_device and orbx_compute_stereo_matches_batch_device:
+ * milliseconds averaged over the (up to 64) most recent calls since
+ * orbx_matcher_set_timing(m, 1). */
 int orbx_matcher_set_timing(orbx_matcher* m, int enable);
 int orbx_matcher_last_ms(orbx_matcher* m, float* ms);
 
@@ -356,15 +357,35 @@ int orbx_search_for_triangulation(orbx_matcher* m, const orbx_frame_view* kf1, c
                                   const int32_t* fv2_node, const int32_t* fv2_off, const int32_t* fv2_idx,
                                   int fv2_n, const float* F12, int only_stereo, int32_t* pairs, int* npairs);
 
-/* Frame::ComputeStereoMatches (Frame.cc:673-885) for the last orbx_extract_batch of
- * `ex` where frame `left_frame` / `right_frame` hold the left / right images and
- * keys_* / desc_* their extracted keypoints.  maxD = mbf / minZ (this fork reads mb
- * before it is set, Frame.cc:711-713; upstream's value is fx).  Writes mvuRight and
- * mvDepth (n_left floats each, -1 = no match). */
-int orbx_compute_stereo_matches(orbx_matcher* m, orbx_extractor* ex, int left_frame, int right_frame,
-                                const orbx_frame_view* left, const orbx_keypoint* keys_r,
+/* Frame::ComputeStereoMatches (Frame.cc:673-885) of one stereo Frame, as the stereo Frame
+ * constructor runs it (Frame.cc:99-178): the left image was extracted by `ex_left` (frame
+ * `left_frame` of its last extraction, mpORBextractorLeft) and the right image by
+ * `ex_right` (frame `right_frame`, mpORBextractorRight); the two may be one extractor
+ * holding both images.  The SAD refinement reads both extractors' mvImagePyramid
+ * (Frame.cc:782-818).  left: mvKeys / mDescriptors / mbf; keys_r / desc_r: mvKeysRight /
+ * mDescriptorsRight.  maxD = mbf / minZ (this fork reads mb before it is set,
+ * Frame.cc:711-713; upstream's value is fx).  Writes mvuRight and mvDepth (n_left floats
+ * each, -1 = no match), including this fork's in-loop outlier pass (Frame.cc:868-884).
+ * Host buffers; synchronous. */
+int orbx_compute_stereo_matches(orbx_matcher* m, orbx_extractor* ex_left, int left_frame, orbx_extractor* ex_right,
+                                int right_frame, const orbx_frame_view* left, const orbx_keypoint* keys_r,
                                 const uint8_t* desc_r, int n_right, float max_disparity, float* u_right,
                                 float* depth);
+
+/* The same for B stereo Frames in HBM (configs[2]): pair b's left image is frame
+ * left_frame0 + b of ex_left's last extraction with keypoints d_kps_l + b*cap
+ * (min(d_n_l[b], cap) of them, the orbx_extract_batch_device layout), its right image
+ * frame right_frame0 + b of ex_right's.  Scale factors come from the extractors.
+ * Outputs d_u_right / d_depth [B][cap] (slots past a pair's count are -1).  Enqueued on
+ * `stream` (or the matcher's) without synchronising: the caller orders it after both
+ * extractions (and before either extractor's next extraction, which overwrites the
+ * pyramids).  cap <= 8192. */
+int orbx_compute_stereo_matches_batch_device(orbx_matcher* m, orbx_extractor* ex_left, int left_frame0,
+                                             orbx_extractor* ex_right, int right_frame0, int batch,
+                                             const orbx_keypoint* d_kps_l, const uint8_t* d_desc_l,
+                                             const int32_t* d_n_l, const orbx_keypoint* d_kps_r,
+                                             const uint8_t* d_desc_r, const int32_t* d_n_r, int cap, float bf,
+                                             float max_disparity, float* d_u_right, float* d_depth, void* stream);
 
 /* ---- Frame: undistortion and grid (§8(f) rank 3) ----
  * Camera intrinsics and distortion: Frame::mK and Frame::mDistCoef [k1 k2 p1 p2 (k3)]

@@ -46,7 +46,7 @@ EXPORTED = [
     "orbx_compute_image_bounds", "orbx_assign_features_to_grid", "orbx_assign_features_to_grid_device",
     "orbx_fuse", "orbx_fuse_sim3", "orbx_search_by_sim3", "orbx_compute_distinctive_descriptors",
     "orbx_compute_distinctive_descriptors_device", "orbx_extractor_status", "orbx_extractor_status_device",
-    "orbx_extractor_set_node_capacity",
+    "orbx_extractor_set_node_capacity", "orbx_compute_stereo_matches_batch_device",
 ]
 
 
@@ -120,7 +120,9 @@ def lib() -> C.CDLL:
     L.orbx_search_by_projection_frame.argtypes = [vp, vp, i32p, vp, i32p, u8p, vp, C.c_float, C.c_int, ip]
     L.orbx_search_for_triangulation.argtypes = [vp, vp, u8p, i32p, i32p, i32p, C.c_int, vp, u8p, i32p, i32p, i32p,
                                                 C.c_int, fp, C.c_int, i32p, ip]
-    L.orbx_compute_stereo_matches.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, u8p, C.c_int, C.c_float, fp, fp]
+    L.orbx_compute_stereo_matches.argtypes = [vp, vp, C.c_int, vp, C.c_int, vp, vp, u8p, C.c_int, C.c_float, fp, fp]
+    L.orbx_compute_stereo_matches_batch_device.argtypes = [vp, vp, C.c_int, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp,
+                                                           vp, C.c_int, C.c_float, C.c_float, vp, vp, vp]
     L.orbx_match_sequence_device.argtypes = [vp, C.c_int, vp, vp, vp, C.c_int, vp, C.c_float, C.c_float, C.c_float,
                                              C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, fp, C.c_int,
                                              C.c_float, C.c_float, vp, vp, vp]

@@ -271,6 +271,29 @@ int ensure_host_staging(orbx_extractor* ex, size_t in_bytes, size_t out_slots, i
 
 }  // namespace
 
+int orbx::extractor_pyramid(orbx_extractor* ex, PyrView* v) {
+    if (!ex || !v) return fail(ORBX_ERR_ARG, "null argument");
+    if (!ex->have_pyramid) return fail(ORBX_ERR_STATE, "no extraction yet");
+    const Plan& p = ex->plan;
+    v->base = ex->db.pyr;
+    v->frame_bytes = p.pyr_frame_bytes;
+    v->nframes = ex->last_batch;
+    v->W = p.W;
+    v->H = p.H;
+    v->L = p.L;
+    for (int l = 0; l < p.L; l++) {
+        v->off[l] = p.lv[l].off;
+        v->pitch[l] = p.lv[l].pitch;
+        v->w[l] = p.lv[l].w;
+        v->h[l] = p.lv[l].h;
+        v->scale[l] = ex->prm.scale[l];
+        v->inv_scale[l] = ex->prm.inv_scale[l];
+    }
+    v->device = ex->device;
+    v->stream = ex->last_stream;
+    return ORBX_OK;
+}
+
 extern "C" {
 
 const char* orbx_version(void) { return "orbx 0.1 (gfx950)"; }

@@ -31,6 +31,22 @@ struct DeviceBuffers {
 // Kernel status bits (DeviceBuffers::status)
 enum : int { kStatusNodeOverflow = ORBX_STATUS_NODE_OVERFLOW, kStatusIterations = ORBX_STATUS_ITERATIONS };
 
+// The pyramid an extractor kept from its last extraction (mvImagePyramid, ORBextractor.h:162):
+// frame f's level l ROI starts at base + f * frame_bytes + off[l], rows pitch[l] bytes apart.
+struct PyrView {
+    const uint8_t* base = nullptr;
+    long long frame_bytes = 0;
+    int nframes = 0;           // frames of the last extraction
+    int W = 0, H = 0, L = 0;
+    long long off[kMaxLevels];
+    int pitch[kMaxLevels], w[kMaxLevels], h[kMaxLevels];
+    float scale[kMaxLevels], inv_scale[kMaxLevels];
+    int device = 0;
+    hipStream_t stream = nullptr;  // stream of the last extraction
+};
+// Fills `v` for extractor `ex` (ORBX_ERR_STATE before any extraction).
+int extractor_pyramid(orbx_extractor* ex, PyrView* v);
+
 constexpr int kStages = 6;
 extern const char* const kStageNames[kStages];
 
@@ -58,7 +74,7 @@ hipError_t launch_seq_build(const SeqArgs& A, int npairs, ProjQuery* queries, Pr
 hipError_t launch_triangulation(const TriProblem* d_probs, int nprob, unsigned long long* scratch, int max_n2,
                                 int max_nq, hipStream_t stream);
 
-hipError_t launch_stereo(const StereoProblem& pb, StereoResult* out, hipStream_t stream);
+hipError_t launch_stereo(const StereoBatch& sb, int batch, hipStream_t stream);
 hipError_t launch_bow(const BowProblem* d_prob, int n2, int nitems, hipStream_t stream);
 hipError_t launch_init(const InitProblem* d_prob, int n1, int n2, int nq, hipStream_t stream);
 hipError_t launch_window_best(const BestProblem* d_prob, int nq, hipStream_t stream);

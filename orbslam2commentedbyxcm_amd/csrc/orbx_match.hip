@@ -9,6 +9,7 @@
 // `dist < bestDist` / `else if (dist < bestDist2)` updates exactly.
 #include <hip/hip_runtime.h>
 
+#include "orbx_block_sort.h"
 #include "orbx_kernels.h"
 
 namespace orbx {
@@ -904,43 +905,129 @@ hipError_t launch_triangulation(const TriProblem* d_probs, int nprob, unsigned l
 
 // ------------------------------------------------------------------ stereo
 
-// One wave per left keypoint: Frame::ComputeStereoMatches' row-band Hamming search,
-// 11x11 SAD refinement on the pyramid level over shifts -5..5 and the parabola fit
-// (Frame.cc:724-866).  The per-keypoint results feed the host's sequential outlier
-// pass (Frame.cc:868-884).
-__global__ __launch_bounds__(256) void k_stereo(StereoProblem pb, StereoResult* __restrict__ out) {
+// Frame::ComputeStereoMatches (Frame.cc:673-885) for B left/right pairs, three launches:
+//   k_stereo_rows     vRowIndices (cc:693-708) of each pair as a CSR over image rows;
+//   k_stereo          one wave per left keypoint: row-band Hamming search, 11x11 SAD over
+//                     shifts -5..5 on the pyramid level, parabola fit (cc:720-866);
+//   k_stereo_outlier  this fork's outlier pass, which sits inside the iL loop
+//                     (cc:868-884, hazard H8): after every iteration that reaches it,
+//                     vDistIdx is sorted and entries with dist >= 1.5*1.4*median are
+//                     invalidated.
+// The row lists hold right keypoints in any order: the search keeps the smallest
+// (distance, iR), which is the reference's first-wins `dist < bestDist` over its
+// ascending-iR lists.
+
+// Exclusive prefix sum of a[0, n) in place by one workgroup of NT threads (tmp: NT ints
+// of LDS); returns the total.  Must be called by all NT threads.
+template <int NT>
+__device__ int block_exscan_inplace(int* a, int n, int* tmp) {
+    const int t = threadIdx.x;
+    const int seg = (n + NT - 1) / NT;
+    const int b = t * seg, e = min(n, b + seg);
+    int sum = 0;
+    for (int i = b; i < e; i++) sum += a[i];
+    tmp[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < NT; o <<= 1) {
+        const int v = t >= o ? tmp[t - o] : 0;
+        __syncthreads();
+        tmp[t] += v;
+        __syncthreads();
+    }
+    int run = tmp[t] - sum;  // exclusive prefix of this thread's segment
+    const int total = tmp[NT - 1];
+    for (int i = b; i < e; i++) {
+        const int v = a[i];
+        a[i] = run;
+        run += v;
+    }
+    __syncthreads();
+    return total;
+}
+
+constexpr int kStereoRowThreads = 1024;
+
+__global__ __launch_bounds__(kStereoRowThreads) void k_stereo_rows(StereoBatch sb) {
+    extern __shared__ __align__(16) int s_rows[];  // cnt [rows + 1], then cursors [rows]
+    __shared__ int s_tmp[kStereoRowThreads];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int rows = sb.rows;
+    int* cnt = s_rows;
+    int* cur = s_rows + rows + 1;
+    const int nr = min(sb.n_r[b], sb.cap);
+    const orbx_keypoint* kr = sb.keys_r + (size_t)b * sb.cap;
+    for (int y = tid; y <= rows; y += kStereoRowThreads) cnt[y] = 0;
+    __syncthreads();
+    // a right keypoint covers rows floor(y - r) .. ceil(y + r), r = 2 * scale[octave]
+    // (cc:695-707; rows outside the image, which keypoints >= 16 px inside never reach,
+    // are dropped)
+    for (int iR = tid; iR < nr; iR += kStereoRowThreads) {
+        const orbx_keypoint kp = kr[iR];
+        const float r = 2.0f * sb.scale[kp.octave];
+        const int maxr = (int)ceilf(kp.y + r), minr = (int)floorf(kp.y - r);
+        for (int yi = max(minr, 0); yi <= min(maxr, rows - 1); yi++) atomicAdd(&cnt[yi], 1);
+    }
+    __syncthreads();
+    const int total = block_exscan_inplace<kStereoRowThreads>(cnt, rows, s_tmp);
+    for (int y = tid; y < rows; y += kStereoRowThreads) cur[y] = cnt[y];
+    if (tid == 0) cnt[rows] = total;
+    __syncthreads();
+    int32_t* off = sb.row_off + (size_t)b * (rows + 1);
+    for (int y = tid; y <= rows; y += kStereoRowThreads) off[y] = cnt[y];
+    int32_t* idx = sb.row_idx + (size_t)b * sb.band_cap;
+    for (int iR = tid; iR < nr; iR += kStereoRowThreads) {
+        const orbx_keypoint kp = kr[iR];
+        const float r = 2.0f * sb.scale[kp.octave];
+        const int maxr = (int)ceilf(kp.y + r), minr = (int)floorf(kp.y - r);
+        for (int yi = max(minr, 0); yi <= min(maxr, rows - 1); yi++) {
+            const int pos = atomicAdd(&cur[yi], 1);
+            if (pos < sb.band_cap) idx[pos] = iR;
+        }
+    }
+}
+
+// One wave per left keypoint of pair blockIdx.y.
+__global__ __launch_bounds__(256) void k_stereo(StereoBatch sb) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int b = blockIdx.y;
     const int iL = blockIdx.x * 4 + wave;
-    if (iL >= pb.nl) return;
+    const int nl = min(sb.n_l[b], sb.cap);
+    if (iL >= nl) return;
     StereoResult res;
     res.reach_sort = 0;
     res.pushed = 0;
     res.dist = 0;
     res.u_right = -1.f;
     res.depth = -1.f;
-    const orbx_keypoint kpL = pb.keys_l[iL];
+    StereoResult* out = sb.res + (size_t)b * sb.cap + iL;
+    const orbx_keypoint kpL = sb.keys_l[(size_t)b * sb.cap + iL];
     const int levelL = kpL.octave;
     const float vL = kpL.y, uL = kpL.x;
     const int row = (int)vL;
-    const int cbeg = pb.row_off[row], cend = pb.row_off[row + 1];
+    const int32_t* roff = sb.row_off + (size_t)b * (sb.rows + 1);
+    const int cbeg = row >= 0 && row < sb.rows ? roff[row] : 0;
+    const int cend = row >= 0 && row < sb.rows ? min(roff[row + 1], sb.band_cap) : 0;
     const float minD = 0.f;
-    if (cend == cbeg || uL - minD < 0) {
-        if (lane == 0) out[iL] = res;
+    if (cend == cbeg || uL - minD < 0) {  // cc:727-735
+        if (lane == 0) *out = res;
         return;
     }
-    const float minU = uL - pb.max_d, maxU = uL - minD;
-    const unsigned long long* dl = (const unsigned long long*)(pb.desc_l + (size_t)iL * 32);
+    const float minU = uL - sb.max_d, maxU = uL - minD;
+    const int32_t* ridx = sb.row_idx + (size_t)b * sb.band_cap;
+    const orbx_keypoint* kr = sb.keys_r + (size_t)b * sb.cap;
+    const uint8_t* dr = sb.desc_r + (size_t)b * sb.cap * 32;
+    const unsigned long long* dl = (const unsigned long long*)(sb.desc_l + ((size_t)b * sb.cap + iL) * 32);
     const unsigned long long q0 = dl[0], q1 = dl[1], q2 = dl[2], q3 = dl[3];
     unsigned long long best = kNoKey;
     for (int p = cbeg + lane; p < cend; p += 64) {
-        const int iR = pb.row_idx[p];
-        const orbx_keypoint kpR = pb.keys_r[iR];
+        const int iR = ridx[p];
+        const orbx_keypoint kpR = kr[iR];
         if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
         const float uR = kpR.x;
         if (uR >= minU && uR <= maxU) {
-            const unsigned long long* t = (const unsigned long long*)(pb.desc_r + (size_t)iR * 32);
+            const unsigned long long* t = (const unsigned long long*)(dr + (size_t)iR * 32);
             const int d = __popcll(q0 ^ t[0]) + __popcll(q1 ^ t[1]) + __popcll(q2 ^ t[2]) + __popcll(q3 ^ t[3]);
-            const unsigned long long key = ((unsigned long long)d << 32) | (unsigned)(p - cbeg);
+            const unsigned long long key = ((unsigned long long)d << 32) | (unsigned)iR;
             best = key < best ? key : best;
         }
     }
@@ -952,23 +1039,23 @@ __global__ __launch_bounds__(256) void k_stereo(StereoProblem pb, StereoResult* 
     res.reach_sort = 1;
     const int bestDist = best == kNoKey ? 100 : (int)(best >> 32);  // starts at TH_HIGH, strict <
     if (bestDist < 75) {                                             // thOrbDist = (TH_HIGH + TH_LOW) / 2
-        const int bestIdxR = pb.row_idx[cbeg + (int)(best & 0xffffffffu)];
-        const float uR0 = pb.keys_r[bestIdxR].x;
-        const float scaleFactor = pb.inv_scale[levelL];
+        const int bestIdxR = (int)(best & 0xffffffffu);
+        const float uR0 = kr[bestIdxR].x;
+        const float scaleFactor = sb.inv_scale[levelL];
         const float scaleduL = roundf(kpL.x * scaleFactor);
         const float scaledvL = roundf(kpL.y * scaleFactor);
         const float scaleduR0 = roundf(uR0 * scaleFactor);
         const int w = 5, L = 5;
         const float iniu = scaleduR0 + L - w;
         const float endu = scaleduR0 + L + w + 1;
-        if (iniu < 0 || endu >= pb.level_w[levelL]) {
+        if (iniu < 0 || endu >= sb.level_w[levelL]) {  // cc:810-811
             res.reach_sort = 0;
-            if (lane == 0) out[iL] = res;
+            if (lane == 0) *out = res;
             return;
         }
-        const int pitch = pb.level_pitch[levelL];
-        const uint8_t* IL = pb.lev_l[levelL];
-        const uint8_t* IR = pb.lev_r[levelL];
+        const int pitch = sb.level_pitch[levelL];
+        const uint8_t* IL = sb.pyr_l + (size_t)b * sb.fb_l + sb.level_off[levelL];
+        const uint8_t* IR = sb.pyr_r + (size_t)b * sb.fb_r + sb.level_off[levelL];
         const int yl0 = (int)scaledvL - w, xl0 = (int)scaleduL - w;
         const int cl = IL[(size_t)(yl0 + w) * pitch + xl0 + w];
         float vd[11];
@@ -981,8 +1068,8 @@ __global__ __launch_bounds__(256) void k_stereo(StereoProblem pb, StereoResult* 
             for (int k = lane; k < 121; k += 64) {
                 const int yy = k / 11, xx = k - yy * 11;
                 const int a = (int)IL[(size_t)(yl0 + yy) * pitch + xl0 + xx] - cl;
-                const int b = (int)IR[(size_t)(yl0 + yy) * pitch + xr0 + xx] - cr;
-                acc += a > b ? a - b : b - a;
+                const int c = (int)IR[(size_t)(yl0 + yy) * pitch + xr0 + xx] - cr;
+                acc += a > c ? a - c : c - a;
             }
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
@@ -993,9 +1080,9 @@ __global__ __launch_bounds__(256) void k_stereo(StereoProblem pb, StereoResult* 
             }
             vd[L + incR] = dist;
         }
-        if (bestincR == -L || bestincR == L) {
+        if (bestincR == -L || bestincR == L) {  // cc:834-835
             res.reach_sort = 0;
-            if (lane == 0) out[iL] = res;
+            if (lane == 0) *out = res;
             return;
         }
         float dist1 = vd[0], dist2 = vd[0], dist3 = vd[0];
@@ -1006,30 +1093,223 @@ __global__ __launch_bounds__(256) void k_stereo(StereoProblem pb, StereoResult* 
             if (k == L + bestincR + 1) dist3 = vd[k];
         }
         const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
-        if (deltaR < -1 || deltaR > 1) {
+        if (deltaR < -1 || deltaR > 1) {  // cc:845-846
             res.reach_sort = 0;
-            if (lane == 0) out[iL] = res;
+            if (lane == 0) *out = res;
             return;
         }
-        float bestuR = pb.scale[levelL] * (scaleduR0 + (float)bestincR + deltaR);
+        float bestuR = sb.scale[levelL] * (scaleduR0 + (float)bestincR + deltaR);
         float disparity = (uL - bestuR);
-        if (disparity >= minD && disparity < pb.max_d) {
+        if (disparity >= minD && disparity < sb.max_d) {
             if (disparity <= 0) {
                 disparity = 0.01f;
                 bestuR = (float)((double)uL - 0.01);
             }
-            res.depth = pb.bf / disparity;
+            res.depth = sb.bf / disparity;
             res.u_right = bestuR;
             res.pushed = 1;
             res.dist = bestDistS;
         }
     }
-    if (lane == 0) out[iL] = res;
+    if (lane == 0) *out = res;
 }
 
-hipError_t launch_stereo(const StereoProblem& pb, StereoResult* out, hipStream_t stream) {
-    if (pb.nl <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_stereo, dim3((pb.nl + 3) / 4), dim3(256), 0, stream, pb, out);
+// The in-loop outlier pass (cc:868-884) of one pair per 1024-thread workgroup.
+//
+// The pass at iteration t marks every pushed entry whose dist >= thDist_t = 1.5f * 1.4f *
+// median_t, where median_t is the (s_t / 2)-th smallest dist of the s_t entries pushed
+// so far (vDistIdx sorted by (dist, iL)); a marked entry stays -1.  So entry j ends
+// invalid iff (float)dist_j >= min over reaching iterations t >= j of thDist_t.
+//   1. the pushed (dist, iL) keys are block-sorted: an entry's rank is its position in
+//      the reference's sorted vDistIdx at the end of the loop;
+//   2. the iterations are cut into 16 chunks, one per wave.  A wave sets the rank bits
+//      of the entries pushed before its chunk, finds their (s/2)-th rank, and walks its
+//      chunk in order: each push moves the median rank by at most one present rank
+//      (nearest set bit), so every reaching iteration's median costs O(1);
+//   3. a suffix minimum of thDist over the iterations, then one comparison per entry.
+// An empty vDistIdx at a reaching iteration (the reference reads vDistIdx[0] of an
+// empty vector there) marks nothing.
+constexpr int kStereoOutThreads = 1024;
+constexpr int kStereoOutWaves = kStereoOutThreads / 64;
+
+__global__ __launch_bounds__(kStereoOutThreads) void k_stereo_outlier(StereoBatch sb, int n2) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ float s_seg[kStereoOutThreads];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int N = min(sb.n_l[b], sb.cap);
+    const StereoResult* R = sb.res + (size_t)b * sb.cap;
+    unsigned long long* skey = (unsigned long long*)smem;                   // n2 (sort)
+    uint16_t* rank = (uint16_t*)(smem + (size_t)8 * n2);                      // n2
+    uint8_t* flag = (uint8_t*)(smem + (size_t)10 * n2);                       // n2: 1 pushed, 2 reaches the pass
+    unsigned long long* bits = (unsigned long long*)(smem + (size_t)11 * n2); // per wave n2 / 64 words
+    const int nw = n2 >> 6;
+    // 1. sort the pushed entries by (dist, iL)
+    const int ne = n2 / kSortThreads;
+    unsigned long long r[kSortPer];
+#pragma unroll
+    for (int e = 0; e < kSortPer; e++) {
+        r[e] = ~0ull;
+        const int i = e * kSortThreads + tid;
+        if (e < ne && i < N) {
+            const StereoResult x = R[i];
+            flag[i] = (uint8_t)((x.pushed ? 1 : 0) | (x.reach_sort ? 2 : 0));
+            if (x.pushed) r[e] = ((unsigned long long)(unsigned)x.dist << 32) | (unsigned)i;
+        }
+    }
+    block_bitonic_sort64(r, ne, skey);
+    for (int m = tid; m < n2; m += kStereoOutThreads) {
+        const unsigned long long k = skey[m];
+        if (k != ~0ull) rank[(int)(k & 0xffffffffu)] = (uint16_t)m;
+    }
+    // sorted dist values (u32) over the first half of the sort buffer, thresholds over the second
+    unsigned dv[kSortPer];
+#pragma unroll
+    for (int e = 0; e < kSortPer; e++)
+        if (e < ne) dv[e] = (unsigned)(skey[e * kSortThreads + tid] >> 32);
+    __syncthreads();
+    unsigned* sdist = (unsigned*)smem;
+    float* thr = (float*)(smem + (size_t)4 * n2);
+#pragma unroll
+    for (int e = 0; e < kSortPer; e++)
+        if (e < ne) sdist[e * kSortThreads + tid] = dv[e];
+    unsigned long long* W = bits + (size_t)wave * nw;
+    for (int w = lane; w < nw; w += 64) W[w] = 0ull;
+    __syncthreads();
+    // 2. per-wave chunk walk
+    const int chunk = (N + kStereoOutWaves - 1) / kStereoOutWaves;
+    const int t0 = min(N, wave * chunk), t1 = min(N, t0 + chunk);
+    for (int j = lane; j < t0; j += 64)
+        if (flag[j] & 1) atomicOr(&W[rank[j] >> 6], 1ull << (rank[j] & 63));
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    // s = entries pushed before t0; m = rank of the (s / 2)-th of them (order statistic)
+    int s = 0;
+    for (int w = lane; w < nw; w += 64) s += __popcll(W[w]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    int m = -1;
+    if (s > 0) {
+        const int k = s >> 1;
+        int base = 0;
+        for (int w0 = 0; w0 < nw; w0 += 64) {
+            const unsigned long long word = w0 + lane < nw ? W[w0 + lane] : 0ull;
+            const int c = __popcll(word);
+            int incl = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(incl, o);
+                if (lane >= o) incl += v;
+            }
+            const unsigned long long hit = __ballot(base + incl > k);
+            if (hit) {
+                const int src = __ffsll((long long)hit) - 1;
+                if (lane == src) {
+                    int need = k - (base + incl - c);  // set bits of this word to skip
+                    unsigned long long x = word;
+                    while (need-- > 0) x &= x - 1;
+                    m = (w0 + lane) * 64 + __ffsll((long long)x) - 1;
+                }
+                m = __shfl(m, src);
+                break;
+            }
+            base += __shfl(incl, 63);
+        }
+    }
+    if (lane == 0) {
+        int kc = s > 0 ? (s >> 1) : 0;
+        for (int t = t0; t < t1; t++) {
+            const int f = flag[t];
+            if (f & 1) {
+                const int rt = rank[t];
+                W[rt >> 6] |= 1ull << (rt & 63);
+                s++;
+                if (s == 1) {
+                    m = rt;
+                    kc = 0;
+                } else {
+                    if (rt < m) kc++;
+                    const int k = s >> 1;
+                    if (kc < k) {  // next present rank above m
+                        int w = m >> 6;
+                        unsigned long long x = (m & 63) == 63 ? 0ull : (W[w] & (~0ull << ((m & 63) + 1)));
+                        while (!x) x = W[++w];
+                        m = w * 64 + __ffsll((long long)x) - 1;
+                        kc++;
+                    } else if (kc > k) {  // previous present rank below m
+                        int w = m >> 6;
+                        unsigned long long x = W[w] & ((1ull << (m & 63)) - 1);
+                        while (!x) x = W[--w];
+                        m = w * 64 + 63 - __clzll((long long)x);
+                        kc--;
+                    }
+                }
+            }
+            thr[t] = ((f & 2) && s > 0) ? 1.5f * 1.4f * (float)sdist[m] : __int_as_float(0x7f800000);
+        }
+    }
+    __syncthreads();
+    // 3. suffix minimum over t, then the marks
+    const int seg = (N + kStereoOutThreads - 1) / kStereoOutThreads;
+    const int a = tid * seg, e = min(N, a + seg);
+    float mn = __int_as_float(0x7f800000);
+    for (int i = e - 1; i >= a; i--) {
+        mn = fminf(mn, thr[i]);
+        thr[i] = mn;
+    }
+    s_seg[tid] = mn;
+    __syncthreads();
+    for (int o = 1; o < kStereoOutThreads; o <<= 1) {
+        const float v = tid + o < kStereoOutThreads ? s_seg[tid + o] : __int_as_float(0x7f800000);
+        __syncthreads();
+        s_seg[tid] = fminf(s_seg[tid], v);
+        __syncthreads();
+    }
+    float* ur = sb.u_right + (size_t)b * sb.cap;
+    float* dp = sb.depth + (size_t)b * sb.cap;
+    for (int i = tid; i < sb.cap; i += kStereoOutThreads) {
+        float u = -1.f, d = -1.f;
+        if (i < N && (flag[i] & 1)) {
+            const int q = i / seg;
+            const float after = q + 1 < kStereoOutThreads ? s_seg[q + 1] : __int_as_float(0x7f800000);
+            const float th = fminf(thr[i], after);
+            const StereoResult x = R[i];
+            if ((float)x.dist < th) {
+                u = x.u_right;
+                d = x.depth;
+            }
+        }
+        ur[i] = u;
+        dp[i] = d;
+    }
+}
+
+size_t stereo_outlier_lds(int cap) {
+    int n2 = kSortThreads;
+    while (n2 < cap) n2 <<= 1;
+    return (size_t)13 * n2;
+}
+
+hipError_t launch_stereo(const StereoBatch& sb, int batch, hipStream_t stream) {
+    if (batch <= 0) return hipSuccess;
+    if (sb.cap > kSortMaxKeys || sb.rows <= 0) return hipErrorInvalidValue;
+    const size_t rows_lds = (size_t)(2 * sb.rows + 1) * 4;
+    if (rows_lds > 150 * 1024) return hipErrorInvalidValue;
+    if (rows_lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_stereo_rows, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)rows_lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_stereo_rows, dim3(batch), dim3(kStereoRowThreads), rows_lds, stream, sb);
+    hipLaunchKernelGGL(k_stereo, dim3((sb.cap + 3) / 4, batch), dim3(256), 0, stream, sb);
+    int n2 = kSortThreads;
+    while (n2 < sb.cap) n2 <<= 1;
+    const size_t lds = stereo_outlier_lds(sb.cap);
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_stereo_outlier, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_stereo_outlier, dim3(batch), dim3(kStereoOutThreads), lds, stream, sb, n2);
     return hipGetLastError();
 }
 

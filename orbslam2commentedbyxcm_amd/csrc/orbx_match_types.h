@@ -171,24 +171,6 @@ struct BestProblem {
     int32_t* best;              // out [nq]: keypoint index or -1
 };
 
-struct StereoProblem {
-    const orbx_keypoint* keys_l;
-    const uint8_t* desc_l;
-    int nl;
-    const orbx_keypoint* keys_r;
-    const uint8_t* desc_r;
-    const int32_t* row_off;     // vRowIndices as CSR over image rows
-    const int32_t* row_idx;
-    const uint8_t* lev_l[32];   // mvImagePyramid ROIs of the left / right extractor
-    const uint8_t* lev_r[32];
-    int level_pitch[32];
-    int level_w[32];
-    float scale[32];            // mvScaleFactors
-    float inv_scale[32];        // mvInvScaleFactors
-    float bf;                   // mbf
-    float max_d;                // maxD = mbf / minZ
-};
-
 struct StereoResult {
     int reach_sort;  // the iteration reaches the in-loop outlier pass (no `continue`)
     int pushed;      // (dist, iL) was appended to vDistIdx
@@ -196,5 +178,37 @@ struct StereoResult {
     float u_right;
     float depth;
 };
+
+// Frame::ComputeStereoMatches (Frame.cc:673-885) over B left/right pairs: pair b's left
+// keypoints keys_l[b*cap ...] (min(n_l[b], cap) of them), right keypoints keys_r[b*cap
+// ...], pyramid levels of the left / right extractor at pyr_l + b*fb_l / pyr_r + b*fb_r.
+struct StereoBatch {
+    const orbx_keypoint* keys_l;  // mvKeys
+    const uint8_t* desc_l;        // mDescriptors
+    const int32_t* n_l;
+    const orbx_keypoint* keys_r;  // mvKeysRight
+    const uint8_t* desc_r;        // mDescriptorsRight
+    const int32_t* n_r;
+    int cap;                      // keypoint slots per frame
+    int rows;                     // vRowIndices size: mvImagePyramid[0].rows
+    int band_cap;                 // row_idx slots per pair
+    int32_t* row_off;             // [B][rows + 1]  vRowIndices as CSR over image rows
+    int32_t* row_idx;             // [B][band_cap]
+    const uint8_t* pyr_l;         // mvImagePyramid ROIs of the left / right extractor
+    const uint8_t* pyr_r;
+    long long fb_l, fb_r;         // pyramid bytes per frame
+    long long level_off[32];      // level l of a frame block at + level_off[l], rows level_pitch[l] apart
+    int level_pitch[32];
+    int level_w[32];
+    float scale[32];              // mvScaleFactors
+    float inv_scale[32];          // mvInvScaleFactors
+    float bf;                     // mbf
+    float max_d;                  // maxD = mbf / minZ
+    StereoResult* res;            // [B][cap] per-keypoint results before the outlier pass
+    float* u_right;               // [B][cap] out: mvuRight (-1 = none; slots >= n_l[b] too)
+    float* depth;                 // [B][cap] out: mvDepth
+};
+
+
 
 }  // namespace orbx

@@ -155,6 +155,9 @@ struct orbx_matcher {
     hipEvent_t ev[kRing][2] = {};
     long long ncalls = 0;
     bool small = false;  // orbx_matcher_set_footprint
+    // device-only scratch of the batched device calls (no pinned mirror)
+    char* dscr = nullptr;
+    size_t dscr_cap = 0;
 };
 
 namespace {
@@ -253,6 +256,7 @@ void orbx_matcher_destroy(orbx_matcher* m) {
     (void)hipSetDevice(m->device);
     if (m->stream) (void)hipStreamSynchronize(m->stream);
     m->arena.release();
+    if (m->dscr) (void)hipFree(m->dscr);
     for (auto& slot : m->ev)
         for (auto& e : slot)
             if (e) (void)hipEventDestroy(e);
@@ -1290,11 +1294,51 @@ int orbx_compute_distinctive_descriptors(int device, int nmp, const int32_t* off
     return ORBX_OK;
 }
 
-// Frame::ComputeStereoMatches, Frame.cc:673-885
-int orbx_compute_stereo_matches(orbx_matcher* m, orbx_extractor* ex, int left_frame, int right_frame,
-                                const orbx_frame_view* left, const orbx_keypoint* keys_r, const uint8_t* desc_r,
-                                int n_right, float max_disparity, float* u_right, float* depth) {
-    if (!m || !ex || !left || !u_right || !depth || (n_right && (!keys_r || !desc_r)))
+// Frame::ComputeStereoMatches, Frame.cc:673-885.  Both entry points fill a StereoBatch
+// and run k_stereo_rows / k_stereo / k_stereo_outlier (orbx_match.hip).
+namespace {
+
+// Level geometry of a stereo pair's pyramids; the two extractors must share it.
+int stereo_levels(orbx_extractor* ex_l, orbx_extractor* ex_r, StereoBatch& sb, PyrView& vl, PyrView& vr) {
+    int rc = extractor_pyramid(ex_l, &vl);
+    if (rc != ORBX_OK) return rc;
+    rc = extractor_pyramid(ex_r, &vr);
+    if (rc != ORBX_OK) return rc;
+    if (vl.W != vr.W || vl.H != vr.H || vl.L != vr.L || vl.device != vr.device)
+        return fail(ORBX_ERR_ARG, "left and right extractors hold pyramids of different geometry");
+    for (int l = 0; l < vl.L; l++)
+        if (vl.scale[l] != vr.scale[l] || vl.off[l] != vr.off[l] || vl.pitch[l] != vr.pitch[l])
+            return fail(ORBX_ERR_ARG, "left and right extractors differ in their scale pyramid");
+    sb.rows = vl.h[0];  // mpORBextractorLeft->mvImagePyramid[0].rows (cc:682)
+    for (int l = 0; l < vl.L; l++) {
+        sb.level_off[l] = vl.off[l];
+        sb.level_pitch[l] = vl.pitch[l];
+        sb.level_w[l] = vl.w[l];  // mpORBextractorRight->mvImagePyramid[l].cols (cc:810)
+        sb.scale[l] = vl.scale[l];
+        sb.inv_scale[l] = vl.inv_scale[l];
+    }
+    sb.fb_l = vl.frame_bytes;
+    sb.fb_r = vr.frame_bytes;
+    // rows one right keypoint covers: ceil(y + r) - floor(y - r) + 1 <= 2r + 3, r = 2 scale[l]
+    int band = 0;
+    for (int l = 0; l < vl.L; l++) band = std::max(band, (int)std::ceil(4.0f * vl.scale[l]) + 3);
+    sb.band_cap = band * sb.cap;
+    return ORBX_OK;
+}
+
+size_t stereo_scratch(const StereoBatch& sb, int batch) {
+    return pad(sizeof(int32_t) * (size_t)batch * (sb.rows + 1)) + pad(sizeof(int32_t) * (size_t)batch * sb.band_cap) +
+           pad(sizeof(StereoResult) * (size_t)batch * sb.cap);
+}
+
+}  // namespace
+
+int orbx_compute_stereo_matches(orbx_matcher* m, orbx_extractor* ex_left, int left_frame, orbx_extractor* ex_right,
+                                int right_frame, const orbx_frame_view* left, const orbx_keypoint* keys_r,
+                                const uint8_t* desc_r, int n_right, float max_disparity, float* u_right,
+                                float* depth) {
+    if (!m || !ex_left || !ex_right || !left || !u_right || !depth || (n_right && (!keys_r || !desc_r)) ||
+        n_right < 0 || left->n < 0)
         return fail(ORBX_ERR_ARG, "null argument");
     const int N = left->n;
     for (int i = 0; i < N; i++) {
@@ -1302,111 +1346,126 @@ int orbx_compute_stereo_matches(orbx_matcher* m, orbx_extractor* ex, int left_fr
         depth[i] = -1.0f;
     }
     if (N == 0) return ORBX_OK;
-    StereoProblem pb{};
-    int nRows = 0;
-    for (int l = 0; l < left->nlevels && l < 32; l++) {
-        const uint8_t* pl = nullptr;
-        const uint8_t* pr = nullptr;
-        size_t pitch = 0;
-        int w = 0, h = 0;
-        int rc = orbx_pyramid_level_device(ex, left_frame, l, &pl, &pitch, &w, &h);
-        if (rc != ORBX_OK) return rc;
-        rc = orbx_pyramid_level_device(ex, right_frame, l, &pr, nullptr, nullptr, nullptr);
-        if (rc != ORBX_OK) return rc;
-        pb.lev_l[l] = pl;
-        pb.lev_r[l] = pr;
-        pb.level_pitch[l] = (int)pitch;
-        pb.level_w[l] = w;
-        pb.scale[l] = left->scale_factors[l];
-        pb.inv_scale[l] = 1.0f / left->scale_factors[l];  // mvInvScaleFactors (ORBextractor.cc:468)
-        if (l == 0) nRows = h;
-    }
-    // vRowIndices (cc:693-708): right keypoint indices per row band
-    std::vector<int32_t> off((size_t)nRows + 1, 0);
-    auto band = [&](int iR, int& minr, int& maxr) {
-        const float kpY = keys_r[iR].y;
-        const float r = 2.0f * left->scale_factors[keys_r[iR].octave];
-        maxr = (int)std::ceil(kpY + r);
-        minr = (int)std::floor(kpY - r);
-    };
-    for (int iR = 0; iR < n_right; iR++) {
-        int a, b;
-        band(iR, a, b);
-        for (int yi = std::max(a, 0); yi <= std::min(b, nRows - 1); yi++) off[(size_t)yi + 1]++;
-    }
-    for (int y = 0; y < nRows; y++) off[(size_t)y + 1] += off[(size_t)y];
-    std::vector<int32_t> idx((size_t)off[(size_t)nRows] + 1);
-    std::vector<int32_t> fillc((size_t)nRows, 0);
-    for (int iR = 0; iR < n_right; iR++) {
-        int a, b;
-        band(iR, a, b);
-        for (int yi = std::max(a, 0); yi <= std::min(b, nRows - 1); yi++)
-            idx[(size_t)off[(size_t)yi] + fillc[(size_t)yi]++] = iR;
-    }
+    StereoBatch sb{};
+    sb.cap = std::max(N, n_right);
+    if (sb.cap > 8192) return fail(ORBX_ERR_UNSUPPORTED, "more than 8192 keypoints per image");
+    PyrView vl, vr;
+    int rc = stereo_levels(ex_left, ex_right, sb, vl, vr);
+    if (rc != ORBX_OK) return rc;
+    if (left_frame < 0 || left_frame >= vl.nframes || right_frame < 0 || right_frame >= vr.nframes)
+        return fail(ORBX_ERR_ARG, "frame index outside the extractor's last batch");
     for (int i = 0; i < N; i++)
-        if (left->keys[i].y < 0 || (int)left->keys[i].y >= nRows) return fail(ORBX_ERR_ARG, "left keypoint row");
+        if (left->keys[i].y < 0 || (int)left->keys[i].y >= sb.rows || left->keys[i].octave < 0 ||
+            left->keys[i].octave >= vl.L)
+            return fail(ORBX_ERR_ARG, "left keypoint outside the pyramid");
+    for (int i = 0; i < n_right; i++)
+        if (keys_r[i].octave < 0 || keys_r[i].octave >= vl.L) return fail(ORBX_ERR_ARG, "right keypoint octave");
+    sb.pyr_l = vl.base + (size_t)left_frame * vl.frame_bytes;
+    sb.pyr_r = vr.base + (size_t)right_frame * vr.frame_bytes;
+    sb.bf = left->bf;
+    sb.max_d = max_disparity;
     HIP_TRY(hipSetDevice(m->device));
-    const int nidx = off[(size_t)nRows];
-    const size_t need = pad(sizeof(orbx_keypoint) * N) + pad((size_t)N * 32) + pad(sizeof(orbx_keypoint) * n_right) +
-                        pad((size_t)n_right * 32) + pad(sizeof(int32_t) * (nRows + 1)) +
-                        pad(sizeof(int32_t) * (nidx + 1)) + pad(sizeof(StereoResult) * N);
+    const size_t need = pad(sizeof(orbx_keypoint) * sb.cap) * 2 + pad((size_t)sb.cap * 32) * 2 + 2 * pad(sizeof(int32_t)) +
+                        2 * pad(sizeof(float) * sb.cap) + stereo_scratch(sb, 1);
     HIP_TRY(m->arena.reserve(need));
     m->arena.used = 0;
-    auto* d_kl = m->arena.take<orbx_keypoint>(N);
-    auto* d_dl = m->arena.take<uint8_t>((size_t)N * 32);
-    auto* d_kr = m->arena.take<orbx_keypoint>(n_right);
-    auto* d_dr = m->arena.take<uint8_t>((size_t)n_right * 32);
-    auto* d_off = m->arena.take<int32_t>(nRows + 1);
-    auto* d_idx = m->arena.take<int32_t>(nidx + 1);
-    auto* d_res = m->arena.take<StereoResult>(N);
-    // the extractor's stream produced the pyramids: order this stream after it
+    auto* d_kl = m->arena.take<orbx_keypoint>(sb.cap);
+    auto* d_dl = m->arena.take<uint8_t>((size_t)sb.cap * 32);
+    auto* d_kr = m->arena.take<orbx_keypoint>(sb.cap);
+    auto* d_dr = m->arena.take<uint8_t>((size_t)sb.cap * 32);
+    auto* d_nl = m->arena.take<int32_t>(1);
+    auto* d_nr = m->arena.take<int32_t>(1);
+    auto* d_ur = m->arena.take<float>(sb.cap);
+    auto* d_dp = m->arena.take<float>(sb.cap);
+    sb.row_off = m->arena.take<int32_t>((size_t)sb.rows + 1);
+    sb.row_idx = m->arena.take<int32_t>((size_t)sb.band_cap);
+    sb.res = m->arena.take<StereoResult>(sb.cap);
+    // the extractors' streams produced the pyramids: order this stream after them
+    HIP_TRY(hipStreamSynchronize(vl.stream));
+    if (vr.stream != vl.stream) HIP_TRY(hipStreamSynchronize(vr.stream));
     hipStream_t s = m->stream;
-    HIP_TRY(hipStreamSynchronize((hipStream_t)orbx_extractor_stream(ex)));
     m->arena.up(d_kl, left->keys, sizeof(orbx_keypoint) * N);
     m->arena.up(d_dl, left->desc, (size_t)N * 32);
     if (n_right) {
         m->arena.up(d_kr, keys_r, sizeof(orbx_keypoint) * n_right);
         m->arena.up(d_dr, desc_r, (size_t)n_right * 32);
     }
-    m->arena.up(d_off, off.data(), sizeof(int32_t) * (nRows + 1));
-    if (nidx) m->arena.up(d_idx, idx.data(), sizeof(int32_t) * nidx);
-    pb.keys_l = d_kl;
-    pb.desc_l = d_dl;
-    pb.nl = N;
-    pb.keys_r = d_kr;
-    pb.desc_r = d_dr;
-    pb.row_off = d_off;
-    pb.row_idx = d_idx;
-    pb.bf = left->bf;
-    pb.max_d = max_disparity;
+    const int32_t nl = N, nr = n_right;
+    m->arena.up(d_nl, &nl, sizeof(nl));
+    m->arena.up(d_nr, &nr, sizeof(nr));
+    sb.keys_l = d_kl;
+    sb.desc_l = d_dl;
+    sb.n_l = d_nl;
+    sb.keys_r = d_kr;
+    sb.desc_r = d_dr;
+    sb.n_r = d_nr;
+    sb.u_right = d_ur;
+    sb.depth = d_dp;
     HIP_TRY(m->arena.flush(s));
-    HIP_TRY(launch_stereo(pb, d_res, s));
-    std::vector<StereoResult> res((size_t)N);
-    HIP_TRY(m->arena.down(res.data(), d_res, sizeof(StereoResult) * N, s));
+    HIP_TRY(launch_stereo(sb, 1, s));
+    HIP_TRY(m->arena.down(u_right, d_ur, sizeof(float) * N, s));
+    HIP_TRY(m->arena.down(depth, d_dp, sizeof(float) * N, s));
     HIP_TRY(m->arena.sync(s));
-    // Sequential outlier pass of this fork (Frame.cc:868-884): after every left keypoint
-    // that reaches it, vDistIdx (sorted by (dist, iL)) is re-scanned from the back and
-    // entries with dist >= 1.5f*1.4f*median are invalidated.  An empty vDistIdx is
-    // skipped (the reference's vDistIdx[0] read on an empty vector has no effect
-    // because its marking loop then runs zero times).
-    std::vector<std::pair<int, int>> vd;
-    vd.reserve((size_t)N);
-    for (int iL = 0; iL < N; iL++) {
-        const StereoResult& r = res[(size_t)iL];
-        if (r.pushed) {
-            u_right[iL] = r.u_right;
-            depth[iL] = r.depth;
-            const std::pair<int, int> e(r.dist, iL);
-            vd.insert(std::upper_bound(vd.begin(), vd.end(), e), e);
-        }
-        if (!r.reach_sort || vd.empty()) continue;
-        const float median = (float)vd[vd.size() / 2].first;
-        const float thDist = 1.5f * 1.4f * median;
-        for (int i = (int)vd.size() - 1; i >= 0; i--) {
-            if ((float)vd[(size_t)i].first < thDist) break;
-            u_right[vd[(size_t)i].second] = -1;
-            depth[vd[(size_t)i].second] = -1;
-        }
+    return ORBX_OK;
+}
+
+int orbx_compute_stereo_matches_batch_device(orbx_matcher* m, orbx_extractor* ex_left, int left_frame0,
+                                             orbx_extractor* ex_right, int right_frame0, int batch,
+                                             const orbx_keypoint* d_kps_l, const uint8_t* d_desc_l,
+                                             const int32_t* d_n_l, const orbx_keypoint* d_kps_r,
+                                             const uint8_t* d_desc_r, const int32_t* d_n_r, int cap, float bf,
+                                             float max_disparity, float* d_u_right, float* d_depth, void* stream) {
+    if (!m || !ex_left || !ex_right || batch < 0 || cap <= 0) return fail(ORBX_ERR_ARG, "bad argument");
+    if (batch == 0) return ORBX_OK;
+    if (!d_kps_l || !d_desc_l || !d_n_l || !d_kps_r || !d_desc_r || !d_n_r || !d_u_right || !d_depth)
+        return fail(ORBX_ERR_ARG, "null buffer");
+    if (cap > 8192) return fail(ORBX_ERR_UNSUPPORTED, "cap above 8192 keypoints per image");
+    StereoBatch sb{};
+    sb.cap = cap;
+    PyrView vl, vr;
+    int rc = stereo_levels(ex_left, ex_right, sb, vl, vr);
+    if (rc != ORBX_OK) return rc;
+    if (left_frame0 < 0 || left_frame0 + batch > vl.nframes || right_frame0 < 0 || right_frame0 + batch > vr.nframes)
+        return fail(ORBX_ERR_ARG, "pair range outside the extractors' last batches");
+    HIP_TRY(hipSetDevice(m->device));
+    hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+    const size_t need = stereo_scratch(sb, batch);
+    if (m->dscr_cap < need) {
+        HIP_TRY(hipStreamSynchronize(s));
+        if (m->dscr) HIP_TRY(hipFree(m->dscr));
+        m->dscr = nullptr;
+        m->dscr_cap = 0;
+        HIP_TRY(hipMalloc((void**)&m->dscr, need));
+        m->dscr_cap = need;
+    }
+    char* p = m->dscr;
+    sb.row_off = (int32_t*)p;
+    p += pad(sizeof(int32_t) * (size_t)batch * (sb.rows + 1));
+    sb.row_idx = (int32_t*)p;
+    p += pad(sizeof(int32_t) * (size_t)batch * sb.band_cap);
+    sb.res = (StereoResult*)p;
+    sb.keys_l = d_kps_l;
+    sb.desc_l = d_desc_l;
+    sb.n_l = d_n_l;
+    sb.keys_r = d_kps_r;
+    sb.desc_r = d_desc_r;
+    sb.n_r = d_n_r;
+    sb.pyr_l = vl.base + (size_t)left_frame0 * vl.frame_bytes;
+    sb.pyr_r = vr.base + (size_t)right_frame0 * vr.frame_bytes;
+    sb.bf = bf;
+    sb.max_d = max_disparity;
+    sb.u_right = d_u_right;
+    sb.depth = d_depth;
+    hipEvent_t* ev = m->ev[m->ncalls % orbx_matcher::kRing];
+    if (m->timing) {
+        for (int i = 0; i < 2; i++)
+            if (!ev[i]) HIP_TRY(hipEventCreate(&ev[i]));
+        HIP_TRY(hipEventRecord(ev[0], s));
+    }
+    HIP_TRY(launch_stereo(sb, batch, s));
+    if (m->timing) {
+        HIP_TRY(hipEventRecord(ev[1], s));
+        m->ncalls++;
     }
     return ORBX_OK;
 }

@@ -335,18 +335,35 @@ class ORBmatcher:
         return nm.value, out[:len(f1.keys)].copy()
 
     # Frame::ComputeStereoMatches  Frame.cc:673-885
-    def ComputeStereoMatches(self, extractor, left_frame: int, right_frame: int, left: FrameView, keys_r, desc_r,
-                             maxD: float):
+    def ComputeStereoMatches(self, ex_left, left_frame: int, ex_right, right_frame: int, left: FrameView, keys_r,
+                             desc_r, maxD: float):
+        """mvuRight, mvDepth of a stereo Frame whose left image is frame `left_frame` of
+        ex_left's last extraction (mpORBextractorLeft) and right image frame `right_frame`
+        of ex_right's (mpORBextractorRight); both pyramids are read (Frame.cc:782-818)."""
         kr = np.ascontiguousarray(keys_r, dtype=L.KEYPOINT_DTYPE)
         dr = np.ascontiguousarray(desc_r, dtype=np.uint8)
         lv = left.c()
         n = len(left.keys)
         ur = np.zeros(max(n, 1), dtype=np.float32)
         dp = np.zeros(max(n, 1), dtype=np.float32)
-        L.check(L.lib().orbx_compute_stereo_matches(self._h, extractor._h, left_frame, right_frame, C.addressof(lv),
-                                                    kr.ctypes.data, dr.ctypes.data_as(U8P), len(kr), float(maxD),
+        L.check(L.lib().orbx_compute_stereo_matches(self._h, ex_left._h, int(left_frame), ex_right._h,
+                                                    int(right_frame), C.addressof(lv), kr.ctypes.data,
+                                                    dr.ctypes.data_as(U8P), len(kr), float(maxD),
                                                     ur.ctypes.data_as(F32P), dp.ctypes.data_as(F32P)))
         return ur[:n].copy(), dp[:n].copy()
+
+    def ComputeStereoMatchesBatchDevice(self, ex_left, ex_right, d_kps_l, d_desc_l, d_n_l, d_kps_r, d_desc_r, d_n_r,
+                                        bf: float, maxD: float, d_u_right, d_depth, left_frame0: int = 0,
+                                        right_frame0: int = 0, stream=None) -> None:
+        """ComputeStereoMatches for B pairs in HBM (device tensors in the
+        orbx_extract_batch_device layout; outputs (B, cap) float32), asynchronous."""
+        B, cap = d_desc_l.shape[0], d_desc_l.shape[1]
+        s = None if stream is None else C.c_void_p(getattr(stream, "cuda_stream", stream))
+        p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+        L.check(L.lib().orbx_compute_stereo_matches_batch_device(
+            self._h, ex_left._h, int(left_frame0), ex_right._h, int(right_frame0), int(B), p(d_kps_l), p(d_desc_l),
+            p(d_n_l), p(d_kps_r), p(d_desc_r), p(d_n_r), int(cap), float(bf), float(maxD), p(d_u_right), p(d_depth),
+            s))
 
     def match_sequence_device(self, d_kps, d_desc, d_n, d_Tcw, d_cur_mp, d_nmatches, scale_factors, fx, fy, cx, cy,
                               width, height, depth: float = 5.0, th: float = 15.0, stream=None) -> None:

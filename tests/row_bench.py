@@ -170,7 +170,7 @@ def rows(O, reps: int):
         pl, pr = O.pyramid(left, p), O.pyramid(right, p)
         ms = ORBmatcher(0.6, True)
         add("a18", "Frame::ComputeStereoMatches Frame.cc:673-885", f"{len(kl)} x {len(kr)} keypoints, {W}x{H}",
-            lambda: ms.ComputeStereoMatches(ex, 0, 1, view, kr, dr, maxD=fx),
+            lambda: ms.ComputeStereoMatches(ex, 0, ex, 1, view, kr, dr, maxD=fx),
             lambda: O.compute_stereo_matches(view, kr, dr, pl, pr, fx))
 
     # f2 SearchByBoW (KF -> F, KF -> KF), SearchForInitialization

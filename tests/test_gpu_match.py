@@ -118,8 +118,21 @@ def test_search_for_triangulation(oracle, orbx_built, seed, stereo, only_stereo,
     assert len(pr) > 20
 
 
+KITTI_FX, KITTI_BF = 718.856, 386.1448
+
+
+def _stereo_view(kl, dl, W, H, sf, fx=KITTI_FX, bf=KITTI_BF):
+    return FrameView(keys=kl, desc=dl, fx=fx, fy=fx, cx=W / 2, cy=H / 2, bf=bf, b=bf / fx, max_x=W, max_y=H,
+                     scale_factors=sf, level_sigma2=sf * sf)
+
+
+def _stereo_ref(oracle, left, right, kl, dl, kr, dr, p, view):
+    return oracle.compute_stereo_matches(view, kr, dr, oracle.pyramid(left, p), oracle.pyramid(right, p), view.fx)
+
+
 @pytest.mark.parametrize("seed,W,H", [(0, 640, 480), (1, 1241, 376)])
 def test_compute_stereo_matches(oracle, orbx_built, seed, W, H):
+    """One extractor holding both images (frames 0 and 1 of its last batch)."""
     left, right, _ = synth.stereo_pair(seed, W, H, max_disp=48)
     nf = 2000 if W > 1000 else 1000
     ex = ORBextractor(nf, 1.2, 8, 20, 7)
@@ -127,17 +140,95 @@ def test_compute_stereo_matches(oracle, orbx_built, seed, W, H):
     kl, dl = kps[0][: n[0]], desc[0][: n[0]]
     kr, dr = kps[1][: n[1]], desc[1][: n[1]]
     p = oracle.params(nf, 1.2, 8, 20, 7)
-    sf = np.array(p.scale[:8], np.float32)
-    fx = 718.856
-    bf = 386.1448
-    view = FrameView(keys=kl, desc=dl, fx=fx, fy=fx, cx=W / 2, cy=H / 2, bf=bf, b=bf / fx, max_x=W, max_y=H,
-                     scale_factors=sf, level_sigma2=sf * sf)
+    view = _stereo_view(kl, dl, W, H, np.array(p.scale[:8], np.float32))
     m = ORBmatcher(0.6, True)
-    ur_g, dp_g = m.ComputeStereoMatches(ex, 0, 1, view, kr, dr, maxD=fx)
-    ur_r, dp_r = oracle.compute_stereo_matches(view, kr, dr, oracle.pyramid(left, p), oracle.pyramid(right, p), fx)
+    ur_g, dp_g = m.ComputeStereoMatches(ex, 0, ex, 1, view, kr, dr, maxD=view.fx)
+    ur_r, dp_r = _stereo_ref(oracle, left, right, kl, dl, kr, dr, p, view)
     assert np.array_equal(ur_g, ur_r), np.nonzero(ur_g != ur_r)[0][:10]
     assert np.array_equal(dp_g, dp_r)
     assert (ur_r >= 0).sum() > 100
+
+
+def test_stereo_frame_two_extractors_two_threads(oracle, orbx_built):
+    """The stereo Frame constructor's shape (Frame.cc:127-131, 682-818): mpORBextractorLeft
+    and mpORBextractorRight extract L and R from two host threads at once, then
+    ComputeStereoMatches reads both extractors' pyramids."""
+    import threading
+
+    W, H, nf = 1241, 376, 2000
+    left, right, _ = synth.stereo_pair(5, W, H, max_disp=48)
+    exl, exr = ORBextractor(nf, 1.2, 8, 20, 7), ORBextractor(nf, 1.2, 8, 20, 7)
+    out = {}
+
+    def run(name, ex, img):
+        out[name] = ex(img)
+
+    ts = [threading.Thread(target=run, args=("L", exl, left)), threading.Thread(target=run, args=("R", exr, right))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    (kl, dl), (kr, dr) = out["L"], out["R"]
+    p = oracle.params(nf, 1.2, 8, 20, 7)
+    for img, (k, d) in ((left, out["L"]), (right, out["R"])):
+        k0, d0, _ = oracle.extract(img, p)
+        assert np.array_equal(k.view(np.uint8), k0.view(np.uint8)) and np.array_equal(d, d0)
+    view = _stereo_view(kl, dl, W, H, exl.GetScaleFactors())
+    m = ORBmatcher(0.6, True)
+    ur_g, dp_g = m.ComputeStereoMatches(exl, 0, exr, 0, view, kr, dr, maxD=view.fx)
+    ur_r, dp_r = _stereo_ref(oracle, left, right, kl, dl, kr, dr, p, view)
+    assert np.array_equal(ur_g, ur_r) and np.array_equal(dp_g, dp_r)
+    assert (ur_r >= 0).sum() > 200
+
+
+@pytest.mark.parametrize("W,H,nf,B,shared", [(1241, 376, 2000, 16, False), (640, 480, 1000, 8, False),
+                                             (752, 480, 1200, 6, True)])
+def test_compute_stereo_matches_batch_device(oracle, orbx_built, W, H, nf, B, shared):
+    """Batched device ComputeStereoMatches (configs[2] shape: left frames on one extractor,
+    right frames on another, or both on one extractor) == the oracle, pair by pair."""
+    import torch
+
+    pairs = [synth.stereo_pair(30 + b, W, H, max_disp=48) for b in range(B)]
+    dev = torch.device("cuda", 0)
+    exl = ORBextractor(nf, 1.2, 8, 20, 7)
+    exr = exl if shared else ORBextractor(nf, 1.2, 8, 20, 7)
+    cap = exl.max_keypoints(W, H)
+    L_ = np.stack([p[0] for p in pairs])
+    R_ = np.stack([p[1] for p in pairs])
+    imgs = torch.from_numpy(np.concatenate([L_, R_]) if shared else np.concatenate([L_, R_])).to(dev)
+    kps = torch.empty((2 * B, cap, 7), dtype=torch.int32, device=dev)
+    desc = torch.empty((2 * B, cap, 32), dtype=torch.uint8, device=dev)
+    n = torch.empty((2 * B,), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    if shared:
+        exl.extract_batch_device(imgs, kps, desc, n)
+        l0, r0 = 0, B
+    else:
+        exl.extract_batch_device(imgs[:B], kps[:B], desc[:B], n[:B])
+        exr.extract_batch_device(imgs[B:], kps[B:], desc[B:], n[B:])
+        l0, r0 = 0, 0
+    torch.cuda.synchronize()
+    ur = torch.full((B, cap), 7.0, dtype=torch.float32, device=dev)
+    dp = torch.full((B, cap), 7.0, dtype=torch.float32, device=dev)
+    m = ORBmatcher(0.6, True)
+    m.ComputeStereoMatchesBatchDevice(exl, exr, kps[:B], desc[:B], n[:B], kps[B:], desc[B:], n[B:], KITTI_BF,
+                                      KITTI_FX, ur, dp, left_frame0=l0, right_frame0=r0)
+    torch.cuda.synchronize()
+    hk = kps.cpu().numpy().view(np.uint8).reshape(2 * B, cap, 28).view(oracle.KEYPOINT_DTYPE).reshape(2 * B, cap)
+    hd, hn, hur, hdp = desc.cpu().numpy(), n.cpu().numpy(), ur.cpu().numpy(), dp.cpu().numpy()
+    p = oracle.params(nf, 1.2, 8, 20, 7)
+    sf = exl.GetScaleFactors()
+    total = 0
+    for b in range(B):
+        kl, dl = hk[b][: hn[b]], hd[b][: hn[b]]
+        kr, dr = hk[B + b][: hn[B + b]], hd[B + b][: hn[B + b]]
+        view = _stereo_view(kl, dl, W, H, sf)
+        ur_r, dp_r = _stereo_ref(oracle, pairs[b][0], pairs[b][1], kl, dl, kr, dr, p, view)
+        assert np.array_equal(hur[b, : hn[b]], ur_r), (b, np.nonzero(hur[b, : hn[b]] != ur_r)[0][:10])
+        assert np.array_equal(hdp[b, : hn[b]], dp_r), b
+        assert (hur[b, hn[b]:] == -1).all() and (hdp[b, hn[b]:] == -1).all()
+        total += int((ur_r >= 0).sum())
+    assert total > 100 * B
 
 
 def test_descriptor_distance_and_windows(oracle, orbx_built):
