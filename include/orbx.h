@@ -357,6 +357,41 @@ int orbx_search_for_triangulation(orbx_matcher* m, const orbx_frame_view* kf1, c
                                   const int32_t* fv2_node, const int32_t* fv2_off, const int32_t* fv2_idx,
                                   int fv2_n, const float* F12, int only_stereo, int32_t* pairs, int* npairs);
 
+/* One KeyFrame as SearchForTriangulation reads it, left in HBM by the batched device
+ * calls (frame b of their [B][cap] layouts): orbx_extract_batch_device (keys, desc, n),
+ * orbx_compute_stereo_matches_batch_device (u_right), orbx_vocabulary_transform_batch_device
+ * (the FeatureVector CSR fv_node / fv_off / fv_idx / nfv).  Device pointers, except Tcw:
+ * the pose stays a host value as in the reference (KeyFrame::GetPose). */
+typedef struct {
+    const orbx_keypoint* keys;   /* mvKeysUn (cap slots) */
+    const uint8_t* desc;         /* mDescriptors (cap x 32) */
+    const int32_t* n;            /* N (one device int; min(*n, cap) keypoints are read) */
+    const float* u_right;        /* mvuRight (cap) or NULL (monocular) */
+    const uint8_t* has_mp;       /* GetMapPoint(i) != NULL (cap) */
+    const int32_t* fv_node;      /* mFeatVec node ids, ascending (cap) */
+    const int32_t* fv_off;       /* node k's keypoints: fv_idx[fv_off[k] .. fv_off[k+1]) (cap + 1) */
+    const int32_t* fv_idx;       /* (cap) */
+    const int32_t* nfv;          /* node count (one device int) */
+    float Tcw[12];               /* host: mTcw rows 0..2 */
+} orbx_keyframe_device;
+
+/* LocalMapping::CreateNewMapPoints' matching loop (LocalMapping.cc:235-305) over many
+ * keyframe pairs at once: for p < npairs, SearchForTriangulation(KF1 = kfs[pairs[2p]],
+ * KF2 = kfs[pairs[2p+1]], F12 + 9p, vMatchedPairs, only_stereo) (ORBmatcher.cc:850-1056),
+ * with the matcher's checkOri (LocalMapping uses ORBmatcher(0.6, false)).  `cam` gives
+ * the shared intrinsics fx, fy, cx, cy and the level tables (nlevels, scale_factors,
+ * level_sigma2); its keys / desc / u_right / Tcw are not read.  pairs and F12 (row-major
+ * 3x3, LocalMapping::ComputeF12) are host arrays; the epipole comes from the host poses.
+ * Outputs (device): d_matches12 [P][cap] (vMatches12: KF2 index or -1), d_pairs
+ * [P][cap][2] (vMatchedPairs, idx1 order) and d_npairs [P].  Enqueued on `stream` (or the
+ * matcher's) without synchronising; the host tables are staged through pinned memory, so
+ * they may be reused on return.  Successive calls on one matcher must use one stream
+ * (they share its device work area).  cap <= 8192. */
+int orbx_search_for_triangulation_batch_device(orbx_matcher* m, int nkf, const orbx_keyframe_device* kfs,
+                                               const orbx_frame_view* cam, int npairs, const int32_t* pairs,
+                                               const float* F12, int only_stereo, int cap, int32_t* d_matches12,
+                                               int32_t* d_pairs, int32_t* d_npairs, void* stream);
+
 /* Frame::ComputeStereoMatches (Frame.cc:673-885) of one stereo Frame, as the stereo Frame
  * constructor runs it (Frame.cc:99-178): the left image was extracted by `ex_left` (frame
  * `left_frame` of its last extraction, mpORBextractorLeft) and the right image by

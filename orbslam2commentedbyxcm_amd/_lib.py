@@ -47,6 +47,7 @@ EXPORTED = [
     "orbx_fuse", "orbx_fuse_sim3", "orbx_search_by_sim3", "orbx_compute_distinctive_descriptors",
     "orbx_compute_distinctive_descriptors_device", "orbx_extractor_status", "orbx_extractor_status_device",
     "orbx_extractor_set_node_capacity", "orbx_compute_stereo_matches_batch_device",
+    "orbx_search_for_triangulation_batch_device",
 ]
 
 
@@ -123,6 +124,8 @@ def lib() -> C.CDLL:
     L.orbx_compute_stereo_matches.argtypes = [vp, vp, C.c_int, vp, C.c_int, vp, vp, u8p, C.c_int, C.c_float, fp, fp]
     L.orbx_compute_stereo_matches_batch_device.argtypes = [vp, vp, C.c_int, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp,
                                                            vp, C.c_int, C.c_float, C.c_float, vp, vp, vp]
+    L.orbx_search_for_triangulation_batch_device.argtypes = [vp, C.c_int, vp, vp, C.c_int, i32p, fp, C.c_int,
+                                                             C.c_int, vp, vp, vp, vp]
     L.orbx_match_sequence_device.argtypes = [vp, C.c_int, vp, vp, vp, C.c_int, vp, C.c_float, C.c_float, C.c_float,
                                              C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, fp, C.c_int,
                                              C.c_float, C.c_float, vp, vp, vp]

@@ -73,6 +73,8 @@ hipError_t launch_seq_build(const SeqArgs& A, int npairs, ProjQuery* queries, Pr
 
 hipError_t launch_triangulation(const TriProblem* d_probs, int nprob, unsigned long long* scratch, int max_n2,
                                 int max_nq, hipStream_t stream);
+// k_tri_setup (queries + problems from the keyframe tables) then k_triangulation
+hipError_t launch_triangulation_batch(const TriBatch& tb, unsigned long long* scratch, hipStream_t stream);
 
 hipError_t launch_stereo(const StereoBatch& sb, int batch, hipStream_t stream);
 hipError_t launch_bow(const BowProblem* d_prob, int n2, int nitems, hipStream_t stream);

@@ -746,6 +746,7 @@ __device__ void score_tri(const TriProblem& pb, const TriQuery& Q, const uint8_t
                           unsigned long long& best) {
     const int lane = threadIdx.x & 63;
     best = kNoKey;
+    if (Q.beg >= Q.end) return;  // no shared node (batched tables: filtered queries), wave-uniform
     const orbx_keypoint kp1 = pb.keys1[Q.idx1];
     const unsigned long long* d1 = (const unsigned long long*)(pb.desc1 + (size_t)Q.idx1 * 32);
     const unsigned long long q0 = d1[0], q1 = d1[1], q2 = d1[2], q3 = d1[3];
@@ -827,7 +828,7 @@ __global__ __launch_bounds__(kTriThreads) void k_triangulation(const TriProblem*
                     l_idx2 = pb.fv2_idx[Q.beg + (int)(0xffffffffu - (unsigned)(l_best & 0xffffffffu))];
                     l_a2 = pb.keys2[l_idx2].angle;
                 }
-                l_a1 = pb.keys1[Q.idx1].angle;
+                if (Q.idx1 >= 0) l_a1 = pb.keys1[Q.idx1].angle;
             }
             const int cnt = pb.nq - q0 < 64 ? pb.nq - q0 : 64;
             for (int j = 0; j < cnt; j++) {
@@ -844,6 +845,7 @@ __global__ __launch_bounds__(kTriThreads) void k_triangulation(const TriProblem*
                                : -1;
                     if (idx2 >= 0) a2 = pb.keys2[idx2].angle;
                 }
+                if (idx1 < 0) continue;  // batched tables: a feature index outside [0, N)
                 if (lane == 0) pb.matches12[idx1] = idx2;
                 if (idx2 < 0) continue;
                 if (lane == 0) matched2[idx2] = 1;
@@ -886,6 +888,103 @@ __global__ __launch_bounds__(kTriThreads) void k_triangulation(const TriProblem*
                 if (b != ind1 && b != ind2 && b != ind3) pb.matches12[mlist[m]] = -1;
             }
         }
+        if (pb.pairs_out) {
+            // vMatchedPairs (cc:1045-1053): vMatches12 compacted in idx1 order, 64 at a time
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            int cnt = 0;
+            for (int base = 0; base < pb.n1; base += 64) {
+                const int i = base + lane;
+                const int v = i < pb.n1 ? pb.matches12[i] : -1;
+                const unsigned long long mask = __ballot(v >= 0);
+                const int pre = __popcll(mask & ((1ull << lane) - 1ull));
+                if (v >= 0) {
+                    pb.pairs_out[2 * (cnt + pre)] = i;
+                    pb.pairs_out[2 * (cnt + pre) + 1] = v;
+                }
+                cnt += __popcll(mask);
+            }
+            if (lane == 0) *pb.npairs_out = cnt;
+        }
+    }
+}
+
+// Batched form: one workgroup per (KF1, KF2) pair builds that pair's query table and
+// problem record on the device from the keyframe tables (the FeatureVector merge of
+// ORBmatcher.cc:886-1019).  Query q is KF1's q-th FeatureVector entry, so the table is in
+// the reference's visiting order (nodes ascending, keypoints in node-list order); an
+// entry whose node KF2 lacks, whose keypoint already has a MapPoint (cc:905-909) or that
+// fails bOnlyStereo (cc:913-916) gets an empty candidate range.
+constexpr int kTriSetupThreads = 256;
+
+__global__ __launch_bounds__(kTriSetupThreads) void k_tri_setup(TriBatch tb) {
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const TriPair pr = tb.pairs[p];
+    const TriKF A = tb.kfs[pr.kf1];
+    const TriKF B = tb.kfs[pr.kf2];
+    const int cap = tb.cap;
+    const int n1 = min(max(*A.n, 0), cap), n2 = min(max(*B.n, 0), cap);
+    const int nfv1 = min(max(*A.nfv, 0), n1), nfv2 = min(max(*B.nfv, 0), n2);
+    int32_t* m12 = tb.matches12 + (size_t)p * cap;
+    for (int i = tid; i < cap; i += kTriSetupThreads) m12[i] = -1;
+    TriQuery* Q = tb.q + (size_t)p * cap;
+    const int nq = min(A.fv_off[nfv1], n1);
+    for (int q = tid; q < nq; q += kTriSetupThreads) Q[q] = TriQuery{-1, 0, 0, 0};  // entries no node covers
+    __syncthreads();
+    for (int j1 = tid; j1 < nfv1; j1 += kTriSetupThreads) {
+        const int node = A.fv_node[j1];
+        int lo = 0, hi = nfv2;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (B.fv_node[mid] < node) lo = mid + 1;
+            else hi = mid;
+        }
+        const bool shared = lo < nfv2 && B.fv_node[lo] == node;
+        const int beg = shared ? B.fv_off[lo] : 0, end = shared ? min(B.fv_off[lo + 1], n2) : 0;
+        const int q1 = min(A.fv_off[j1 + 1], nq);
+        for (int q = max(A.fv_off[j1], 0); q < q1; q++) {
+            int idx1 = A.fv_idx[q];
+            TriQuery t;
+            t.beg = t.end = 0;
+            t.stereo1 = 0;
+            if (idx1 < 0 || idx1 >= n1) {
+                idx1 = -1;
+            } else {
+                const bool st1 = A.u_right && A.u_right[idx1] >= 0;
+                t.stereo1 = st1 ? 1 : 0;
+                if (shared && !A.has_mp[idx1] && (!tb.only_stereo || st1)) {
+                    t.beg = beg;
+                    t.end = end;
+                }
+            }
+            t.idx1 = idx1;
+            Q[q] = t;
+        }
+    }
+    if (tid == 0) {
+        TriProblem pb{};
+        pb.keys1 = A.keys;
+        pb.desc1 = A.desc;
+        pb.keys2 = B.keys;
+        pb.desc2 = B.desc;
+        pb.u_right2 = B.u_right;
+        pb.has_mp2 = B.has_mp;
+        pb.fv2_idx = B.fv_idx;
+        pb.scale2 = tb.scale2;
+        pb.sigma2_2 = tb.sigma2_2;
+        for (int k = 0; k < 9; k++) pb.F12[k] = pr.F12[k];
+        pb.ex = pr.ex;
+        pb.ey = pr.ey;
+        pb.only_stereo = tb.only_stereo;
+        pb.check_ori = tb.check_ori;
+        pb.n2 = n2;
+        pb.q = Q;
+        pb.nq = nq;
+        pb.matches12 = m12;
+        pb.scratch_off = (long long)p * cap;
+        pb.n1 = n1;
+        pb.pairs_out = tb.pairs_out + (size_t)p * cap * 2;
+        pb.npairs_out = tb.npairs_out + p;
+        tb.probs[p] = pb;
     }
 }
 
@@ -901,6 +1000,15 @@ hipError_t launch_triangulation(const TriProblem* d_probs, int nprob, unsigned l
     }
     hipLaunchKernelGGL(k_triangulation, dim3(nprob), dim3(kTriThreads), lds, stream, d_probs, scratch);
     return hipGetLastError();
+}
+
+hipError_t launch_triangulation_batch(const TriBatch& tb, unsigned long long* scratch, hipStream_t stream) {
+    if (tb.npairs <= 0) return hipSuccess;
+    if (tb.cap <= 0 || tb.cap > 8192) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_tri_setup, dim3(tb.npairs), dim3(kTriSetupThreads), 0, stream, tb);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_triangulation(tb.probs, tb.npairs, scratch, tb.cap, tb.cap, stream);
 }
 
 // ------------------------------------------------------------------ stereo

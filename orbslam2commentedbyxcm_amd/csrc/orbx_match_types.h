@@ -98,6 +98,47 @@ struct TriProblem {
     int nq;
     int32_t* matches12;         // out: vMatches12 (KF1 n), pre-filled with -1
     long long scratch_off;
+    int n1;                     // KF1 keypoints (read by the pair compaction only)
+    int32_t* pairs_out;         // or null: vMatchedPairs (idx1, idx2) in idx1 order
+    int32_t* npairs_out;        // its count
+};
+
+// Batched SearchForTriangulation (orbx_search_for_triangulation_batch_device): one
+// keyframe's device arrays (orbx_keyframe_device without the host pose) ...
+struct TriKF {
+    const orbx_keypoint* keys;
+    const uint8_t* desc;
+    const int32_t* n;
+    const float* u_right;
+    const uint8_t* has_mp;
+    const int32_t* fv_node;
+    const int32_t* fv_off;
+    const int32_t* fv_idx;
+    const int32_t* nfv;
+};
+
+// ... and one (KF1, KF2) pair with the host-side quantities of the reference's loop
+// (F12 from LocalMapping::ComputeF12, the epipole of ORBmatcher.cc:858-865).
+struct TriPair {
+    int kf1, kf2;
+    float F12[9];
+    float ex, ey;
+};
+
+struct TriBatch {
+    const TriKF* kfs;
+    const TriPair* pairs;
+    int npairs;
+    int cap;
+    int only_stereo;
+    int check_ori;
+    const float* scale2;        // mvScaleFactors (shared camera)
+    const float* sigma2_2;      // mvLevelSigma2
+    TriQuery* q;                // [P][cap]
+    TriProblem* probs;          // [P]
+    int32_t* matches12;         // [P][cap]
+    int32_t* pairs_out;         // [P][cap][2]
+    int32_t* npairs_out;        // [P]
 };
 
 // SearchByBoW (KF->F and KF->KF): one shared vocabulary node.  Its queries (side-1

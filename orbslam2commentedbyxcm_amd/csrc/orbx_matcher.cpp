@@ -111,6 +111,56 @@ struct Arena {
 
 size_t pad(size_t b) { return ((b + 255) & ~(size_t)255) + 256; }
 
+// Pinned staging for the asynchronous device calls' small host tables: a ring of slots,
+// each reused only once the copy that last read it has run (its event), so a call never
+// waits on the stream (a pageable hipMemcpyAsync would).
+struct StageRing {
+    static constexpr int kSlots = 4;
+    char* host[kSlots] = {};
+    size_t cap[kSlots] = {};
+    hipEvent_t ev[kSlots] = {};
+    bool pending[kSlots] = {};
+    int next = 0;
+    hipError_t get(size_t bytes, char** out, int* slot) {
+        const int k = next;
+        next = (next + 1) % kSlots;
+        if (pending[k]) {
+            const hipError_t e = hipEventSynchronize(ev[k]);
+            if (e != hipSuccess) return e;
+            pending[k] = false;
+        }
+        if (cap[k] < bytes) {
+            if (host[k]) (void)hipHostFree(host[k]);
+            host[k] = nullptr;
+            cap[k] = 0;
+            const hipError_t e = hipHostMalloc((void**)&host[k], bytes, hipHostMallocDefault);
+            if (e != hipSuccess) return e;
+            cap[k] = bytes;
+        }
+        if (!ev[k]) {
+            const hipError_t e = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        *out = host[k];
+        *slot = k;
+        return hipSuccess;
+    }
+    hipError_t copied(int slot, hipStream_t s) {
+        pending[slot] = true;
+        return hipEventRecord(ev[slot], s);
+    }
+    void release() {
+        for (int k = 0; k < kSlots; k++) {
+            if (host[k]) (void)hipHostFree(host[k]);
+            if (ev[k]) (void)hipEventDestroy(ev[k]);
+            host[k] = nullptr;
+            ev[k] = nullptr;
+            cap[k] = 0;
+            pending[k] = false;
+        }
+    }
+};
+
 // x_c = R x + t, float products summed left to right (gemm accumulation unpinned)
 void project(const float* Tcw, const float* X, float* xc) {
     for (int r = 0; r < 3; r++)
@@ -158,6 +208,10 @@ struct orbx_matcher {
     // device-only scratch of the batched device calls (no pinned mirror)
     char* dscr = nullptr;
     size_t dscr_cap = 0;
+    // tables of orbx_search_for_triangulation_batch_device (device-only)
+    char* tscr = nullptr;
+    size_t tscr_cap = 0;
+    StageRing stage;
 };
 
 namespace {
@@ -257,6 +311,8 @@ void orbx_matcher_destroy(orbx_matcher* m) {
     if (m->stream) (void)hipStreamSynchronize(m->stream);
     m->arena.release();
     if (m->dscr) (void)hipFree(m->dscr);
+    if (m->tscr) (void)hipFree(m->tscr);
+    m->stage.release();
     for (auto& slot : m->ev)
         for (auto& e : slot)
             if (e) (void)hipEventDestroy(e);
@@ -736,6 +792,115 @@ int orbx_search_for_triangulation(orbx_matcher* m, const orbx_frame_view* kf1, c
         np++;
     }
     *npairs = np;
+    return ORBX_OK;
+}
+
+// LocalMapping::CreateNewMapPoints' SearchForTriangulation loop (LocalMapping.cc:235-305)
+// over keyframes in HBM: the host part of ORBmatcher.cc:850-1056 (the epipole, cc:858-865)
+// per pair here, the FeatureVector merge and the scoring / commit on the device.
+int orbx_search_for_triangulation_batch_device(orbx_matcher* m, int nkf, const orbx_keyframe_device* kfs,
+                                               const orbx_frame_view* cam, int npairs, const int32_t* pairs,
+                                               const float* F12, int only_stereo, int cap, int32_t* d_matches12,
+                                               int32_t* d_pairs, int32_t* d_npairs, void* stream) {
+    if (!m || nkf < 0 || npairs < 0 || !cam) return fail(ORBX_ERR_ARG, "bad argument");
+    if (npairs == 0) return ORBX_OK;
+    if (!kfs || !pairs || !F12 || !d_matches12 || !d_pairs || !d_npairs) return fail(ORBX_ERR_ARG, "null buffer");
+    if (cap <= 0) return fail(ORBX_ERR_ARG, "bad cap");
+    if (cap > 8192) return fail(ORBX_ERR_UNSUPPORTED, "cap above 8192 keypoints per keyframe");
+    if (cam->nlevels < 1 || cam->nlevels > ORBX_MAX_LEVELS || !cam->scale_factors || !cam->level_sigma2)
+        return fail(ORBX_ERR_ARG, "bad level tables");
+    for (int k = 0; k < nkf; k++) {
+        const orbx_keyframe_device& K = kfs[k];
+        if (!K.keys || !K.desc || !K.n || !K.has_mp || !K.fv_node || !K.fv_off || !K.fv_idx || !K.nfv)
+            return fail(ORBX_ERR_ARG, "null keyframe array");
+    }
+    std::vector<TriKF> tk((size_t)nkf);
+    for (int k = 0; k < nkf; k++) {
+        const orbx_keyframe_device& K = kfs[k];
+        tk[(size_t)k] = TriKF{K.keys, K.desc, K.n, K.u_right, K.has_mp, K.fv_node, K.fv_off, K.fv_idx, K.nfv};
+    }
+    std::vector<TriPair> tp((size_t)npairs);
+    for (int p = 0; p < npairs; p++) {
+        const int a = pairs[2 * p], b = pairs[2 * p + 1];
+        if (a < 0 || a >= nkf || b < 0 || b >= nkf) return fail(ORBX_ERR_ARG, "keyframe index out of range");
+        TriPair& t = tp[(size_t)p];
+        t.kf1 = a;
+        t.kf2 = b;
+        std::memcpy(t.F12, F12 + 9 * (size_t)p, sizeof(t.F12));
+        // epipole of KF1's centre in KF2 (cc:858-865), as orbx_search_for_triangulation
+        float Cw[3], C2[3];
+        centre(kfs[a].Tcw, Cw);
+        project(kfs[b].Tcw, Cw, C2);
+        const float invz = 1.0f / C2[2];
+        t.ex = cam->fx * C2[0] * invz + cam->cx;
+        t.ey = cam->fy * C2[1] * invz + cam->cy;
+    }
+    HIP_TRY(hipSetDevice(m->device));
+    hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+    const size_t P = (size_t)npairs;
+    const size_t need = pad(sizeof(TriKF) * (size_t)nkf) + pad(sizeof(TriPair) * P) + 2 * pad(sizeof(float) * 32) +
+                        pad(sizeof(TriQuery) * P * cap) + pad(sizeof(TriProblem) * P) +
+                        pad(sizeof(unsigned long long) * P * cap);
+    if (m->tscr_cap < need) {
+        HIP_TRY(hipStreamSynchronize(s));
+        if (m->tscr) HIP_TRY(hipFree(m->tscr));
+        m->tscr = nullptr;
+        m->tscr_cap = 0;
+        HIP_TRY(hipMalloc((void**)&m->tscr, need));
+        m->tscr_cap = need;
+    }
+    // tables first (one staged copy), then the device-only work areas
+    const size_t tab = pad(sizeof(TriKF) * (size_t)nkf) + pad(sizeof(TriPair) * P) + 2 * pad(sizeof(float) * 32);
+    char* q = m->tscr;
+    auto take = [&q](size_t bytes) {
+        char* r = q;
+        q += pad(bytes);
+        return r;
+    };
+    TriBatch tb{};
+    auto* d_kf = (TriKF*)take(sizeof(TriKF) * (size_t)nkf);
+    auto* d_tp = (TriPair*)take(sizeof(TriPair) * P);
+    auto* d_sc = (float*)take(sizeof(float) * 32);
+    auto* d_sg = (float*)take(sizeof(float) * 32);
+    tb.q = (TriQuery*)take(sizeof(TriQuery) * P * cap);
+    tb.probs = (TriProblem*)take(sizeof(TriProblem) * P);
+    auto* d_scr = (unsigned long long*)take(sizeof(unsigned long long) * P * cap);
+    char* h = nullptr;
+    int slot = 0;
+    HIP_TRY(m->stage.get(tab, &h, &slot));
+    std::memset(h, 0, tab);
+    std::memcpy(h + ((char*)d_kf - m->tscr), tk.data(), sizeof(TriKF) * (size_t)nkf);
+    std::memcpy(h + ((char*)d_tp - m->tscr), tp.data(), sizeof(TriPair) * P);
+    float* hs = (float*)(h + ((char*)d_sc - m->tscr));
+    float* hg = (float*)(h + ((char*)d_sg - m->tscr));
+    for (int l = 0; l < cam->nlevels; l++) {
+        hs[l] = cam->scale_factors[l];
+        hg[l] = cam->level_sigma2[l];
+    }
+    HIP_TRY(hipMemcpyAsync(m->tscr, h, tab, hipMemcpyHostToDevice, s));
+    HIP_TRY(m->stage.copied(slot, s));
+    tb.kfs = d_kf;
+    tb.pairs = d_tp;
+    tb.npairs = npairs;
+    tb.cap = cap;
+    tb.only_stereo = only_stereo ? 1 : 0;
+    tb.check_ori = m->check_ori;
+    tb.scale2 = d_sc;
+    tb.sigma2_2 = d_sg;
+    tb.matches12 = d_matches12;
+    tb.pairs_out = d_pairs;
+    tb.npairs_out = d_npairs;
+    hipEvent_t* ev = m->ev[m->ncalls % orbx_matcher::kRing];
+    if (m->timing) {
+        for (int i = 0; i < 2; i++)
+            if (!ev[i]) HIP_TRY(hipEventCreate(&ev[i]));
+        HIP_TRY(hipEventRecord(ev[0], s));
+    }
+    HIP_TRY(launch_triangulation_batch(tb, d_scr, s));
+    if (m->timing) {
+        HIP_TRY(hipEventRecord(ev[1], s));
+        m->ncalls++;
+    }
     return ORBX_OK;
 }
 

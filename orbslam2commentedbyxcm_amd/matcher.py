@@ -28,6 +28,28 @@ class _FrameViewC(C.Structure):
                 ("scale_factors", F32P), ("level_sigma2", F32P), ("Tcw", C.c_float * 12)]
 
 
+class _KeyFrameDeviceC(C.Structure):
+    """orbx_keyframe_device: device pointers + the host pose."""
+    _fields_ = [("keys", C.c_void_p), ("desc", C.c_void_p), ("n", C.c_void_p), ("u_right", C.c_void_p),
+                ("has_mp", C.c_void_p), ("fv_node", C.c_void_p), ("fv_off", C.c_void_p), ("fv_idx", C.c_void_p),
+                ("nfv", C.c_void_p), ("Tcw", C.c_float * 12)]
+
+
+def keyframe_device(keys, desc, n, has_mp, fv_node, fv_off, fv_idx, nfv, Tcw, u_right=None) -> _KeyFrameDeviceC:
+    """One orbx_keyframe_device record from device tensors (or raw device addresses) of
+    one keyframe: keys (cap, 7) int32 words, desc (cap, 32) u8, n / nfv 1-element int32,
+    has_mp (cap,) u8, fv_node / fv_idx (cap,) int32, fv_off (cap + 1,) int32, u_right
+    (cap,) f32 or None; Tcw a host 3x4 (or 4x4) pose."""
+    def a(t):
+        return None if t is None else (int(t) if isinstance(t, int) else t.data_ptr())
+
+    r = _KeyFrameDeviceC()
+    r.keys, r.desc, r.n, r.u_right = a(keys), a(desc), a(n), a(u_right)
+    r.has_mp, r.fv_node, r.fv_off, r.fv_idx, r.nfv = a(has_mp), a(fv_node), a(fv_off), a(fv_idx), a(nfv)
+    r.Tcw[:] = list(_f32(Tcw)[:3, :4].reshape(-1))
+    return r
+
+
 class _MapPointsC(C.Structure):
     _fields_ = [("n", C.c_int), ("pos", F32P), ("desc", U8P), ("observations", I32P), ("bad", U8P),
                 ("max_distance", F32P), ("min_distance", F32P), ("normal", F32P)]
@@ -289,6 +311,25 @@ class ORBmatcher:
             o2.ctypes.data_as(I32P), i2.ctypes.data_as(I32P), len(n2), F.ctypes.data_as(F32P),
             1 if bOnlyStereo else 0, pairs.ctypes.data_as(I32P), C.byref(npairs)))
         return pairs[: npairs.value].copy()
+
+    def SearchForTriangulationBatchDevice(self, kfs, cam: FrameView, pairs, F12, cap: int, d_matches12, d_pairs,
+                                          d_npairs, bOnlyStereo: bool = False, stream=None) -> None:
+        """LocalMapping::CreateNewMapPoints' SearchForTriangulation loop over keyframes in
+        HBM (orbx_search_for_triangulation_batch_device): kfs = list of keyframe_device
+        records, pairs (P, 2) (KF1, KF2) indices into kfs, F12 (P, 3, 3) host floats,
+        cam the shared intrinsics + level tables.  Device outputs d_matches12 (P, cap),
+        d_pairs (P, cap, 2), d_npairs (P,) int32; asynchronous."""
+        pr = np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1, 2)
+        F = _f32(F12).reshape(-1, 9)
+        if len(F) != len(pr):
+            raise ValueError("one F12 per pair")
+        tab = (_KeyFrameDeviceC * max(len(kfs), 1))(*kfs)
+        cv = cam.c()
+        s = None if stream is None else C.c_void_p(getattr(stream, "cuda_stream", stream))
+        p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+        L.check(L.lib().orbx_search_for_triangulation_batch_device(
+            self._h, len(kfs), C.addressof(tab), C.addressof(cv), len(pr), pr.ctypes.data_as(I32P),
+            F.ctypes.data_as(F32P), 1 if bOnlyStereo else 0, int(cap), p(d_matches12), p(d_pairs), p(d_npairs), s))
 
     # SearchByBoW(KeyFrame* pKF, Frame& F, vpMapPointMatches)  ORBmatcher.cc:228-392
     def SearchByBoWFrame(self, kf: FrameView, kf_mp, kf_fv, f: FrameView, f_fv):

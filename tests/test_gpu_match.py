@@ -370,3 +370,105 @@ def test_match_sequence_device(oracle, orbx_built, small, prm):
         assert nm[p + 1] == nr
         assert np.array_equal(mp[p + 1][: n[p + 1]], ref)
         assert nr > 200
+
+
+def _kf_views(oracle, seed, prm=S.C1):
+    """Four keyframes of one canvas (two stereo, two monocular), their has-MapPoint
+    flags and FeatureVector CSRs."""
+    A, B = S.two_views(oracle, seed, stereo=True, prm=prm)
+    _, C = S.two_views(oracle, seed, dx=-5, dy=6, prm=prm)
+    _, D = S.two_views(oracle, seed, dx=11, dy=3, prm=prm)
+    rng = np.random.default_rng(seed + 21)
+    views = [A, B, C, D]
+    has = [(rng.random(len(V.keys)) < 0.2).astype(np.uint8) for V in views]
+    fvs = [S.fv(V, nnodes=40 if prm is S.C1 else 160) for V in views]
+    return views, has, fvs
+
+
+def _upload_kfs(views, has, fvs, cap, dev):
+    import torch
+    from orbslam2commentedbyxcm_amd.matcher import keyframe_device
+    keep, recs = [], []
+    for V, h, (fn, fo, fi) in zip(views, has, fvs):
+        n = len(V.keys)
+        assert n <= cap
+        kp = np.zeros((cap, 7), np.int32)
+        kp[:n] = np.ascontiguousarray(V.keys).view(np.int32).reshape(n, 7)
+        de = np.zeros((cap, 32), np.uint8)
+        de[:n] = V.desc
+        hm = np.zeros(cap, np.uint8)
+        hm[:n] = h
+        node = np.zeros(cap, np.int32)
+        node[:len(fn)] = fn
+        off = np.zeros(cap + 1, np.int32)
+        off[:len(fo)] = fo
+        idx = np.zeros(cap, np.int32)
+        idx[:len(fi)] = fi
+        t = {k: torch.from_numpy(v).to(dev) for k, v in
+             dict(kp=kp, de=de, hm=hm, node=node, off=off, idx=idx, n=np.array([n], np.int32),
+                  nfv=np.array([len(fn)], np.int32)).items()}
+        if V.u_right is not None:
+            ur = np.full(cap, -1.0, np.float32)
+            ur[:n] = V.u_right
+            t["ur"] = torch.from_numpy(ur).to(dev)
+        keep.append(t)
+        recs.append(keyframe_device(t["kp"], t["de"], t["n"], t["hm"], t["node"], t["off"], t["idx"], t["nfv"],
+                                    V.Tcw, t.get("ur")))
+    return keep, recs
+
+
+@pytest.mark.parametrize("seed,check_ori,only_stereo,prm", [(0, False, False, S.C1), (1, True, False, S.C1),
+                                                            (2, False, True, S.C1), (3, False, False, S.C5)])
+def test_search_for_triangulation_batch_device(oracle, orbx_built, seed, check_ori, only_stereo, prm):
+    """LocalMapping's SearchForTriangulation loop over keyframes in HBM: every ordered
+    pair of four keyframes (stereo and monocular) in one call, each pair's vMatchedPairs,
+    vMatches12 and count equal to the oracle's."""
+    import torch
+    views, has, fvs = _kf_views(oracle, seed, prm)
+    dev = torch.device("cuda", 0)
+    cap = max(len(V.keys) for V in views) + 37
+    keep, recs = _upload_kfs(views, has, fvs, cap, dev)
+    pairs = [(i, j) for i in range(4) for j in range(4) if i != j]
+    F12 = np.stack([S.fundamental(views[i], views[j]) for i, j in pairs])
+    P = len(pairs)
+    d_m12 = torch.empty((P, cap), dtype=torch.int32, device=dev)
+    d_pairs = torch.empty((P, cap, 2), dtype=torch.int32, device=dev)
+    d_np = torch.empty((P,), dtype=torch.int32, device=dev)
+    m = ORBmatcher(0.6, check_ori)
+    cam = FrameView(keys=views[0].keys[:0], desc=views[0].desc[:0], scale_factors=views[0].scale_factors,
+                    level_sigma2=views[0].level_sigma2)
+    m.SearchForTriangulationBatchDevice(recs, cam, np.array(pairs), F12, cap, d_m12, d_pairs, d_np,
+                                        bOnlyStereo=only_stereo)
+    torch.cuda.synchronize(dev)
+    m12, pg, npg = d_m12.cpu().numpy(), d_pairs.cpu().numpy(), d_np.cpu().numpy()
+    total = 0
+    for p, (i, j) in enumerate(pairs):
+        pr = oracle.search_for_triangulation(views[i], has[i], fvs[i], views[j], has[j], fvs[j], F12[p],
+                                             only_stereo, check_ori)
+        assert npg[p] == len(pr), (p, npg[p], len(pr))
+        assert np.array_equal(pg[p, :npg[p]], pr), p
+        want = np.full(cap, -1, np.int32)
+        want[pr[:, 0]] = pr[:, 1]
+        assert np.array_equal(m12[p], want), p
+        total += len(pr)
+    assert total > (20 if only_stereo else 200)
+    # the host call on the same pair agrees too (one table, two entry points)
+    i, j = pairs[0]
+    assert np.array_equal(m.SearchForTriangulation(views[i], has[i], fvs[i], views[j], has[j], fvs[j], F12[0],
+                                                   only_stereo), pg[0, :npg[0]])
+
+
+def test_search_for_triangulation_batch_device_rejects(orbx_built):
+    from orbslam2commentedbyxcm_amd import _lib as L
+    from orbslam2commentedbyxcm_amd.matcher import keyframe_device
+    import torch
+    dev = torch.device("cuda", 0)
+    z = torch.zeros(16, dtype=torch.int32, device=dev)
+    rec = keyframe_device(z, z, z, z, z, z, z, z, np.eye(4, dtype=np.float32))
+    m = ORBmatcher(0.6, False)
+    cam = FrameView(keys=np.zeros(0, L.KEYPOINT_DTYPE), desc=np.zeros((0, 32), np.uint8),
+                    scale_factors=np.ones(8, np.float32))
+    with pytest.raises(L.OrbxError):
+        m.SearchForTriangulationBatchDevice([rec], cam, np.array([[0, 1]]), np.zeros((1, 3, 3)), 8, z, z, z)
+    with pytest.raises(L.OrbxError):
+        m.SearchForTriangulationBatchDevice([rec], cam, np.array([[0, 0]]), np.zeros((1, 3, 3)), 9000, z, z, z)
