@@ -10,6 +10,10 @@ its covisible neighbours (LocalMapping.cc:235-305), which live on other ranks.  
 rank publishes its keyframe block -- keypoints, descriptors, has-MapPoint flags,
 vocabulary node per keypoint (the FeatureVector), pose -- and all-gathers the
 others'; the matching then runs locally on every rank.
+
+This module is the host-staged form (numpy KeyFrameBlocks, for callers whose keyframes
+live on the host).  The device-resident form -- one HBM slab per rank, all-gathered
+device to device, matched by one batched launch -- is keyframes.py (configs[3]).
 """
 from __future__ import annotations
 

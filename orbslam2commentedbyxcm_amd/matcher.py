@@ -50,6 +50,11 @@ def keyframe_device(keys, desc, n, has_mp, fv_node, fv_off, fv_idx, nfv, Tcw, u_
     return r
 
 
+def keyframe_table(records):
+    """A ctypes array of keyframe_device records (build once, pass to every call)."""
+    return (_KeyFrameDeviceC * max(len(records), 1))(*records)
+
+
 class _MapPointsC(C.Structure):
     _fields_ = [("n", C.c_int), ("pos", F32P), ("desc", U8P), ("observations", I32P), ("bad", U8P),
                 ("max_distance", F32P), ("min_distance", F32P), ("normal", F32P)]
@@ -323,12 +328,12 @@ class ORBmatcher:
         F = _f32(F12).reshape(-1, 9)
         if len(F) != len(pr):
             raise ValueError("one F12 per pair")
-        tab = (_KeyFrameDeviceC * max(len(kfs), 1))(*kfs)
+        tab = kfs if isinstance(kfs, C.Array) else keyframe_table(kfs)
         cv = cam.c()
         s = None if stream is None else C.c_void_p(getattr(stream, "cuda_stream", stream))
         p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
         L.check(L.lib().orbx_search_for_triangulation_batch_device(
-            self._h, len(kfs), C.addressof(tab), C.addressof(cv), len(pr), pr.ctypes.data_as(I32P),
+            self._h, len(tab) if len(kfs) else 0, C.addressof(tab), C.addressof(cv), len(pr), pr.ctypes.data_as(I32P),
             F.ctypes.data_as(F32P), 1 if bOnlyStereo else 0, int(cap), p(d_matches12), p(d_pairs), p(d_npairs), s))
 
     # SearchByBoW(KeyFrame* pKF, Frame& F, vpMapPointMatches)  ORBmatcher.cc:228-392

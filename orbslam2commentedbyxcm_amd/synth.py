@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import numpy as np
 
-__all__ = ["frame", "frames", "stereo_pair"]
+__all__ = ["frame", "frames", "stereo_pair", "StereoSequence"]
 
 
 def _rng(seed: int) -> np.random.Generator:
@@ -110,6 +110,35 @@ def sequence(seed: int, n: int, width: int = 640, height: int = 480, step: int =
         ox, oy = margin + off[i, 0], margin + off[i, 1]
         out[i] = canvas[oy:oy + height, ox:ox + width]
     return out, off
+
+
+class StereoSequence:
+    """Rectified stereo views of one fronto-parallel textured plane along a random walk
+    (configs[3]'s EuRoC-shaped stream).  The left camera of view i sits at canvas offset
+    off[i] (up to `step` px per axis per frame); the right camera, one stereo baseline to
+    its right, sees the plane `disp` px further along x, so right(x) = left(x + disp)
+    exactly.  views(idx) renders only the listed views (a rank renders its own shard)."""
+
+    def __init__(self, seed: int, n: int, width: int = 752, height: int = 480, step: int = 8, margin: int = 128,
+                 disp: int = 13):
+        self.width, self.height, self.margin, self.disp = width, height, margin, disp
+        self.canvas = frame(seed, width + 2 * margin + disp, height + 2 * margin, n_shapes=320)
+        g = _rng(seed + 7)
+        off = np.zeros((n, 2), dtype=np.int64)
+        for i in range(1, n):
+            off[i] = np.clip(off[i - 1] + g.integers(-step, step + 1, 2), -margin, margin)
+        self.off = off
+
+    def views(self, idx):
+        idx = list(idx)
+        W, H, m, d = self.width, self.height, self.margin, self.disp
+        left = np.empty((len(idx), H, W), dtype=np.uint8)
+        right = np.empty_like(left)
+        for k, i in enumerate(idx):
+            ox, oy = m + self.off[i, 0], m + self.off[i, 1]
+            left[k] = self.canvas[oy:oy + H, ox:ox + W]
+            right[k] = self.canvas[oy:oy + H, ox + d:ox + d + W]
+        return left, right
 
 
 def stereo_pair(seed: int, width: int = 1241, height: int = 376, max_disp: int = 64):

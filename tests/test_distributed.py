@@ -145,3 +145,85 @@ def test_triangulate_with_gathered_neighbours(oracle, orbx_built):
                                              nb.has_mp, feature_vector_csr(nb.fv_node), F12, False, False)
         assert np.array_equal(pg, pr), (len(pg), len(pr))
         assert len(pr) > 20
+
+
+# ---- configs[3]: keyframe slabs, the neighbour plan and the slab all-gather (keyframes.py)
+
+def test_slab_layout_fields_disjoint_and_aligned():
+    from orbslam2commentedbyxcm_amd.keyframes import SlabLayout
+    lay = SlabLayout(5, 1301)
+    spans = sorted((lay.offset[n], lay.offset[n] + 5 * lay.stride[n]) for n, *_ in SlabLayout.FIELDS)
+    assert all(a % 256 == 0 for a, _ in spans)
+    assert all(spans[i][1] <= spans[i + 1][0] for i in range(len(spans) - 1))
+    assert spans[-1][1] <= lay.nbytes and lay.nbytes % 256 == 0
+    assert lay.address(1000, 2, 3, "desc") == 1000 + 2 * lay.nbytes + lay.offset["desc"] + 3 * 1301 * 32
+
+
+@pytest.mark.parametrize("world,batch", [(1, 16), (2, 8), (8, 4)])
+def test_neighbour_plan(world, batch):
+    from orbslam2commentedbyxcm_amd import synth
+    from orbslam2commentedbyxcm_amd.keyframes import (EUROC, plan_neighbours, record_index, stream_poses,
+                                                      window_index)
+    s = EUROC
+    N = world * batch
+    seq = synth.StereoSequence.__new__(synth.StereoSequence)  # offsets only (no canvas needed)
+    rng = np.random.default_rng(1)
+    off = np.cumsum(rng.integers(-16, 17, (N, 2)), axis=0)
+    depth = s["bf"] / 13
+    T = stream_poses(off, s["fx"], s["fy"], depth)
+    mb = s["bf"] / s["fx"]
+    plans = [plan_neighbours(T, r, world, batch, 4, mb, s) for r in range(world)]
+    allpairs = set()
+    for r, pl in enumerate(plans):
+        assert len(pl.pairs) + pl.skipped_baseline == batch * min(4, N - 1)
+        for p in range(len(pl.pairs)):
+            g, h = int(pl.kf1_window[p]), int(pl.kf2_window[p])
+            assert g % world == r and g != h and abs(g - h) <= 4
+            assert tuple(pl.pairs[p]) == (record_index(g, world, batch), record_index(h, world, batch))
+            # baseline test passed: camera centres at least mb apart
+            assert np.hypot(*(off[g] - off[h])) * depth / s["fx"] >= mb * (1 - 1e-5)
+            assert np.allclose(pl.F12[p], compute_f12(T[g][:3], T[h][:3], s["fx"], s["fy"], s["cx"], s["cy"]))
+            allpairs.add((g, h))
+    # every rank plans its own keyframes: the union is the whole window's plan
+    assert {g for g, _ in allpairs} <= set(range(N))
+    assert all(window_index(g % world, g // world, world) == g for g in range(N))
+    del seq
+
+
+def _slab_worker(rank, world, port, outdir):
+    import torch
+    import torch.distributed as dist
+
+    from orbslam2commentedbyxcm_amd.keyframes import SlabLayout, gather_slabs
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        lay = SlabLayout(3, 50)
+        slab = torch.zeros(lay.nbytes, dtype=torch.uint8)
+        v = lay.views(slab)
+        for i in range(3):
+            v["desc"][i].fill_(10 * rank + i)
+            v["n"][i] = 100 * rank + i
+            v["fv_off"][i] = torch.arange(51, dtype=torch.int32) + rank
+        gathered = torch.zeros(world * lay.nbytes, dtype=torch.uint8)
+        gather_slabs(slab, gathered)
+        buf = gathered.numpy()
+        ok = True
+        for q in range(world):
+            for i in range(3):
+                d = buf[lay.address(0, q, i, "desc"):][:50 * 32]
+                n = buf[lay.address(0, q, i, "n"):][:4].view(np.int32)[0]
+                fo = buf[lay.address(0, q, i, "fv_off"):][:51 * 4].view(np.int32)
+                ok &= bool((d == 10 * q + i).all()) and n == 100 * q + i and bool((fo == np.arange(51) + q).all())
+        with open(os.path.join(outdir, f"s{rank}"), "w") as f:
+            f.write(f"{int(ok)}\n")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_slabs_gloo_world2(tmp_path):
+    import torch.multiprocessing as mp
+
+    world = 2
+    mp.spawn(_slab_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    assert all(open(tmp_path / f"s{r}").read().strip() == "1" for r in range(world))

@@ -1,0 +1,81 @@
+"""configs[3] on one GPU: the frame-sharded stereo keyframe pipeline
+(orbslam2commentedbyxcm_amd/keyframes.py) -- extraction of L and R, ComputeStereoMatches,
+ComputeBoW, close-point MapPoints and the batched SearchForTriangulation against stream
+neighbours -- checked keyframe by keyframe and pair by pair against the oracle, including
+the double-buffered (pipelined) steps."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("B,nn,steps", [(8, 4, 3), (12, 10, 2)])
+def test_keyframe_pipeline_matches_oracle(oracle, orbx_built, B, nn, steps):
+    import torch
+
+    import euroc_bench as E
+    from orbslam2commentedbyxcm_amd import synth
+    from orbslam2commentedbyxcm_amd.keyframes import StereoKeyFramePipeline
+    # a smaller tree of the same depth (k=8, L=6: FeatureVector nodes at level 2, 64 of them)
+    pl = StereoKeyFramePipeline(B, 0, 1, device=0, nn=nn, vocab_text=synth.vocabulary_text(11, 8, 6, 0, 0))
+    assert len(pl.plan.pairs) > B
+    pl.run(steps)
+    torch.cuda.synchronize()
+    res = pl.host_results()
+    assert pl.status()
+    ok = E.OracleKeyFrames(oracle, pl, oracle.Vocab(pl.vocab_text))
+    r = E.check(pl, ok, res, B, 8)
+    assert r["bit_exact"], r
+    assert r["pairs_checked"] == len(pl.plan.pairs)
+    assert r["mean_triangulation_matches_ref"] > 10, r
+    assert (res["ur"] >= 0).sum() > 50 * B
+
+
+def _rank(rank, world, port, outdir):
+    import json
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    import euroc_bench as E
+    from oracle import oracle as O
+    from orbslam2commentedbyxcm_amd import synth
+    from orbslam2commentedbyxcm_amd.keyframes import StereoKeyFramePipeline
+
+    # several ranks on the one GPU of the test box: gloo carries the slab exchange (the
+    # RCCL all_gather_into_tensor needs one GPU per rank); everything else is the N-GPU path
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        pl = StereoKeyFramePipeline(6, rank, world, device=0, nn=4, vocab_text=synth.vocabulary_text(11, 8, 6, 0, 0))
+        pl.run(3)
+        torch.cuda.synchronize()
+        res = pl.host_results()
+        out = {"pairs": len(pl.plan.pairs), "status": pl.status()}
+        O.build()
+        ok = E.OracleKeyFrames(O, pl, O.Vocab(pl.vocab_text))
+        out.update(E.check(pl, ok, res, 6, 4))
+        with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
+            json.dump(out, f)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_keyframe_pipeline_world2_gloo_on_one_gpu(orbx_built, tmp_path):
+    """The N-rank layout at world size 2: keyframe g on rank g % 2, neighbours read from the
+    gathered slabs (the other rank's keyframes), every rank's keyframes, gathered
+    neighbours and pair lists bit-exact vs the oracle."""
+    import json
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_rank, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        out = json.loads(open(tmp_path / f"r{r}.json").read())
+        assert out["status"] and out["bit_exact"], out
+        assert out["gathered_neighbours_checked"] > 6 and out["pairs_checked"] == out["pairs"] > 6, out
