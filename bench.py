@@ -352,8 +352,10 @@ def main():
     pipeline = match and not args.no_pipeline
     pl = SequencePipeline(B, W, H, lanes=args.lanes, pipelined=pipeline, match=match, device=local_rank,
                           fx=FX, fy=FY, cx=CX, cy=CY, depth=DEPTH, th=TH,
-                          small_matcher=os.environ.get("ORBX_MATCH_BIG", "0") != "1",
-                          match_stream=_match_stream(dev) if match else None)
+                          match_stream=_match_stream(dev) if match else None,
+                          nbuf=int(os.environ.get("ORBX_PIPE_NBUF", "2")),
+                          matcher_mode=None if "ORBX_MATCH_MODE" not in os.environ
+                          else int(os.environ["ORBX_MATCH_MODE"]))
     S = pl.S
     d_frames = torch.from_numpy(frames_np).to(dev)
     d_T = torch.from_numpy(T).to(dev)

@@ -334,11 +334,13 @@ int orbx_compute_distinctive_descriptors(int device, int nmp, const int32_t* off
 int orbx_compute_distinctive_descriptors_device(int nmp, const int32_t* d_off, const uint8_t* d_desc, int32_t* d_best,
                                                 uint8_t* d_out_desc, void* stream);
 
-/* Footprint of orbx_match_sequence_device's search kernel: 0 (default) = 1024 threads
- * per problem with keypoint descriptors and query state in LDS (fastest alone); 1 =
- * 256 threads and global-memory query state, for running concurrently with extraction
- * on another stream (leaves wave slots and LDS to the other kernels).  Same results. */
-int orbx_matcher_set_footprint(orbx_matcher* m, int small);
+/* Footprint of orbx_match_sequence_device's search: 0 (default) = one 1024-thread
+ * workgroup per problem with keypoint descriptors and query state in LDS (fastest alone);
+ * 1 = 256 threads and global-memory query state; 2 = split into three launches (grid
+ * sort per problem, scoring spread over all problems' queries, one wave per problem for
+ * the ordered commit), for running concurrently with extraction on another stream.
+ * Same results in every mode. */
+int orbx_matcher_set_footprint(orbx_matcher* m, int mode);
 
 /* HIP-event timing of orbx_match_sequence_device and orbx_compute_stereo_matches_batch_device:
  * milliseconds averaged over the (up to 64) most recent calls since

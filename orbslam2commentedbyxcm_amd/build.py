@@ -65,6 +65,31 @@ def build(verbose: bool = False) -> Path:
     return LIB
 
 
+def build_variant(tag: str, defines: list[str]) -> Path:
+    """A/B build: the same sources with extra -D defines into _ab/liborbx_<tag>.so (load
+    it with ORBX_LIB=...; tools/ab.sh, tools/ab_args.sh)."""
+    out_dir = CSRC.parent / "_ab"
+    obj = out_dir / f"obj_{tag}"
+    obj.mkdir(parents=True, exist_ok=True)
+    flags = FLAGS + [f"-D{d}" for d in defines]
+
+    def comp(src):
+        out = obj / (src + ".o")
+        r = subprocess.run([HIPCC, *flags, "-c", str(CSRC / src), "-o", str(out)], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src}:\n{r.stderr}")
+        return out
+
+    with cf.ThreadPoolExecutor(max_workers=4) as pool:
+        objs = list(pool.map(comp, SOURCES))
+    lib = out_dir / f"liborbx_{tag}.so"
+    r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(lib), *map(str, objs)],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    return lib
+
+
 def clean() -> None:
     shutil.rmtree(OBJ, ignore_errors=True)
     LIB.unlink(missing_ok=True)

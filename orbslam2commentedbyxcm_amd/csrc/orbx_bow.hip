@@ -24,6 +24,16 @@
 #include "orbx_kernels.h"
 
 namespace orbx {
+
+// Orders a wave's LDS accesses between the steps of a single-wave sequential loop (a
+// wave's LDS operations execute in issue order, so this only stops the compiler from
+// moving them).  Unlike a workgroup fence it does not wait for the wave's outstanding
+// global stores, which would put a memory round trip into every step.
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 namespace {
 
 constexpr int kBowThreads = 1024;
@@ -180,8 +190,7 @@ __global__ __launch_bounds__(kBowThreads) void k_bow(const BowProblem* __restric
                         atomicAdd(&s_hist[bin], 1);
                     }
                 }
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                __builtin_amdgcn_wave_barrier();
+                wave_lds_fence();
             }
         }
     }
@@ -383,8 +392,7 @@ __global__ __launch_bounds__(kBowThreads) void k_init(const InitProblem* __restr
                         s_hist[bin]++;
                     }
                 }
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                __builtin_amdgcn_wave_barrier();
+                wave_lds_fence();
             }
         }
         if (pb.check_ori && lane == 0) three_maxima(s_hist, s_ind);

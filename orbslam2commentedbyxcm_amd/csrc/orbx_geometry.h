@@ -18,7 +18,10 @@ constexpr int kEdge = 19;        // EDGE_THRESHOLD, ORBextractor.cc:46
 constexpr int kMinBorder = 16;   // EDGE_THRESHOLD - 3, ORBextractor.cc:1032
 constexpr int kMaxIni = 16;      // octree root nodes supported per level
 constexpr int kCellMax = 64;     // max detection-window width/height of a FAST cell
-constexpr int kLtTW = 64, kLtTH = 48;  // k_level_tiles output tile (columns x rows)
+#ifndef ORBX_LT_TH
+#define ORBX_LT_TH 48
+#endif
+constexpr int kLtTW = 64, kLtTH = ORBX_LT_TH;  // k_level_tiles output tile (columns x rows)
 
 // Parameters + derived per-level members (ORBextractor.h:204-219).
 struct OrbParams {

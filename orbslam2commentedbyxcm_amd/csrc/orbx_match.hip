@@ -112,6 +112,15 @@ __global__ __launch_bounds__(256) void k_window_match(const uint8_t* __restrict_
     }
 }
 
+// Orders a wave's LDS accesses between the steps of a single-wave sequential loop (a
+// wave's LDS operations execute in issue order, so this only stops the compiler from
+// moving them).  Unlike a workgroup fence it does not wait for the wave's outstanding
+// global stores, which would put a memory round trip into every step.
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // ------------------------------------------------------------------ projection search
 
 __device__ __forceinline__ bool kp_blocked(int fmp, const ProjParams& P) {
@@ -139,6 +148,7 @@ __device__ __forceinline__ CellRange cell_range(const ProjProblem& pb, float x, 
     return c;
 }
 
+constexpr int kXcds = 8;  // MI355X: 8 XCDs, workgroups dealt round robin, one L2 each
 constexpr unsigned kNoKey32 = 0xffffffffu;
 constexpr unsigned long long kNoKey = ~0ull;
 constexpr int kNoCell = 0xfff;
@@ -163,6 +173,7 @@ __device__ __forceinline__ int sk_oct(unsigned k) { return (int)(k & 31u); }
 
 constexpr int kProjThreads = 1024;      // default workgroup size of k_proj_search
 constexpr int kProjThreadsSmall = 256;  // small-footprint variant (overlapped with other work)
+constexpr int kProjThreadsTiny = 64;    // one wave per problem (a background stream's footprint)
 constexpr int kTopK = 8;                   // candidate-list length per query
 constexpr unsigned kNoEntry = 0xffffffffu;  // no further candidate
 constexpr unsigned kTrunc = 0xfffffffeu;    // further candidates exist but are not listed
@@ -258,7 +269,7 @@ __device__ void score_rowk(const ProjProblem& pb, const ProjParams& P, const Que
                     const float disty = kp.y - Q.v;
                     if (!(fabsf(distx) < Q.r && fabsf(disty) < Q.r)) continue;
                     if (Q.post_max >= 0 && (oct < Q.post_min || oct > Q.post_max)) continue;
-                    if (kp_blocked(sfmp[p], P)) continue;
+                    if (sfmp && kp_blocked(sfmp[p], P)) continue;  // null: nothing claimed yet
                     int d;
                     if (G.sdesc) {
                         if (Q.er_max >= 0.f && pb.u_right) {
@@ -346,14 +357,15 @@ __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~(siz
 
 // LDS layout of k_proj_search (byte offsets), shared by the kernel and its launcher.
 struct ProjLds {
-    size_t skey, cstart, sxy, sfmp, owner, sdesc, qk, qmp, qang, mlist, mbin, total;
+    size_t skey, cstart, sxy, sfmp, owner, sang, sdesc, qk, qmp, qang, mlist, mbin, total;
     __host__ __device__ ProjLds(int n, int n2, int nq, bool dlds, bool qlds) {
         skey = 0;
         cstart = align16((size_t)n2 * 4);
         sxy = align16(cstart + (size_t)(kNumCells + 1) * 2);
         sfmp = sxy + (size_t)n * 8;
         owner = sfmp + (size_t)n * 4;
-        size_t o = align16(owner + (size_t)n * 4);
+        sang = owner + (size_t)n * 4;  // keypoint angles in sorted order: the replay's histogram bins
+        size_t o = align16(sang + (size_t)n * 4);
         sdesc = o;
         if (dlds) o += (size_t)n * 32;
         qk = o;
@@ -364,6 +376,158 @@ struct ProjLds {
         total = qlds ? mbin + (size_t)nq * 4 : o;
     }
 };
+
+// Wave 0's sequential replay (H5) of one problem over the per-query candidate lists qk
+// (8 entries per query) built by the scoring phase: every query takes the first still
+// unclaimed entries of its list, the queries of a 64-query chunk before the first one an
+// earlier query of the chunk touches commit together, a query whose list ran out is
+// re-scored against the current claims; then the rotation histogram (ORBmatcher.cc:
+// 1750-1786, 1935-1977).  sfmp / owner: the claims and the owner map by sorted position
+// (LDS); angle_of(p): the angle of the keypoint at sorted position p.  Whole wave active.
+template <typename AngleFn>
+__device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const SortedGrid& G, int* sfmp, int* owner,
+                            const uint4* qk, const int* qmp, const float* qang, int* mlist, int* mbin, int* s_hist,
+                            AngleFn angle_of, unsigned long long* st) {
+    const int lane = threadIdx.x & 63;
+    const int nq = pb.nq;
+    int nmatch = 0, nrec = 0, nrescore = 0, niter = 0;
+    const float factor = kHistoLength / 360.0f;
+    const int need = P.ratio_mode ? 2 : 1;
+    const unsigned long long below = (1ull << lane) - 1;
+    for (int base = 0; base < nq; base += 64) {
+        const int q = base + lane;
+        int mp = -1;
+        float qa = 0.f;
+        unsigned e[kTopK];
+#pragma unroll
+        for (int j = 0; j < kTopK; j++) e[j] = kNoEntry;
+        QueryReg mine;  // consumed only by a re-scoring (loads overlap the first round)
+        if (q < nq) mine = load_query(pb, q);
+        if (q < nq) {
+            mp = qmp[q];
+            const uint4 v = qk[2 * q], w = qk[2 * q + 1];
+            e[0] = v.x; e[1] = v.y; e[2] = v.z; e[3] = v.w;
+            e[4] = w.x; e[5] = w.y; e[6] = w.z; e[7] = w.w;
+            qa = qang[q];
+        }
+        int start = 0;
+        while (true) {
+            niter++;
+            const bool act = lane >= start && mp >= 0;
+            unsigned c1 = kNoEntry, c2 = kNoEntry;
+            bool exhausted = false;
+            if (act) {
+                int found = 0;
+#pragma unroll
+                for (int j = 0; j < kTopK; j++) {
+                    if (e[j] < kTrunc && found < 2 && !kp_blocked(sfmp[ent_pos(e[j])], P)) {
+                        if (found == 0) c1 = e[j];
+                        else c2 = e[j];
+                        found++;
+                    }
+                }
+                // a full (or truncated) list may hide unlisted candidates
+                exhausted = e[kTopK - 1] != kNoEntry && found < need;
+            }
+            bool acc = false;
+            if (act && !exhausted && c1 != kNoEntry && ent_dist(c1) <= P.accept_th) {
+                acc = true;
+                if (P.ratio_mode) {
+                    const int bestLevel2 = c2 == kNoEntry ? -1 : ent_oct(c2);
+                    const int bestDist2 = c2 == kNoEntry ? 256 : ent_dist(c2);
+                    if (ent_oct(c1) == bestLevel2 && (float)ent_dist(c1) > P.nnratio * (float)bestDist2)
+                        acc = false;
+                }
+            }
+            const int tpos = acc ? ent_pos(c1) : -1;
+            // A query depends on an earlier one of the chunk if that one claims its best
+            // (or, with the ratio test, second best) keypoint.
+            // owner[p] = lowest lane of this round claiming p (LDS ops of a wave are
+            // executed in order: all atomics, then all reads, then the reset).
+            if (acc) atomicMin(&owner[tpos], lane);
+            bool conf = exhausted;
+            if (act && !exhausted) {
+                if (c1 != kNoEntry && owner[ent_pos(c1)] < lane) conf = true;
+                if (P.ratio_mode && c2 != kNoEntry && owner[ent_pos(c2)] < lane) conf = true;
+            }
+            if (acc) owner[tpos] = 0x7fffffff;
+            const unsigned long long cm = __ballot(conf);
+            const int f = cm ? __ffsll((long long)cm) - 1 : 64;
+            const bool com = acc && lane < f;
+            const unsigned long long comm = __ballot(com);
+            if (com) sfmp[tpos] = mp;
+            nmatch += __popcll(comm);
+            if (P.check_ori) {
+                if (com) {
+                    float rot = qa - angle_of(tpos);
+                    if (rot < 0.0f) rot += 360.0f;
+                    int bin = (int)roundf(rot * factor);
+                    if (bin == kHistoLength) bin = 0;
+                    const int r = nrec + __popcll(comm & below);
+                    mlist[r] = tpos;
+                    mbin[r] = bin;
+                    atomicAdd(&s_hist[bin], 1);
+                }
+                nrec += __popcll(comm);
+            }
+            if (f >= 64) break;
+            if (__builtin_amdgcn_readlane((int)exhausted, f)) {
+                nrescore++;
+                wave_lds_fence();
+                unsigned ne[kTopK];
+                score_rowk(pb, P, bcast_query(mine, f), lane < 16, G, sfmp, ne);
+#pragma unroll
+                for (int j = 0; j < kTopK; j++) {
+                    const unsigned v = (unsigned)__builtin_amdgcn_readlane((int)ne[j], 0);
+                    if (lane == f) e[j] = v;
+                }
+            }
+            start = f;
+            wave_lds_fence();
+        }
+        wave_lds_fence();
+    }
+    // the match list (global scratch in some modes) is read back by other lanes below
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    if (P.check_ori) {
+        // ComputeThreeMaxima, ORBmatcher.cc:1935-1977
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < kHistoLength; i++) {
+            const int s = s_hist[i];
+            if (s > max1) {
+                max3 = max2; max2 = max1; max1 = s;
+                ind3 = ind2; ind2 = ind1; ind1 = i;
+            } else if (s > max2) {
+                max3 = max2; max2 = s;
+                ind3 = ind2; ind2 = i;
+            } else if (s > max3) {
+                max3 = s;
+                ind3 = i;
+            }
+        }
+        if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+        else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+        int bad = 0;
+        for (int m = lane; m < nrec; m += 64) {
+            const int b = mbin[m];
+            if (b != ind1 && b != ind2 && b != ind3) {
+                sfmp[mlist[m]] = -1;
+                bad++;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o);
+        nmatch -= bad;
+    }
+    if (lane == 0) *pb.nmatches = nmatch;
+    if (st && lane == 0) {
+        st[3] = wall_clock64();
+        st[5] = nrescore;
+        st[6] = nq;
+        st[7] = niter;
+    }
+}
 
 // One workgroup per problem (one SearchByProjection call).
 //  1. the frame's keypoints are sorted into grid order in LDS (with their descriptors
@@ -401,6 +565,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     float2* sxy = (float2*)(smem + L.sxy);
     int* sfmp = (int*)(smem + L.sfmp);
     int* owner = (int*)(smem + L.owner);
+    float* sang = (float*)(smem + L.sang);
     uint4* sdesc = DLDS ? (uint4*)(smem + L.sdesc) : nullptr;
     uint4* qk;
     int *qmp, *mlist, *mbin;
@@ -439,6 +604,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
         sxy[p] = make_float2(kp.x, kp.y);
         sfmp[p] = pb.frame_mp[i];
         owner[p] = 0x7fffffff;
+        sang[p] = kp.angle;
     }
     if (DLDS) {
         for (int t = tid; t < 2 * n; t += NT) {
@@ -479,148 +645,200 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     }
     __syncthreads();
     if (st && tid == 0) st[2] = wall_clock64();
-    if (wave == 0) {
-        int nmatch = 0, nrec = 0, nrescore = 0, niter = 0;
-        const float factor = kHistoLength / 360.0f;
-        const int need = P.ratio_mode ? 2 : 1;
-        const unsigned long long below = (1ull << lane) - 1;
-        for (int base = 0; base < nq; base += 64) {
-            const int q = base + lane;
-            int mp = -1;
-            float qa = 0.f;
-            unsigned e[kTopK];
-#pragma unroll
-            for (int j = 0; j < kTopK; j++) e[j] = kNoEntry;
-            QueryReg mine;  // consumed only by a re-scoring (loads overlap the first round)
-            if (q < nq) mine = load_query(pb, q);
-            if (q < nq) {
-                mp = qmp[q];
-                const uint4 v = qk[2 * q], w = qk[2 * q + 1];
-                e[0] = v.x; e[1] = v.y; e[2] = v.z; e[3] = v.w;
-                e[4] = w.x; e[5] = w.y; e[6] = w.z; e[7] = w.w;
-                qa = qang[q];
-            }
-            int start = 0;
-            while (true) {
-                niter++;
-                const bool act = lane >= start && mp >= 0;
-                unsigned c1 = kNoEntry, c2 = kNoEntry;
-                bool exhausted = false;
-                if (act) {
-                    int found = 0;
-#pragma unroll
-                    for (int j = 0; j < kTopK; j++) {
-                        if (e[j] < kTrunc && found < 2 && !kp_blocked(sfmp[ent_pos(e[j])], P)) {
-                            if (found == 0) c1 = e[j];
-                            else c2 = e[j];
-                            found++;
-                        }
-                    }
-                    // a full (or truncated) list may hide unlisted candidates
-                    exhausted = e[kTopK - 1] != kNoEntry && found < need;
-                }
-                bool acc = false;
-                if (act && !exhausted && c1 != kNoEntry && ent_dist(c1) <= P.accept_th) {
-                    acc = true;
-                    if (P.ratio_mode) {
-                        const int bestLevel2 = c2 == kNoEntry ? -1 : ent_oct(c2);
-                        const int bestDist2 = c2 == kNoEntry ? 256 : ent_dist(c2);
-                        if (ent_oct(c1) == bestLevel2 && (float)ent_dist(c1) > P.nnratio * (float)bestDist2)
-                            acc = false;
-                    }
-                }
-                const int tpos = acc ? ent_pos(c1) : -1;
-                // A query depends on an earlier one of the chunk if that one claims its best
-                // (or, with the ratio test, second best) keypoint.
-                // owner[p] = lowest lane of this round claiming p (LDS ops of a wave are
-                // executed in order: all atomics, then all reads, then the reset).
-                if (acc) atomicMin(&owner[tpos], lane);
-                bool conf = exhausted;
-                if (act && !exhausted) {
-                    if (c1 != kNoEntry && owner[ent_pos(c1)] < lane) conf = true;
-                    if (P.ratio_mode && c2 != kNoEntry && owner[ent_pos(c2)] < lane) conf = true;
-                }
-                if (acc) owner[tpos] = 0x7fffffff;
-                const unsigned long long cm = __ballot(conf);
-                const int f = cm ? __ffsll((long long)cm) - 1 : 64;
-                const bool com = acc && lane < f;
-                const unsigned long long comm = __ballot(com);
-                if (com) sfmp[tpos] = mp;
-                nmatch += __popcll(comm);
-                if (P.check_ori) {
-                    if (com) {
-                        float rot = qa - pb.keys[sk_idx(skey[tpos])].angle;
-                        if (rot < 0.0f) rot += 360.0f;
-                        int bin = (int)roundf(rot * factor);
-                        if (bin == kHistoLength) bin = 0;
-                        const int r = nrec + __popcll(comm & below);
-                        mlist[r] = tpos;
-                        mbin[r] = bin;
-                        atomicAdd(&s_hist[bin], 1);
-                    }
-                    nrec += __popcll(comm);
-                }
-                if (f >= 64) break;
-                if (__builtin_amdgcn_readlane((int)exhausted, f)) {
-                    nrescore++;
-                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                    __builtin_amdgcn_wave_barrier();
-                    unsigned ne[kTopK];
-                    score_rowk(pb, P, bcast_query(mine, f), lane < 16, G, sfmp, ne);
-#pragma unroll
-                    for (int j = 0; j < kTopK; j++) {
-                        const unsigned v = (unsigned)__builtin_amdgcn_readlane((int)ne[j], 0);
-                        if (lane == f) e[j] = v;
-                    }
-                }
-                start = f;
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                __builtin_amdgcn_wave_barrier();
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-            __builtin_amdgcn_wave_barrier();
+    // The replay is wave 0's alone: the other waves leave now, so their registers and
+    // wave slots go back to whatever runs beside this kernel for the rest of its life.
+    if (wave != 0) return;
+    proj_replay(pb, P, G, sfmp, owner, qk, qmp, qang, mlist, mbin, s_hist,
+                [&](int tpos) { return sang[tpos]; }, st);
+    wave_lds_fence();
+    for (int p = lane; p < n; p += 64) pb.frame_mp[sk_idx(skey[p])] = sfmp[p];
+    if (st && lane == 0) st[4] = wall_clock64();
+}
+
+// ---- the batched sequence matcher in three launches (orbx_match_sequence_device)
+//
+// k_proj_search keeps a whole workgroup per problem for the grid sort, the scoring and
+// the replay, so most of its lifetime is one wave replaying while the rest of the
+// workgroup's slots and LDS sit idle beside the extraction.  The sequence path splits it:
+//   k_seq_grid    one workgroup per problem: the current frame's keypoints sorted into
+//                 grid order (the SortedGrid, here in global memory, with the sorted
+//                 descriptors and angles);
+//   k_seq_score   16 queries per workgroup over all problems (XCD-aware: a problem's
+//                 workgroups share one L2 with its grid): each query's 8-entry list;
+//   k_seq_commit  one wave per problem: the replay (proj_replay) with the claims in LDS.
+// Results are identical to k_proj_search's (same lists, same replay).
+
+// Byte layout of one problem's grid in the global grid area.
+struct SeqGridLayout {
+    size_t skey, cstart, sxy, sang, sdesc, total;
+    __host__ __device__ SeqGridLayout(int cap) {
+        int n2 = 1;
+        while (n2 < cap) n2 <<= 1;
+        skey = 0;
+        cstart = align16((size_t)n2 * 4);
+        sxy = align16(cstart + (size_t)(kNumCells + 1) * 2);
+        sang = align16(sxy + (size_t)cap * 8);
+        sdesc = align16(sang + (size_t)cap * 4);
+        total = (sdesc + (size_t)cap * 32 + 255) & ~(size_t)255;
+    }
+};
+
+__device__ __forceinline__ SortedGrid seq_grid(unsigned char* base, const SeqGridLayout& g) {
+    return SortedGrid{(const unsigned*)(base + g.skey), (const uint16_t*)(base + g.cstart),
+                      (const float2*)(base + g.sxy), (const uint4*)(base + g.sdesc)};
+}
+
+constexpr int kSeqGridThreads = 256;
+
+__global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem* __restrict__ probs,
+                                                              unsigned char* __restrict__ grids, int cap) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const ProjProblem pb = probs[blockIdx.x];
+    const SeqGridLayout gl(cap);
+    unsigned char* gb = grids + (size_t)blockIdx.x * gl.total;
+    const int tid = threadIdx.x, n = pb.n;
+    int n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    unsigned* skey = (unsigned*)smem;
+    for (int i = tid; i < n2; i += kSeqGridThreads) {
+        unsigned key = 0xffffffffu;
+        if (i < n) {
+            const orbx_keypoint& kp = pb.keys[i];
+            const int px = (int)roundf((kp.x - pb.min_x) * pb.inv_w);  // Frame::PosInGrid, Frame.cc:558-567
+            const int py = (int)roundf((kp.y - pb.min_y) * pb.inv_h);
+            const int cell = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? kNoCell : px * kGridRows + py;
+            key = ((unsigned)cell << 18) | ((unsigned)i << 5) | ((unsigned)kp.octave & 31u);
         }
-        if (P.check_ori) {
-            // ComputeThreeMaxima, ORBmatcher.cc:1935-1977
-            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
-            for (int i = 0; i < kHistoLength; i++) {
-                const int s = s_hist[i];
-                if (s > max1) {
-                    max3 = max2; max2 = max1; max1 = s;
-                    ind3 = ind2; ind2 = ind1; ind1 = i;
-                } else if (s > max2) {
-                    max3 = max2; max2 = s;
-                    ind3 = ind2; ind2 = i;
-                } else if (s > max3) {
-                    max3 = s;
-                    ind3 = i;
-                }
-            }
-            if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
-            else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
-            int bad = 0;
-            for (int m = lane; m < nrec; m += 64) {
-                const int b = mbin[m];
-                if (b != ind1 && b != ind2 && b != ind3) {
-                    sfmp[mlist[m]] = -1;
-                    bad++;
-                }
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o);
-            nmatch -= bad;
-        }
-        if (lane == 0) *pb.nmatches = nmatch;
-        if (st && tid == 0) {
-            st[3] = wall_clock64();
-            st[5] = nrescore;
-            st[6] = nq;
-            st[7] = niter;
-        }
+        skey[i] = key;
     }
     __syncthreads();
-    for (int p = tid; p < n; p += NT) pb.frame_mp[sk_idx(skey[p])] = sfmp[p];
-    if (st && tid == 0) st[4] = wall_clock64();
+    block_bitonic_sort<kSeqGridThreads>(skey, n2);
+    unsigned* gkey = (unsigned*)(gb + gl.skey);
+    float2* sxy = (float2*)(gb + gl.sxy);
+    float* sang = (float*)(gb + gl.sang);
+    uint4* sdesc = (uint4*)(gb + gl.sdesc);
+    uint16_t* cstart = (uint16_t*)(gb + gl.cstart);
+    for (int p = tid; p < n; p += kSeqGridThreads) {
+        const unsigned k = skey[p];
+        const int i = sk_idx(k);
+        const orbx_keypoint& kp = pb.keys[i];
+        gkey[p] = k;
+        sxy[p] = make_float2(kp.x, kp.y);
+        sang[p] = kp.angle;
+    }
+    for (int t = tid; t < 2 * n; t += kSeqGridThreads) {
+        const int i = sk_idx(skey[t >> 1]);
+        sdesc[t] = ((const uint4*)(pb.desc + (size_t)i * 32))[t & 1];
+    }
+    for (int p = tid; p <= n; p += kSeqGridThreads) {
+        const int prev = p == 0 ? -1 : (int)(skey[p - 1] >> 18);
+        const int cur = p == n ? kNumCells : (int)(skey[p] >> 18);
+        const int hi = cur < kNumCells ? cur : kNumCells;
+        for (int c = prev + 1; c <= hi; c++) cstart[c] = (uint16_t)p;
+    }
+}
+
+constexpr int kSeqScoreThreads = 256;  // 16 queries (4 per wave, one 16-lane row each)
+constexpr int kSeqScoreQ = kSeqScoreThreads / 16;
+
+__global__ __launch_bounds__(kSeqScoreThreads) void k_seq_score(const ProjProblem* __restrict__ probs, int nprob,
+                                                                int qblocks, ProjParams P,
+                                                                unsigned char* __restrict__ grids, int cap,
+                                                                unsigned long long* __restrict__ scratch,
+                                                                const long long* __restrict__ scratch_off) {
+    // XCD x (= lin % 8) runs problems x, x + 8, ...: a problem's workgroups share its L2
+    const int lin = blockIdx.x, x = lin % kXcds, k = lin / kXcds;
+    const int j = k / qblocks, blk = k - j * qblocks;
+    const int p = x + kXcds * j;
+    if (p >= nprob) return;  // whole workgroup: XCD x has fewer problems
+    const ProjProblem pb = probs[p];
+    const SeqGridLayout gl(cap);
+    const SortedGrid G = seq_grid(grids + (size_t)p * gl.total, gl);
+    const int q = blk * kSeqScoreQ + (threadIdx.x >> 4);
+    if (blk * kSeqScoreQ >= pb.nq) return;  // whole workgroup past the queries
+    const QueryReg cur = load_query(pb, min(q, pb.nq - 1));
+    const int mp = q < pb.nq ? cur.q.mp : -1;
+    unsigned e[kTopK];
+    score_rowk(pb, P, cur, mp >= 0, G, nullptr, e);
+    if ((threadIdx.x & 15) == 0 && q < pb.nq) {
+        unsigned long long* g = scratch + scratch_off[p];
+        uint4* qk = (uint4*)g;
+        int* qmp = (int*)(g + 4 * (size_t)pb.nq);
+        float* qang = (float*)(qmp + pb.nq);
+        qk[2 * q] = make_uint4(e[0], e[1], e[2], e[3]);
+        qk[2 * q + 1] = make_uint4(e[4], e[5], e[6], e[7]);
+        qmp[q] = mp;
+        qang[q] = cur.q.angle;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_seq_commit(const ProjProblem* __restrict__ probs, ProjParams P,
+                                                   unsigned char* __restrict__ grids, int cap,
+                                                   unsigned long long* __restrict__ scratch,
+                                                   const long long* __restrict__ scratch_off) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ int s_hist[kHistoLength];
+    const ProjProblem pb = probs[blockIdx.x];
+    const SeqGridLayout gl(cap);
+    const SortedGrid G = seq_grid(grids + (size_t)blockIdx.x * gl.total, gl);
+    const float* gang = (const float*)(grids + (size_t)blockIdx.x * gl.total + gl.sang);
+    const int lane = threadIdx.x, n = pb.n, nq = pb.nq;
+    int* sfmp = (int*)smem;
+    int* owner = sfmp + n;
+    float* sang = (float*)(owner + n);
+    for (int p = lane; p < n; p += 64) {
+        sfmp[p] = pb.frame_mp[sk_idx(G.skey[p])];
+        owner[p] = 0x7fffffff;
+        sang[p] = gang[p];
+    }
+    if (lane < kHistoLength) s_hist[lane] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    unsigned long long* g = scratch + scratch_off[blockIdx.x];
+    const uint4* qk = (const uint4*)g;
+    const int* qmp = (const int*)(g + 4 * (size_t)nq);
+    const float* qang = (const float*)(qmp + nq);
+    int* mlist = (int*)(qang + nq);
+    int* mbin = mlist + nq;
+    proj_replay(pb, P, G, sfmp, owner, qk, qmp, qang, mlist, mbin, s_hist, [&](int tpos) { return sang[tpos]; },
+                nullptr);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    for (int p = lane; p < n; p += 64) pb.frame_mp[sk_idx(G.skey[p])] = sfmp[p];
+}
+
+size_t seq_grid_bytes(int cap) { return SeqGridLayout(cap).total; }
+
+hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned char* grids,
+                            int cap, unsigned long long* scratch, const long long* d_scratch_off, hipStream_t stream) {
+    if (nprob <= 0) return hipSuccess;
+    if (cap <= 0 || cap >= 8192) return hipErrorInvalidValue;  // 13-bit keypoint positions
+    int n2 = 1;
+    while (n2 < cap) n2 <<= 1;
+    const size_t lds_grid = (size_t)n2 * 4;
+    const size_t lds_commit = (size_t)cap * 12;
+    if (lds_grid > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_seq_grid, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds_grid);
+        if (e != hipSuccess) return e;
+    }
+    if (lds_commit > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_seq_commit, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds_commit);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_seq_grid, dim3(nprob), dim3(kSeqGridThreads), lds_grid, stream, d_probs, grids, cap);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int qblocks = (cap + kSeqScoreQ - 1) / kSeqScoreQ;
+    const int per_xcd = (nprob + kXcds - 1) / kXcds;
+    hipLaunchKernelGGL(k_seq_score, dim3(kXcds * per_xcd * qblocks), dim3(kSeqScoreThreads), 0, stream, d_probs,
+                       nprob, qblocks, P, grids, cap, scratch, d_scratch_off);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_seq_commit, dim3(nprob), dim3(64), lds_commit, stream, d_probs, P, grids, cap, scratch,
+                       d_scratch_off);
+    return hipGetLastError();
 }
 
 // Batched TrackWithMotionModel matching over a device-resident sequence: problem p
@@ -704,7 +922,8 @@ hipError_t launch_seq_build(const SeqArgs& A, int npairs, ProjQuery* queries, Pr
 }
 
 hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned long long* scratch,
-                              const long long* d_scratch_off, int max_n, int max_nq, hipStream_t stream, bool small) {
+                              const long long* d_scratch_off, int max_n, int max_nq, hipStream_t stream, bool small,
+                              bool tiny) {
     if (nprob <= 0) return hipSuccess;
     if (max_n >= 8192) return hipErrorInvalidValue;  // 13-bit keypoint positions
     int n2 = 1;
@@ -712,6 +931,7 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
     const size_t limit = 160 * 1024 - 256;  // minus the static histogram
     // Fast: LDS-resident descriptors (the scoring loads), then LDS-resident query state,
     // 1024 threads.  Small (meant to run beside other kernels): neither, 256 threads.
+    small = small || tiny;
     bool dlds = !small, qlds = !small;
     if (!small && ProjLds(max_n, n2, max_nq, true, true).total > limit) {
         qlds = false;
@@ -723,7 +943,10 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
     const size_t lds = ProjLds(max_n, n2, max_nq, dlds, qlds).total;
     if (lds > limit) return hipErrorInvalidValue;
     const void* fn;
-    if (small)
+    const int nt = tiny ? kProjThreadsTiny : (small ? kProjThreadsSmall : kProjThreads);
+    if (tiny)
+        fn = (const void*)k_proj_search<false, false, kProjThreadsTiny>;
+    else if (small)
         fn = (const void*)k_proj_search<false, false, kProjThreadsSmall>;
     else
         fn = qlds ? (dlds ? (const void*)k_proj_search<true, true, kProjThreads>
@@ -735,7 +958,7 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
         if (e != hipSuccess) return e;
     }
     void* args[] = {(void*)&d_probs, (void*)&P, (void*)&scratch, (void*)&d_scratch_off};
-    return hipLaunchKernel(fn, dim3(nprob), dim3(small ? kProjThreadsSmall : kProjThreads), args, lds, stream);
+    return hipLaunchKernel(fn, dim3(nprob), dim3(nt), args, lds, stream);
 }
 
 // ------------------------------------------------------------------ triangulation
@@ -861,8 +1084,7 @@ __global__ __launch_bounds__(kTriThreads) void k_triangulation(const TriProblem*
                     }
                     nrec++;
                 }
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                __builtin_amdgcn_wave_barrier();
+                wave_lds_fence();
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");

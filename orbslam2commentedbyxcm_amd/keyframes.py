@@ -25,7 +25,7 @@ keyframes whose views overlap most, then the baseline skip) depends only on the 
 is made once on the host, as LocalMapping does per keyframe.
 
 tests/euroc_bench.py (bench.py --workload euroc) times this object;
-tests/test_gpu_keyframes.py checks its output against the CPU oracle, and
+tests/test_gpu_keyframes.py checks its output against the CPU parity oracle, and
 tests/test_distributed.py covers the layout, the plan and the gather at world size 2 on
 gloo.
 """

@@ -428,10 +428,11 @@ class ORBmatcher:
     def set_timing(self, enable: bool = True) -> None:
         L.check(L.lib().orbx_matcher_set_timing(self._h, 1 if enable else 0))
 
-    def set_footprint(self, small: bool) -> None:
-        """small=True: the batched sequence search uses 256 threads and global query
-        state, to run beside extraction on another stream (orbx_matcher_set_footprint)."""
-        L.check(L.lib().orbx_matcher_set_footprint(self._h, 1 if small else 0))
+    def set_footprint(self, mode) -> None:
+        """Search-kernel footprint of match_sequence_device (orbx_matcher_set_footprint):
+        0 / False = one 1024-thread workgroup per problem, 1 / True = 256 threads with
+        global query state, 2 = split into grid / score / commit launches."""
+        L.check(L.lib().orbx_matcher_set_footprint(self._h, int(mode)))
 
     def last_ms(self) -> float:
         t = C.c_float()

@@ -29,7 +29,8 @@ class SequencePipeline:
     def __init__(self, batch: int, width: int, height: int, lanes: int = 2, pipelined: bool = True,
                  match: bool = True, device: int = 0, params=(1000, 1.2, 8, 20, 7), fx: float = 500.0,
                  fy: float = 500.0, cx: float = 320.0, cy: float = 240.0, depth: float = 5.0, th: float = 15.0,
-                 nnratio: float = 0.9, check_ori: bool = True, small_matcher: bool = True, match_stream=None):
+                 nnratio: float = 0.9, check_ori: bool = True, match_stream=None,
+                 nbuf: int = 2, matcher_mode: int | None = None):
         import torch
 
         self.B, self.W, self.H = int(batch), int(width), int(height)
@@ -40,13 +41,16 @@ class SequencePipeline:
         self.fx, self.fy, self.cx, self.cy, self.depth, self.th = fx, fy, cx, cy, depth, th
         self.exs = [ORBextractor(*params, device=device) for _ in range(self.S)]
         self.matcher = ORBmatcher(nnratio, check_ori, device=device)
-        self.matcher.set_footprint(small_matcher and self.pipelined)
+        # matcher_mode: orbx_matcher_set_footprint.  Default 0 (one 1024-thread workgroup per
+        # problem): beside the pipelined extraction it measured 182-184k frames/s against
+        # 176-181k for 1 (256 threads) and 167-169k for 2 (split launches), profiles/r02_e_*
+        self.matcher.set_footprint(0 if matcher_mode is None else matcher_mode)
         self.sf = self.exs[0].GetScaleFactors()
         self.cap = self.exs[0].max_keypoints(self.W, self.H)
         self.bounds = [(self.B * c // self.S, self.B * (c + 1) // self.S) for c in range(self.S)]
         self.streams = [torch.cuda.ExternalStream(e.stream_handle(), device=self.dev) for e in self.exs]
         self.ms = match_stream if match_stream is not None else torch.cuda.Stream(device=self.dev)
-        nbuf = 2 if self.pipelined else 1
+        nbuf = max(2, int(nbuf)) if self.pipelined else 1
         B, cap = self.B, self.cap
         i32 = dict(dtype=torch.int32, device=self.dev)
         self.kps = [torch.empty((B, cap, 7), **i32) for _ in range(nbuf)]

@@ -18,12 +18,12 @@ from orbslam2commentedbyxcm_amd.pipeline import SequencePipeline, sequence_poses
 pytestmark = pytest.mark.gpu
 
 
-def _run(B, lanes, pipelined, steps, seed=1000):
+def _run(B, lanes, pipelined, steps, seed=1000, matcher_mode=None):
     import torch
 
     frames, off = synth.sequence(seed, B)
     T = sequence_poses(off)
-    pl = SequencePipeline(B, 640, 480, lanes=lanes, pipelined=pipelined)
+    pl = SequencePipeline(B, 640, 480, lanes=lanes, pipelined=pipelined, matcher_mode=matcher_mode)
     d_frames = torch.from_numpy(frames).to(pl.dev)
     d_T = torch.from_numpy(T).to(pl.dev)
     torch.cuda.synchronize()
@@ -32,10 +32,12 @@ def _run(B, lanes, pipelined, steps, seed=1000):
     return frames, T, pl
 
 
-@pytest.mark.parametrize("B,lanes,pipelined,steps", [(256, 2, True, 2), (16, 1, False, 1), (8, 2, True, 3),
-                                                     (12, 2, False, 2), (256, 2, False, 1)])
-def test_sequence_pipeline_matches_oracle(oracle, orbx_built, B, lanes, pipelined, steps):
-    frames, T, pl = _run(B, lanes, pipelined, steps)
+@pytest.mark.parametrize("B,lanes,pipelined,steps,mode", [(256, 2, True, 2, None), (16, 1, False, 1, None),
+                                                          (8, 2, True, 3, None), (12, 2, False, 2, None),
+                                                          (256, 2, False, 1, None), (256, 2, True, 2, 2),
+                                                          (13, 2, True, 3, 2)])
+def test_sequence_pipeline_matches_oracle(oracle, orbx_built, B, lanes, pipelined, steps, mode):
+    frames, T, pl = _run(B, lanes, pipelined, steps, matcher_mode=mode)
     res = pl.host_results()
     assert not pl.status().any()
     r = checks.check_sequence(frames, T, res, pl.sf)
