@@ -391,6 +391,7 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
     const int lane = threadIdx.x & 63;
     const int nq = pb.nq;
     int nmatch = 0, nrec = 0, nrescore = 0, niter = 0;
+    unsigned long long t_res = 0, t_first = 0;  // diagnostics (stamps): re-scoring, chunk loads + first round
     const float factor = kHistoLength / 360.0f;
     const int need = P.ratio_mode ? 2 : 1;
     const unsigned long long below = (1ull << lane) - 1;
@@ -401,6 +402,7 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
         unsigned e[kTopK];
 #pragma unroll
         for (int j = 0; j < kTopK; j++) e[j] = kNoEntry;
+        const unsigned long long t_chunk = st ? wall_clock64() : 0;
         QueryReg mine;  // consumed only by a re-scoring (loads overlap the first round)
         if (q < nq) mine = load_query(pb, q);
         if (q < nq) {
@@ -417,10 +419,16 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
             unsigned c1 = kNoEntry, c2 = kNoEntry;
             bool exhausted = false;
             if (act) {
+                // all the list's claim words in one batch of independent LDS reads (and
+                // Observations() loads), not one dependent read per entry
+                const int last = pb.n > 0 ? pb.n - 1 : 0;
+                bool blk[kTopK];
+#pragma unroll
+                for (int j = 0; j < kTopK; j++) blk[j] = kp_blocked(sfmp[min(ent_pos(e[j]), last)], P);
                 int found = 0;
 #pragma unroll
                 for (int j = 0; j < kTopK; j++) {
-                    if (e[j] < kTrunc && found < 2 && !kp_blocked(sfmp[ent_pos(e[j])], P)) {
+                    if (e[j] < kTrunc && found < 2 && !blk[j]) {
                         if (found == 0) c1 = e[j];
                         else c2 = e[j];
                         found++;
@@ -471,7 +479,9 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
                 nrec += __popcll(comm);
             }
             if (f >= 64) break;
+            if (st && start == 0) t_first += wall_clock64() - t_chunk;
             if (__builtin_amdgcn_readlane((int)exhausted, f)) {
+                const unsigned long long t0 = st ? wall_clock64() : 0;
                 nrescore++;
                 wave_lds_fence();
                 unsigned ne[kTopK];
@@ -481,6 +491,7 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
                     const unsigned v = (unsigned)__builtin_amdgcn_readlane((int)ne[j], 0);
                     if (lane == f) e[j] = v;
                 }
+                if (st) t_res += wall_clock64() - t0;
             }
             start = f;
             wave_lds_fence();
@@ -526,6 +537,8 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
         st[5] = nrescore;
         st[6] = nq;
         st[7] = niter;
+        st[8] = t_res;
+        st[9] = t_first;
     }
 }
 
@@ -555,7 +568,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int kWaves = NT / 64;
     const int n = pb.n, nq = pb.nq;
-    unsigned long long* st = P.stamps ? P.stamps + 8 * blockIdx.x : nullptr;
+    unsigned long long* st = P.stamps ? P.stamps + 12 * blockIdx.x : nullptr;
     if (st && tid == 0) st[0] = wall_clock64();
     int n2 = 1;
     while (n2 < n) n2 <<= 1;

@@ -616,7 +616,8 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     const bool stamps = !split && getenv("ORBX_MATCH_STAMPS") != nullptr;  // k_proj_search phases only
     unsigned long long* d_st = nullptr;
     if (stamps) {
-        HIP_TRY(hipMalloc(&d_st, sizeof(unsigned long long) * 8 * npairs));
+        HIP_TRY(hipMalloc(&d_st, sizeof(unsigned long long) * 12 * npairs));
+        HIP_TRY(hipMemsetAsync(d_st, 0, sizeof(unsigned long long) * 12 * npairs, s));
         P.stamps = d_st;
     }
     if (split) {
@@ -630,14 +631,16 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
         m->ncalls++;
     }
     if (stamps) {
-        std::vector<unsigned long long> h((size_t)8 * npairs);
+        std::vector<unsigned long long> h((size_t)12 * npairs);
         HIP_TRY(hipStreamSynchronize(s));
         HIP_TRY(hipMemcpy(h.data(), d_st, h.size() * 8, hipMemcpyDeviceToHost));
         HIP_TRY(hipFree(d_st));
-        double ph[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0}, resc = 0, nq = 0, nit = 0;
+        double ph[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0}, resc = 0, nq = 0, nit = 0, tres = 0, tfirst = 0;
         unsigned long long t0 = ~0ull, t1 = 0;
         for (int p = 0; p < npairs; p++) {
-            const unsigned long long* r = &h[(size_t)8 * p];
+            const unsigned long long* r = &h[(size_t)12 * p];
+            tres += (double)r[8] * 0.01;
+            tfirst += (double)r[9] * 0.01;
             for (int k = 0; k < 4; k++) {
                 const double d = (double)(r[k + 1] - r[k]) * 0.01;  // 100 MHz -> us
                 ph[k] += d;
@@ -651,9 +654,10 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
         }
         fprintf(stderr,
                 "[orbx stamps] pairs=%d span=%.1fus | mean/max us: sort %.1f/%.1f score %.1f/%.1f commit %.1f/%.1f "
-                "store %.1f/%.1f | rescored %.1f of %.1f queries, %.1f replay rounds\n",
+                "store %.1f/%.1f | rescored %.1f of %.1f queries (%.1f us), %.1f replay rounds (chunk loads + first "
+                "rounds %.1f us)\n",
                 npairs, (double)(t1 - t0) * 0.01, ph[0] / npairs, mx[0], ph[1] / npairs, mx[1], ph[2] / npairs, mx[2],
-                ph[3] / npairs, mx[3], resc / npairs, nq / npairs, nit / npairs);
+                ph[3] / npairs, mx[3], resc / npairs, nq / npairs, tres / npairs, nit / npairs, tfirst / npairs);
     }
     return ORBX_OK;
 }
