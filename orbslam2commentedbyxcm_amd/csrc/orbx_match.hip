@@ -1032,9 +1032,13 @@ __global__ __launch_bounds__(kTriThreads) void k_triangulation(const TriProblem*
     const TriProblem pb = probs[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint8_t* matched2 = smem;  // vbMatched2, n2 bytes
-    int* mlist = (int*)(smem + ((pb.n2 + 15) & ~15));
+    int* owner = (int*)(smem + ((pb.n2 + 15) & ~15));  // lowest lane of a commit round wanting KF2 keypoint i
+    int* mlist = owner + pb.n2;
     int* mbin = mlist + pb.nq;
-    for (int i = tid; i < pb.n2; i += kTriThreads) matched2[i] = 0;
+    for (int i = tid; i < pb.n2; i += kTriThreads) {
+        matched2[i] = 0;
+        owner[i] = 0x7fffffff;
+    }
     if (tid < kHistoLength) s_hist[tid] = 0;
     __syncthreads();
     unsigned long long* keys = scratch + pb.scratch_off;
@@ -1066,39 +1070,73 @@ __global__ __launch_bounds__(kTriThreads) void k_triangulation(const TriProblem*
                 }
                 if (Q.idx1 >= 0) l_a1 = pb.keys1[Q.idx1].angle;
             }
-            const int cnt = pb.nq - q0 < 64 ? pb.nq - q0 : 64;
-            for (int j = 0; j < cnt; j++) {
-                const int idx1 = __builtin_amdgcn_readlane(l_idx1, j);
-                unsigned long long best = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(l_best >> 32), j) << 32) |
-                                          (unsigned)__builtin_amdgcn_readlane((int)(unsigned)l_best, j);
-                int idx2 = __builtin_amdgcn_readlane(l_idx2, j);
-                float a2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l_a2), j));
-                if (best != kNoKey && matched2[idx2]) {  // taken by an earlier query: re-score
-                    const TriQuery Q = pb.q[q0 + j];
-                    score_tri(pb, Q, matched2, best);
-                    idx2 = best != kNoKey
-                               ? pb.fv2_idx[Q.beg + (int)(0xffffffffu - (unsigned)(best & 0xffffffffu))]
-                               : -1;
-                    if (idx2 >= 0) a2 = pb.keys2[idx2].angle;
+            // Rounds over the chunk: a lane's pre-scored best is still its answer unless an
+            // earlier query took that keypoint (vbMatched2) or an earlier lane of this round
+            // wants it too (owner map).  All lanes before the first such conflict commit at
+            // once; the conflicting query is re-scored against the current vbMatched2 (now
+            // holding every earlier claim) and commits alone; the next round starts after it.
+            int start = 0;
+            while (true) {
+                const bool act = lane >= start && ql < pb.nq && l_idx1 >= 0 && l_idx2 >= 0;
+                const bool taken = act && matched2[l_idx2];
+                if (act && !taken) atomicMin(&owner[l_idx2], lane);
+                const bool dup = act && !taken && owner[l_idx2] < lane;
+                if (act && !taken) owner[l_idx2] = 0x7fffffff;
+                const unsigned long long cm = __ballot(taken || dup);
+                const int f = cm ? __ffsll((long long)cm) - 1 : 64;
+                const bool com = act && lane < f;
+                if (com) {
+                    pb.matches12[l_idx1] = l_idx2;
+                    matched2[l_idx2] = 1;
                 }
-                if (idx1 < 0) continue;  // batched tables: a feature index outside [0, N)
-                if (lane == 0) pb.matches12[idx1] = idx2;
-                if (idx2 < 0) continue;
-                if (lane == 0) matched2[idx2] = 1;
                 if (pb.check_ori) {
-                    float rot = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l_a1), j)) - a2;
-                    if (rot < 0.0f) rot += 360.0f;
-                    int bin = (int)roundf(rot * factor);
-                    if (bin == kHistoLength) bin = 0;
-                    if (lane == 0) {
-                        mlist[nrec] = idx1;
-                        mbin[nrec] = bin;
-                        s_hist[bin]++;
+                    const unsigned long long comm = __ballot(com);
+                    if (com) {
+                        float rot = l_a1 - l_a2;
+                        if (rot < 0.0f) rot += 360.0f;
+                        int bin = (int)roundf(rot * factor);
+                        if (bin == kHistoLength) bin = 0;
+                        const int r = nrec + __popcll(comm & ((1ull << lane) - 1ull));
+                        mlist[r] = l_idx1;
+                        mbin[r] = bin;
+                        atomicAdd(&s_hist[bin], 1);
                     }
-                    nrec++;
+                    nrec += __popcll(comm);
                 }
+                if (f >= 64) break;
+                wave_lds_fence();
+                // query q0 + f: re-score against the current claims, commit alone
+                const TriQuery Q = pb.q[q0 + f];
+                unsigned long long best;
+                score_tri(pb, Q, matched2, best);
+                const int idx1 = __builtin_amdgcn_readlane(l_idx1, f);
+                const int idx2 = best != kNoKey
+                                     ? pb.fv2_idx[Q.beg + (int)(0xffffffffu - (unsigned)(best & 0xffffffffu))]
+                                     : -1;
+                if (lane == f) l_idx2 = -1;  // resolved
+                if (idx2 >= 0) {
+                    if (lane == 0) {
+                        pb.matches12[idx1] = idx2;
+                        matched2[idx2] = 1;
+                    }
+                    if (pb.check_ori) {
+                        float rot = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l_a1), f)) -
+                                    pb.keys2[idx2].angle;
+                        if (rot < 0.0f) rot += 360.0f;
+                        int bin = (int)roundf(rot * factor);
+                        if (bin == kHistoLength) bin = 0;
+                        if (lane == 0) {
+                            mlist[nrec] = idx1;
+                            mbin[nrec] = bin;
+                            s_hist[bin]++;
+                        }
+                        nrec++;
+                    }
+                }
+                start = f + 1;
                 wave_lds_fence();
             }
+            wave_lds_fence();
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         if (pb.check_ori) {
@@ -1226,7 +1264,7 @@ __global__ __launch_bounds__(kTriSetupThreads) void k_tri_setup(TriBatch tb) {
 hipError_t launch_triangulation(const TriProblem* d_probs, int nprob, unsigned long long* scratch, int max_n2,
                                 int max_nq, hipStream_t stream) {
     if (nprob <= 0) return hipSuccess;
-    const size_t lds = (size_t)((max_n2 + 15) & ~15) + (size_t)max_nq * 8;
+    const size_t lds = (size_t)((max_n2 + 15) & ~15) + (size_t)max_n2 * 4 + (size_t)max_nq * 8;
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)k_triangulation, hipFuncAttributeMaxDynamicSharedMemorySize,

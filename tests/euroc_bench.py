@@ -214,8 +214,8 @@ def main(argv=None):
     ap = argparse.ArgumentParser(prog="bench.py --workload euroc")
     ap.add_argument("--workload", default="euroc")
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64, help="keyframes per rank per step")
     ap.add_argument("--nn", type=int, default=10, help="covisible neighbours (LocalMapping.cc:237, stereo)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
