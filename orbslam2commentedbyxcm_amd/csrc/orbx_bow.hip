@@ -285,6 +285,44 @@ __device__ void init_scan(const InitProblem& pb, int i1, const int* md, unsigned
 
 }  // namespace
 
+// Phase 1 on its own launch, one wave per query over as many CUs as there are queries
+// (a query's window walk is a chain of dependent gathers): each query's 8 nearest window
+// candidates into pb.lists, exact up to where a lane holding more than 4 candidates runs
+// out (then marked truncated in pb.trunc).
+constexpr int kInitScanThreads = 256;
+
+__global__ __launch_bounds__(kInitScanThreads) void k_init_scan(const InitProblem* __restrict__ probs) {
+    const InitProblem& pb = probs[0];
+    const int lane = threadIdx.x & 63;
+    const int q = blockIdx.x * (kInitScanThreads / 64) + (threadIdx.x >> 6);
+    if (q >= pb.nq) return;  // whole wave
+    unsigned long long l[4];
+    int seen;
+    init_scan<4>(pb, pb.q_idx1[q], nullptr, l, seen);
+    int cnt = 0, tr = 0, used = 0;
+    for (; cnt < kInitList; cnt++) {
+        const unsigned long long m = wave_min_u64(l[0]);
+        if (m == kNone) break;
+        if (lane == 0) pb.lists[(size_t)q * kInitList + cnt] = m;
+        if (l[0] == m) {  // the owner pops its head
+            l[0] = l[1];
+            l[1] = l[2];
+            l[2] = l[3];
+            l[3] = kNone;
+            used++;
+        }
+        // an owner that listed all 4 of more than 4 seen: the next entry is unknown
+        const int stop = __any(used == 4 && seen > 4 && l[0] == kNone);
+        if (stop) {
+            tr = 1;
+            cnt++;
+            break;
+        }
+    }
+    if (cnt == kInitList && __any(l[0] != kNone || (seen > used && used == 4))) tr = 1;
+    if (lane == 0) pb.trunc[q] = cnt | tr << 8;
+}
+
 __global__ __launch_bounds__(kBowThreads) void k_init(const InitProblem* __restrict__ probs, int lists_lds) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_hist[kHistoLength];
@@ -294,20 +332,23 @@ __global__ __launch_bounds__(kBowThreads) void k_init(const InitProblem* __restr
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // LDS: the candidate lists first (8-byte aligned; in the problem's global buffer
     // when they do not fit), then 4-byte arrays, then the bins
-    unsigned long long* lists = lists_lds ? (unsigned long long*)smem : pb.lists;  // [nq * kInitList]
-    int* md = (int*)(smem + (lists_lds ? (size_t)8 * kInitList * pb.nq : 0));      // vMatchedDistance [n2]
+    const unsigned long long* lists = pb.lists;  // [nq * kInitList], from k_init_scan
+    const int* trunc = pb.trunc;                 // listed count | truncated << 8 [nq]
+    (void)lists_lds;
+    int* md = (int*)smem;                        // vMatchedDistance [n2]
     int* m21 = md + pb.n2;         // vnMatches21 [n2]
     int* m12 = m21 + pb.n2;        // vnMatches12 [n1]
     int* items = m12 + pb.n1;      // rotHist entries (F1 index) [nq]
-    int* trunc = items + pb.nq;    // listed count | truncated << 8 [nq]
-    int* qi1 = trunc + pb.nq;      // the queries' F1 keypoints [nq]
+    int* qi1 = items + pb.nq;      // the queries' F1 keypoints [nq]
     float* ang1 = (float*)(qi1 + pb.nq);  // keypoint angles of F1 [n1] and F2 [n2]
     float* ang2 = ang1 + pb.n1;
-    uint8_t* bins = (uint8_t*)(ang2 + pb.n2);
+    int* owner = (int*)(ang2 + pb.n2);  // lowest lane of a commit round taking F2 keypoint i [n2]
+    uint8_t* bins = (uint8_t*)(owner + pb.n2);
     for (int i = tid; i < pb.n2; i += kBowThreads) {
         md[i] = INT_MAX;
         m21[i] = -1;
         ang2[i] = pb.keys2[i].angle;
+        owner[i] = 0x7fffffff;
     }
     for (int i = tid; i < pb.n1; i += kBowThreads) {
         m12[i] = -1;
@@ -317,45 +358,22 @@ __global__ __launch_bounds__(kBowThreads) void k_init(const InitProblem* __restr
     if (tid < kHistoLength) s_hist[tid] = 0;
     if (tid == 0) s_nrec = 0;
 
-    // phase 1: each query's 8 nearest window candidates, exact up to where a lane
-    // holding more than 4 candidates runs out (then marked truncated)
-    for (int q = wave; q < pb.nq; q += kBowWaves) {
-        unsigned long long l[4];
-        int seen;
-        init_scan<4>(pb, pb.q_idx1[q], nullptr, l, seen);
-        int cnt = 0, tr = 0, used = 0;
-        for (; cnt < kInitList; cnt++) {
-            const unsigned long long m = wave_min_u64(l[0]);
-            if (m == kNone) break;
-            if (lane == 0) lists[(size_t)q * kInitList + cnt] = m;
-            if (l[0] == m) {  // the owner pops its head
-                l[0] = l[1];
-                l[1] = l[2];
-                l[2] = l[3];
-                l[3] = kNone;
-                used++;
-            }
-            // an owner that listed all 4 of more than 4 seen: the next entry is unknown
-            const int stop = __any(used == 4 && seen > 4 && l[0] == kNone);
-            if (stop) {
-                tr = 1;
-                cnt++;
-                break;
-            }
-        }
-        if (cnt == kInitList && __any(l[0] != kNone || (seen > used && used == 4))) tr = 1;
-        if (lane == 0) trunc[q] = cnt | tr << 8;
-    }
+    // phase 1 (the candidate lists) ran in k_init_scan
     __syncthreads();
 
-    // phase 2: the reference's sequential loop over F1's level-0 keypoints (wave 0)
+    // phase 2: the reference's sequential loop over F1's level-0 keypoints (wave 0), in
+    // rounds over chunks of 64 queries.  A query's decision reads vMatchedDistance only at
+    // its listed entries (or, when its truncated list runs short, at its whole window), and
+    // a commit changes it at one entry (its best).  So every query before the first one
+    // whose list holds a keypoint an earlier query of the round takes (an LDS owner map),
+    // or that needs the rescan, decides exactly as in the sequential loop and all of them
+    // commit at once; the first conflicting query is then decided alone.
     if (wave == 0) {
-        for (int q = 0; q < pb.nq; q++) {
-            const int i1 = qi1[q];
-            const int t = trunc[q];
-            const int cnt = t & 0xff, tr = t >> 8;
+        auto decide = [&](int q, unsigned long long& best, unsigned long long& second) {
             // the first two listed entries still available, in list order: lane k checks
             // entry k against vMatchedDistance, the two lowest set ballot bits win
+            const int t = trunc[q];
+            const int cnt = t & 0xff, tr = t >> 8;
             unsigned long long e = kNone;
             bool avail = false;
             if (lane < cnt) {
@@ -364,37 +382,101 @@ __global__ __launch_bounds__(kBowThreads) void k_init(const InitProblem* __restr
             }
             const unsigned long long bal = __ballot(avail);
             const int found = __popcll(bal) < 2 ? __popcll(bal) : 2;
-            unsigned long long best = kNone, second = kNone;
+            best = kNone;
+            second = kNone;
             if (found >= 1) best = shfl_u64(e, __ffsll((long long)bal) - 1);
             if (found >= 2) second = shfl_u64(e, __ffsll((long long)(bal & (bal - 1))) - 1);
             if (found < 2 && tr) {  // the list ran out: rescan the window against vMatchedDistance
                 unsigned long long l[2];
                 int seen;
-                init_scan<2>(pb, i1, md, l, seen);
+                init_scan<2>(pb, qi1[q], md, l, seen);
                 best = wave_min_u64(l[0]);
                 second = wave_min_u64(l[0] == best ? l[1] : l[0]);
             }
+        };
+        auto accepted = [&](unsigned long long best, unsigned long long second) {
             const int bestDist = best == kNone ? INT_MAX : e_dist(best);
             const int bestDist2 = second == kNone ? INT_MAX : e_dist(second);
-            if (bestDist <= kThLow && (float)bestDist < (float)bestDist2 * pb.nnratio) {
-                const int i2 = e_idx(best);
-                if (lane == 0) {
-                    const int prev = m21[i2];
-                    if (prev >= 0) m12[prev] = -1;
-                    m12[i1] = i2;
-                    m21[i2] = i1;
-                    md[i2] = bestDist;
-                    if (pb.check_ori) {
-                        const int bin = rot_bin(ang1[i1], ang2[i2]);
-                        items[s_nrec] = i1;
-                        bins[s_nrec] = (uint8_t)bin;
-                        s_nrec++;
-                        s_hist[bin]++;
+            return bestDist <= kThLow && (float)bestDist < (float)bestDist2 * pb.nnratio;
+        };
+        // commit of query i1 taking F2 keypoint i2 (one lane per query)
+        auto commit = [&](int i1, unsigned long long best, int slot) {
+            const int i2 = e_idx(best);
+            const int prev = m21[i2];
+            if (prev >= 0) m12[prev] = -1;
+            m12[i1] = i2;
+            m21[i2] = i1;
+            md[i2] = e_dist(best);
+            if (pb.check_ori) {
+                const int bin = rot_bin(ang1[i1], ang2[i2]);
+                items[slot] = i1;
+                bins[slot] = (uint8_t)bin;
+                atomicAdd(&s_hist[bin], 1);
+            }
+        };
+        int nrec = 0;
+        for (int q0 = 0; q0 < pb.nq; q0 += 64) {
+            const int q = q0 + lane;
+            const bool valid = q < pb.nq;
+            // this lane's query: its listed entries and whether the list is truncated
+            unsigned long long L[kInitList];
+            int cnt = 0, tr = 0, i1 = -1;
+            if (valid) {
+                const int t = trunc[q];
+                cnt = t & 0xff;
+                tr = t >> 8;
+                i1 = qi1[q];
+            }
+#pragma unroll
+            for (int k = 0; k < kInitList; k++) L[k] = (k < cnt) ? lists[(size_t)q * kInitList + k] : kNone;
+            int start = 0;
+            while (true) {
+                const bool act = valid && lane >= start;
+                unsigned long long best = kNone, second = kNone;
+                bool rescan = false;
+                if (act) {
+                    int found = 0;
+#pragma unroll
+                    for (int k = 0; k < kInitList; k++) {
+                        if (L[k] != kNone && found < 2 && md[e_idx(L[k])] > e_dist(L[k])) {
+                            if (found == 0) best = L[k];
+                            else second = L[k];
+                            found++;
+                        }
                     }
+                    rescan = found < 2 && tr;
                 }
+                const bool acc = act && !rescan && accepted(best, second);
+                if (acc) atomicMin(&owner[e_idx(best)], lane);
+                bool conf = rescan;
+                if (act && !rescan) {
+#pragma unroll
+                    for (int k = 0; k < kInitList; k++)
+                        if (L[k] != kNone && owner[e_idx(L[k])] < lane) conf = true;
+                }
+                if (acc) owner[e_idx(best)] = 0x7fffffff;
+                const unsigned long long cm = __ballot(conf);
+                const int f = cm ? __ffsll((long long)cm) - 1 : 64;
+                const bool com = acc && lane < f;
+                const unsigned long long comm = __ballot(com);
+                if (com) commit(i1, best, nrec + __popcll(comm & ((1ull << lane) - 1ull)));
+                if (pb.check_ori) nrec += __popcll(comm);
+                if (f >= 64) break;
+                wave_lds_fence();
+                // query q0 + f alone, against every earlier commit
+                unsigned long long b1, b2;
+                decide(q0 + f, b1, b2);
+                if (accepted(b1, b2)) {
+                    if (lane == 0) commit(qi1[q0 + f], b1, nrec);
+                    if (pb.check_ori) nrec++;
+                }
+                start = f + 1;
                 wave_lds_fence();
             }
+            wave_lds_fence();
         }
+        if (lane == 0) s_nrec = nrec;
+        wave_lds_fence();
         if (pb.check_ori && lane == 0) three_maxima(s_hist, s_ind);
     }
     __syncthreads();
@@ -410,10 +492,15 @@ __global__ __launch_bounds__(kBowThreads) void k_init(const InitProblem* __restr
 }
 
 hipError_t launch_init(const InitProblem* d_prob, int n1, int n2, int nq, hipStream_t stream) {
-    const size_t base = (size_t)4 * (3 * n2 + 2 * n1 + 3 * nq) + (size_t)nq + 16;
-    const int lists_lds = base + (size_t)8 * kInitList * nq <= 160 * 1024;
-    const size_t lds = base + (lists_lds ? (size_t)8 * kInitList * nq : 0);
+    const size_t lds = (size_t)4 * (4 * n2 + 2 * n1 + 2 * nq) + (size_t)nq + 16;
+    const int lists_lds = 0;
     if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (nq > 0) {
+        const int per = kInitScanThreads / 64;
+        hipLaunchKernelGGL(k_init_scan, dim3((nq + per - 1) / per), dim3(kInitScanThreads), 0, stream, d_prob);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)k_init, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

@@ -683,7 +683,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
 
 // Byte layout of one problem's grid in the global grid area.
 struct SeqGridLayout {
-    size_t skey, cstart, sxy, sang, sdesc, total;
+    size_t skey, cstart, sxy, sang, sfmp, sdesc, total;
     __host__ __device__ SeqGridLayout(int cap) {
         int n2 = 1;
         while (n2 < cap) n2 <<= 1;
@@ -691,7 +691,8 @@ struct SeqGridLayout {
         cstart = align16((size_t)n2 * 4);
         sxy = align16(cstart + (size_t)(kNumCells + 1) * 2);
         sang = align16(sxy + (size_t)cap * 8);
-        sdesc = align16(sang + (size_t)cap * 4);
+        sfmp = align16(sang + (size_t)cap * 4);  // the claims (mvpMapPoints) before the search, sorted
+        sdesc = align16(sfmp + (size_t)cap * 4);
         total = (sdesc + (size_t)cap * 32 + 255) & ~(size_t)255;
     }
 };
@@ -729,6 +730,7 @@ __global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem*
     unsigned* gkey = (unsigned*)(gb + gl.skey);
     float2* sxy = (float2*)(gb + gl.sxy);
     float* sang = (float*)(gb + gl.sang);
+    int* gfmp = (int*)(gb + gl.sfmp);
     uint4* sdesc = (uint4*)(gb + gl.sdesc);
     uint16_t* cstart = (uint16_t*)(gb + gl.cstart);
     for (int p = tid; p < n; p += kSeqGridThreads) {
@@ -738,6 +740,7 @@ __global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem*
         gkey[p] = k;
         sxy[p] = make_float2(kp.x, kp.y);
         sang[p] = kp.angle;
+        gfmp[p] = pb.frame_mp[i];
     }
     for (int t = tid; t < 2 * n; t += kSeqGridThreads) {
         const int i = sk_idx(skey[t >> 1]);
@@ -772,7 +775,8 @@ __global__ __launch_bounds__(kSeqScoreThreads) void k_seq_score(const ProjProble
     const QueryReg cur = load_query(pb, min(q, pb.nq - 1));
     const int mp = q < pb.nq ? cur.q.mp : -1;
     unsigned e[kTopK];
-    score_rowk(pb, P, cur, mp >= 0, G, nullptr, e);
+    const int* sfmp0 = (const int*)(grids + (size_t)p * gl.total + gl.sfmp);  // the claims before the search
+    score_rowk(pb, P, cur, mp >= 0, G, sfmp0, e);
     if ((threadIdx.x & 15) == 0 && q < pb.nq) {
         unsigned long long* g = scratch + scratch_off[p];
         uint4* qk = (uint4*)g;

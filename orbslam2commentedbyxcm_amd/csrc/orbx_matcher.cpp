@@ -231,6 +231,10 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
                   pad(sizeof(int32_t) * n) + pad(sizeof(ProjQuery) * nq) + pad((size_t)nq * 32) +
                   pad(sizeof(int32_t) * (nobs ? nobs : 1)) + pad(sizeof(ProjProblem)) + pad(8 * kProjScratchWords * (size_t)nq) +
                   pad(sizeof(long long)) + pad(sizeof(int32_t));
+    // one problem: the split launches (grid sort, scoring spread over nq / 16 workgroups,
+    // one-wave commit) finish sooner than one workgroup doing all three
+    const int gcap = n > nq ? n : nq;
+    need += pad(seq_grid_bytes(gcap));
     HIP_TRY(m->arena.reserve(need));
     m->arena.used = 0;
     auto* d_keys = m->arena.take<orbx_keypoint>(n);
@@ -244,6 +248,7 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
     auto* d_scr = m->arena.take<unsigned long long>(kProjScratchWords * (size_t)nq);
     auto* d_off = m->arena.take<long long>(1);
     auto* d_nm = m->arena.take<int32_t>(1);
+    auto* d_grid = m->arena.take<unsigned char>(seq_grid_bytes(gcap));
     hipStream_t s = m->stream;
     m->arena.up(d_keys, f->keys, sizeof(orbx_keypoint) * n);
     m->arena.up(d_desc, f->desc, (size_t)n * 32);
@@ -273,7 +278,10 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
     ProjParams P = base_params;
     P.mp_obs = d_obs;
     HIP_TRY(m->arena.flush(s));
-    HIP_TRY(launch_proj_search(d_prob, 1, P, d_scr, d_off, n, nq, s));
+    if (gcap < 8192)
+        HIP_TRY(launch_seq_split(d_prob, 1, P, d_grid, gcap, d_scr, d_off, s));
+    else
+        HIP_TRY(launch_proj_search(d_prob, 1, P, d_scr, d_off, n, nq, s));
     int nm = 0;
     HIP_TRY(m->arena.down(frame_mp, d_fmp, sizeof(int32_t) * n, s));
     HIP_TRY(m->arena.down(&nm, d_nm, sizeof(int32_t), s));
