@@ -76,10 +76,11 @@ def sequence_matches(ref, T: np.ndarray, sf, fx=500.0, fy=500.0, cx=320.0, cy=24
         return [None] + list(ex.map(one, range(1, len(ref))))
 
 
-def check_sequence(frames: np.ndarray, T: np.ndarray, res: dict, sf, threads: int = 0, **kw) -> dict:
+def check_sequence(frames: np.ndarray, T: np.ndarray, res: dict, sf, threads: int = 0,
+                   params=(1000, 1.2, 8, 20, 7), **kw) -> dict:
     """Every frame's extraction and every pair's matches of a SequencePipeline result
     (host copies: kps, desc, n, mp, nm) against the oracle."""
-    ref = extract_all(frames, threads=threads)
+    ref = extract_all(frames, params=params, threads=threads)
     bad_frames = compare_extraction(ref, res["kps"], res["desc"], res["n"])
     out = {"frames_checked": len(frames), "frames_mismatched": len(bad_frames), "first_bad_frames": bad_frames[:8]}
     if "mp" in res:
