@@ -236,9 +236,13 @@ __device__ __forceinline__ QueryReg bcast_query(const QueryReg& x, int src) {
 // The candidate windows hold a few to a few tens of keypoints, so a row keeps its lanes
 // busy where a whole wave per query would mostly idle.  `valid` false: no query in this
 // row (out = kNoEntry).  Must be called with the whole wave active.
-__device__ void score_rowk(const ProjProblem& pb, const ProjParams& P, const QueryReg& QR, bool valid,
-                           const SortedGrid& G, const int* sfmp, unsigned out[kTopK]) {
-    const int r = threadIdx.x & 15;
+// K = 64: one query per wave, all lanes over its window (the replay's re-scoring of a
+// query whose list ran out, a single query on the critical path).
+template <int K>
+__device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const QueryReg& QR, bool valid,
+                             const SortedGrid& G, const int* sfmp, unsigned out[kTopK]) {
+    static_assert(K == 16 || K == 64, "a DPP row or a wave");
+    const int r = threadIdx.x & (K - 1);
     const ProjQuery& Q = QR.q;
     unsigned k[4] = {kNoEntry, kNoEntry, kNoEntry, kNoEntry};
     int seen = 0;
@@ -251,10 +255,16 @@ __device__ void score_rowk(const ProjProblem& pb, const ProjParams& P, const Que
             const unsigned long long q3 = (unsigned long long)QR.d1.w << 32 | QR.d1.z;
             const bool check_levels = (Q.min_level > 0) || (Q.max_level >= 0);
             const int ncol = cr.x1 - cr.x0 + 1;
-            // 4, 2 or 1 lanes per column (ncol <= 4, <= 8, more): shifts, no division
-            const int sh = ncol <= 4 ? 2 : (ncol <= 8 ? 1 : 0);
+            // lanes per column: the most (up to 4 in a row, 16 in a wave) that still cover
+            // every column in one pass; shifts, no division
+            int sh = 0;
+            if (K == 16) {
+                sh = ncol <= 4 ? 2 : (ncol <= 8 ? 1 : 0);
+            } else {
+                sh = ncol <= 4 ? 4 : (ncol <= 8 ? 3 : (ncol <= 16 ? 2 : (ncol <= 32 ? 1 : 0)));
+            }
             const int lpc = 1 << sh, c0 = r >> sh, sub = r & (lpc - 1);
-            for (int c = c0; c < ncol; c += 16) {
+            for (int c = c0; c < ncol; c += K) {
                 const int cc = (cr.x0 + c) * kGridRows;
                 const int beg = G.cstart[cc + cr.y0], end = G.cstart[cc + cr.y1 + 1];
                 for (int p = beg + sub; p < end; p += lpc) {
@@ -306,8 +316,9 @@ __device__ void score_rowk(const ProjProblem& pb, const ProjParams& P, const Que
             }
         }
     }
-    // Row top-kTopK: keys are unique (distinct positions), so one lane pops each minimum.
-    const int rsh = threadIdx.x & 48;  // first lane of this row
+    // Group top-kTopK: keys are unique (distinct positions), so one lane pops each minimum.
+    const int rsh = K == 16 ? (threadIdx.x & 48) : 0;  // first lane of this group
+    const unsigned long long gmask = K == 16 ? 0xffffull : ~0ull;
     bool over = seen > 4;
     bool trunc = false;
     unsigned m[kTopK];
@@ -315,8 +326,12 @@ __device__ void score_rowk(const ProjProblem& pb, const ProjParams& P, const Que
     for (int j = 0; j < kTopK; j++) {
         // a lane whose listed candidates are used up but that saw more makes the rest unknown
         const unsigned long long dry = __ballot(over && k[0] == kNoEntry);
-        trunc = trunc || ((dry >> rsh) & 0xffffull) != 0;
+        trunc = trunc || ((dry >> rsh) & gmask) != 0;
         m[j] = row_min_u32(k[0]);
+        if (K == 64) {
+            m[j] = umin_(m[j], (unsigned)__shfl_xor((int)m[j], 16));
+            m[j] = umin_(m[j], (unsigned)__shfl_xor((int)m[j], 32));
+        }
         if (k[0] == m[j] && m[j] != kNoEntry) {
             k[0] = k[1];
             k[1] = k[2];
@@ -330,6 +345,11 @@ __device__ void score_rowk(const ProjProblem& pb, const ProjParams& P, const Que
         out[j] = m[j] >= kTrunc ? m[j]
                                 : ((m[j] >> 13) << 18) | ((unsigned)sk_oct(G.skey[m[j] & 0x1fffu]) << 13) |
                                       (m[j] & 0x1fffu);
+}
+
+__device__ __forceinline__ void score_rowk(const ProjProblem& pb, const ProjParams& P, const QueryReg& QR, bool valid,
+                                           const SortedGrid& G, const int* sfmp, unsigned out[kTopK]) {
+    score_groupk<16>(pb, P, QR, valid, G, sfmp, out);
 }
 
 // Ascending in-place bitonic sort of n2 (power of two) u32 keys by the workgroup.
@@ -485,12 +505,10 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
                 nrescore++;
                 wave_lds_fence();
                 unsigned ne[kTopK];
-                score_rowk(pb, P, bcast_query(mine, f), lane < 16, G, sfmp, ne);
+                score_groupk<64>(pb, P, bcast_query(mine, f), true, G, sfmp, ne);  // wave-uniform result
 #pragma unroll
-                for (int j = 0; j < kTopK; j++) {
-                    const unsigned v = (unsigned)__builtin_amdgcn_readlane((int)ne[j], 0);
-                    if (lane == f) e[j] = v;
-                }
+                for (int j = 0; j < kTopK; j++)
+                    if (lane == f) e[j] = ne[j];
                 if (st) t_res += wall_clock64() - t0;
             }
             start = f;
