@@ -154,22 +154,125 @@ constexpr unsigned long long kNoKey = ~0ull;
 constexpr int kNoCell = 0xfff;
 constexpr int kNumCells = kGridCols * kGridRows;
 
-// The frame's keypoints sorted by (grid cell, index) -- Frame::mGrid flattened: cell
-// c = ix*FRAME_GRID_ROWS + iy holds sorted positions [cstart[c], cstart[c+1]).  The
-// cells of one grid column are contiguous, so GetFeaturesInArea's walk (ix ascending,
-// iy ascending, index ascending) is a list of contiguous runs and a candidate's sorted
-// position is its rank in the reference's iteration order.  The per-keypoint state the
-// scans read (position, octave, mvpMapPoints claim) is kept in sorted order in LDS, 20
-// bytes per keypoint plus a u16 cell table; descriptors stay in global memory unless
-// they fit too, angles are read from global memory at commit time.
+// The frame's keypoints sorted by (grid cell, index) -- Frame::mGrid flattened, cell
+// c = ix*FRAME_GRID_ROWS + iy.  GetFeaturesInArea walks cells ix ascending, iy
+// ascending, index ascending, so a keypoint's sorted position is its rank in the
+// reference's iteration order; candidate keys (distance << 13 | position) therefore
+// order ties exactly as the reference's strict `<` updates do, whatever order the
+// lanes visit the candidates in.  The per-keypoint state the scans read (position,
+// claim, descriptor) is kept in sorted order.
+//
+// Octave runs.  Every projection search filters candidates by octave (a window of 1-3
+// levels around the predicted one) and the window radius grows with the octave
+// (th * scale[level]): at 5000 features x 12 levels a top-level window covers ~800
+// keypoints of which ~5 % are in the level range.  So the scan does not walk cells: a
+// grid column's keypoints are also listed bucketed by (octave, block of 8 grid rows)
+// -- orun, u16 entries position | (iy & 7) << 13 -- with bucket starts in bstart,
+// [ix][octave][block] (+ one sentinel).  A query visits, per column of its window and
+// per octave of its range, the buckets of the blocks its rows touch, and drops the rows
+// of the two end blocks outside the window (iy & 7 in the entry).  Octaves >= noct share
+// the last bucket (the host sets noct above every keypoint's octave).
+constexpr int kRowBlk = 8;                    // grid rows per bucket block
+constexpr int kNumBlk = kGridRows / kRowBlk;  // 6
+static_assert(kGridRows % kRowBlk == 0, "row blocks tile the grid");
+__host__ __device__ constexpr int bucket_table_len(int noct) { return kGridCols * noct * kNumBlk + 1; }
+
 struct SortedGrid {
     const unsigned* skey;     // (cell << 18) | (index << 5) | octave, ascending
-    const uint16_t* cstart;
+    const uint16_t* bstart;   // bucket starts into orun, [ix][octave][block], + sentinel
+    const uint16_t* orun;     // sorted positions bucketed by (column, octave, row block)
     const float2* sxy;        // x, y
     const uint4* sdesc;       // 2 x uint4 per keypoint, or null (descriptors read from global)
+    int noct;                 // octave buckets per column
 };
 __device__ __forceinline__ int sk_idx(unsigned k) { return (int)((k >> 5) & 0x1fffu); }
 __device__ __forceinline__ int sk_oct(unsigned k) { return (int)(k & 31u); }
+
+// bucket of the keypoint with sorted key k in grid column ix: octave-major, then block
+__device__ __forceinline__ int bucket_of(unsigned k, int ix, int noct) {
+    const int iy = (int)(k >> 18) - ix * kGridRows;
+    const int o = sk_oct(k) < noct ? sk_oct(k) : noct - 1;
+    return o * kNumBlk + (iy >> 3);
+}
+
+// colstart[c] = first sorted position whose grid column is >= c (c = 0..kGridCols;
+// off-grid keypoints sort last, so colstart[kGridCols] counts the keypoints in the
+// grid).  Each entry is written once.
+template <int NT>
+__device__ void build_colstart(const unsigned* skey, int n, uint16_t* colstart) {
+    for (int p = threadIdx.x; p <= n; p += NT) {
+        const int prev = p == 0 ? -1 : min((int)(skey[p - 1] >> 18) / kGridRows, kGridCols);
+        const int cur = p == n ? kGridCols : min((int)(skey[p] >> 18) / kGridRows, kGridCols);
+        for (int c = prev + 1; c <= cur; c++) colstart[c] = (uint16_t)p;
+    }
+}
+
+// Inclusive prefix sum over the 64 lanes of a wave (all lanes active): DPP row_shr
+// 1/2/4/8 inside each 16-lane row, then row_bcast:15 and row_bcast:31 across rows.
+__device__ __forceinline__ unsigned wave_inclusive_sum(unsigned v) {
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+    return v;
+}
+
+// LDS scratch of build_octave_runs: one u32 counter per bucket
+__host__ __device__ constexpr size_t octave_runs_scratch(int noct) {
+    return (size_t)kGridCols * noct * kNumBlk * 4;
+}
+
+// The octave runs of a sorted grid (after build_colstart and a barrier): LDS counters
+// per bucket, one wave-scan per column from colstart[ix] for the bucket starts, then
+// every keypoint takes a slot of its bucket.  Slots inside a bucket come in atomic
+// order: the scan's result does not depend on the order it visits candidates in (keys
+// carry the sorted position).  cnt: octave_runs_scratch(noct) bytes of LDS.  Whole
+// workgroup; the caller puts a barrier after it.
+template <int NT>
+__device__ void build_octave_runs(const unsigned* skey, const uint16_t* colstart, int noct, uint16_t* bstart,
+                                  uint16_t* orun, unsigned* cnt) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int kW = NT / 64;
+    const int nb = noct * kNumBlk, nt = kGridCols * nb, ng = colstart[kGridCols];
+    for (int t = tid; t < nt; t += NT) cnt[t] = 0u;
+    __syncthreads();
+    for (int p = tid; p < ng; p += NT) {
+        const unsigned k = skey[p];
+        const int ix = (int)(k >> 18) / kGridRows;
+        atomicAdd(&cnt[ix * nb + bucket_of(k, ix, noct)], 1u);
+    }
+    __syncthreads();
+    const int per = (nb + 63) >> 6;  // consecutive buckets per lane, <= 3 (noct <= 32)
+    for (int ix = wave; ix < kGridCols; ix += kW) {
+        unsigned v[3], sum = 0;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int u = lane * per + j;
+            v[j] = (j < per && u < nb) ? cnt[ix * nb + u] : 0u;
+            sum += v[j];
+        }
+        unsigned run = colstart[ix] + wave_inclusive_sum(sum) - sum;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int u = lane * per + j;
+            if (j < per && u < nb) {
+                cnt[ix * nb + u] = run;
+                bstart[ix * nb + u] = (uint16_t)run;
+                run += v[j];
+            }
+        }
+    }
+    if (tid == 0) bstart[nt] = (uint16_t)ng;
+    __syncthreads();
+    for (int p = tid; p < ng; p += NT) {
+        const unsigned k = skey[p];
+        const int ix = (int)(k >> 18) / kGridRows, iy = (int)(k >> 18) - ix * kGridRows;
+        const unsigned slot = atomicAdd(&cnt[ix * nb + bucket_of(k, ix, noct)], 1u);
+        orun[slot] = (uint16_t)(p | ((iy & (kRowBlk - 1)) << 13));
+    }
+}
 
 constexpr int kProjThreads = 1024;      // default workgroup size of k_proj_search
 constexpr int kProjThreadsSmall = 256;  // small-footprint variant (overlapped with other work)
@@ -253,7 +356,21 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
             const unsigned long long q1 = (unsigned long long)QR.d0.w << 32 | QR.d0.z;
             const unsigned long long q2 = (unsigned long long)QR.d1.y << 32 | QR.d1.x;
             const unsigned long long q3 = (unsigned long long)QR.d1.w << 32 | QR.d1.z;
-            const bool check_levels = (Q.min_level > 0) || (Q.max_level >= 0);
+            // the candidates' octave range: GetFeaturesInArea's level filter (applied
+            // only when minLevel > 0 || maxLevel >= 0, Frame.cc:515-521) and the
+            // overload's own post filter (a14)
+            int olo = 0, ohi = 31;
+            if ((Q.min_level > 0) || (Q.max_level >= 0)) {
+                olo = Q.min_level > 0 ? Q.min_level : 0;
+                if (Q.max_level >= 0) ohi = Q.max_level;
+            }
+            if (Q.post_max >= 0) {
+                olo = max(olo, Q.post_min);
+                ohi = min(ohi, Q.post_max);
+            }
+            const int noct = G.noct;
+            const int blo = min(olo, noct - 1), bhi = olo > ohi ? -1 : min(ohi, noct - 1);
+            const int b0 = cr.y0 >> 3, b1 = cr.y1 >> 3, ylo = cr.y0 & 7, yhi = cr.y1 & 7;
             const int ncol = cr.x1 - cr.x0 + 1;
             // lanes per column: the most (up to 4 in a row, 16 in a wave) that still cover
             // every column in one pass; shifts, no division
@@ -265,52 +382,54 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
             }
             const int lpc = 1 << sh, c0 = r >> sh, sub = r & (lpc - 1);
             for (int c = c0; c < ncol; c += K) {
-                const int cc = (cr.x0 + c) * kGridRows;
-                const int beg = G.cstart[cc + cr.y0], end = G.cstart[cc + cr.y1 + 1];
-                for (int p = beg + sub; p < end; p += lpc) {
-                    const float2 kp = G.sxy[p];
-                    const unsigned sk = G.skey[p];
-                    const int oct = sk_oct(sk);
-                    if (check_levels) {
-                        if (oct < Q.min_level) continue;
-                        if (Q.max_level >= 0 && oct > Q.max_level) continue;
-                    }
-                    const float distx = kp.x - Q.u;
-                    const float disty = kp.y - Q.v;
-                    if (!(fabsf(distx) < Q.r && fabsf(disty) < Q.r)) continue;
-                    if (Q.post_max >= 0 && (oct < Q.post_min || oct > Q.post_max)) continue;
-                    if (sfmp && kp_blocked(sfmp[p], P)) continue;  // null: nothing claimed yet
-                    int d;
-                    if (G.sdesc) {
-                        if (Q.er_max >= 0.f && pb.u_right) {
-                            const float ur = pb.u_right[sk_idx(sk)];
-                            if (ur > 0 && fabsf(Q.ur - ur) > Q.er_max) continue;
+                const int ix = cr.x0 + c;
+                for (int o = blo; o <= bhi; o++) {
+                    // the rows y0..y1 of this column and octave: blocks b0..b1, whose
+                    // first / last block also hold rows outside the window
+                    const uint16_t* bt = G.bstart + (ix * noct + o) * kNumBlk;
+                    const int s0 = bt[b0], e0 = bt[b0 + 1], s1 = bt[b1], e1 = bt[b1 + 1];
+                    for (int a = s0 + sub; a < e1; a += lpc) {
+                        const int ent = G.orun[a];
+                        const int p = ent & 0x1fff, yr = ent >> 13;
+                        if ((a < e0 && yr < ylo) || (a >= s1 && yr > yhi)) continue;
+                        const float2 kp = G.sxy[p];
+                        const float distx = kp.x - Q.u;
+                        const float disty = kp.y - Q.v;
+                        if (!(fabsf(distx) < Q.r && fabsf(disty) < Q.r)) continue;
+                        if (sfmp && kp_blocked(sfmp[p], P)) continue;  // null: nothing claimed yet
+                        int d;
+                        if (G.sdesc) {
+                            if (Q.er_max >= 0.f && pb.u_right) {
+                                const float ur = pb.u_right[sk_idx(G.skey[p])];
+                                if (ur > 0 && fabsf(Q.ur - ur) > Q.er_max) continue;
+                            }
+                            const uint4 a4 = G.sdesc[2 * p], b4 = G.sdesc[2 * p + 1];
+                            d = __popcll(q0 ^ ((unsigned long long)a4.y << 32 | a4.x)) +
+                                __popcll(q1 ^ ((unsigned long long)a4.w << 32 | a4.z)) +
+                                __popcll(q2 ^ ((unsigned long long)b4.y << 32 | b4.x)) +
+                                __popcll(q3 ^ ((unsigned long long)b4.w << 32 | b4.z));
+                        } else {
+                            const int i = sk_idx(G.skey[p]);
+                            if (Q.er_max >= 0.f && pb.u_right) {
+                                const float ur = pb.u_right[i];
+                                if (ur > 0 && fabsf(Q.ur - ur) > Q.er_max) continue;
+                            }
+                            const unsigned long long* tt = (const unsigned long long*)(pb.desc + (size_t)i * 32);
+                            d = __popcll(q0 ^ tt[0]) + __popcll(q1 ^ tt[1]) + __popcll(q2 ^ tt[2]) +
+                                __popcll(q3 ^ tt[3]);
                         }
-                        const uint4 a = G.sdesc[2 * p], b = G.sdesc[2 * p + 1];
-                        d = __popcll(q0 ^ ((unsigned long long)a.y << 32 | a.x)) +
-                            __popcll(q1 ^ ((unsigned long long)a.w << 32 | a.z)) +
-                            __popcll(q2 ^ ((unsigned long long)b.y << 32 | b.x)) +
-                            __popcll(q3 ^ ((unsigned long long)b.w << 32 | b.z));
-                    } else {
-                        const int i = sk_idx(sk);
-                        if (Q.er_max >= 0.f && pb.u_right) {
-                            const float ur = pb.u_right[i];
-                            if (ur > 0 && fabsf(Q.ur - ur) > Q.er_max) continue;
+                        const unsigned key = ((unsigned)d << 13) | (unsigned)p;
+                        seen++;
+                        if (key < k[3]) {
+                            if (key < k[2]) {
+                                k[3] = k[2];
+                                if (key < k[1]) {
+                                    k[2] = k[1];
+                                    if (key < k[0]) { k[1] = k[0]; k[0] = key; }
+                                    else k[1] = key;
+                                } else k[2] = key;
+                            } else k[3] = key;
                         }
-                        const unsigned long long* tt = (const unsigned long long*)(pb.desc + (size_t)i * 32);
-                        d = __popcll(q0 ^ tt[0]) + __popcll(q1 ^ tt[1]) + __popcll(q2 ^ tt[2]) + __popcll(q3 ^ tt[3]);
-                    }
-                    const unsigned key = ((unsigned)d << 13) | (unsigned)p;
-                    seen++;
-                    if (key < k[3]) {
-                        if (key < k[2]) {
-                            k[3] = k[2];
-                            if (key < k[1]) {
-                                k[2] = k[1];
-                                if (key < k[0]) { k[1] = k[0]; k[0] = key; }
-                                else k[1] = key;
-                            } else k[2] = key;
-                        } else k[3] = key;
                     }
                 }
             }
@@ -377,11 +496,13 @@ __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~(siz
 
 // LDS layout of k_proj_search (byte offsets), shared by the kernel and its launcher.
 struct ProjLds {
-    size_t skey, cstart, sxy, sfmp, owner, sang, sdesc, qk, qmp, qang, mlist, mbin, total;
-    __host__ __device__ ProjLds(int n, int n2, int nq, bool dlds, bool qlds) {
+    size_t skey, colstart, bstart, orun, sxy, sfmp, owner, sang, sdesc, qk, qmp, qang, mlist, mbin, total;
+    __host__ __device__ ProjLds(int n, int n2, int nq, bool dlds, bool qlds, int noct) {
         skey = 0;
-        cstart = align16((size_t)n2 * 4);
-        sxy = align16(cstart + (size_t)(kNumCells + 1) * 2);
+        colstart = align16((size_t)n2 * 4);
+        bstart = align16(colstart + (size_t)(kGridCols + 1) * 2);
+        orun = align16(bstart + (size_t)bucket_table_len(noct) * 2);
+        sxy = align16(orun + (size_t)n * 2);  // also build_octave_runs' counters, before the fill
         sfmp = sxy + (size_t)n * 8;
         owner = sfmp + (size_t)n * 4;
         sang = owner + (size_t)n * 4;  // keypoint angles in sorted order: the replay's histogram bins
@@ -394,6 +515,7 @@ struct ProjLds {
         mlist = qang + (size_t)nq * 4;
         mbin = mlist + (size_t)nq * 4;
         total = qlds ? mbin + (size_t)nq * 4 : o;
+        if (total < sxy + octave_runs_scratch(noct)) total = sxy + octave_runs_scratch(noct);
     }
 };
 
@@ -590,9 +712,11 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     if (st && tid == 0) st[0] = wall_clock64();
     int n2 = 1;
     while (n2 < n) n2 <<= 1;
-    const ProjLds L(n, n2, nq, DLDS, QLDS);
+    const ProjLds L(n, n2, nq, DLDS, QLDS, P.noct);
     unsigned* skey = (unsigned*)(smem + L.skey);
-    uint16_t* cstart = (uint16_t*)(smem + L.cstart);
+    uint16_t* colstart = (uint16_t*)(smem + L.colstart);
+    uint16_t* bstart = (uint16_t*)(smem + L.bstart);
+    uint16_t* orun = (uint16_t*)(smem + L.orun);
     float2* sxy = (float2*)(smem + L.sxy);
     int* sfmp = (int*)(smem + L.sfmp);
     int* owner = (int*)(smem + L.owner);
@@ -629,6 +753,13 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     if (tid < kHistoLength) s_hist[tid] = 0;
     __syncthreads();
     block_bitonic_sort<NT>(skey, n2);
+    if (st && tid == 0) st[10] = wall_clock64();
+    build_colstart<NT>(skey, n, colstart);
+    __syncthreads();
+    if (st && tid == 0) st[11] = wall_clock64();
+    // the octave runs' counters live where the per-keypoint state goes next
+    build_octave_runs<NT>(skey, colstart, P.noct, bstart, orun, (unsigned*)(smem + L.sxy));
+    __syncthreads();
     for (int p = tid; p < n; p += NT) {
         const int i = sk_idx(skey[p]);
         const orbx_keypoint& kp = pb.keys[i];
@@ -643,16 +774,9 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
             sdesc[t] = ((const uint4*)(pb.desc + (size_t)i * 32))[t & 1];
         }
     }
-    // cstart[c] = first sorted position whose cell >= c (each cell written once)
-    for (int p = tid; p <= n; p += NT) {
-        const int prev = p == 0 ? -1 : (int)(skey[p - 1] >> 18);
-        const int cur = p == n ? kNumCells : (int)(skey[p] >> 18);
-        const int hi = cur < kNumCells ? cur : kNumCells;
-        for (int c = prev + 1; c <= hi; c++) cstart[c] = (uint16_t)p;
-    }
     __syncthreads();
     if (st && tid == 0) st[1] = wall_clock64();
-    const SortedGrid G{skey, cstart, sxy, sdesc};
+    const SortedGrid G{skey, bstart, orun, sxy, sdesc, P.noct};
     {
         constexpr int kStep = kWaves * 4;
         int qb = wave * 4;
@@ -701,13 +825,14 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
 
 // Byte layout of one problem's grid in the global grid area.
 struct SeqGridLayout {
-    size_t skey, cstart, sxy, sang, sfmp, sdesc, total;
-    __host__ __device__ SeqGridLayout(int cap) {
+    size_t skey, bstart, orun, sxy, sang, sfmp, sdesc, total;
+    __host__ __device__ SeqGridLayout(int cap, int noct) {
         int n2 = 1;
         while (n2 < cap) n2 <<= 1;
         skey = 0;
-        cstart = align16((size_t)n2 * 4);
-        sxy = align16(cstart + (size_t)(kNumCells + 1) * 2);
+        bstart = align16((size_t)n2 * 4);
+        orun = align16(bstart + (size_t)bucket_table_len(noct) * 2);
+        sxy = align16(orun + (size_t)cap * 2);
         sang = align16(sxy + (size_t)cap * 8);
         sfmp = align16(sang + (size_t)cap * 4);  // the claims (mvpMapPoints) before the search, sorted
         sdesc = align16(sfmp + (size_t)cap * 4);
@@ -715,18 +840,19 @@ struct SeqGridLayout {
     }
 };
 
-__device__ __forceinline__ SortedGrid seq_grid(unsigned char* base, const SeqGridLayout& g) {
-    return SortedGrid{(const unsigned*)(base + g.skey), (const uint16_t*)(base + g.cstart),
-                      (const float2*)(base + g.sxy), (const uint4*)(base + g.sdesc)};
+__device__ __forceinline__ SortedGrid seq_grid(unsigned char* base, const SeqGridLayout& g, int noct) {
+    return SortedGrid{(const unsigned*)(base + g.skey), (const uint16_t*)(base + g.bstart),
+                      (const uint16_t*)(base + g.orun), (const float2*)(base + g.sxy),
+                      (const uint4*)(base + g.sdesc), noct};
 }
 
 constexpr int kSeqGridThreads = 256;
 
 __global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem* __restrict__ probs,
-                                                              unsigned char* __restrict__ grids, int cap) {
+                                                              unsigned char* __restrict__ grids, int cap, int noct) {
     extern __shared__ __align__(16) unsigned char smem[];
     const ProjProblem pb = probs[blockIdx.x];
-    const SeqGridLayout gl(cap);
+    const SeqGridLayout gl(cap, noct);
     unsigned char* gb = grids + (size_t)blockIdx.x * gl.total;
     const int tid = threadIdx.x, n = pb.n;
     int n2 = 1;
@@ -750,7 +876,8 @@ __global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem*
     float* sang = (float*)(gb + gl.sang);
     int* gfmp = (int*)(gb + gl.sfmp);
     uint4* sdesc = (uint4*)(gb + gl.sdesc);
-    uint16_t* cstart = (uint16_t*)(gb + gl.cstart);
+    uint16_t* colstart = (uint16_t*)(smem + align16((size_t)n2 * 4));
+    unsigned* cnt = (unsigned*)(smem + align16(align16((size_t)n2 * 4) + (size_t)(kGridCols + 1) * 2));
     for (int p = tid; p < n; p += kSeqGridThreads) {
         const unsigned k = skey[p];
         const int i = sk_idx(k);
@@ -764,12 +891,10 @@ __global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem*
         const int i = sk_idx(skey[t >> 1]);
         sdesc[t] = ((const uint4*)(pb.desc + (size_t)i * 32))[t & 1];
     }
-    for (int p = tid; p <= n; p += kSeqGridThreads) {
-        const int prev = p == 0 ? -1 : (int)(skey[p - 1] >> 18);
-        const int cur = p == n ? kNumCells : (int)(skey[p] >> 18);
-        const int hi = cur < kNumCells ? cur : kNumCells;
-        for (int c = prev + 1; c <= hi; c++) cstart[c] = (uint16_t)p;
-    }
+    build_colstart<kSeqGridThreads>(skey, n, colstart);
+    __syncthreads();
+    build_octave_runs<kSeqGridThreads>(skey, colstart, noct, (uint16_t*)(gb + gl.bstart), (uint16_t*)(gb + gl.orun),
+                                       cnt);
 }
 
 constexpr int kSeqScoreThreads = 256;  // 16 queries (4 per wave, one 16-lane row each)
@@ -786,8 +911,8 @@ __global__ __launch_bounds__(kSeqScoreThreads) void k_seq_score(const ProjProble
     const int p = x + kXcds * j;
     if (p >= nprob) return;  // whole workgroup: XCD x has fewer problems
     const ProjProblem pb = probs[p];
-    const SeqGridLayout gl(cap);
-    const SortedGrid G = seq_grid(grids + (size_t)p * gl.total, gl);
+    const SeqGridLayout gl(cap, P.noct);
+    const SortedGrid G = seq_grid(grids + (size_t)p * gl.total, gl, P.noct);
     const int q = blk * kSeqScoreQ + (threadIdx.x >> 4);
     if (blk * kSeqScoreQ >= pb.nq) return;  // whole workgroup past the queries
     const QueryReg cur = load_query(pb, min(q, pb.nq - 1));
@@ -814,8 +939,8 @@ __global__ __launch_bounds__(64) void k_seq_commit(const ProjProblem* __restrict
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_hist[kHistoLength];
     const ProjProblem pb = probs[blockIdx.x];
-    const SeqGridLayout gl(cap);
-    const SortedGrid G = seq_grid(grids + (size_t)blockIdx.x * gl.total, gl);
+    const SeqGridLayout gl(cap, P.noct);
+    const SortedGrid G = seq_grid(grids + (size_t)blockIdx.x * gl.total, gl, P.noct);
     const float* gang = (const float*)(grids + (size_t)blockIdx.x * gl.total + gl.sang);
     const int lane = threadIdx.x, n = pb.n, nq = pb.nq;
     int* sfmp = (int*)smem;
@@ -842,7 +967,7 @@ __global__ __launch_bounds__(64) void k_seq_commit(const ProjProblem* __restrict
     for (int p = lane; p < n; p += 64) pb.frame_mp[sk_idx(G.skey[p])] = sfmp[p];
 }
 
-size_t seq_grid_bytes(int cap) { return SeqGridLayout(cap).total; }
+size_t seq_grid_bytes(int cap, int noct) { return SeqGridLayout(cap, noct).total; }
 
 hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned char* grids,
                             int cap, unsigned long long* scratch, const long long* d_scratch_off, hipStream_t stream) {
@@ -850,7 +975,8 @@ hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjPar
     if (cap <= 0 || cap >= 8192) return hipErrorInvalidValue;  // 13-bit keypoint positions
     int n2 = 1;
     while (n2 < cap) n2 <<= 1;
-    const size_t lds_grid = (size_t)n2 * 4;
+    if (P.noct < 1 || P.noct > 32) return hipErrorInvalidValue;
+    const size_t lds_grid = align16(align16((size_t)n2 * 4) + (size_t)(kGridCols + 1) * 2) + octave_runs_scratch(P.noct);
     const size_t lds_commit = (size_t)cap * 12;
     if (lds_grid > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)k_seq_grid, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -862,7 +988,8 @@ hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjPar
                                            (int)lds_commit);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_seq_grid, dim3(nprob), dim3(kSeqGridThreads), lds_grid, stream, d_probs, grids, cap);
+    hipLaunchKernelGGL(k_seq_grid, dim3(nprob), dim3(kSeqGridThreads), lds_grid, stream, d_probs, grids, cap,
+                       P.noct);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int qblocks = (cap + kSeqScoreQ - 1) / kSeqScoreQ;
@@ -961,6 +1088,7 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
                               bool tiny) {
     if (nprob <= 0) return hipSuccess;
     if (max_n >= 8192) return hipErrorInvalidValue;  // 13-bit keypoint positions
+    if (P.noct < 1 || P.noct > 32) return hipErrorInvalidValue;
     int n2 = 1;
     while (n2 < max_n) n2 <<= 1;
     const size_t limit = 160 * 1024 - 256;  // minus the static histogram
@@ -968,14 +1096,14 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
     // 1024 threads.  Small (meant to run beside other kernels): neither, 256 threads.
     small = small || tiny;
     bool dlds = !small, qlds = !small;
-    if (!small && ProjLds(max_n, n2, max_nq, true, true).total > limit) {
+    if (!small && ProjLds(max_n, n2, max_nq, true, true, P.noct).total > limit) {
         qlds = false;
-        if (ProjLds(max_n, n2, max_nq, true, false).total > limit) {
+        if (ProjLds(max_n, n2, max_nq, true, false, P.noct).total > limit) {
             dlds = false;
-            qlds = ProjLds(max_n, n2, max_nq, false, true).total <= limit;
+            qlds = ProjLds(max_n, n2, max_nq, false, true, P.noct).total <= limit;
         }
     }
-    const size_t lds = ProjLds(max_n, n2, max_nq, dlds, qlds).total;
+    const size_t lds = ProjLds(max_n, n2, max_nq, dlds, qlds, P.noct).total;
     if (lds > limit) return hipErrorInvalidValue;
     const void* fn;
     const int nt = tiny ? kProjThreadsTiny : (small ? kProjThreadsSmall : kProjThreads);

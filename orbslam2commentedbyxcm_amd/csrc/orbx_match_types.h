@@ -54,6 +54,7 @@ struct ProjParams {
     float nnratio;
     int check_ori;          // rotation-consistency histogram (a12, a13)
     unsigned long long* stamps;  // optional: per-problem wall_clock64 phase stamps (diagnostics)
+    int noct;               // octave buckets of the sorted grid: > every keypoint octave (1..32)
 };
 
 // Batched frame-to-frame matching over an extracted device sequence.

@@ -234,7 +234,14 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
     // one problem: the split launches (grid sort, scoring spread over nq / 16 workgroups,
     // one-wave commit) finish sooner than one workgroup doing all three
     const int gcap = n > nq ? n : nq;
-    need += pad(seq_grid_bytes(gcap));
+    // octave buckets of the device grid: one per octave present (the grid keys hold
+    // octave & 31)
+    int noct = 1;
+    for (int i = 0; i < n; i++) {
+        const int o = f->keys[i].octave & 31;
+        if (o + 1 > noct) noct = o + 1;
+    }
+    need += pad(seq_grid_bytes(gcap, noct));
     HIP_TRY(m->arena.reserve(need));
     m->arena.used = 0;
     auto* d_keys = m->arena.take<orbx_keypoint>(n);
@@ -248,7 +255,7 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
     auto* d_scr = m->arena.take<unsigned long long>(kProjScratchWords * (size_t)nq);
     auto* d_off = m->arena.take<long long>(1);
     auto* d_nm = m->arena.take<int32_t>(1);
-    auto* d_grid = m->arena.take<unsigned char>(seq_grid_bytes(gcap));
+    auto* d_grid = m->arena.take<unsigned char>(seq_grid_bytes(gcap, noct));
     hipStream_t s = m->stream;
     m->arena.up(d_keys, f->keys, sizeof(orbx_keypoint) * n);
     m->arena.up(d_desc, f->desc, (size_t)n * 32);
@@ -277,6 +284,7 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
     m->arena.up(d_off, &zero, sizeof(zero));
     ProjParams P = base_params;
     P.mp_obs = d_obs;
+    P.noct = noct;
     HIP_TRY(m->arena.flush(s));
     if (gcap < 8192)
         HIP_TRY(launch_seq_split(d_prob, 1, P, d_grid, gcap, d_scr, d_off, s));
@@ -570,7 +578,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     const size_t np1 = (size_t)(npairs > 0 ? npairs : 1);
     const size_t need = pad(sizeof(ProjQuery) * np1 * cap) + pad(sizeof(ProjProblem) * np1) +
                         pad(sizeof(long long) * np1) + pad(sizeof(unsigned long long) * kProjScratchWords * np1 * cap) +
-                        (split ? pad(seq_grid_bytes(cap) * np1) : 0);
+                        (split ? pad(seq_grid_bytes(cap, nlevels) * np1) : 0);
     if (m->arena.cap < need) {
         HIP_TRY(hipStreamSynchronize(s));
         HIP_TRY(m->arena.reserve(need));
@@ -580,7 +588,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     auto* d_prob = m->arena.take<ProjProblem>(npairs > 0 ? npairs : 1);
     auto* d_off = m->arena.take<long long>(npairs > 0 ? npairs : 1);
     auto* d_scr = m->arena.take<unsigned long long>(kProjScratchWords * (size_t)(npairs > 0 ? npairs : 1) * cap);
-    auto* d_grids = split ? m->arena.take<unsigned char>(seq_grid_bytes(cap) * np1) : nullptr;
+    auto* d_grids = split ? m->arena.take<unsigned char>(seq_grid_bytes(cap, nlevels) * np1) : nullptr;
     if (npairs == 0) {  // otherwise k_seq_build initialises both outputs
         HIP_TRY(hipMemsetAsync(d_cur_mp, 0xff, sizeof(int32_t) * (size_t)batch * cap, s));
         HIP_TRY(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * (size_t)batch, s));
@@ -619,6 +627,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     P.accept_th = TH_HIGH;
     P.ratio_mode = 0;
     P.check_ori = m->check_ori;
+    P.noct = nlevels;  // the extractor's keypoints have octave < nlevels
     // ORBX_MATCH_STAMPS=1: per-phase wall-clock breakdown of the search kernel to stderr
     // (diagnostics only; synchronises the stream).
     const bool stamps = !split && getenv("ORBX_MATCH_STAMPS") != nullptr;  // k_proj_search phases only
@@ -644,6 +653,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
         HIP_TRY(hipMemcpy(h.data(), d_st, h.size() * 8, hipMemcpyDeviceToHost));
         HIP_TRY(hipFree(d_st));
         double ph[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0}, resc = 0, nq = 0, nit = 0, tres = 0, tfirst = 0;
+        double tbit = 0, tfill = 0, tbuild = 0;
         unsigned long long t0 = ~0ull, t1 = 0;
         for (int p = 0; p < npairs; p++) {
             const unsigned long long* r = &h[(size_t)12 * p];
@@ -657,15 +667,19 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
             resc += (double)r[5];
             nq += (double)r[6];
             nit += (double)r[7];
+            tbit += (double)(r[10] - r[0]) * 0.01;
+            tfill += (double)(r[11] - r[10]) * 0.01;
+            tbuild += (double)(r[1] - r[11]) * 0.01;
             if (r[0] < t0) t0 = r[0];
             if (r[4] > t1) t1 = r[4];
         }
         fprintf(stderr,
                 "[orbx stamps] pairs=%d span=%.1fus | mean/max us: sort %.1f/%.1f score %.1f/%.1f commit %.1f/%.1f "
                 "store %.1f/%.1f | rescored %.1f of %.1f queries (%.1f us), %.1f replay rounds (chunk loads + first "
-                "rounds %.1f us)\n",
+                "rounds %.1f us) | sort = bitonic %.1f + column starts %.1f + octave runs and fill %.1f us\n",
                 npairs, (double)(t1 - t0) * 0.01, ph[0] / npairs, mx[0], ph[1] / npairs, mx[1], ph[2] / npairs, mx[2],
-                ph[3] / npairs, mx[3], resc / npairs, nq / npairs, tres / npairs, nit / npairs, tfirst / npairs);
+                ph[3] / npairs, mx[3], resc / npairs, nq / npairs, tres / npairs, nit / npairs, tfirst / npairs,
+                tbit / npairs, tfill / npairs, tbuild / npairs);
     }
     return ORBX_OK;
 }
