@@ -338,8 +338,10 @@ int orbx_compute_distinctive_descriptors_device(int nmp, const int32_t* d_off, c
  * workgroup per problem with keypoint descriptors and query state in LDS (fastest alone);
  * 1 = 256 threads and global-memory query state; 2 = split into three launches (grid
  * sort per problem, scoring spread over all problems' queries, one wave per problem for
- * the ordered commit), for running concurrently with extraction on another stream.
- * Same results in every mode. */
+ * the ordered commit); 3 = one wave per problem; 4 = lean: 1024 threads with only the
+ * sorted grid and the claims in LDS (descriptors, query state and angles in global
+ * memory), the form that leaves the most LDS to extraction running concurrently on
+ * another stream.  Same results in every mode. */
 int orbx_matcher_set_footprint(orbx_matcher* m, int mode);
 
 /* HIP-event timing of orbx_match_sequence_device and orbx_compute_stereo_matches_batch_device:

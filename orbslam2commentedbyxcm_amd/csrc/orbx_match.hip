@@ -447,9 +447,11 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
         const unsigned long long dry = __ballot(over && k[0] == kNoEntry);
         trunc = trunc || ((dry >> rsh) & gmask) != 0;
         m[j] = row_min_u32(k[0]);
-        if (K == 64) {
-            m[j] = umin_(m[j], (unsigned)__shfl_xor((int)m[j], 16));
-            m[j] = umin_(m[j], (unsigned)__shfl_xor((int)m[j], 32));
+        if (K == 64) {  // the four rows' minima by v_readlane: wave-uniform, no LDS round trip
+            m[j] = umin_(umin_((unsigned)__builtin_amdgcn_readlane((int)m[j], 0),
+                               (unsigned)__builtin_amdgcn_readlane((int)m[j], 16)),
+                         umin_((unsigned)__builtin_amdgcn_readlane((int)m[j], 32),
+                               (unsigned)__builtin_amdgcn_readlane((int)m[j], 48)));
         }
         if (k[0] == m[j] && m[j] != kNoEntry) {
             k[0] = k[1];
@@ -505,8 +507,10 @@ struct ProjLds {
         sxy = align16(orun + (size_t)n * 2);  // also build_octave_runs' counters, before the fill
         sfmp = sxy + (size_t)n * 8;
         owner = sfmp + (size_t)n * 4;
-        sang = owner + (size_t)n * 4;  // keypoint angles in sorted order: the replay's histogram bins
-        size_t o = align16(sang + (size_t)n * 4);
+        // keypoint angles in sorted order (the rotation bins), with the LDS-resident query
+        // state only; the lean form reads them from the keypoints after the replay
+        sang = owner + (size_t)n * 4;
+        size_t o = align16(sang + (qlds ? (size_t)n * 4 : 0));
         sdesc = o;
         if (dlds) o += (size_t)n * 32;
         qk = o;
@@ -540,7 +544,6 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
     for (int base = 0; base < nq; base += 64) {
         const int q = base + lane;
         int mp = -1;
-        float qa = 0.f;
         unsigned e[kTopK];
 #pragma unroll
         for (int j = 0; j < kTopK; j++) e[j] = kNoEntry;
@@ -552,32 +555,51 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
             const uint4 v = qk[2 * q], w = qk[2 * q + 1];
             e[0] = v.x; e[1] = v.y; e[2] = v.z; e[3] = v.w;
             e[4] = w.x; e[5] = w.y; e[6] = w.z; e[7] = w.w;
-            qa = qang[q];
         }
         int start = 0;
+        // Per lane: c1 / c2 = the first two unclaimed entries of its list, exhausted = a
+        // full or truncated list ran out.  They only change when a claim lands on c1 or
+        // c2, so a round re-derives them only for the lanes whose c1 / c2 an earlier lane
+        // committed (and for a re-scored lane), not the whole list of every lane.
+        unsigned c1 = kNoEntry, c2 = kNoEntry;
+        bool exhausted = false;
+        bool refresh = true;
         while (true) {
             niter++;
             const bool act = lane >= start && mp >= 0;
-            unsigned c1 = kNoEntry, c2 = kNoEntry;
-            bool exhausted = false;
-            if (act) {
-                // all the list's claim words in one batch of independent LDS reads (and
-                // Observations() loads), not one dependent read per entry
-                const int last = pb.n > 0 ? pb.n - 1 : 0;
-                bool blk[kTopK];
+            if (__ballot(act && refresh)) {
+                if (act && refresh) {
+                    // all the list's claim words in one batch of independent LDS reads (and
+                    // Observations() loads), not one dependent read per entry
+                    const int last = pb.n > 0 ? pb.n - 1 : 0;
+                    int fm[kTopK];
+                    bool blk[kTopK];
 #pragma unroll
-                for (int j = 0; j < kTopK; j++) blk[j] = kp_blocked(sfmp[min(ent_pos(e[j]), last)], P);
-                int found = 0;
+                    for (int j = 0; j < kTopK; j++) fm[j] = sfmp[min(ent_pos(e[j]), last)];
+                    if (P.blocked_mode == 1) {
 #pragma unroll
-                for (int j = 0; j < kTopK; j++) {
-                    if (e[j] < kTrunc && found < 2 && !blk[j]) {
-                        if (found == 0) c1 = e[j];
-                        else c2 = e[j];
-                        found++;
+                        for (int j = 0; j < kTopK; j++) blk[j] = fm[j] >= 0;
+                    } else {
+                        int ob[kTopK];
+#pragma unroll
+                        for (int j = 0; j < kTopK; j++) ob[j] = P.mp_obs[fm[j] >= 0 ? fm[j] : 0];
+#pragma unroll
+                        for (int j = 0; j < kTopK; j++) blk[j] = fm[j] >= 0 && ob[j] > 0;
                     }
+                    int found = 0;
+                    c1 = kNoEntry;
+                    c2 = kNoEntry;
+#pragma unroll
+                    for (int j = 0; j < kTopK; j++) {
+                        if (e[j] < kTrunc && found < 2 && !blk[j]) {
+                            if (found == 0) c1 = e[j];
+                            else c2 = e[j];
+                            found++;
+                        }
+                    }
+                    // a full (or truncated) list may hide unlisted candidates
+                    exhausted = e[kTopK - 1] != kNoEntry && found < need;
                 }
-                // a full (or truncated) list may hide unlisted candidates
-                exhausted = e[kTopK - 1] != kNoEntry && found < need;
             }
             bool acc = false;
             if (act && !exhausted && c1 != kNoEntry && ent_dist(c1) <= P.accept_th) {
@@ -591,16 +613,19 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
             }
             const int tpos = acc ? ent_pos(c1) : -1;
             // A query depends on an earlier one of the chunk if that one claims its best
-            // (or, with the ratio test, second best) keypoint.
+            // (or, with the ratio test, second best) keypoint.  Without the ratio test a
+            // query that does not accept its c1 cannot be affected: every later entry is
+            // at least as far (the list is in key order), so it stays unmatched.
             // owner[p] = lowest lane of this round claiming p (LDS ops of a wave are
             // executed in order: all atomics, then all reads, then the reset).
             if (acc) atomicMin(&owner[tpos], lane);
-            bool conf = exhausted;
+            int o1 = 0x7fffffff, o2 = 0x7fffffff;
             if (act && !exhausted) {
-                if (c1 != kNoEntry && owner[ent_pos(c1)] < lane) conf = true;
-                if (P.ratio_mode && c2 != kNoEntry && owner[ent_pos(c2)] < lane) conf = true;
+                if (c1 != kNoEntry && (acc || P.ratio_mode)) o1 = owner[ent_pos(c1)];
+                if (P.ratio_mode && c2 != kNoEntry) o2 = owner[ent_pos(c2)];
             }
             if (acc) owner[tpos] = 0x7fffffff;
+            const bool conf = (act && exhausted) || o1 < lane || o2 < lane;
             const unsigned long long cm = __ballot(conf);
             const int f = cm ? __ffsll((long long)cm) - 1 : 64;
             const bool com = acc && lane < f;
@@ -608,20 +633,19 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
             if (com) sfmp[tpos] = mp;
             nmatch += __popcll(comm);
             if (P.check_ori) {
+                // the match is recorded with its query; the rotation bins are computed
+                // after the replay, off the sequential path
                 if (com) {
-                    float rot = qa - angle_of(tpos);
-                    if (rot < 0.0f) rot += 360.0f;
-                    int bin = (int)roundf(rot * factor);
-                    if (bin == kHistoLength) bin = 0;
                     const int r = nrec + __popcll(comm & below);
                     mlist[r] = tpos;
-                    mbin[r] = bin;
-                    atomicAdd(&s_hist[bin], 1);
+                    mbin[r] = q;
                 }
                 nrec += __popcll(comm);
             }
             if (f >= 64) break;
             if (st && start == 0) t_first += wall_clock64() - t_chunk;
+            // c1 / c2 claimed by a committed lane (lanes < f), or lane f itself
+            refresh = lane == f || o1 < f || o2 < f;
             if (__builtin_amdgcn_readlane((int)exhausted, f)) {
                 const unsigned long long t0 = st ? wall_clock64() : 0;
                 nrescore++;
@@ -641,6 +665,21 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
     // the match list (global scratch in some modes) is read back by other lanes below
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     __builtin_amdgcn_wave_barrier();
+    if (P.check_ori) {
+        // rotHist of the committed matches (ORBmatcher.cc:1750-1757): bin of (query angle
+        // - keypoint angle); integer counts, so the order of the additions is immaterial
+        for (int m = lane; m < nrec; m += 64) {
+            const int tpos = mlist[m];
+            float rot = qang[mbin[m]] - angle_of(tpos);
+            if (rot < 0.0f) rot += 360.0f;
+            int bin = (int)roundf(rot * factor);
+            if (bin == kHistoLength) bin = 0;
+            mbin[m] = bin;
+            atomicAdd(&s_hist[bin], 1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    }
     if (P.check_ori) {
         // ComputeThreeMaxima, ORBmatcher.cc:1935-1977
         int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
@@ -766,7 +805,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
         sxy[p] = make_float2(kp.x, kp.y);
         sfmp[p] = pb.frame_mp[i];
         owner[p] = 0x7fffffff;
-        sang[p] = kp.angle;
+        if (QLDS) sang[p] = kp.angle;
     }
     if (DLDS) {
         for (int t = tid; t < 2 * n; t += NT) {
@@ -804,7 +843,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     // wave slots go back to whatever runs beside this kernel for the rest of its life.
     if (wave != 0) return;
     proj_replay(pb, P, G, sfmp, owner, qk, qmp, qang, mlist, mbin, s_hist,
-                [&](int tpos) { return sang[tpos]; }, st);
+                [&](int tpos) { return QLDS ? sang[tpos] : pb.keys[sk_idx(skey[tpos])].angle; }, st);
     wave_lds_fence();
     for (int p = lane; p < n; p += 64) pb.frame_mp[sk_idx(skey[p])] = sfmp[p];
     if (st && lane == 0) st[4] = wall_clock64();
@@ -1085,7 +1124,7 @@ hipError_t launch_seq_build(const SeqArgs& A, int npairs, ProjQuery* queries, Pr
 
 hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned long long* scratch,
                               const long long* d_scratch_off, int max_n, int max_nq, hipStream_t stream, bool small,
-                              bool tiny) {
+                              bool tiny, bool lean) {
     if (nprob <= 0) return hipSuccess;
     if (max_n >= 8192) return hipErrorInvalidValue;  // 13-bit keypoint positions
     if (P.noct < 1 || P.noct > 32) return hipErrorInvalidValue;
@@ -1095,8 +1134,10 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
     // Fast: LDS-resident descriptors (the scoring loads), then LDS-resident query state,
     // 1024 threads.  Small (meant to run beside other kernels): neither, 256 threads.
     small = small || tiny;
-    bool dlds = !small, qlds = !small;
-    if (!small && ProjLds(max_n, n2, max_nq, true, true, P.noct).total > limit) {
+    // lean: 1024 threads, but only the grid and the claims in LDS (descriptors and query
+    // state in global memory) -- the form that shares a CU best with other kernels
+    bool dlds = !small && !lean, qlds = !small && !lean;
+    if (dlds && ProjLds(max_n, n2, max_nq, true, true, P.noct).total > limit) {
         qlds = false;
         if (ProjLds(max_n, n2, max_nq, true, false, P.noct).total > limit) {
             dlds = false;

@@ -204,7 +204,7 @@ struct orbx_matcher {
     bool timing = false;
     hipEvent_t ev[kRing][2] = {};
     long long ncalls = 0;
-    int footprint = 0;  // orbx_matcher_set_footprint: 0 full, 1 small, 2 split, 3 one wave
+    int footprint = 0;  // orbx_matcher_set_footprint: 0 full, 1 small, 2 split, 3 one wave, 4 lean
     // device-only scratch of the batched device calls (no pinned mirror)
     char* dscr = nullptr;
     size_t dscr_cap = 0;
@@ -641,7 +641,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
         HIP_TRY(launch_seq_split(d_prob, npairs, P, d_grids, cap, d_scr, d_off, s));
     } else {
         HIP_TRY(launch_proj_search(d_prob, npairs, P, d_scr, d_off, cap, cap, s, m->footprint == 1,
-                                   m->footprint == 3));
+                                   m->footprint == 3, m->footprint == 4));
     }
     if (m->timing) {
         HIP_TRY(hipEventRecord(ev[1], s));
@@ -686,7 +686,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
 
 int orbx_matcher_set_footprint(orbx_matcher* m, int small) {
     if (!m) return fail(ORBX_ERR_ARG, "null matcher");
-    if (small < 0 || small > 3) return fail(ORBX_ERR_ARG, "footprint is 0, 1, 2 or 3");
+    if (small < 0 || small > 4) return fail(ORBX_ERR_ARG, "footprint is 0, 1, 2, 3 or 4");
     m->footprint = small;
     return ORBX_OK;
 }

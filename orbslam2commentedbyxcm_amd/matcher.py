@@ -431,7 +431,8 @@ class ORBmatcher:
     def set_footprint(self, mode) -> None:
         """Search-kernel footprint of match_sequence_device (orbx_matcher_set_footprint):
         0 / False = one 1024-thread workgroup per problem, 1 / True = 256 threads with
-        global query state, 2 = split into grid / score / commit launches."""
+        global query state, 2 = split into grid / score / commit launches, 3 = one wave
+        per problem, 4 = lean (1024 threads, only the grid and the claims in LDS)."""
         L.check(L.lib().orbx_matcher_set_footprint(self._h, int(mode)))
 
     def last_ms(self) -> float:
