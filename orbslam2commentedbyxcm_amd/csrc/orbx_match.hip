@@ -536,7 +536,7 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
                             AngleFn angle_of, unsigned long long* st) {
     const int lane = threadIdx.x & 63;
     const int nq = pb.nq;
-    int nmatch = 0, nrec = 0, nrescore = 0, niter = 0;
+    int nmatch = 0, nrec = 0, nrescore = 0, niter = 0, ntrunc = 0;
     unsigned long long t_res = 0, t_first = 0;  // diagnostics (stamps): re-scoring, chunk loads + first round
     const float factor = kHistoLength / 360.0f;
     const int need = P.ratio_mode ? 2 : 1;
@@ -597,8 +597,19 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
                             found++;
                         }
                     }
-                    // a full (or truncated) list may hide unlisted candidates
+                    // a full (or truncated) list may hide unlisted candidates -- but they are
+                    // at least as far as its last exact entry (the list holds the smallest
+                    // keys), so when that entry, or the unclaimed c1 of a ratio test, is
+                    // already beyond the acceptance threshold the query stays unmatched
                     exhausted = e[kTopK - 1] != kNoEntry && found < need;
+                    if (exhausted) {
+                        int lastd = -1;
+#pragma unroll
+                        for (int j = 0; j < kTopK; j++)
+                            if (e[j] < kTrunc) lastd = ent_dist(e[j]);
+                        if (found == 0 && lastd > P.accept_th) exhausted = false;
+                        if (found == 1 && ent_dist(c1) > P.accept_th) exhausted = false;
+                    }
                 }
             }
             bool acc = false;
@@ -649,6 +660,12 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
             if (__builtin_amdgcn_readlane((int)exhausted, f)) {
                 const unsigned long long t0 = st ? wall_clock64() : 0;
                 nrescore++;
+                if (st) {  // diagnostics: the list ran out at a truncation, not at its 8th entry
+                    bool tr = false;
+#pragma unroll
+                    for (int j = 0; j < kTopK; j++) tr = tr || e[j] == kTrunc;
+                    ntrunc += __builtin_amdgcn_readlane((int)tr, f);
+                }
                 wave_lds_fence();
                 unsigned ne[kTopK];
                 score_groupk<64>(pb, P, bcast_query(mine, f), true, G, sfmp, ne);  // wave-uniform result
@@ -714,6 +731,7 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
     if (st && lane == 0) {
         st[3] = wall_clock64();
         st[5] = nrescore;
+        st[12] = ntrunc;
         st[6] = nq;
         st[7] = niter;
         st[8] = t_res;
@@ -747,7 +765,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int kWaves = NT / 64;
     const int n = pb.n, nq = pb.nq;
-    unsigned long long* st = P.stamps ? P.stamps + 12 * blockIdx.x : nullptr;
+    unsigned long long* st = P.stamps ? P.stamps + kStampWords * blockIdx.x : nullptr;
     if (st && tid == 0) st[0] = wall_clock64();
     int n2 = 1;
     while (n2 < n) n2 <<= 1;

@@ -44,6 +44,8 @@ struct ProjProblem {
 // Global scratch per query (u64 words) when the per-query state does not fit in LDS.
 constexpr int kProjScratchWords = 6;  // 8-entry candidate list (32 B) + mp, angle, match list, bin
 
+constexpr int kStampWords = 16;  // ProjParams::stamps words per problem
+
 // Call-level semantics of the SearchByProjection overload being executed.
 struct ProjParams {
     const int32_t* mp_obs;  // Observations() per MapPoint id (blocked_mode 0)
@@ -53,7 +55,7 @@ struct ProjParams {
     int ratio_mode;         // 1: reject if bestLevel==bestLevel2 && best > nnratio*second (a11)
     float nnratio;
     int check_ori;          // rotation-consistency histogram (a12, a13)
-    unsigned long long* stamps;  // optional: per-problem wall_clock64 phase stamps (diagnostics)
+    unsigned long long* stamps;  // optional: kStampWords per-problem phase stamps and counters (diagnostics)
     int noct;               // octave buckets of the sorted grid: > every keypoint octave (1..32)
 };
 

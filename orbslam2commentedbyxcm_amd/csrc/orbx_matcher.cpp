@@ -633,8 +633,8 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     const bool stamps = !split && getenv("ORBX_MATCH_STAMPS") != nullptr;  // k_proj_search phases only
     unsigned long long* d_st = nullptr;
     if (stamps) {
-        HIP_TRY(hipMalloc(&d_st, sizeof(unsigned long long) * 12 * npairs));
-        HIP_TRY(hipMemsetAsync(d_st, 0, sizeof(unsigned long long) * 12 * npairs, s));
+        HIP_TRY(hipMalloc(&d_st, sizeof(unsigned long long) * kStampWords * npairs));
+        HIP_TRY(hipMemsetAsync(d_st, 0, sizeof(unsigned long long) * kStampWords * npairs, s));
         P.stamps = d_st;
     }
     if (split) {
@@ -648,15 +648,15 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
         m->ncalls++;
     }
     if (stamps) {
-        std::vector<unsigned long long> h((size_t)12 * npairs);
+        std::vector<unsigned long long> h((size_t)kStampWords * npairs);
         HIP_TRY(hipStreamSynchronize(s));
         HIP_TRY(hipMemcpy(h.data(), d_st, h.size() * 8, hipMemcpyDeviceToHost));
         HIP_TRY(hipFree(d_st));
         double ph[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0}, resc = 0, nq = 0, nit = 0, tres = 0, tfirst = 0;
-        double tbit = 0, tfill = 0, tbuild = 0;
+        double tbit = 0, tfill = 0, tbuild = 0, rtrunc = 0;
         unsigned long long t0 = ~0ull, t1 = 0;
         for (int p = 0; p < npairs; p++) {
-            const unsigned long long* r = &h[(size_t)12 * p];
+            const unsigned long long* r = &h[(size_t)kStampWords * p];
             tres += (double)r[8] * 0.01;
             tfirst += (double)r[9] * 0.01;
             for (int k = 0; k < 4; k++) {
@@ -665,6 +665,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
                 if (d > mx[k]) mx[k] = d;
             }
             resc += (double)r[5];
+            rtrunc += (double)r[12];
             nq += (double)r[6];
             nit += (double)r[7];
             tbit += (double)(r[10] - r[0]) * 0.01;
@@ -676,10 +677,11 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
         fprintf(stderr,
                 "[orbx stamps] pairs=%d span=%.1fus | mean/max us: sort %.1f/%.1f score %.1f/%.1f commit %.1f/%.1f "
                 "store %.1f/%.1f | rescored %.1f of %.1f queries (%.1f us), %.1f replay rounds (chunk loads + first "
-                "rounds %.1f us) | sort = bitonic %.1f + column starts %.1f + octave runs and fill %.1f us\n",
+                "rounds %.1f us) | sort = bitonic %.1f + column starts %.1f + octave runs and fill %.1f us | re-scored at a "
+                "truncation %.1f\n",
                 npairs, (double)(t1 - t0) * 0.01, ph[0] / npairs, mx[0], ph[1] / npairs, mx[1], ph[2] / npairs, mx[2],
                 ph[3] / npairs, mx[3], resc / npairs, nq / npairs, tres / npairs, nit / npairs, tfirst / npairs,
-                tbit / npairs, tfill / npairs, tbuild / npairs);
+                tbit / npairs, tfill / npairs, tbuild / npairs, rtrunc / npairs);
     }
     return ORBX_OK;
 }
