@@ -473,38 +473,86 @@ __device__ __forceinline__ void score_rowk(const ProjProblem& pb, const ProjPara
     score_groupk<16>(pb, P, QR, valid, G, sfmp, out);
 }
 
-// Ascending in-place bitonic sort of n2 (power of two) u32 keys by the workgroup.
+__host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// LDS scratch of grid_sort: one u32 counter per grid cell + the off-grid bucket
+constexpr size_t kGridSortScratch = (size_t)(kNumCells + 1) * 4;
+
+// In-place exclusive scan of a[0..n) (u32) by the workgroup: contiguous segments per
+// thread, a DPP wave scan, the wave totals through LDS.  Ends with a barrier.
 template <int NT>
-__device__ void block_bitonic_sort(unsigned* a, int n2) {
-    for (int k = 2; k <= n2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < n2; i += NT) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const unsigned x = a[i], y = a[l];
-                    const bool up = (i & k) == 0;
-                    if ((x > y) == up) {
-                        a[i] = y;
-                        a[l] = x;
-                    }
-                }
-            }
-            __syncthreads();
-        }
+__device__ void block_exscan_u32(unsigned* a, int n) {
+    __shared__ unsigned s_wsum[NT / 64];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int per = (n + NT - 1) / NT, b = t * per, e = min(n, b + per);
+    unsigned sum = 0;
+    for (int i = b; i < e; i++) sum += a[i];
+    const unsigned incl = wave_inclusive_sum(sum);
+    if (lane == 63) s_wsum[wave] = incl;
+    __syncthreads();
+    unsigned run = incl - sum;
+    for (int w = 0; w < wave; w++) run += s_wsum[w];
+    for (int i = b; i < e; i++) {
+        const unsigned v = a[i];
+        a[i] = run;
+        run += v;
     }
+    __syncthreads();
 }
 
-__host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+// The frame's keypoints sorted by (grid cell, index) into skey[0..n): a counting sort
+// over the cells (Frame::PosInGrid, Frame.cc:558-567; off-grid keypoints last), then
+// each cell's few keys put in index order by one thread.  cnt: kGridSortScratch bytes
+// of LDS.  Whole workgroup; ends with a barrier.
+template <int NT>
+__device__ void grid_sort(const ProjProblem& pb, unsigned* skey, unsigned* cnt) {
+    const int tid = threadIdx.x, n = pb.n;
+    for (int c = tid; c <= kNumCells; c += NT) cnt[c] = 0u;
+    __syncthreads();
+    for (int i = tid; i < n; i += NT) {
+        const orbx_keypoint& kp = pb.keys[i];
+        const int px = (int)roundf((kp.x - pb.min_x) * pb.inv_w);
+        const int py = (int)roundf((kp.y - pb.min_y) * pb.inv_h);
+        const bool in = !(px < 0 || px >= kGridCols || py < 0 || py >= kGridRows);
+        atomicAdd(&cnt[in ? px * kGridRows + py : kNumCells], 1u);
+    }
+    __syncthreads();
+    block_exscan_u32<NT>(cnt, kNumCells + 1);
+    for (int i = tid; i < n; i += NT) {
+        const orbx_keypoint& kp = pb.keys[i];
+        const int px = (int)roundf((kp.x - pb.min_x) * pb.inv_w);
+        const int py = (int)roundf((kp.y - pb.min_y) * pb.inv_h);
+        const bool in = !(px < 0 || px >= kGridCols || py < 0 || py >= kGridRows);
+        const int cell = in ? px * kGridRows + py : kNoCell;
+        const unsigned slot = atomicAdd(&cnt[in ? cell : kNumCells], 1u);
+        skey[slot] = ((unsigned)cell << 18) | ((unsigned)i << 5) | ((unsigned)kp.octave & 31u);
+    }
+    __syncthreads();
+    // cnt[c] is now the end of cell c; a cell holds a handful of keys
+    for (int c = tid; c <= kNumCells; c += NT) {
+        const int b = c == 0 ? 0 : (int)cnt[c - 1], e = (int)cnt[c];
+        for (int i = b + 1; i < e; i++) {
+            const unsigned v = skey[i];
+            int j = i - 1;
+            while (j >= b && skey[j] > v) {
+                skey[j + 1] = skey[j];
+                j--;
+            }
+            skey[j + 1] = v;
+        }
+    }
+    __syncthreads();
+}
 
 // LDS layout of k_proj_search (byte offsets), shared by the kernel and its launcher.
 struct ProjLds {
     size_t skey, colstart, bstart, orun, sxy, sfmp, owner, sang, sdesc, qk, qmp, qang, mlist, mbin, total;
-    __host__ __device__ ProjLds(int n, int n2, int nq, bool dlds, bool qlds, int noct) {
+    __host__ __device__ ProjLds(int n, int nq, bool dlds, bool qlds, int noct) {
         skey = 0;
-        colstart = align16((size_t)n2 * 4);
+        colstart = align16((size_t)n * 4);
         bstart = align16(colstart + (size_t)(kGridCols + 1) * 2);
         orun = align16(bstart + (size_t)bucket_table_len(noct) * 2);
-        sxy = align16(orun + (size_t)n * 2);  // also build_octave_runs' counters, before the fill
+        sxy = align16(orun + (size_t)n * 2);
         sfmp = sxy + (size_t)n * 8;
         owner = sfmp + (size_t)n * 4;
         // keypoint angles in sorted order (the rotation bins), with the LDS-resident query
@@ -519,7 +567,9 @@ struct ProjLds {
         mlist = qang + (size_t)nq * 4;
         mbin = mlist + (size_t)nq * 4;
         total = qlds ? mbin + (size_t)nq * 4 : o;
-        if (total < sxy + octave_runs_scratch(noct)) total = sxy + octave_runs_scratch(noct);
+        // grid_sort's and build_octave_runs' counters, before the fill
+        const size_t scr = octave_runs_scratch(noct) > kGridSortScratch ? octave_runs_scratch(noct) : kGridSortScratch;
+        if (total < sxy + scr) total = sxy + scr;
     }
 };
 
@@ -767,9 +817,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     const int n = pb.n, nq = pb.nq;
     unsigned long long* st = P.stamps ? P.stamps + kStampWords * blockIdx.x : nullptr;
     if (st && tid == 0) st[0] = wall_clock64();
-    int n2 = 1;
-    while (n2 < n) n2 <<= 1;
-    const ProjLds L(n, n2, nq, DLDS, QLDS, P.noct);
+    const ProjLds L(n, nq, DLDS, QLDS, P.noct);
     unsigned* skey = (unsigned*)(smem + L.skey);
     uint16_t* colstart = (uint16_t*)(smem + L.colstart);
     uint16_t* bstart = (uint16_t*)(smem + L.bstart);
@@ -796,20 +844,8 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
         mlist = (int*)(qang + nq);
         mbin = mlist + nq;
     }
-    for (int i = tid; i < n2; i += NT) {
-        unsigned key = 0xffffffffu;
-        if (i < n) {
-            const orbx_keypoint& kp = pb.keys[i];
-            const int px = (int)roundf((kp.x - pb.min_x) * pb.inv_w);  // Frame::PosInGrid, Frame.cc:558-567
-            const int py = (int)roundf((kp.y - pb.min_y) * pb.inv_h);
-            const int cell = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? kNoCell : px * kGridRows + py;
-            key = ((unsigned)cell << 18) | ((unsigned)i << 5) | ((unsigned)kp.octave & 31u);
-        }
-        skey[i] = key;
-    }
     if (tid < kHistoLength) s_hist[tid] = 0;
-    __syncthreads();
-    block_bitonic_sort<NT>(skey, n2);
+    grid_sort<NT>(pb, skey, (unsigned*)(smem + L.sxy));  // counters where the keypoint state goes next
     if (st && tid == 0) st[10] = wall_clock64();
     build_colstart<NT>(skey, n, colstart);
     __syncthreads();
@@ -884,10 +920,8 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
 struct SeqGridLayout {
     size_t skey, bstart, orun, sxy, sang, sfmp, sdesc, total;
     __host__ __device__ SeqGridLayout(int cap, int noct) {
-        int n2 = 1;
-        while (n2 < cap) n2 <<= 1;
         skey = 0;
-        bstart = align16((size_t)n2 * 4);
+        bstart = align16((size_t)cap * 4);
         orun = align16(bstart + (size_t)bucket_table_len(noct) * 2);
         sxy = align16(orun + (size_t)cap * 2);
         sang = align16(sxy + (size_t)cap * 8);
@@ -912,29 +946,16 @@ __global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem*
     const SeqGridLayout gl(cap, noct);
     unsigned char* gb = grids + (size_t)blockIdx.x * gl.total;
     const int tid = threadIdx.x, n = pb.n;
-    int n2 = 1;
-    while (n2 < n) n2 <<= 1;
+    // LDS: skey [cap], colstart [kGridCols + 1], counters
     unsigned* skey = (unsigned*)smem;
-    for (int i = tid; i < n2; i += kSeqGridThreads) {
-        unsigned key = 0xffffffffu;
-        if (i < n) {
-            const orbx_keypoint& kp = pb.keys[i];
-            const int px = (int)roundf((kp.x - pb.min_x) * pb.inv_w);  // Frame::PosInGrid, Frame.cc:558-567
-            const int py = (int)roundf((kp.y - pb.min_y) * pb.inv_h);
-            const int cell = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? kNoCell : px * kGridRows + py;
-            key = ((unsigned)cell << 18) | ((unsigned)i << 5) | ((unsigned)kp.octave & 31u);
-        }
-        skey[i] = key;
-    }
-    __syncthreads();
-    block_bitonic_sort<kSeqGridThreads>(skey, n2);
+    uint16_t* colstart = (uint16_t*)(smem + align16((size_t)cap * 4));
+    unsigned* cnt = (unsigned*)(smem + align16(align16((size_t)cap * 4) + (size_t)(kGridCols + 1) * 2));
+    grid_sort<kSeqGridThreads>(pb, skey, cnt);
     unsigned* gkey = (unsigned*)(gb + gl.skey);
     float2* sxy = (float2*)(gb + gl.sxy);
     float* sang = (float*)(gb + gl.sang);
     int* gfmp = (int*)(gb + gl.sfmp);
     uint4* sdesc = (uint4*)(gb + gl.sdesc);
-    uint16_t* colstart = (uint16_t*)(smem + align16((size_t)n2 * 4));
-    unsigned* cnt = (unsigned*)(smem + align16(align16((size_t)n2 * 4) + (size_t)(kGridCols + 1) * 2));
     for (int p = tid; p < n; p += kSeqGridThreads) {
         const unsigned k = skey[p];
         const int i = sk_idx(k);
@@ -1030,10 +1051,9 @@ hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjPar
                             int cap, unsigned long long* scratch, const long long* d_scratch_off, hipStream_t stream) {
     if (nprob <= 0) return hipSuccess;
     if (cap <= 0 || cap >= 8192) return hipErrorInvalidValue;  // 13-bit keypoint positions
-    int n2 = 1;
-    while (n2 < cap) n2 <<= 1;
     if (P.noct < 1 || P.noct > 32) return hipErrorInvalidValue;
-    const size_t lds_grid = align16(align16((size_t)n2 * 4) + (size_t)(kGridCols + 1) * 2) + octave_runs_scratch(P.noct);
+    const size_t scr = octave_runs_scratch(P.noct) > kGridSortScratch ? octave_runs_scratch(P.noct) : kGridSortScratch;
+    const size_t lds_grid = align16(align16((size_t)cap * 4) + (size_t)(kGridCols + 1) * 2) + scr;
     const size_t lds_commit = (size_t)cap * 12;
     if (lds_grid > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)k_seq_grid, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1146,8 +1166,6 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
     if (nprob <= 0) return hipSuccess;
     if (max_n >= 8192) return hipErrorInvalidValue;  // 13-bit keypoint positions
     if (P.noct < 1 || P.noct > 32) return hipErrorInvalidValue;
-    int n2 = 1;
-    while (n2 < max_n) n2 <<= 1;
     const size_t limit = 160 * 1024 - 256;  // minus the static histogram
     // Fast: LDS-resident descriptors (the scoring loads), then LDS-resident query state,
     // 1024 threads.  Small (meant to run beside other kernels): neither, 256 threads.
@@ -1155,14 +1173,14 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
     // lean: 1024 threads, but only the grid and the claims in LDS (descriptors and query
     // state in global memory) -- the form that shares a CU best with other kernels
     bool dlds = !small && !lean, qlds = !small && !lean;
-    if (dlds && ProjLds(max_n, n2, max_nq, true, true, P.noct).total > limit) {
+    if (dlds && ProjLds(max_n, max_nq, true, true, P.noct).total > limit) {
         qlds = false;
-        if (ProjLds(max_n, n2, max_nq, true, false, P.noct).total > limit) {
+        if (ProjLds(max_n, max_nq, true, false, P.noct).total > limit) {
             dlds = false;
-            qlds = ProjLds(max_n, n2, max_nq, false, true, P.noct).total <= limit;
+            qlds = ProjLds(max_n, max_nq, false, true, P.noct).total <= limit;
         }
     }
-    const size_t lds = ProjLds(max_n, n2, max_nq, dlds, qlds, P.noct).total;
+    const size_t lds = ProjLds(max_n, max_nq, dlds, qlds, P.noct).total;
     if (lds > limit) return hipErrorInvalidValue;
     const void* fn;
     const int nt = tiny ? kProjThreadsTiny : (small ? kProjThreadsSmall : kProjThreads);

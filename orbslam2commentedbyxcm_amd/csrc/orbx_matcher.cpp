@@ -677,7 +677,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
         fprintf(stderr,
                 "[orbx stamps] pairs=%d span=%.1fus | mean/max us: sort %.1f/%.1f score %.1f/%.1f commit %.1f/%.1f "
                 "store %.1f/%.1f | rescored %.1f of %.1f queries (%.1f us), %.1f replay rounds (chunk loads + first "
-                "rounds %.1f us) | sort = bitonic %.1f + column starts %.1f + octave runs and fill %.1f us | re-scored at a "
+                "rounds %.1f us) | sort = grid counting sort %.1f + column starts %.1f + octave runs and fill %.1f us | re-scored at a "
                 "truncation %.1f\n",
                 npairs, (double)(t1 - t0) * 0.01, ph[0] / npairs, mx[0], ph[1] / npairs, mx[1], ph[2] / npairs, mx[2],
                 ph[3] / npairs, mx[3], resc / npairs, nq / npairs, tres / npairs, nit / npairs, tfirst / npairs,
