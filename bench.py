@@ -111,7 +111,7 @@ def newest_profiles(pattern: str):
     numbers in their tags (r01v9 < r01v10)."""
     import re
     files = [f for f in (ROOT / "profiles").glob(pattern) if "vocab" not in f.name]
-    return sorted(files, key=lambda f: [int(x) for x in re.findall(r"\d+", f.name)])
+    return sorted(files, key=lambda f: ([int(x) for x in re.findall(r"\d+", f.name)], f.name))
 
 
 def pmc_valu(stage: str):
