@@ -107,6 +107,14 @@ int orbx_extract_batch_device(orbx_extractor* ex, int batch, const uint8_t* d_im
 /* The extractor's hipStream_t (as void*). */
 void* orbx_extractor_stream(orbx_extractor* ex);
 
+/* Scheduling hook for running other work beside a batched extraction (no reference
+ * counterpart): from now on every extraction records `*event` (a hipEvent_t owned by the
+ * extractor) on its stream right after stage `stage` -- 1 pyramid, 2 blur + FAST
+ * strength, 3 FAST cells, 4 octree; 0 stops recording.  orbx_stream_wait_event makes
+ * another stream wait for the latest record (hipStreamWaitEvent). */
+int orbx_extractor_set_stage_event(orbx_extractor* ex, int stage, void** event);
+int orbx_stream_wait_event(void* stream, void* event);
+
 /* Kernel status of the last extraction (any path), per frame: 0 = complete; bit 0
  * (ORBX_STATUS_NODE_OVERFLOW) = an octree level needed more nodes than its capacity,
  * bit 1 (ORBX_STATUS_ITERATIONS) = an octree loop hit its iteration guard; either way

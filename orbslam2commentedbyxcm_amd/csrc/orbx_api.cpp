@@ -83,6 +83,9 @@ struct orbx_extractor {
     int last_batch = 0;
     bool have_pyramid = false;
     hipStream_t last_stream = nullptr;  // stream of the last extraction (status reads order after it)
+    // orbx_extractor_set_stage_event: recorded after stage `stage_after` of every extraction
+    hipEvent_t stage_ev = nullptr;
+    int stage_after = 0;
 };
 
 namespace {
@@ -157,7 +160,7 @@ int run_device(orbx_extractor* ex, int batch, const uint8_t* d_imgs, size_t fram
         ev = slot;
     }
     hipError_t e = launch_extract(ex->plan, ex->db, batch, d_imgs, frame_pitch, stride, d_kps, d_desc, cap, d_n,
-                                  stream, ev);
+                                  stream, ev, ex->stage_ev, ex->stage_after);
     if (e != hipSuccess) return hip_fail(e, "launch_extract");
     if (ex->db.oct_stamps) {  // diagnostics: per-level k_octree phase times (us) to stderr
         const int L = ex->plan.L;
@@ -339,6 +342,7 @@ void orbx_extractor_destroy(orbx_extractor* ex) {
     for (auto& slot : ex->ev)
         for (auto& e : slot)
             if (e) (void)hipEventDestroy(e);
+    if (ex->stage_ev) (void)hipEventDestroy(ex->stage_ev);
     if (ex->stream) (void)hipStreamDestroy(ex->stream);
     delete ex;
 }
@@ -370,6 +374,21 @@ int orbx_extractor_max_keypoints(orbx_extractor* ex, int width, int height, int*
 }
 
 void* orbx_extractor_stream(orbx_extractor* ex) { return ex ? (void*)ex->stream : nullptr; }
+
+int orbx_extractor_set_stage_event(orbx_extractor* ex, int stage, void** event) {
+    if (!ex || stage < 0 || stage > 4) return fail(ORBX_ERR_ARG, "stage is 0 (off) or 1..4");
+    HIP_TRY(hipSetDevice(ex->device));
+    if (!ex->stage_ev) HIP_TRY(hipEventCreateWithFlags(&ex->stage_ev, hipEventDisableTiming));
+    ex->stage_after = stage;
+    if (event) *event = stage > 0 ? (void*)ex->stage_ev : nullptr;
+    return ORBX_OK;
+}
+
+int orbx_stream_wait_event(void* stream, void* event) {
+    if (!event) return fail(ORBX_ERR_ARG, "null event");
+    HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0));
+    return ORBX_OK;
+}
 
 int orbx_extractor_status(orbx_extractor* ex, int batch, int* flags, int* any) {
     if (!ex || batch < 0) return fail(ORBX_ERR_ARG, "bad argument");

@@ -1442,7 +1442,8 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
 
 hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, const uint8_t* d_imgs,
                           size_t frame_pitch, size_t stride, void* kps, uint8_t* desc, int cap,
-                          int* n_per_frame, hipStream_t stream, hipEvent_t* ev) {
+                          int* n_per_frame, hipStream_t stream, hipEvent_t* ev, hipEvent_t stage_ev,
+                          int stage_after) {
     const int L = plan.L;
     const long long fb = plan.pyr_frame_bytes;
     const int ncells = (int)plan.cells.size();
@@ -1461,6 +1462,7 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
                            plan.pz_lds_a);
     }
     if (ev) (void)hipEventRecord(ev[1], stream);
+    if (stage_ev && stage_after == 1) (void)hipEventRecord(stage_ev, stream);
     {
         dim3 grid(plan.tiles_total * batch);
         int tq = plan.prm.ini_th < plan.prm.min_th ? plan.prm.ini_th : plan.prm.min_th;
@@ -1469,6 +1471,7 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
                            plan.tiles_total, batch, tq);
     }
     if (ev) (void)hipEventRecord(ev[2], stream);
+    if (stage_ev && stage_after == 2) (void)hipEventRecord(stage_ev, stream);
     {
         dim3 grid(((ncells + 3) / 4) * batch);
         const size_t fc_lds = 4 * (size_t)((((plan.fc_wr + 2) * kFcStride + 2 * plan.fc_wr * plan.fc_wc) + 15) & ~15);
@@ -1477,6 +1480,7 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
                            plan.fc_wr, plan.fc_wc);
     }
     if (ev) (void)hipEventRecord(ev[3], stream);
+    if (stage_ev && stage_after == 3) (void)hipEventRecord(stage_ev, stream);
     {
         const int NC = (plan.max_ncap + 63) & ~63;
         const size_t lds = (size_t)NC * (8 + 16 + 12 + 8 + 8 + 16 + 2);
@@ -1486,6 +1490,7 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
                            db.kept, plan.kept_per_frame, db.kept_count, db.status, NC, batch, db.oct_stamps);
     }
     if (ev) (void)hipEventRecord(ev[4], stream);
+    if (stage_ev && stage_after == 4) (void)hipEventRecord(stage_ev, stream);
     {
         dim3 grid(((plan.kept_per_frame + 7) / 8) * batch);
         hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, stream, db.pyr, db.blur, fb, db.lv, L, db.kept,

@@ -127,6 +127,14 @@ class ORBextractor:
     def stream_handle(self) -> int:
         return L.lib().orbx_extractor_stream(self._h) or 0
 
+    def set_stage_event(self, stage: int) -> int:
+        """orbx_extractor_set_stage_event: every extraction records the returned hipEvent_t
+        right after stage `stage` (1 pyramid, 2 blur + FAST strength, 3 FAST cells,
+        4 octree; 0 = off).  Wait on it with stream_wait_event."""
+        ev = C.c_void_p()
+        L.check(L.lib().orbx_extractor_set_stage_event(self._h, int(stage), C.byref(ev)))
+        return ev.value or 0
+
     # ---- kernel status of the last extraction (orbx_extractor_status)
     STATUS_NODE_OVERFLOW = 1
     STATUS_ITERATIONS = 2
@@ -175,3 +183,8 @@ class ORBextractor:
         if self._pyr_cache is None:
             self._pyr_cache = [self.pyramid_level(lv) for lv in range(self.nlevels)]
         return self._pyr_cache
+
+
+def stream_wait_event(stream: int, event: int) -> None:
+    """hipStreamWaitEvent(stream, event) through the library (orbx_stream_wait_event)."""
+    L.check(L.lib().orbx_stream_wait_event(C.c_void_p(stream), C.c_void_p(event)))

@@ -30,7 +30,7 @@ class SequencePipeline:
                  match: bool = True, device: int = 0, params=(1000, 1.2, 8, 20, 7), fx: float = 500.0,
                  fy: float = 500.0, cx: float = 320.0, cy: float = 240.0, depth: float = 5.0, th: float = 15.0,
                  nnratio: float = 0.9, check_ori: bool = True, match_stream=None,
-                 nbuf: int = 2, matcher_mode: int | None = None):
+                 nbuf: int = 2, matcher_mode: int | None = None, match_after_stage: int = 0):
         import torch
 
         self.B, self.W, self.H = int(batch), int(width), int(height)
@@ -63,6 +63,11 @@ class SequencePipeline:
         self.ev_ex = [[torch.cuda.Event() for _ in range(self.S)] for _ in range(nbuf)]  # [buffer][lane]
         self.ev_m = [torch.cuda.Event() for _ in range(nbuf)]
         self.used = [False] * nbuf
+        # match_after_stage k (pipelined only): the matching of batch j-1 also waits until
+        # every lane's extraction of batch j has passed stage k (1 pyramid, 2 blur + FAST
+        # strength, 3 FAST cells, 4 octree), so it runs beside the later stages
+        self.stage_ev = [e.set_stage_event(match_after_stage) for e in self.exs] \
+            if (self.pipelined and match_after_stage) else None
         self.it = 0            # extractions issued
         self.pending = None    # buffer extracted but not yet matched (pipelined)
         self.last = None       # buffer holding the newest complete result
@@ -78,9 +83,13 @@ class SequencePipeline:
             self.ev_ex[b][c].record(self.streams[c])
         self.used[b] = True
 
-    def _match(self, b, Tcw):
+    def _match(self, b, Tcw, after_next=False):
         for c in range(self.S):
             self.ms.wait_event(self.ev_ex[b][c])
+        if after_next and self.stage_ev:
+            from .extractor import stream_wait_event
+            for ev in self.stage_ev:
+                stream_wait_event(self.ms.cuda_stream, ev)
         self.matcher.match_sequence_device(self.kps[b], self.desc[b], self.n[b], Tcw, self.mp[b], self.nm[b],
                                            self.sf, self.fx, self.fy, self.cx, self.cy, self.W, self.H,
                                            depth=self.depth, th=self.th, stream=self.ms.cuda_stream)
@@ -98,7 +107,7 @@ class SequencePipeline:
             return
         if self.pipelined:
             if self.pending is not None:
-                self._match(self.pending, Tcw)
+                self._match(self.pending, Tcw, after_next=True)
                 self.last = self.pending
             self.pending = b
         else:
