@@ -360,7 +360,8 @@ def main():
                           nbuf=int(os.environ.get("ORBX_PIPE_NBUF", "2")),
                           matcher_mode=None if "ORBX_MATCH_MODE" not in os.environ
                           else int(os.environ["ORBX_MATCH_MODE"]),
-                          match_after_stage=int(os.environ.get("ORBX_MATCH_AFTER", "0")))
+                          match_after_stage=int(os.environ.get("ORBX_MATCH_AFTER", "0")),
+                          lane_offset_stage=int(os.environ.get("ORBX_LANE_OFFSET", "2")))
     S = pl.S
     d_frames = torch.from_numpy(frames_np).to(dev)
     d_T = torch.from_numpy(T).to(dev)
