@@ -447,6 +447,7 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
     for (int i = tid; i < kTH * kTW / 4; i += 256) ((uint32_t*)s_m)[i] = 0u;
     __syncthreads();
     // ---- blur rows: 2 rows x 4 columns per task (dot4), stored as row-pair u16 dwords
+#ifndef ORBX_EXP_NO_BLURROW
     for (int i = tid; i < ((kTH + 6) / 2) * (kTW / 4); i += 256) {
         const int pr = i >> 4, c0 = 4 + 4 * (i & 15);
         const uint32_t* ra = (const uint32_t*)&s_in[2 * pr][c0];
@@ -457,9 +458,11 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
         *(uint4*)&s_rowp[pr][c0 - 4] = make_uint4(a[0] | (b[0] << 16), a[1] | (b[1] << 16), a[2] | (b[2] << 16),
                                                   a[3] | (b[3] << 16));
     }
+#endif
     // ---- FAST compass test on the detection area, compaction of the survivors.
     // A thread always owns columns 4j..4j+3 (j = tid & 15) of rows tid/16 + 16 i, so
     // its detection-area column mask is computed once.
+#ifndef ORBX_EXP_NO_COMPASS
     {
         const int j = tid & 15, c0 = 4 + 4 * j, x0 = X0 + 4 * j;
         unsigned colmask = 0;
@@ -533,9 +536,11 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
             }
         }
     }
+#endif
     __syncthreads();
     // ---- blur columns (4 outputs per task) -> global; exact strength of the survivors
     uint8_t* bout = blur + (size_t)f * fb + g.off;
+#ifndef ORBX_EXP_NO_BLURCOL
     for (int i = tid; i < kTH * (kTW / 4); i += 256) {
         const int r = i >> 4, c = 4 * (i & 15);
         const int y = Y0 + r, x = X0 + c;
@@ -569,12 +574,15 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
         else
             for (int k = 0; x + k < g.w; k++) o[k] = (uint8_t)(packed >> (8 * k));
     }
+#endif
     const int n = s_n;
+#ifndef ORBX_EXP_NO_STRENGTH
     for (int i = tid; i < n; i += 256) {
         const int rc = s_list[i];
         const int r = rc >> 8, c = rc & 255;
         s_m[r][c] = (uint8_t)fast_strength(&s_in[r + 3][c + 4], kSW);
     }
+#endif
     __syncthreads();
     uint8_t* mout = score + (size_t)f * fb + g.off;
     for (int i = tid; i < kTH * (kTW / 4); i += 256) {
