@@ -349,7 +349,8 @@ int orbx_compute_distinctive_descriptors_device(int nmp, const int32_t* d_off, c
  * the ordered commit); 3 = one wave per problem; 4 = lean: 1024 threads with only the
  * sorted grid and the claims in LDS (descriptors, query state and angles in global
  * memory), the form that leaves the most LDS to extraction running concurrently on
- * another stream.  Same results in every mode. */
+ * another stream; 5 = lean split: mode 4's workgroup sorts and scores, then a one-wave
+ * kernel with only the claims in LDS replays.  Same results in every mode. */
 int orbx_matcher_set_footprint(orbx_matcher* m, int mode);
 
 /* HIP-event timing of orbx_match_sequence_device and orbx_compute_stereo_matches_batch_device:

@@ -67,7 +67,8 @@ hipError_t launch_hamming_matrix(const uint8_t* a, int na, const uint8_t* b, int
 
 hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned long long* scratch,
                               const long long* d_scratch_off, int max_n, int max_nq, hipStream_t stream,
-                              bool small = false, bool tiny = false, bool lean = false);
+                              bool small = false, bool tiny = false, bool lean = false,
+                              unsigned char* split_grids = nullptr);
 
 // k_seq_grid + k_seq_score + k_seq_commit: the split form of launch_proj_search for the
 // batched sequence matcher (grids: nprob x seq_grid_bytes(cap) bytes of device memory)

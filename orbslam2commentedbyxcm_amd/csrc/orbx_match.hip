@@ -789,6 +789,27 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
     }
 }
 
+// Byte layout of one problem's grid in the global grid area.
+struct SeqGridLayout {
+    size_t skey, bstart, orun, sxy, sang, sfmp, sdesc, total;
+    __host__ __device__ SeqGridLayout(int cap, int noct) {
+        skey = 0;
+        bstart = align16((size_t)cap * 4);
+        orun = align16(bstart + (size_t)bucket_table_len(noct) * 2);
+        sxy = align16(orun + (size_t)cap * 2);
+        sang = align16(sxy + (size_t)cap * 8);
+        sfmp = align16(sang + (size_t)cap * 4);  // the claims (mvpMapPoints) before the search, sorted
+        sdesc = align16(sfmp + (size_t)cap * 4);
+        total = (sdesc + (size_t)cap * 32 + 255) & ~(size_t)255;
+    }
+};
+
+__device__ __forceinline__ SortedGrid seq_grid(unsigned char* base, const SeqGridLayout& g, int noct) {
+    return SortedGrid{(const unsigned*)(base + g.skey), (const uint16_t*)(base + g.bstart),
+                      (const uint16_t*)(base + g.orun), (const float2*)(base + g.sxy),
+                      (const uint4*)(base + g.sdesc), noct};
+}
+
 // One workgroup per problem (one SearchByProjection call).
 //  1. the frame's keypoints are sorted into grid order in LDS (with their descriptors
 //     when DLDS);
@@ -805,10 +826,13 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
 // claimed again), so the first unblocked entries of a query's initial list are exactly
 // its best / second best against the current state while the list has them.
 // QLDS: per-query state in LDS; otherwise in the problem's global scratch.
-template <bool QLDS, bool DLDS, int NT>
+// SPLIT: no replay here -- the sorted grid is published to `grids` (SeqGridLayout, no
+// sorted descriptors) and k_seq_commit replays with one wave and a small LDS footprint.
+template <bool QLDS, bool DLDS, int NT, bool SPLIT = false>
 __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restrict__ probs, ProjParams P,
                                                               unsigned long long* __restrict__ scratch,
-                                                              const long long* __restrict__ scratch_off) {
+                                                              const long long* __restrict__ scratch_off,
+                                                              unsigned char* __restrict__ grids, int gcap) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_hist[kHistoLength];
     const ProjProblem pb = probs[blockIdx.x];
@@ -893,6 +917,19 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     }
     __syncthreads();
     if (st && tid == 0) st[2] = wall_clock64();
+    if (SPLIT) {
+        const SeqGridLayout gl(gcap, P.noct);
+        unsigned char* gb = grids + (size_t)blockIdx.x * gl.total;
+        const int nb = bucket_table_len(P.noct);
+        for (int p = tid; p < n; p += NT) {
+            ((unsigned*)(gb + gl.skey))[p] = skey[p];
+            ((uint16_t*)(gb + gl.orun))[p] = orun[p];
+            ((float2*)(gb + gl.sxy))[p] = sxy[p];
+            ((float*)(gb + gl.sang))[p] = pb.keys[sk_idx(skey[p])].angle;
+        }
+        for (int t = tid; t < nb; t += NT) ((uint16_t*)(gb + gl.bstart))[t] = bstart[t];
+        return;
+    }
     // The replay is wave 0's alone: the other waves leave now, so their registers and
     // wave slots go back to whatever runs beside this kernel for the rest of its life.
     if (wave != 0) return;
@@ -915,27 +952,6 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
 //                 workgroups share one L2 with its grid): each query's 8-entry list;
 //   k_seq_commit  one wave per problem: the replay (proj_replay) with the claims in LDS.
 // Results are identical to k_proj_search's (same lists, same replay).
-
-// Byte layout of one problem's grid in the global grid area.
-struct SeqGridLayout {
-    size_t skey, bstart, orun, sxy, sang, sfmp, sdesc, total;
-    __host__ __device__ SeqGridLayout(int cap, int noct) {
-        skey = 0;
-        bstart = align16((size_t)cap * 4);
-        orun = align16(bstart + (size_t)bucket_table_len(noct) * 2);
-        sxy = align16(orun + (size_t)cap * 2);
-        sang = align16(sxy + (size_t)cap * 8);
-        sfmp = align16(sang + (size_t)cap * 4);  // the claims (mvpMapPoints) before the search, sorted
-        sdesc = align16(sfmp + (size_t)cap * 4);
-        total = (sdesc + (size_t)cap * 32 + 255) & ~(size_t)255;
-    }
-};
-
-__device__ __forceinline__ SortedGrid seq_grid(unsigned char* base, const SeqGridLayout& g, int noct) {
-    return SortedGrid{(const unsigned*)(base + g.skey), (const uint16_t*)(base + g.bstart),
-                      (const uint16_t*)(base + g.orun), (const float2*)(base + g.sxy),
-                      (const uint4*)(base + g.sdesc), noct};
-}
 
 constexpr int kSeqGridThreads = 256;
 
@@ -1013,12 +1029,13 @@ __global__ __launch_bounds__(kSeqScoreThreads) void k_seq_score(const ProjProble
 __global__ __launch_bounds__(64) void k_seq_commit(const ProjProblem* __restrict__ probs, ProjParams P,
                                                    unsigned char* __restrict__ grids, int cap,
                                                    unsigned long long* __restrict__ scratch,
-                                                   const long long* __restrict__ scratch_off) {
+                                                   const long long* __restrict__ scratch_off, int use_sdesc) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_hist[kHistoLength];
     const ProjProblem pb = probs[blockIdx.x];
     const SeqGridLayout gl(cap, P.noct);
-    const SortedGrid G = seq_grid(grids + (size_t)blockIdx.x * gl.total, gl, P.noct);
+    SortedGrid G = seq_grid(grids + (size_t)blockIdx.x * gl.total, gl, P.noct);
+    if (!use_sdesc) G.sdesc = nullptr;  // descriptors by keypoint index from the frame
     const float* gang = (const float*)(grids + (size_t)blockIdx.x * gl.total + gl.sang);
     const int lane = threadIdx.x, n = pb.n, nq = pb.nq;
     int* sfmp = (int*)smem;
@@ -1076,7 +1093,7 @@ hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjPar
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_seq_commit, dim3(nprob), dim3(64), lds_commit, stream, d_probs, P, grids, cap, scratch,
-                       d_scratch_off);
+                       d_scratch_off, 1);
     return hipGetLastError();
 }
 
@@ -1162,7 +1179,7 @@ hipError_t launch_seq_build(const SeqArgs& A, int npairs, ProjQuery* queries, Pr
 
 hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned long long* scratch,
                               const long long* d_scratch_off, int max_n, int max_nq, hipStream_t stream, bool small,
-                              bool tiny, bool lean) {
+                              bool tiny, bool lean, unsigned char* split_grids) {
     if (nprob <= 0) return hipSuccess;
     if (max_n >= 8192) return hipErrorInvalidValue;  // 13-bit keypoint positions
     if (P.noct < 1 || P.noct > 32) return hipErrorInvalidValue;
@@ -1180,6 +1197,10 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
             qlds = ProjLds(max_n, max_nq, false, true, P.noct).total <= limit;
         }
     }
+    if (split_grids) {  // lean scoring kernel + k_seq_commit
+        if (small) return hipErrorInvalidValue;
+        dlds = qlds = false;
+    }
     const size_t lds = ProjLds(max_n, max_nq, dlds, qlds, P.noct).total;
     if (lds > limit) return hipErrorInvalidValue;
     const void* fn;
@@ -1188,6 +1209,8 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
         fn = (const void*)k_proj_search<false, false, kProjThreadsTiny>;
     else if (small)
         fn = (const void*)k_proj_search<false, false, kProjThreadsSmall>;
+    else if (split_grids)
+        fn = (const void*)k_proj_search<false, false, kProjThreads, true>;
     else
         fn = qlds ? (dlds ? (const void*)k_proj_search<true, true, kProjThreads>
                           : (const void*)k_proj_search<true, false, kProjThreads>)
@@ -1197,8 +1220,19 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    void* args[] = {(void*)&d_probs, (void*)&P, (void*)&scratch, (void*)&d_scratch_off};
-    return hipLaunchKernel(fn, dim3(nprob), dim3(nt), args, lds, stream);
+    int gcap = max_n;
+    void* args[] = {(void*)&d_probs, (void*)&P, (void*)&scratch, (void*)&d_scratch_off, (void*)&split_grids,
+                    (void*)&gcap};
+    hipError_t e = hipLaunchKernel(fn, dim3(nprob), dim3(nt), args, lds, stream);
+    if (e != hipSuccess || !split_grids) return e;
+    const size_t lds_commit = (size_t)max_n * 12;
+    if (lds_commit > 64 * 1024) {
+        e = hipFuncSetAttribute((const void*)k_seq_commit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_commit);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_seq_commit, dim3(nprob), dim3(64), lds_commit, stream, d_probs, P, split_grids, max_n, scratch,
+                       d_scratch_off, 0);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ triangulation

@@ -204,7 +204,7 @@ struct orbx_matcher {
     bool timing = false;
     hipEvent_t ev[kRing][2] = {};
     long long ncalls = 0;
-    int footprint = 0;  // orbx_matcher_set_footprint: 0 full, 1 small, 2 split, 3 one wave, 4 lean
+    int footprint = 0;  // orbx_matcher_set_footprint: 0 full, 1 small, 2 split, 3 one wave, 4 lean, 5 lean split
     // device-only scratch of the batched device calls (no pinned mirror)
     char* dscr = nullptr;
     size_t dscr_cap = 0;
@@ -575,10 +575,11 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     hipStream_t s = stream ? (hipStream_t)stream : m->stream;
     const int npairs = batch - 1;
     const bool split = m->footprint == 2;
+    const bool grids = split || m->footprint == 5;  // a global grid area per problem
     const size_t np1 = (size_t)(npairs > 0 ? npairs : 1);
     const size_t need = pad(sizeof(ProjQuery) * np1 * cap) + pad(sizeof(ProjProblem) * np1) +
                         pad(sizeof(long long) * np1) + pad(sizeof(unsigned long long) * kProjScratchWords * np1 * cap) +
-                        (split ? pad(seq_grid_bytes(cap, nlevels) * np1) : 0);
+                        (grids ? pad(seq_grid_bytes(cap, nlevels) * np1) : 0);
     if (m->arena.cap < need) {
         HIP_TRY(hipStreamSynchronize(s));
         HIP_TRY(m->arena.reserve(need));
@@ -588,7 +589,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     auto* d_prob = m->arena.take<ProjProblem>(npairs > 0 ? npairs : 1);
     auto* d_off = m->arena.take<long long>(npairs > 0 ? npairs : 1);
     auto* d_scr = m->arena.take<unsigned long long>(kProjScratchWords * (size_t)(npairs > 0 ? npairs : 1) * cap);
-    auto* d_grids = split ? m->arena.take<unsigned char>(seq_grid_bytes(cap, nlevels) * np1) : nullptr;
+    auto* d_grids = grids ? m->arena.take<unsigned char>(seq_grid_bytes(cap, nlevels) * np1) : nullptr;
     if (npairs == 0) {  // otherwise k_seq_build initialises both outputs
         HIP_TRY(hipMemsetAsync(d_cur_mp, 0xff, sizeof(int32_t) * (size_t)batch * cap, s));
         HIP_TRY(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * (size_t)batch, s));
@@ -630,7 +631,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
     P.noct = nlevels;  // the extractor's keypoints have octave < nlevels
     // ORBX_MATCH_STAMPS=1: per-phase wall-clock breakdown of the search kernel to stderr
     // (diagnostics only; synchronises the stream).
-    const bool stamps = !split && getenv("ORBX_MATCH_STAMPS") != nullptr;  // k_proj_search phases only
+    const bool stamps = !grids && getenv("ORBX_MATCH_STAMPS") != nullptr;  // k_proj_search phases only
     unsigned long long* d_st = nullptr;
     if (stamps) {
         HIP_TRY(hipMalloc(&d_st, sizeof(unsigned long long) * kStampWords * npairs));
@@ -641,7 +642,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
         HIP_TRY(launch_seq_split(d_prob, npairs, P, d_grids, cap, d_scr, d_off, s));
     } else {
         HIP_TRY(launch_proj_search(d_prob, npairs, P, d_scr, d_off, cap, cap, s, m->footprint == 1,
-                                   m->footprint == 3, m->footprint == 4));
+                                   m->footprint == 3, m->footprint == 4, m->footprint == 5 ? d_grids : nullptr));
     }
     if (m->timing) {
         HIP_TRY(hipEventRecord(ev[1], s));
@@ -688,7 +689,7 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
 
 int orbx_matcher_set_footprint(orbx_matcher* m, int small) {
     if (!m) return fail(ORBX_ERR_ARG, "null matcher");
-    if (small < 0 || small > 4) return fail(ORBX_ERR_ARG, "footprint is 0, 1, 2, 3 or 4");
+    if (small < 0 || small > 5) return fail(ORBX_ERR_ARG, "footprint is 0 .. 5");
     m->footprint = small;
     return ORBX_OK;
 }

@@ -42,12 +42,15 @@ class SequencePipeline:
         self.fx, self.fy, self.cx, self.cy, self.depth, self.th = fx, fy, cx, cy, depth, th
         self.exs = [ORBextractor(*params, device=device) for _ in range(self.S)]
         self.matcher = ORBmatcher(nnratio, check_ori, device=device)
-        # matcher_mode: orbx_matcher_set_footprint.  Default 4 (lean: one 1024-thread
-        # workgroup per problem with only the sorted grid and the claims in LDS): beside the
-        # pipelined extraction it measured 190-192k frames/s against 185-190k for 0 (grid,
-        # descriptors and query state in LDS, ~118 KB per workgroup), 176-181k for 1 (256
-        # threads) and 167-169k for 2 (split launches); profiles/r02_e_*, r02_k_*
-        self.matcher.set_footprint(4 if matcher_mode is None else matcher_mode)
+        # matcher_mode: orbx_matcher_set_footprint.  Default 5 (lean split: one 1024-thread
+        # workgroup per problem sorts and scores with only the grid and the claims in LDS,
+        # then a one-wave kernel replays with only the claims in LDS).  Beside the pipelined
+        # extraction 4 (lean, replay in the scoring workgroup) measured 190-192k frames/s
+        # against 185-190k for 0 (grid, descriptors and query state in LDS, ~118 KB per
+        # workgroup), 176-181k for 1 (256 threads) and 167-169k for 2 (split launches);
+        # 5 measured 197.4k vs 196.3k for 4 at C1 and 66.3k vs 63.9k at configs[4]
+        # (profiles/r02_e_*, r02_k_*, r02_m_split_ab.log)
+        self.matcher.set_footprint(5 if matcher_mode is None else matcher_mode)
         self.sf = self.exs[0].GetScaleFactors()
         self.cap = self.exs[0].max_keypoints(self.W, self.H)
         self.bounds = [(self.B * c // self.S, self.B * (c + 1) // self.S) for c in range(self.S)]

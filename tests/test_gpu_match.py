@@ -308,8 +308,8 @@ def test_c5_search_for_triangulation(oracle, orbx_built, stereo):
     assert len(pr) > 100
 
 
-@pytest.mark.parametrize("small,prm", [(0, S.C1), (1, S.C1), (2, S.C1), (3, S.C1), (4, S.C1), (0, S.C5), (1, S.C5),
-                                       (2, S.C5), (3, S.C5), (4, S.C5)])
+@pytest.mark.parametrize("small,prm", [(0, S.C1), (1, S.C1), (2, S.C1), (3, S.C1), (4, S.C1), (5, S.C1), (0, S.C5),
+                                       (1, S.C5), (2, S.C5), (3, S.C5), (4, S.C5), (5, S.C5)])
 def test_match_sequence_device(oracle, orbx_built, small, prm):
     """Batched frame-to-frame matching on device-resident frames == per-pair oracle
     (both kernel footprints: 1024 threads, 256 threads; C1 and configs[4]'s 5000 x 12)."""
