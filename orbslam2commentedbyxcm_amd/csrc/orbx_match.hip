@@ -547,17 +547,17 @@ __device__ void grid_sort(const ProjProblem& pb, unsigned* skey, unsigned* cnt) 
 // LDS layout of k_proj_search (byte offsets), shared by the kernel and its launcher.
 struct ProjLds {
     size_t skey, colstart, bstart, orun, sxy, sfmp, owner, sang, sdesc, qk, qmp, qang, mlist, mbin, total;
-    __host__ __device__ ProjLds(int n, int nq, bool dlds, bool qlds, int noct) {
+    __host__ __device__ ProjLds(int n, int nq, bool dlds, bool qlds, int noct, bool replay = true) {
         skey = 0;
         colstart = align16((size_t)n * 4);
         bstart = align16(colstart + (size_t)(kGridCols + 1) * 2);
         orun = align16(bstart + (size_t)bucket_table_len(noct) * 2);
         sxy = align16(orun + (size_t)n * 2);
         sfmp = sxy + (size_t)n * 8;
-        owner = sfmp + (size_t)n * 4;
+        owner = sfmp + (size_t)n * 4;  // the replay's owner map (none without the replay)
         // keypoint angles in sorted order (the rotation bins), with the LDS-resident query
         // state only; the lean form reads them from the keypoints after the replay
-        sang = owner + (size_t)n * 4;
+        sang = owner + (replay ? (size_t)n * 4 : 0);
         size_t o = align16(sang + (qlds ? (size_t)n * 4 : 0));
         sdesc = o;
         if (dlds) o += (size_t)n * 32;
@@ -841,7 +841,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     const int n = pb.n, nq = pb.nq;
     unsigned long long* st = P.stamps ? P.stamps + kStampWords * blockIdx.x : nullptr;
     if (st && tid == 0) st[0] = wall_clock64();
-    const ProjLds L(n, nq, DLDS, QLDS, P.noct);
+    const ProjLds L(n, nq, DLDS, QLDS, P.noct, !SPLIT);
     unsigned* skey = (unsigned*)(smem + L.skey);
     uint16_t* colstart = (uint16_t*)(smem + L.colstart);
     uint16_t* bstart = (uint16_t*)(smem + L.bstart);
@@ -882,7 +882,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
         const orbx_keypoint& kp = pb.keys[i];
         sxy[p] = make_float2(kp.x, kp.y);
         sfmp[p] = pb.frame_mp[i];
-        owner[p] = 0x7fffffff;
+        if (!SPLIT) owner[p] = 0x7fffffff;
         if (QLDS) sang[p] = kp.angle;
     }
     if (DLDS) {
@@ -1038,13 +1038,13 @@ __global__ __launch_bounds__(64) void k_seq_commit(const ProjProblem* __restrict
     if (!use_sdesc) G.sdesc = nullptr;  // descriptors by keypoint index from the frame
     const float* gang = (const float*)(grids + (size_t)blockIdx.x * gl.total + gl.sang);
     const int lane = threadIdx.x, n = pb.n, nq = pb.nq;
+    // LDS: the claims and the owner map only (8 B per keypoint); the rotation bins read
+    // the grid's angles from global memory after the replay
     int* sfmp = (int*)smem;
     int* owner = sfmp + n;
-    float* sang = (float*)(owner + n);
     for (int p = lane; p < n; p += 64) {
         sfmp[p] = pb.frame_mp[sk_idx(G.skey[p])];
         owner[p] = 0x7fffffff;
-        sang[p] = gang[p];
     }
     if (lane < kHistoLength) s_hist[lane] = 0;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -1055,7 +1055,7 @@ __global__ __launch_bounds__(64) void k_seq_commit(const ProjProblem* __restrict
     const float* qang = (const float*)(qmp + nq);
     int* mlist = (int*)(qang + nq);
     int* mbin = mlist + nq;
-    proj_replay(pb, P, G, sfmp, owner, qk, qmp, qang, mlist, mbin, s_hist, [&](int tpos) { return sang[tpos]; },
+    proj_replay(pb, P, G, sfmp, owner, qk, qmp, qang, mlist, mbin, s_hist, [&](int tpos) { return gang[tpos]; },
                 nullptr);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -1071,7 +1071,7 @@ hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjPar
     if (P.noct < 1 || P.noct > 32) return hipErrorInvalidValue;
     const size_t scr = octave_runs_scratch(P.noct) > kGridSortScratch ? octave_runs_scratch(P.noct) : kGridSortScratch;
     const size_t lds_grid = align16(align16((size_t)cap * 4) + (size_t)(kGridCols + 1) * 2) + scr;
-    const size_t lds_commit = (size_t)cap * 12;
+    const size_t lds_commit = (size_t)cap * 8;
     if (lds_grid > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)k_seq_grid, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)lds_grid);
@@ -1201,7 +1201,7 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
         if (small) return hipErrorInvalidValue;
         dlds = qlds = false;
     }
-    const size_t lds = ProjLds(max_n, max_nq, dlds, qlds, P.noct).total;
+    const size_t lds = ProjLds(max_n, max_nq, dlds, qlds, P.noct, split_grids == nullptr).total;
     if (lds > limit) return hipErrorInvalidValue;
     const void* fn;
     const int nt = tiny ? kProjThreadsTiny : (small ? kProjThreadsSmall : kProjThreads);
@@ -1225,7 +1225,7 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
                     (void*)&gcap};
     hipError_t e = hipLaunchKernel(fn, dim3(nprob), dim3(nt), args, lds, stream);
     if (e != hipSuccess || !split_grids) return e;
-    const size_t lds_commit = (size_t)max_n * 12;
+    const size_t lds_commit = (size_t)max_n * 8;
     if (lds_commit > 64 * 1024) {
         e = hipFuncSetAttribute((const void*)k_seq_commit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_commit);
         if (e != hipSuccess) return e;
