@@ -9,6 +9,8 @@
 // `dist < bestDist` / `else if (dist < bestDist2)` updates exactly.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "orbx_block_sort.h"
 #include "orbx_kernels.h"
 
@@ -299,6 +301,15 @@ __device__ __forceinline__ unsigned row_min_u32(unsigned v) {
     return v;
 }
 
+// The same over the 8 lanes of each half DPP row (quad_perm [1,0,3,2], [2,3,0,1],
+// row_half_mirror).
+__device__ __forceinline__ unsigned half_row_min_u32(unsigned v) {
+    v = umin_(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));
+    v = umin_(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));
+    v = umin_(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false));
+    return v;
+}
+
 // A query and its MapPoint descriptor held in registers (loaded ahead of use so the
 // global latency overlaps the LDS work of the previous query).
 struct QueryReg {
@@ -344,7 +355,7 @@ __device__ __forceinline__ QueryReg bcast_query(const QueryReg& x, int src) {
 template <int K>
 __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const QueryReg& QR, bool valid,
                              const SortedGrid& G, const int* sfmp, unsigned out[kTopK]) {
-    static_assert(K == 16 || K == 64, "a DPP row or a wave");
+    static_assert(K == 8 || K == 16 || K == 64, "half a DPP row, a DPP row or a wave");
     const int r = threadIdx.x & (K - 1);
     const ProjQuery& Q = QR.q;
     unsigned k[4] = {kNoEntry, kNoEntry, kNoEntry, kNoEntry};
@@ -375,7 +386,9 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
             // lanes per column: the most (up to 4 in a row, 16 in a wave) that still cover
             // every column in one pass; shifts, no division
             int sh = 0;
-            if (K == 16) {
+            if (K == 8) {
+                sh = ncol <= 2 ? 2 : (ncol <= 4 ? 1 : 0);
+            } else if (K == 16) {
                 sh = ncol <= 4 ? 2 : (ncol <= 8 ? 1 : 0);
             } else {
                 sh = ncol <= 4 ? 4 : (ncol <= 8 ? 3 : (ncol <= 16 ? 2 : (ncol <= 32 ? 1 : 0)));
@@ -436,8 +449,8 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
         }
     }
     // Group top-kTopK: keys are unique (distinct positions), so one lane pops each minimum.
-    const int rsh = K == 16 ? (threadIdx.x & 48) : 0;  // first lane of this group
-    const unsigned long long gmask = K == 16 ? 0xffffull : ~0ull;
+    const int rsh = K == 64 ? 0 : (threadIdx.x & (63 & ~(K - 1)));  // first lane of this group
+    const unsigned long long gmask = K == 64 ? ~0ull : ((1ull << K) - 1);
     bool over = seen > 4;
     bool trunc = false;
     unsigned m[kTopK];
@@ -446,7 +459,7 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
         // a lane whose listed candidates are used up but that saw more makes the rest unknown
         const unsigned long long dry = __ballot(over && k[0] == kNoEntry);
         trunc = trunc || ((dry >> rsh) & gmask) != 0;
-        m[j] = row_min_u32(k[0]);
+        m[j] = K == 8 ? half_row_min_u32(k[0]) : row_min_u32(k[0]);
         if (K == 64) {  // the four rows' minima by v_readlane: wave-uniform, no LDS round trip
             m[j] = umin_(umin_((unsigned)__builtin_amdgcn_readlane((int)m[j], 0),
                                (unsigned)__builtin_amdgcn_readlane((int)m[j], 16)),
@@ -468,9 +481,10 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
                                       (m[j] & 0x1fffu);
 }
 
+constexpr int kScoreRow = 16;  // lanes per query of k_seq_score
 __device__ __forceinline__ void score_rowk(const ProjProblem& pb, const ProjParams& P, const QueryReg& QR, bool valid,
                                            const SortedGrid& G, const int* sfmp, unsigned out[kTopK]) {
-    score_groupk<16>(pb, P, QR, valid, G, sfmp, out);
+    score_groupk<kScoreRow>(pb, P, QR, valid, G, sfmp, out);
 }
 
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -894,19 +908,24 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     __syncthreads();
     if (st && tid == 0) st[1] = wall_clock64();
     const SortedGrid G{skey, bstart, orun, sxy, sdesc, P.noct};
-    {
-        constexpr int kStep = kWaves * 4;
-        int qb = wave * 4;
+    // KR lanes per query: 8 for pyramids of up to 8 levels (windows of a few cells: twice
+    // the queries per pass; C1 scoring 88 -> 68 us), 16 above (the top levels' windows
+    // span tens of columns; 8 lanes there truncate more lists and re-score more)
+    auto pass = [&](auto kr) {
+        constexpr int KR = decltype(kr)::value;
+        constexpr int kQw = 64 / KR;  // queries per wave and pass
+        constexpr int kStep = kWaves * kQw;
+        int qb = wave * kQw;
         QueryReg cur;
-        if (qb < nq) cur = load_query(pb, min(qb + (lane >> 4), nq - 1));
+        if (qb < nq) cur = load_query(pb, min(qb + lane / KR, nq - 1));
         for (; qb < nq; qb += kStep) {
-            const int q = qb + (lane >> 4);
+            const int q = qb + lane / KR;
             QueryReg nxt;
             if (qb + kStep < nq) nxt = load_query(pb, min(q + kStep, nq - 1));  // prefetch
             const int mp = q < nq ? cur.q.mp : -1;
             unsigned e[kTopK];
-            score_rowk(pb, P, cur, mp >= 0, G, sfmp, e);
-            if ((lane & 15) == 0 && q < nq) {
+            score_groupk<KR>(pb, P, cur, mp >= 0, G, sfmp, e);
+            if ((lane & (KR - 1)) == 0 && q < nq) {
                 qk[2 * q] = make_uint4(e[0], e[1], e[2], e[3]);
                 qk[2 * q + 1] = make_uint4(e[4], e[5], e[6], e[7]);
                 qmp[q] = mp;
@@ -914,7 +933,9 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
             }
             cur = nxt;
         }
-    }
+    };
+    if (P.noct <= 8) pass(std::integral_constant<int, 8>{});
+    else pass(std::integral_constant<int, 16>{});
     __syncthreads();
     if (st && tid == 0) st[2] = wall_clock64();
     if (SPLIT) {
@@ -992,7 +1013,7 @@ __global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem*
 }
 
 constexpr int kSeqScoreThreads = 256;  // 16 queries (4 per wave, one 16-lane row each)
-constexpr int kSeqScoreQ = kSeqScoreThreads / 16;
+constexpr int kSeqScoreQ = kSeqScoreThreads / kScoreRow;
 
 __global__ __launch_bounds__(kSeqScoreThreads) void k_seq_score(const ProjProblem* __restrict__ probs, int nprob,
                                                                 int qblocks, ProjParams P,
@@ -1007,14 +1028,14 @@ __global__ __launch_bounds__(kSeqScoreThreads) void k_seq_score(const ProjProble
     const ProjProblem pb = probs[p];
     const SeqGridLayout gl(cap, P.noct);
     const SortedGrid G = seq_grid(grids + (size_t)p * gl.total, gl, P.noct);
-    const int q = blk * kSeqScoreQ + (threadIdx.x >> 4);
+    const int q = blk * kSeqScoreQ + (int)threadIdx.x / kScoreRow;
     if (blk * kSeqScoreQ >= pb.nq) return;  // whole workgroup past the queries
     const QueryReg cur = load_query(pb, min(q, pb.nq - 1));
     const int mp = q < pb.nq ? cur.q.mp : -1;
     unsigned e[kTopK];
     const int* sfmp0 = (const int*)(grids + (size_t)p * gl.total + gl.sfmp);  // the claims before the search
     score_rowk(pb, P, cur, mp >= 0, G, sfmp0, e);
-    if ((threadIdx.x & 15) == 0 && q < pb.nq) {
+    if ((threadIdx.x & (kScoreRow - 1)) == 0 && q < pb.nq) {
         unsigned long long* g = scratch + scratch_off[p];
         uint4* qk = (uint4*)g;
         int* qmp = (int*)(g + 4 * (size_t)pb.nq);
