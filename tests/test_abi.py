@@ -78,3 +78,15 @@ def test_product_never_imports_oracle():
     for f in list(pkg.rglob("*.py")) + list(pkg.rglob("*.cpp")) + list(pkg.rglob("*.hip")) + list(pkg.rglob("*.h")):
         text = f.read_text(errors="replace")
         assert "oracle" not in re.sub(r"#.*|//.*", "", text).replace("parity oracle", ""), f
+
+
+def test_stage_event_arguments(orbx_built):
+    """orbx_extractor_set_stage_event / orbx_stream_wait_event reject bad arguments
+    without a GPU (null extractor, stage outside 0..4, null event)."""
+    import ctypes as C
+
+    from orbslam2commentedbyxcm_amd import _lib as L
+
+    ev = C.c_void_p()
+    assert L.lib().orbx_extractor_set_stage_event(None, 2, C.byref(ev)) == L.ORBX_ERR_ARG
+    assert L.lib().orbx_stream_wait_event(None, None) == L.ORBX_ERR_ARG

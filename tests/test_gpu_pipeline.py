@@ -18,12 +18,13 @@ from orbslam2commentedbyxcm_amd.pipeline import SequencePipeline, sequence_poses
 pytestmark = pytest.mark.gpu
 
 
-def _run(B, lanes, pipelined, steps, seed=1000, matcher_mode=None):
+def _run(B, lanes, pipelined, steps, seed=1000, matcher_mode=None, lane_offset=2, match_after=0):
     import torch
 
     frames, off = synth.sequence(seed, B)
     T = sequence_poses(off)
-    pl = SequencePipeline(B, 640, 480, lanes=lanes, pipelined=pipelined, matcher_mode=matcher_mode)
+    pl = SequencePipeline(B, 640, 480, lanes=lanes, pipelined=pipelined, matcher_mode=matcher_mode,
+                          lane_offset_stage=lane_offset, match_after_stage=match_after)
     d_frames = torch.from_numpy(frames).to(pl.dev)
     d_T = torch.from_numpy(T).to(pl.dev)
     torch.cuda.synchronize()
@@ -32,12 +33,16 @@ def _run(B, lanes, pipelined, steps, seed=1000, matcher_mode=None):
     return frames, T, pl
 
 
-@pytest.mark.parametrize("B,lanes,pipelined,steps,mode", [(256, 2, True, 2, None), (16, 1, False, 1, None),
-                                                          (8, 2, True, 3, None), (12, 2, False, 2, None),
-                                                          (256, 2, False, 1, None), (256, 2, True, 2, 2),
-                                                          (13, 2, True, 3, 2)])
-def test_sequence_pipeline_matches_oracle(oracle, orbx_built, B, lanes, pipelined, steps, mode):
-    frames, T, pl = _run(B, lanes, pipelined, steps, matcher_mode=mode)
+@pytest.mark.parametrize("B,lanes,pipelined,steps,mode,offset,after",
+                         [(256, 2, True, 2, None, 2, 0), (16, 1, False, 1, None, 2, 0), (8, 2, True, 3, None, 2, 0),
+                          (12, 2, False, 2, None, 2, 0), (256, 2, False, 1, None, 2, 0), (256, 2, True, 2, 2, 2, 0),
+                          (13, 2, True, 3, 2, 2, 0), (256, 2, True, 2, 4, 0, 0), (24, 3, True, 3, 0, 1, 0),
+                          (16, 2, True, 3, None, 0, 2)])
+def test_sequence_pipeline_matches_oracle(oracle, orbx_built, B, lanes, pipelined, steps, mode, offset, after):
+    """Every frame and pair of the newest batch == the oracle, over matcher footprints
+    (None = the default lean split), lanes in step (offset 0) or out of phase, and the
+    matcher started after a later extraction stage of the next batch (after > 0)."""
+    frames, T, pl = _run(B, lanes, pipelined, steps, matcher_mode=mode, lane_offset=offset, match_after=after)
     res = pl.host_results()
     assert not pl.status().any()
     r = checks.check_sequence(frames, T, res, pl.sf)
