@@ -279,7 +279,14 @@ __device__ void build_octave_runs(const unsigned* skey, const uint16_t* colstart
 constexpr int kProjThreads = 1024;      // default workgroup size of k_proj_search
 constexpr int kProjThreadsSmall = 256;  // small-footprint variant (overlapped with other work)
 constexpr int kProjThreadsTiny = 64;    // one wave per problem (a background stream's footprint)
-constexpr int kTopK = 8;                   // candidate-list length per query
+#ifndef ORBX_TOPK
+#define ORBX_TOPK 8
+#endif
+constexpr int kTopK = ORBX_TOPK;           // candidate-list length per query
+static_assert(kTopK % 4 == 0, "lists are stored as uint4s");
+constexpr int kListVec = kTopK / 4;        // uint4s per stored list
+constexpr int kListWords = kTopK / 2;      // u64 words per stored list
+static_assert(kProjScratchWords >= kListWords + 2, "per-query global scratch holds the list, mp + angle, match + bin");
 constexpr unsigned kNoEntry = 0xffffffffu;  // no further candidate
 constexpr unsigned kTrunc = 0xfffffffeu;    // further candidates exist but are not listed
 
@@ -616,9 +623,11 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
         if (q < nq) mine = load_query(pb, q);
         if (q < nq) {
             mp = qmp[q];
-            const uint4 v = qk[2 * q], w = qk[2 * q + 1];
-            e[0] = v.x; e[1] = v.y; e[2] = v.z; e[3] = v.w;
-            e[4] = w.x; e[5] = w.y; e[6] = w.z; e[7] = w.w;
+#pragma unroll
+            for (int v = 0; v < kListVec; v++) {
+                const uint4 x4 = qk[kListVec * q + v];
+                e[4 * v] = x4.x; e[4 * v + 1] = x4.y; e[4 * v + 2] = x4.z; e[4 * v + 3] = x4.w;
+            }
         }
         int start = 0;
         // Per lane: c1 / c2 = the first two unclaimed entries of its list, exhausted = a
@@ -877,7 +886,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     } else {
         unsigned long long* g = scratch + scratch_off[blockIdx.x];
         qk = (uint4*)g;
-        qmp = (int*)(g + 4 * (size_t)nq);
+        qmp = (int*)(g + kListWords * (size_t)nq);
         qang = (float*)(qmp + nq);
         mlist = (int*)(qang + nq);
         mbin = mlist + nq;
@@ -926,8 +935,9 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
             unsigned e[kTopK];
             score_groupk<KR>(pb, P, cur, mp >= 0, G, sfmp, e);
             if ((lane & (KR - 1)) == 0 && q < nq) {
-                qk[2 * q] = make_uint4(e[0], e[1], e[2], e[3]);
-                qk[2 * q + 1] = make_uint4(e[4], e[5], e[6], e[7]);
+#pragma unroll
+                for (int v = 0; v < kListVec; v++)
+                    qk[kListVec * q + v] = make_uint4(e[4 * v], e[4 * v + 1], e[4 * v + 2], e[4 * v + 3]);
                 qmp[q] = mp;
                 qang[q] = cur.q.angle;
             }
@@ -1038,10 +1048,11 @@ __global__ __launch_bounds__(kSeqScoreThreads) void k_seq_score(const ProjProble
     if ((threadIdx.x & (kScoreRow - 1)) == 0 && q < pb.nq) {
         unsigned long long* g = scratch + scratch_off[p];
         uint4* qk = (uint4*)g;
-        int* qmp = (int*)(g + 4 * (size_t)pb.nq);
+        int* qmp = (int*)(g + kListWords * (size_t)pb.nq);
         float* qang = (float*)(qmp + pb.nq);
-        qk[2 * q] = make_uint4(e[0], e[1], e[2], e[3]);
-        qk[2 * q + 1] = make_uint4(e[4], e[5], e[6], e[7]);
+#pragma unroll
+        for (int v = 0; v < kListVec; v++)
+            qk[kListVec * q + v] = make_uint4(e[4 * v], e[4 * v + 1], e[4 * v + 2], e[4 * v + 3]);
         qmp[q] = mp;
         qang[q] = cur.q.angle;
     }
@@ -1072,7 +1083,7 @@ __global__ __launch_bounds__(64) void k_seq_commit(const ProjProblem* __restrict
     __builtin_amdgcn_wave_barrier();
     unsigned long long* g = scratch + scratch_off[blockIdx.x];
     const uint4* qk = (const uint4*)g;
-    const int* qmp = (const int*)(g + 4 * (size_t)nq);
+    const int* qmp = (const int*)(g + kListWords * (size_t)nq);
     const float* qang = (const float*)(qmp + nq);
     int* mlist = (int*)(qang + nq);
     int* mbin = mlist + nq;
