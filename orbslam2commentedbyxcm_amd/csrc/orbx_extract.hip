@@ -538,43 +538,7 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
     }
 #endif
     __syncthreads();
-    // ---- blur columns (4 outputs per task) -> global; exact strength of the survivors
-    uint8_t* bout = blur + (size_t)f * fb + g.off;
-#ifndef ORBX_EXP_NO_BLURCOL
-    for (int i = tid; i < kTH * (kTW / 4); i += 256) {
-        const int r = i >> 4, c = 4 * (i & 15);
-        const int y = Y0 + r, x = X0 + c;
-        if (y >= g.h || x >= g.w) continue;
-        // staged rows r..r+6, as 4 row pairs starting at r (even r) or r-1 (odd r),
-        // one v_dot2_u32_u16 per pair and column
-        unsigned s[4] = {1u << 15, 1u << 15, 1u << 15, 1u << 15};  // + the rounding half
-        const int p0 = r >> 1;
-        const bool odd = r & 1;
-        const ushort2_t w0 = odd ? ushort2_t{0, 18} : ushort2_t{18, 34};
-        const ushort2_t w1 = odd ? ushort2_t{34, 49} : ushort2_t{49, 55};
-        const ushort2_t w2 = odd ? ushort2_t{55, 49} : ushort2_t{49, 34};
-        const ushort2_t w3 = odd ? ushort2_t{34, 18} : ushort2_t{18, 0};
-        const ushort2_t wk[4] = {w0, w1, w2, w3};
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint4 q = *(const uint4*)&s_rowp[p0 + k][c];
-            s[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, q.x), wk[k], s[0], false);
-            s[1] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, q.y), wk[k], s[1], false);
-            s[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, q.z), wk[k], s[2], false);
-            s[3] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, q.w), wk[k], s[3], false);
-        }
-        uint32_t packed = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const unsigned v = s[k] >> 16;
-            packed |= (v > 255 ? 255u : v) << (8 * k);
-        }
-        uint8_t* o = bout + (size_t)y * g.pitch + x;
-        if (x + 4 <= g.w) *(uint32_t*)o = packed;
-        else
-            for (int k = 0; x + k < g.w; k++) o[k] = (uint8_t)(packed >> (8 * k));
-    }
-#endif
+    // ---- exact strength of the survivors
     const int n = s_n;
 #ifndef ORBX_EXP_NO_STRENGTH
     for (int i = tid; i < n; i += 256) {
@@ -584,16 +548,60 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
     }
 #endif
     __syncthreads();
+    // ---- blur columns and the strength map -> global, two rows x 4 columns per task:
+    // rows 2p and 2p+1 read the same four row-pair dwords (staged rows 2p..2p+7), one
+    // v_dot2_u32_u16 per pair, column and row, then (sum + 2^15) >> 16
+    uint8_t* bout = blur + (size_t)f * fb + g.off;
     uint8_t* mout = score + (size_t)f * fb + g.off;
-    for (int i = tid; i < kTH * (kTW / 4); i += 256) {
-        const int r = i >> 4, c = 4 * (i & 15);
-        const int y = Y0 + r, x = X0 + c;
-        if (y >= g.h || x >= g.w) continue;
-        const uint32_t packed = *(const uint32_t*)&s_m[r][c];
-        uint8_t* o = mout + (size_t)y * g.pitch + x;
-        if (x + 4 <= g.w) *(uint32_t*)o = packed;
-        else
-            for (int k = 0; x + k < g.w; k++) o[k] = (uint8_t)(packed >> (8 * k));
+    for (int i = tid; i < (kTH / 2) * (kTW / 4); i += 256) {
+        const int rp = i >> 4, c = 4 * (i & 15);
+        const int r = 2 * rp, y = Y0 + r, x = X0 + c;
+        if (y >= g.h || x >= g.w) continue;  // kTH is even: row y + 1 is then out too
+        const bool two = y + 1 < g.h;
+        uint4 q[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) q[k] = *(const uint4*)&s_rowp[rp + k][c];
+        const ushort2_t we[4] = {ushort2_t{18, 34}, ushort2_t{49, 55}, ushort2_t{49, 34}, ushort2_t{18, 0}};
+        const ushort2_t wo[4] = {ushort2_t{0, 18}, ushort2_t{34, 49}, ushort2_t{55, 49}, ushort2_t{34, 18}};
+        unsigned se[4] = {1u << 15, 1u << 15, 1u << 15, 1u << 15};  // + the rounding half
+        unsigned so[4] = {1u << 15, 1u << 15, 1u << 15, 1u << 15};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            se[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, q[k].x), we[k], se[0], false);
+            se[1] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, q[k].y), we[k], se[1], false);
+            se[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, q[k].z), we[k], se[2], false);
+            se[3] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, q[k].w), we[k], se[3], false);
+            so[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, q[k].x), wo[k], so[0], false);
+            so[1] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, q[k].y), wo[k], so[1], false);
+            so[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, q[k].z), wo[k], so[2], false);
+            so[3] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, q[k].w), wo[k], so[3], false);
+        }
+        uint32_t pe = 0, po = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const unsigned ve = se[k] >> 16, vo = so[k] >> 16;
+            pe |= (ve > 255 ? 255u : ve) << (8 * k);
+            po |= (vo > 255 ? 255u : vo) << (8 * k);
+        }
+        const uint32_t me = *(const uint32_t*)&s_m[r][c], mo = *(const uint32_t*)&s_m[r + 1][c];
+        const size_t off = (size_t)y * g.pitch + x;
+        if (x + 4 <= g.w) {
+            *(uint32_t*)(bout + off) = pe;
+            *(uint32_t*)(mout + off) = me;
+            if (two) {
+                *(uint32_t*)(bout + off + g.pitch) = po;
+                *(uint32_t*)(mout + off + g.pitch) = mo;
+            }
+        } else {
+            for (int k = 0; x + k < g.w; k++) {
+                bout[off + k] = (uint8_t)(pe >> (8 * k));
+                mout[off + k] = (uint8_t)(me >> (8 * k));
+                if (two) {
+                    bout[off + g.pitch + k] = (uint8_t)(po >> (8 * k));
+                    mout[off + g.pitch + k] = (uint8_t)(mo >> (8 * k));
+                }
+            }
+        }
     }
 }
 
