@@ -232,24 +232,13 @@ def cpu_baseline(frames_np, T, sf, seconds: float, threads: int, W=640, H=480, p
                       f"scalar port built {flags} (no OpenCV / IPP SIMD)"}
 
 def _match_stream(dev):
-    """The matcher's stream.  ORBX_MATCH_CUSTRIDE=k (tuning knob) restricts it to every
-    k-th compute unit (hipExtStreamCreateWithCUMask), so the concurrent extraction keeps
-    the other CUs' LDS and wave slots to itself."""
+    """ORBX_MATCH_PRIO=p (tuning knob): the matcher on a torch stream of priority p over
+    every CU instead of the pipeline's own stream (ORBX_MATCH_CUSTRIDE=k: on CUs 0, k,
+    2k, ... only; default 1 = every CU)."""
     import torch
-    k = int(os.environ.get("ORBX_MATCH_CUSTRIDE", "0"))
-    if k <= 1:  # ORBX_MATCH_PRIO=-1: high-priority matcher stream (tuning knob)
-        return torch.cuda.Stream(device=dev, priority=int(os.environ.get("ORBX_MATCH_PRIO", "0")))
-    import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
-    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    words = (ctypes.c_uint32 * ((ncu + 31) // 32))()
-    for i in range(0, ncu, k):
-        words[i // 32] |= 1 << (i % 32)
-    h = ctypes.c_void_p()
-    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(words)), words)
-    if rc != 0:
-        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {rc}")
-    return torch.cuda.ExternalStream(h.value, device=dev)
+    if "ORBX_MATCH_PRIO" not in os.environ:
+        return None
+    return torch.cuda.Stream(device=dev, priority=int(os.environ["ORBX_MATCH_PRIO"]))
 
 
 def launch_ranks(n: int, argv) -> int:
@@ -361,7 +350,8 @@ def main():
                           matcher_mode=None if "ORBX_MATCH_MODE" not in os.environ
                           else int(os.environ["ORBX_MATCH_MODE"]),
                           match_after_stage=int(os.environ.get("ORBX_MATCH_AFTER", "0")),
-                          lane_offset_stage=int(os.environ.get("ORBX_LANE_OFFSET", "2")))
+                          lane_offset_stage=int(os.environ.get("ORBX_LANE_OFFSET", "2")),
+                          match_cu_stride=int(os.environ.get("ORBX_MATCH_CUSTRIDE", "1")))
     S = pl.S
     d_frames = torch.from_numpy(frames_np).to(dev)
     d_T = torch.from_numpy(T).to(dev)
@@ -461,7 +451,8 @@ def main():
                                    "against its predecessor" + ("" if match else " (match disabled)"),
                        "frames_per_gpu_step": B, "global_batch": B * world, "width": W, "height": H,
                        "parallelism": f"frame-sharded x{world}", "lanes_per_gpu": S,
-                       "pipelined_match": pipeline},
+                       "pipelined_match": pipeline,
+                       "match_cu_stride": None if pl._own_ms is None else int(os.environ.get("ORBX_MATCH_CUSTRIDE", "1"))},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_unit": "bytes per launch (PMC FETCH_SIZEx2 + WRITE_SIZE)",

@@ -390,6 +390,30 @@ int orbx_stream_wait_event(void* stream, void* event) {
     return ORBX_OK;
 }
 
+int orbx_stream_create_cu_strided(int device, int cu_stride, void** stream) {
+    if (!stream || cu_stride < 1) return fail(ORBX_ERR_ARG, "bad argument");
+    *stream = nullptr;
+    HIP_TRY(hipSetDevice(device));
+    int ncu = 0;
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+    hipStream_t s = nullptr;
+    if (cu_stride == 1) {
+        HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    } else {
+        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; i += cu_stride) mask[(size_t)i / 32] |= 1u << (i % 32);
+        HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+    }
+    *stream = (void*)s;
+    return ORBX_OK;
+}
+
+int orbx_stream_destroy(void* stream) {
+    if (!stream) return fail(ORBX_ERR_ARG, "null stream");
+    HIP_TRY(hipStreamDestroy((hipStream_t)stream));
+    return ORBX_OK;
+}
+
 int orbx_extractor_status(orbx_extractor* ex, int batch, int* flags, int* any) {
     if (!ex || batch < 0) return fail(ORBX_ERR_ARG, "bad argument");
     if (!ex->have_pyramid) return fail(ORBX_ERR_STATE, "no extraction yet");

@@ -330,7 +330,16 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 
 constexpr int kTW = kLtTW, kTH = kLtTH;  // level tile (outputs) of k_level_tiles
 static_assert(kTW == 64 && kTH % 16 == 0, "k_level_tiles maps 16 column quads x kTH rows");
-constexpr int kSW = kTW + 8;       // staged row: image columns X0-4 .. X0+67
+#ifndef ORBX_LT_LOAD
+#define ORBX_LT_LOAD 16  // k_level_tiles staging load width in bytes (4 or 16)
+#endif
+constexpr int kLU = ORBX_LT_LOAD;  // staged row: image columns X0-kSX .. X0+63+kSX
+constexpr int kSX = kLU == 16 ? 16 : 4;
+// row pitch: 16-byte loads stage 96 columns + 8 pad bytes (26 dwords: rows r and r + 16
+// share a bank of ds_read_b32's 32; 24 dwords would put rows r and r + 4 together)
+constexpr int kSW = kLU == 16 ? kTW + 2 * kSX + 8 : kTW + 2 * kSX;
+static_assert(kLU == 4 || kLU == 16, "staging load width");
+typedef std::conditional_t<kLU == 16, uint4, uint32_t> lt_load_t;
 
 typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
 
@@ -386,9 +395,16 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
                                                      const LevelGeom* __restrict__ lv, int L, int tiles_pf,
                                                      int nframes, int tq) {
     __shared__ __align__(16) uint8_t s_in[kTH + 6][kSW];
-    __shared__ __align__(16) uint32_t s_rowp[(kTH + 6) / 2][kTW];  // (row 2p, row 2p+1) u16 pairs
     __shared__ __align__(16) uint8_t s_m[kTH][kTW];
-    __shared__ uint16_t s_list[kTH * kTW + 128];  // + per-lane dump slots for branch-free appends
+    // the survivor list (+ per-lane dump slots for branch-free appends) and, after the
+    // strength pass, the blur row sums as (row 2p, row 2p+1) u16 pairs share one buffer
+    constexpr int kListB = (kTH * kTW + 128) * 2, kRowpB = (kTH + 6) / 2 * kTW * 4;
+#ifndef ORBX_LT_LDS_PAD
+#define ORBX_LT_LDS_PAD 0
+#endif
+    __shared__ __align__(16) uint8_t s_u[(kListB > kRowpB ? kListB : kRowpB) + ORBX_LT_LDS_PAD];
+    uint16_t* const s_list = (uint16_t*)s_u;
+    uint32_t (*const s_rowp)[kTW] = (uint32_t (*)[kTW])s_u;
     __shared__ int s_n;
     int f, tile;
     xcd_frame_block(tiles_pf, nframes, f, tile);
@@ -400,71 +416,49 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
     const int ty = t / g.tiles_x;
     const int X0 = (t - ty * g.tiles_x) * kTW, Y0 = ty * kTH;
     const uint8_t* img = pyr + (size_t)f * fb + g.off;
-    // ---- stage rows Y0-3 .. Y0+34, columns X0-4 .. X0+67 (REFLECT_101 at the ROI edges)
-    // (all loads of a thread are issued before the LDS stores: no per-load round trip)
-    if (X0 >= 4 && X0 + kTW + 4 <= g.w) {
-        constexpr int kN = (kTH + 6) * (kSW / 4), kPer = (kN + 255) / 256;
-        uint32_t v[kPer];
+    // ---- stage rows Y0-3 .. Y0+kTH+2, columns X0-16 .. X0+79 (REFLECT_101 at the ROI
+    // edges) as 16-byte loads (pitch and level offsets are multiples of 64); all loads
+    // of a thread are issued before the LDS stores: no per-load round trip
+    {
+        constexpr int kRow = (kTW + 2 * kSX) / kLU, kN = (kTH + 6) * kRow, kPer = (kN + 255) / 256;
+        const bool edge = !(X0 >= kSX && X0 + kTW + kSX <= g.w);
+        lt_load_t v[kPer];
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             const int i = min(tid + 256 * k, kN - 1);
-            const int r = i / (kSW / 4), c4 = i - r * (kSW / 4);
-            v[k] = *(const uint32_t*)(img + (size_t)reflect101(Y0 + r - 3, g.h) * g.pitch + X0 - 4 + 4 * c4);
+            const int r = i / kRow, cu = i - r * kRow;
+            // edge tile: the start column clamped into the row (a load holding an in-range
+            // column never clamps: X0 and pitch are multiples of 64)
+            const int col = edge ? min(max(X0 - kSX + kLU * cu, 0), g.pitch - kLU) : X0 - kSX + kLU * cu;
+            v[k] = *(const lt_load_t*)(img + (size_t)reflect101(Y0 + r - 3, g.h) * g.pitch + col);
         }
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             const int i = tid + 256 * k;
-            if (i < kN) ((uint32_t*)s_in)[i] = v[k];
+            const int r = i / kRow, cu = i - r * kRow;
+            if (i < kN) *(lt_load_t*)&s_in[r][kLU * cu] = v[k];
         }
-    } else {
-        // edge tile: the same dword loads with the start column clamped into the row
-        // (an in-range column's dword never clamps: pitch >= w rounded up to 4), then
-        // the only reflected columns anything reads, -3..-1 and w..w+2 (the blur's
-        // reach; FAST stays inside [16, w - 16)), are rewritten from the staged row.
-        constexpr int kN = (kTH + 6) * (kSW / 4), kPer = (kN + 255) / 256;
-        uint32_t v[kPer];
-#pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            const int i = min(tid + 256 * k, kN - 1);
-            const int r = i / (kSW / 4), c4 = i - r * (kSW / 4);
-            const int col = min(max(X0 - 4 + 4 * c4, 0), g.pitch - 4);
-            v[k] = *(const uint32_t*)(img + (size_t)reflect101(Y0 + r - 3, g.h) * g.pitch + col);
-        }
-#pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            const int i = tid + 256 * k;
-            if (i < kN) ((uint32_t*)s_in)[i] = v[k];
-        }
-        __syncthreads();
-        for (int i = tid; i < (kTH + 6) * 6; i += 256) {
-            const int r = i / 6, k = i - 6 * r;
-            const int col = k < 3 ? -1 - k : g.w + k - 3;  // REFLECT_101 source: -col or 2w - 2 - col
-            const int sc = col - X0 + 4, ss = (k < 3 ? -col : 2 * g.w - 2 - col) - X0 + 4;
-            if (sc >= 0 && sc < kSW) s_in[r][sc] = s_in[r][ss];
+        if (edge) {
+            // the only reflected columns anything reads, -3..-1 and w..w+2 (the blur's
+            // reach; FAST stays inside [16, w - 16)), are rewritten from the staged row
+            __syncthreads();
+            for (int i = tid; i < (kTH + 6) * 6; i += 256) {
+                const int r = i / 6, k = i - 6 * r;
+                const int col = k < 3 ? -1 - k : g.w + k - 3;  // REFLECT_101 source: -col or 2w - 2 - col
+                const int sc = col - X0 + kSX, ss = (k < 3 ? -col : 2 * g.w - 2 - col) - X0 + kSX;
+                if (sc >= 0 && sc < kSW) s_in[r][sc] = s_in[r][ss];
+            }
         }
     }
     if (tid == 0) s_n = 0;
     for (int i = tid; i < kTH * kTW / 4; i += 256) ((uint32_t*)s_m)[i] = 0u;
     __syncthreads();
-    // ---- blur rows: 2 rows x 4 columns per task (dot4), stored as row-pair u16 dwords
-#ifndef ORBX_EXP_NO_BLURROW
-    for (int i = tid; i < ((kTH + 6) / 2) * (kTW / 4); i += 256) {
-        const int pr = i >> 4, c0 = 4 + 4 * (i & 15);
-        const uint32_t* ra = (const uint32_t*)&s_in[2 * pr][c0];
-        const uint32_t* rb = (const uint32_t*)&s_in[2 * pr + 1][c0];
-        uint32_t a[4], b[4];
-        blur_row4(ra[-1], ra[0], ra[1], a);
-        blur_row4(rb[-1], rb[0], rb[1], b);
-        *(uint4*)&s_rowp[pr][c0 - 4] = make_uint4(a[0] | (b[0] << 16), a[1] | (b[1] << 16), a[2] | (b[2] << 16),
-                                                  a[3] | (b[3] << 16));
-    }
-#endif
     // ---- FAST compass test on the detection area, compaction of the survivors.
     // A thread always owns columns 4j..4j+3 (j = tid & 15) of rows tid/16 + 16 i, so
     // its detection-area column mask is computed once.
 #ifndef ORBX_EXP_NO_COMPASS
     {
-        const int j = tid & 15, c0 = 4 + 4 * j, x0 = X0 + 4 * j;
+        const int j = tid & 15, c0 = kSX + 4 * j, x0 = X0 + 4 * j;
         unsigned colmask = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) colmask |= (x0 + k >= kEdge && x0 + k < g.w - kEdge) ? 1u << k : 0u;
@@ -544,7 +538,22 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
     for (int i = tid; i < n; i += 256) {
         const int rc = s_list[i];
         const int r = rc >> 8, c = rc & 255;
-        s_m[r][c] = (uint8_t)fast_strength(&s_in[r + 3][c + 4], kSW);
+        s_m[r][c] = (uint8_t)fast_strength(&s_in[r + 3][c + kSX], kSW);
+    }
+#endif
+    __syncthreads();
+    // ---- blur rows (into the survivor list's buffer, free now): 2 rows x 4 columns per
+    // task (dot4), stored as row-pair u16 dwords
+#ifndef ORBX_EXP_NO_BLURROW
+    for (int i = tid; i < ((kTH + 6) / 2) * (kTW / 4); i += 256) {
+        const int pr = i >> 4, c0 = kSX + 4 * (i & 15);
+        const uint32_t* ra = (const uint32_t*)&s_in[2 * pr][c0];
+        const uint32_t* rb = (const uint32_t*)&s_in[2 * pr + 1][c0];
+        uint32_t a[4], b[4];
+        blur_row4(ra[-1], ra[0], ra[1], a);
+        blur_row4(rb[-1], rb[0], rb[1], b);
+        *(uint4*)&s_rowp[pr][c0 - kSX] = make_uint4(a[0] | (b[0] << 16), a[1] | (b[1] << 16), a[2] | (b[2] << 16),
+                                                  a[3] | (b[3] << 16));
     }
 #endif
     __syncthreads();

@@ -188,3 +188,15 @@ class ORBextractor:
 def stream_wait_event(stream: int, event: int) -> None:
     """hipStreamWaitEvent(stream, event) through the library (orbx_stream_wait_event)."""
     L.check(L.lib().orbx_stream_wait_event(C.c_void_p(stream), C.c_void_p(event)))
+
+
+def stream_create_cu_strided(device: int, cu_stride: int) -> int:
+    """orbx_stream_create_cu_strided: a hipStream_t whose kernels run only on CUs 0, k,
+    2k, ... (k = cu_stride); release it with stream_destroy."""
+    s = C.c_void_p()
+    L.check(L.lib().orbx_stream_create_cu_strided(int(device), int(cu_stride), C.byref(s)))
+    return s.value or 0
+
+
+def stream_destroy(stream: int) -> None:
+    L.check(L.lib().orbx_stream_destroy(C.c_void_p(stream)))

@@ -8,7 +8,8 @@ all in HBM:
 * the batch is split into `lanes` contiguous chunks, each extracted by its own
   ORBextractor on its own HIP stream, so one chunk's latency-bound kernels (octree,
   describe) overlap another's;
-* one ORBmatcher matches all B-1 pairs on a third stream once every lane is done;
+* one ORBmatcher matches all B-1 pairs on a third stream once every lane is done (a
+  stream of its own, created before the lanes' streams);
 * pipelined (default): keypoint / descriptor / match buffers are double-buffered, so
   batch j is extracted while batch j-1 is matched; the next use of a buffer waits for
   the matching that last read it (events in both directions).  Not pipelined: the same
@@ -31,7 +32,7 @@ class SequencePipeline:
                  fy: float = 500.0, cx: float = 320.0, cy: float = 240.0, depth: float = 5.0, th: float = 15.0,
                  nnratio: float = 0.9, check_ori: bool = True, match_stream=None,
                  nbuf: int = 2, matcher_mode: int | None = None, match_after_stage: int = 0,
-                 lane_offset_stage: int = 2):
+                 lane_offset_stage: int = 2, match_cu_stride: int = 1):
         import torch
 
         self.B, self.W, self.H = int(batch), int(width), int(height)
@@ -40,6 +41,20 @@ class SequencePipeline:
         self.pipelined = bool(pipelined) and self.match
         self.dev = torch.device("cuda", device)
         self.fx, self.fy, self.cx, self.cy, self.depth, self.th = fx, fy, cx, cy, depth, th
+        # The matcher's stream is created here, before the extraction lanes' streams
+        # (orbx_stream_create_cu_strided; match_cu_stride k > 1 also confines it to CUs
+        # 0, k, 2k, ...).  HIP hands out its hardware queues in stream-creation order, and
+        # the three busy streams run concurrently only on queues of their own: created
+        # after the lanes' streams, or taken from torch's stream pool, the same matcher
+        # stream measured 193-197k frames/s against 214-217k (k = 1 and k = 4 alike;
+        # profiles/r02_n_stream_order_ab.log)
+        self._own_ms = None
+        if match_stream is not None:
+            self.ms = match_stream
+        else:
+            from .extractor import stream_create_cu_strided
+            self._own_ms = stream_create_cu_strided(device, max(1, int(match_cu_stride)))
+            self.ms = torch.cuda.ExternalStream(self._own_ms, device=self.dev)
         self.exs = [ORBextractor(*params, device=device) for _ in range(self.S)]
         self.matcher = ORBmatcher(nnratio, check_ori, device=device)
         # matcher_mode: orbx_matcher_set_footprint.  Default 5 (lean split: one 1024-thread
@@ -55,7 +70,6 @@ class SequencePipeline:
         self.cap = self.exs[0].max_keypoints(self.W, self.H)
         self.bounds = [(self.B * c // self.S, self.B * (c + 1) // self.S) for c in range(self.S)]
         self.streams = [torch.cuda.ExternalStream(e.stream_handle(), device=self.dev) for e in self.exs]
-        self.ms = match_stream if match_stream is not None else torch.cuda.Stream(device=self.dev)
         nbuf = max(2, int(nbuf)) if self.pipelined else 1
         B, cap = self.B, self.cap
         i32 = dict(dtype=torch.int32, device=self.dev)
@@ -82,6 +96,20 @@ class SequencePipeline:
         self.it = 0            # extractions issued
         self.pending = None    # buffer extracted but not yet matched (pipelined)
         self.last = None       # buffer holding the newest complete result
+
+    def close(self):
+        """Release the matcher stream this pipeline created (after synchronising)."""
+        if self._own_ms:
+            from .extractor import stream_destroy
+            self.ms.synchronize()
+            stream_destroy(self._own_ms)
+            self._own_ms = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     # -- launches -----------------------------------------------------------------
     def _extract(self, frames, b):
