@@ -351,7 +351,8 @@ def main():
                           else int(os.environ["ORBX_MATCH_MODE"]),
                           match_after_stage=int(os.environ.get("ORBX_MATCH_AFTER", "0")),
                           lane_offset_stage=int(os.environ.get("ORBX_LANE_OFFSET", "2")),
-                          match_cu_stride=int(os.environ.get("ORBX_MATCH_CUSTRIDE", "1")))
+                          match_cu_stride=int(os.environ.get("ORBX_MATCH_CUSTRIDE", "1")),
+                          match_priority=int(os.environ.get("ORBX_MATCH_STREAM_PRIO", "0")))
     S = pl.S
     d_frames = torch.from_numpy(frames_np).to(dev)
     d_T = torch.from_numpy(T).to(dev)

@@ -115,13 +115,14 @@ void* orbx_extractor_stream(orbx_extractor* ex);
 int orbx_extractor_set_stage_event(orbx_extractor* ex, int stage, void** event);
 int orbx_stream_wait_event(void* stream, void* event);
 
-/* A HIP stream on `device` whose kernels run only on compute units 0, k, 2k, ...
- * (hipExtStreamCreateWithCUMask; k = 1: every CU, a plain non-blocking stream).  The
- * batched front end creates its matcher stream with it before the extraction lanes'
- * streams, so that the three busy streams get hardware queues of their own (DESIGN.md
- * section 5).  No reference counterpart: ORB-SLAM2 tracks one frame at a time.
- * Release with orbx_stream_destroy. */
-int orbx_stream_create_cu_strided(int device, int cu_stride, void** stream);
+/* A non-blocking HIP stream on `device`.  cu_stride k > 1: its kernels run only on
+ * compute units 0, k, 2k, ... (hipExtStreamCreateWithCUMask, default priority);
+ * otherwise hipStreamCreateWithPriority with `priority` (HIP's range: lower numbers
+ * are higher priorities; 0 = default).  The batched front end creates its matcher
+ * stream with it before the extraction lanes' streams, so that the three busy streams
+ * get hardware queues of their own.  No reference counterpart:
+ * ORB-SLAM2 tracks one frame at a time.  Release with orbx_stream_destroy. */
+int orbx_stream_create(int device, int cu_stride, int priority, void** stream);
 int orbx_stream_destroy(void* stream);
 
 /* Kernel status of the last extraction (any path), per frame: 0 = complete; bit 0

@@ -31,7 +31,7 @@ EXPORTED = [
     "orbx_extractor_create", "orbx_extractor_destroy", "orbx_extractor_levels",
     "orbx_extractor_features_per_level", "orbx_extractor_max_keypoints", "orbx_extract",
     "orbx_extract_batch", "orbx_extract_batch_device", "orbx_extractor_stream", "orbx_extractor_set_stage_event",
-    "orbx_stream_wait_event", "orbx_stream_create_cu_strided", "orbx_stream_destroy",
+    "orbx_stream_wait_event", "orbx_stream_create", "orbx_stream_destroy",
     "orbx_extractor_set_timing", "orbx_extractor_stage_times", "orbx_pyramid_level",
     "orbx_pyramid_level_device", "orbx_hamming", "orbx_hamming_matrix_device",
     "orbx_window_match_device", "orbx_window_match", "orbx_version", "orbx_device_count",
@@ -104,7 +104,7 @@ def lib() -> C.CDLL:
     L.orbx_extractor_stream.restype = vp
     L.orbx_extractor_set_stage_event.argtypes = [vp, C.c_int, C.POINTER(vp)]
     L.orbx_stream_wait_event.argtypes = [vp, vp]
-    L.orbx_stream_create_cu_strided.argtypes = [C.c_int, C.c_int, C.POINTER(vp)]
+    L.orbx_stream_create.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(vp)]
     L.orbx_stream_destroy.argtypes = [vp]
     L.orbx_extractor_status.argtypes = [vp, C.c_int, ip, ip]
     L.orbx_extractor_status_device.argtypes = [vp, C.POINTER(vp)]

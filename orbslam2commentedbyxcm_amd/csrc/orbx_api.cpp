@@ -390,15 +390,16 @@ int orbx_stream_wait_event(void* stream, void* event) {
     return ORBX_OK;
 }
 
-int orbx_stream_create_cu_strided(int device, int cu_stride, void** stream) {
+int orbx_stream_create(int device, int cu_stride, int priority, void** stream) {
     if (!stream || cu_stride < 1) return fail(ORBX_ERR_ARG, "bad argument");
+    if (cu_stride > 1 && priority != 0) return fail(ORBX_ERR_ARG, "a CU-masked stream has the default priority");
     *stream = nullptr;
     HIP_TRY(hipSetDevice(device));
     int ncu = 0;
     HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
     hipStream_t s = nullptr;
     if (cu_stride == 1) {
-        HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority));
     } else {
         std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
         for (int i = 0; i < ncu; i += cu_stride) mask[(size_t)i / 32] |= 1u << (i % 32);

@@ -83,6 +83,8 @@ __device__ __forceinline__ void xcd_frame_block(int per_frame, int nframes, int&
 
 // ------------------------------------------------------------------ pyramid
 
+typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+
 // 24 x 24 -> high 32 bits of the 48-bit product (v_mul_hi_u32_u24)
 __device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
     return (uint32_t)(((unsigned long long)(a & 0xffffff) * (b & 0xffffff)) >> 32);
@@ -124,7 +126,13 @@ __device__ __forceinline__ QuadSplit quad_split(int nq, int tid) {
     return s;
 }
 
-__global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ src, size_t frame_pitch, size_t stride,
+#ifdef ORBX_PZ_WAVES
+#define ORBX_PZ_ATTR __attribute__((amdgpu_waves_per_eu(ORBX_PZ_WAVES)))
+#else
+#define ORBX_PZ_ATTR
+#endif
+template <bool WIN>
+__global__ __launch_bounds__(256) ORBX_PZ_ATTR void k_pyramid(const uint8_t* __restrict__ src, size_t frame_pitch, size_t stride,
                                                  int vec4, uint8_t* __restrict__ pyr, long long fb,
                                                  const LevelGeom* __restrict__ lv, int L,
                                                  const int16_t* __restrict__ rtab, int pz_off, int tiles_pf,
@@ -184,54 +192,87 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ src
     // h = S[sx0]*a0 + S[sx1]*a1 is kept as hm = h & ~15 and the vertical step
     // (b*(h>>4))>>16 = (b*hm)>>20 is one v_mul_hi_u32_u24 of (b << 12, hm).  The result
     // needs no saturation: a0 + a1 <= 2049 and b0 + b1 <= 2049 bound it by 255.
+#ifdef ORBX_EXP_PZ_L0ONLY
+    if (L > 0) return;  // timing ablation: level 0 only
+#endif
     for (int l = 1; l < L; l++) {
-        __syncthreads();
         const int16_t* Rp = R + 8 * (l - 1);
         const int16_t* Rl = R + 8 * l;
         const int sxa = Rp[0] & ~3, sy0 = Rp[1], sstride = 4 * ((Rp[2] - sxa + 3) >> 2);
         const int x0 = Rl[0], y0 = Rl[1], x1 = Rl[2], y1 = Rl[3];
         const int ox0 = Rl[4], oy0 = Rl[5], ox1 = Rl[6], oy1 = Rl[7];
-        if (!(x1 > x0 && y1 > y0)) continue;  // block-uniform
-        const uint8_t* sb = s_pz + ((l & 1) ? 0 : lds_a);
-        uint8_t* ob = s_pz + ((l & 1) ? lds_a : 0);
         const LevelGeom& g = lv[l];
         const int16_t* xt = rtab + g.xtab_off;
         const int xa = x0 & ~3;
         const int nq = (x1 - xa + 3) >> 2, hn = y1 - y0, ostride = 4 * nq;
         const QuadSplit sp = quad_split(nq, tid);
-        if (sp.gr >= sp.G) continue;
         const int rc = (hn + sp.G - 1) / sp.G;
         const int ra = sp.gr * rc, rb = min(hn, ra + rc);
-        if (ra >= rb) continue;
+        const bool act = x1 > x0 && y1 > y0 && sp.gr < sp.G && ra < rb;
+        // the first quad's column taps (sx0, sx1, a0, a1 as 4 x int16) and the first 8
+        // rows' taps are loaded before the barrier: their latency hides in the wait for
+        // the previous level.  Columns outside [x0, x1) (quad widening) borrow the nearest
+        // column's taps (the quad's source span stays monotone): their bytes are computed
+        // but never read by the next level and never owned.
+        const int16_t* yt = rtab + g.ytab_off + 4 * (y0 + ra);
+        int2 xtp[4], yv[8];  // rtab is padded at the end: 8 rows' taps are always readable
+        if (act) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int x = xa + 4 * sp.q + k;
+                xtp[k] = *(const int2*)(xt + 4 * min(max(x, x0), x1 - 1));
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) yv[k] = *(const int2*)(yt + 4 * k);
+        }
+        __syncthreads();
+        if (!act) continue;
+        const uint8_t* sb = s_pz + ((l & 1) ? 0 : lds_a);
+        uint8_t* ob = s_pz + ((l & 1) ? lds_a : 0);
         // owned rows of this thread's run, relative to the rectangle
         const int wlo = max(ra, oy0 - y0), whi = min(rb, oy1 - y0);
         for (int qq = sp.q; qq < nq; qq += sp.nqp) {
             const int x = xa + 4 * qq;
             // 0: not owned, 1: whole quad owned, 2: partly owned
             const int own = (x + 4 <= ox0 || x >= ox1) ? 0 : ((x >= ox0 && x + 4 <= ox1) ? 1 : 2);
+            if (qq != sp.q) {  // a second quad (rectangles over 1024 columns): reload
+#pragma unroll
+                for (int k = 0; k < 4; k++) xtp[k] = *(const int2*)(xt + 4 * min(max(x + k, x0), x1 - 1));
+#pragma unroll
+                for (int k = 0; k < 8; k++) yv[k] = *(const int2*)(yt + 4 * k);
+            }
             int c0[4], c1[4];
             uint32_t a0[4], a1[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                // columns outside [x0, x1) (quad widening) borrow x0's taps: their bytes
-                // are computed but never read by the next level and never owned
-                const int dx = x + k >= x0 && x + k < x1 ? x + k : x0;
-                const int2 t = *(const int2*)(xt + 4 * dx);  // sx0, sx1, a0, a1 as 4 x int16
-                c0[k] = (int16_t)(t.x & 0xffff) - sxa;
-                c1[k] = (int16_t)(t.x >> 16) - sxa;
-                a0[k] = (uint32_t)(t.y & 0xffff);
-                a1[k] = (uint32_t)t.y >> 16;
+                c0[k] = (int16_t)(xtp[k].x & 0xffff) - sxa;
+                c1[k] = (int16_t)(xtp[k].x >> 16) - sxa;
+                a0[k] = (uint32_t)(xtp[k].y & 0xffff);
+                a1[k] = (uint32_t)xtp[k].y >> 16;
             }
-            const int16_t* yp = rtab + g.ytab_off + 4 * (y0 + ra);
+            // WIN (the plan checked that every quad's source bytes c0[0] .. c1[3] span at
+            // most 8): the row's bytes come from three aligned dwords, shifted to start
+            // at c0[0] (two v_alignbyte); then per column one v_perm_b32 pairs bytes c0,
+            // c1 as u16 halves and one v_dot2_u32_u16 with (a0, a1) gives h.
+            const int wbase = c0[0] & ~3, wsh = c0[0] & 3;
+            uint32_t wsel[4];
+            ushort2_t wab[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                wsel[k] = (uint32_t)(c0[k] - c0[0]) | 0x0c00u | ((uint32_t)(c1[k] - c0[0]) << 16) | 0x0c000000u;
+                wab[k] = ushort2_t{(unsigned short)a0[k], (unsigned short)a1[k]};
+            }
+            const int16_t* yp = yt;
             uint8_t* lp = ob + ra * ostride + 4 * qq;
             uint8_t* gp = frame + g.off + (size_t)(y0 + ra) * g.pitch + x;
             int s_cur = -1;
             const uint8_t* srow = sb;
             uint32_t hc[4] = {0, 0, 0, 0}, hp[4] = {0, 0, 0, 0};
             for (int rr = ra; rr < rb; rr += 8) {
-                int2 yv[8];  // 8 rows' taps r0, r1, b0, b1 in flight (rtab is padded at the end)
+                if (rr != ra) {  // the next 8 rows' taps
 #pragma unroll
-                for (int k = 0; k < 8; k++) yv[k] = *(const int2*)(yp + 4 * k);
+                    for (int k = 0; k < 8; k++) yv[k] = *(const int2*)(yp + 4 * k);
+                }
                 yp += 32;
 #pragma unroll
                 for (int kb = 0; kb < 8; kb++) {
@@ -247,11 +288,25 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ src
                             s_cur++;
                             srow += sstride;
                         }
+                        if constexpr (WIN) {
+                            const uint32_t* wp = (const uint32_t*)(srow + wbase);
+                            const uint32_t d0 = wp[0], d1 = wp[1], d2 = wp[2];
+                            const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, wsh);
+                            const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, wsh);
 #pragma unroll
-                        for (int k = 0; k < 4; k++) {
-                            hp[k] = hc[k];
-                            // two byte reads (a merged u16 read would be unaligned)
-                            hc[k] = (srow[c0[k]] * a0[k] + srow[c1[k]] * a1[k]) & ~15u;
+                            for (int k = 0; k < 4; k++) {
+                                hp[k] = hc[k];
+                                const uint32_t pr = __builtin_amdgcn_perm(hi, lo, wsel[k]);
+                                hc[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, pr), wab[k], 0u, false) &
+                                        ~15u;
+                            }
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < 4; k++) {
+                                hp[k] = hc[k];
+                                // two byte reads (a merged u16 read would be unaligned)
+                                hc[k] = (srow[c0[k]] * a0[k] + srow[c1[k]] * a1[k]) & ~15u;
+                            }
                         }
                     }
                     const uint32_t b0 = ((uint32_t)t.y & 0xffffu) << 12, b1 = ((uint32_t)t.y >> 16) << 12;
@@ -263,7 +318,11 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ src
                         packed |= v << (8 * k);
                     }
                     *(uint32_t*)lp = packed;
+#ifdef ORBX_EXP_PZ_NOSTORE
+                    if (packed == 0x12345678u && own != 0 && r >= wlo && r < whi) {  // timing ablation
+#else
                     if (own != 0 && r >= wlo && r < whi) {
+#endif
                         if (own == 1) *(uint32_t*)gp = packed;
                         else
                             store_owned_quad(gp, x, ox0, ox1, packed);
@@ -341,7 +400,6 @@ constexpr int kSW = kLU == 16 ? kTW + 2 * kSX + 8 : kTW + 2 * kSX;
 static_assert(kLU == 4 || kLU == 16, "staging load width");
 typedef std::conditional_t<kLU == 16, uint4, uint32_t> lt_load_t;
 
-typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
 
 // Bytes [c+dx, c+dx+3] of a row from its aligned dwords at c-4 (lo), c (mid), c+4 (hi),
 // dx in [-4, 4].
@@ -1477,14 +1535,13 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     {
         const int vec4 = ((uintptr_t)d_imgs % 4 == 0) && (stride % 4 == 0) && (frame_pitch % 4 == 0);
         const size_t lds = (size_t)plan.pz_lds_a + plan.pz_lds_b;
+        auto kern = plan.pz_win ? k_pyramid<true> : k_pyramid<false>;
         if (lds > 64 * 1024) {
-            hipError_t e = hipFuncSetAttribute((const void*)k_pyramid, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)lds);
+            hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(k_pyramid, dim3(plan.pz_tiles * batch), dim3(256), lds, stream, d_imgs, frame_pitch,
-                           stride, vec4, db.pyr, fb, db.lv, L, db.rtab, plan.pz_off, plan.pz_tiles, batch,
-                           plan.pz_lds_a);
+        hipLaunchKernelGGL(kern, dim3(plan.pz_tiles * batch), dim3(256), lds, stream, d_imgs, frame_pitch, stride,
+                           vec4, db.pyr, fb, db.lv, L, db.rtab, plan.pz_off, plan.pz_tiles, batch, plan.pz_lds_a);
     }
     if (ev) (void)hipEventRecord(ev[1], stream);
     if (stage_ev && stage_after == 1) (void)hipEventRecord(stage_ev, stream);

@@ -171,13 +171,25 @@ static bool pyramid_tiles(Plan& plan) {
                                       (int16_t)ox0, (int16_t)oy0, (int16_t)ox1, (int16_t)oy1};
                 std::memcpy(R + 8 * l, r, sizeof(r));
                 // LDS holds the needed columns widened to whole 4-byte quads
+                // (+ 16: k_pyramid<true> reads a row's source window as three dwords, which
+                // can reach 8 bytes past the last row's last quad)
                 const int bytes = any ? 4 * ((x1 - (x0 & ~3) + 3) / 4) * (y1 - y0) : 0;
                 int& buf = (l & 1) ? plan.pz_lds_b : plan.pz_lds_a;
-                buf = std::max(buf, (bytes + 15) & ~15);
+                buf = std::max(buf, ((bytes + 15) & ~15) + 16);
                 nx0 = x0; nx1 = x1; ny0 = y0; ny1 = y1;
             }
         }
     if (plan.pz_lds_a + plan.pz_lds_b > kPzMaxLds) { plan.why = "pyramid tile exceeds LDS (scale factor too large)"; return false; }
+    // k_pyramid<true> needs the source bytes of any 4 consecutive output columns (sx0 of the
+    // first .. sx1 of the last) within 8 bytes: scale factors up to about 2
+    // (ORBX_PZ_BYTE=1 forces the byte-read form: tuning, the output is the same)
+    plan.pz_win = !std::getenv("ORBX_PZ_BYTE");
+    for (int l = 1; l < L && plan.pz_win; l++) {
+        const LevelGeom& g = plan.lv[l];
+        const int16_t* xt = plan.rtab.data() + g.xtab_off;
+        for (int x = 0; x < g.w; x++)
+            if (xt[4 * std::min(x + 3, g.w - 1) + 1] - xt[4 * x] > 7) { plan.pz_win = false; break; }
+    }
     return true;
 }
 

@@ -101,6 +101,7 @@ struct Plan {
     int pz_nx = 0, pz_ny = 0;
     int pz_off = 0;                 // offset (int16 units) of the tile rectangles in rtab
     int pz_lds_a = 0, pz_lds_b = 0; // LDS ping / pong buffers (even / odd levels), bytes
+    bool pz_win = false;            // k_pyramid<true>: every 4 columns' resize taps span <= 8 source bytes
     int fc_wr = 0, fc_wc = 0;       // largest FAST detection window (rows, cols)
     int max_ncap = 0;
     int max_key_cap = 0;

@@ -190,11 +190,11 @@ def stream_wait_event(stream: int, event: int) -> None:
     L.check(L.lib().orbx_stream_wait_event(C.c_void_p(stream), C.c_void_p(event)))
 
 
-def stream_create_cu_strided(device: int, cu_stride: int) -> int:
-    """orbx_stream_create_cu_strided: a hipStream_t whose kernels run only on CUs 0, k,
-    2k, ... (k = cu_stride); release it with stream_destroy."""
+def stream_create(device: int, cu_stride: int = 1, priority: int = 0) -> int:
+    """orbx_stream_create: a non-blocking hipStream_t, on CUs 0, k, 2k, ... only when
+    k = cu_stride > 1, else of HIP priority `priority`; release it with stream_destroy."""
     s = C.c_void_p()
-    L.check(L.lib().orbx_stream_create_cu_strided(int(device), int(cu_stride), C.byref(s)))
+    L.check(L.lib().orbx_stream_create(int(device), int(cu_stride), int(priority), C.byref(s)))
     return s.value or 0
 
 

@@ -216,6 +216,12 @@ class StereoKeyFramePipeline:
         left, right = self.seq.views(self.local)
         self.left_np, self.right_np = left, right
         prm = (s["nfeatures"], s["scale"], s["nlevels"], s["ini_th"], s["min_th"])
+        # the matcher stream first: HIP assigns hardware queues in stream-creation order, and
+        # a stream created after the extractors' (or from torch's pool) can share one with
+        # an extraction stream
+        from .extractor import stream_create
+        self._own_ms = stream_create(device, 1)
+        self.ms = torch.cuda.ExternalStream(self._own_ms, device=self.dev)
         self.sets = [(ORBextractor(*prm, device=device), ORBextractor(*prm, device=device)) for _ in range(2)]
         self.sf = self.sets[0][0].GetScaleFactors()
         self.cap = self.sets[0][0].max_keypoints(self.W, self.H)
@@ -256,7 +262,6 @@ class StereoKeyFramePipeline:
                              max_y=float(self.H), scale_factors=self.sf, level_sigma2=self.sf * self.sf)
         self.streams = [(torch.cuda.ExternalStream(a.stream_handle(), device=self.dev),
                          torch.cuda.ExternalStream(b.stream_handle(), device=self.dev)) for a, b in self.sets]
-        self.ms = torch.cuda.Stream(device=self.dev)
         self.ev_l = [torch.cuda.Event() for _ in range(2)]
         self.ev_r = [torch.cuda.Event() for _ in range(2)]
         self.ev_m = [torch.cuda.Event() for _ in range(2)]
@@ -270,6 +275,20 @@ class StereoKeyFramePipeline:
         from .matcher import keyframe_table
         bufs = [self.gathered] * 2 if self.world > 1 else self.slabs
         self._tabs = [keyframe_table(self.lay.records(b.data_ptr(), self.world, self._rec_poses)) for b in bufs]
+
+    def close(self):
+        """Release the matcher stream this pipeline created (after synchronising)."""
+        if self._own_ms:
+            from .extractor import stream_destroy
+            self.ms.synchronize()
+            stream_destroy(self._own_ms)
+            self._own_ms = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def step(self):
         """Issue one step (asynchronous)."""

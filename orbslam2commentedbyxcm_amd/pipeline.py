@@ -32,7 +32,8 @@ class SequencePipeline:
                  fy: float = 500.0, cx: float = 320.0, cy: float = 240.0, depth: float = 5.0, th: float = 15.0,
                  nnratio: float = 0.9, check_ori: bool = True, match_stream=None,
                  nbuf: int = 2, matcher_mode: int | None = None, match_after_stage: int = 0,
-                 lane_offset_stage: int = 2, match_cu_stride: int = 1):
+                 lane_offset_stage: int = 2, match_cu_stride: int = 1,
+                 match_priority: int = 0):
         import torch
 
         self.B, self.W, self.H = int(batch), int(width), int(height)
@@ -42,8 +43,8 @@ class SequencePipeline:
         self.dev = torch.device("cuda", device)
         self.fx, self.fy, self.cx, self.cy, self.depth, self.th = fx, fy, cx, cy, depth, th
         # The matcher's stream is created here, before the extraction lanes' streams
-        # (orbx_stream_create_cu_strided; match_cu_stride k > 1 also confines it to CUs
-        # 0, k, 2k, ...).  HIP hands out its hardware queues in stream-creation order, and
+        # (orbx_stream_create; match_cu_stride k > 1 also confines it to CUs 0, k,
+        # 2k, ...; match_priority: its HIP stream priority).  HIP hands out its hardware queues in stream-creation order, and
         # the three busy streams run concurrently only on queues of their own: created
         # after the lanes' streams, or taken from torch's stream pool, the same matcher
         # stream measured 193-197k frames/s against 214-217k (k = 1 and k = 4 alike;
@@ -52,8 +53,8 @@ class SequencePipeline:
         if match_stream is not None:
             self.ms = match_stream
         else:
-            from .extractor import stream_create_cu_strided
-            self._own_ms = stream_create_cu_strided(device, max(1, int(match_cu_stride)))
+            from .extractor import stream_create
+            self._own_ms = stream_create(device, max(1, int(match_cu_stride)), int(match_priority))
             self.ms = torch.cuda.ExternalStream(self._own_ms, device=self.dev)
         self.exs = [ORBextractor(*params, device=device) for _ in range(self.S)]
         self.matcher = ORBmatcher(nnratio, check_ori, device=device)

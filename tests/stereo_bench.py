@@ -126,6 +126,11 @@ def main(argv=None):
     from orbslam2commentedbyxcm_amd import ORBextractor
     from orbslam2commentedbyxcm_amd.matcher import ORBmatcher
     dev = torch.device("cuda", 0)
+    # the stereo matcher's stream first: HIP assigns hardware queues in stream-creation
+    # order, and a stream created after the extractors' (or from torch's pool) can share
+    # one with an extraction stream
+    from orbslam2commentedbyxcm_amd.extractor import stream_create
+    ms = torch.cuda.ExternalStream(stream_create(0, 1), device=dev)
     sets = [(ORBextractor(NF, 1.2, 8, 20, 7), ORBextractor(NF, 1.2, 8, 20, 7)) for _ in range(2)]
     matcher = ORBmatcher(0.6, True)
     sf = sets[0][0].GetScaleFactors()
@@ -140,7 +145,6 @@ def main(argv=None):
             "dp": torch.empty((B, cap), dtype=torch.float32, device=dev)} for _ in range(2)]
     streams = [(torch.cuda.ExternalStream(a.stream_handle(), device=dev),
                 torch.cuda.ExternalStream(b.stream_handle(), device=dev)) for a, b in sets]
-    ms = torch.cuda.Stream(device=dev)
     ev_l = [torch.cuda.Event() for _ in range(2)]
     ev_r = [torch.cuda.Event() for _ in range(2)]
     ev_m = [torch.cuda.Event() for _ in range(2)]

@@ -91,6 +91,7 @@ def test_stage_event_arguments(orbx_built):
     assert L.lib().orbx_extractor_set_stage_event(None, 2, C.byref(ev)) == L.ORBX_ERR_ARG
     assert L.lib().orbx_stream_wait_event(None, None) == L.ORBX_ERR_ARG
     st = C.c_void_p()
-    assert L.lib().orbx_stream_create_cu_strided(0, 0, C.byref(st)) == L.ORBX_ERR_ARG
-    assert L.lib().orbx_stream_create_cu_strided(0, 4, None) == L.ORBX_ERR_ARG
+    assert L.lib().orbx_stream_create(0, 0, 0, C.byref(st)) == L.ORBX_ERR_ARG
+    assert L.lib().orbx_stream_create(0, 4, 0, None) == L.ORBX_ERR_ARG
+    assert L.lib().orbx_stream_create(0, 4, -1, C.byref(st)) == L.ORBX_ERR_ARG
     assert L.lib().orbx_stream_destroy(None) == L.ORBX_ERR_ARG

@@ -41,6 +41,25 @@ def test_pyramid_matches_oracle(oracle, orbx_built):
         assert np.array_equal(a, b), f"level {lv}: {(a != b).sum()} pixels differ"
 
 
+@pytest.mark.parametrize("sf,nl,byte", [(1.2, 8, True), (1.5, 6, False), (2.0, 3, False), (2.5, 3, False)])
+def test_pyramid_forms_match_oracle(oracle, orbx_built, monkeypatch, sf, nl, byte):
+    """Both k_pyramid forms: the dword-window one (any 4 columns' resize taps within 8
+    source bytes, scale factors up to 2) and the byte-read one (ORBX_PZ_BYTE=1, or a
+    larger scale factor such as 2.5)."""
+    if byte:
+        monkeypatch.setenv("ORBX_PZ_BYTE", "1")
+    img = synth.frame(12)
+    ex = ORBextractor(1000, sf, nl, 20, 7)
+    kps, desc = ex(img)
+    p = oracle.params(1000, sf, nl, 20, 7)
+    ref = oracle.pyramid(img, p)
+    for lv, (a, b) in enumerate(zip(ex.mvImagePyramid, ref)):
+        assert a.shape == b.shape
+        assert np.array_equal(a, b), f"level {lv}: {(a != b).sum()} pixels differ"
+    kr, dr, _ = oracle.extract(img, p)
+    _cmp(kps, desc, kr, dr)
+
+
 def test_batch_matches_single(oracle, orbx_built):
     imgs = synth.frames(6, first_seed=100)
     ex = ORBextractor(1000, 1.2, 8, 20, 7)
