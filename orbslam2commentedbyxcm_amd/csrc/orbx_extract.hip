@@ -1408,8 +1408,10 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     // mask and the (u + 15)-weighted mask give sum(I) and sum((u+15) I) over the row:
     // m10 += sum((u+15) I) - 15 sum(I), m01 += v sum(I).  The steered-BRIEF patch of the
     // blurred level, rows y-18..y+18 (|rotated pattern point| <= 13*sqrt(2) < 18.5), 44
-    // bytes from (x-18) & ~3, is staged in LDS (48-byte rows, lanes 0..31 rows 0..31,
-    // lanes 0..4 rows 32..36); all loads are issued together, one round of latency.
+    // bytes from (x-18) & ~3, is staged in LDS (48-byte rows as 111 16-byte chunks, four
+    // per lane; the patch loads are the kernel's largest cost: 37 row segments of
+    // separate cache lines per keypoint); all loads are issued together, one round of
+    // latency.
     // Keypoints lie in [19, w-20] x [19, h-20] of their level, so every row exists; a
     // row's last dword may reach 6 bytes past the level width (inside the pitch, or the
     // buffers' slack for the very last row).
@@ -1426,10 +1428,15 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
         const uint8_t* prow = pframe + (uint32_t)(g.off + (long long)(y + v) * pitch + xs);
         const uint4 p0 = *(const uint4*)prow, p1 = *(const uint4*)(prow + 16);
         const uint32_t p2 = *(const uint32_t*)(prow + 32);
-        const uint8_t* brow0 = bframe + (uint32_t)(g.off + (long long)(y - 18 + hl) * pitch + xb);
-        const uint8_t* brow1 = bframe + (uint32_t)(g.off + (long long)(y + 14 + min(hl, 4)) * pitch + xb);
-        const uint4 b00 = *(const uint4*)brow0, b01 = *(const uint4*)(brow0 + 16), b02 = *(const uint4*)(brow0 + 32);
-        const uint4 b10 = *(const uint4*)brow1, b11 = *(const uint4*)(brow1 + 16), b12 = *(const uint4*)(brow1 + 32);
+        // the patch's 37 x 3 16-byte chunks, chunk hl + 32 j (row c / 3, part c % 3):
+        // four load instructions per wave instead of six (37 rows on 32 lanes)
+        const uint8_t* bpatch = bframe + (uint32_t)(g.off + (long long)(y - 18) * pitch + xb);
+        uint4 bch[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int c = min(hl + 32 * j, 110), row = (c * 171) >> 9;
+            bch[j] = *(const uint4*)(bpatch + (uint32_t)(row * pitch + 16 * (c - 3 * row)));
+        }
         const uint4* cm = (const uint4*)c_icm[d0][av];
         const uint4* cw = (const uint4*)c_icw[d0][av];
         const uint4 m0 = cm[0], m1 = cm[1], m2 = cm[2], w0 = cw[0], w1 = cw[1], w2 = cw[2];
@@ -1446,16 +1453,9 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
         const bool row_ok = hl < 31;
         m10 = row_ok ? (int)ws - 15 * (int)cs : 0;
         m01 = row_ok ? v * (int)cs : 0;
-        uint4* bd = (uint4*)(bp + hl * 48);
-        bd[0] = b00;
-        bd[1] = b01;
-        bd[2] = b02;
-        if (hl < 5) {
-            uint4* bd1 = (uint4*)(bp + (32 + hl) * 48);
-            bd1[0] = b10;
-            bd1[1] = b11;
-            bd1[2] = b12;
-        }
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (hl + 32 * j < 111) ((uint4*)bp)[hl + 32 * j] = bch[j];  // chunk c at byte 16 c
     }
     wave_lds_fence();
 #pragma unroll
