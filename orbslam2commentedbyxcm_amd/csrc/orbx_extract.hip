@@ -801,30 +801,30 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
 
 // ------------------------------------------------------------------ block helpers
 
-// In-place exclusive scan of a[0..n) by a 256-thread block; returns the total.
-// `tmp` holds >= 8 ints of LDS.  All threads must call it.
+// In-place exclusive scan of a[0..n) (non-negative) by a 256-thread block; returns the
+// total.  `tmp` holds >= 8 ints of LDS.  All threads must call it.  Each thread sums a
+// contiguous run of ceil(n / 256) entries, one DPP wave scan and one barrier combine the
+// runs, and each thread rewrites its run: two barriers for any n (the octree's node
+// lists reach a few thousand entries).
 __device__ int block_exscan(int* a, int n, int* tmp) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    int carry = 0;
-    for (int base = 0; base < n; base += 256) {
-        const int i = base + tid;
-        const int v = i < n ? a[i] : 0;
-        int x = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(x, o);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) tmp[wave] = x;
-        __syncthreads();
-        int wbase = 0;
-        for (int k = 0; k < wave; k++) wbase += tmp[k];
-        const int chunk_total = tmp[0] + tmp[1] + tmp[2] + tmp[3];
-        if (i < n) a[i] = carry + wbase + x - v;
-        carry += chunk_total;
-        __syncthreads();
+    const int per = (n + 255) >> 8;
+    const int b0 = min(tid * per, n), b1 = min(b0 + per, n);
+    int s = 0;
+    for (int i = b0; i < b1; i++) s += a[i];
+    const int incl = (int)wave_inclusive_sum((uint32_t)s);
+    if (lane == 63) tmp[wave] = incl;
+    __syncthreads();
+    int run = incl - s;
+    for (int k = 0; k < wave; k++) run += tmp[k];
+    const int total = tmp[0] + tmp[1] + tmp[2] + tmp[3];
+    for (int i = b0; i < b1; i++) {
+        const int v = a[i];
+        a[i] = run;
+        run += v;
     }
-    return carry;
+    __syncthreads();
+    return total;
 }
 
 __device__ __forceinline__ int key_x(uint32_t k) { return (int)(k & 0xfffu); }
@@ -1179,31 +1179,40 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
         const NodeBuf& A = cur ? nb1 : nb0;
         const NodeBuf& B = cur ? nb0 : nb1;
         const int prev = size;
-        // processing order: vPrev sorted ascending by (size, address), walked from the back
-        if (tid == 0) s_scal[2] = 0;
-        __syncthreads();
-        int nvloc = 0;
-        // order key of vPrev members: (size, creation rank) + 1, 0 for the others
-        // (`best` is free until phase 5)
-        for (int j = tid; j < size; j += 256)
-            best[j] = A.inV[j] ? (((unsigned long long)A.cnt[j] << 32) | (unsigned)A.crank[j]) + 1 : 0ull;
-        __syncthreads();
+        // processing order: vPrev sorted ascending by (size, address), walked from the back.
+        // The vPrev members are compacted (block scan) with their order keys (size,
+        // creation rank) -- distinct, creation ranks are -- into `best` (free until
+        // phase 5), node ids in sb; a member's rank is the number of larger keys among
+        // the nv members only, counted over the dense list with independent partial sums.
         for (int j = tid; j < size; j += 256) {
+            sa[j] = A.inV[j] ? 1 : 0;
             sc[j] = -1;  // rank of node j in processing order, -1 if not in vPrev
-            const unsigned long long kj = best[j];
-            if (kj) {
-                nvloc++;
-                int r = 0;
-                for (int i = 0; i < size; i++) r += best[i] > kj;
-                sc[j] = r;
-            }
             ccnt[4 * j] = ccnt[4 * j + 1] = ccnt[4 * j + 2] = ccnt[4 * j + 3] = 0;
         }
         __syncthreads();
-        if (nvloc) atomicAdd(&s_scal[2], nvloc);
-        __syncthreads();
-        const int nv = s_scal[2];
+        const int nv = block_exscan(sa, size, s_tmp);
         if (nv == 0) { finish = true; break; }
+        for (int j = tid; j < size; j += 256)
+            if (A.inV[j]) {
+                best[sa[j]] = ((unsigned long long)A.cnt[j] << 32) | (unsigned)A.crank[j];
+                sb[sa[j]] = j;
+            }
+        // pad to a multiple of 4 with keys never larger (past NC the reads land in the
+        // zeroed ccnt)
+        if (tid < 3 && nv + tid < NC) best[nv + tid] = 0ull;
+        __syncthreads();
+        for (int p = tid; p < nv; p += 256) {
+            const unsigned long long kp = best[p];
+            int r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+            for (int i = 0; i < nv; i += 4) {
+                r0 += best[i] > kp;
+                r1 += best[i + 1] > kp;
+                r2 += best[i + 2] > kp;
+                r3 += best[i + 3] > kp;
+            }
+            sc[sb[p]] = r0 + r1 + r2 + r3;
+        }
+        __syncthreads();
         for (int j = tid; j < size; j += 256)
             if (sc[j] >= 0) sa[sc[j]] = j;  // sa[r] = node processed r-th
         FOR_KEYS({
@@ -1221,21 +1230,22 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
             for (int q = 0; q < 4; q++) ne += ccnt[4 * j + q] > 0;
             sb[r] = ne;
         }
+        // K = first r where prev + sum_{i<=r}(ne_i - 1) >= N (break after it), else nv-1.
+        // Every processed node has ne >= 1, so the partial sums never decrease and K is
+        // the number of r whose sum stays below N (capped at nv - 1): a block scan of
+        // ne - 1 (into sa, free now) and a count instead of a one-thread walk.
+        if (tid == 0) s_scal[3] = 0;
         __syncthreads();
-        // K = first r where prev + sum_{i<=r}(ne_i - 1) >= N (break after it), else nv-1
-        if (tid == 0) {
-            int s = prev, kk = nv - 1, e = 0;
-            for (int r = 0; r < nv; r++) {
-                s += sb[r] - 1;
-                if (s >= N) { kk = r; break; }
-            }
-            s_scal[3] = kk;
-            for (int r = 0; r <= kk; r++) e += sb[r];
-            s_scal[4] = e;  // children created
-            s_scal[5] = s;  // new size
-        }
+        for (int r = tid; r < nv; r += 256) sa[r] = sb[r] - 1;
+        block_exscan(sa, nv, s_tmp);
+        int below = 0;
+        for (int r = tid; r < nv; r += 256) below += prev + sa[r] + sb[r] - 1 < N;
+        if (below) atomicAdd(&s_scal[3], below);
         __syncthreads();
-        const int Kp = s_scal[3], Cc = s_scal[4], nsize = s_scal[5];
+        const int Kp = min(s_scal[3], nv - 1);
+        const int inclK = sa[Kp] + sb[Kp] - 1;
+        const int Cc = inclK + Kp + 1;    // children created
+        const int nsize = prev + inclK;   // new size
         if (nsize > NC) { if (tid == 0) atomicOr(&status[f], kStatusNodeOverflow); finish = true; break; }
         // exclusive scan of ne over processing order -> creation ranks / blocks
         const int E_total = block_exscan(sb, Kp + 1, s_tmp);
