@@ -279,10 +279,15 @@ __device__ void build_octave_runs(const unsigned* skey, const uint16_t* colstart
 constexpr int kProjThreads = 1024;      // default workgroup size of k_proj_search
 constexpr int kProjThreadsSmall = 256;  // small-footprint variant (overlapped with other work)
 constexpr int kProjThreadsTiny = 64;    // one wave per problem (a background stream's footprint)
-#ifndef ORBX_TOPK
-#define ORBX_TOPK 8
+constexpr int kTopK = ORBX_TOPK;
+#ifndef ORBX_LANE_TOPK
+#define ORBX_LANE_TOPK 6
 #endif
-constexpr int kTopK = ORBX_TOPK;           // candidate-list length per query
+// candidates each scoring lane keeps before the group merge.  A lane that saw more and
+// runs dry truncates the query's list (a re-scoring on the replay's critical path later):
+// 6 measured configs[4] 81.5k frames/s against 77.0k for 4 and 81.0k for 8, configs[1]
+// unchanged (profiles/r02_n_lane_topk_ab.log)
+constexpr int kLaneTopK = ORBX_LANE_TOPK;           // candidate-list length per query
 static_assert(kTopK % 4 == 0, "lists are stored as uint4s");
 constexpr int kListVec = kTopK / 4;        // uint4s per stored list
 constexpr int kListWords = kTopK / 2;      // u64 words per stored list
@@ -351,8 +356,8 @@ __device__ __forceinline__ QueryReg bcast_query(const QueryReg& x, int src) {
 // against the current claims sfmp, as entries (kNoEntry = no more candidates, kTrunc =
 // more candidates exist than listed).  One 16-lane row per query, four queries per wave:
 // the row's lanes split the columns of the query's cell window (and the sorted-position
-// runs inside them), keep a local top-4 of (distance << 13 | position) and merge them by
-// DPP row minima.  A lane that saw more than 4 candidates only knows its 4 best, so the
+// runs inside them), keep a local top-kLaneTopK of (distance << 13 | position) and merge
+// them by DPP row minima.  A lane that saw more candidates only knows its best ones, so the
 // merged list is exact up to the point where such a lane runs dry; the rest is kTrunc.
 // The candidate windows hold a few to a few tens of keypoints, so a row keeps its lanes
 // busy where a whole wave per query would mostly idle.  `valid` false: no query in this
@@ -365,7 +370,10 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
     static_assert(K == 8 || K == 16 || K == 64, "half a DPP row, a DPP row or a wave");
     const int r = threadIdx.x & (K - 1);
     const ProjQuery& Q = QR.q;
-    unsigned k[4] = {kNoEntry, kNoEntry, kNoEntry, kNoEntry};
+    constexpr int KL = kLaneTopK;
+    unsigned k[KL];
+#pragma unroll
+    for (int i = 0; i < KL; i++) k[i] = kNoEntry;
     int seen = 0;
     if (valid) {
         const CellRange cr = cell_range(pb, Q.u, Q.v, Q.r);
@@ -440,15 +448,10 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
                         }
                         const unsigned key = ((unsigned)d << 13) | (unsigned)p;
                         seen++;
-                        if (key < k[3]) {
-                            if (key < k[2]) {
-                                k[3] = k[2];
-                                if (key < k[1]) {
-                                    k[2] = k[1];
-                                    if (key < k[0]) { k[1] = k[0]; k[0] = key; }
-                                    else k[1] = key;
-                                } else k[2] = key;
-                            } else k[3] = key;
+                        if (key < k[KL - 1]) {  // sorted insert, top down (reads k[i-1] first)
+#pragma unroll
+                            for (int i = KL - 1; i > 0; i--) k[i] = key < k[i - 1] ? k[i - 1] : (key < k[i] ? key : k[i]);
+                            k[0] = key < k[0] ? key : k[0];
                         }
                     }
                 }
@@ -458,7 +461,7 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
     // Group top-kTopK: keys are unique (distinct positions), so one lane pops each minimum.
     const int rsh = K == 64 ? 0 : (threadIdx.x & (63 & ~(K - 1)));  // first lane of this group
     const unsigned long long gmask = K == 64 ? ~0ull : ((1ull << K) - 1);
-    bool over = seen > 4;
+    bool over = seen > KL;
     bool trunc = false;
     unsigned m[kTopK];
 #pragma unroll
@@ -474,10 +477,9 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
                                (unsigned)__builtin_amdgcn_readlane((int)m[j], 48)));
         }
         if (k[0] == m[j] && m[j] != kNoEntry) {
-            k[0] = k[1];
-            k[1] = k[2];
-            k[2] = k[3];
-            k[3] = kNoEntry;
+#pragma unroll
+            for (int i = 0; i < KL - 1; i++) k[i] = k[i + 1];
+            k[KL - 1] = kNoEntry;
         }
         if (trunc) m[j] = kTrunc;
     }
@@ -1064,6 +1066,12 @@ __global__ __launch_bounds__(64) void k_seq_commit(const ProjProblem* __restrict
                                                    const long long* __restrict__ scratch_off, int use_sdesc) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_hist[kHistoLength];
+#ifndef ORBX_NO_REPLAY_PRIO
+    // the replay is one latency-bound wave per problem that shares its CU with the
+    // extraction's throughput waves: the highest wave priority makes the SIMD's arbiter
+    // issue its instructions first
+    __builtin_amdgcn_s_setprio(3);
+#endif
     const ProjProblem pb = probs[blockIdx.x];
     const SeqGridLayout gl(cap, P.noct);
     SortedGrid G = seq_grid(grids + (size_t)blockIdx.x * gl.total, gl, P.noct);

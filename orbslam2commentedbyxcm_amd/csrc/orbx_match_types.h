@@ -42,7 +42,11 @@ struct ProjProblem {
 };
 
 // Global scratch per query (u64 words) when the per-query state does not fit in LDS.
-constexpr int kProjScratchWords = 6;  // 8-entry candidate list (32 B) + mp, angle, match list, bin
+#ifndef ORBX_TOPK
+#define ORBX_TOPK 8  // candidate-list length per query (build constant, a multiple of 4)
+#endif
+// the candidate list (ORBX_TOPK u32) + mp, angle, match list, bin
+constexpr int kProjScratchWords = ORBX_TOPK / 2 + 2;
 
 constexpr int kStampWords = 16;  // ProjParams::stamps words per problem
 
