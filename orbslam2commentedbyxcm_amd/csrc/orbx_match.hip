@@ -597,7 +597,7 @@ struct ProjLds {
 };
 
 // Wave 0's sequential replay (H5) of one problem over the per-query candidate lists qk
-// (8 entries per query) built by the scoring phase: every query takes the first still
+// (kTopK entries per query) built by the scoring phase: every query takes the first still
 // unclaimed entries of its list, the queries of a 64-query chunk before the first one an
 // earlier query of the chunk touches commit together, a query whose list ran out is
 // re-scored against the current claims; then the rotation histogram (ORBmatcher.cc:
@@ -982,7 +982,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
 //                 grid order (the SortedGrid, here in global memory, with the sorted
 //                 descriptors and angles);
 //   k_seq_score   16 queries per workgroup over all problems (XCD-aware: a problem's
-//                 workgroups share one L2 with its grid): each query's 8-entry list;
+//                 workgroups share one L2 with its grid): each query's kTopK-entry list;
 //   k_seq_commit  one wave per problem: the replay (proj_replay) with the claims in LDS.
 // Results are identical to k_proj_search's (same lists, same replay).
 

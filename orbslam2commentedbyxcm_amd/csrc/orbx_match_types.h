@@ -43,7 +43,11 @@ struct ProjProblem {
 
 // Global scratch per query (u64 words) when the per-query state does not fit in LDS.
 #ifndef ORBX_TOPK
-#define ORBX_TOPK 8  // candidate-list length per query (build constant, a multiple of 4)
+// candidate-list length per query (build constant, a multiple of 4).  12 measured
+// configs[4] 86.6k frames/s against 81.5k for 8 and 85.0k for 16 (a list that runs out
+// is re-scored on the replay's critical path), configs[1] within noise
+// (profiles/r02_n_topk_ab.log)
+#define ORBX_TOPK 12
 #endif
 // the candidate list (ORBX_TOPK u32) + mp, angle, match list, bin
 constexpr int kProjScratchWords = ORBX_TOPK / 2 + 2;
