@@ -764,6 +764,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
                                max(max(p[1], p[kFcStride - 1]), max(p[kFcStride], p[kFcStride + 1])));
             return M > nb;  // M > tc >= 1, so M >= 2
         };
+        // the first kFcKeep x 64 candidates' outcomes at both thresholds are kept as
+        // wave masks, so the write pass below re-tests only candidates past them
+        constexpr int kFcKeep = 4;
+        unsigned long long mi[kFcKeep], mm[kFcKeep];
         int cnt_i = 0, cnt_m = 0;
         for (int i0 = 0; i0 < n; i0 += 64) {
             bool ki = false, km = false;
@@ -773,8 +777,12 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
                 ki = lm && M > ti;
                 km = lm && M > tm;
             }
-            cnt_i += __popcll(__ballot(ki));
-            cnt_m += __popcll(__ballot(km));
+            const unsigned long long bi = __ballot(ki), bm = __ballot(km);
+#pragma unroll
+            for (int u = 0; u < kFcKeep; u++)
+                if (i0 == 64 * u) { mi[u] = bi; mm[u] = bm; }
+            cnt_i += __popcll(bi);
+            cnt_m += __popcll(bm);
         }
         const bool use_ini = cnt_i > 0;
         count = use_ini ? cnt_i : cnt_m;
@@ -785,7 +793,21 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
             for (int i0 = 0; i0 < n; i0 += 64) {
                 bool keep = false;
                 int r = 0, cc = 0, M = 0;
-                if (i0 + lane < n) keep = keep_of(i0 + lane, r, cc, M) && M > t;
+                if (i0 < 64 * kFcKeep) {
+                    unsigned long long km = 0;
+#pragma unroll
+                    for (int u = 0; u < kFcKeep; u++)
+                        if (i0 == 64 * u) km = use_ini ? mi[u] : mm[u];
+                    keep = (km >> lane) & 1ull;
+                    if (keep) {
+                        const int rc = list[i0 + lane];
+                        r = rc >> 8;
+                        cc = rc & 255;
+                        M = m[(r + 1) * kFcStride + cc + 1];
+                    }
+                } else if (i0 + lane < n) {
+                    keep = keep_of(i0 + lane, r, cc, M) && M > t;
+                }
                 const unsigned long long b = __ballot(keep);
                 if (keep) {
                     const int xr = c.x0 + 3 + cc - kMinBorder;  // relative to minBorderX
