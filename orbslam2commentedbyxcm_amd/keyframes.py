@@ -222,6 +222,10 @@ class StereoKeyFramePipeline:
         from .extractor import stream_create
         self._own_ms = stream_create(device, 1)
         self.ms = torch.cuda.ExternalStream(self._own_ms, device=self.dev)
+        # SearchForTriangulation on a stream of its own: the triangulation of step j runs
+        # beside the stereo matching and BoW of step j + 1 instead of after them
+        self._own_ts = stream_create(device, 1)
+        self.ts = torch.cuda.ExternalStream(self._own_ts, device=self.dev)
         self.sets = [(ORBextractor(*prm, device=device), ORBextractor(*prm, device=device)) for _ in range(2)]
         self.sf = self.sets[0][0].GetScaleFactors()
         self.cap = self.sets[0][0].max_keypoints(self.W, self.H)
@@ -265,6 +269,7 @@ class StereoKeyFramePipeline:
         self.ev_l = [torch.cuda.Event() for _ in range(2)]
         self.ev_r = [torch.cuda.Event() for _ in range(2)]
         self.ev_m = [torch.cuda.Event() for _ in range(2)]
+        self.ev_s = [torch.cuda.Event() for _ in range(2)]  # stereo + BoW (+ all-gather) of a set done
         self.used = [False, False]
         self.it = 0
         self.last = 0
@@ -278,8 +283,12 @@ class StereoKeyFramePipeline:
 
     def close(self):
         """Release the matcher stream this pipeline created (after synchronising)."""
+        from .extractor import stream_destroy
+        if self._own_ts:
+            self.ts.synchronize()
+            stream_destroy(self._own_ts)
+            self._own_ts = None
         if self._own_ms:
-            from .extractor import stream_destroy
             self.ms.synchronize()
             stream_destroy(self._own_ms)
             self._own_ms = None
@@ -318,10 +327,13 @@ class StereoKeyFramePipeline:
             torch.logical_and(v["u_right"] >= 0, rt["depth"] < self.th_depth, out=v["has_mp"].view(torch.bool))
             if self.world > 1:
                 gather_slabs(self.slabs[k], self.gathered, self.group)
+        self.ev_s[k].record(ms)
+        ts = self.ts
+        ts.wait_event(self.ev_s[k])
         if len(self.plan.pairs):
             self.tri.SearchForTriangulationBatchDevice(self._tabs[k], self.cam, self.plan.pairs, self.plan.F12,
-                                                       self.cap, self.m12, self.tri_pairs, self.tri_n, stream=ms)
-        self.ev_m[k].record(ms)
+                                                       self.cap, self.m12, self.tri_pairs, self.tri_n, stream=ts)
+        self.ev_m[k].record(ts)  # after the stereo, BoW and gather (waited for) and the triangulation
         self.used[k] = True
         self.last = k
         self.it += 1
