@@ -18,13 +18,15 @@ from orbslam2commentedbyxcm_amd.pipeline import SequencePipeline, sequence_poses
 pytestmark = pytest.mark.gpu
 
 
-def _run(B, lanes, pipelined, steps, seed=1000, matcher_mode=None, lane_offset=2, match_after=0):
+def _run(B, lanes, pipelined, steps, seed=1000, matcher_mode=None, lane_offset=2, match_after=0, cu_stride=1,
+         priority=0):
     import torch
 
     frames, off = synth.sequence(seed, B)
     T = sequence_poses(off)
     pl = SequencePipeline(B, 640, 480, lanes=lanes, pipelined=pipelined, matcher_mode=matcher_mode,
-                          lane_offset_stage=lane_offset, match_after_stage=match_after)
+                          lane_offset_stage=lane_offset, match_after_stage=match_after, match_cu_stride=cu_stride,
+                          match_priority=priority)
     d_frames = torch.from_numpy(frames).to(pl.dev)
     d_T = torch.from_numpy(T).to(pl.dev)
     torch.cuda.synchronize()
@@ -53,6 +55,18 @@ def test_sequence_pipeline_matches_oracle(oracle, orbx_built, B, lanes, pipeline
     b1 = pl.bounds[0][1]
     if lanes > 1 and b1 < B:
         assert res["nm"][b1] > 200
+
+
+@pytest.mark.parametrize("cu_stride,priority", [(4, 0), (1, -1)])
+def test_matcher_stream_forms_match_oracle(oracle, orbx_built, cu_stride, priority):
+    """The matcher on a CU-masked stream (orbx_stream_create with cu_stride 4) or on a
+    high-priority one: the same output, and the pipeline releases its stream."""
+    frames, T, pl = _run(24, 2, True, 3, seed=1100, cu_stride=cu_stride, priority=priority)
+    res = pl.host_results()
+    r = checks.check_sequence(frames, T, res, pl.sf)
+    assert r["frames_mismatched"] == 0 and r["pairs_mismatched"] == 0, r
+    pl.close()
+    assert pl._own_ms is None
 
 
 def test_device_status_reports_forced_overflow(oracle, orbx_built):
