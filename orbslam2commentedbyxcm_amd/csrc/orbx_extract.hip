@@ -849,6 +849,40 @@ __device__ int block_exscan(int* a, int n, int* tmp) {
     return total;
 }
 
+// Two in-place exclusive scans (a[0..n), b[0..n), non-negative) in one pass: the same
+// two barriers as one block_exscan.  Totals in ta / tb.  tmp: >= 8 ints.
+__device__ void block_exscan2(int* a, int* b, int n, int* tmp, int& ta, int& tb) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int per = (n + 255) >> 8;
+    const int b0 = min(tid * per, n), b1 = min(b0 + per, n);
+    int sa = 0, sb = 0;
+    for (int i = b0; i < b1; i++) {
+        sa += a[i];
+        sb += b[i];
+    }
+    const int ia = (int)wave_inclusive_sum((uint32_t)sa), ib = (int)wave_inclusive_sum((uint32_t)sb);
+    if (lane == 63) {
+        tmp[wave] = ia;
+        tmp[4 + wave] = ib;
+    }
+    __syncthreads();
+    int ra = ia - sa, rb = ib - sb;
+    for (int k = 0; k < wave; k++) {
+        ra += tmp[k];
+        rb += tmp[4 + k];
+    }
+    ta = tmp[0] + tmp[1] + tmp[2] + tmp[3];
+    tb = tmp[4] + tmp[5] + tmp[6] + tmp[7];
+    for (int i = b0; i < b1; i++) {
+        const int va = a[i], vb = b[i];
+        a[i] = ra;
+        b[i] = rb;
+        ra += va;
+        rb += vb;
+    }
+    __syncthreads();
+}
+
 __device__ __forceinline__ int key_x(uint32_t k) { return (int)(k & 0xfffu); }
 __device__ __forceinline__ int key_y(uint32_t k) { return (int)((k >> 12) & 0xfffu); }
 __device__ __forceinline__ int key_resp(uint32_t k) { return (int)(k >> 24); }
@@ -1133,8 +1167,8 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
         }
         if (g2) atomicAdd(&s_scal[1], g2);
         __syncthreads();
-        const int C = block_exscan(sa, size, s_tmp);
-        const int T = block_exscan(sb, size, s_tmp);
+        int C, T;
+        block_exscan2(sa, sb, size, s_tmp, C, T);
         const int G = s_scal[1];
         const int nsize = C + T;
         if (nsize > NC) { if (tid == 0) atomicOr(&status[f], kStatusNodeOverflow); finish = true; break; }
