@@ -824,10 +824,11 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
 // ------------------------------------------------------------------ block helpers
 
 // In-place exclusive scan of a[0..n) (non-negative) by a 256-thread block; returns the
-// total.  `tmp` holds >= 8 ints of LDS.  All threads must call it.  Each thread sums a
-// contiguous run of ceil(n / 256) entries, one DPP wave scan and one barrier combine the
-// runs, and each thread rewrites its run: two barriers for any n (the octree's node
-// lists reach a few thousand entries).
+// total.  `tmp` holds >= 8 ints of LDS.  All threads must call it, after a barrier that
+// makes every thread's writes to a[] visible: each thread sums a contiguous run of
+// ceil(n / 256) entries (written by other threads), one DPP wave scan and one barrier
+// combine the runs, and each thread rewrites its run: two barriers for any n (the
+// octree's node lists reach a few thousand entries).
 __device__ int block_exscan(int* a, int n, int* tmp) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int per = (n + 255) >> 8;
@@ -1291,8 +1292,8 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
         // the number of r whose sum stays below N (capped at nv - 1): a block scan of
         // ne - 1 (into sa, free now) and a count instead of a one-thread walk.
         if (tid == 0) s_scal[3] = 0;
-        __syncthreads();
-        for (int r = tid; r < nv; r += 256) sa[r] = sb[r] - 1;
+        for (int r = tid; r < nv; r += 256) sa[r] = sb[r] - 1;  // sb[r]: this thread's own entry
+        __syncthreads();  // block_exscan reads contiguous runs, not the strided entries written here
         block_exscan(sa, nv, s_tmp);
         int below = 0;
         for (int r = tid; r < nv; r += 256) below += prev + sa[r] + sb[r] - 1 < N;
