@@ -285,6 +285,36 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
                                const float* scale_factors, int nlevels, float depth, float th,
                                int32_t* d_cur_mp, int32_t* d_nmatches, void* stream);
 
+/* The general form: a sequence of Frames in the orbx_extract_batch_device layout, for
+ * b >= 1 frame b (CurrentFrame) matched against frame b-1 (LastFrame) with
+ * SearchByProjection(CurrentFrame, LastFrame, th, mono) (ORBmatcher.cc:1620-1789),
+ * including the stereo / RGB-D octave ranges for motion along the optical axis
+ * (bForward / bBackward, cc:1650-1701) and the mvuRight check (cc:1722-1729).
+ * LastFrame keypoint i's MapPoint (id i, Observations() > 0) sits at mp_pos
+ * (LastFrame.mvpMapPoints[i]->GetWorldPos()) or, without mp_pos, at `depth` on its
+ * viewing ray; has_mp clears keypoints with no MapPoint or flagged mvbOutlier. */
+typedef struct {
+    int batch;                    /* B frames */
+    const orbx_keypoint* kps;     /* [B][cap] mvKeysUn (device) */
+    const uint8_t* desc;          /* [B][cap][32] mDescriptors */
+    const int32_t* n;             /* [B] keypoint counts */
+    int cap;
+    const float* Tcw;             /* [B][12] mTcw rows 0..2 (device) */
+    const float* u_right;         /* [B][cap] mvuRight (device) or NULL */
+    const float* mp_pos;          /* [B][cap][3] (device) or NULL */
+    const uint8_t* has_mp;        /* [B][cap] (device) or NULL = every keypoint */
+    float depth;                  /* MapPoint depth when mp_pos is NULL */
+    float fx, fy, cx, cy, bf, b;  /* fx, fy, cx, cy, mbf, mb (mb > 0 unless mono) */
+    float min_x, max_x, min_y, max_y;
+    int nlevels;
+    const float* scale_factors;   /* host: mvScaleFactors (nlevels) */
+    float th;
+    int mono;                     /* bMono */
+    int32_t* cur_mp;              /* [B][cap] out: CurrentFrame.mvpMapPoints as LastFrame indices, -1 */
+    int32_t* nmatches;            /* [B] out (frame 0: 0) */
+} orbx_sequence;
+int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* seq, void* stream);
+
 /* ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches)
  * (ORBmatcher.cc:228-392; Tracking::TrackReferenceKeyFrame / Relocalization).
  * kf_mp[i]: MapPoint id of KF keypoint i, -1 for NULL or isBad().  FeatureVectors as

@@ -328,6 +328,38 @@ def sbp_local(F, frame_mp, queries, mps, track, th, nnratio):
                            C.addressof(m), C.addressof(t), th, nnratio)
 
 
+class FrustumTrack:
+    """Frame::IsInFrustum's per-MapPoint outputs (the attributes of matcher.Track)."""
+
+    def __init__(self, n):
+        self.in_view = np.zeros(n, np.uint8)
+        self.proj_x = np.zeros(n, np.float32)
+        self.proj_y = np.zeros(n, np.float32)
+        self.proj_xr = np.zeros(n, np.float32)
+        self.scale_level = np.zeros(n, np.int32)
+        self.view_cos = np.zeros(n, np.float32)
+
+
+def is_in_frustum(F, mps, ids=None, viewing_cos_limit=0.5):
+    """Frame::IsInFrustum(pMP, viewingCosLimit) (Frame.cc:412-477) for MapPoints `ids`
+    (default: all) -> FrustumTrack indexed by MapPoint id."""
+    keep = []
+    f = _frame(F, keep)
+    m = _mappoints(mps, keep)
+    n = len(mps.desc)
+    ids = np.arange(n, dtype=np.int32) if ids is None else np.ascontiguousarray(ids, np.int32)
+    t = FrustumTrack(n)
+    L = lib()
+    L.ora_is_in_frustum.argtypes = [C.c_void_p, C.c_void_p, I32P, C.c_int, C.c_float, U8P, F32P, F32P, F32P, I32P,
+                                    F32P]
+    L.ora_is_in_frustum.restype = None
+    L.ora_is_in_frustum(C.addressof(f), C.addressof(m), ids.ctypes.data_as(I32P), len(ids), float(viewing_cos_limit),
+                        t.in_view.ctypes.data_as(U8P), t.proj_x.ctypes.data_as(F32P), t.proj_y.ctypes.data_as(F32P),
+                        t.proj_xr.ctypes.data_as(F32P), t.scale_level.ctypes.data_as(I32P),
+                        t.view_cos.ctypes.data_as(F32P))
+    return t
+
+
 def sbp_frame(cur, cur_mp, last, last_mp, mps, th, mono, check_ori, last_outlier=None):
     keep = []
     fc = _frame(cur, keep)

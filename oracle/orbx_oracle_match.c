@@ -330,6 +330,53 @@ static float norm3(const float* p) {
     return (float)sqrt(s);
 }
 
+/* ---------------------------------------------------------------- IsInFrustum */
+
+/* Frame::IsInFrustum(pMP, viewingCosLimit), Frame.cc:412-477, for the MapPoint ids
+ * ids[0..n): the Track arrays (indexed by MapPoint id) receive mbTrackInView and, for
+ * points in view, mTrackProjX/Y/XR, mnTrackScaleLevel and mTrackViewCos.  Arithmetic as
+ * the reference writes it: Pc = Rcw*P + tcw (float products left to right),
+ * invz = 1.0f/PcZ in float (Frame.cc:428), the distance bounds 1.2f*mfMaxDistance /
+ * 0.8f*mfMinDistance (MapPoint::GetMax/MinDistanceInvariance), cv::norm and Mat::dot in
+ * double, viewCos = dot/dist in double stored as float, PredictScale(dist, Frame*). */
+void ora_is_in_frustum(const ora_frame* f, const ora_mappoints* mps, const int32_t* ids, int n,
+                       float viewingCosLimit, uint8_t* in_view, float* proj_x, float* proj_y, float* proj_xr,
+                       int32_t* scale_level, float* view_cos) {
+    const float* T = f->Tcw;
+    float Ow[3]; /* mOw = -Rcw^T tcw (Frame::UpdatePoseMatrices) */
+    for (int c = 0; c < 3; c++) Ow[c] = -(T[c] * T[3] + T[4 + c] * T[7] + T[8 + c] * T[11]);
+    for (int k = 0; k < n; k++) {
+        const int mp = ids[k];
+        in_view[mp] = 0;
+        const float* P = mps->pos + 3 * (size_t)mp;
+        float Pc[3];
+        project(T, P, Pc);
+        if (Pc[2] < 0.0f) continue;
+        const float invz = 1.0f / Pc[2];
+        const float u = f->fx * Pc[0] * invz + f->cx;
+        const float v = f->fy * Pc[1] * invz + f->cy;
+        if (u < f->min_x || u > f->max_x) continue;
+        if (v < f->min_y || v > f->max_y) continue;
+        const float maxDistance = 1.2f * mps->max_distance[mp];
+        const float minDistance = 0.8f * mps->min_distance[mp];
+        float PO[3];
+        for (int c = 0; c < 3; c++) PO[c] = P[c] - Ow[c];
+        const float dist = norm3(PO);
+        if (dist < minDistance || dist > maxDistance) continue;
+        const float* Pn = mps->normal + 3 * (size_t)mp;
+        double dot = 0.0;
+        for (int c = 0; c < 3; c++) dot += (double)PO[c] * Pn[c];
+        const float viewCos = (float)(dot / dist);
+        if (viewCos < viewingCosLimit) continue;
+        in_view[mp] = 1;
+        proj_x[mp] = u;
+        proj_xr[mp] = u - f->bf * invz;
+        proj_y[mp] = v;
+        scale_level[mp] = predict_scale(mps->max_distance[mp], dist, f);
+        view_cos[mp] = viewCos;
+    }
+}
+
 /* ---------------------------------------------------------------- a13 */
 
 /* ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>&

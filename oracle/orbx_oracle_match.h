@@ -63,6 +63,9 @@ int ora_features_in_area(const ora_frame* f, const ora_grid* g, float x, float y
 void ora_compute_three_maxima(const int* histo_sizes, int L, int* ind1, int* ind2, int* ind3);
 int ora_sbp_local(const ora_frame* f, int32_t* frame_mp, const int32_t* queries, int nq, const ora_mappoints* mps,
                   const ora_track* trk, float th, float nnratio);
+void ora_is_in_frustum(const ora_frame* f, const ora_mappoints* mps, const int32_t* ids, int n,
+                       float viewingCosLimit, uint8_t* in_view, float* proj_x, float* proj_y, float* proj_xr,
+                       int32_t* scale_level, float* view_cos);
 int ora_sbp_frame(const ora_frame* cur, int32_t* cur_mp, const ora_frame* last, const int32_t* last_mp,
                   const uint8_t* last_outlier, const ora_mappoints* mps, float th, int bMono, int check_ori);
 int ora_sbp_keyframe(const ora_frame* cur, int32_t* cur_mp, const ora_frame* kf, const int32_t* kf_mp,

@@ -48,7 +48,7 @@ EXPORTED = [
     "orbx_fuse", "orbx_fuse_sim3", "orbx_search_by_sim3", "orbx_compute_distinctive_descriptors",
     "orbx_compute_distinctive_descriptors_device", "orbx_extractor_status", "orbx_extractor_status_device",
     "orbx_extractor_set_node_capacity", "orbx_compute_stereo_matches_batch_device",
-    "orbx_search_for_triangulation_batch_device",
+    "orbx_search_for_triangulation_batch_device", "orbx_match_sequence_device_ex",
 ]
 
 
@@ -60,6 +60,17 @@ class Camera(C.Structure):
 class ExtractorParams(C.Structure):
     _fields_ = [("nfeatures", C.c_int), ("scale_factor", C.c_float), ("nlevels", C.c_int),
                 ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int)]
+
+
+class Sequence(C.Structure):
+    """orbx_sequence (include/orbx.h)."""
+    _fields_ = [("batch", C.c_int), ("kps", C.c_void_p), ("desc", C.c_void_p), ("n", C.c_void_p), ("cap", C.c_int),
+                ("Tcw", C.c_void_p), ("u_right", C.c_void_p), ("mp_pos", C.c_void_p), ("has_mp", C.c_void_p),
+                ("depth", C.c_float), ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("bf", C.c_float), ("b", C.c_float), ("min_x", C.c_float), ("max_x", C.c_float),
+                ("min_y", C.c_float), ("max_y", C.c_float), ("nlevels", C.c_int),
+                ("scale_factors", C.POINTER(C.c_float)), ("th", C.c_float), ("mono", C.c_int),
+                ("cur_mp", C.c_void_p), ("nmatches", C.c_void_p)]
 
 
 class OrbxError(RuntimeError):
@@ -134,6 +145,7 @@ def lib() -> C.CDLL:
     L.orbx_match_sequence_device.argtypes = [vp, C.c_int, vp, vp, vp, C.c_int, vp, C.c_float, C.c_float, C.c_float,
                                              C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, fp, C.c_int,
                                              C.c_float, C.c_float, vp, vp, vp]
+    L.orbx_match_sequence_device_ex.argtypes = [vp, C.POINTER(Sequence), vp]
     L.orbx_search_by_projection_keyframe.argtypes = [vp, vp, i32p, vp, i32p, u8p, vp, C.c_float, C.c_int, ip]
     L.orbx_search_by_projection_sim3.argtypes = [vp, vp, fp, i32p, C.c_int, i32p, vp, C.c_int, ip]
     L.orbx_search_by_bow_frame.argtypes = [vp, vp, i32p, i32p, i32p, i32p, C.c_int, vp, i32p, i32p, i32p, C.c_int,

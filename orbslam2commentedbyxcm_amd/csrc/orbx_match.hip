@@ -1138,10 +1138,12 @@ hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjPar
 }
 
 // Batched TrackWithMotionModel matching over a device-resident sequence: problem p
-// matches frame p+1 (CurrentFrame) against frame p (LastFrame).  Every keypoint of
-// the last frame carries a MapPoint at depth `depth` on its viewing ray; projection
-// and query construction follow SearchByProjection(Frame&, const Frame&, th, bMono=true)
-// (ORBmatcher.cc:1644-1701).  One thread per last-frame keypoint slot.
+// matches frame p+1 (CurrentFrame) against frame p (LastFrame).  Keypoint i of the last
+// frame carries MapPoint id i (Observations() > 0) at mp_pos, or, without mp_pos, at
+// depth `depth` on its viewing ray; has_mp masks keypoints without one (or outliers).
+// Projection, the forward / backward octave ranges and query construction follow
+// SearchByProjection(Frame&, const Frame&, th, bMono) (ORBmatcher.cc:1620-1701).  One
+// thread per last-frame keypoint slot.
 __global__ __launch_bounds__(256) void k_seq_build(SeqArgs A, ProjQuery* __restrict__ queries,
                                                    ProjProblem* __restrict__ probs,
                                                    long long* __restrict__ scratch_off) {
@@ -1152,7 +1154,7 @@ __global__ __launch_bounds__(256) void k_seq_build(SeqArgs A, ProjQuery* __restr
         ProjProblem pb{};
         pb.keys = A.kps + (size_t)(p + 1) * A.cap;
         pb.desc = A.desc + (size_t)(p + 1) * A.cap * 32;
-        pb.u_right = nullptr;
+        pb.u_right = A.u_right ? A.u_right + (size_t)(p + 1) * A.cap : nullptr;
         pb.frame_mp = A.cur_mp + (size_t)(p + 1) * A.cap;
         pb.n = A.n[p + 1] < A.cap ? A.n[p + 1] : A.cap;
         pb.q = queries + (size_t)p * A.cap;
@@ -1175,16 +1177,27 @@ __global__ __launch_bounds__(256) void k_seq_build(SeqArgs A, ProjQuery* __restr
     if (p == 0 && i == 0) A.nmatches[0] = 0;
     ProjQuery q{};
     q.mp = -1;
-    if (i < nlast) {
-        const orbx_keypoint kp = A.kps[(size_t)p * A.cap + i];
+    const size_t slot = (size_t)p * A.cap + i;
+    if (i < nlast && !(A.has_mp && !A.has_mp[slot])) {
+        const orbx_keypoint kp = A.kps[slot];
         const float* Tl = A.Tcw + 12 * (size_t)p;
         const float* Tc = A.Tcw + 12 * (size_t)(p + 1);
-        // MapPoint: last-frame camera point on the keypoint ray, to world: Xw = Rl^T (Xc - tl)
-        const float z = A.depth;
-        const float Xc[3] = {(kp.x - A.cx) / A.fx * z, (kp.y - A.cy) / A.fy * z, z};
         float Xw[3];
-        for (int c = 0; c < 3; c++)
-            Xw[c] = Tl[c] * (Xc[0] - Tl[3]) + Tl[4 + c] * (Xc[1] - Tl[7]) + Tl[8 + c] * (Xc[2] - Tl[11]);
+        if (A.mp_pos) {
+            for (int c = 0; c < 3; c++) Xw[c] = A.mp_pos[3 * slot + c];
+        } else {
+            // MapPoint: last-frame camera point on the keypoint ray, to world: Xw = Rl^T (Xc - tl)
+            const float z = A.depth;
+            const float Xc[3] = {(kp.x - A.cx) / A.fx * z, (kp.y - A.cy) / A.fy * z, z};
+            for (int c = 0; c < 3; c++)
+                Xw[c] = Tl[c] * (Xc[0] - Tl[3]) + Tl[4 + c] * (Xc[1] - Tl[7]) + Tl[8 + c] * (Xc[2] - Tl[11]);
+        }
+        // twc = -Rcw^T tcw; tlc = Rlw*twc + tlw (cc:1637-1651), float products left to right
+        float twc[3];
+        for (int c = 0; c < 3; c++) twc[c] = -(Tc[c] * Tc[3] + Tc[4 + c] * Tc[7] + Tc[8 + c] * Tc[11]);
+        const float tlcz = Tl[8] * twc[0] + Tl[9] * twc[1] + Tl[10] * twc[2] + Tl[11];
+        const bool bForward = tlcz > A.b && !A.mono;
+        const bool bBackward = -tlcz > A.b && !A.mono;
         float x3Dc[3];
         for (int r = 0; r < 3; r++)
             x3Dc[r] = Tc[4 * r] * Xw[0] + Tc[4 * r + 1] * Xw[1] + Tc[4 * r + 2] * Xw[2] + Tc[4 * r + 3];
@@ -1198,15 +1211,23 @@ __global__ __launch_bounds__(256) void k_seq_build(SeqArgs A, ProjQuery* __restr
             q.ur = u - A.bf * invzc;
             q.r = A.th * A.scale[o];
             q.er_max = q.r;
-            q.min_level = o - 1;  // bMono: GetFeaturesInArea(u, v, radius, nLastOctave-1, nLastOctave+1)
-            q.max_level = o + 1;
+            if (bForward) {  // GetFeaturesInArea(u, v, radius, nLastOctave)
+                q.min_level = o;
+                q.max_level = -1;
+            } else if (bBackward) {  // (u, v, radius, 0, nLastOctave)
+                q.min_level = 0;
+                q.max_level = o;
+            } else {  // (u, v, radius, nLastOctave-1, nLastOctave+1)
+                q.min_level = o - 1;
+                q.max_level = o + 1;
+            }
             q.post_min = -1;
             q.post_max = -1;
             q.mp = i;
             q.angle = kp.angle;
         }
     }
-    queries[(size_t)p * A.cap + i] = q;
+    queries[slot] = q;
 }
 
 hipError_t launch_seq_build(const SeqArgs& A, int npairs, ProjQuery* queries, ProjProblem* probs,

@@ -74,9 +74,13 @@ struct SeqArgs {
     const int32_t* n;          // [B]
     int cap;
     const float* Tcw;          // [B][12]
-    float fx, fy, cx, cy, bf;
+    const float* u_right;      // [B][cap] mvuRight or null (monocular)
+    const float* mp_pos;       // [B][cap][3] world position of keypoint i's MapPoint, or null: depth model
+    const uint8_t* has_mp;     // [B][cap] LastFrame keypoint has a (non-outlier) MapPoint, or null: all
+    float fx, fy, cx, cy, bf, b;
     float min_x, max_x, min_y, max_y;
-    float depth;               // MapPoint depth along the last frame's rays
+    float depth;               // depth model: MapPoint depth along the last frame's rays
+    int mono;                  // bMono
     float th;                  // search radius factor
     float scale[32];           // mvScaleFactors
     int32_t* cur_mp;           // [B][cap] out (pre-filled -1)

@@ -561,16 +561,49 @@ int orbx_search_by_projection_sim3(orbx_matcher* m, const orbx_frame_view* kf, c
     return run_proj(m, kf, matched, qs, qd, mps, P, nmatches);
 }
 
-// Batched SearchByProjection(CurrentFrame, LastFrame, th, bMono=true) over a device
+// Batched SearchByProjection(CurrentFrame, LastFrame, th, bMono) over a device
 // sequence written by orbx_extract_batch_device (see include/orbx.h).
 int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* d_kps, const uint8_t* d_desc,
                                const int32_t* d_n, int cap, const float* d_Tcw, float fx, float fy, float cx,
                                float cy, float min_x, float max_x, float min_y, float max_y,
                                const float* scale_factors, int nlevels, float depth, float th, int32_t* d_cur_mp,
                                int32_t* d_nmatches, void* stream) {
-    if (!m || batch < 0 || cap <= 0 || !scale_factors || nlevels < 1 || nlevels > 32) return fail(ORBX_ERR_ARG, "bad argument");
+    orbx_sequence q{};
+    q.batch = batch;
+    q.kps = d_kps;
+    q.desc = d_desc;
+    q.n = d_n;
+    q.cap = cap;
+    q.Tcw = d_Tcw;
+    q.depth = depth;
+    q.fx = fx;
+    q.fy = fy;
+    q.cx = cx;
+    q.cy = cy;
+    q.min_x = min_x;
+    q.max_x = max_x;
+    q.min_y = min_y;
+    q.max_y = max_y;
+    q.nlevels = nlevels;
+    q.scale_factors = scale_factors;
+    q.th = th;
+    q.mono = 1;
+    q.cur_mp = d_cur_mp;
+    q.nmatches = d_nmatches;
+    return orbx_match_sequence_device_ex(m, &q, stream);
+}
+
+int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void* stream) {
+    if (!m || !sq) return fail(ORBX_ERR_ARG, "null argument");
+    const int batch = sq->batch, cap = sq->cap, nlevels = sq->nlevels;
+    if (batch < 0 || cap <= 0 || !sq->scale_factors || nlevels < 1 || nlevels > 32)
+        return fail(ORBX_ERR_ARG, "bad argument");
     if (batch == 0) return ORBX_OK;
-    if (!d_kps || !d_desc || !d_n || !d_Tcw || !d_cur_mp || !d_nmatches) return fail(ORBX_ERR_ARG, "null buffer");
+    if (!sq->kps || !sq->desc || !sq->n || !sq->Tcw || !sq->cur_mp || !sq->nmatches)
+        return fail(ORBX_ERR_ARG, "null buffer");
+    if (!sq->mono && !(sq->b > 0.f)) return fail(ORBX_ERR_ARG, "stereo / RGB-D sequence needs the baseline mb > 0");
+    int32_t* d_cur_mp = sq->cur_mp;
+    int32_t* d_nmatches = sq->nmatches;
     HIP_TRY(hipSetDevice(m->device));
     hipStream_t s = stream ? (hipStream_t)stream : m->stream;
     const int npairs = batch - 1;
@@ -596,23 +629,28 @@ int orbx_match_sequence_device(orbx_matcher* m, int batch, const orbx_keypoint* 
         return ORBX_OK;
     }
     SeqArgs A{};
-    A.kps = d_kps;
-    A.desc = d_desc;
-    A.n = d_n;
+    A.kps = sq->kps;
+    A.desc = sq->desc;
+    A.n = sq->n;
     A.cap = cap;
-    A.Tcw = d_Tcw;
-    A.fx = fx;
-    A.fy = fy;
-    A.cx = cx;
-    A.cy = cy;
-    A.bf = 0.f;
-    A.min_x = min_x;
-    A.max_x = max_x;
-    A.min_y = min_y;
-    A.max_y = max_y;
-    A.depth = depth;
-    A.th = th;
-    for (int l = 0; l < nlevels; l++) A.scale[l] = scale_factors[l];
+    A.Tcw = sq->Tcw;
+    A.u_right = sq->u_right;
+    A.mp_pos = sq->mp_pos;
+    A.has_mp = sq->has_mp;
+    A.fx = sq->fx;
+    A.fy = sq->fy;
+    A.cx = sq->cx;
+    A.cy = sq->cy;
+    A.bf = sq->bf;
+    A.b = sq->b;
+    A.min_x = sq->min_x;
+    A.max_x = sq->max_x;
+    A.min_y = sq->min_y;
+    A.max_y = sq->max_y;
+    A.depth = sq->depth;
+    A.mono = sq->mono ? 1 : 0;
+    A.th = sq->th;
+    for (int l = 0; l < nlevels; l++) A.scale[l] = sq->scale_factors[l];
     A.cur_mp = d_cur_mp;
     A.nmatches = d_nmatches;
     hipEvent_t* ev = m->ev[m->ncalls % orbx_matcher::kRing];

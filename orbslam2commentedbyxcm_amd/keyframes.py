@@ -20,7 +20,11 @@ One step on every rank = for its B stereo keyframes of a W*B-keyframe window:
    pair in one launch (orbx_search_for_triangulation_batch_device), ORBmatcher(0.6, false).
 
 Step k+1's extraction overlaps step k's stereo / BoW / gather / triangulation: two
-extractor pairs and two slabs alternate.  The neighbour plan (covisibility proxy: the nn
+extractor pairs, two slabs, two gathered buffers and two sets of triangulation outputs
+alternate, and a set is reused only after the triangulation that last read it (its
+event) -- so the gather of step k+1 never overwrites neighbours that step k's
+triangulation is still reading.  `windows` > 1 gives each step its own keyframe window
+(same poses, another texture), so a cross-step ordering fault changes bytes.  The neighbour plan (covisibility proxy: the nn
 keyframes whose views overlap most, then the baseline skip) depends only on the poses and
 is made once on the host, as LocalMapping does per keyframe.
 
@@ -191,7 +195,8 @@ class StereoKeyFramePipeline:
     """Device-resident configs[3] step for one rank (see the module docstring)."""
 
     def __init__(self, batch: int, rank: int = 0, world: int = 1, device: int = 0, nn: int = 10, seq_seed: int = 3,
-                 vocab_text: bytes | None = None, settings: dict | None = None, group=None):
+                 vocab_text: bytes | None = None, settings: dict | None = None, group=None, windows: int = 1,
+                 on_step_done=None):
         import torch
 
         from . import synth
@@ -210,11 +215,15 @@ class StereoKeyFramePipeline:
         N = self.world * self.B
         # keyframes ~13 px apart on average (a stereo baseline at this depth), so about half
         # of the g +- 1 neighbours fail LocalMapping's baseline test and the rest pass
-        self.seq = synth.StereoSequence(seq_seed, N, self.W, self.H, step=16, margin=256, disp=disp)
+        # window w: the same walk (poses, neighbour plan) over its own texture
+        self.seqs = [synth.StereoSequence(seq_seed, N, self.W, self.H, step=16, margin=256, disp=disp,
+                                          canvas_seed=seq_seed + 1000 * w if w else None)
+                     for w in range(max(1, int(windows)))]
+        self.seq = self.seqs[0]
         self.poses = stream_poses(self.seq.off, s["fx"], s["fy"], self.depth)
         self.local = [window_index(self.rank, i, self.world) for i in range(self.B)]
-        left, right = self.seq.views(self.local)
-        self.left_np, self.right_np = left, right
+        views = [sq.views(self.local) for sq in self.seqs]
+        self.left_np, self.right_np = views[0]
         prm = (s["nfeatures"], s["scale"], s["nlevels"], s["ini_th"], s["min_th"])
         # the matcher stream first: HIP assigns hardware queues in stream-creation order, and
         # a stream created after the extractors' (or from torch's pool) can share one with
@@ -250,12 +259,15 @@ class StereoKeyFramePipeline:
         self.bow = [{"bow_word": torch.empty((self.B, self.cap), **i32),
                      "bow_value": torch.empty((self.B, self.cap), dtype=torch.float64, device=self.dev),
                      "nbow": torch.empty((self.B,), **i32)} for _ in range(2)]
-        self.gathered = torch.zeros(self.world * self.lay.nbytes, **u8) if self.world > 1 else None
+        # one gathered buffer per set: step j+1's all-gather (set k') must not overwrite the
+        # neighbours step j's triangulation (set k) is reading on the other stream
+        self.gathered = [torch.zeros(self.world * self.lay.nbytes, **u8) for _ in range(2)] \
+            if self.world > 1 else None
         self.plan = plan_neighbours(self.poses, self.rank, self.world, self.B, nn, self.mb, s)
         P = max(len(self.plan.pairs), 1)
-        self.m12 = torch.empty((P, self.cap), **i32)
-        self.tri_pairs = torch.empty((P, self.cap, 2), **i32)
-        self.tri_n = torch.empty((P,), **i32)
+        self.m12 = [torch.empty((P, self.cap), **i32) for _ in range(2)]
+        self.tri_pairs = [torch.empty((P, self.cap, 2), **i32) for _ in range(2)]
+        self.tri_n = [torch.empty((P,), **i32) for _ in range(2)]
         win_poses = [None] * (self.world * self.B)
         for g in range(self.world * self.B):
             win_poses[record_index(g, self.world, self.B)] = self.poses[g]
@@ -271,14 +283,19 @@ class StereoKeyFramePipeline:
         self.ev_m = [torch.cuda.Event() for _ in range(2)]
         self.ev_s = [torch.cuda.Event() for _ in range(2)]  # stereo + BoW (+ all-gather) of a set done
         self.used = [False, False]
+        self.window_of = [0, 0]  # the window each set last held
+        # on_step_done(k): called after a step's triangulation is enqueued on self.ts and
+        # before the event that releases set k -- consumer work enqueued on self.ts there
+        # (e.g. copying the results out) finishes before the set is reused
+        self.on_step_done = on_step_done
         self.it = 0
         self.last = 0
-        self.d_left = torch.from_numpy(left).to(self.dev)
-        self.d_right = torch.from_numpy(right).to(self.dev)
+        self.inputs = [(torch.from_numpy(lf).to(self.dev), torch.from_numpy(rg).to(self.dev)) for lf, rg in views]
+        self.d_left, self.d_right = self.inputs[0]
         torch.cuda.synchronize(self.dev)
         # the keyframe tables are fixed per buffer: build the ctypes arrays once
         from .matcher import keyframe_table
-        bufs = [self.gathered] * 2 if self.world > 1 else self.slabs
+        bufs = self.gathered if self.world > 1 else self.slabs
         self._tabs = [keyframe_table(self.lay.records(b.data_ptr(), self.world, self._rec_poses)) for b in bufs]
 
     def close(self):
@@ -306,11 +323,14 @@ class StereoKeyFramePipeline:
         k = self.it % 2
         (exl, exr), (sl, sr) = self.sets[k], self.streams[k]
         v, rt, bw = self.sv[k], self.right[k], self.bow[k]
-        if self.used[k]:  # the work that last read this set's pyramids and slab is done
+        if self.used[k]:  # the work that last read this set's pyramids, slab and gathered buffer is done
             sl.wait_event(self.ev_m[k])
             sr.wait_event(self.ev_m[k])
-        exl.extract_batch_device(self.d_left, v["kps"], v["desc"], v["n"])
-        exr.extract_batch_device(self.d_right, rt["kps"], rt["desc"], rt["n"])
+        w = self.it % len(self.inputs)
+        self.window_of[k] = w
+        d_left, d_right = self.inputs[w]
+        exl.extract_batch_device(d_left, v["kps"], v["desc"], v["n"])
+        exr.extract_batch_device(d_right, rt["kps"], rt["desc"], rt["n"])
         self.ev_l[k].record(sl)
         self.ev_r[k].record(sr)
         ms = self.ms
@@ -326,13 +346,16 @@ class StereoKeyFramePipeline:
             # Tracking::CreateNewKeyFrame: a MapPoint for every stereo point closer than mThDepth
             torch.logical_and(v["u_right"] >= 0, rt["depth"] < self.th_depth, out=v["has_mp"].view(torch.bool))
             if self.world > 1:
-                gather_slabs(self.slabs[k], self.gathered, self.group)
+                gather_slabs(self.slabs[k], self.gathered[k], self.group)
         self.ev_s[k].record(ms)
         ts = self.ts
         ts.wait_event(self.ev_s[k])
         if len(self.plan.pairs):
             self.tri.SearchForTriangulationBatchDevice(self._tabs[k], self.cam, self.plan.pairs, self.plan.F12,
-                                                       self.cap, self.m12, self.tri_pairs, self.tri_n, stream=ts)
+                                                       self.cap, self.m12[k], self.tri_pairs[k], self.tri_n[k],
+                                                       stream=ts)
+        if self.on_step_done is not None:
+            self.on_step_done(k)
         self.ev_m[k].record(ts)  # after the stereo, BoW and gather (waited for) and the triangulation
         self.used[k] = True
         self.last = k
@@ -354,27 +377,35 @@ class StereoKeyFramePipeline:
             st["triangulation"] = self.tri.last_ms()
         return st
 
-    def host_results(self) -> dict:
-        """Host copies of the newest step's outputs (call after synchronising)."""
-        from . import _lib as L
-
-        k = self.last
+    def results(self, k=None) -> dict:
+        """Device tensors of set k (default: the newest step's): every field the step
+        writes, the triangulation outputs and (world > 1) the gathered buffer."""
+        k = self.last if k is None else k
         v, rt = self.sv[k], self.right[k]
+        P = len(self.plan.pairs)
+        r = {"kps": v["kps"], "dl": v["desc"], "nl": v["n"], "kr": rt["kps"], "dr": rt["desc"], "nr": rt["n"],
+             "ur": v["u_right"], "depth": rt["depth"], "has_mp": v["has_mp"], "fv_node": v["fv_node"],
+             "fv_off": v["fv_off"], "fv_idx": v["fv_idx"], "nfv": v["nfv"], "tri_n": self.tri_n[k][:P],
+             "tri_pairs": self.tri_pairs[k][:P]}
+        if self.world > 1:
+            r["gathered"] = self.gathered[k]
+        return r
+
+    def to_host(self, r: dict) -> dict:
+        """Host form of results() (or of clones of it)."""
+        from . import _lib as L
         B, cap = self.B, self.cap
 
         def kp(t):
             return t.cpu().numpy().view(np.uint8).reshape(B, cap, KP_BYTES).view(L.KEYPOINT_DTYPE).reshape(B, cap)
 
-        r = {"kl": kp(v["kps"]), "dl": v["desc"].cpu().numpy(), "nl": v["n"].cpu().numpy(),
-             "kr": kp(rt["kps"]), "dr": rt["desc"].cpu().numpy(), "nr": rt["n"].cpu().numpy(),
-             "ur": v["u_right"].cpu().numpy(), "depth": rt["depth"].cpu().numpy(),
-             "has_mp": v["has_mp"].cpu().numpy(), "fv_node": v["fv_node"].cpu().numpy(),
-             "fv_off": v["fv_off"].cpu().numpy(), "fv_idx": v["fv_idx"].cpu().numpy(),
-             "nfv": v["nfv"].cpu().numpy(), "tri_n": self.tri_n.cpu().numpy()[:len(self.plan.pairs)],
-             "tri_pairs": self.tri_pairs.cpu().numpy()[:len(self.plan.pairs)]}
-        if self.world > 1:
-            r["gathered"] = self.gathered.cpu().numpy()
-        return r
+        out = {name: t.cpu().numpy() for name, t in r.items() if name not in ("kps", "kr")}
+        out["kl"], out["kr"] = kp(r["kps"]), kp(r["kr"])
+        return out
+
+    def host_results(self) -> dict:
+        """Host copies of the newest step's outputs (call after synchronising)."""
+        return self.to_host(self.results())
 
     def status(self) -> bool:
         """True if every extraction of the newest step completed its octree."""

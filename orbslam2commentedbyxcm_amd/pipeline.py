@@ -33,7 +33,7 @@ class SequencePipeline:
                  nnratio: float = 0.9, check_ori: bool = True, match_stream=None,
                  nbuf: int = 2, matcher_mode: int | None = None, match_after_stage: int = 0,
                  lane_offset_stage: int = 2, match_cu_stride: int = 1,
-                 match_priority: int = 0):
+                 match_priority: int = 0, on_matched=None):
         import torch
 
         self.B, self.W, self.H = int(batch), int(width), int(height)
@@ -82,6 +82,7 @@ class SequencePipeline:
         self.ev_ex = [[torch.cuda.Event() for _ in range(self.S)] for _ in range(nbuf)]  # [buffer][lane]
         self.ev_m = [torch.cuda.Event() for _ in range(nbuf)]
         self.used = [False] * nbuf
+        self.T_of = [None] * nbuf  # the poses of the batch extracted into each buffer
         # match_after_stage k (pipelined only): the matching of batch j-1 also waits until
         # every lane's extraction of batch j has passed stage k (1 pyramid, 2 blur + FAST
         # strength, 3 FAST cells, 4 octree), so it runs beside the later stages
@@ -94,6 +95,11 @@ class SequencePipeline:
         # alone 216.5k against 210.8k (profiles/r02_l_lane_offset_ab.log)
         self.lane_ev = [e.set_stage_event(lane_offset_stage) for e in self.exs] \
             if (lane_offset_stage and not match_after_stage and self.S > 1) else None
+        # on_matched(b): called right after a batch's matching is enqueued on self.ms and
+        # before the event that releases its buffer b for reuse -- work the consumer
+        # enqueues on self.ms there (e.g. copying the results out) finishes before the
+        # buffer is overwritten
+        self.on_matched = on_matched
         self.it = 0            # extractions issued
         self.pending = None    # buffer extracted but not yet matched (pipelined)
         self.last = None       # buffer holding the newest complete result
@@ -113,7 +119,8 @@ class SequencePipeline:
             pass
 
     # -- launches -----------------------------------------------------------------
-    def _extract(self, frames, b):
+    def _extract(self, frames, Tcw, b):
+        self.T_of[b] = Tcw
         for c in range(self.S):
             b0, b1 = self.bounds[c]
             if self.used[b] and self.match:
@@ -126,7 +133,8 @@ class SequencePipeline:
             self.ev_ex[b][c].record(self.streams[c])
         self.used[b] = True
 
-    def _match(self, b, Tcw, after_next=False):
+    def _match(self, b, after_next=False):
+        Tcw = self.T_of[b]
         for c in range(self.S):
             self.ms.wait_event(self.ev_ex[b][c])
         if after_next and self.stage_ev:
@@ -136,30 +144,33 @@ class SequencePipeline:
         self.matcher.match_sequence_device(self.kps[b], self.desc[b], self.n[b], Tcw, self.mp[b], self.nm[b],
                                            self.sf, self.fx, self.fy, self.cx, self.cy, self.W, self.H,
                                            depth=self.depth, th=self.th, stream=self.ms.cuda_stream)
+        if self.on_matched is not None:
+            self.on_matched(b)
         self.ev_m[b].record(self.ms)
 
     def step(self, frames, Tcw):
         """Issue one step (asynchronous).  Pipelined: extracts this batch and matches the
-        previous one; call drain() after the last step."""
+        previous one (with the poses passed alongside that batch); call drain() after the
+        last step.  `frames` and `Tcw` must stay untouched until the batch is matched."""
         nbuf = len(self.kps)
         b = self.it % nbuf
-        self._extract(frames, b)
+        self._extract(frames, Tcw, b)
         self.it += 1
         if not self.match:
             self.last = b
             return
         if self.pipelined:
             if self.pending is not None:
-                self._match(self.pending, Tcw, after_next=True)
+                self._match(self.pending, after_next=True)
                 self.last = self.pending
             self.pending = b
         else:
-            self._match(b, Tcw)
+            self._match(b)
             self.last = b
 
-    def drain(self, Tcw):
+    def drain(self, Tcw=None):
         if self.pipelined and self.pending is not None:
-            self._match(self.pending, Tcw)
+            self._match(self.pending)
             self.last = self.pending
             self.pending = None
 
@@ -170,13 +181,14 @@ class SequencePipeline:
         self.drain(Tcw)
 
     # -- results ------------------------------------------------------------------
-    def results(self) -> dict:
-        """Device tensors of the newest complete batch (call after synchronising)."""
-        b = self.last
+    def results(self, b=None) -> dict:
+        """Device tensors of the newest complete batch, or of buffer b (call after
+        synchronising, or after ev_m[b] for a buffer whose matching was issued)."""
+        b = self.last if b is None else b
         return {"kps": self.kps[b], "desc": self.desc[b], "n": self.n[b], "mp": self.mp[b], "nm": self.nm[b]}
 
-    def host_results(self) -> dict:
-        r = self.results()
+    def host_results(self, b=None) -> dict:
+        r = self.results(b)
         B, cap = self.B, self.cap
         from . import _lib as L
         return {"kps": r["kps"].cpu().numpy().view(np.uint8).reshape(B, cap, 28).view(L.KEYPOINT_DTYPE).reshape(B, cap),

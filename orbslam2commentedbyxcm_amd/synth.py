@@ -112,6 +112,79 @@ def sequence(seed: int, n: int, width: int = 640, height: int = 480, step: int =
     return out, off
 
 
+def plane_views(seed: int, rel_poses, width: int = 640, height: int = 480, fx: float = 500.0, fy: float = 500.0,
+                cx: float = 320.0, cy: float = 240.0, z0: float = 5.0):
+    """Views of one textured plane under general camera motion (rotation about any axis,
+    motion along the optical axis).
+
+    The plane is Z = z0 in the frame of a reference camera that sees the canvas' central
+    width x height crop pixel for pixel.  rel_poses[k] is camera k's pose relative to that
+    camera (4x4, X_k = R X_ref + t).  Pixel (u, v) of camera k is the ray from its centre
+    C = -R^T t along R^T K^-1 (u, v, 1); where it meets the plane, (X, Y, z0), it reads the
+    canvas at (fx X / z0 + cx, fy Y / z0 + cy) + margin, bilinearly (float64, rounded).
+    The canvas is sized so that every view fits inside it.
+
+    Returns (views (n, h, w) u8, depths (n, h, w) f32), depths being each pixel's Z in its
+    own camera (the ray parameter, as K^-1 (u, v, 1) has unit z)."""
+    Kinv = np.array([[1 / fx, 0, -cx / fx], [0, 1 / fy, -cy / fy], [0, 0, 1]], np.float64)
+    vv, uu = np.mgrid[0:height, 0:width].astype(np.float64)
+    rays = np.stack([uu, vv, np.ones_like(uu)], -1) @ Kinv.T          # (h, w, 3), unit z
+    hits = []
+    for T in rel_poses:
+        T = np.asarray(T, np.float64)
+        R, t = T[:3, :3], T[:3, 3]
+        C = -R.T @ t
+        a = rays @ R                                                  # R^T ray, per pixel
+        if (a[..., 2] <= 0).any():
+            raise ValueError("a view looks away from the plane")
+        s = (z0 - C[2]) / a[..., 2]
+        if (s <= 0).any():
+            raise ValueError("the plane is behind a camera")
+        X = C[None, None, :] + s[..., None] * a
+        hits.append((fx * X[..., 0] / z0 + cx, fy * X[..., 1] / z0 + cy, s))
+    lo_x = min(float(h[0].min()) for h in hits)
+    hi_x = max(float(h[0].max()) for h in hits)
+    lo_y = min(float(h[1].min()) for h in hits)
+    hi_y = max(float(h[1].max()) for h in hits)
+    mx = int(np.ceil(max(0.0, -lo_x, hi_x - (width - 1)))) + 2
+    my = int(np.ceil(max(0.0, -lo_y, hi_y - (height - 1)))) + 2
+    W, H = width + 2 * mx, height + 2 * my
+    canvas = frame(seed, W, H, n_shapes=int(200 * W * H / (640 * 480))).astype(np.float64)
+    views = np.empty((len(hits), height, width), np.uint8)
+    depths = np.empty((len(hits), height, width), np.float32)
+    for k, (px, py, s) in enumerate(hits):
+        px = px + mx
+        py = py + my
+        x0 = np.clip(np.floor(px).astype(np.int64), 0, W - 2)
+        y0 = np.clip(np.floor(py).astype(np.int64), 0, H - 2)
+        ax = np.clip(px - x0, 0.0, 1.0)
+        ay = np.clip(py - y0, 0.0, 1.0)
+        v = ((1 - ax) * (1 - ay) * canvas[y0, x0] + ax * (1 - ay) * canvas[y0, x0 + 1]
+             + (1 - ax) * ay * canvas[y0 + 1, x0] + ax * ay * canvas[y0 + 1, x0 + 1])
+        views[k] = np.clip(np.rint(v), 0, 255).astype(np.uint8)
+        depths[k] = s.astype(np.float32)
+    return views, depths
+
+
+def rotation(axis: str, degrees: float) -> np.ndarray:
+    """3x3 rotation about the camera's x, y or z (optical) axis."""
+    a = np.deg2rad(degrees)
+    c, s = np.cos(a), np.sin(a)
+    if axis == "x":
+        return np.array([[1, 0, 0], [0, c, -s], [0, s, c]])
+    if axis == "y":
+        return np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+    return np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]])
+
+
+def camera_pose(R, centre) -> np.ndarray:
+    """4x4 Tcw of a camera with orientation R (world -> camera) and centre `centre`."""
+    T = np.eye(4)
+    T[:3, :3] = R
+    T[:3, 3] = -np.asarray(R, np.float64) @ np.asarray(centre, np.float64)
+    return T
+
+
 class StereoSequence:
     """Rectified stereo views of one fronto-parallel textured plane along a random walk
     (configs[3]'s EuRoC-shaped stream).  The left camera of view i sits at canvas offset
@@ -120,9 +193,12 @@ class StereoSequence:
     exactly.  views(idx) renders only the listed views (a rank renders its own shard)."""
 
     def __init__(self, seed: int, n: int, width: int = 752, height: int = 480, step: int = 8, margin: int = 128,
-                 disp: int = 13):
+                 disp: int = 13, canvas_seed: int | None = None):
+        """canvas_seed (default: seed) draws the texture; the walk always comes from seed,
+        so streams that differ only in canvas_seed share their poses."""
         self.width, self.height, self.margin, self.disp = width, height, margin, disp
-        self.canvas = frame(seed, width + 2 * margin + disp, height + 2 * margin, n_shapes=320)
+        self.canvas = frame(seed if canvas_seed is None else canvas_seed, width + 2 * margin + disp,
+                            height + 2 * margin, n_shapes=320)
         g = _rng(seed + 7)
         off = np.zeros((n, 2), dtype=np.int64)
         for i in range(1, n):

@@ -45,9 +45,10 @@ class OracleKeyFrames:
     (extraction of L and R, ComputeStereoMatches, ComputeBoW, has-MapPoint), by window
     index, computed on demand on a thread pool."""
 
-    def __init__(self, O, pl, vocab):
+    def __init__(self, O, pl, vocab, window: int = 0):
         from orbslam2commentedbyxcm_amd.matcher import FrameView, feature_vector_csr
         self.O, self.pl, self.V = O, pl, vocab
+        self.seq = pl.seqs[window]  # the keyframe window (texture) the checked step extracted
         s = pl.s
         self.p = O.params(s["nfeatures"], s["scale"], s["nlevels"], s["ini_th"], s["min_th"])
         self.FrameView, self.csr = FrameView, feature_vector_csr
@@ -61,7 +62,7 @@ class OracleKeyFrames:
 
     def compute(self, g: int) -> dict:
         O, p, pl = self.O, self.p, self.pl
-        left, right = pl.seq.views([g])
+        left, right = self.seq.views([g])
         kl, dl, _ = O.extract(left[0], p)
         kr, dr, _ = O.extract(right[0], p)
         v = self.view(kl, dl, pl.poses[g])

@@ -106,6 +106,104 @@ def fundamental(A, B):
     return (Ki.T @ tx @ R12 @ Ki).astype(np.float32)
 
 
+# ---- general camera motion: rotation about every axis, motion along the optical axis
+
+# The world frame is not any camera's frame: G maps world points into the reference
+# camera's frame, so every Tcw below has a full rotation and translation.
+G = synth.camera_pose(synth.rotation("y", 17.0) @ synth.rotation("x", -9.0) @ synth.rotation("z", 31.0),
+                      [1.3, -0.7, 2.1])
+
+
+def _rel(rots, centre):
+    R = np.eye(3)
+    for ax, deg in rots:
+        R = R @ synth.rotation(ax, deg)
+    return synth.camera_pose(R, centre)
+
+
+# (camera A, camera B), each relative to the reference camera that looks straight at the
+# textured plane Z = Z0.  With the stereo baseline mb = 0.54, "forward" moves B's centre
+# 0.9 along A's optical axis (tlc.z > mb: ORBmatcher.cc:1650's bForward), "backward"
+# 1.0 against it (bBackward).  Rolls of 8-25 degrees shift every keypoint angle, so the
+# rotation histogram (ORBmatcher.cc:1750-1786) sees a real, non-zero rotation.
+POSED = {
+    "roll20": (_rel([("z", 2.0)], [0.05, 0.0, 0.0]), _rel([("z", 20.0), ("x", 1.5)], [0.2, -0.1, 0.1])),
+    "forward": (_rel([("z", -3.0)], [0.0, 0.0, 0.0]), _rel([("z", 8.0), ("y", 1.0)], [0.1, 0.05, 0.9])),
+    "backward": (_rel([("z", 4.0)], [0.0, 0.0, 0.2]), _rel([("z", -12.0)], [-0.1, 0.1, -0.8])),
+    "tilt": (_rel([("x", 2.0), ("y", -2.0)], [0.0, 0.0, 0.0]),
+             _rel([("z", 25.0), ("x", -4.0), ("y", 5.0)], [0.2, 0.2, 0.3])),
+}
+
+
+def _world_pose(rel):
+    return (np.asarray(rel, np.float64) @ G).astype(np.float32)
+
+
+def plane_points(rel, x, y):
+    """Where the rays of camera `rel` through pixels (x, y) meet the plane Z = Z0 of the
+    reference camera: (reference-frame points (n, 3), depth in that camera (n,)), float64."""
+    R, t = np.asarray(rel, np.float64)[:3, :3], np.asarray(rel, np.float64)[:3, 3]
+    C = -R.T @ t
+    ray = np.stack([(np.asarray(x, np.float64) - CX) / FX, (np.asarray(y, np.float64) - CY) / FY,
+                    np.ones(len(x))], 1)
+    a = ray @ R
+    s = (Z0 - C[2]) / a[:, 2]
+    return C[None, :] + s[:, None] * a, s
+
+
+def to_world(X_ref):
+    Gi = np.linalg.inv(G)
+    return X_ref @ Gi[:3, :3].T + Gi[:3, 3]
+
+
+def posed_views(O, seed, scene, stereo=False, prm=C1, extra=()):
+    """Views A and B (plus any `extra` relative poses) of one plane under the poses
+    POSED[scene]: FrameViews with Tcw in the world frame; stereo views get mvuRight from
+    the plane's true depth (+-0.5 px noise, 30 % without a right match)."""
+    rels = list(POSED[scene]) + list(extra)
+    imgs, _ = synth.plane_views(seed, rels, 640, 480, FX, FY, CX, CY, Z0)
+    bf = 0.54 * FX if stereo else 0.0
+    b = bf / FX if stereo else 0.0
+    views = []
+    rng = np.random.default_rng(seed + 11)
+    for img, rel in zip(imgs, rels):
+        V = _view(O, img, _world_pose(rel), bf=bf, b=b, prm=prm)
+        V.rel = rel
+        V.img = img
+        if stereo:
+            _, z = plane_points(rel, V.keys["x"], V.keys["y"])
+            ur = (V.keys["x"] - bf / z + rng.normal(0, 0.5, len(V.keys))).astype(np.float32)
+            ur[rng.random(len(V.keys)) < 0.3] = -1.0
+            V.u_right = ur
+        views.append(V)
+    return views
+
+
+def posed_mappoints(A, seed=0, obs_zero_frac=0.1, depth_noise=0.002):
+    """MapPoints of view A's keypoints on the plane, in world coordinates."""
+    rng = np.random.default_rng(seed + 3)
+    n = len(A.keys)
+    X, s = plane_points(A.rel, A.keys["x"], A.keys["y"])
+    R, t = np.asarray(A.rel)[:3, :3], np.asarray(A.rel)[:3, 3]
+    C = -R.T @ t
+    X = C[None, :] + (X - C[None, :]) * (1.0 + rng.normal(0, depth_noise, n))[:, None]
+    pos = to_world(X).astype(np.float32)
+    obs = rng.integers(1, 4, n).astype(np.int32)
+    obs[rng.random(n) < obs_zero_frac] = 0
+    return MapPoints(desc=A.desc.copy(), observations=obs, pos=pos, bad=(rng.random(n) < 0.03).astype(np.uint8))
+
+
+def rotation_bins(last_keys, cur_keys, cur_mp, last_index_of_mp=None):
+    """Occupied bins of the rotation histogram (ORBmatcher.cc:1750-1757) over the matches
+    cur_mp (MapPoint id per current keypoint; id = last keypoint index unless mapped)."""
+    j = np.nonzero(cur_mp >= 0)[0]
+    i = cur_mp[j] if last_index_of_mp is None else last_index_of_mp[cur_mp[j]]
+    rot = (last_keys["angle"][i] - cur_keys["angle"][j]).astype(np.float32)
+    rot[rot < 0] += np.float32(360.0)
+    b = np.round(rot * np.float32(30 / 360.0)).astype(int) % 30
+    return np.bincount(b, minlength=30)
+
+
 def vocab_nodes(V, nnodes=40, levelsup_bits=3):
     """Synthetic vocabulary node per keypoint (stands in for DBoW2 transform at levelsup 4)."""
     d = V.desc.astype(np.int64)
@@ -114,3 +212,19 @@ def vocab_nodes(V, nnodes=40, levelsup_bits=3):
 
 def fv(V, **kw):
     return feature_vector_csr(vocab_nodes(V, **kw))
+
+
+# a short posed sequence: alternating motion along the optical axis (|dz| > mb = 0.54
+# between some neighbours: bForward / bBackward), rolls of a few degrees per frame
+SEQ_ROLL = [0.0, 5.0, 10.0, 4.0, -3.0, 6.0, 12.0, 8.0]
+SEQ_Z = [0.0, 0.7, 0.05, -0.65, 0.0, 0.6, 0.6, -0.1]
+SEQ_TILT = [(0.0, 0.0), (1.0, -0.5), (-1.0, 1.5), (0.5, 0.5), (2.0, -1.0), (0.0, 1.0), (-1.5, 0.0), (1.0, 1.0)]
+
+
+def posed_sequence(seed, n):
+    """n views of one plane along SEQ_*: (views (n, 480, 640) u8, relative poses, world Tcw (n, 12) f32)."""
+    rels = [_rel([("z", SEQ_ROLL[k]), ("x", SEQ_TILT[k][0]), ("y", SEQ_TILT[k][1])],
+                 [0.03 * k, -0.02 * k, SEQ_Z[k]]) for k in range(n)]
+    imgs, _ = synth.plane_views(seed, rels, 640, 480, FX, FY, CX, CY, Z0)
+    T = np.stack([_world_pose(r)[:3, :4].reshape(12) for r in rels]).astype(np.float32)
+    return imgs, rels, T

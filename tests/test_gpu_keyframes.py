@@ -9,33 +9,53 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("B,nn,steps", [(8, 4, 3), (12, 10, 2)])
-def test_keyframe_pipeline_matches_oracle(oracle, orbx_built, B, nn, steps):
+def _run_snapshots(pl, steps):
+    """Issue `steps` steps back to back (no host synchronisation between them); each
+    step's outputs are cloned on the triangulation stream when it is enqueued (before its
+    set is released), then returned as host dicts with the window each step used."""
     import torch
 
+    snaps = []
+
+    def grab(k):
+        snaps.append((pl.window_of[k], {name: t.clone() for name, t in pl.results(k).items()}))
+
+    pl.on_step_done = grab
+    with torch.cuda.stream(pl.ts):
+        pl.run(steps)
+    torch.cuda.synchronize()
+    assert len(snaps) == steps
+    return [(w, pl.to_host(r)) for w, r in snaps]
+
+
+@pytest.mark.parametrize("B,nn,steps,windows", [(8, 4, 4, 2), (12, 10, 3, 3)])
+def test_keyframe_pipeline_matches_oracle(oracle, orbx_built, B, nn, steps, windows):
+    """Every step (its own keyframe window: same poses, another texture), not only the
+    last, against the oracle."""
     import euroc_bench as E
     from orbslam2commentedbyxcm_amd import synth
     from orbslam2commentedbyxcm_amd.keyframes import StereoKeyFramePipeline
     # a smaller tree of the same depth (k=8, L=6: FeatureVector nodes at level 2, 64 of them)
-    pl = StereoKeyFramePipeline(B, 0, 1, device=0, nn=nn, vocab_text=synth.vocabulary_text(11, 8, 6, 0, 0))
+    pl = StereoKeyFramePipeline(B, 0, 1, device=0, nn=nn, vocab_text=synth.vocabulary_text(11, 8, 6, 0, 0),
+                                windows=windows)
     assert len(pl.plan.pairs) > B
-    pl.run(steps)
-    torch.cuda.synchronize()
-    res = pl.host_results()
+    snaps = _run_snapshots(pl, steps)
     assert pl.status()
-    ok = E.OracleKeyFrames(oracle, pl, oracle.Vocab(pl.vocab_text))
-    r = E.check(pl, ok, res, B, 8)
-    assert r["bit_exact"], r
-    assert r["pairs_checked"] == len(pl.plan.pairs)
-    assert r["mean_triangulation_matches_ref"] > 10, r
-    assert (res["ur"] >= 0).sum() > 50 * B
+    oks = {}
+    for j, (w, res) in enumerate(snaps):
+        assert w == j % windows
+        ok = oks.setdefault(w, E.OracleKeyFrames(oracle, pl, oracle.Vocab(pl.vocab_text), window=w))
+        r = E.check(pl, ok, res, B, 8)
+        assert r["bit_exact"], (j, r)
+        assert r["pairs_checked"] == len(pl.plan.pairs)
+        assert r["mean_triangulation_matches_ref"] > 10, r
+        assert (res["ur"] >= 0).sum() > 50 * B
 
 
 def _rank(rank, world, port, outdir):
     import json
     import os
 
-    import torch
     import torch.distributed as dist
 
     import euroc_bench as E
@@ -47,14 +67,18 @@ def _rank(rank, world, port, outdir):
     # RCCL all_gather_into_tensor needs one GPU per rank); everything else is the N-GPU path
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        pl = StereoKeyFramePipeline(6, rank, world, device=0, nn=4, vocab_text=synth.vocabulary_text(11, 8, 6, 0, 0))
-        pl.run(3)
-        torch.cuda.synchronize()
-        res = pl.host_results()
-        out = {"pairs": len(pl.plan.pairs), "status": pl.status()}
+        pl = StereoKeyFramePipeline(6, rank, world, device=0, nn=4, vocab_text=synth.vocabulary_text(11, 8, 6, 0, 0),
+                                    windows=2)
+        snaps = _run_snapshots(pl, 4)
         O.build()
-        ok = E.OracleKeyFrames(O, pl, O.Vocab(pl.vocab_text))
-        out.update(E.check(pl, ok, res, 6, 4))
+        oks = {}
+        steps = []
+        for j, (w, res) in enumerate(snaps):
+            ok = oks.setdefault(w, E.OracleKeyFrames(O, pl, O.Vocab(pl.vocab_text), window=w))
+            r = E.check(pl, ok, res, 6, 4)
+            r["window"] = w
+            steps.append(r)
+        out = {"pairs": len(pl.plan.pairs), "status": pl.status(), "steps": steps}
         with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
             json.dump(out, f)
         dist.barrier()
@@ -64,8 +88,9 @@ def _rank(rank, world, port, outdir):
 
 def test_keyframe_pipeline_world2_gloo_on_one_gpu(orbx_built, tmp_path):
     """The N-rank layout at world size 2: keyframe g on rank g % 2, neighbours read from the
-    gathered slabs (the other rank's keyframes), every rank's keyframes, gathered
-    neighbours and pair lists bit-exact vs the oracle."""
+    gathered slabs (the other rank's keyframes).  Four pipelined steps over two keyframe
+    windows; every step's keyframes, gathered neighbours and pair lists bit-exact vs the
+    oracle (a gather that overwrote neighbours still being read would mix two windows)."""
     import json
     import socket
 
@@ -77,5 +102,7 @@ def test_keyframe_pipeline_world2_gloo_on_one_gpu(orbx_built, tmp_path):
     mp.spawn(_rank, args=(2, port, str(tmp_path)), nprocs=2, join=True)
     for r in range(2):
         out = json.loads(open(tmp_path / f"r{r}.json").read())
-        assert out["status"] and out["bit_exact"], out
-        assert out["gathered_neighbours_checked"] > 6 and out["pairs_checked"] == out["pairs"] > 6, out
+        assert out["status"] and len(out["steps"]) == 4, out
+        for j, st in enumerate(out["steps"]):
+            assert st["window"] == j % 2 and st["bit_exact"], (r, j, st)
+            assert st["gathered_neighbours_checked"] > 6 and st["pairs_checked"] == out["pairs"] > 6, (r, j, st)

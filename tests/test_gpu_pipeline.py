@@ -98,3 +98,41 @@ def test_device_status_reports_forced_overflow(oracle, orbx_built):
     kr, dr, _ = oracle.extract(frames[0], oracle.params(1000, 1.2, 8, 20, 7))
     assert np.array_equal(kp.view(np.uint8), kr.view(np.uint8)) and np.array_equal(ds, dr)
     assert not ex.status().any()
+
+
+@pytest.mark.parametrize("B,lanes,pipelined,steps", [(16, 2, True, 5), (24, 3, True, 4), (12, 1, False, 3),
+                                                     (256, 2, True, 3)])
+def test_sequence_pipeline_distinct_batch_every_step(oracle, orbx_built, B, lanes, pipelined, steps):
+    """Every step gets its own batch (its own canvas and poses) and steps are issued
+    back to back with no host synchronisation; each batch's outputs are copied out on the
+    matcher stream as soon as its matching is enqueued (SequencePipeline.on_matched, before
+    the buffer is released), so a buffer reused too early, an event waited on the wrong
+    buffer or a batch matched with another batch's poses shows up as a mismatch."""
+    import torch
+
+    batches = [synth.sequence(2000 + j, B) for j in range(steps)]
+    snaps = []
+    pl = None
+
+    def grab(b):
+        r = pl.results(b)
+        snaps.append({k: v.clone() for k, v in r.items()})
+
+    pl = SequencePipeline(B, 640, 480, lanes=lanes, pipelined=pipelined, on_matched=grab)
+    dev_in = [(torch.from_numpy(f).to(pl.dev), torch.from_numpy(sequence_poses(o)).to(pl.dev)) for f, o in batches]
+    torch.cuda.synchronize()
+    with torch.cuda.stream(pl.ms):  # the clones run on the matcher stream, after the matching
+        for frames, T in dev_in:
+            pl.step(frames, T)
+        pl.drain()
+    torch.cuda.synchronize()
+    assert len(snaps) == steps
+    from orbslam2commentedbyxcm_amd import _lib as L
+    for j, ((frames, off), snap) in enumerate(zip(batches, snaps)):
+        cap = pl.cap
+        res = {"kps": snap["kps"].cpu().numpy().view(np.uint8).reshape(B, cap, 28).view(L.KEYPOINT_DTYPE)
+               .reshape(B, cap), "desc": snap["desc"].cpu().numpy(), "n": snap["n"].cpu().numpy(),
+               "mp": snap["mp"].cpu().numpy(), "nm": snap["nm"].cpu().numpy()}
+        r = checks.check_sequence(frames, sequence_poses(off), res, pl.sf)
+        assert r["frames_mismatched"] == 0 and r["pairs_mismatched"] == 0, (j, r)
+        assert r["mean_matches_per_pair_ref"] > 200, (j, r)
