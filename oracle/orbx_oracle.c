@@ -532,13 +532,28 @@ static void divide_node(const ora_node* p, const ora_keypoint* keys, ora_node c[
 
 typedef struct { int size; ora_node* node; } size_ptr;
 
+/* Hazard H1.  std::sort on pair<int, ExtractorNode*> (ORBextractor.cc:899-913) orders equal
+ * sizes by node address, i.e. by the heap.  Mode 0 (shipped, = the GPU): allocation order,
+ * what a monotonic allocator gives -- the later-created node sorts last and is split first.
+ * Mode 1 (measurement only, tests/h1_tie_count.py): the opposite, earlier-created first.
+ * g_octree_ties counts, per thread, final-phase passes in which a split node shared its
+ * size with another node of the pass (the order then depends on the tie-break). */
+static _Thread_local int g_octree_tie_mode = 0;
+static _Thread_local long g_octree_ties = 0;
+
+void ora_set_octree_tie_mode(int mode) { g_octree_tie_mode = mode; }
+long ora_octree_ties(int reset) {
+    const long t = g_octree_ties;
+    if (reset) g_octree_ties = 0;
+    return t;
+}
+
 static int cmp_size_ptr(const void* a, const void* b) {
     const size_ptr* x = (const size_ptr*)a;
     const size_ptr* y = (const size_ptr*)b;
     if (x->size != y->size) return x->size < y->size ? -1 : 1;
-    /* std::sort on pair<int, ExtractorNode*>: equal sizes order by node address.
-     * Hazard H1: fixed here to allocation order (a monotonic allocator). */
-    return x->node->seq < y->node->seq ? -1 : (x->node->seq > y->node->seq ? 1 : 0);
+    const int later = x->node->seq < y->node->seq ? -1 : (x->node->seq > y->node->seq ? 1 : 0);
+    return g_octree_tie_mode ? -later : later;
 }
 
 /* Push the non-empty children n1..n4 to the list front; record those with >1 key. */
@@ -618,13 +633,23 @@ int ora_distribute_octree(const ora_keypoint* keys, int n, int minX, int maxX, i
                 memcpy(vprev, vsz, sizeof(size_ptr) * (size_t)nprev);
                 nvsz = 0;
                 qsort(vprev, (size_t)nprev, sizeof(size_ptr), cmp_size_ptr);
+                int jstop = 0;
                 for (int j = nprev - 1; j >= 0; j--) {
                     ora_node c[4];
                     divide_node(vprev[j].node, keys, c);
                     push_children(&L, c, vsz, &nvsz);
                     list_erase(&L, vprev[j].node);
+                    jstop = j;
                     if (L.size >= N) break;
                 }
+                /* a tie decides the order if a split node (index >= jstop) has a neighbour
+                 * of equal size in the sorted pass */
+                for (int j = jstop; j < nprev; j++)
+                    if ((j > 0 && vprev[j - 1].size == vprev[j].size) ||
+                        (j + 1 < nprev && vprev[j + 1].size == vprev[j].size)) {
+                        g_octree_ties++;
+                        break;
+                    }
                 if (L.size >= N || L.size == prevSize) finish = 1;
             }
         }

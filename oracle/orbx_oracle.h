@@ -65,6 +65,8 @@ float ora_ic_angle(const uint8_t* img, size_t stride, float x, float y, const in
 void ora_cos_sin(float angle_deg, float* c, float* s);
 /* 0: (float)cos((double)r) (default); 1: cosf / sinf as ORBextractor.cc:123-125 (calling thread) */
 void ora_set_trig_mode(int mode);
+void ora_set_octree_tie_mode(int mode);
+long ora_octree_ties(int reset);
 void ora_orb_descriptor(const uint8_t* img, size_t stride, float x, float y, float angle_deg,
                         uint8_t* desc);
 int ora_distribute_octree(const ora_keypoint* keys, int n, int minX, int maxX, int minY,
