@@ -88,10 +88,12 @@ def stage_bytes(W, H, n_kps, nlevels=8, scale=1.2):
     }
 
 
-# stage -> kernels of one launch of that stage (rocprofv3 kernel names)
+# stage -> kernels of one launch of that stage (rocprofv3 kernel names); the match stage
+# is the pipeline's lean split footprint (build, sort + score, one-wave replay)
 STAGE_KERNELS = {"pyramid": ["orbx::k_pyramid"], "score_blur": ["orbx::k_level_tiles"],
                  "fast_cells": ["orbx::k_fast_cells"], "octree": ["orbx::k_octree"],
-                 "describe": ["orbx::k_describe"], "match": ["orbx::k_seq_build", "orbx::k_proj_search"]}
+                 "describe": ["orbx::k_describe"],
+                 "match": ["orbx::k_seq_build", "orbx::k_proj_search", "orbx::k_seq_commit"]}
 
 
 def _stage_sum(ks: dict, stage: str, field: str):
@@ -114,6 +116,23 @@ def newest_profiles(pattern: str):
     return sorted(files, key=lambda f: ([int(x) for x in re.findall(r"\d+", f.name)], f.name))
 
 
+def rocprof_mean_ms(stage: str, workload: str):
+    """Mean duration (ms) per launch of `stage`'s kernels in the newest committed kernel
+    trace of this workload's bench (profiles/<tag>_<workload>_kernel_stats.csv: rocprofv3
+    --kernel-trace --stats of the command the driver runs, tools/prof_bench.sh), the
+    profile-side check of the HIP-event time, or (None, None)."""
+    import csv
+    files = newest_profiles(f"*_{workload}_kernel_stats.csv")
+    if not files:
+        return None, None
+    ks = {}
+    for r in csv.DictReader(open(files[-1])):
+        name = r["Name"].split("(")[0].replace("void ", "")
+        ks[name] = {"avg_ns": float(r["AverageNs"])}
+    tot = _stage_sum(ks, stage, "avg_ns")
+    return (None if tot is None else tot * 1e-6), files[-1].name
+
+
 def pmc_valu(stage: str):
     """VALU wave-instructions per launch of `stage` from the newest profiles/*_pmc_valu.json
     (tools/pmc_valu.sh + tools/pmc_valu.py), or (None, None)."""
@@ -125,16 +144,34 @@ def pmc_valu(stage: str):
     return (None if tot is None else int(tot)), files[-1].name
 
 
-def pmc_traffic(stage: str):
-    """HBM bytes per launch of `stage` from the newest committed PMC summary
-    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate FETCH_SIZE /
-    WRITE_SIZE rocprofv3 passes of this bench), or (None, None)."""
-    files = newest_profiles("*_pmc_traffic.json")
+def pmc_traffic(stage: str, workload: str = "tum"):
+    """HBM bytes per launch of `stage` from the newest committed PMC summary of this
+    workload's bench (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from
+    separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes; configs[1] files carry no workload
+    tag, the others <tag>_<workload>_pmc_traffic.json), or (None, None)."""
+    files = newest_profiles(f"*_{workload}_pmc_traffic.json")
+    if workload == "tum":
+        files = [f for f in newest_profiles("*_pmc_traffic.json")
+                 if not any(w in f.name for w in ("_tum5k_", "_kitti_", "_euroc_"))]
     if not files:
         return None, None
     ks = json.loads(files[-1].read_text())["kernels"]
     tot = _stage_sum(ks, stage, "traffic_bytes")
     return (None if tot is None else int(tot)), files[-1].name
+
+
+def profile_fields(dom: str, algorithmic_bytes: float, event_ms: float, workload: str) -> dict:
+    """Roofline fields that come from the committed profiles of this workload's bench:
+    the PMC traffic per launch and the kernel-trace mean duration, with the fraction of
+    HBM peak recomputed from that mean (the profile-side check of the HIP-event `frac`)."""
+    traffic, traffic_src = pmc_traffic(dom, workload)
+    prof_ms, prof_src = rocprof_mean_ms(dom, workload)
+    return {"traffic": traffic, "traffic_unit": "bytes per launch (PMC FETCH_SIZEx2 + WRITE_SIZE)",
+            "traffic_source": traffic_src, "kernels": STAGE_KERNELS.get(dom),
+            "event_ms": round(event_ms, 4),
+            "rocprof_mean_ms": None if prof_ms is None else round(prof_ms, 4), "rocprof_source": prof_src,
+            "frac_rocprof": None if not prof_ms else
+            round(algorithmic_bytes / (prof_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
 
 
 def cpu_model() -> str:
@@ -391,20 +428,22 @@ def main():
     mean_kps = float(n_host.mean())
     mean_matches = float(res["nm"][1:].mean()) if match and B > 1 else 0.0
 
-    stage_ms = pl.exs[0].stage_times()
-    if match:
-        stage_ms["match"] = pl.matcher.last_ms()
+    stage_ms = pl.stage_times()  # HIP events, mean over the lanes' launches
     pl.set_timing(False)
     bytes_pf = stage_bytes(W, H, mean_kps, nlevels=prm[2], scale=prm[1])
     # Dominant kernel: the longest stage on the critical path.  Pipelined, the matcher
-    # runs beside the next batch's extraction on its own stream (its event time includes
-    # that contention), so the extraction stages are the critical path.
-    kernels = {k: v for k, v in stage_ms.items() if k != "total" and not (pipeline and k == "match")}
+    # runs beside the next batch's extraction on its own stream, so the step is set by
+    # whichever is longer: a lane's extraction (its longest stage is reported) or the
+    # matcher (configs[4]: its launch is then the critical path).
+    kernels = {k: v for k, v in stage_ms.items() if k not in ("total", "match")}
     dom = max(kernels, key=kernels.get)
-    Bc = pl.bounds[0][1] - pl.bounds[0][0]  # frames of lane 0, whose events time the stages
-    achieved = bytes_pf[dom] * Bc / (stage_ms[dom] * 1e-3) / 1e9
-    # the committed PMC summaries are passes of the configs[1] bench
-    traffic, traffic_src = pmc_traffic(dom) if not c5 else (None, None)
+    if match and pipeline and stage_ms.get("match", 0.0) > stage_ms.get("total", 0.0):
+        dom = "match"
+    # frames per launch: a lane's batch for extraction stages, every pair for the matcher
+    per_launch = (B - 1) if dom == "match" else (pl.bounds[0][1] - pl.bounds[0][0])
+    achieved = bytes_pf[dom] * per_launch / (stage_ms[dom] * 1e-3) / 1e9
+    wl = "tum5k" if c5 else "tum"
+    prof = profile_fields(dom, bytes_pf[dom] * per_launch, stage_ms[dom], wl)
     valu, valu_src = pmc_valu(dom) if not c5 else (None, None)
     issue = None
     if valu:
@@ -455,9 +494,11 @@ def main():
                        "pipelined_match": pipeline,
                        "match_cu_stride": None if pl._own_ms is None else int(os.environ.get("ORBX_MATCH_CUSTRIDE", "1"))},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "traffic_unit": "bytes per launch (PMC FETCH_SIZEx2 + WRITE_SIZE)",
-                         "traffic_source": traffic_src, "algorithmic_bytes_per_launch": int(bytes_pf[dom] * Bc),
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), **prof,
+                         "algorithmic_bytes_per_launch": int(bytes_pf[dom] * per_launch),
+                         "units_per_launch": per_launch,
+                         "event_ms_note": "HIP events on the launching stream around the stage, mean over the timed "
+                                          "steps and the lanes",
                          "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()}, "issue": issue,
                          # the S lanes launch the same kernel on S streams at once, so a
                          # launch's duration is shared with S - 1 concurrent launches

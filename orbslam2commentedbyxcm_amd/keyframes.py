@@ -366,12 +366,16 @@ class StereoKeyFramePipeline:
             self.step()
 
     def set_timing(self, enable: bool):
-        self.sets[0][0].set_timing(enable)
+        for ex in (e for st in self.sets for e in st):
+            ex.set_timing(enable)
         self.stereo.set_timing(enable)
         self.tri.set_timing(enable)
 
     def stage_times(self) -> dict:
-        st = self.sets[0][0].stage_times()
+        """HIP-event ms per launch: extraction stages averaged over the four extractors
+        (L and R of both sets), the stereo matching and the triangulation."""
+        per = [e.stage_times() for st in self.sets for e in st]
+        st = {k: sum(p[k] for p in per) / len(per) for k in per[0]}
         st["stereo"] = self.stereo.last_ms()
         if len(self.plan.pairs):
             st["triangulation"] = self.tri.last_ms()

@@ -200,9 +200,19 @@ class SequencePipeline:
         return np.concatenate([e.status(b1 - b0) for e, (b0, b1) in zip(self.exs, self.bounds)])
 
     def set_timing(self, enable: bool):
-        self.exs[0].set_timing(enable)
+        for e in self.exs:
+            e.set_timing(enable)
         if self.match:
             self.matcher.set_timing(enable)
+
+    def stage_times(self) -> dict:
+        """HIP-event stage times (ms per launch) averaged over the lanes' extractors (each
+        lane's launches time its own frames), plus the matcher's ("match")."""
+        per = [e.stage_times() for e in self.exs]
+        out = {k: sum(p[k] for p in per) / len(per) for k in per[0]}
+        if self.match:
+            out["match"] = self.matcher.last_ms()
+        return out
 
 
 def sequence_poses(off: np.ndarray, fx: float = 500.0, fy: float = 500.0, depth: float = 5.0) -> np.ndarray:

@@ -332,7 +332,8 @@ def main(argv=None):
                        "triangulation_pairs_per_step": tot_pairs, "baseline_skipped_per_step": tot_skipped,
                        "triangulation_matches_per_step": tot_matches},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         **bench.profile_fields(dom, bytes_pf[dom] * B, stage_ms[dom], "euroc"),
                          "algorithmic_bytes_per_launch": int(bytes_pf[dom] * B),
                          "bytes_model": "SURVEY.md §8(d) per-stage algorithmic bytes per image x B images per launch",
                          "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},

@@ -7,7 +7,7 @@
 bench.py --workload kitti is the entry point.)
 
 Workload: B = 128 synthetic 1241x376 stereo pairs per step (right = left shifted by a
-blockwise disparity field, synth.stereo_pair; 32 distinct pairs tiled), ORB parameters
+blockwise disparity field, synth.stereo_pair; all distinct by default), ORB parameters
 2000 features, scale 1.2, 8 levels, FAST 20/7 (KITTI's settings).  One step = the stereo
 Frame constructor's hot path for all B pairs (Frame.cc:99-178):
   1. mpORBextractorLeft on the B left images and mpORBextractorRight on the B right
@@ -47,9 +47,23 @@ FX, BF = 718.856, 386.1448  # KITTI 00-02 calibration (Camera.fx, Camera.bf)
 HBM_PEAK_GBS = 8000.0
 
 
-def make_pairs(n_distinct: int):
+def _pair(i):
     from orbslam2commentedbyxcm_amd import synth
-    return [synth.stereo_pair(5000 + i, W, H, max_disp=64)[:2] for i in range(n_distinct)]
+    return synth.stereo_pair(5000 + i, W, H, max_disp=64)[:2]
+
+
+def make_pairs(n_distinct: int, workers: int = 1):
+    """The distinct stereo pairs; workers > 1 renders them in a process pool (before the
+    process touches the GPU)."""
+    if workers > 1 and n_distinct > 1:
+        import multiprocessing as mp
+        pool = mp.get_context("fork").Pool(min(workers, n_distinct))
+        try:
+            return list(pool.imap(_pair, range(n_distinct), chunksize=2))
+        finally:
+            pool.close()
+            pool.join()
+    return [_pair(i) for i in range(n_distinct)]
 
 
 def oracle_pair(O, p, left, right, sf):
@@ -106,7 +120,7 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=128, help="stereo pairs per step")
-    ap.add_argument("--distinct", type=int, default=32)
+    ap.add_argument("--distinct", type=int, default=0, help="distinct pairs (0 = the batch size)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -116,7 +130,7 @@ def main(argv=None):
     if args.gpus != 1:
         raise SystemExit("--workload kitti is a single-GPU configuration (configs[2])")
 
-    pairs = make_pairs(min(args.distinct, B))
+    pairs = make_pairs(min(args.distinct or B, B), workers=min(16, len(os.sched_getaffinity(0))))
     idx = [b % len(pairs) for b in range(B)]
     left_np = np.stack([pairs[i][0] for i in idx])
     right_np = np.stack([pairs[i][1] for i in idx])
@@ -174,7 +188,8 @@ def main(argv=None):
     for _ in range(max(args.warmup, 2)):
         step()
     torch.cuda.synchronize(dev)
-    sets[0][0].set_timing(True)
+    for ex in (e for st in sets for e in st):
+        ex.set_timing(True)
     matcher.set_timing(True)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -183,9 +198,11 @@ def main(argv=None):
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     value = B * args.steps / el
-    stage_ms = sets[0][0].stage_times()
+    per = [e.stage_times() for st in sets for e in st]  # every extractor's launches (L and R, both sets)
+    stage_ms = {s: sum(p[s] for p in per) / len(per) for s in per[0]}
     stage_ms["stereo"] = matcher.last_ms()
-    sets[0][0].set_timing(False)
+    for ex in (e for st in sets for e in st):
+        ex.set_timing(False)
     matcher.set_timing(False)
 
     k = state["last"]
@@ -256,7 +273,8 @@ def main(argv=None):
                                f"extractors + Frame::ComputeStereoMatches of every pair (bf {BF}, maxD = fx)",
                    "pairs_per_step": B, "width": W, "height": H},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                     **bench.profile_fields(dom, bytes_pf[dom] * B, stage_ms[dom], "kitti"),
                      "algorithmic_bytes_per_launch": int(bytes_pf[dom] * B),
                      "bytes_model": "SURVEY.md §8(d) per-stage algorithmic bytes per image x B images per launch",
                      "stage_ms": {s: round(v, 4) for s, v in stage_ms.items()},

@@ -39,10 +39,31 @@ def test_pmc_summaries_cover_the_stages():
 
 
 def test_stage_sum_prefix_and_missing():
-    ks = {"orbx::k_seq_build": {"x": 1}, "orbx::k_proj_search<false, false, 256>": {"x": 2}}
-    assert bench._stage_sum(ks, "match", "x") == 3
+    ks = {"orbx::k_seq_build": {"x": 1}, "orbx::k_proj_search<false, false, 1024, true>": {"x": 2},
+          "orbx::k_seq_commit": {"x": 4}}
+    assert bench._stage_sum(ks, "match", "x") == 7
+    assert bench._stage_sum({k: v for k, v in ks.items() if "commit" not in k}, "match", "x") is None
     assert bench._stage_sum(ks, "pyramid", "x") is None
     assert bench._stage_sum({}, "no-such-stage", "x") is None
+
+
+def test_profile_fields_read_the_workload_trace(tmp_path, monkeypatch):
+    """A bench line's rocprof mean comes from the newest <tag>_<workload>_kernel_stats.csv and
+    its frac_rocprof follows from it and the algorithmic bytes."""
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    hdr = '"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"\n'
+    (prof / "r03a_tum_kernel_stats.csv").write_text(
+        hdr + '"orbx::k_level_tiles(unsigned char const*)",50,1,400000.0,1,1,1,1\n')
+    (prof / "r03b_tum_kernel_stats.csv").write_text(
+        hdr + '"orbx::k_level_tiles(unsigned char const*)",50,1,300000.0,1,1,1,1\n')
+    (prof / "r03c_tum5k_kernel_stats.csv").write_text(
+        hdr + '"orbx::k_level_tiles(unsigned char const*)",50,1,900000.0,1,1,1,1\n')
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    f = bench.profile_fields("score_blur", 2.4e8, 0.3, "tum")
+    assert f["rocprof_source"] == "r03b_tum_kernel_stats.csv" and f["rocprof_mean_ms"] == 0.3
+    assert abs(f["frac_rocprof"] - 2.4e8 / 0.3e-3 / 1e9 / bench.HBM_PEAK_GBS) < 1e-5
+    assert bench.profile_fields("score_blur", 1.0, 0.3, "kitti")["rocprof_mean_ms"] is None
 
 
 def test_newest_profile_is_highest_tag():
