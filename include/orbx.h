@@ -310,10 +310,58 @@ typedef struct {
     const float* scale_factors;   /* host: mvScaleFactors (nlevels) */
     float th;
     int mono;                     /* bMono */
-    int32_t* cur_mp;              /* [B][cap] out: CurrentFrame.mvpMapPoints as LastFrame indices, -1 */
+    int global_ids;               /* 0: MapPoint id = LastFrame keypoint index i; 1: id = (b-1)*cap + i */
+    int32_t* cur_mp;              /* [B][cap] out: CurrentFrame.mvpMapPoints as MapPoint ids, -1 */
     int32_t* nmatches;            /* [B] out (frame 0: 0) */
 } orbx_sequence;
 int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* seq, void* stream);
+
+/* Tracking::SearchLocalPoints (Tracking.cc:1280-1336) for B Frames in HBM -- the
+ * per-frame TrackLocalMap search.  For frame b:
+ *   1. mvpMapPoints (frame_mp [b][cap], MapPoint ids, -1 = NULL; e.g. the
+ *      orbx_match_sequence_device_ex output with global ids): bad MapPoints are set to
+ *      NULL, the rest are "seen" and not projected again (Tracking.cc:1286-1299);
+ *   2. Frame::IsInFrustum(pMP, viewing_cos_limit) (Frame.cc:412-477) for every entry of
+ *      frame b's local map (mvpLocalMapPoints, local_ids[local_off[b] .. local_off[b+1]))
+ *      that is neither seen nor bad;
+ *   3. SearchByProjection(F, vpLocalMapPoints, th) (ORBmatcher.cc:61-173) with the
+ *      matcher's nnratio (Tracking uses ORBmatcher(0.8)) over the points in view, in list
+ *      order: frame_mp is updated in place, nmatches [b] receives its count.
+ * MapPoints live in a device table indexed by id.  local_off is a host array (B + 1
+ * ints: it sizes the launch); every other pointer is a device pointer.  cap and the
+ * longest local map must stay below 8192.  Asynchronous on `stream` (or the matcher's). */
+typedef struct {
+    int n;                        /* MapPoints in the table */
+    const float* pos;             /* [n][3] GetWorldPos() */
+    const uint8_t* desc;          /* [n][32] GetDescriptor() */
+    const float* normal;          /* [n][3] GetNormal() */
+    const float* max_distance;    /* [n] mfMaxDistance */
+    const float* min_distance;    /* [n] mfMinDistance */
+    const int32_t* observations;  /* [n] Observations() */
+    const uint8_t* bad;           /* [n] isBad() or NULL */
+} orbx_mappoints_device;
+
+typedef struct {
+    int batch;
+    const orbx_keypoint* kps;     /* [B][cap] mvKeysUn */
+    const uint8_t* desc;          /* [B][cap][32] mDescriptors */
+    const int32_t* n;             /* [B] keypoint counts */
+    int cap;
+    const float* u_right;         /* [B][cap] mvuRight or NULL */
+    const float* Tcw;             /* [B][12] mTcw rows 0..2 */
+    float fx, fy, cx, cy, bf;
+    float min_x, max_x, min_y, max_y;
+    int nlevels;
+    const float* scale_factors;   /* host: mvScaleFactors (nlevels) */
+    const int32_t* local_off;     /* host: [B + 1] */
+    const int32_t* local_ids;     /* device: local map MapPoint ids, frame after frame */
+    float th;                     /* 1; 3 for RGB-D; 5 right after a relocalisation (Tracking.cc:1320-1331) */
+    float viewing_cos_limit;      /* 0.5 (Tracking.cc:1314) */
+    int32_t* frame_mp;            /* [B][cap] in/out */
+    int32_t* nmatches;            /* [B] out */
+} orbx_local_map_batch;
+int orbx_search_local_points_device(orbx_matcher* m, const orbx_mappoints_device* mps,
+                                    const orbx_local_map_batch* lm, void* stream);
 
 /* ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches)
  * (ORBmatcher.cc:228-392; Tracking::TrackReferenceKeyFrame / Relocalization).
@@ -503,6 +551,20 @@ int orbx_assign_features_to_grid(int device, const orbx_keypoint* keys_un, int n
 int orbx_assign_features_to_grid_device(int batch, const orbx_keypoint* d_keys_un, const int32_t* d_n, int cap,
                                         const float* bounds, int32_t* d_cell_start, int32_t* d_cell_idx,
                                         void* stream);
+
+/* The MapPoints a stereo / RGB-D keyframe is born with (Tracking::CreateNewKeyFrame,
+ * Tracking.cc:1069-1121) for B frames in HBM, as an orbx_mappoints_device table with id
+ * b*cap + i: for every keypoint i < n[b] with depth z > 0 (d_depth [B][cap] = mvDepth, the
+ * caller's selection of close points; or `const_depth` for every keypoint when d_depth is
+ * NULL), pos = Frame::UnprojectStereo(i) (Frame.cc:912-927) and normal / mfMaxDistance /
+ * mfMinDistance from MapPoint::UpdateNormalAndDepth with the frame as the only observation
+ * (MapPoint.cc:386-439); observations 1, bad 0.  Other slots: bad 1, observations 0.
+ * Outputs [B*cap] (pos, normal: x3).  scale_factors is a host array.  Asynchronous. */
+int orbx_create_mappoints_device(int batch, const orbx_keypoint* d_kps, const int32_t* d_n, int cap,
+                                 const float* d_depth, float const_depth, const float* d_Tcw, float fx, float fy,
+                                 float cx, float cy, const float* scale_factors, int nlevels, float* d_pos,
+                                 float* d_normal, float* d_max_distance, float* d_min_distance,
+                                 int32_t* d_observations, uint8_t* d_bad, void* stream);
 
 /* ---- DBoW2 vocabulary (TemplatedVocabulary<FORB::TDescriptor, FORB>, §8(f) rank 1) ----
  * The tree lives in HBM as its CSR edge list.  Scoring / weighting

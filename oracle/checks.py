@@ -98,3 +98,69 @@ def check_sequence(frames: np.ndarray, T: np.ndarray, res: dict, sf, threads: in
                     if len(frames) > 1 else 0.0})
     out["bit_exact"] = out["frames_mismatched"] == 0 and out.get("pairs_mismatched", 0) == 0
     return out
+
+
+def sequence_local(ref, T: np.ndarray, sf, cap: int, local_window: int = 3, fx=500.0, fy=500.0, cx=320.0, cy=240.0,
+                   W=640, H=480, depth=5.0, th=15.0, local_th=1.0, threads: int = 0):
+    """Oracle of SequencePipeline(local_map=True) on the oracle's own extraction `ref`:
+    every keypoint's MapPoint (ora_create_mappoints at `depth`, id f*cap + i), then per
+    frame b >= 1 TrackWithMotionModel's SearchByProjection against frame b-1's MapPoints
+    (ORBmatcher(0.9, true)) and Tracking::SearchLocalPoints against the MapPoints of frames
+    b-1 .. b-local_window (ORBmatcher(0.8)).  -> per frame (nm, nm_local, frame_mp)."""
+    from orbslam2commentedbyxcm_amd.matcher import FrameView, MapPoints
+    B = len(ref)
+    N = B * cap
+
+    def view(k, d, t):
+        return FrameView(keys=k, desc=d, fx=fx, fy=fy, cx=cx, cy=cy, max_x=float(W), max_y=float(H),
+                         scale_factors=sf, Tcw=np.vstack([t.reshape(3, 4), [0, 0, 0, 1]]).astype(np.float32))
+
+    pos = np.zeros((N, 3), np.float32)
+    nrm = np.zeros((N, 3), np.float32)
+    mx = np.zeros(N, np.float32)
+    mn = np.zeros(N, np.float32)
+    desc = np.zeros((N, 32), np.uint8)
+    bad = np.ones(N, np.uint8)
+    for f, (k, d) in enumerate(ref):
+        m = O.create_mappoints(view(k, d, T[f]), const_depth=depth)
+        sl = slice(f * cap, f * cap + len(k))
+        pos[sl], nrm[sl], mx[sl], mn[sl] = m["pos"], m["normal"], m["max_distance"], m["min_distance"]
+        desc[sl] = d
+        bad[sl] = 1 - m["valid"]
+    obs = (1 - bad).astype(np.int32)
+    mps = MapPoints(desc=desc, observations=obs, pos=pos, bad=bad, max_distance=mx, min_distance=mn, normal=nrm)
+
+    def one(b):
+        (lk, ld), (ck, cd) = ref[b - 1], ref[b]
+        cur = np.full(len(ck), -1, np.int32)
+        last_mp = np.where(bad[(b - 1) * cap:(b - 1) * cap + len(lk)] == 0,
+                           np.arange((b - 1) * cap, (b - 1) * cap + len(lk)), -1).astype(np.int32)
+        nm = O.sbp_frame(view(ck, cd, T[b]), cur, view(lk, ld, T[b - 1]), last_mp, mps, th, True, True)
+        ids = np.concatenate([np.arange(f * cap, (f + 1) * cap, dtype=np.int32)
+                              for f in range(max(0, b - local_window), b)])
+        nl = O.search_local_points(view(ck, cd, T[b]), cur, ids, mps, local_th, 0.8)
+        return nm, nl, cur
+
+    with ThreadPoolExecutor(_threads(threads)) as ex:
+        return [None] + list(ex.map(one, range(1, B)))
+
+
+def check_sequence_local(frames: np.ndarray, T: np.ndarray, res: dict, sf, cap: int, threads: int = 0,
+                         params=(1000, 1.2, 8, 20, 7), **kw) -> dict:
+    """A SequencePipeline(local_map=True) result (kps, desc, n, mp, nm, nm_local) against
+    sequence_local: every frame's extraction and every frame's final mvpMapPoints."""
+    ref = extract_all(frames, params=params, threads=threads)
+    bad_frames = compare_extraction(ref, res["kps"], res["desc"], res["n"])
+    out = {"frames_checked": len(frames), "frames_mismatched": len(bad_frames), "first_bad_frames": bad_frames[:8]}
+    mref = sequence_local(ref, T, sf, cap, threads=threads, **kw)
+    bad_pairs = []
+    for b in range(1, len(frames)):
+        nm, nl, cur = mref[b]
+        m = int(res["n"][b])
+        if int(res["nm"][b]) != nm or int(res["nm_local"][b]) != nl or not np.array_equal(res["mp"][b, :m], cur):
+            bad_pairs.append(b)
+    out.update({"pairs_checked": len(frames) - 1, "pairs_mismatched": len(bad_pairs), "first_bad_pairs": bad_pairs[:8],
+                "mean_matches_per_pair_ref": float(np.mean([mref[b][0] for b in range(1, len(frames))])),
+                "mean_local_matches_ref": float(np.mean([mref[b][1] for b in range(1, len(frames))]))})
+    out["bit_exact"] = out["frames_mismatched"] == 0 and out["pairs_mismatched"] == 0
+    return out

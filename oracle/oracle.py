@@ -370,6 +370,42 @@ def is_in_frustum(F, mps, ids=None, viewing_cos_limit=0.5):
     return t
 
 
+def create_mappoints(F, depth=None, const_depth=0.0):
+    """Tracking::CreateNewKeyFrame's MapPoints of one Frame (UnprojectStereo +
+    UpdateNormalAndDepth) -> dict pos (n,3), normal (n,3), max_distance, min_distance (n,),
+    valid (n,) u8."""
+    keep = []
+    f = _frame(F, keep)
+    n = len(F.keys)
+    out = {"pos": np.zeros((n, 3), np.float32), "normal": np.zeros((n, 3), np.float32),
+           "max_distance": np.zeros(n, np.float32), "min_distance": np.zeros(n, np.float32),
+           "valid": np.zeros(n, np.uint8)}
+    d = None if depth is None else np.ascontiguousarray(depth, np.float32)
+    L = lib()
+    L.ora_create_mappoints.argtypes = [C.c_void_p, F32P, C.c_float, F32P, F32P, F32P, F32P, U8P]
+    L.ora_create_mappoints.restype = None
+    L.ora_create_mappoints(C.addressof(f), None if d is None else d.ctypes.data_as(F32P), float(const_depth),
+                           out["pos"].ctypes.data_as(F32P), out["normal"].ctypes.data_as(F32P),
+                           out["max_distance"].ctypes.data_as(F32P), out["min_distance"].ctypes.data_as(F32P),
+                           out["valid"].ctypes.data_as(U8P))
+    return out
+
+
+def search_local_points(F, frame_mp, local_ids, mps, th, nnratio=0.8, viewing_cos_limit=0.5):
+    """Tracking::SearchLocalPoints (Tracking.cc:1280-1336) for one Frame, restated over the
+    oracle's IsInFrustum and SearchByProjection(F, vpMapPoints, th): frame_mp (MapPoint ids)
+    is updated in place (bad MapPoints set to NULL first); returns the search's nmatches."""
+    bad = np.zeros(len(mps.desc), np.uint8) if mps.bad is None else np.asarray(mps.bad, np.uint8)
+    for i in np.nonzero(frame_mp >= 0)[0]:
+        if bad[frame_mp[i]]:
+            frame_mp[i] = -1
+    seen = set(int(x) for x in frame_mp[frame_mp >= 0])
+    ids = np.asarray(local_ids, np.int32)
+    test = np.array([m for m in ids if int(m) not in seen and not bad[m]], np.int32)
+    trk = is_in_frustum(F, mps, test, viewing_cos_limit)
+    return sbp_local(F, frame_mp, ids, mps, trk, th, nnratio)
+
+
 def sbp_frame(cur, cur_mp, last, last_mp, mps, th, mono, check_ori, last_outlier=None):
     keep = []
     fc = _frame(cur, keep)

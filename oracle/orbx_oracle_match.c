@@ -377,6 +377,47 @@ void ora_is_in_frustum(const ora_frame* f, const ora_mappoints* mps, const int32
     }
 }
 
+/* ---------------------------------------------------------------- MapPoint creation */
+
+/* Tracking::CreateNewKeyFrame's MapPoints of one Frame (Tracking.cc:1069-1121): keypoint
+ * i with depth z > 0 (depth[i], or const_depth when depth is NULL) gets
+ * Frame::UnprojectStereo(i) (Frame.cc:912-927: x3Dc = ((u-cx)*z*invfx, (v-cy)*z*invfy, z),
+ * mRwc*x3Dc + mOw) and MapPoint::UpdateNormalAndDepth with this frame as its only
+ * observation (MapPoint.cc:386-439: normal = PC / cv::norm(PC), i.e. PC * (float)(1/n);
+ * mfMaxDistance = |PC| * mvScaleFactors[octave]; mfMinDistance = mfMaxDistance /
+ * mvScaleFactors[nLevels-1]).  valid[i] = 0 where no MapPoint is made. */
+void ora_create_mappoints(const ora_frame* f, const float* depth, float const_depth, float* pos, float* normal,
+                          float* max_distance, float* min_distance, uint8_t* valid) {
+    const float* T = f->Tcw;
+    const float invfx = 1.0f / f->fx, invfy = 1.0f / f->fy;
+    float Ow[3];
+    for (int r = 0; r < 3; r++) Ow[r] = -(T[r] * T[3] + T[4 + r] * T[7] + T[8 + r] * T[11]);
+    for (int i = 0; i < f->n; i++) {
+        const float z = depth ? depth[i] : const_depth;
+        valid[i] = 0;
+        if (!(z > 0)) continue;
+        const float x = (f->keys[i].x - f->cx) * z * invfx;
+        const float y = (f->keys[i].y - f->cy) * z * invfy;
+        float P[3], PC[3];
+        for (int r = 0; r < 3; r++) P[r] = T[r] * x + T[4 + r] * y + T[8 + r] * z + Ow[r];
+        for (int c = 0; c < 3; c++) PC[c] = P[c] - Ow[c];
+        const double n = sqrt((double)PC[0] * PC[0] + (double)PC[1] * PC[1] + (double)PC[2] * PC[2]);
+        const float inv = (float)(1.0 / n);
+        const float dist = (float)n;
+        int oct = f->keys[i].octave;
+        if (oct < 0) oct = 0;
+        if (oct >= f->nlevels) oct = f->nlevels - 1;
+        const float mx = dist * f->scale_factors[oct];
+        for (int c = 0; c < 3; c++) {
+            pos[3 * i + c] = P[c];
+            normal[3 * i + c] = PC[c] * inv;
+        }
+        max_distance[i] = mx;
+        min_distance[i] = mx / f->scale_factors[f->nlevels - 1];
+        valid[i] = 1;
+    }
+}
+
 /* ---------------------------------------------------------------- a13 */
 
 /* ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>&

@@ -66,6 +66,8 @@ int ora_sbp_local(const ora_frame* f, int32_t* frame_mp, const int32_t* queries,
 void ora_is_in_frustum(const ora_frame* f, const ora_mappoints* mps, const int32_t* ids, int n,
                        float viewingCosLimit, uint8_t* in_view, float* proj_x, float* proj_y, float* proj_xr,
                        int32_t* scale_level, float* view_cos);
+void ora_create_mappoints(const ora_frame* f, const float* depth, float const_depth, float* pos, float* normal,
+                          float* max_distance, float* min_distance, uint8_t* valid);
 int ora_sbp_frame(const ora_frame* cur, int32_t* cur_mp, const ora_frame* last, const int32_t* last_mp,
                   const uint8_t* last_outlier, const ora_mappoints* mps, float th, int bMono, int check_ori);
 int ora_sbp_keyframe(const ora_frame* cur, int32_t* cur_mp, const ora_frame* kf, const int32_t* kf_mp,

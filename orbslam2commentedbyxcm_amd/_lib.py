@@ -49,6 +49,7 @@ EXPORTED = [
     "orbx_compute_distinctive_descriptors_device", "orbx_extractor_status", "orbx_extractor_status_device",
     "orbx_extractor_set_node_capacity", "orbx_compute_stereo_matches_batch_device",
     "orbx_search_for_triangulation_batch_device", "orbx_match_sequence_device_ex",
+    "orbx_search_local_points_device", "orbx_create_mappoints_device",
 ]
 
 
@@ -70,7 +71,25 @@ class Sequence(C.Structure):
                 ("bf", C.c_float), ("b", C.c_float), ("min_x", C.c_float), ("max_x", C.c_float),
                 ("min_y", C.c_float), ("max_y", C.c_float), ("nlevels", C.c_int),
                 ("scale_factors", C.POINTER(C.c_float)), ("th", C.c_float), ("mono", C.c_int),
-                ("cur_mp", C.c_void_p), ("nmatches", C.c_void_p)]
+                ("global_ids", C.c_int), ("cur_mp", C.c_void_p), ("nmatches", C.c_void_p)]
+
+
+class MapPointsDevice(C.Structure):
+    """orbx_mappoints_device."""
+    _fields_ = [("n", C.c_int), ("pos", C.c_void_p), ("desc", C.c_void_p), ("normal", C.c_void_p),
+                ("max_distance", C.c_void_p), ("min_distance", C.c_void_p), ("observations", C.c_void_p),
+                ("bad", C.c_void_p)]
+
+
+class LocalMapBatch(C.Structure):
+    """orbx_local_map_batch."""
+    _fields_ = [("batch", C.c_int), ("kps", C.c_void_p), ("desc", C.c_void_p), ("n", C.c_void_p), ("cap", C.c_int),
+                ("u_right", C.c_void_p), ("Tcw", C.c_void_p), ("fx", C.c_float), ("fy", C.c_float),
+                ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float), ("min_x", C.c_float),
+                ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float), ("nlevels", C.c_int),
+                ("scale_factors", C.POINTER(C.c_float)), ("local_off", C.POINTER(C.c_int32)),
+                ("local_ids", C.c_void_p), ("th", C.c_float), ("viewing_cos_limit", C.c_float),
+                ("frame_mp", C.c_void_p), ("nmatches", C.c_void_p)]
 
 
 class OrbxError(RuntimeError):
@@ -146,6 +165,9 @@ def lib() -> C.CDLL:
                                              C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, fp, C.c_int,
                                              C.c_float, C.c_float, vp, vp, vp]
     L.orbx_match_sequence_device_ex.argtypes = [vp, C.POINTER(Sequence), vp]
+    L.orbx_search_local_points_device.argtypes = [vp, C.POINTER(MapPointsDevice), C.POINTER(LocalMapBatch), vp]
+    L.orbx_create_mappoints_device.argtypes = [C.c_int, vp, vp, C.c_int, vp, C.c_float, vp, C.c_float, C.c_float,
+                                               C.c_float, C.c_float, fp, C.c_int, vp, vp, vp, vp, vp, vp, vp]
     L.orbx_search_by_projection_keyframe.argtypes = [vp, vp, i32p, vp, i32p, u8p, vp, C.c_float, C.c_int, ip]
     L.orbx_search_by_projection_sim3.argtypes = [vp, vp, fp, i32p, C.c_int, i32p, vp, C.c_int, ip]
     L.orbx_search_by_bow_frame.argtypes = [vp, vp, i32p, i32p, i32p, i32p, C.c_int, vp, i32p, i32p, i32p, C.c_int,

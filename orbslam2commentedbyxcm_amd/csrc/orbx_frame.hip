@@ -3,6 +3,8 @@
 //   Frame::UndistortKeyPoints   Frame.cc:586-628  (cv::undistortPoints, OpenCV 3.3.1)
 //   Frame::ComputeImageBounds   Frame.cc:636-665
 //   Frame::AssignFeaturesToGrid Frame.cc:351-370  (+ PosInGrid 558-567)
+//   the stereo / RGB-D MapPoints of a new keyframe (Tracking.cc:1069-1121):
+//   Frame::UnprojectStereo Frame.cc:912-927 + MapPoint::UpdateNormalAndDepth MapPoint.cc:386-439
 // so a batch extracted by orbx_extract_batch_device gets mvKeysUn and mGrid without a
 // host round trip.  Undistortion is one thread per keypoint in double precision (the
 // 5-iteration fixed point of cvUndistortPoints, same operation order as the oracle,
@@ -125,6 +127,67 @@ __global__ __launch_bounds__(kSortThreads) void k_grid(GridArgs G, const orbx_ke
         if (p == m - 1)
             for (int q = c + 1; q <= kCells; q++) cs[q] = m;  // every key valid: tail cells start at m
     }
+}
+
+// Tracking::CreateNewKeyFrame's MapPoints of B frames (one thread per keypoint slot, id
+// b*cap + i): Frame::UnprojectStereo (x3Dc = ((u-cx)*z*invfx, (v-cy)*z*invfy, z), Pos =
+// Rwc*x3Dc + Ow) and UpdateNormalAndDepth with the frame as the only observation (normal =
+// PC * (float)(1/|PC|), mfMaxDistance = |PC| * mvScaleFactors[octave], mfMinDistance =
+// mfMaxDistance / mvScaleFactors[nLevels-1]).  Float products summed left to right, norms
+// in double.  Slots without a keypoint or with z <= 0: bad.
+struct MapPointArgs {
+    const orbx_keypoint* kps;
+    const int32_t* n;
+    int cap;
+    const float* depth;    // [B][cap] mvDepth or null (const_depth for every keypoint)
+    float const_depth;
+    const float* Tcw;      // [B][12]
+    float fx, fy, cx, cy;
+    float scale[32];
+    int nlevels;
+    float* pos;
+    float* normal;
+    float* max_distance;
+    float* min_distance;
+    int32_t* observations;
+    uint8_t* bad;
+};
+
+__global__ __launch_bounds__(256) void k_create_mappoints(MapPointArgs A, int total) {
+    const int id = blockIdx.x * 256 + threadIdx.x;
+    if (id >= total) return;
+    const int b = id / A.cap, i = id - b * A.cap;
+    const int n = A.n[b] < A.cap ? A.n[b] : A.cap;
+    const float z = i < n ? (A.depth ? A.depth[id] : A.const_depth) : 0.f;
+    A.observations[id] = 0;
+    A.bad[id] = 1;
+    if (!(z > 0)) return;  // UnprojectStereo returns an empty Mat
+    const orbx_keypoint kp = A.kps[id];
+    const float* T = A.Tcw + 12 * (size_t)b;
+    const float invfx = 1.0f / A.fx, invfy = 1.0f / A.fy;
+    const float x = (kp.x - A.cx) * z * invfx;
+    const float y = (kp.y - A.cy) * z * invfy;
+    float Ow[3], P[3], PC[3];
+    for (int r = 0; r < 3; r++) Ow[r] = -(T[r] * T[3] + T[4 + r] * T[7] + T[8 + r] * T[11]);
+    for (int r = 0; r < 3; r++) P[r] = T[r] * x + T[4 + r] * y + T[8 + r] * z + Ow[r];  // Rwc[r][c] = Rcw[c][r]
+    double ss = 0.0;
+    for (int c = 0; c < 3; c++) {
+        PC[c] = P[c] - Ow[c];
+        ss += (double)PC[c] * (double)PC[c];
+    }
+    const double nrm = sqrt(ss);
+    const float inv = (float)(1.0 / nrm);
+    const float dist = (float)nrm;
+    const int oct = kp.octave < 0 ? 0 : (kp.octave >= A.nlevels ? A.nlevels - 1 : kp.octave);
+    const float mx = dist * A.scale[oct];
+    for (int c = 0; c < 3; c++) {
+        A.pos[3 * (size_t)id + c] = P[c];
+        A.normal[3 * (size_t)id + c] = PC[c] * inv;
+    }
+    A.max_distance[id] = mx;
+    A.min_distance[id] = mx / A.scale[A.nlevels - 1];
+    A.observations[id] = 1;
+    A.bad[id] = 0;
 }
 
 }  // namespace orbx
@@ -253,6 +316,44 @@ int orbx_compute_image_bounds(int device, const orbx_camera* cam, int cols, int 
     bounds[1] = u[2] > u[6] ? u[2] : u[6];  // max(top-right x, bottom-right x)
     bounds[2] = u[1] < u[3] ? u[1] : u[3];  // min(top-left y, top-right y)
     bounds[3] = u[5] > u[7] ? u[5] : u[7];  // max(bottom-left y, bottom-right y)
+    return ORBX_OK;
+}
+
+int orbx_create_mappoints_device(int batch, const orbx_keypoint* d_kps, const int32_t* d_n, int cap,
+                                 const float* d_depth, float const_depth, const float* d_Tcw, float fx, float fy,
+                                 float cx, float cy, const float* scale_factors, int nlevels, float* d_pos,
+                                 float* d_normal, float* d_max_distance, float* d_min_distance,
+                                 int32_t* d_observations, uint8_t* d_bad, void* stream) {
+    if (batch < 0 || cap <= 0 || !scale_factors || nlevels < 1 || nlevels > 32) return fail(ORBX_ERR_ARG, "bad argument");
+    if (batch == 0) return ORBX_OK;
+    if (!d_kps || !d_n || !d_Tcw || !d_pos || !d_normal || !d_max_distance || !d_min_distance || !d_observations ||
+        !d_bad)
+        return fail(ORBX_ERR_ARG, "null buffer");
+    MapPointArgs A{};
+    A.kps = d_kps;
+    A.n = d_n;
+    A.cap = cap;
+    A.depth = d_depth;
+    A.const_depth = const_depth;
+    A.Tcw = d_Tcw;
+    A.fx = fx;
+    A.fy = fy;
+    A.cx = cx;
+    A.cy = cy;
+    for (int l = 0; l < nlevels; l++) A.scale[l] = scale_factors[l];
+    A.nlevels = nlevels;
+    A.pos = d_pos;
+    A.normal = d_normal;
+    A.max_distance = d_max_distance;
+    A.min_distance = d_min_distance;
+    A.observations = d_observations;
+    A.bad = d_bad;
+    const long long total = (long long)batch * cap;
+    if (total >= (1ll << 31)) return fail(ORBX_ERR_ARG, "batch * cap too large");
+    hipLaunchKernelGGL(k_create_mappoints, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A,
+                       (int)total);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(ORBX_ERR_HIP, hipGetErrorString(e));
     return ORBX_OK;
 }
 

@@ -78,6 +78,9 @@ hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjPar
 
 hipError_t launch_seq_build(const SeqArgs& A, int npairs, ProjQuery* queries, ProjProblem* probs,
                             long long* scratch_off, hipStream_t stream);
+// k_local_build: Tracking::SearchLocalPoints' problem per frame (one workgroup each)
+hipError_t launch_local_build(const LocalArgs& A, int batch, ProjQuery* queries, uint8_t* qdesc, ProjProblem* probs,
+                              long long* scratch_off, hipStream_t stream);
 
 hipError_t launch_triangulation(const TriProblem* d_probs, int nprob, unsigned long long* scratch, int max_n2,
                                 int max_nq, hipStream_t stream);

@@ -1223,11 +1223,164 @@ __global__ __launch_bounds__(256) void k_seq_build(SeqArgs A, ProjQuery* __restr
             }
             q.post_min = -1;
             q.post_max = -1;
-            q.mp = i;
+            q.mp = A.global_ids ? (int)slot : i;
             q.angle = kp.angle;
         }
     }
     queries[slot] = q;
+}
+
+// ---- Tracking::SearchLocalPoints (Tracking.cc:1280-1336) over a batch of Frames: one
+// 1024-thread workgroup per frame builds that frame's SearchByProjection problem.
+//   1. mCurrentFrame.mvpMapPoints: a bad MapPoint is set to NULL, the others are marked
+//      as seen (mnLastFrameSeen, mbTrackInView = false) -- an LDS hash set of their ids;
+//   2. every local MapPoint (mvpLocalMapPoints order) that is neither seen nor bad goes
+//      through Frame::IsInFrustum(pMP, 0.5) (Frame.cc:412-477); those in view become the
+//      queries of SearchByProjection(F, vpLocalMapPoints, th) (ORBmatcher.cc:61-173), in
+//      list order, with r = RadiusByViewingCos(viewCos) (* th when th != 1) *
+//      mvScaleFactors[nPredictedLevel] and the levels [nPredictedLevel-1, nPredictedLevel].
+// The search itself is the projection matcher's (a11 semantics: Observations() blocking,
+// the ratio test on equal levels).  Queries not in view keep their slot with mp = -1.
+constexpr int kLocalThreads = 1024;
+
+__device__ __forceinline__ unsigned local_hash(int id, int mask) {
+    return ((unsigned)id * 2654435761u) & (unsigned)mask;
+}
+
+__global__ __launch_bounds__(kLocalThreads) void k_local_build(LocalArgs A, ProjQuery* __restrict__ queries,
+                                                               uint8_t* __restrict__ qdesc,
+                                                               ProjProblem* __restrict__ probs,
+                                                               long long* __restrict__ scratch_off) {
+    extern __shared__ int hset[];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int mask = A.hash_size - 1;
+    const int n = A.n[b] < A.cap ? A.n[b] : A.cap;
+    int32_t* fmp = A.frame_mp + (size_t)b * A.cap;
+    for (int t = tid; t < A.hash_size; t += kLocalThreads) hset[t] = -1;
+    __syncthreads();
+    for (int i = tid; i < n; i += kLocalThreads) {
+        const int mp = fmp[i];
+        if (mp < 0) continue;
+        if (A.bad && A.bad[mp]) {  // Tracking.cc:1288-1290
+            fmp[i] = -1;
+            continue;
+        }
+        unsigned h = local_hash(mp, mask);
+        while (true) {  // open addressing; a frame holds at most cap < hash_size / 2 ids
+            const int old = atomicCAS(&hset[h], -1, mp);
+            if (old == -1 || old == mp) break;
+            h = (h + 1) & (unsigned)mask;
+        }
+    }
+    __syncthreads();
+    const int lo = A.local_off[b], hi = A.local_off[b + 1];
+    const float* T = A.Tcw + 12 * (size_t)b;
+    float Ow[3];  // mOw = -Rcw^T tcw
+    for (int c = 0; c < 3; c++) Ow[c] = -(T[c] * T[3] + T[4 + c] * T[7] + T[8 + c] * T[11]);
+    const bool bFactor = A.th != 1.0f;  // ORBmatcher.cc:66
+    for (int j = lo + tid; j < hi; j += kLocalThreads) {
+        const int mp = A.local_ids[j];
+        ProjQuery q{};
+        q.mp = -1;
+        bool in_view = !(A.bad && A.bad[mp]);
+        if (in_view) {  // pMP->mnLastFrameSeen == mCurrentFrame.mnId (Tracking.cc:1306-1307)
+            unsigned h = local_hash(mp, mask);
+            while (true) {
+                const int v = hset[h];
+                if (v == mp) {
+                    in_view = false;
+                    break;
+                }
+                if (v == -1) break;
+                h = (h + 1) & (unsigned)mask;
+            }
+        }
+        float u = 0.f, v = 0.f, ur = 0.f, viewCos = 0.f;
+        int pred = 0;
+        if (in_view) {  // Frame::IsInFrustum (Frame.cc:412-477)
+            const float* P = A.pos + 3 * (size_t)mp;
+            float Pc[3];
+            for (int r = 0; r < 3; r++) Pc[r] = T[4 * r] * P[0] + T[4 * r + 1] * P[1] + T[4 * r + 2] * P[2] + T[4 * r + 3];
+            in_view = !(Pc[2] < 0.0f);
+            if (in_view) {
+                const float invz = 1.0f / Pc[2];
+                u = A.fx * Pc[0] * invz + A.cx;
+                v = A.fy * Pc[1] * invz + A.cy;
+                ur = u - A.bf * invz;
+                in_view = !(u < A.min_x || u > A.max_x) && !(v < A.min_y || v > A.max_y);
+            }
+            if (in_view) {
+                const float maxDistance = 1.2f * A.max_distance[mp];
+                const float minDistance = 0.8f * A.min_distance[mp];
+                float PO[3];
+                for (int c = 0; c < 3; c++) PO[c] = P[c] - Ow[c];
+                double ss = 0.0;  // cv::norm: squares in double
+                for (int c = 0; c < 3; c++) ss += (double)PO[c] * (double)PO[c];
+                const float dist = (float)sqrt(ss);
+                in_view = !(dist < minDistance || dist > maxDistance);
+                if (in_view) {
+                    const float* Pn = A.normal + 3 * (size_t)mp;
+                    double dot = 0.0;  // Mat::dot in double
+                    for (int c = 0; c < 3; c++) dot += (double)PO[c] * (double)Pn[c];
+                    viewCos = (float)(dot / (double)dist);
+                    in_view = !(viewCos < A.cos_limit);
+                    if (in_view) {  // MapPoint::PredictScale(dist, Frame*) (MapPoint.cc:494-509)
+                        const float ratio = A.max_distance[mp] / dist;
+                        int ns = (int)ceil(log((double)ratio) / (double)A.log_scale);
+                        pred = ns < 0 ? 0 : (ns >= A.nlevels ? A.nlevels - 1 : ns);
+                    }
+                }
+            }
+        }
+        if (in_view) {
+            float r = (double)viewCos > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos, ORBmatcher.cc:176-183
+            if (bFactor) r *= A.th;
+            q.u = u;
+            q.v = v;
+            q.ur = ur;
+            q.r = r * A.scale[pred];
+            q.er_max = r * A.scale[pred];
+            q.min_level = pred - 1;
+            q.max_level = pred;
+            q.post_min = -1;
+            q.post_max = -1;
+            q.mp = mp;
+            q.angle = 0.f;
+            const uint4* src = (const uint4*)(A.mdesc + (size_t)mp * 32);
+            uint4* dst = (uint4*)(qdesc + (size_t)j * 32);
+            dst[0] = src[0];
+            dst[1] = src[1];
+        }
+        queries[j] = q;
+    }
+    if (tid == 0) {
+        ProjProblem pb{};
+        pb.keys = A.kps + (size_t)b * A.cap;
+        pb.desc = A.desc + (size_t)b * A.cap * 32;
+        pb.u_right = A.u_right ? A.u_right + (size_t)b * A.cap : nullptr;
+        pb.frame_mp = fmp;
+        pb.n = n;
+        pb.q = queries + lo;
+        pb.qdesc = qdesc + (size_t)lo * 32;
+        pb.nq = hi - lo;
+        pb.min_x = A.min_x;
+        pb.min_y = A.min_y;
+        pb.inv_w = (float)kGridCols / (A.max_x - A.min_x);
+        pb.inv_h = (float)kGridRows / (A.max_y - A.min_y);
+        pb.nmatches = A.nmatches + b;
+        probs[b] = pb;
+        scratch_off[b] = (long long)lo * kProjScratchWords;
+    }
+}
+
+hipError_t launch_local_build(const LocalArgs& A, int batch, ProjQuery* queries, uint8_t* qdesc, ProjProblem* probs,
+                              long long* scratch_off, hipStream_t stream) {
+    if (batch <= 0) return hipSuccess;
+    if (A.hash_size < 2 * A.cap || (A.hash_size & (A.hash_size - 1)) || A.hash_size > 16384)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_local_build, dim3(batch), dim3(kLocalThreads), (size_t)A.hash_size * 4, stream, A, queries,
+                       qdesc, probs, scratch_off);
+    return hipGetLastError();
 }
 
 hipError_t launch_seq_build(const SeqArgs& A, int npairs, ProjQuery* queries, ProjProblem* probs,

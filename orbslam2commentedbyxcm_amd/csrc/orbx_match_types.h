@@ -81,10 +81,41 @@ struct SeqArgs {
     float min_x, max_x, min_y, max_y;
     float depth;               // depth model: MapPoint depth along the last frame's rays
     int mono;                  // bMono
+    int global_ids;            // MapPoint ids written: 0 = LastFrame keypoint index i, 1 = (b-1)*cap + i
     float th;                  // search radius factor
     float scale[32];           // mvScaleFactors
     int32_t* cur_mp;           // [B][cap] out (pre-filled -1)
     int32_t* nmatches;         // [B] out
+};
+
+// Tracking::SearchLocalPoints over a batch of Frames (orbx_search_local_points_device):
+// Frame::IsInFrustum of every local MapPoint, then SearchByProjection(Frame&, vector<MapPoint*>, th).
+struct LocalArgs {
+    const orbx_keypoint* kps;  // [B][cap] mvKeysUn
+    const uint8_t* desc;       // [B][cap][32]
+    const int32_t* n;          // [B]
+    const float* u_right;      // [B][cap] or null
+    int cap;
+    const float* Tcw;          // [B][12]
+    float fx, fy, cx, cy, bf;
+    float min_x, max_x, min_y, max_y;
+    float scale[32];           // mvScaleFactors
+    int nlevels;
+    float log_scale;           // mfLogScaleFactor = (float)log(mfScaleFactor)
+    int nmp;                   // MapPoint table
+    const float* pos;          // [nmp][3]
+    const uint8_t* mdesc;      // [nmp][32]
+    const float* normal;       // [nmp][3]
+    const float* max_distance; // [nmp] mfMaxDistance
+    const float* min_distance; // [nmp] mfMinDistance
+    const uint8_t* bad;        // [nmp] or null
+    const int32_t* local_off;  // [B+1] frame b's local map = local_ids[local_off[b] .. local_off[b+1])
+    const int32_t* local_ids;
+    float th;                  // SearchByProjection th
+    float cos_limit;           // IsInFrustum viewingCosLimit
+    int32_t* frame_mp;         // [B][cap] in/out: mvpMapPoints as MapPoint ids
+    int32_t* nmatches;         // [B] out
+    int hash_size;             // LDS hash slots (power of two >= 2 cap)
 };
 
 // SearchForTriangulation: one unmatched KF1 keypoint of a shared vocabulary node.

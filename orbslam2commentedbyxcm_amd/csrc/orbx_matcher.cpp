@@ -211,6 +211,9 @@ struct orbx_matcher {
     // tables of orbx_search_for_triangulation_batch_device (device-only)
     char* tscr = nullptr;
     size_t tscr_cap = 0;
+    // queries, problems and grids of orbx_search_local_points_device (device-only)
+    char* lscr = nullptr;
+    size_t lscr_cap = 0;
     StageRing stage;
 };
 
@@ -328,6 +331,7 @@ void orbx_matcher_destroy(orbx_matcher* m) {
     m->arena.release();
     if (m->dscr) (void)hipFree(m->dscr);
     if (m->tscr) (void)hipFree(m->tscr);
+    if (m->lscr) (void)hipFree(m->lscr);
     m->stage.release();
     for (auto& slot : m->ev)
         for (auto& e : slot)
@@ -649,6 +653,7 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
     A.max_y = sq->max_y;
     A.depth = sq->depth;
     A.mono = sq->mono ? 1 : 0;
+    A.global_ids = sq->global_ids ? 1 : 0;
     A.th = sq->th;
     for (int l = 0; l < nlevels; l++) A.scale[l] = sq->scale_factors[l];
     A.cur_mp = d_cur_mp;
@@ -722,6 +727,114 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
                 ph[3] / npairs, mx[3], resc / npairs, nq / npairs, tres / npairs, nit / npairs, tfirst / npairs,
                 tbit / npairs, tfill / npairs, tbuild / npairs, rtrunc / npairs);
     }
+    return ORBX_OK;
+}
+
+// Tracking::SearchLocalPoints for a batch of Frames in HBM (see include/orbx.h)
+int orbx_search_local_points_device(orbx_matcher* m, const orbx_mappoints_device* mps,
+                                    const orbx_local_map_batch* lm, void* stream) {
+    if (!m || !mps || !lm) return fail(ORBX_ERR_ARG, "null argument");
+    const int B = lm->batch, cap = lm->cap, nlevels = lm->nlevels;
+    if (B < 0 || cap <= 0 || cap >= 8192 || !lm->scale_factors || nlevels < 2 || nlevels > 32 || !lm->local_off)
+        return fail(ORBX_ERR_ARG, "bad argument");
+    if (B == 0) return ORBX_OK;
+    if (!lm->kps || !lm->desc || !lm->n || !lm->Tcw || !lm->frame_mp || !lm->nmatches || !mps->pos || !mps->desc ||
+        !mps->normal || !mps->max_distance || !mps->min_distance || !mps->observations)
+        return fail(ORBX_ERR_ARG, "null buffer");
+    int maxnq = 0;
+    for (int b = 0; b < B; b++) {
+        const int c = lm->local_off[b + 1] - lm->local_off[b];
+        if (lm->local_off[b] < 0 || c < 0) return fail(ORBX_ERR_ARG, "local_off must be non-decreasing from 0");
+        if (c > maxnq) maxnq = c;
+    }
+    const int total = lm->local_off[B];
+    if (maxnq >= 8192) return fail(ORBX_ERR_ARG, "a local map of 8192 or more MapPoints");
+    if (total > 0 && !lm->local_ids) return fail(ORBX_ERR_ARG, "null local_ids");
+    const int gcap = cap > maxnq ? cap : maxnq;  // grid / query capacity of one problem
+    HIP_TRY(hipSetDevice(m->device));
+    hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+    const bool split = m->footprint == 2;
+    const bool grids = split || m->footprint == 5;
+    const size_t nt = (size_t)(total > 0 ? total : 1);
+    const size_t need = pad(sizeof(ProjQuery) * nt) + pad(nt * 32) + pad(sizeof(ProjProblem) * B) +
+                        pad(sizeof(long long) * B) + pad(sizeof(unsigned long long) * kProjScratchWords * nt) +
+                        pad(sizeof(int32_t) * (B + 1)) + (grids ? pad(seq_grid_bytes(gcap, nlevels) * B) : 0);
+    if (m->lscr_cap < need) {
+        HIP_TRY(hipStreamSynchronize(s));
+        if (m->lscr) HIP_TRY(hipFree(m->lscr));
+        m->lscr = nullptr;
+        m->lscr_cap = 0;
+        HIP_TRY(hipMalloc((void**)&m->lscr, need));
+        m->lscr_cap = need;
+    }
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        char* p = m->lscr + o;
+        o += pad(bytes);
+        return p;
+    };
+    auto* d_q = (ProjQuery*)take(sizeof(ProjQuery) * nt);
+    auto* d_qd = (uint8_t*)take(nt * 32);
+    auto* d_prob = (ProjProblem*)take(sizeof(ProjProblem) * B);
+    auto* d_off = (long long*)take(sizeof(long long) * B);
+    auto* d_scr = (unsigned long long*)take(sizeof(unsigned long long) * kProjScratchWords * nt);
+    auto* d_loff = (int32_t*)take(sizeof(int32_t) * (B + 1));
+    auto* d_grids = grids ? (unsigned char*)take(seq_grid_bytes(gcap, nlevels) * B) : nullptr;
+    char* h = nullptr;
+    int slot = 0;
+    HIP_TRY(m->stage.get(sizeof(int32_t) * (B + 1), &h, &slot));
+    std::memcpy(h, lm->local_off, sizeof(int32_t) * (B + 1));
+    HIP_TRY(hipMemcpyAsync(d_loff, h, sizeof(int32_t) * (B + 1), hipMemcpyHostToDevice, s));
+    HIP_TRY(m->stage.copied(slot, s));
+    LocalArgs A{};
+    A.kps = lm->kps;
+    A.desc = lm->desc;
+    A.n = lm->n;
+    A.u_right = lm->u_right;
+    A.cap = cap;
+    A.Tcw = lm->Tcw;
+    A.fx = lm->fx;
+    A.fy = lm->fy;
+    A.cx = lm->cx;
+    A.cy = lm->cy;
+    A.bf = lm->bf;
+    A.min_x = lm->min_x;
+    A.max_x = lm->max_x;
+    A.min_y = lm->min_y;
+    A.max_y = lm->max_y;
+    for (int l = 0; l < nlevels; l++) A.scale[l] = lm->scale_factors[l];
+    A.nlevels = nlevels;
+    A.log_scale = (float)std::log((double)lm->scale_factors[1]);  // Frame::mfLogScaleFactor
+    A.nmp = mps->n;
+    A.pos = mps->pos;
+    A.mdesc = mps->desc;
+    A.normal = mps->normal;
+    A.max_distance = mps->max_distance;
+    A.min_distance = mps->min_distance;
+    A.bad = mps->bad;
+    A.local_off = d_loff;
+    A.local_ids = lm->local_ids;
+    A.th = lm->th;
+    A.cos_limit = lm->viewing_cos_limit;
+    A.frame_mp = lm->frame_mp;
+    A.nmatches = lm->nmatches;
+    int hs = 256;
+    while (hs < 2 * cap) hs <<= 1;
+    A.hash_size = hs;
+    HIP_TRY(launch_local_build(A, B, d_q, d_qd, d_prob, d_off, s));
+    ProjParams P{};
+    P.mp_obs = mps->observations;
+    P.blocked_mode = 0;  // a keypoint whose MapPoint has Observations() > 0 is taken (ORBmatcher.cc:117-119)
+    P.accept_th = TH_HIGH;
+    P.ratio_mode = 1;
+    P.nnratio = m->nnratio;
+    P.check_ori = 0;
+    P.noct = nlevels;
+    if (split)
+        HIP_TRY(launch_seq_split(d_prob, B, P, d_grids, gcap, d_scr, d_off, s));
+    else
+        HIP_TRY(launch_proj_search(d_prob, B, P, d_scr, d_off, gcap, gcap, s, m->footprint == 1, m->footprint == 3,
+                                   m->footprint == 4, m->footprint == 5 ? d_grids : nullptr));
     return ORBX_OK;
 }
 

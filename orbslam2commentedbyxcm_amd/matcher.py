@@ -428,7 +428,7 @@ class ORBmatcher:
     def match_sequence_device_ex(self, d_kps, d_desc, d_n, d_Tcw, d_cur_mp, d_nmatches, scale_factors, fx, fy, cx,
                                  cy, width, height, th: float = 15.0, mono: bool = True, bf: float = 0.0,
                                  b: float = 0.0, d_u_right=None, d_mp_pos=None, d_has_mp=None, depth: float = 5.0,
-                                 stream=None) -> None:
+                                 global_ids: bool = False, stream=None) -> None:
         """orbx_match_sequence_device_ex: TrackWithMotionModel's SearchByProjection(frame b,
         frame b-1, th, mono) for every b >= 1 of a device sequence, stereo included
         (d_u_right (B, cap) f32), LastFrame MapPoints at d_mp_pos (B, cap, 3) f32 (or at
@@ -444,10 +444,45 @@ class ORBmatcher:
         q.min_x, q.max_x, q.min_y, q.max_y = 0.0, float(width), 0.0, float(height)
         q.nlevels = len(sf)
         q.scale_factors = sf.ctypes.data_as(F32P)
-        q.th, q.mono = th, 1 if mono else 0
+        q.th, q.mono, q.global_ids = th, 1 if mono else 0, 1 if global_ids else 0
         q.cur_mp, q.nmatches = ptr(d_cur_mp), ptr(d_nmatches)
         s = None if stream is None else C.c_void_p(getattr(stream, "cuda_stream", stream))
         L.check(L.lib().orbx_match_sequence_device_ex(self._h, C.byref(q), s))
+
+    def search_local_points_device(self, mps: dict, d_kps, d_desc, d_n, d_Tcw, local_off, d_local_ids, d_frame_mp,
+                                   d_nmatches, scale_factors, fx, fy, cx, cy, width, height, th: float = 1.0,
+                                   viewing_cos_limit: float = 0.5, bf: float = 0.0, d_u_right=None,
+                                   stream=None) -> None:
+        """orbx_search_local_points_device: Tracking::SearchLocalPoints (IsInFrustum +
+        SearchByProjection(F, vpLocalMapPoints, th)) for every frame of a device batch.
+        mps: device tensors pos (n, 3) f32, desc (n, 32) u8, normal (n, 3) f32,
+        max_distance / min_distance (n,) f32, observations (n,) i32, optional bad (n,) u8;
+        local_off (B + 1) host ints, d_local_ids device i32; d_frame_mp (B, cap) i32 in/out,
+        d_nmatches (B,) i32 out.  Asynchronous."""
+        B, cap = d_desc.shape[0], d_desc.shape[1]
+        ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
+        mv = L.MapPointsDevice()
+        mv.n = int(mps["pos"].shape[0])
+        mv.pos, mv.desc, mv.normal = ptr(mps["pos"]), ptr(mps["desc"]), ptr(mps["normal"])
+        mv.max_distance, mv.min_distance = ptr(mps["max_distance"]), ptr(mps["min_distance"])
+        mv.observations, mv.bad = ptr(mps["observations"]), ptr(mps.get("bad"))
+        sf = _f32(scale_factors)
+        off = np.ascontiguousarray(local_off, dtype=np.int32)
+        if len(off) != B + 1:
+            raise ValueError("local_off needs batch + 1 entries")
+        q = L.LocalMapBatch()
+        q.batch, q.cap = B, cap
+        q.kps, q.desc, q.n, q.u_right, q.Tcw = ptr(d_kps), ptr(d_desc), ptr(d_n), ptr(d_u_right), ptr(d_Tcw)
+        q.fx, q.fy, q.cx, q.cy, q.bf = fx, fy, cx, cy, bf
+        q.min_x, q.max_x, q.min_y, q.max_y = 0.0, float(width), 0.0, float(height)
+        q.nlevels = len(sf)
+        q.scale_factors = sf.ctypes.data_as(F32P)
+        q.local_off = off.ctypes.data_as(I32P)
+        q.local_ids = ptr(d_local_ids)
+        q.th, q.viewing_cos_limit = th, viewing_cos_limit
+        q.frame_mp, q.nmatches = ptr(d_frame_mp), ptr(d_nmatches)
+        s = None if stream is None else C.c_void_p(getattr(stream, "cuda_stream", stream))
+        L.check(L.lib().orbx_search_local_points_device(self._h, C.byref(mv), C.byref(q), s))
 
     def set_timing(self, enable: bool = True) -> None:
         L.check(L.lib().orbx_matcher_set_timing(self._h, 1 if enable else 0))
@@ -479,6 +514,32 @@ class ORBmatcher:
                                           *(L.i32ptr(out[k]) for k in ("best_idx", "best_dist", "best_level",
                                                                        "second_dist", "second_level"))))
         return out
+
+
+def create_mappoints_device(d_kps, d_n, d_Tcw, scale_factors, fx, fy, cx, cy, out: dict, d_depth=None,
+                            const_depth: float = 0.0, stream=None) -> None:
+    """orbx_create_mappoints_device: the MapPoints of B frames (id b*cap + i) into the device
+    tensors of `out` -- pos / normal (B*cap, 3) f32, max_distance / min_distance (B*cap,)
+    f32, observations (B*cap,) i32, bad (B*cap,) u8.  Asynchronous."""
+    B, cap = d_kps.shape[0], d_kps.shape[1]
+    sf = _f32(scale_factors)
+    ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
+    s = None if stream is None else C.c_void_p(getattr(stream, "cuda_stream", stream))
+    L.check(L.lib().orbx_create_mappoints_device(
+        B, ptr(d_kps), ptr(d_n), cap, ptr(d_depth), float(const_depth), ptr(d_Tcw), fx, fy, cx, cy,
+        sf.ctypes.data_as(F32P), len(sf), ptr(out["pos"]), ptr(out["normal"]), ptr(out["max_distance"]),
+        ptr(out["min_distance"]), ptr(out["observations"]), ptr(out["bad"]), s))
+
+
+def mappoint_table(B: int, cap: int, device) -> dict:
+    """Device tensors for create_mappoints_device / search_local_points_device (id b*cap + i)."""
+    import torch
+    f32 = dict(dtype=torch.float32, device=device)
+    N = B * cap
+    return {"pos": torch.empty((N, 3), **f32), "normal": torch.empty((N, 3), **f32),
+            "max_distance": torch.empty((N,), **f32), "min_distance": torch.empty((N,), **f32),
+            "observations": torch.empty((N,), dtype=torch.int32, device=device),
+            "bad": torch.empty((N,), dtype=torch.uint8, device=device)}
 
 
 def ComputeDistinctiveDescriptors(off, desc, device: int = 0):

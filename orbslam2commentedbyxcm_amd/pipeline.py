@@ -3,7 +3,9 @@
 One step = ORBextractor::operator() on B frames (ORBextractor.cc:1513-1629) plus
 TrackWithMotionModel's SearchByProjection(CurrentFrame, LastFrame, th, bMono)
 (Tracking.cc:966-994, ORBmatcher.cc:1620-1789) of every frame against its predecessor,
-all in HBM:
+and optionally (local_map=True) TrackLocalMap's SearchLocalPoints (Tracking.cc:1280-1336:
+IsInFrustum + SearchByProjection(F, vpLocalMapPoints, th), ORBmatcher.cc:61-173) of every
+frame against the MapPoints of its `local_window` predecessors, all in HBM:
 
 * the batch is split into `lanes` contiguous chunks, each extracted by its own
   ORBextractor on its own HIP stream, so one chunk's latency-bound kernels (octree,
@@ -33,7 +35,8 @@ class SequencePipeline:
                  nnratio: float = 0.9, check_ori: bool = True, match_stream=None,
                  nbuf: int = 2, matcher_mode: int | None = None, match_after_stage: int = 0,
                  lane_offset_stage: int = 2, match_cu_stride: int = 1,
-                 match_priority: int = 0, on_matched=None):
+                 match_priority: int = 0, on_matched=None, local_map: bool = False, local_window: int = 3,
+                 local_th: float = 1.0):
         import torch
 
         self.B, self.W, self.H = int(batch), int(width), int(height)
@@ -69,6 +72,23 @@ class SequencePipeline:
         self.matcher.set_footprint(5 if matcher_mode is None else matcher_mode)
         self.sf = self.exs[0].GetScaleFactors()
         self.cap = self.exs[0].max_keypoints(self.W, self.H)
+        # TrackLocalMap stage: every keypoint of the batch makes a MapPoint (id b*cap + i,
+        # at `depth` on its ray: Tracking::CreateNewKeyFrame's UnprojectStereo), which
+        # TrackWithMotionModel projects (global ids) and frame b's local map lists -- the
+        # MapPoints of frames b-1 .. b-local_window, every slot (empty slots are bad).
+        # SearchLocalPoints uses ORBmatcher(0.8) (Tracking.cc:1320).
+        self.local_map = bool(local_map) and self.match
+        self.local_th = float(local_th)
+        if self.local_map:
+            self.lmatcher = ORBmatcher(0.8, False, device=device)
+            self.lmatcher.set_footprint(5 if matcher_mode is None else matcher_mode)
+            off, ids = [0], []
+            for b in range(self.B):
+                for f in range(max(0, b - int(local_window)), b):
+                    ids.append(np.arange(f * self.cap, (f + 1) * self.cap, dtype=np.int32))
+                off.append(off[-1] + (b - max(0, b - int(local_window))) * self.cap)
+            self.local_off = np.array(off, np.int32)
+            self.d_local_ids = torch.from_numpy(np.concatenate(ids) if ids else np.zeros(1, np.int32)).to(self.dev)
         self.bounds = [(self.B * c // self.S, self.B * (c + 1) // self.S) for c in range(self.S)]
         self.streams = [torch.cuda.ExternalStream(e.stream_handle(), device=self.dev) for e in self.exs]
         nbuf = max(2, int(nbuf)) if self.pipelined else 1
@@ -79,6 +99,11 @@ class SequencePipeline:
         self.n = [torch.empty((B,), **i32) for _ in range(nbuf)]
         self.mp = [torch.empty((B, cap), **i32) for _ in range(nbuf)]
         self.nm = [torch.empty((B,), **i32) for _ in range(nbuf)]
+        if self.local_map:
+            from .matcher import mappoint_table
+            self.tab = [mappoint_table(B, cap, self.dev) for _ in range(nbuf)]
+            self.nm_local = [torch.empty((B,), **i32) for _ in range(nbuf)]
+            self._lt = []  # (start, end) event pairs of the local stage while timing
         self.ev_ex = [[torch.cuda.Event() for _ in range(self.S)] for _ in range(nbuf)]  # [buffer][lane]
         self.ev_m = [torch.cuda.Event() for _ in range(nbuf)]
         self.used = [False] * nbuf
@@ -100,6 +125,7 @@ class SequencePipeline:
         # enqueues on self.ms there (e.g. copying the results out) finishes before the
         # buffer is overwritten
         self.on_matched = on_matched
+        self._timing = False
         self.it = 0            # extractions issued
         self.pending = None    # buffer extracted but not yet matched (pipelined)
         self.last = None       # buffer holding the newest complete result
@@ -141,12 +167,40 @@ class SequencePipeline:
             from .extractor import stream_wait_event
             for ev in self.stage_ev:
                 stream_wait_event(self.ms.cuda_stream, ev)
-        self.matcher.match_sequence_device(self.kps[b], self.desc[b], self.n[b], Tcw, self.mp[b], self.nm[b],
-                                           self.sf, self.fx, self.fy, self.cx, self.cy, self.W, self.H,
-                                           depth=self.depth, th=self.th, stream=self.ms.cuda_stream)
+        if self.local_map:
+            self._match_local(b, Tcw)
+        else:
+            self.matcher.match_sequence_device(self.kps[b], self.desc[b], self.n[b], Tcw, self.mp[b], self.nm[b],
+                                               self.sf, self.fx, self.fy, self.cx, self.cy, self.W, self.H,
+                                               depth=self.depth, th=self.th, stream=self.ms.cuda_stream)
         if self.on_matched is not None:
             self.on_matched(b)
         self.ev_m[b].record(self.ms)
+
+    def _match_local(self, b, Tcw):
+        """MapPoints of the batch, TrackWithMotionModel against them, then SearchLocalPoints."""
+        import torch
+
+        from .matcher import create_mappoints_device
+        s = self.ms.cuda_stream
+        tab = self.tab[b]
+        create_mappoints_device(self.kps[b], self.n[b], Tcw, self.sf, self.fx, self.fy, self.cx, self.cy, tab,
+                                const_depth=self.depth, stream=s)
+        self.matcher.match_sequence_device_ex(self.kps[b], self.desc[b], self.n[b], Tcw, self.mp[b], self.nm[b],
+                                              self.sf, self.fx, self.fy, self.cx, self.cy, self.W, self.H,
+                                              th=self.th, d_mp_pos=tab["pos"], global_ids=True, stream=s)
+        timed = self._timing
+        if timed:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(self.ms)
+        mps = dict(tab, desc=self.desc[b].view(-1, 32))
+        self.lmatcher.search_local_points_device(mps, self.kps[b], self.desc[b], self.n[b], Tcw, self.local_off,
+                                                 self.d_local_ids, self.mp[b], self.nm_local[b], self.sf, self.fx,
+                                                 self.fy, self.cx, self.cy, self.W, self.H, th=self.local_th,
+                                                 stream=s)
+        if timed:
+            ev[1].record(self.ms)
+            self._lt.append(ev)
 
     def step(self, frames, Tcw):
         """Issue one step (asynchronous).  Pipelined: extracts this batch and matches the
@@ -185,15 +239,21 @@ class SequencePipeline:
         """Device tensors of the newest complete batch, or of buffer b (call after
         synchronising, or after ev_m[b] for a buffer whose matching was issued)."""
         b = self.last if b is None else b
-        return {"kps": self.kps[b], "desc": self.desc[b], "n": self.n[b], "mp": self.mp[b], "nm": self.nm[b]}
+        r = {"kps": self.kps[b], "desc": self.desc[b], "n": self.n[b], "mp": self.mp[b], "nm": self.nm[b]}
+        if self.local_map:
+            r["nm_local"] = self.nm_local[b]
+        return r
 
     def host_results(self, b=None) -> dict:
         r = self.results(b)
         B, cap = self.B, self.cap
         from . import _lib as L
-        return {"kps": r["kps"].cpu().numpy().view(np.uint8).reshape(B, cap, 28).view(L.KEYPOINT_DTYPE).reshape(B, cap),
-                "desc": r["desc"].cpu().numpy(), "n": r["n"].cpu().numpy(), "mp": r["mp"].cpu().numpy(),
-                "nm": r["nm"].cpu().numpy()}
+        out = {"kps": r["kps"].cpu().numpy().view(np.uint8).reshape(B, cap, 28).view(L.KEYPOINT_DTYPE).reshape(B, cap),
+               "desc": r["desc"].cpu().numpy(), "n": r["n"].cpu().numpy(), "mp": r["mp"].cpu().numpy(),
+               "nm": r["nm"].cpu().numpy()}
+        if "nm_local" in r:
+            out["nm_local"] = r["nm_local"].cpu().numpy()
+        return out
 
     def status(self) -> np.ndarray:
         """Octree status words of every frame of the newest extraction (0 = complete)."""
@@ -204,6 +264,9 @@ class SequencePipeline:
             e.set_timing(enable)
         if self.match:
             self.matcher.set_timing(enable)
+        self._timing = bool(enable)
+        if enable and self.local_map:
+            self._lt = []
 
     def stage_times(self) -> dict:
         """HIP-event stage times (ms per launch) averaged over the lanes' extractors (each
@@ -212,6 +275,8 @@ class SequencePipeline:
         out = {k: sum(p[k] for p in per) / len(per) for k in per[0]}
         if self.match:
             out["match"] = self.matcher.last_ms()
+        if self.local_map and self._lt:
+            out["local_map"] = sum(a.elapsed_time(b) for a, b in self._lt) / len(self._lt)
         return out
 
 

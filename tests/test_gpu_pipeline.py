@@ -136,3 +136,39 @@ def test_sequence_pipeline_distinct_batch_every_step(oracle, orbx_built, B, lane
         r = checks.check_sequence(frames, sequence_poses(off), res, pl.sf)
         assert r["frames_mismatched"] == 0 and r["pairs_mismatched"] == 0, (j, r)
         assert r["mean_matches_per_pair_ref"] > 200, (j, r)
+
+
+@pytest.mark.parametrize("B,lanes,pipelined,steps,mode", [(16, 2, True, 3, None), (12, 1, False, 2, None),
+                                                          (256, 2, True, 2, None), (24, 2, True, 3, 2)])
+def test_sequence_pipeline_local_map_matches_oracle(oracle, orbx_built, B, lanes, pipelined, steps, mode):
+    """The front end with TrackLocalMap: MapPoints of every keypoint (CreateNewKeyFrame's
+    UnprojectStereo at the model depth), TrackWithMotionModel against them, then
+    SearchLocalPoints against the MapPoints of the three previous frames; every frame's
+    final mvpMapPoints and both match counts against the oracle, on distinct batches."""
+    import torch
+
+    batches = [synth.sequence(3000 + j, B) for j in range(steps)]
+    snaps = []
+    pl = None
+
+    def grab(b):
+        snaps.append({k: v.clone() for k, v in pl.results(b).items()})
+
+    pl = SequencePipeline(B, 640, 480, lanes=lanes, pipelined=pipelined, on_matched=grab, local_map=True,
+                          matcher_mode=mode)
+    dev_in = [(torch.from_numpy(f).to(pl.dev), torch.from_numpy(sequence_poses(o)).to(pl.dev)) for f, o in batches]
+    torch.cuda.synchronize()
+    with torch.cuda.stream(pl.ms):
+        for frames, T in dev_in:
+            pl.step(frames, T)
+        pl.drain()
+    torch.cuda.synchronize()
+    assert len(snaps) == steps
+    from orbslam2commentedbyxcm_amd import _lib as L
+    cap = pl.cap
+    for j, ((frames, off), snap) in enumerate(zip(batches, snaps)):
+        res = {k: v.cpu().numpy() for k, v in snap.items() if k != "kps"}
+        res["kps"] = snap["kps"].cpu().numpy().view(np.uint8).reshape(B, cap, 28).view(L.KEYPOINT_DTYPE).reshape(B, cap)
+        r = checks.check_sequence_local(frames, sequence_poses(off), res, pl.sf, cap)
+        assert r["bit_exact"], (j, r)
+        assert r["mean_matches_per_pair_ref"] > 200 and r["mean_local_matches_ref"] > 50, (j, r)

@@ -278,3 +278,159 @@ def test_posed_match_sequence_device(oracle, orbx_built, stereo, check_ori, foot
     if stereo:
         assert forward >= 2 and backward >= 2
     assert max(occupied) >= 2
+
+
+def _sequence_on_gpu(oracle, B, seed, prm=S.C1):
+    import torch
+
+    from orbslam2commentedbyxcm_amd import ORBextractor
+    imgs, rels, T = S.posed_sequence(seed, B)
+    dev = torch.device("cuda", 0)
+    ex = ORBextractor(*prm)
+    cap = ex.max_keypoints(640, 480)
+    d_kps = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)
+    d_desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
+    d_n = torch.empty((B,), dtype=torch.int32, device=dev)
+    ex.extract_batch_device(torch.from_numpy(imgs).to(dev), d_kps, d_desc, d_n)
+    torch.cuda.synchronize()
+    n = d_n.cpu().numpy()
+    kps = d_kps.cpu().numpy().view(np.uint8).reshape(B, cap, 28).view(oracle.KEYPOINT_DTYPE).reshape(B, cap)
+    return dict(ex=ex, cap=cap, d_kps=d_kps, d_desc=d_desc, d_n=d_n, n=n, kps=kps, desc=d_desc.cpu().numpy(),
+                rels=rels, T=T, dev=dev)
+
+
+def _mappoint_table(seq, seed):
+    """Every keypoint of the sequence as a MapPoint (id = frame * cap + index): world
+    position on the plane, MapPoint::UpdateNormalAndDepth's normal and distances from the
+    frame that made it, Observations() in 0..3, a few bad."""
+    rng = np.random.default_rng(seed)
+    B, cap = len(seq["n"]), seq["cap"]
+    N = B * cap
+    pos = np.zeros((N, 3), np.float32)
+    desc = np.zeros((N, 32), np.uint8)
+    nrm = np.zeros((N, 3), np.float32)
+    mx = np.ones(N, np.float32)
+    mn = np.ones(N, np.float32)
+    sf = seq["ex"].GetScaleFactors()
+    for f in range(B):
+        k = seq["kps"][f][: seq["n"][f]]
+        X, _ = S.plane_points(seq["rels"][f], k["x"], k["y"])
+        P = S.to_world(X * (1.0 + rng.normal(0, 0.002, len(k)))[:, None]).astype(np.float32)
+        T = np.vstack([seq["T"][f].reshape(3, 4), [0, 0, 0, 1]]).astype(np.float32)
+        Ow = -(T[:3, :3].T @ T[:3, 3])
+        PO = P - Ow[None, :]
+        dist = np.linalg.norm(PO.astype(np.float64), axis=1).astype(np.float32)
+        sl = slice(f * cap, f * cap + len(k))
+        pos[sl], desc[sl] = P, seq["desc"][f][: len(k)]
+        nrm[sl] = (PO / dist[:, None]).astype(np.float32)
+        mx[sl] = (dist * sf[k["octave"]]).astype(np.float32)
+        mn[sl] = (mx[sl] / sf[-1]).astype(np.float32)
+    obs = rng.integers(0, 4, N).astype(np.int32)
+    bad = (rng.random(N) < 0.03).astype(np.uint8)
+    return dict(pos=pos, desc=desc, normal=nrm, max_distance=mx, min_distance=mn, observations=obs, bad=bad)
+
+
+@pytest.mark.parametrize("th,nnratio,footprint,stereo", [(1.0, 0.8, 5, False), (3.0, 0.8, 5, True),
+                                                          (5.0, 0.6, 2, False), (1.0, 0.8, 0, True)])
+def test_search_local_points_device(oracle, orbx_built, th, nnratio, footprint, stereo):
+    """Tracking::SearchLocalPoints on the device (orbx_search_local_points_device): for each
+    frame of a posed sequence, its local map = the MapPoints of its neighbours in the
+    sequence, its mvpMapPoints pre-set as TrackWithMotionModel would have left them (some
+    of them bad), IsInFrustum + SearchByProjection(F, vpLocalMapPoints, th) vs the oracle."""
+    import torch
+
+    from orbslam2commentedbyxcm_amd.matcher import FrameView, MapPoints
+
+    B = 8
+    seq = _sequence_on_gpu(oracle, B, 30)
+    cap, n = seq["cap"], seq["n"]
+    tab = _mappoint_table(seq, 31)
+    rng = np.random.default_rng(32)
+    # local maps: the MapPoints of frames b-2, b-1, b+1 (existing slots), shuffled per frame
+    lists, off = [], [0]
+    for b in range(B):
+        ids = np.concatenate([np.arange(f * cap, f * cap + n[f]) for f in (b - 2, b - 1, b + 1) if 0 <= f < B])
+        ids = rng.permutation(ids).astype(np.int32)
+        lists.append(ids)
+        off.append(off[-1] + len(ids))
+    local_ids = np.concatenate(lists).astype(np.int32)
+    # mvpMapPoints before the search: ~25 % of keypoints hold an id from the local map
+    fmp0 = np.full((B, cap), -1, np.int32)
+    for b in range(B):
+        sel = np.nonzero(rng.random(n[b]) < 0.25)[0]
+        fmp0[b, sel] = rng.choice(lists[b], len(sel), replace=False)
+    ur = np.full((B, cap), -1.0, np.float32)
+    bf = 0.54 * S.FX if stereo else 0.0
+    if stereo:
+        for b in range(B):
+            k = seq["kps"][b][: n[b]]
+            _, z = S.plane_points(seq["rels"][b], k["x"], k["y"])
+            u = (k["x"] - bf / z + rng.normal(0, 0.5, n[b])).astype(np.float32)
+            u[rng.random(n[b]) < 0.3] = -1.0
+            ur[b, : n[b]] = u
+    dev = seq["dev"]
+    d_tab = {k: torch.from_numpy(v).to(dev) for k, v in tab.items()}
+    d_fmp = torch.from_numpy(fmp0).to(dev)
+    d_nm = torch.full((B,), -7, dtype=torch.int32, device=dev)
+    sf = seq["ex"].GetScaleFactors()
+    m = ORBmatcher(nnratio, False)
+    m.set_footprint(footprint)
+    m.search_local_points_device(d_tab, seq["d_kps"], seq["d_desc"], seq["d_n"],
+                                 torch.from_numpy(seq["T"]).to(dev), np.array(off), torch.from_numpy(local_ids).to(dev),
+                                 d_fmp, d_nm, sf, S.FX, S.FY, S.CX, S.CY, 640, 480, th=th, bf=bf,
+                                 d_u_right=torch.from_numpy(ur).to(dev) if stereo else None)
+    torch.cuda.synchronize()
+    fmp, nm = d_fmp.cpu().numpy(), d_nm.cpu().numpy()
+    mps = MapPoints(desc=tab["desc"], observations=tab["observations"], pos=tab["pos"], bad=tab["bad"],
+                    max_distance=tab["max_distance"], min_distance=tab["min_distance"], normal=tab["normal"])
+    total = 0
+    for b in range(B):
+        F = FrameView(keys=seq["kps"][b][: n[b]], desc=seq["desc"][b][: n[b]], fx=S.FX, fy=S.FY, cx=S.CX, cy=S.CY,
+                      bf=bf, scale_factors=sf, Tcw=np.vstack([seq["T"][b].reshape(3, 4), [0, 0, 0, 1]]),
+                      u_right=ur[b][: n[b]] if stereo else None)
+        ref = fmp0[b][: n[b]].copy()
+        nr = oracle.search_local_points(F, ref, lists[b], mps, th, nnratio)
+        assert nm[b] == nr, (b, nm[b], nr)
+        assert np.array_equal(fmp[b][: n[b]], ref), (b, np.nonzero(fmp[b][: n[b]] != ref)[0][:10])
+        total += nr
+    assert total > 100 * B
+
+
+def test_create_mappoints_device(oracle, orbx_built):
+    """Tracking::CreateNewKeyFrame's MapPoints on the device (UnprojectStereo +
+    UpdateNormalAndDepth) == the oracle's, bit for bit, for per-keypoint depths (some not
+    positive) on a posed sequence, and for the constant-depth form."""
+    import torch
+
+    from orbslam2commentedbyxcm_amd.matcher import FrameView, create_mappoints_device, mappoint_table
+
+    B = 6
+    seq = _sequence_on_gpu(oracle, B, 40)
+    cap, n = seq["cap"], seq["n"]
+    rng = np.random.default_rng(41)
+    depth = np.zeros((B, cap), np.float32)
+    for b in range(B):
+        k = seq["kps"][b][: n[b]]
+        _, z = S.plane_points(seq["rels"][b], k["x"], k["y"])
+        d = z.astype(np.float32)
+        d[rng.random(n[b]) < 0.2] = -1.0
+        depth[b, : n[b]] = d
+    sf = seq["ex"].GetScaleFactors()
+    d_T = torch.from_numpy(seq["T"]).to(seq["dev"])
+    for const in (None, 5.0):
+        tab = mappoint_table(B, cap, seq["dev"])
+        create_mappoints_device(seq["d_kps"], seq["d_n"], d_T, sf, S.FX, S.FY, S.CX, S.CY, tab,
+                                d_depth=None if const else torch.from_numpy(depth).to(seq["dev"]),
+                                const_depth=const or 0.0)
+        torch.cuda.synchronize()
+        got = {k: v.cpu().numpy() for k, v in tab.items()}
+        for b in range(B):
+            F = FrameView(keys=seq["kps"][b][: n[b]], desc=seq["desc"][b][: n[b]], fx=S.FX, fy=S.FY, cx=S.CX,
+                          cy=S.CY, scale_factors=sf, Tcw=np.vstack([seq["T"][b].reshape(3, 4), [0, 0, 0, 1]]))
+            r = oracle.create_mappoints(F, None if const else depth[b][: n[b]], const or 0.0)
+            sl = slice(b * cap, b * cap + n[b])
+            v = r["valid"] > 0
+            assert np.array_equal(got["bad"][sl], 1 - r["valid"]) and got["bad"][b * cap + n[b]:(b + 1) * cap].all()
+            assert np.array_equal(got["observations"][sl], r["valid"].astype(np.int32))
+            for k in ("pos", "normal", "max_distance", "min_distance"):
+                assert np.array_equal(got[k][sl][v].view(np.uint32), r[k][v].view(np.uint32)), (b, k)
