@@ -344,6 +344,8 @@ def main():
     ap.add_argument("--lanes", type=int, default=2,
                     help="split the batch into this many contiguous chunks, each on its own extractor stream, so "
                          "one chunk's latency-bound kernels overlap another's")
+    ap.add_argument("--no-local-map", action="store_true",
+                    help="skip the second measurement of the step with TrackLocalMap's SearchLocalPoints")
     ap.add_argument("--selftest-launch", action="store_true", help=argparse.SUPPRESS)
     args, _ = ap.parse_known_args()
 
@@ -464,10 +466,59 @@ def main():
                                             cy=CY, W=W, H=H, depth=DEPTH, th=TH))
         parity["bit_exact"] = parity["bit_exact"] and parity["octree_status_clean"]
 
+    # The same step with TrackLocalMap (SearchLocalPoints against the MapPoints of the three
+    # previous frames, after TrackWithMotionModel against the previous frame's MapPoints):
+    # a second pipeline, timed the same way, checked the same way.
+    local = None
+    sf_main = pl.sf
+    match_cu = None if (not match or pl._own_ms is None) else int(os.environ.get("ORBX_MATCH_CUSTRIDE", "1"))
+    if match and not args.no_local_map:
+        pl.close()
+        del pl
+        pl2 = SequencePipeline(B, W, H, lanes=args.lanes, pipelined=pipeline, device=local_rank, params=prm, fx=FX,
+                               fy=FY, cx=CX, cy=CY, depth=DEPTH, th=TH, local_map=True)
+        pl2.run(d_frames, d_T, max(args.warmup, 1))
+        sync()
+        pl2.set_timing(True)
+        barrier()
+        sync()
+        t0 = time.perf_counter()
+        pl2.run(d_frames, d_T, args.steps)
+        sync()
+        barrier()
+        sync()
+        el2 = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el2], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el2 = float(t.item())
+        st2 = pl2.stage_times()
+        pl2.set_timing(False)
+        res2 = pl2.host_results()
+        local = {"value": round(B * args.steps * world / el2, 2), "unit": "frames/s",
+                 "ms_per_step": round(el2 / args.steps * 1e3, 4),
+                 "step": "extract + MapPoints of every keypoint (CreateNewKeyFrame's UnprojectStereo at the model "
+                         "depth) + TrackWithMotionModel SearchByProjection vs the previous frame's MapPoints + "
+                         "TrackLocalMap SearchLocalPoints (IsInFrustum + SearchByProjection(F, vpLocalMapPoints, "
+                         "th=1), ORBmatcher(0.8)) vs the MapPoints of the 3 previous frames",
+                 "stage_ms": {k: round(v, 4) for k, v in st2.items()},
+                 "mean_matches_per_pair": round(float(res2["nm"][1:].mean()), 1),
+                 "mean_local_matches_per_frame": round(float(res2["nm_local"][1:].mean()), 1)}
+        if rank == 0 and args.parity_frames != 0:
+            from oracle import checks
+            nchk = B if args.parity_frames < 0 else min(B, max(2, args.parity_frames))
+            sub = {k: v[:nchk] for k, v in res2.items()}
+            pr = checks.check_sequence_local(frames_np[:nchk], T[:nchk], sub, pl2.sf, pl2.cap, params=prm, fx=FX,
+                                             fy=FY, cx=CX, cy=CY, W=W, H=H, depth=DEPTH, th=TH)
+            pr["octree_status_clean"] = not bool(pl2.status().any())
+            pr["bit_exact"] = pr["bit_exact"] and pr["octree_status_clean"]
+            local["parity"] = pr
+        pl2.close()
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        cpu = cpu_baseline(frames_np[:32], T[:32], pl.sf, args.cpu_seconds, threads, W, H, params=prm)
+        cpu = cpu_baseline(frames_np[:32], T[:32], sf_main, args.cpu_seconds, threads, W, H, params=prm)
 
     if rank == 0:
         out = {
@@ -492,7 +543,7 @@ def main():
                        "frames_per_gpu_step": B, "global_batch": B * world, "width": W, "height": H,
                        "parallelism": f"frame-sharded x{world}", "lanes_per_gpu": S,
                        "pipelined_match": pipeline,
-                       "match_cu_stride": None if pl._own_ms is None else int(os.environ.get("ORBX_MATCH_CUSTRIDE", "1"))},
+                       "match_cu_stride": match_cu},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), **prof,
                          "algorithmic_bytes_per_launch": int(bytes_pf[dom] * per_launch),
@@ -507,6 +558,7 @@ def main():
                          "frac_all_lanes": round(achieved * S / HBM_PEAK_GBS, 5)},
             "cpu_baseline": cpu,
             "parity": parity,
+            "with_local_map": local,
             "mean_keypoints_per_frame": round(mean_kps, 1),
             "mean_matches_per_pair": round(mean_matches, 1),
         }
