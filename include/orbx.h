@@ -115,10 +115,12 @@ void* orbx_extractor_stream(orbx_extractor* ex);
 int orbx_extractor_set_stage_event(orbx_extractor* ex, int stage, void** event);
 int orbx_stream_wait_event(void* stream, void* event);
 
-/* A non-blocking HIP stream on `device`.  cu_stride k > 1: its kernels run only on
- * compute units 0, k, 2k, ... (hipExtStreamCreateWithCUMask, default priority);
- * otherwise hipStreamCreateWithPriority with `priority` (HIP's range: lower numbers
- * are higher priorities; 0 = default).  The batched front end creates its matcher
+/* A HIP stream on `device`.  cu_stride k > 1: its kernels run only on compute units 0,
+ * k, 2k, ... (hipExtStreamCreateWithCUMask: default priority, and a blocking stream --
+ * it synchronises with the null stream, so a caller that issues null-stream work beside
+ * it serialises against it); otherwise a non-blocking stream from
+ * hipStreamCreateWithPriority with `priority` (HIP's range: lower numbers are higher
+ * priorities; 0 = default).  The batched front end creates its matcher
  * stream with it before the extraction lanes' streams, so that the three busy streams
  * get hardware queues of their own.  No reference counterpart:
  * ORB-SLAM2 tracks one frame at a time.  Release with orbx_stream_destroy. */
@@ -142,7 +144,8 @@ int orbx_extractor_status(orbx_extractor* ex, int batch, int* flags, int* any);
 int orbx_extractor_status_device(orbx_extractor* ex, const int32_t** d_status);
 /* Test hook: cap every level's octree node capacity at `cap` (0 = the bound the
  * reference's algorithm guarantees, max(N+4, 4*nIni+4) per level), so that the overflow
- * status can be exercised.  Takes effect at the next extraction. */
+ * status can be exercised.  Frees the extractor's buffers (pyramids included) after
+ * draining the whole device; takes effect at the next extraction. */
 int orbx_extractor_set_node_capacity(orbx_extractor* ex, int cap);
 
 /* Per-stage HIP-event timing (ms) of extraction calls, averaged over the (up to 64)

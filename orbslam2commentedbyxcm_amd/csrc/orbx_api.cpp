@@ -441,8 +441,10 @@ int orbx_extractor_status_device(orbx_extractor* ex, const int32_t** d_status) {
 int orbx_extractor_set_node_capacity(orbx_extractor* ex, int cap) {
     if (!ex || cap < 0) return fail(ORBX_ERR_ARG, "bad argument");
     HIP_TRY(hipSetDevice(ex->device));
-    HIP_TRY(hipStreamSynchronize(ex->stream));
-    if (ex->last_stream) HIP_TRY(hipStreamSynchronize(ex->last_stream));
+    // the buffers freed below include the pyramids, which consumers on other streams read
+    // (orbx_compute_stereo_matches_batch_device on a matcher's stream): a test hook, so
+    // the whole device is drained rather than only this extractor's streams
+    HIP_TRY(hipDeviceSynchronize());
     ex->prm.node_cap_limit = cap;
     free_buffers(ex->db);  // replanned (and reallocated) by the next extraction
     ex->plan = Plan();
