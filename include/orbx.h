@@ -331,8 +331,9 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* seq, voi
  *      matcher's nnratio (Tracking uses ORBmatcher(0.8)) over the points in view, in list
  *      order: frame_mp is updated in place, nmatches [b] receives its count.
  * MapPoints live in a device table indexed by id.  local_off is a host array (B + 1
- * ints: it sizes the launch); every other pointer is a device pointer.  cap and the
- * longest local map must stay below 8192.  Asynchronous on `stream` (or the matcher's). */
+ * ints: it sizes the launch); every other pointer is a device pointer.  cap must stay
+ * below 8192 (keypoints); a local map may hold up to 2^20 MapPoints.  Asynchronous on
+ * `stream` (or the matcher's). */
 typedef struct {
     int n;                        /* MapPoints in the table */
     const float* pos;             /* [n][3] GetWorldPos() */

@@ -925,10 +925,34 @@ __device__ __forceinline__ void wave_count(int* a, int idx) {
     }
 }
 
+// The same with the four quadrant counters of a node packed as u16 pairs in two words
+// (word 2*node + q/2, half q%2): atomicAdd(quadrant q of node nd, 1) per distinct (nd, q).
+__device__ __forceinline__ void wave_count_q(uint32_t* a, int idx) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long act = __ballot(1);
+    while (act) {
+        const int leader = __ffsll((long long)act) - 1;
+        const int t = __builtin_amdgcn_readlane(idx, leader);
+        const unsigned long long m = __ballot(idx == t);
+        if (lane == leader) atomicAdd(&a[t >> 1], (uint32_t)__popcll(m) << (16 * (t & 1)));
+        act &= ~m;
+    }
+}
+__device__ __forceinline__ void add_q(uint32_t* a, int nd, int q) {
+    atomicAdd(&a[2 * nd + (q >> 1)], 1u << (16 * (q & 1)));
+}
+__device__ __forceinline__ int get_q(const uint32_t* a, int nd, int q) {
+    return (int)((a[2 * nd + (q >> 1)] >> (16 * (q & 1))) & 0xffffu);
+}
+// Keys per level the packed counters and keys hold (u16 counts); a level with more
+// FAST keypoints is flagged kStatusNodeOverflow.
+constexpr int kOctMaxKeys = 65535;
+constexpr int kOctNodeBytes = 4 + 8 + 8 + 8 + 2 + 4 + 16 + 2;  // best, ccnt, sa+sb, cnt x2, sc, crank x2, boxes, inV
+
 struct NodeBuf {
     int16_t *x0, *y0, *x1, *y1;
     int* cnt;
-    int* crank;     // creation rank within the step that created the node
+    int16_t* crank;  // creation rank within the step that created the node (< NC)
     uint8_t* inV;   // member of vSizeAndPointerToNode (created last step with >1 key)
 };
 
@@ -982,15 +1006,19 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
     const LevelGeom& g = lv[l];
     const int N = g.N;
 
-    // LDS carve-up (NC nodes)
-    unsigned long long* best = (unsigned long long*)smem;               // NC u64
-    int* ccnt = (int*)(best + NC);                                      // 4*NC
-    int* sa = ccnt + 4 * NC;                                            // NC
+    // LDS carve-up (NC nodes, kOctNodeBytes = 52 B each: at configs[4]'s NC = 960 three
+    // workgroups fit a CU).  best: the final phase's (size << 16 | creation rank) keys,
+    // then each node's (response << 24 | ~key index) maximum; ccnt: four u16 quadrant
+    // counters per node, reused for the children's positions; sc: per-node ne / ranks.
+    uint32_t* best = (uint32_t*)smem;                                   // NC
+    uint32_t* ccnt = best + NC;                                         // 2*NC (must follow best)
+    uint16_t* cpos = (uint16_t*)ccnt;                                   // [4*NC] child positions
+    int* sa = (int*)(ccnt + 2 * NC);                                    // NC
     int* sb = sa + NC;                                                  // NC
-    int* sc = sb + NC;                                                  // NC
-    int* cntb = sc + NC;                                                // 2*NC
-    int* crkb = cntb + 2 * NC;                                          // 2*NC
-    int16_t* boxb = (int16_t*)(crkb + 2 * NC);                          // 8*NC
+    int* cntb = sb + NC;                                                // 2*NC
+    int16_t* sc = (int16_t*)(cntb + 2 * NC);                            // NC
+    int16_t* crkb = sc + NC;                                            // 2*NC
+    int16_t* boxb = crkb + 2 * NC;                                      // 8*NC
     uint8_t* inVb = (uint8_t*)(boxb + 8 * NC);                          // 2*NC
     NodeBuf nb0, nb1;
     nb0.x0 = boxb;
@@ -1053,6 +1081,13 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
     if (st && tid == 0) {
         st[1] = wall_clock64();
         st[6] = n;
+    }
+    if (n > kOctMaxKeys) {  // beyond the u16 counters (never on real frames): flagged, not truncated silently
+        if (tid == 0) {
+            atomicOr(&status[f], kStatusNodeOverflow);
+            kept_count[(size_t)f * L + l] = 0;
+        }
+        return;
     }
 
     // The per-key state (packed key, node) of key k lives with thread k % 256 for the
@@ -1138,9 +1173,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
         const NodeBuf& A = cur ? nb1 : nb0;
         const NodeBuf& B = cur ? nb0 : nb1;
         const int prev = size;
-        for (int j = tid; j < size; j += 256) {
-            ccnt[4 * j] = ccnt[4 * j + 1] = ccnt[4 * j + 2] = ccnt[4 * j + 3] = 0;
-        }
+        for (int j = tid; j < size; j += 256) ccnt[2 * j] = ccnt[2 * j + 1] = 0u;
         if (tid == 0) s_scal[1] = 0;
         __syncthreads();
         const bool few = size <= 64;
@@ -1148,8 +1181,8 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
             const int nd = NN;
             if (A.cnt[nd] >= 2) {
                 const int q = quadrant(key_x(KK), key_y(KK), A.x0[nd], A.y0[nd], A.x1[nd], A.y1[nd]);
-                if (few) wave_count(ccnt, 4 * nd + q);
-                else atomicAdd(&ccnt[4 * nd + q], 1);
+                if (few) wave_count_q(ccnt, 4 * nd + q);
+                else add_q(ccnt, nd, q);
             }
         })
         __syncthreads();
@@ -1159,12 +1192,12 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
             int ne = 0;
             if (split)
                 for (int q = 0; q < 4; q++) {
-                    ne += ccnt[4 * j + q] > 0;
-                    g2 += ccnt[4 * j + q] > 1;
+                    ne += get_q(ccnt, j, q) > 0;
+                    g2 += get_q(ccnt, j, q) > 1;
                 }
             sa[j] = ne;
             sb[j] = split ? 0 : 1;
-            sc[j] = ne;
+            sc[j] = (int16_t)ne;
         }
         if (g2) atomicAdd(&s_scal[1], g2);
         __syncthreads();
@@ -1179,7 +1212,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
                 const int P = C - sa[j] - ne;  // block of the children: sum of ne over later split nodes
                 int r = 0;
                 for (int q = 0; q < 4; q++) {
-                    const int cq = ccnt[4 * j + q];
+                    const int cq = get_q(ccnt, j, q);  // slot q is still a count (earlier slots hold positions)
                     if (cq > 0) {
                         const int pos = P + (ne - 1 - r);  // pushed front in n1..n4 order
                         int cx0, cy0, cx1, cy1;
@@ -1189,9 +1222,9 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
                         B.x1[pos] = (int16_t)cx1;
                         B.y1[pos] = (int16_t)cy1;
                         B.cnt[pos] = cq;
-                        B.crank[pos] = sa[j] + r;
+                        B.crank[pos] = (int16_t)(sa[j] + r);
                         B.inV[pos] = cq > 1;
-                        ccnt[4 * j + q] = pos;
+                        cpos[4 * j + q] = (uint16_t)pos;
                         r++;
                     }
                 }
@@ -1212,7 +1245,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
             const int nd = NN;
             if (A.cnt[nd] >= 2) {
                 const int q = quadrant(key_x(KK), key_y(KK), A.x0[nd], A.y0[nd], A.x1[nd], A.y1[nd]);
-                NN = ccnt[4 * nd + q];
+                NN = cpos[4 * nd + q];
             } else {
                 NN = sb[nd];
             }
@@ -1244,22 +1277,22 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
         for (int j = tid; j < size; j += 256) {
             sa[j] = A.inV[j] ? 1 : 0;
             sc[j] = -1;  // rank of node j in processing order, -1 if not in vPrev
-            ccnt[4 * j] = ccnt[4 * j + 1] = ccnt[4 * j + 2] = ccnt[4 * j + 3] = 0;
+            ccnt[2 * j] = ccnt[2 * j + 1] = 0u;
         }
         __syncthreads();
         const int nv = block_exscan(sa, size, s_tmp);
         if (nv == 0) { finish = true; break; }
         for (int j = tid; j < size; j += 256)
             if (A.inV[j]) {
-                best[sa[j]] = ((unsigned long long)A.cnt[j] << 32) | (unsigned)A.crank[j];
+                best[sa[j]] = ((uint32_t)A.cnt[j] << 16) | (uint32_t)(uint16_t)A.crank[j];
                 sb[sa[j]] = j;
             }
         // pad to a multiple of 4 with keys never larger (past NC the reads land in the
         // zeroed ccnt)
-        if (tid < 3 && nv + tid < NC) best[nv + tid] = 0ull;
+        if (tid < 3 && nv + tid < NC) best[nv + tid] = 0u;
         __syncthreads();
         for (int p = tid; p < nv; p += 256) {
-            const unsigned long long kp = best[p];
+            const uint32_t kp = best[p];
             int r0 = 0, r1 = 0, r2 = 0, r3 = 0;
             for (int i = 0; i < nv; i += 4) {
                 r0 += best[i] > kp;
@@ -1267,7 +1300,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
                 r2 += best[i + 2] > kp;
                 r3 += best[i + 3] > kp;
             }
-            sc[sb[p]] = r0 + r1 + r2 + r3;
+            sc[sb[p]] = (int16_t)(r0 + r1 + r2 + r3);
         }
         __syncthreads();
         for (int j = tid; j < size; j += 256)
@@ -1276,7 +1309,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
             const int nd = NN;
             if (A.inV[nd]) {
                 const int q = quadrant(key_x(KK), key_y(KK), A.x0[nd], A.y0[nd], A.x1[nd], A.y1[nd]);
-                atomicAdd(&ccnt[4 * nd + q], 1);
+                add_q(ccnt, nd, q);
             }
         })
         __syncthreads();
@@ -1284,7 +1317,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
         for (int r = tid; r < nv; r += 256) {
             const int j = sa[r];
             int ne = 0;
-            for (int q = 0; q < 4; q++) ne += ccnt[4 * j + q] > 0;
+            for (int q = 0; q < 4; q++) ne += get_q(ccnt, j, q) > 0;
             sb[r] = ne;
         }
         // K = first r where prev + sum_{i<=r}(ne_i - 1) >= N (break after it), else nv-1.
@@ -1310,7 +1343,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
         // processed flag per node, then position of unprocessed nodes
         for (int j = tid; j < size; j += 256) {
             const int r = sc[j];
-            sc[j] = (r >= 0 && r <= Kp) ? r : -1;
+            sc[j] = (int16_t)((r >= 0 && r <= Kp) ? r : -1);
         }
         __syncthreads();
         // D_j = number of processed nodes before j (list order)
@@ -1331,12 +1364,12 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
                 sa[j] = pos;
             } else {
                 int ne = 0;
-                for (int q = 0; q < 4; q++) ne += ccnt[4 * j + q] > 0;
+                for (int q = 0; q < 4; q++) ne += get_q(ccnt, j, q) > 0;
                 const int Er = sb[r];
                 const int Bk = Cc - Er - ne;
                 int rr = 0;
                 for (int q = 0; q < 4; q++) {
-                    const int cq = ccnt[4 * j + q];
+                    const int cq = get_q(ccnt, j, q);
                     if (cq > 0) {
                         const int pos = Bk + (ne - 1 - rr);
                         int cx0, cy0, cx1, cy1;
@@ -1346,9 +1379,9 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
                         B.x1[pos] = (int16_t)cx1;
                         B.y1[pos] = (int16_t)cy1;
                         B.cnt[pos] = cq;
-                        B.crank[pos] = Er + rr;
+                        B.crank[pos] = (int16_t)(Er + rr);
                         B.inV[pos] = cq > 1;
-                        ccnt[4 * j + q] = pos;
+                        cpos[4 * j + q] = (uint16_t)pos;
                         rr++;
                     }
                 }
@@ -1359,7 +1392,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
             const int nd = NN;
             if (sc[nd] >= 0) {
                 const int q = quadrant(key_x(KK), key_y(KK), A.x0[nd], A.y0[nd], A.x1[nd], A.y1[nd]);
-                NN = ccnt[4 * nd + q];
+                NN = cpos[4 * nd + q];
             } else {
                 NN = sa[nd];
             }
@@ -1372,10 +1405,10 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
 
     if (st && tid == 0) st[3] = wall_clock64();
     // ---- 5. best key per node (cc:984-1009)
-    for (int j = tid; j < size; j += 256) best[j] = 0ull;
+    for (int j = tid; j < size; j += 256) best[j] = 0u;
     __syncthreads();
     FOR_KEYS({
-        const unsigned long long v = ((unsigned long long)key_resp(KK) << 32) | (0xffffffffu - (unsigned)k);
+        const uint32_t v = ((uint32_t)key_resp(KK) << 24) | (0xffffffu - (uint32_t)k);  // k <= kOctMaxKeys
         atomicMax(&best[NN], v);
     })
 #undef FOR_KEYS
@@ -1383,7 +1416,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
     const int outn = size < g.ncap ? size : g.ncap;
     uint32_t* out = kept + (size_t)f * kept_pf + g.out_off;
     for (int j = tid; j < outn; j += 256) {
-        const unsigned k = 0xffffffffu - (unsigned)(best[j] & 0xffffffffull);
+        const unsigned k = 0xffffffu - (best[j] & 0xffffffu);
         out[j] = K[k];
     }
     if (tid == 0) {
@@ -1632,7 +1665,14 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     if (stage_ev && stage_after == 3) (void)hipEventRecord(stage_ev, stream);
     {
         const int NC = (plan.max_ncap + 63) & ~63;
-        const size_t lds = (size_t)NC * (8 + 16 + 12 + 8 + 8 + 16 + 2);
+        const size_t lds = (size_t)NC * kOctNodeBytes;
+        // int16 node ids / ranks, and one workgroup's LDS (beside its static arrays)
+        if (NC > 32767 || lds > 152 * 1024) return hipErrorInvalidValue;
+        if (lds > 64 * 1024) {
+            const hipError_t e =
+                hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
         dim3 grid(L * batch);
         hipLaunchKernelGGL(k_octree, grid, dim3(256), lds, stream, db.lv, L, db.slots, plan.slots_per_frame,
                            db.cells, db.cell_count, ncells, db.keys, db.key_node, plan.keys_per_frame,

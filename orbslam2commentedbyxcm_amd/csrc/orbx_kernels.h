@@ -71,10 +71,12 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
                               unsigned char* split_grids = nullptr);
 
 // k_seq_grid + k_seq_score + k_seq_commit: the split form of launch_proj_search for the
-// batched sequence matcher (grids: nprob x seq_grid_bytes(cap) bytes of device memory)
+// batched sequence matcher (grids: nprob x seq_grid_bytes(cap) bytes of device memory).
+// cap: keypoints per problem (the grids); qcap: queries per problem (0: cap)
 size_t seq_grid_bytes(int cap, int noct);
 hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned char* grids,
-                            int cap, unsigned long long* scratch, const long long* d_scratch_off, hipStream_t stream);
+                            int cap, unsigned long long* scratch, const long long* d_scratch_off, hipStream_t stream,
+                            int qcap = 0);
 
 hipError_t launch_seq_build(const SeqArgs& A, int npairs, ProjQuery* queries, ProjProblem* probs,
                             long long* scratch_off, hipStream_t stream);

@@ -352,6 +352,18 @@ __device__ __forceinline__ QueryReg bcast_query(const QueryReg& x, int src) {
     return r;
 }
 
+// Lane `src`'s query for each lane (src may differ per lane; ds_bpermute per word).
+__device__ __forceinline__ QueryReg shfl_query(const QueryReg& x, int src) {
+    constexpr int kW = (int)(sizeof(QueryReg) / 4);
+    int w[kW];
+    __builtin_memcpy(w, &x, sizeof(QueryReg));
+#pragma unroll
+    for (int i = 0; i < kW; i++) w[i] = __shfl(w[i], src);
+    QueryReg r;
+    __builtin_memcpy(&r, w, sizeof(QueryReg));
+    return r;
+}
+
 // The kTopK best candidates of a query (GetFeaturesInArea + the overload's filters)
 // against the current claims sfmp, as entries (kNoEntry = no more candidates, kTrunc =
 // more candidates exist than listed).  One 16-lane row per query, four queries per wave:
@@ -569,7 +581,7 @@ __device__ void grid_sort(const ProjProblem& pb, unsigned* skey, unsigned* cnt) 
 
 // LDS layout of k_proj_search (byte offsets), shared by the kernel and its launcher.
 struct ProjLds {
-    size_t skey, colstart, bstart, orun, sxy, sfmp, owner, sang, sdesc, qk, qmp, qang, mlist, mbin, total;
+    size_t skey, colstart, bstart, orun, sxy, sfmp, owner, sang, elist, sdesc, qk, qmp, qang, mlist, mbin, total;
     __host__ __device__ ProjLds(int n, int nq, bool dlds, bool qlds, int noct, bool replay = true) {
         skey = 0;
         colstart = align16((size_t)n * 4);
@@ -582,6 +594,8 @@ struct ProjLds {
         // state only; the lean form reads them from the keypoints after the replay
         sang = owner + (replay ? (size_t)n * 4 : 0);
         size_t o = align16(sang + (qlds ? (size_t)n * 4 : 0));
+        elist = o;  // the replay wave's lists (kTopK x 64 entries)
+        if (replay) o += (size_t)kTopK * 64 * 4;
         sdesc = o;
         if (dlds) o += (size_t)n * 32;
         qk = o;
@@ -605,8 +619,8 @@ struct ProjLds {
 // (LDS); angle_of(p): the angle of the keypoint at sorted position p.  Whole wave active.
 template <typename AngleFn>
 __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const SortedGrid& G, int* sfmp, int* owner,
-                            const uint4* qk, const int* qmp, const float* qang, int* mlist, int* mbin, int* s_hist,
-                            AngleFn angle_of, unsigned long long* st) {
+                            unsigned* elist, const uint4* qk, const int* qmp, const float* qang, int* mlist,
+                            int* mbin, int* s_hist, AngleFn angle_of, unsigned long long* st) {
     const int lane = threadIdx.x & 63;
     const int nq = pb.nq;
     int nmatch = 0, nrec = 0, nrescore = 0, niter = 0, ntrunc = 0;
@@ -614,6 +628,234 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
     const float factor = kHistoLength / 360.0f;
     const int need = P.ratio_mode ? 2 : 1;
     const unsigned long long below = (1ull << lane) - 1;
+#ifndef ORBX_REPLAY_ROUNDS
+    // Fixpoint form.  The reference's loop is a function of the query order: query l's
+    // choice (first two unclaimed entries, acceptance) depends only on the claims of the
+    // queries before it.  Within a 64-query chunk every lane evaluates its choice against
+    // the committed claims plus the current proposals of the earlier lanes (an LDS owner
+    // map: owner[p] = lowest lane proposing p), and all lanes re-evaluate together until
+    // no lane changes (Jacobi iteration: after t iterations the first t lanes are final,
+    // so it converges, and its fixpoint is the sequential result).  A chunk with k
+    // independent conflicts then costs one iteration plus the longest dependency chain,
+    // not k rounds.  Sequence points stop the commit: a lane whose list ran out (it is
+    // re-scored against the committed claims) and a lane accepting a MapPoint whose claim
+    // does not block (a11: Observations() == 0) -- it commits alone after the lanes
+    // before it.
+    const int lastp = pb.n > 0 ? pb.n - 1 : 0;
+    int guard = 0;
+    // a chunk's lists, MapPoints and queries (the latter for a re-scoring) are loaded
+    // while the chunk before it replays
+    uint4 nx_l[kListVec];
+    int nx_mp = -1;
+    QueryReg nx_q;
+    auto fetch = [&](int qn) {
+        nx_mp = -1;
+        if (qn < nq) {
+            nx_q = load_query(pb, qn);
+            nx_mp = qmp[qn];
+#pragma unroll
+            for (int v = 0; v < kListVec; v++) nx_l[v] = qk[kListVec * qn + v];
+        }
+    };
+    fetch(lane);
+    for (int base = 0; base < nq && guard >= 0; base += 64) {
+        const int q = base + lane;
+        const unsigned long long t_chunk = st ? wall_clock64() : 0;
+        int mp = nx_mp;
+        unsigned e[kTopK];
+#pragma unroll
+        for (int v = 0; v < kListVec; v++) {
+            e[4 * v] = mp >= 0 ? nx_l[v].x : kNoEntry;
+            e[4 * v + 1] = mp >= 0 ? nx_l[v].y : kNoEntry;
+            e[4 * v + 2] = mp >= 0 ? nx_l[v].z : kNoEntry;
+            e[4 * v + 3] = mp >= 0 ? nx_l[v].w : kNoEntry;
+        }
+        const QueryReg mine = nx_q;  // consumed only by a re-scoring
+        fetch(q + 64);
+        // Per lane, derived once per list (at the chunk's start and after a re-scoring):
+        // the list itself in LDS (elist[j][lane]: an entry is picked by a per-lane index,
+        // conflict-free), its entries' owner-map slots, vm = the real entries (bits), full =
+        // it may hide unlisted candidates, lastgt = its last real entry is beyond the
+        // acceptance threshold.
+        unsigned vm = 0;
+        bool full = false, lastgt = false;
+        int oa[kTopK];
+        auto set_list = [&]() {
+            vm = 0;
+            int lastd = -1;
+#pragma unroll
+            for (int j = 0; j < kTopK; j++) {
+                elist[j * 64 + lane] = e[j];
+                oa[j] = min(ent_pos(e[j]), lastp);
+                vm |= (e[j] < kTrunc ? 1u : 0u) << j;
+                if (e[j] < kTrunc) lastd = ent_dist(e[j]);
+            }
+            full = e[kTopK - 1] != kNoEntry;
+            lastgt = lastd > P.accept_th;
+        };
+        set_list();
+        // this lane's claims block later queries (a11: only a MapPoint with observations)
+        bool bself = false;
+        // cblk bit j: entry j is taken by a committed claim (the claims before the chunk:
+        // one batch of independent LDS reads, and Observations() loads for a11)
+        unsigned cblk = 0;
+        if (mp >= 0) {
+            bself = P.blocked_mode == 1 || P.mp_obs[mp] > 0;
+            int fm[kTopK];
+#pragma unroll
+            for (int j = 0; j < kTopK; j++) fm[j] = sfmp[oa[j]];
+            if (P.blocked_mode == 1) {
+#pragma unroll
+                for (int j = 0; j < kTopK; j++) cblk |= (fm[j] >= 0 ? 1u : 0u) << j;
+            } else {
+                int ob[kTopK];
+#pragma unroll
+                for (int j = 0; j < kTopK; j++) ob[j] = P.mp_obs[fm[j] >= 0 ? fm[j] : 0];
+#pragma unroll
+                for (int j = 0; j < kTopK; j++) cblk |= (fm[j] >= 0 && ob[j] > 0 ? 1u : 0u) << j;
+            }
+        }
+        // a lane's choice given the blocked entries bm: c1 (its best free entry), whether
+        // it accepts c1, and whether its list ran out (exhausted: unlisted candidates may
+        // be the answer).  Bit arithmetic on the free mask; c1 / c2 read from elist.
+        unsigned c1 = kNoEntry;
+        bool exh = false, acc = false;
+        auto eval = [&](unsigned bm) {
+            const unsigned fm = vm & ~bm;
+            const int cnt = __popc(fm);
+            const unsigned a1 = fm ? elist[__builtin_ctz(fm) * 64 + lane] : kNoEntry;
+            // a full (or truncated) list may hide unlisted candidates -- but they are at
+            // least as far as its last exact entry (the list holds the smallest keys), so
+            // when that entry, or the free c1 of a ratio test, is already beyond the
+            // acceptance threshold the query stays unmatched
+            bool x = full && cnt < need;
+            if (x && ((cnt == 0 && lastgt) || (cnt == 1 && ent_dist(a1) > P.accept_th))) x = false;
+            bool a = !x && fm != 0 && ent_dist(a1) <= P.accept_th;
+            if (a && P.ratio_mode) {
+                const unsigned f2 = fm & (fm - 1);
+                const unsigned a2 = f2 ? elist[__builtin_ctz(f2) * 64 + lane] : kNoEntry;
+                const int bestLevel2 = a2 == kNoEntry ? -1 : ent_oct(a2);
+                const int bestDist2 = a2 == kNoEntry ? 256 : ent_dist(a2);
+                if (ent_oct(a1) == bestLevel2 && (float)ent_dist(a1) > P.nnratio * (float)bestDist2) a = false;
+            }
+            c1 = a1;
+            exh = x;
+            acc = a;
+        };
+        // what later lanes and the commit see of a lane's choice
+        auto sig = [&]() { return exh ? kTrunc : (acc ? c1 : kNoEntry); };
+        if (mp >= 0) eval(cblk);
+        int start = 0;
+        int ow[kTopK];
+        bool first = true;
+        while (true) {
+            niter++;
+            if (++guard > 66 * (nq + 64)) {  // never reached: <= 65 iterations per fixpoint
+                guard = -1;
+                break;
+            }
+            const bool act = lane >= start && mp >= 0;
+            const int prop = act && acc && bself ? ent_pos(c1) : -1;
+            const unsigned old = sig();
+            // owner[p] = lowest lane proposing p (LDS ops of a wave are executed in order:
+            // all atomics, then all reads, then the reset)
+            if (prop >= 0) atomicMin(&owner[prop], lane);
+#pragma unroll
+            for (int j = 0; j < kTopK; j++) ow[j] = act ? owner[oa[j]] : 0x7fffffff;
+            if (prop >= 0) owner[prop] = 0x7fffffff;
+            unsigned sb = 0;
+#pragma unroll
+            for (int j = 0; j < kTopK; j++) sb |= (ow[j] < lane ? 1u : 0u) << j;
+            if (act) eval(cblk | sb);
+            if (__ballot(act && sig() != old)) continue;
+            // fixpoint: every active lane's choice is the sequential one up to the first
+            // sequence point f
+            const bool nbl = act && acc && !bself;
+            const unsigned long long sm = __ballot(act && (exh || nbl));
+            const int f = sm ? __ffsll((long long)sm) - 1 : 64;
+            const bool fnb = f < 64 && __builtin_amdgcn_readlane((int)nbl, f);
+            const int lim = fnb ? f + 1 : f;  // lanes below lim commit
+            const bool com = act && acc && lane < lim;
+            const unsigned long long comm = __ballot(com);
+            if (com) sfmp[ent_pos(c1)] = mp;
+            nmatch += __popcll(comm);
+            if (P.check_ori) {
+                // the match is recorded with its query; the rotation bins are computed
+                // after the replay, off the sequential path
+                if (com) {
+                    const int r = nrec + __popcll(comm & below);
+                    mlist[r] = ent_pos(c1);
+                    mbin[r] = q;
+                }
+                nrec += __popcll(comm);
+            }
+            if (st && first) t_first += wall_clock64() - t_chunk;
+            first = false;
+            if (f >= 64) break;
+            // the committed lanes' claims, for the lanes after them: the entries a lane
+            // below f proposed (blocking proposals only reach the owner map)
+#pragma unroll
+            for (int j = 0; j < kTopK; j++) cblk |= (act && lane >= lim && ow[j] < f ? 1u : 0u) << j;
+            start = lim;
+            if (!fnb) {
+                // lane f's list ran out: re-score it against the current claims.  Any list
+                // that is exact against the claims of some moment stays valid later
+                // (claims only ever block more keypoints), so the other exhausted lanes
+                // of the chunk are re-scored in the same pass, one 16-lane row each.
+                const unsigned long long t0 = st ? wall_clock64() : 0;
+                wave_lds_fence();
+                unsigned long long X = __ballot(act && exh && lane >= f);
+                if (st) {  // diagnostics: the list ran out at a truncation, not at its last entry
+                    bool tr = false;
+#pragma unroll
+                    for (int j = 0; j < kTopK; j++) tr = tr || e[j] == kTrunc;
+                    ntrunc += __builtin_amdgcn_readlane((int)tr, f);
+                }
+                unsigned ne[kTopK];
+#ifndef ORBX_RESCORE_SINGLE
+                if (__popcll(X) > 1) {
+                    // rows 0..3 take the first four exhausted lanes
+                    const int row = lane >> 4;
+                    unsigned long long x = X;
+                    for (int r = 0; r < row; r++) x &= x - 1;
+                    const bool valid = x != 0;
+                    const int src = valid ? __ffsll((long long)x) - 1 : f;
+                    score_groupk<16>(pb, P, shfl_query(mine, src), valid, G, sfmp, ne);
+                    const int myrow = __popcll(X & below);
+                    const bool mine_row = ((X >> lane) & 1ull) && myrow < 4;
+#pragma unroll
+                    for (int j = 0; j < kTopK; j++) {
+                        const unsigned v = (unsigned)__shfl((int)ne[j], (myrow & 3) * 16);
+                        if (mine_row) e[j] = v;
+                    }
+                    nrescore += __popcll(X) < 4 ? __popcll(X) : 4;
+                    if (mine_row) {
+                        cblk = 0;
+                        set_list();
+                        eval(0);
+                    }
+                } else
+#endif
+                {
+                    score_groupk<64>(pb, P, bcast_query(mine, f), true, G, sfmp, ne);  // wave-uniform result
+#pragma unroll
+                    for (int j = 0; j < kTopK; j++)
+                        if (lane == f) e[j] = ne[j];
+                    nrescore++;
+                    if (lane == f) {
+                        cblk = 0;  // the new list holds free keypoints only
+                        set_list();
+                        eval(0);   // lane f is the first active lane: no earlier proposals
+                    }
+                }
+                if (st) t_res += wall_clock64() - t0;
+            }
+            wave_lds_fence();
+        }
+        wave_lds_fence();
+    }
+    if (guard < 0) nmatch = -1;  // a broken fixpoint (never observed): fail the parity check loudly
+#else
     for (int base = 0; base < nq; base += 64) {
         const int q = base + lane;
         int mp = -1;
@@ -754,6 +996,7 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
         }
         wave_lds_fence();
     }
+#endif
     // the match list (global scratch in some modes) is read back by other lanes below
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -966,7 +1209,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     // The replay is wave 0's alone: the other waves leave now, so their registers and
     // wave slots go back to whatever runs beside this kernel for the rest of its life.
     if (wave != 0) return;
-    proj_replay(pb, P, G, sfmp, owner, qk, qmp, qang, mlist, mbin, s_hist,
+    proj_replay(pb, P, G, sfmp, owner, (unsigned*)(smem + L.elist), qk, qmp, qang, mlist, mbin, s_hist,
                 [&](int tpos) { return QLDS ? sang[tpos] : pb.keys[sk_idx(skey[tpos])].angle; }, st);
     wave_lds_fence();
     for (int p = lane; p < n; p += 64) pb.frame_mp[sk_idx(skey[p])] = sfmp[p];
@@ -1078,9 +1321,10 @@ __global__ __launch_bounds__(64) void k_seq_commit(const ProjProblem* __restrict
     if (!use_sdesc) G.sdesc = nullptr;  // descriptors by keypoint index from the frame
     const float* gang = (const float*)(grids + (size_t)blockIdx.x * gl.total + gl.sang);
     const int lane = threadIdx.x, n = pb.n, nq = pb.nq;
-    // LDS: the claims and the owner map only (8 B per keypoint); the rotation bins read
-    // the grid's angles from global memory after the replay
-    int* sfmp = (int*)smem;
+    // LDS: the replay's lists, the claims and the owner map only (8 B per keypoint); the
+    // rotation bins read the grid's angles from global memory after the replay
+    unsigned* elist = (unsigned*)smem;
+    int* sfmp = (int*)(elist + kTopK * 64);
     int* owner = sfmp + n;
     for (int p = lane; p < n; p += 64) {
         sfmp[p] = pb.frame_mp[sk_idx(G.skey[p])];
@@ -1095,7 +1339,7 @@ __global__ __launch_bounds__(64) void k_seq_commit(const ProjProblem* __restrict
     const float* qang = (const float*)(qmp + nq);
     int* mlist = (int*)(qang + nq);
     int* mbin = mlist + nq;
-    proj_replay(pb, P, G, sfmp, owner, qk, qmp, qang, mlist, mbin, s_hist, [&](int tpos) { return gang[tpos]; },
+    proj_replay(pb, P, G, sfmp, owner, elist, qk, qmp, qang, mlist, mbin, s_hist, [&](int tpos) { return gang[tpos]; },
                 nullptr);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -1104,14 +1348,19 @@ __global__ __launch_bounds__(64) void k_seq_commit(const ProjProblem* __restrict
 
 size_t seq_grid_bytes(int cap, int noct) { return SeqGridLayout(cap, noct).total; }
 
+// k_seq_commit's dynamic LDS: the replay's lists, then the claims and the owner map
+static size_t seq_commit_lds(int cap) { return (size_t)kTopK * 64 * 4 + (size_t)cap * 8; }
+
 hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned char* grids,
-                            int cap, unsigned long long* scratch, const long long* d_scratch_off, hipStream_t stream) {
+                            int cap, unsigned long long* scratch, const long long* d_scratch_off, hipStream_t stream,
+                            int qcap) {
     if (nprob <= 0) return hipSuccess;
     if (cap <= 0 || cap >= 8192) return hipErrorInvalidValue;  // 13-bit keypoint positions
+    if (qcap <= 0) qcap = cap;
     if (P.noct < 1 || P.noct > 32) return hipErrorInvalidValue;
     const size_t scr = octave_runs_scratch(P.noct) > kGridSortScratch ? octave_runs_scratch(P.noct) : kGridSortScratch;
     const size_t lds_grid = align16(align16((size_t)cap * 4) + (size_t)(kGridCols + 1) * 2) + scr;
-    const size_t lds_commit = (size_t)cap * 8;
+    const size_t lds_commit = seq_commit_lds(cap);
     if (lds_grid > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)k_seq_grid, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)lds_grid);
@@ -1126,7 +1375,7 @@ hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjPar
                        P.noct);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const int qblocks = (cap + kSeqScoreQ - 1) / kSeqScoreQ;
+    const int qblocks = (qcap + kSeqScoreQ - 1) / kSeqScoreQ;
     const int per_xcd = (nprob + kXcds - 1) / kXcds;
     hipLaunchKernelGGL(k_seq_score, dim3(kXcds * per_xcd * qblocks), dim3(kSeqScoreThreads), 0, stream, d_probs,
                        nprob, qblocks, P, grids, cap, scratch, d_scratch_off);
@@ -1439,7 +1688,7 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
                     (void*)&gcap};
     hipError_t e = hipLaunchKernel(fn, dim3(nprob), dim3(nt), args, lds, stream);
     if (e != hipSuccess || !split_grids) return e;
-    const size_t lds_commit = (size_t)max_n * 8;
+    const size_t lds_commit = seq_commit_lds(max_n);
     if (lds_commit > 64 * 1024) {
         e = hipFuncSetAttribute((const void*)k_seq_commit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_commit);
         if (e != hipSuccess) return e;

@@ -748,9 +748,10 @@ int orbx_search_local_points_device(orbx_matcher* m, const orbx_mappoints_device
         if (c > maxnq) maxnq = c;
     }
     const int total = lm->local_off[B];
-    if (maxnq >= 8192) return fail(ORBX_ERR_ARG, "a local map of 8192 or more MapPoints");
+    if (maxnq > (1 << 20)) return fail(ORBX_ERR_ARG, "a local map of more than 2^20 MapPoints");
     if (total > 0 && !lm->local_ids) return fail(ORBX_ERR_ARG, "null local_ids");
-    const int gcap = cap > maxnq ? cap : maxnq;  // grid / query capacity of one problem
+    // grids hold a frame's keypoints (cap < 8192, 13-bit sorted positions); the queries
+    // (local MapPoints) are not position-encoded, so a local map may exceed that
     HIP_TRY(hipSetDevice(m->device));
     hipStream_t s = stream ? (hipStream_t)stream : m->stream;
     const bool split = m->footprint == 2;
@@ -758,7 +759,7 @@ int orbx_search_local_points_device(orbx_matcher* m, const orbx_mappoints_device
     const size_t nt = (size_t)(total > 0 ? total : 1);
     const size_t need = pad(sizeof(ProjQuery) * nt) + pad(nt * 32) + pad(sizeof(ProjProblem) * B) +
                         pad(sizeof(long long) * B) + pad(sizeof(unsigned long long) * kProjScratchWords * nt) +
-                        pad(sizeof(int32_t) * (B + 1)) + (grids ? pad(seq_grid_bytes(gcap, nlevels) * B) : 0);
+                        pad(sizeof(int32_t) * (B + 1)) + (grids ? pad(seq_grid_bytes(cap, nlevels) * B) : 0);
     if (m->lscr_cap < need) {
         HIP_TRY(hipStreamSynchronize(s));
         if (m->lscr) HIP_TRY(hipFree(m->lscr));
@@ -779,7 +780,7 @@ int orbx_search_local_points_device(orbx_matcher* m, const orbx_mappoints_device
     auto* d_off = (long long*)take(sizeof(long long) * B);
     auto* d_scr = (unsigned long long*)take(sizeof(unsigned long long) * kProjScratchWords * nt);
     auto* d_loff = (int32_t*)take(sizeof(int32_t) * (B + 1));
-    auto* d_grids = grids ? (unsigned char*)take(seq_grid_bytes(gcap, nlevels) * B) : nullptr;
+    auto* d_grids = grids ? (unsigned char*)take(seq_grid_bytes(cap, nlevels) * B) : nullptr;
     char* h = nullptr;
     int slot = 0;
     HIP_TRY(m->stage.get(sizeof(int32_t) * (B + 1), &h, &slot));
@@ -831,9 +832,9 @@ int orbx_search_local_points_device(orbx_matcher* m, const orbx_mappoints_device
     P.check_ori = 0;
     P.noct = nlevels;
     if (split)
-        HIP_TRY(launch_seq_split(d_prob, B, P, d_grids, gcap, d_scr, d_off, s));
+        HIP_TRY(launch_seq_split(d_prob, B, P, d_grids, cap, d_scr, d_off, s, maxnq > 0 ? maxnq : 1));
     else
-        HIP_TRY(launch_proj_search(d_prob, B, P, d_scr, d_off, gcap, gcap, s, m->footprint == 1, m->footprint == 3,
+        HIP_TRY(launch_proj_search(d_prob, B, P, d_scr, d_off, cap, maxnq, s, m->footprint == 1, m->footprint == 3,
                                    m->footprint == 4, m->footprint == 5 ? d_grids : nullptr));
     return ORBX_OK;
 }

@@ -172,3 +172,27 @@ def test_sequence_pipeline_local_map_matches_oracle(oracle, orbx_built, B, lanes
         r = checks.check_sequence_local(frames, sequence_poses(off), res, pl.sf, cap)
         assert r["bit_exact"], (j, r)
         assert r["mean_matches_per_pair_ref"] > 200 and r["mean_local_matches_ref"] > 50, (j, r)
+
+
+def test_sequence_pipeline_local_map_c5_large_local_map(oracle, orbx_built):
+    """configs[4] (5000 features x 12 levels) with TrackLocalMap: each frame's local map
+    is the MapPoints of its three predecessors, 3 x cap > 8192 entries (more than the 13-bit
+    keypoint positions of the grids can name: queries are not position-encoded)."""
+    import torch
+
+    prm = (5000, 1.2, 12, 20, 7)
+    B = 8
+    frames, off = synth.sequence(3100, B)
+    T = sequence_poses(off)
+    pl = SequencePipeline(B, 640, 480, lanes=2, pipelined=True, params=prm, local_map=True)
+    assert 3 * pl.cap > 8192
+    d_frames = torch.from_numpy(frames).to(pl.dev)
+    d_T = torch.from_numpy(T).to(pl.dev)
+    torch.cuda.synchronize()
+    pl.run(d_frames, d_T, 2)
+    torch.cuda.synchronize()
+    res = pl.host_results()
+    r = checks.check_sequence_local(frames, T, res, pl.sf, pl.cap, params=prm)
+    assert r["bit_exact"], r
+    assert r["mean_local_matches_ref"] > 50, r
+    pl.close()
