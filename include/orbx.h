@@ -128,7 +128,8 @@ int orbx_stream_create(int device, int cu_stride, int priority, void** stream);
 int orbx_stream_destroy(void* stream);
 
 /* Kernel status of the last extraction (any path), per frame: 0 = complete; bit 0
- * (ORBX_STATUS_NODE_OVERFLOW) = an octree level needed more nodes than its capacity,
+ * (ORBX_STATUS_NODE_OVERFLOW) = an octree level needed more nodes than its capacity
+ * (or held more than 65535 FAST keypoints, the octree's u16 counters),
  * bit 1 (ORBX_STATUS_ITERATIONS) = an octree loop hit its iteration guard; either way
  * that frame's keypoints are truncated and differ from the reference's DistributeOctTree
  * (ORBextractor.cc:667-1013).  The host paths (orbx_extract, orbx_extract_batch) turn a
@@ -450,6 +451,11 @@ int orbx_matcher_set_footprint(orbx_matcher* m, int mode);
  * orbx_matcher_set_timing(m, 1). */
 int orbx_matcher_set_timing(orbx_matcher* m, int enable);
 int orbx_matcher_last_ms(orbx_matcher* m, float* ms);
+/* Wall time (microseconds) of the newest drop-in host call on m (the SearchByProjection
+ * overloads, SearchForTriangulation, SearchByBoW, SearchForInitialization, Fuse,
+ * SearchBySim3, ComputeStereoMatches): entry to return, i.e. what a C++ caller such as
+ * Tracking pays per call, without any binding overhead.  -1 for a null matcher. */
+double orbx_matcher_last_call_us(const orbx_matcher* m);
 
 /* SearchForTriangulation(KF1, KF2, F12, vMatchedPairs, bOnlyStereo)
  * ORBmatcher.cc:850-1056 (LocalMapping::CreateNewMapPoints, LocalMapping.cc:305).

@@ -37,7 +37,7 @@ EXPORTED = [
     "orbx_window_match_device", "orbx_window_match", "orbx_version", "orbx_device_count",
     "orbx_last_error", "orbx_matcher_create", "orbx_matcher_destroy", "orbx_search_by_projection_local",
     "orbx_search_by_projection_frame", "orbx_search_for_triangulation", "orbx_compute_stereo_matches",
-    "orbx_match_sequence_device", "orbx_matcher_set_timing", "orbx_matcher_last_ms",
+    "orbx_match_sequence_device", "orbx_matcher_set_timing", "orbx_matcher_last_ms", "orbx_matcher_last_call_us",
     "orbx_search_by_projection_keyframe", "orbx_search_by_projection_sim3", "orbx_matcher_set_footprint",
     "orbx_vocabulary_load_text_file", "orbx_vocabulary_load_text", "orbx_vocabulary_destroy",
     "orbx_vocabulary_info", "orbx_vocabulary_stream", "orbx_vocabulary_transform_features",
@@ -189,6 +189,8 @@ def lib() -> C.CDLL:
     L.orbx_matcher_set_timing.argtypes = [vp, C.c_int]
     L.orbx_matcher_set_footprint.argtypes = [vp, C.c_int]
     L.orbx_matcher_last_ms.argtypes = [vp, fp]
+    L.orbx_matcher_last_call_us.argtypes = [vp]
+    L.orbx_matcher_last_call_us.restype = C.c_double
     dp = C.POINTER(C.c_double)
     L.orbx_vocabulary_load_text_file.argtypes = [C.c_char_p, C.c_int, C.POINTER(vp)]
     L.orbx_vocabulary_load_text.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.POINTER(vp)]

@@ -76,7 +76,7 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
 size_t seq_grid_bytes(int cap, int noct);
 hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned char* grids,
                             int cap, unsigned long long* scratch, const long long* d_scratch_off, hipStream_t stream,
-                            int qcap = 0);
+                            int qcap = 0, int replay_rt = 0);
 
 hipError_t launch_seq_build(const SeqArgs& A, int npairs, ProjQuery* queries, ProjProblem* probs,
                             long long* scratch_off, hipStream_t stream);

@@ -612,11 +612,15 @@ struct ProjLds {
 
 // Wave 0's sequential replay (H5) of one problem over the per-query candidate lists qk
 // (kTopK entries per query) built by the scoring phase: every query takes the first still
-// unclaimed entries of its list, the queries of a 64-query chunk before the first one an
-// earlier query of the chunk touches commit together, a query whose list ran out is
-// re-scored against the current claims; then the rotation histogram (ORBmatcher.cc:
-// 1750-1786, 1935-1977).  sfmp / owner: the claims and the owner map by sorted position
-// (LDS); angle_of(p): the angle of the keypoint at sorted position p.  Whole wave active.
+// unclaimed entries of its list (claims only ever block more keypoints, so these are its
+// exact best / second best while the list has them), resolved 64 queries at a time as a
+// fixpoint (below); a query whose list ran out is re-scored against the current claims;
+// then the rotation histogram (ORBmatcher.cc:1750-1786, 1935-1977).  sfmp / owner: the
+// claims and the owner map by sorted position (LDS, owner initialised to 0x7fffffff);
+// elist: kTopK x 64 words of LDS; angle_of(p): the angle of the keypoint at sorted
+// position p.  Whole wave active.  (The previous form committed the chunk's prefix
+// before its first conflict per round: configs[4] 447 rounds and 796 us per problem
+// against 191 iterations and 445 us for this one, configs[1] 73 -> 59 us.)
 template <typename AngleFn>
 __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const SortedGrid& G, int* sfmp, int* owner,
                             unsigned* elist, const uint4* qk, const int* qmp, const float* qang, int* mlist,
@@ -628,7 +632,6 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
     const float factor = kHistoLength / 360.0f;
     const int need = P.ratio_mode ? 2 : 1;
     const unsigned long long below = (1ull << lane) - 1;
-#ifndef ORBX_REPLAY_ROUNDS
     // Fixpoint form.  The reference's loop is a function of the query order: query l's
     // choice (first two unclaimed entries, acceptance) depends only on the claims of the
     // queries before it.  Within a 64-query chunk every lane evaluates its choice against
@@ -761,11 +764,12 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
             // all atomics, then all reads, then the reset)
             if (prop >= 0) atomicMin(&owner[prop], lane);
 #pragma unroll
-            for (int j = 0; j < kTopK; j++) ow[j] = act ? owner[oa[j]] : 0x7fffffff;
+            for (int j = 0; j < kTopK; j++) ow[j] = owner[oa[j]];  // every lane: no exec-masked reads
             if (prop >= 0) owner[prop] = 0x7fffffff;
+            // bit j: entry j proposed by an earlier lane (ow - lane < 0; ow >= 0, lane < 64)
             unsigned sb = 0;
 #pragma unroll
-            for (int j = 0; j < kTopK; j++) sb |= (ow[j] < lane ? 1u : 0u) << j;
+            for (int j = 0; j < kTopK; j++) sb |= ((unsigned)(ow[j] - lane) >> 31) << j;
             if (act) eval(cblk | sb);
             if (__ballot(act && sig() != old)) continue;
             // fixpoint: every active lane's choice is the sequential one up to the first
@@ -795,7 +799,7 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
             // the committed lanes' claims, for the lanes after them: the entries a lane
             // below f proposed (blocking proposals only reach the owner map)
 #pragma unroll
-            for (int j = 0; j < kTopK; j++) cblk |= (act && lane >= lim && ow[j] < f ? 1u : 0u) << j;
+            for (int j = 0; j < kTopK; j++) cblk |= (act && lane >= lim ? (unsigned)(ow[j] - f) >> 31 : 0u) << j;
             start = lim;
             if (!fnb) {
                 // lane f's list ran out: re-score it against the current claims.  Any list
@@ -812,7 +816,6 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
                     ntrunc += __builtin_amdgcn_readlane((int)tr, f);
                 }
                 unsigned ne[kTopK];
-#ifndef ORBX_RESCORE_SINGLE
                 if (__popcll(X) > 1) {
                     // rows 0..3 take the first four exhausted lanes
                     const int row = lane >> 4;
@@ -834,9 +837,7 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
                         set_list();
                         eval(0);
                     }
-                } else
-#endif
-                {
+                } else {
                     score_groupk<64>(pb, P, bcast_query(mine, f), true, G, sfmp, ne);  // wave-uniform result
 #pragma unroll
                     for (int j = 0; j < kTopK; j++)
@@ -855,148 +856,6 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
         wave_lds_fence();
     }
     if (guard < 0) nmatch = -1;  // a broken fixpoint (never observed): fail the parity check loudly
-#else
-    for (int base = 0; base < nq; base += 64) {
-        const int q = base + lane;
-        int mp = -1;
-        unsigned e[kTopK];
-#pragma unroll
-        for (int j = 0; j < kTopK; j++) e[j] = kNoEntry;
-        const unsigned long long t_chunk = st ? wall_clock64() : 0;
-        QueryReg mine;  // consumed only by a re-scoring (loads overlap the first round)
-        if (q < nq) mine = load_query(pb, q);
-        if (q < nq) {
-            mp = qmp[q];
-#pragma unroll
-            for (int v = 0; v < kListVec; v++) {
-                const uint4 x4 = qk[kListVec * q + v];
-                e[4 * v] = x4.x; e[4 * v + 1] = x4.y; e[4 * v + 2] = x4.z; e[4 * v + 3] = x4.w;
-            }
-        }
-        int start = 0;
-        // Per lane: c1 / c2 = the first two unclaimed entries of its list, exhausted = a
-        // full or truncated list ran out.  They only change when a claim lands on c1 or
-        // c2, so a round re-derives them only for the lanes whose c1 / c2 an earlier lane
-        // committed (and for a re-scored lane), not the whole list of every lane.
-        unsigned c1 = kNoEntry, c2 = kNoEntry;
-        bool exhausted = false;
-        bool refresh = true;
-        while (true) {
-            niter++;
-            const bool act = lane >= start && mp >= 0;
-            if (__ballot(act && refresh)) {
-                if (act && refresh) {
-                    // all the list's claim words in one batch of independent LDS reads (and
-                    // Observations() loads), not one dependent read per entry
-                    const int last = pb.n > 0 ? pb.n - 1 : 0;
-                    int fm[kTopK];
-                    bool blk[kTopK];
-#pragma unroll
-                    for (int j = 0; j < kTopK; j++) fm[j] = sfmp[min(ent_pos(e[j]), last)];
-                    if (P.blocked_mode == 1) {
-#pragma unroll
-                        for (int j = 0; j < kTopK; j++) blk[j] = fm[j] >= 0;
-                    } else {
-                        int ob[kTopK];
-#pragma unroll
-                        for (int j = 0; j < kTopK; j++) ob[j] = P.mp_obs[fm[j] >= 0 ? fm[j] : 0];
-#pragma unroll
-                        for (int j = 0; j < kTopK; j++) blk[j] = fm[j] >= 0 && ob[j] > 0;
-                    }
-                    int found = 0;
-                    c1 = kNoEntry;
-                    c2 = kNoEntry;
-#pragma unroll
-                    for (int j = 0; j < kTopK; j++) {
-                        if (e[j] < kTrunc && found < 2 && !blk[j]) {
-                            if (found == 0) c1 = e[j];
-                            else c2 = e[j];
-                            found++;
-                        }
-                    }
-                    // a full (or truncated) list may hide unlisted candidates -- but they are
-                    // at least as far as its last exact entry (the list holds the smallest
-                    // keys), so when that entry, or the unclaimed c1 of a ratio test, is
-                    // already beyond the acceptance threshold the query stays unmatched
-                    exhausted = e[kTopK - 1] != kNoEntry && found < need;
-                    if (exhausted) {
-                        int lastd = -1;
-#pragma unroll
-                        for (int j = 0; j < kTopK; j++)
-                            if (e[j] < kTrunc) lastd = ent_dist(e[j]);
-                        if (found == 0 && lastd > P.accept_th) exhausted = false;
-                        if (found == 1 && ent_dist(c1) > P.accept_th) exhausted = false;
-                    }
-                }
-            }
-            bool acc = false;
-            if (act && !exhausted && c1 != kNoEntry && ent_dist(c1) <= P.accept_th) {
-                acc = true;
-                if (P.ratio_mode) {
-                    const int bestLevel2 = c2 == kNoEntry ? -1 : ent_oct(c2);
-                    const int bestDist2 = c2 == kNoEntry ? 256 : ent_dist(c2);
-                    if (ent_oct(c1) == bestLevel2 && (float)ent_dist(c1) > P.nnratio * (float)bestDist2)
-                        acc = false;
-                }
-            }
-            const int tpos = acc ? ent_pos(c1) : -1;
-            // A query depends on an earlier one of the chunk if that one claims its best
-            // (or, with the ratio test, second best) keypoint.  Without the ratio test a
-            // query that does not accept its c1 cannot be affected: every later entry is
-            // at least as far (the list is in key order), so it stays unmatched.
-            // owner[p] = lowest lane of this round claiming p (LDS ops of a wave are
-            // executed in order: all atomics, then all reads, then the reset).
-            if (acc) atomicMin(&owner[tpos], lane);
-            int o1 = 0x7fffffff, o2 = 0x7fffffff;
-            if (act && !exhausted) {
-                if (c1 != kNoEntry && (acc || P.ratio_mode)) o1 = owner[ent_pos(c1)];
-                if (P.ratio_mode && c2 != kNoEntry) o2 = owner[ent_pos(c2)];
-            }
-            if (acc) owner[tpos] = 0x7fffffff;
-            const bool conf = (act && exhausted) || o1 < lane || o2 < lane;
-            const unsigned long long cm = __ballot(conf);
-            const int f = cm ? __ffsll((long long)cm) - 1 : 64;
-            const bool com = acc && lane < f;
-            const unsigned long long comm = __ballot(com);
-            if (com) sfmp[tpos] = mp;
-            nmatch += __popcll(comm);
-            if (P.check_ori) {
-                // the match is recorded with its query; the rotation bins are computed
-                // after the replay, off the sequential path
-                if (com) {
-                    const int r = nrec + __popcll(comm & below);
-                    mlist[r] = tpos;
-                    mbin[r] = q;
-                }
-                nrec += __popcll(comm);
-            }
-            if (f >= 64) break;
-            if (st && start == 0) t_first += wall_clock64() - t_chunk;
-            // c1 / c2 claimed by a committed lane (lanes < f), or lane f itself
-            refresh = lane == f || o1 < f || o2 < f;
-            if (__builtin_amdgcn_readlane((int)exhausted, f)) {
-                const unsigned long long t0 = st ? wall_clock64() : 0;
-                nrescore++;
-                if (st) {  // diagnostics: the list ran out at a truncation, not at its 8th entry
-                    bool tr = false;
-#pragma unroll
-                    for (int j = 0; j < kTopK; j++) tr = tr || e[j] == kTrunc;
-                    ntrunc += __builtin_amdgcn_readlane((int)tr, f);
-                }
-                wave_lds_fence();
-                unsigned ne[kTopK];
-                score_groupk<64>(pb, P, bcast_query(mine, f), true, G, sfmp, ne);  // wave-uniform result
-#pragma unroll
-                for (int j = 0; j < kTopK; j++)
-                    if (lane == f) e[j] = ne[j];
-                if (st) t_res += wall_clock64() - t0;
-            }
-            start = f;
-            wave_lds_fence();
-        }
-        wave_lds_fence();
-    }
-#endif
     // the match list (global scratch in some modes) is read back by other lanes below
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -1055,6 +914,288 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
         st[8] = t_res;
         st[9] = t_first;
     }
+}
+
+// The replay over RT threads (RT / 64 waves): the fixpoint of proj_replay over chunks of
+// RT queries instead of 64.  The iterations a chunk takes are set by its longest
+// dependency chain, not by its size, so wider chunks mean fewer iterations per query;
+// every exhausted list of a chunk is re-scored at the first sequence point (each wave
+// its own lanes, four per 16-lane-row pass), so a chunk rarely stops twice.
+// owner[p] (zero-initialised, n words): (iteration << 10 | 1023 - thread) of the lowest
+// thread proposing p this iteration (atomicMax; stale iterations are ignored, so the map
+// is never reset).  elist: kTopK x RT words.  Whole workgroup of RT threads.
+template <int RT, typename AngleFn>
+__device__ void proj_replay_block(const ProjProblem& pb, const ProjParams& P, const SortedGrid& G, int* sfmp,
+                                  unsigned* owner, unsigned* elist, const uint4* qk, const int* qmp,
+                                  const float* qang, int* mlist, int* mbin, int* s_hist, AngleFn angle_of,
+                                  unsigned long long* st) {
+    static_assert(RT % 64 == 0 && RT <= 1024, "whole waves, 10-bit thread tags");
+    constexpr int kW = RT / 64;
+    __shared__ int s_key;
+    __shared__ int s_wc[kW];
+    __shared__ int s_bad;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nq = pb.nq;
+    const int lastp = pb.n > 0 ? pb.n - 1 : 0;
+    const int need = P.ratio_mode ? 2 : 1;
+    const unsigned long long below = (1ull << lane) - 1;
+    const float factor = kHistoLength / 360.0f;
+    int nmatch = 0, nrec = 0, nrescore = 0, niter = 0;  // block-uniform
+    unsigned it = 0;
+    long long guard = 0;
+    bool broken = false;
+    if (tid == 0) s_key = 0x7fffffff;
+    // a chunk's lists, MapPoints and queries are loaded while the chunk before it replays
+    uint4 nx_l[kListVec];
+    int nx_mp = -1;
+    QueryReg nx_q;
+    auto fetch = [&](int qn) {
+        nx_mp = -1;
+        if (qn < nq) {
+            nx_q = load_query(pb, qn);
+            nx_mp = qmp[qn];
+#pragma unroll
+            for (int v = 0; v < kListVec; v++) nx_l[v] = qk[kListVec * qn + v];
+        }
+    };
+    fetch(tid);
+    __syncthreads();
+    for (int base = 0; base < nq && !broken; base += RT) {
+        if (it > (1u << 20)) {  // keep iteration << 10 in 31 bits: restart the tags
+            for (int p = tid; p < pb.n; p += RT) owner[p] = 0u;
+            it = 0;
+            __syncthreads();
+        }
+        const int q = base + tid;
+        const int mp = nx_mp;
+        unsigned e[kTopK];
+#pragma unroll
+        for (int v = 0; v < kListVec; v++) {
+            e[4 * v] = mp >= 0 ? nx_l[v].x : kNoEntry;
+            e[4 * v + 1] = mp >= 0 ? nx_l[v].y : kNoEntry;
+            e[4 * v + 2] = mp >= 0 ? nx_l[v].z : kNoEntry;
+            e[4 * v + 3] = mp >= 0 ? nx_l[v].w : kNoEntry;
+        }
+        const QueryReg mine = nx_q;
+        fetch(q + RT);
+        unsigned vm = 0;
+        bool full = false, lastgt = false;
+        int oa[kTopK];
+        auto set_list = [&]() {
+            vm = 0;
+            int lastd = -1;
+#pragma unroll
+            for (int j = 0; j < kTopK; j++) {
+                elist[j * RT + tid] = e[j];
+                oa[j] = min(ent_pos(e[j]), lastp);
+                vm |= (e[j] < kTrunc ? 1u : 0u) << j;
+                if (e[j] < kTrunc) lastd = ent_dist(e[j]);
+            }
+            full = e[kTopK - 1] != kNoEntry;
+            lastgt = lastd > P.accept_th;
+        };
+        set_list();
+        bool bself = false;
+        unsigned cblk = 0;
+        if (mp >= 0) {
+            bself = P.blocked_mode == 1 || P.mp_obs[mp] > 0;
+            int fm[kTopK];
+#pragma unroll
+            for (int j = 0; j < kTopK; j++) fm[j] = sfmp[oa[j]];
+            if (P.blocked_mode == 1) {
+#pragma unroll
+                for (int j = 0; j < kTopK; j++) cblk |= (fm[j] >= 0 ? 1u : 0u) << j;
+            } else {
+                int ob[kTopK];
+#pragma unroll
+                for (int j = 0; j < kTopK; j++) ob[j] = P.mp_obs[fm[j] >= 0 ? fm[j] : 0];
+#pragma unroll
+                for (int j = 0; j < kTopK; j++) cblk |= (fm[j] >= 0 && ob[j] > 0 ? 1u : 0u) << j;
+            }
+        }
+        unsigned c1 = kNoEntry;
+        bool exh = false, acc = false;
+        auto eval = [&](unsigned bm) {
+            const unsigned fm = vm & ~bm;
+            const int cnt = __popc(fm);
+            const unsigned a1 = fm ? elist[__builtin_ctz(fm) * RT + tid] : kNoEntry;
+            bool x = full && cnt < need;
+            if (x && ((cnt == 0 && lastgt) || (cnt == 1 && ent_dist(a1) > P.accept_th))) x = false;
+            bool a = !x && fm != 0 && ent_dist(a1) <= P.accept_th;
+            if (a && P.ratio_mode) {
+                const unsigned f2 = fm & (fm - 1);
+                const unsigned a2 = f2 ? elist[__builtin_ctz(f2) * RT + tid] : kNoEntry;
+                const int bestLevel2 = a2 == kNoEntry ? -1 : ent_oct(a2);
+                const int bestDist2 = a2 == kNoEntry ? 256 : ent_dist(a2);
+                if (ent_oct(a1) == bestLevel2 && (float)ent_dist(a1) > P.nnratio * (float)bestDist2) a = false;
+            }
+            c1 = a1;
+            exh = x;
+            acc = a;
+        };
+        auto sig = [&]() { return exh ? kTrunc : (acc ? c1 : kNoEntry); };
+        if (mp >= 0) eval(cblk);
+        int start = 0;
+        unsigned ow[kTopK];
+        while (true) {
+            niter++;
+            if (++guard > 66ll * (nq + RT)) {  // never reached: <= RT + 1 iterations per fixpoint
+                broken = true;
+                break;
+            }
+            it++;
+            const bool act = tid >= start && mp >= 0;
+            const unsigned old = sig();
+            if (act && acc && bself) atomicMax(&owner[ent_pos(c1)], (it << 10) | (unsigned)(1023 - tid));
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kTopK; j++) ow[j] = owner[oa[j]];
+            // bit j: entry j proposed this iteration by a thread before this one
+            unsigned sb = 0;
+#pragma unroll
+            for (int j = 0; j < kTopK; j++)
+                sb |= ((ow[j] >> 10) == it && (int)(1023u - (ow[j] & 1023u)) < tid ? 1u : 0u) << j;
+            if (act) eval(cblk | sb);
+            if (__syncthreads_or(act && sig() != old)) continue;
+            // fixpoint: the first sequence point f (exhausted, or a non-blocking acceptor)
+            const bool nbl = act && acc && !bself;
+            int key = act && (exh || nbl) ? 2 * tid + (exh ? 0 : 1) : 0x7fffffff;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) key = min(key, __shfl_xor(key, o));
+            if (lane == 0 && key != 0x7fffffff) atomicMin(&s_key, key);
+            __syncthreads();
+            const int K = s_key;
+            const int f = K == 0x7fffffff ? RT : (K >> 1);
+            const bool fnb = K != 0x7fffffff && (K & 1);
+            const int lim = fnb ? f + 1 : f;  // threads below lim commit
+            const bool com = act && acc && tid < lim;
+            if (com) sfmp[ent_pos(c1)] = mp;
+            const unsigned long long cm = __ballot(com);
+            if (lane == 0) s_wc[wave] = __popcll(cm);
+            __syncthreads();
+            if (tid == 0) s_key = 0x7fffffff;  // read by every thread before the barrier above
+            int tot = 0, woff = 0;
+#pragma unroll
+            for (int w = 0; w < kW; w++) {
+                const int c = s_wc[w];
+                woff += w < wave ? c : 0;
+                tot += c;
+            }
+            if (P.check_ori && com) {
+                const int r = nrec + woff + __popcll(cm & below);
+                mlist[r] = ent_pos(c1);
+                mbin[r] = q;
+            }
+            nmatch += tot;
+            if (P.check_ori) nrec += tot;
+            if (f >= RT) break;
+            // the committed threads' claims, for the threads after them
+            if (act && tid >= lim) {
+#pragma unroll
+                for (int j = 0; j < kTopK; j++)
+                    cblk |= ((ow[j] >> 10) == it && (int)(1023u - (ow[j] & 1023u)) < f ? 1u : 0u) << j;
+            }
+            start = lim;
+            if (!fnb) {
+                // every exhausted list at or after f, against the current claims (sfmp is
+                // published by the barrier above)
+                unsigned long long X = __ballot(act && exh && tid >= f);
+                while (X) {
+                    unsigned ne[kTopK];
+                    if (__popcll(X) == 1) {
+                        const int src = __ffsll((long long)X) - 1;
+                        score_groupk<64>(pb, P, bcast_query(mine, src), true, G, sfmp, ne);
+#pragma unroll
+                        for (int j = 0; j < kTopK; j++)
+                            if (lane == src) e[j] = ne[j];
+                        nrescore++;
+                        if (lane == src) {
+                            cblk = 0;
+                            set_list();
+                            eval(0);
+                        }
+                        X = 0;
+                    } else {
+                        const int row = lane >> 4;
+                        unsigned long long x = X;
+                        for (int r = 0; r < row; r++) x &= x - 1;
+                        const bool valid = x != 0;
+                        const int src = valid ? __ffsll((long long)x) - 1 : 0;
+                        score_groupk<16>(pb, P, shfl_query(mine, src), valid, G, sfmp, ne);
+                        const int myrow = __popcll(X & below);
+                        const bool take = ((X >> lane) & 1ull) && myrow < 4;
+#pragma unroll
+                        for (int j = 0; j < kTopK; j++) {
+                            const unsigned v = (unsigned)__shfl((int)ne[j], (myrow & 3) * 16);
+                            if (take) e[j] = v;
+                        }
+                        nrescore += __popcll(X) < 4 ? __popcll(X) : 4;
+                        if (take) {
+                            cblk = 0;
+                            set_list();
+                            eval(0);
+                        }
+                        for (int r = 0; r < 4 && X; r++) X &= X - 1;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // every thread keeps the same counters; the match list is complete after the barrier
+    __syncthreads();
+    if (P.check_ori && !broken) {
+        // rotHist of the committed matches (ORBmatcher.cc:1750-1757)
+        for (int m = tid; m < nrec; m += RT) {
+            const int tpos = mlist[m];
+            float rot = qang[mbin[m]] - angle_of(tpos);
+            if (rot < 0.0f) rot += 360.0f;
+            int bin = (int)roundf(rot * factor);
+            if (bin == kHistoLength) bin = 0;
+            mbin[m] = bin;
+            atomicAdd(&s_hist[bin], 1);
+        }
+        if (tid == 0) s_bad = 0;
+        __syncthreads();
+        // ComputeThreeMaxima, ORBmatcher.cc:1935-1977 (every thread, same result)
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < kHistoLength; i++) {
+            const int s = s_hist[i];
+            if (s > max1) {
+                max3 = max2; max2 = max1; max1 = s;
+                ind3 = ind2; ind2 = ind1; ind1 = i;
+            } else if (s > max2) {
+                max3 = max2; max2 = s;
+                ind3 = ind2; ind2 = i;
+            } else if (s > max3) {
+                max3 = s;
+                ind3 = i;
+            }
+        }
+        if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+        else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+        int bad = 0;
+        for (int m = tid; m < nrec; m += RT) {
+            const int b = mbin[m];
+            if (b != ind1 && b != ind2 && b != ind3) {
+                sfmp[mlist[m]] = -1;
+                bad++;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o);
+        if (lane == 0 && bad) atomicAdd(&s_bad, bad);
+        __syncthreads();
+        nmatch -= s_bad;
+    }
+    if (tid == 0) *pb.nmatches = broken ? -1 : nmatch;  // a broken fixpoint (never observed) fails parity loudly
+    if (st && tid == 0) {
+        st[3] = wall_clock64();
+        st[5] = nrescore;
+        st[6] = nq;
+        st[7] = niter;
+    }
+    __syncthreads();
 }
 
 // Byte layout of one problem's grid in the global grid area.
@@ -1231,6 +1372,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
 
 constexpr int kSeqGridThreads = 256;
 
+template <int kSeqGridThreads>  // (shadows the batch default of the same name)
 __global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem* __restrict__ probs,
                                                               unsigned char* __restrict__ grids, int cap, int noct) {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -1303,76 +1445,116 @@ __global__ __launch_bounds__(kSeqScoreThreads) void k_seq_score(const ProjProble
     }
 }
 
-__global__ __launch_bounds__(64) void k_seq_commit(const ProjProblem* __restrict__ probs, ProjParams P,
+template <int RT>
+__global__ __launch_bounds__(RT) void k_seq_commit(const ProjProblem* __restrict__ probs, ProjParams P,
                                                    unsigned char* __restrict__ grids, int cap,
                                                    unsigned long long* __restrict__ scratch,
                                                    const long long* __restrict__ scratch_off, int use_sdesc) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_hist[kHistoLength];
 #ifndef ORBX_NO_REPLAY_PRIO
-    // the replay is one latency-bound wave per problem that shares its CU with the
-    // extraction's throughput waves: the highest wave priority makes the SIMD's arbiter
-    // issue its instructions first
+    // the replay is latency-bound and shares its CU with the extraction's throughput
+    // waves: the highest wave priority makes the SIMD's arbiter issue its instructions first
     __builtin_amdgcn_s_setprio(3);
 #endif
     const ProjProblem pb = probs[blockIdx.x];
+    unsigned long long* st = P.stamps ? P.stamps + kStampWords * blockIdx.x : nullptr;  // diagnostics
+    if (st && threadIdx.x == 0) st[13] = wall_clock64();
     const SeqGridLayout gl(cap, P.noct);
     SortedGrid G = seq_grid(grids + (size_t)blockIdx.x * gl.total, gl, P.noct);
     if (!use_sdesc) G.sdesc = nullptr;  // descriptors by keypoint index from the frame
     const float* gang = (const float*)(grids + (size_t)blockIdx.x * gl.total + gl.sang);
-    const int lane = threadIdx.x, n = pb.n, nq = pb.nq;
+    const int tid = threadIdx.x, n = pb.n, nq = pb.nq;
     // LDS: the replay's lists, the claims and the owner map only (8 B per keypoint); the
     // rotation bins read the grid's angles from global memory after the replay
     unsigned* elist = (unsigned*)smem;
-    int* sfmp = (int*)(elist + kTopK * 64);
+    int* sfmp = (int*)(elist + kTopK * RT);
     int* owner = sfmp + n;
-    for (int p = lane; p < n; p += 64) {
+    for (int p = tid; p < n; p += RT) {
         sfmp[p] = pb.frame_mp[sk_idx(G.skey[p])];
-        owner[p] = 0x7fffffff;
+        owner[p] = RT == 64 ? 0x7fffffff : 0;
     }
-    if (lane < kHistoLength) s_hist[lane] = 0;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    __builtin_amdgcn_wave_barrier();
+    if (tid < kHistoLength) s_hist[tid] = 0;
+    __syncthreads();
     unsigned long long* g = scratch + scratch_off[blockIdx.x];
     const uint4* qk = (const uint4*)g;
     const int* qmp = (const int*)(g + kListWords * (size_t)nq);
     const float* qang = (const float*)(qmp + nq);
     int* mlist = (int*)(qang + nq);
     int* mbin = mlist + nq;
-    proj_replay(pb, P, G, sfmp, owner, elist, qk, qmp, qang, mlist, mbin, s_hist, [&](int tpos) { return gang[tpos]; },
-                nullptr);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    for (int p = lane; p < n; p += 64) pb.frame_mp[sk_idx(G.skey[p])] = sfmp[p];
+    if constexpr (RT == 64)
+        proj_replay(pb, P, G, sfmp, owner, elist, qk, qmp, qang, mlist, mbin, s_hist,
+                    [&](int tpos) { return gang[tpos]; }, st);
+    else
+        proj_replay_block<RT>(pb, P, G, sfmp, (unsigned*)owner, elist, qk, qmp, qang, mlist, mbin, s_hist,
+                              [&](int tpos) { return gang[tpos]; }, st);
+    __syncthreads();
+    int32_t* out = P.out_mp ? P.out_mp : pb.frame_mp;
+    for (int p = tid; p < n; p += RT) out[sk_idx(G.skey[p])] = sfmp[p];
 }
 
 size_t seq_grid_bytes(int cap, int noct) { return SeqGridLayout(cap, noct).total; }
 
 // k_seq_commit's dynamic LDS: the replay's lists, then the claims and the owner map
-static size_t seq_commit_lds(int cap) { return (size_t)kTopK * 64 * 4 + (size_t)cap * 8; }
+static size_t seq_commit_lds(int cap, int rt) { return (size_t)kTopK * rt * 4 + (size_t)cap * 8; }
+
+// Threads of the replay workgroup: `rt` if given (64, 256 or 1024), else ORBX_REPLAY_THREADS,
+// else 256 for a batch (four waves: configs[4] 93.4-94.2k -> 93.8-95.2k frames/s and
+// configs[1] 217.7-219.0k -> 222.3-223.8k against one wave; 1024 threads is slower in
+// both, its iterations cost more than the chains it shortens) and one wave for a single
+// problem (the drop-in host calls: their scenes' conflict chains run across the whole
+// chunk, 90 iterations of ~1.9 us at 256 against 109 of ~1.2 us at 64 for a12).
+static int replay_threads(int rt, int nprob) {
+    if (rt != 64 && rt != 256 && rt != 1024) {
+        static const int env = [] {
+            const char* v = getenv("ORBX_REPLAY_THREADS");
+            return v ? atoi(v) : 0;
+        }();
+        rt = env;
+    }
+    if (rt != 64 && rt != 256 && rt != 1024) rt = nprob == 1 ? 64 : 256;
+    return rt;
+}
+
+static hipError_t launch_seq_commit(int rt, const ProjProblem* d_probs, int nprob, const ProjParams& P,
+                                    unsigned char* grids, int cap, unsigned long long* scratch,
+                                    const long long* d_scratch_off, int use_sdesc, hipStream_t stream) {
+    rt = replay_threads(rt, nprob);
+    const size_t lds = seq_commit_lds(cap, rt);
+    const void* fn = rt == 64 ? (const void*)k_seq_commit<64>
+                              : (rt == 256 ? (const void*)k_seq_commit<256> : (const void*)k_seq_commit<1024>);
+    if (lds > 150 * 1024) return hipErrorInvalidValue;
+    if (lds > 64 * 1024) {
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    void* args[] = {(void*)&d_probs, (void*)&P, (void*)&grids, (void*)&cap, (void*)&scratch, (void*)&d_scratch_off,
+                    (void*)&use_sdesc};
+    return hipLaunchKernel(fn, dim3(nprob), dim3(rt), args, lds, stream);
+}
 
 hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned char* grids,
                             int cap, unsigned long long* scratch, const long long* d_scratch_off, hipStream_t stream,
-                            int qcap) {
+                            int qcap, int replay_rt) {
     if (nprob <= 0) return hipSuccess;
     if (cap <= 0 || cap >= 8192) return hipErrorInvalidValue;  // 13-bit keypoint positions
     if (qcap <= 0) qcap = cap;
     if (P.noct < 1 || P.noct > 32) return hipErrorInvalidValue;
     const size_t scr = octave_runs_scratch(P.noct) > kGridSortScratch ? octave_runs_scratch(P.noct) : kGridSortScratch;
     const size_t lds_grid = align16(align16((size_t)cap * 4) + (size_t)(kGridCols + 1) * 2) + scr;
-    const size_t lds_commit = seq_commit_lds(cap);
+    // a few problems (the drop-in host calls): 1024 threads per grid, the sort is then on
+    // the call's critical path (28 -> ~10 us at C1); a batch: 256, beside the extraction
+    const bool wide = nprob < 32;
+    const void* gfn = wide ? (const void*)k_seq_grid<1024> : (const void*)k_seq_grid<kSeqGridThreads>;
     if (lds_grid > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_seq_grid, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)lds_grid);
+        hipError_t e = hipFuncSetAttribute(gfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_grid);
         if (e != hipSuccess) return e;
     }
-    if (lds_commit > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_seq_commit, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)lds_commit);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(k_seq_grid, dim3(nprob), dim3(kSeqGridThreads), lds_grid, stream, d_probs, grids, cap,
-                       P.noct);
+    if (wide)
+        hipLaunchKernelGGL(k_seq_grid<1024>, dim3(nprob), dim3(1024), lds_grid, stream, d_probs, grids, cap, P.noct);
+    else
+        hipLaunchKernelGGL(k_seq_grid<kSeqGridThreads>, dim3(nprob), dim3(kSeqGridThreads), lds_grid, stream, d_probs,
+                           grids, cap, P.noct);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int qblocks = (qcap + kSeqScoreQ - 1) / kSeqScoreQ;
@@ -1381,9 +1563,7 @@ hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjPar
                        nprob, qblocks, P, grids, cap, scratch, d_scratch_off);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_seq_commit, dim3(nprob), dim3(64), lds_commit, stream, d_probs, P, grids, cap, scratch,
-                       d_scratch_off, 1);
-    return hipGetLastError();
+    return launch_seq_commit(replay_rt, d_probs, nprob, P, grids, cap, scratch, d_scratch_off, 1, stream);
 }
 
 // Batched TrackWithMotionModel matching over a device-resident sequence: problem p
@@ -1688,14 +1868,7 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
                     (void*)&gcap};
     hipError_t e = hipLaunchKernel(fn, dim3(nprob), dim3(nt), args, lds, stream);
     if (e != hipSuccess || !split_grids) return e;
-    const size_t lds_commit = seq_commit_lds(max_n);
-    if (lds_commit > 64 * 1024) {
-        e = hipFuncSetAttribute((const void*)k_seq_commit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_commit);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(k_seq_commit, dim3(nprob), dim3(64), lds_commit, stream, d_probs, P, split_grids, max_n, scratch,
-                       d_scratch_off, 0);
-    return hipGetLastError();
+    return launch_seq_commit(0, d_probs, nprob, P, split_grids, max_n, scratch, d_scratch_off, 0, stream);
 }
 
 // ------------------------------------------------------------------ triangulation

@@ -65,6 +65,8 @@ struct ProjParams {
     int check_ori;          // rotation-consistency histogram (a12, a13)
     unsigned long long* stamps;  // optional: kStampWords per-problem phase stamps and counters (diagnostics)
     int noct;               // octave buckets of the sorted grid: > every keypoint octave (1..32)
+    int32_t* out_mp;        // optional (k_seq_commit): mvpMapPoints written here instead of
+                            // frame_mp -- host-mapped memory for the single host calls
 };
 
 // Batched frame-to-frame matching over an extracted device sequence.

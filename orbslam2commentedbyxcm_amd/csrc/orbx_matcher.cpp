@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <new>
@@ -215,7 +216,26 @@ struct orbx_matcher {
     char* lscr = nullptr;
     size_t lscr_cap = 0;
     StageRing stage;
+    // wall time of the newest drop-in host call (entry to return), as a C++ caller sees it
+    double last_call_us = 0.0;
+    // host-mapped pinned results of the single projection calls (mvpMapPoints + count):
+    // the commit kernel writes them over PCIe, so a call needs no device-to-host copy
+    int32_t* hmp = nullptr;
+    int32_t* hmp_dev = nullptr;
+    size_t hmp_cap = 0;
 };
+
+namespace {
+// Scoped: stores the enclosing host call's wall time in m->last_call_us.
+struct CallClock {
+    orbx_matcher* m;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    explicit CallClock(orbx_matcher* mm) : m(mm) {}
+    ~CallClock() {
+        if (m) m->last_call_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    }
+};
+}  // namespace
 
 namespace {
 
@@ -228,6 +248,7 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
         if (nmatches) *nmatches = 0;
         return ORBX_OK;
     }
+    const auto t_stage0 = std::chrono::steady_clock::now();
     HIP_TRY(hipSetDevice(m->device));
     const int nobs = mps->n;
     size_t need = pad(sizeof(orbx_keypoint) * n) + pad((size_t)n * 32) + pad(sizeof(float) * n) +
@@ -288,15 +309,58 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
     ProjParams P = base_params;
     P.mp_obs = d_obs;
     P.noct = noct;
+    // ORBX_CALL_STAMPS=1: the call's host phases and the replay's counters to stderr
+    // (diagnostics only)
+    static const bool call_stamps = getenv("ORBX_CALL_STAMPS") != nullptr;
+    unsigned long long* d_st = nullptr;
+    const auto t_flush = std::chrono::steady_clock::now();
+    if (call_stamps) {
+        HIP_TRY(hipMalloc(&d_st, sizeof(unsigned long long) * kStampWords));
+        HIP_TRY(hipMemsetAsync(d_st, 0, sizeof(unsigned long long) * kStampWords, s));
+        P.stamps = d_st;
+    }
+    // results straight into host-mapped memory (k_seq_commit's out_mp and the count)
+    const bool mapped = gcap < 8192;
+    if (mapped && m->hmp_cap < (size_t)n + 1) {
+        HIP_TRY(hipStreamSynchronize(s));
+        if (m->hmp) (void)hipHostFree(m->hmp);
+        m->hmp = m->hmp_dev = nullptr;
+        m->hmp_cap = 0;
+        HIP_TRY(hipHostMalloc((void**)&m->hmp, sizeof(int32_t) * ((size_t)n + 1), hipHostMallocMapped));
+        HIP_TRY(hipHostGetDevicePointer((void**)&m->hmp_dev, m->hmp, 0));
+        m->hmp_cap = (size_t)n + 1;
+    }
+    if (mapped) {
+        P.out_mp = m->hmp_dev + 1;
+        pb.nmatches = m->hmp_dev;
+        m->arena.up(d_prob, &pb, sizeof(pb));
+    }
     HIP_TRY(m->arena.flush(s));
-    if (gcap < 8192)
+    if (mapped)
         HIP_TRY(launch_seq_split(d_prob, 1, P, d_grid, gcap, d_scr, d_off, s));
     else
         HIP_TRY(launch_proj_search(d_prob, 1, P, d_scr, d_off, n, nq, s));
     int nm = 0;
-    HIP_TRY(m->arena.down(frame_mp, d_fmp, sizeof(int32_t) * n, s));
-    HIP_TRY(m->arena.down(&nm, d_nm, sizeof(int32_t), s));
+    if (!mapped) {
+        HIP_TRY(m->arena.down(frame_mp, d_fmp, sizeof(int32_t) * n, s));
+        HIP_TRY(m->arena.down(&nm, d_nm, sizeof(int32_t), s));
+    }
+    const auto t_enq = std::chrono::steady_clock::now();
     HIP_TRY(m->arena.sync(s));
+    if (mapped) {
+        std::memcpy(frame_mp, m->hmp + 1, sizeof(int32_t) * n);
+        nm = m->hmp[0];
+    }
+    if (call_stamps) {
+        const auto t_done = std::chrono::steady_clock::now();
+        unsigned long long h[kStampWords];
+        HIP_TRY(hipMemcpy(h, d_st, sizeof(h), hipMemcpyDeviceToHost));
+        HIP_TRY(hipFree(d_st));
+        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        fprintf(stderr, "[orbx call] n=%d nq=%d | host staging %.1f us, enqueue %.1f us, wait %.1f us | replay %.1f us, "
+                "%llu iterations, %llu re-scored\n", n, nq, us(t_stage0, t_flush), us(t_flush, t_enq), us(t_enq, t_done),
+                (double)(h[3] - h[13]) * 0.01, h[7], h[5]);
+    }
     if (nmatches) *nmatches = nm;
     return ORBX_OK;
 }
@@ -333,6 +397,7 @@ void orbx_matcher_destroy(orbx_matcher* m) {
     if (m->tscr) (void)hipFree(m->tscr);
     if (m->lscr) (void)hipFree(m->lscr);
     m->stage.release();
+    if (m->hmp) (void)hipHostFree(m->hmp);
     for (auto& slot : m->ev)
         for (auto& e : slot)
             if (e) (void)hipEventDestroy(e);
@@ -344,6 +409,7 @@ void orbx_matcher_destroy(orbx_matcher* m) {
 int orbx_search_by_projection_local(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp,
                                     const int32_t* queries, int nq, const orbx_mappoints* mps, const orbx_track* trk,
                                     float th, int* nmatches) {
+    const CallClock clock_(m);
     if (!m || !f || !frame_mp || !mps || !trk || (nq && !queries)) return fail(ORBX_ERR_ARG, "null argument");
     const bool bFactor = th != 1.0;  // ORBmatcher.cc:66
     std::vector<ProjQuery> qs;
@@ -387,6 +453,7 @@ int orbx_search_by_projection_local(orbx_matcher* m, const orbx_frame_view* f, i
 int orbx_search_by_projection_frame(orbx_matcher* m, const orbx_frame_view* cur, int32_t* cur_mp,
                                     const orbx_frame_view* last, const int32_t* last_mp, const uint8_t* last_outlier,
                                     const orbx_mappoints* mps, float th, int mono, int* nmatches) {
+    const CallClock clock_(m);
     if (!m || !cur || !cur_mp || !last || !last_mp || !mps || !mps->pos) return fail(ORBX_ERR_ARG, "null argument");
     float twc[3], tlc[3];
     centre(cur->Tcw, twc);       // twc = -Rcw^T tcw (cc:1637)
@@ -449,6 +516,7 @@ int orbx_search_by_projection_keyframe(orbx_matcher* m, const orbx_frame_view* c
                                        const orbx_frame_view* kf, const int32_t* kf_mp,
                                        const uint8_t* already_found, const orbx_mappoints* mps, float th,
                                        int orb_dist, int* nmatches) {
+    const CallClock clock_(m);
     if (!m || !cur || !cur_mp || !kf || !kf_mp || !mps || !mps->pos || !mps->max_distance || !mps->min_distance)
         return fail(ORBX_ERR_ARG, "null argument");
     if (cur->nlevels < 2) return fail(ORBX_ERR_ARG, "need >= 2 pyramid levels");
@@ -503,6 +571,7 @@ int orbx_search_by_projection_keyframe(orbx_matcher* m, const orbx_frame_view* c
 int orbx_search_by_projection_sim3(orbx_matcher* m, const orbx_frame_view* kf, const float* Scw,
                                    const int32_t* points, int npoints, int32_t* matched,
                                    const orbx_mappoints* mps, int th, int* nmatches) {
+    const CallClock clock_(m);
     if (!m || !kf || !Scw || !matched || !mps || !mps->pos || !mps->max_distance || !mps->min_distance ||
         !mps->normal || (npoints && !points))
         return fail(ORBX_ERR_ARG, "null argument");
@@ -853,6 +922,8 @@ int orbx_matcher_set_timing(orbx_matcher* m, int enable) {
     return ORBX_OK;
 }
 
+double orbx_matcher_last_call_us(const orbx_matcher* m) { return m ? m->last_call_us : -1.0; }
+
 int orbx_matcher_last_ms(orbx_matcher* m, float* ms) {
     if (!m || !ms) return fail(ORBX_ERR_ARG, "null argument");
     if (m->ncalls == 0) return fail(ORBX_ERR_STATE, "no timed call");
@@ -876,6 +947,7 @@ int orbx_search_for_triangulation(orbx_matcher* m, const orbx_frame_view* kf1, c
                                   const orbx_frame_view* kf2, const uint8_t* kf2_has_mp, const int32_t* fv2_node,
                                   const int32_t* fv2_off, const int32_t* fv2_idx, int fv2_n, const float* F12,
                                   int only_stereo, int32_t* pairs, int* npairs) {
+    const CallClock clock_(m);
     if (!m || !kf1 || !kf2 || !kf1_has_mp || !kf2_has_mp || !F12 || !pairs || !npairs)
         return fail(ORBX_ERR_ARG, "null argument");
     // epipole of KF1's centre in KF2 (cc:858-865)
@@ -1218,6 +1290,7 @@ int orbx_search_by_bow_frame(orbx_matcher* m, const orbx_frame_view* kf, const i
                              const int32_t* kf_fv_node, const int32_t* kf_fv_off, const int32_t* kf_fv_idx,
                              int kf_fv_n, const orbx_frame_view* f, const int32_t* f_fv_node, const int32_t* f_fv_off,
                              const int32_t* f_fv_idx, int f_fv_n, int32_t* matches, int* nmatches) {
+    const CallClock clock_(m);
     if (!m || !kf || !f || !kf_mp || !matches || !nmatches || (kf_fv_n && (!kf_fv_node || !kf_fv_off || !kf_fv_idx)) ||
         (f_fv_n && (!f_fv_node || !f_fv_off || !f_fv_idx)) || kf_fv_n < 0 || f_fv_n < 0)
         return fail(ORBX_ERR_ARG, "null argument");
@@ -1231,6 +1304,7 @@ int orbx_search_by_bow_keyframes(orbx_matcher* m, const orbx_frame_view* kf1, co
                                  const orbx_frame_view* kf2, const int32_t* mp2, const int32_t* fv2_node,
                                  const int32_t* fv2_off, const int32_t* fv2_idx, int fv2_n, int32_t* matches12,
                                  int* nmatches) {
+    const CallClock clock_(m);
     if (!m || !kf1 || !kf2 || !mp1 || !mp2 || !matches12 || !nmatches || (fv1_n && (!fv1_node || !fv1_off || !fv1_idx)) ||
         (fv2_n && (!fv2_node || !fv2_off || !fv2_idx)) || fv1_n < 0 || fv2_n < 0)
         return fail(ORBX_ERR_ARG, "null argument");
@@ -1241,6 +1315,7 @@ int orbx_search_by_bow_keyframes(orbx_matcher* m, const orbx_frame_view* kf1, co
 // ORBmatcher::SearchForInitialization, ORBmatcher.cc:539-683
 int orbx_search_for_initialization(orbx_matcher* m, const orbx_frame_view* f1, const orbx_frame_view* f2,
                                    float* prev_matched, int32_t* matches12, int window_size, int* nmatches) {
+    const CallClock clock_(m);
     if (!m || !f1 || !f2 || !prev_matched || !matches12 || !nmatches) return fail(ORBX_ERR_ARG, "null argument");
     const int n1 = f1->n, n2 = f2->n;
     if (n1 >= (1 << 20) || n2 >= (1 << 20)) return fail(ORBX_ERR_UNSUPPORTED, "more than 2^20 keypoints");
@@ -1456,6 +1531,7 @@ bool mps_ok(const orbx_mappoints* mps, bool need_normal) {
 // ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, th), ORBmatcher.cc:1067-1221
 int orbx_fuse(orbx_matcher* m, const orbx_frame_view* kf, const int32_t* points, int npoints, const uint8_t* skip,
               const orbx_mappoints* mps, float th, int32_t* best) {
+    const CallClock clock_(m);
     if (!m || !kf || !skip || !best || !mps_ok(mps, true) || npoints < 0 || (npoints && !points))
         return fail(ORBX_ERR_ARG, "null argument");
     if (kf->nlevels < 2) return fail(ORBX_ERR_ARG, "need >= 2 pyramid levels");
@@ -1495,6 +1571,7 @@ int orbx_fuse(orbx_matcher* m, const orbx_frame_view* kf, const int32_t* points,
 // vector<MapPoint*>& vpReplacePoint), ORBmatcher.cc:1226-1352
 int orbx_fuse_sim3(orbx_matcher* m, const orbx_frame_view* kf, const float* Scw, const int32_t* points, int npoints,
                    const uint8_t* skip, const orbx_mappoints* mps, float th, int32_t* best) {
+    const CallClock clock_(m);
     if (!m || !kf || !Scw || !skip || !best || !mps_ok(mps, true) || npoints < 0 || (npoints && !points))
         return fail(ORBX_ERR_ARG, "null argument");
     if (kf->nlevels < 2) return fail(ORBX_ERR_ARG, "need >= 2 pyramid levels");
@@ -1584,6 +1661,7 @@ int orbx_search_by_sim3(orbx_matcher* m, const orbx_frame_view* kf1, const int32
                         const orbx_frame_view* kf2, const int32_t* mp2, const uint8_t* already2,
                         const orbx_mappoints* mps, float s12, const float* R12, const float* t12, float th,
                         int32_t* matches12, int* nfound) {
+    const CallClock clock_(m);
     if (!m || !kf1 || !kf2 || !mp1 || !mp2 || !R12 || !t12 || !matches12 || !nfound || !mps_ok(mps, false))
         return fail(ORBX_ERR_ARG, "null argument");
     if (kf1->nlevels < 2 || kf2->nlevels < 2) return fail(ORBX_ERR_ARG, "need >= 2 pyramid levels");
@@ -1691,6 +1769,7 @@ int orbx_compute_stereo_matches(orbx_matcher* m, orbx_extractor* ex_left, int le
                                 int right_frame, const orbx_frame_view* left, const orbx_keypoint* keys_r,
                                 const uint8_t* desc_r, int n_right, float max_disparity, float* u_right,
                                 float* depth) {
+    const CallClock clock_(m);
     if (!m || !ex_left || !ex_right || !left || !u_right || !depth || (n_right && (!keys_r || !desc_r)) ||
         n_right < 0 || left->n < 0)
         return fail(ORBX_ERR_ARG, "null argument");

@@ -196,6 +196,11 @@ class ORBmatcher:
             self._destroy(self._h)
             self._h = None
 
+    def last_call_us(self) -> float:
+        """Wall time (us) of this matcher's newest host call inside liborbx (no binding
+        overhead): what a C++ caller pays per call."""
+        return float(L.lib().orbx_matcher_last_call_us(self._h))
+
     @staticmethod
     def DescriptorDistance(a: np.ndarray, b: np.ndarray) -> int:
         """ORBmatcher::DescriptorDistance (ORBmatcher.cc:1983-2003)."""

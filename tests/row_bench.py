@@ -55,12 +55,26 @@ def rows(O, reps: int):
     cpu_reps = max(3, reps // 4)
     out = []
 
-    def add(row, ref, size, gpu_fn, cpu_fn):
+    def add(row, ref, size, gpu_fn, cpu_fn, lib=None):
+        """lib: the ORBmatcher the GPU call runs on -- its in-library wall time per call
+        (orbx_matcher_last_call_us: what a C++ caller pays, without the ctypes binding) is
+        reported beside the Python-side time."""
         gpu_fn()  # warm-up (device init, first allocation)
-        g_ms, g = _time(gpu_fn, reps)
+        lib_us = []
+
+        def g_fn():
+            r = gpu_fn()
+            if lib is not None:
+                lib_us.append(lib.last_call_us())
+            return r
+        g_ms, g = _time(g_fn, reps)
         c_ms, c = _time(cpu_fn, cpu_reps)
-        out.append({"row": row, "reference": ref, "size": size, "gpu_ms": round(g_ms, 4), "cpu_ms": round(c_ms, 4),
-                    "speedup": round(c_ms / g_ms, 2) if g_ms > 0 else None, "bit_exact": bool(_eq(g, c))})
+        rec = {"row": row, "reference": ref, "size": size, "gpu_ms": round(g_ms, 4), "cpu_ms": round(c_ms, 4),
+               "speedup": round(c_ms / g_ms, 2) if g_ms > 0 else None, "bit_exact": bool(_eq(g, c))}
+        if lib_us:
+            lib_ms = statistics.median(lib_us) / 1e3
+            rec.update({"lib_ms": round(lib_ms, 4), "speedup_lib": round(c_ms / lib_ms, 2) if lib_ms > 0 else None})
+        out.append(rec)
 
     # a1-a8 ORBextractor::operator(): one frame per call (host image in, keypoints and
     # descriptors out), the BASELINE configs C1, C3 (KITTI), C5 (5000 features, 12 levels)
@@ -100,7 +114,7 @@ def rows(O, reps: int):
         f = f0.copy()
         return O.sbp_local(B, f, queries, mps, trk, 3.0, 0.8), f
     add("a11", "ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, float) ORBmatcher.cc:61-173",
-        size, a11_g, a11_c)
+        size, a11_g, a11_c, lib=m)
 
     # a12 SearchByProjection(Frame& cur, const Frame& last, th, bMono) -- TrackWithMotionModel
     last_mp = np.arange(nA, dtype=np.int32)
@@ -115,7 +129,7 @@ def rows(O, reps: int):
         c = cur0.copy()
         return O.sbp_frame(B, c, A, last_mp, mps, 15.0, True, True), c
     add("a12", "ORBmatcher::SearchByProjection(Frame&, const Frame&, float, bool) ORBmatcher.cc:1620-1789",
-        size, a12_g, a12_c)
+        size, a12_g, a12_c, lib=m12)
 
     # a13 SearchByProjection(Frame&, KeyFrame*, set<MapPoint*>, th, ORBdist) -- relocalisation
     mpsd = S.with_depth_info(S.mappoints_from(A, 1), A, 1)
@@ -129,7 +143,7 @@ def rows(O, reps: int):
         c = cur0.copy()
         return O.sbp_keyframe(B, c, A, kf_mp, mpsd, 10.0, 100, True), c
     add("a13", "ORBmatcher::SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, float, int) "
-        "ORBmatcher.cc:1792-1924", size, a13_g, a13_c)
+        "ORBmatcher.cc:1792-1924", size, a13_g, a13_c, lib=m12)
 
     # a14 SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th) -- loop closing
     Scw = np.asarray(B.Tcw, np.float32)[:3, :4].copy()
@@ -144,7 +158,7 @@ def rows(O, reps: int):
         c = cur0.copy()
         return O.sbp_sim3(B, Scw, points, c, mpsd, 10), c
     add("a14", "ORBmatcher::SearchByProjection(KeyFrame*, cv::Mat, const vector<MapPoint*>&, "
-        "vector<MapPoint*>&, int) ORBmatcher.cc:398-520", size, a14_g, a14_c)
+        "vector<MapPoint*>&, int) ORBmatcher.cc:398-520", size, a14_g, a14_c, lib=m14)
 
     # a15 SearchForTriangulation -- LocalMapping::CreateNewMapPoints
     has1 = (rng.random(nA) < 0.2).astype(np.uint8)
@@ -154,7 +168,7 @@ def rows(O, reps: int):
     m15 = ORBmatcher(0.6, False)
     add("a15", "ORBmatcher::SearchForTriangulation ORBmatcher.cc:850-1056", size,
         lambda: m15.SearchForTriangulation(A, has1, fv1, B, has2, fv2, F12, False),
-        lambda: O.search_for_triangulation(A, has1, fv1, B, has2, fv2, F12, False, False))
+        lambda: O.search_for_triangulation(A, has1, fv1, B, has2, fv2, F12, False, False), lib=m15)
 
     # a18 Frame::ComputeStereoMatches, 640x480 and KITTI 1241x376
     for W, H, nf in ((640, 480, 1000), (1241, 376, 2000)):
@@ -171,7 +185,7 @@ def rows(O, reps: int):
         ms = ORBmatcher(0.6, True)
         add("a18", "Frame::ComputeStereoMatches Frame.cc:673-885", f"{len(kl)} x {len(kr)} keypoints, {W}x{H}",
             lambda: ms.ComputeStereoMatches(ex, 0, ex, 1, view, kr, dr, maxD=fx),
-            lambda: O.compute_stereo_matches(view, kr, dr, pl, pr, fx))
+            lambda: O.compute_stereo_matches(view, kr, dr, pl, pr, fx), lib=ms)
 
     # f2 SearchByBoW (KF -> F, KF -> KF), SearchForInitialization
     mpb = np.arange(1000, 1000 + nA, dtype=np.int32)
@@ -181,11 +195,11 @@ def rows(O, reps: int):
     mb = ORBmatcher(0.7, True)
     add("f2", "ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) ORBmatcher.cc:228-392", size,
         lambda: mb.SearchByBoWFrame(A, mpb, fv1, B, fv2),
-        lambda: O.search_by_bow_frame(A, mpb, fv1, B, fv2, 0.7, True))
+        lambda: O.search_by_bow_frame(A, mpb, fv1, B, fv2, 0.7, True), lib=mb)
     mk = ORBmatcher(0.75, True)
     add("f2", "ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&) ORBmatcher.cc:696-839", size,
         lambda: mk.SearchByBoWKeyFrames(A, mpb, fv1, B, mpb2, fv2),
-        lambda: O.search_by_bow_keyframes(A, mpb, fv1, B, mpb2, fv2, 0.75, True))
+        lambda: O.search_by_bow_keyframes(A, mpb, fv1, B, mpb2, fv2, 0.75, True), lib=mk)
     prev0 = np.ascontiguousarray(np.stack([A.keys["x"], A.keys["y"]], 1).astype(np.float32))
     mi = ORBmatcher(0.9, True)
 
@@ -196,7 +210,7 @@ def rows(O, reps: int):
 
     def init_c():
         return O.search_for_initialization(A, B, prev0.copy(), 100, 0.9, True)
-    add("f2", "ORBmatcher::SearchForInitialization ORBmatcher.cc:539-683", size, init_g, init_c)
+    add("f2", "ORBmatcher::SearchForInitialization ORBmatcher.cc:539-683", size, init_g, init_c, lib=mi)
 
     # f3 UndistortKeyPoints + ComputeImageBounds + AssignFeaturesToGrid (TUM1 calibration)
     K = [517.306408, 516.469215, 318.643040, 255.313989]
@@ -226,9 +240,10 @@ def rows(O, reps: int):
     skip = (rng.random(nA) < 0.1).astype(np.uint8)
     mf = ORBmatcher(0.6, True)
     add("f4", "ORBmatcher::Fuse(KeyFrame*, const vector<MapPoint*>&, float) ORBmatcher.cc:1067-1221", size,
-        lambda: mf.Fuse(B, fpoints, skip, mpf, 3.0), lambda: O.fuse(B, fpoints, skip, mpf, 3.0))
+        lambda: mf.Fuse(B, fpoints, skip, mpf, 3.0), lambda: O.fuse(B, fpoints, skip, mpf, 3.0), lib=mf)
     add("f4", "ORBmatcher::Fuse(KeyFrame*, cv::Mat Scw, ..., vector<MapPoint*>&) ORBmatcher.cc:1226-1352", size,
-        lambda: mf.FuseSim3(B, Scw, fpoints, skip, mpf, 4.0), lambda: O.fuse_sim3(B, Scw, fpoints, skip, mpf, 4.0))
+        lambda: mf.FuseSim3(B, Scw, fpoints, skip, mpf, 4.0), lambda: O.fuse_sim3(B, Scw, fpoints, skip, mpf, 4.0),
+        lib=mf)
     counts = rng.integers(1, 12, 1000)
     base = rng.integers(0, 256, (len(counts), 32), dtype=np.uint8)
     descs = []
