@@ -72,11 +72,14 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
 
 // k_seq_grid + k_seq_score + k_seq_commit: the split form of launch_proj_search for the
 // batched sequence matcher (grids: nprob x seq_grid_bytes(cap) bytes of device memory).
-// cap: keypoints per problem (the grids); qcap: queries per problem (0: cap)
+// cap: keypoints per problem (the grids); qcap: queries per problem (0: cap).  stage_*
+// (one problem only): k_stage_copy first copies stage_bytes (a multiple of 16) from
+// device-visible pinned host memory to stage_dst -- the call's inputs, d_probs among them
 size_t seq_grid_bytes(int cap, int noct);
 hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned char* grids,
                             int cap, unsigned long long* scratch, const long long* d_scratch_off, hipStream_t stream,
-                            int qcap = 0, int replay_rt = 0);
+                            int qcap = 0, int replay_rt = 0, const void* stage_src = nullptr,
+                            void* stage_dst = nullptr, size_t stage_bytes = 0);
 
 hipError_t launch_seq_build(const SeqArgs& A, int npairs, ProjQuery* queries, ProjProblem* probs,
                             long long* scratch_off, hipStream_t stream);

@@ -7,6 +7,7 @@
 // the query's candidate list and a wave reduction keeps the best and second-best
 // (distance, list position) keys, which reproduces the reference's sequential
 // `dist < bestDist` / `else if (dist < bestDist2)` updates exactly.
+#include <climits>
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -1372,10 +1373,35 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
 
 constexpr int kSeqGridThreads = 256;
 
+// A single host call's inputs, copied from device-visible pinned host memory into the
+// device arena by the GPU itself (many workgroups of coalesced 16-byte loads over PCIe)
+// rather than by a DMA copy: the copy engine's setup latency is most of a small copy's
+// cost, and one workgroup alone reads host memory at only ~7 GB/s (21 us for 150 KB).
+constexpr int kStageThreads = 256, kStageUnroll = 4;
+__global__ __launch_bounds__(kStageThreads) void k_stage_copy(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                              int n16) {
+    const int b0 = blockIdx.x * kStageThreads * kStageUnroll + (int)threadIdx.x;
+    uint4 v[kStageUnroll];
+#pragma unroll
+    for (int u = 0; u < kStageUnroll; u++) {
+        const int i = b0 + u * kStageThreads;
+        if (i < n16) v[u] = src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kStageUnroll; u++) {
+        const int i = b0 + u * kStageThreads;
+        if (i < n16) dst[i] = v[u];
+    }
+}
+
 template <int kSeqGridThreads>  // (shadows the batch default of the same name)
-__global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem* __restrict__ probs,
-                                                              unsigned char* __restrict__ grids, int cap, int noct) {
+__global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem* probs, unsigned char* grids,
+                                                              int cap, int noct, unsigned long long* stamps) {
     extern __shared__ __align__(16) unsigned char smem[];
+    // diagnostics (one problem): words 0, 1, 2, 4, 10, 11 of its stamp row
+    unsigned long long* st = stamps && threadIdx.x == 0 ? stamps + kStampWords * blockIdx.x : nullptr;
+    if (st) st[0] = wall_clock64();
+    if (st) st[1] = wall_clock64();
     const ProjProblem pb = probs[blockIdx.x];
     const SeqGridLayout gl(cap, noct);
     unsigned char* gb = grids + (size_t)blockIdx.x * gl.total;
@@ -1385,6 +1411,7 @@ __global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem*
     uint16_t* colstart = (uint16_t*)(smem + align16((size_t)cap * 4));
     unsigned* cnt = (unsigned*)(smem + align16(align16((size_t)cap * 4) + (size_t)(kGridCols + 1) * 2));
     grid_sort<kSeqGridThreads>(pb, skey, cnt);
+    if (st) st[2] = wall_clock64();
     unsigned* gkey = (unsigned*)(gb + gl.skey);
     float2* sxy = (float2*)(gb + gl.sxy);
     float* sang = (float*)(gb + gl.sang);
@@ -1403,10 +1430,13 @@ __global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem*
         const int i = sk_idx(skey[t >> 1]);
         sdesc[t] = ((const uint4*)(pb.desc + (size_t)i * 32))[t & 1];
     }
+    if (st) st[4] = wall_clock64();
     build_colstart<kSeqGridThreads>(skey, n, colstart);
     __syncthreads();
+    if (st) st[10] = wall_clock64();
     build_octave_runs<kSeqGridThreads>(skey, colstart, noct, (uint16_t*)(gb + gl.bstart), (uint16_t*)(gb + gl.orun),
                                        cnt);
+    if (st) st[11] = wall_clock64();
 }
 
 constexpr int kSeqScoreThreads = 256;  // 16 queries (4 per wave, one 16-lane row each)
@@ -1535,8 +1565,11 @@ static hipError_t launch_seq_commit(int rt, const ProjProblem* d_probs, int npro
 
 hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned char* grids,
                             int cap, unsigned long long* scratch, const long long* d_scratch_off, hipStream_t stream,
-                            int qcap, int replay_rt) {
+                            int qcap, int replay_rt, const void* stage_src, void* stage_dst, size_t stage_bytes) {
     if (nprob <= 0) return hipSuccess;
+    if (stage_bytes && (nprob != 1 || !stage_src || !stage_dst || stage_bytes % 16 || stage_bytes / 16 > INT_MAX))
+        return hipErrorInvalidValue;
+    const int n16 = (int)(stage_bytes / 16);
     if (cap <= 0 || cap >= 8192) return hipErrorInvalidValue;  // 13-bit keypoint positions
     if (qcap <= 0) qcap = cap;
     if (P.noct < 1 || P.noct > 32) return hipErrorInvalidValue;
@@ -1550,11 +1583,20 @@ hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjPar
         hipError_t e = hipFuncSetAttribute(gfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_grid);
         if (e != hipSuccess) return e;
     }
+    const uint4* ssrc = (const uint4*)stage_src;
+    uint4* sdst = (uint4*)stage_dst;
+    if (n16 > 0) {
+        const int blocks = (n16 + kStageThreads * kStageUnroll - 1) / (kStageThreads * kStageUnroll);
+        hipLaunchKernelGGL(k_stage_copy, dim3(blocks), dim3(kStageThreads), 0, stream, ssrc, sdst, n16);
+        const hipError_t ce = hipGetLastError();
+        if (ce != hipSuccess) return ce;
+    }
     if (wide)
-        hipLaunchKernelGGL(k_seq_grid<1024>, dim3(nprob), dim3(1024), lds_grid, stream, d_probs, grids, cap, P.noct);
+        hipLaunchKernelGGL(k_seq_grid<1024>, dim3(nprob), dim3(1024), lds_grid, stream, d_probs, grids, cap, P.noct,
+                           P.stamps);
     else
         hipLaunchKernelGGL(k_seq_grid<kSeqGridThreads>, dim3(nprob), dim3(kSeqGridThreads), lds_grid, stream, d_probs,
-                           grids, cap, P.noct);
+                           grids, cap, P.noct, P.stamps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int qblocks = (qcap + kSeqScoreQ - 1) / kSeqScoreQ;

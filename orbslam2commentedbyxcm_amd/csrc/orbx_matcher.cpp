@@ -47,18 +47,27 @@ constexpr int TH_LOW = 50;    // ORBmatcher.cc:39
 struct Arena {
     char* base = nullptr;
     char* host = nullptr;  // pinned mirror: a call's inputs are staged here and uploaded in one copy
+    char* host_dev = nullptr;  // the mirror's device address (mapped): a kernel can copy it in itself
     size_t cap = 0, used = 0, dirty = 0;
     hipError_t reserve(size_t bytes) {
         dirty = 0;
         if (bytes <= cap) return hipSuccess;
         if (base) (void)hipFree(base);
         if (host) (void)hipHostFree(host);
-        base = host = nullptr;
+        base = host = host_dev = nullptr;
         cap = 0;
+        bytes = (bytes + 15) & ~(size_t)15;
         hipError_t e = hipMalloc((void**)&base, bytes);
-        if (e == hipSuccess) e = hipHostMalloc((void**)&host, bytes, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipHostMalloc((void**)&host, bytes, hipHostMallocMapped);
+        if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&host_dev, host, 0);
         if (e == hipSuccess) cap = bytes;
         return e;
+    }
+    // the staged prefix for an in-kernel copy (instead of flush()): bytes, rounded to 16
+    size_t take_staged() {
+        const size_t b = (dirty + 15) & ~(size_t)15;
+        dirty = 0;
+        return b;
     }
     template <typename T>
     T* take(size_t n) {
@@ -105,7 +114,7 @@ struct Arena {
     void release() {
         if (base) (void)hipFree(base);
         if (host) (void)hipHostFree(host);
-        base = host = nullptr;
+        base = host = host_dev = nullptr;
         cap = used = dirty = 0;
     }
 };
@@ -276,9 +285,10 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
     auto* d_qd = m->arena.take<uint8_t>((size_t)nq * 32);
     auto* d_obs = m->arena.take<int32_t>(nobs ? nobs : 1);
     auto* d_prob = m->arena.take<ProjProblem>(1);
-    auto* d_scr = m->arena.take<unsigned long long>(kProjScratchWords * (size_t)nq);
     auto* d_off = m->arena.take<long long>(1);
     auto* d_nm = m->arena.take<int32_t>(1);
+    // device-only areas last: the staged (uploaded) prefix ends before them
+    auto* d_scr = m->arena.take<unsigned long long>(kProjScratchWords * (size_t)nq);
     auto* d_grid = m->arena.take<unsigned char>(seq_grid_bytes(gcap, noct));
     hipStream_t s = m->stream;
     m->arena.up(d_keys, f->keys, sizeof(orbx_keypoint) * n);
@@ -335,11 +345,15 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
         pb.nmatches = m->hmp_dev;
         m->arena.up(d_prob, &pb, sizeof(pb));
     }
-    HIP_TRY(m->arena.flush(s));
-    if (mapped)
-        HIP_TRY(launch_seq_split(d_prob, 1, P, d_grid, gcap, d_scr, d_off, s));
-    else
+    if (mapped) {
+        // inputs copied in by k_stage_copy (no DMA), results written to mapped memory
+        const size_t staged = m->arena.take_staged();
+        HIP_TRY(launch_seq_split(d_prob, 1, P, d_grid, gcap, d_scr, d_off, s, 0, 0, m->arena.host_dev, m->arena.base,
+                                 staged));
+    } else {
+        HIP_TRY(m->arena.flush(s));
         HIP_TRY(launch_proj_search(d_prob, 1, P, d_scr, d_off, n, nq, s));
+    }
     int nm = 0;
     if (!mapped) {
         HIP_TRY(m->arena.down(frame_mp, d_fmp, sizeof(int32_t) * n, s));
@@ -357,9 +371,11 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
         HIP_TRY(hipMemcpy(h, d_st, sizeof(h), hipMemcpyDeviceToHost));
         HIP_TRY(hipFree(d_st));
         auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-        fprintf(stderr, "[orbx call] n=%d nq=%d | host staging %.1f us, enqueue %.1f us, wait %.1f us | replay %.1f us, "
-                "%llu iterations, %llu re-scored\n", n, nq, us(t_stage0, t_flush), us(t_flush, t_enq), us(t_enq, t_done),
-                (double)(h[3] - h[13]) * 0.01, h[7], h[5]);
+        fprintf(stderr, "[orbx call] n=%d nq=%d | host staging %.1f us, enqueue %.1f us, wait %.1f us | grid: start %.1f, "
+                "sort %.1f, writes %.1f, colstart %.1f, runs %.1f us | replay %.1f us, %llu iterations, %llu re-scored\n",
+                n, nq, us(t_stage0, t_flush), us(t_flush, t_enq), us(t_enq, t_done), (double)(h[1] - h[0]) * 0.01,
+                (double)(h[2] - h[1]) * 0.01, (double)(h[4] - h[2]) * 0.01, (double)(h[10] - h[4]) * 0.01,
+                (double)(h[11] - h[10]) * 0.01, (double)(h[3] - h[13]) * 0.01, h[7], h[5]);
     }
     if (nmatches) *nmatches = nm;
     return ORBX_OK;
