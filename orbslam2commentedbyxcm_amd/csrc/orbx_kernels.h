@@ -76,6 +76,10 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
 // (one problem only): k_stage_copy first copies stage_bytes (a multiple of 16) from
 // device-visible pinned host memory to stage_dst -- the call's inputs, d_probs among them
 size_t seq_grid_bytes(int cap, int noct);
+// k_stage_copy: bytes (a multiple of 16, 16-byte aligned ends) between device memory and
+// device-visible (mapped) pinned host memory, by the GPU's own loads and stores (many
+// workgroups) instead of a DMA copy -- for the small per-call copies of the host calls
+hipError_t launch_stage_copy(const void* src, void* dst, size_t bytes, hipStream_t stream);
 hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjParams& P, unsigned char* grids,
                             int cap, unsigned long long* scratch, const long long* d_scratch_off, hipStream_t stream,
                             int qcap = 0, int replay_rt = 0, const void* stage_src = nullptr,

@@ -1373,6 +1373,8 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
 
 constexpr int kSeqGridThreads = 256;
 
+hipError_t launch_stage_copy(const void* src, void* dst, size_t bytes, hipStream_t stream);
+
 // A single host call's inputs, copied from device-visible pinned host memory into the
 // device arena by the GPU itself (many workgroups of coalesced 16-byte loads over PCIe)
 // rather than by a DMA copy: the copy engine's setup latency is most of a small copy's
@@ -1525,6 +1527,15 @@ __global__ __launch_bounds__(RT) void k_seq_commit(const ProjProblem* __restrict
 
 size_t seq_grid_bytes(int cap, int noct) { return SeqGridLayout(cap, noct).total; }
 
+hipError_t launch_stage_copy(const void* src, void* dst, size_t bytes, hipStream_t stream) {
+    if (!bytes) return hipSuccess;
+    if (bytes % 16 || ((uintptr_t)src | (uintptr_t)dst) % 16 || bytes / 16 > INT_MAX) return hipErrorInvalidValue;
+    const int n16 = (int)(bytes / 16);
+    const int blocks = (n16 + kStageThreads * kStageUnroll - 1) / (kStageThreads * kStageUnroll);
+    hipLaunchKernelGGL(k_stage_copy, dim3(blocks), dim3(kStageThreads), 0, stream, (const uint4*)src, (uint4*)dst, n16);
+    return hipGetLastError();
+}
+
 // k_seq_commit's dynamic LDS: the replay's lists, then the claims and the owner map
 static size_t seq_commit_lds(int cap, int rt) { return (size_t)kTopK * rt * 4 + (size_t)cap * 8; }
 
@@ -1586,9 +1597,7 @@ hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjPar
     const uint4* ssrc = (const uint4*)stage_src;
     uint4* sdst = (uint4*)stage_dst;
     if (n16 > 0) {
-        const int blocks = (n16 + kStageThreads * kStageUnroll - 1) / (kStageThreads * kStageUnroll);
-        hipLaunchKernelGGL(k_stage_copy, dim3(blocks), dim3(kStageThreads), 0, stream, ssrc, sdst, n16);
-        const hipError_t ce = hipGetLastError();
+        const hipError_t ce = launch_stage_copy(ssrc, sdst, (size_t)n16 * 16, stream);
         if (ce != hipSuccess) return ce;
     }
     if (wide)

@@ -89,20 +89,23 @@ struct Arena {
         std::memset(host + o, v, bytes);
         if (o + bytes > dirty) dirty = o + bytes;
     }
-    // one H2D copy of everything staged since the last flush (the prefix [0, dirty))
+    // one upload of everything staged since the last flush (the prefix [0, dirty)): a copy
+    // kernel reading the mapped mirror (a DMA copy's setup latency is most of a small
+    // copy's cost; the GPU's own loads over PCIe are not)
     hipError_t flush(hipStream_t s) {
         if (!dirty) return hipSuccess;
-        const hipError_t e = hipMemcpyAsync(base, host, dirty, hipMemcpyHostToDevice, s);
+        const hipError_t e = launch_stage_copy(host_dev, base, (dirty + 15) & ~(size_t)15, s);
         dirty = 0;
         return e;
     }
-    // D2H of `bytes` at device address d into the pinned mirror; sync() copies it to h
+    // `bytes` at device address d (inside the arena) into the pinned mirror by a copy
+    // kernel writing the mapped mirror; sync() copies it to h
     struct Pending { void* h; size_t o, bytes; };
     std::vector<Pending> pending;
     hipError_t down(void* h, const void* d, size_t bytes, hipStream_t s) {
         const size_t o = (size_t)((const char*)d - base);
         pending.push_back({h, o, bytes});
-        return hipMemcpyAsync(host + o, d, bytes, hipMemcpyDeviceToHost, s);
+        return launch_stage_copy(d, host_dev + o, (bytes + 15) & ~(size_t)15, s);
     }
     hipError_t sync(hipStream_t s) {
         const hipError_t e = hipStreamSynchronize(s);

@@ -1,7 +1,7 @@
 # Drop-in host calls after the in-kernel staging: parity, call phases, the row bench.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_match.py tests/test_gpu_posed.py tests/test_gpu_fuse.py \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_match.py tests/test_gpu_posed.py tests/test_gpu_fuse.py tests/test_cpp_mirror.py tests/test_abi.py \
     tests/test_gpu_bow.py tests/test_gpu_frame.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r3p_pytest.log 2>&1
 rc=$?; tail -2 gpurun_out/r3p_pytest.log
 if [ $rc -ne 0 ]; then exit $rc; fi
