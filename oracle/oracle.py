@@ -706,3 +706,65 @@ class Vocab:
                               fi.ctypes.data_as(I32P), C.byref(nf))
         nb, nf = nb.value, nf.value
         return bw[:nb].copy(), bv[:nb].copy(), fn[:nf].copy(), fo[:nf + 1].copy(), fi[:fo[nf]].copy()
+
+    def transform_features(self, desc: np.ndarray, levelsup: int = 4):
+        """Per-feature tree walk: -> (word, weight, node) arrays (TemplatedVocabulary.h:1220-1259)."""
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(d)
+        w = np.zeros(max(n, 1), np.int32)
+        wt = np.zeros(max(n, 1), np.float64)
+        nd = np.zeros(max(n, 1), np.int32)
+        L = lib()
+        L.ora_vocab_transform_features.argtypes = [C.POINTER(OraVocab), U8P, C.c_int, C.c_int, I32P,
+                                                   C.POINTER(C.c_double), I32P]
+        L.ora_vocab_transform_features(C.byref(self.v), d.ctypes.data_as(U8P), n, int(levelsup),
+                                       w.ctypes.data_as(I32P), wt.ctypes.data_as(C.POINTER(C.c_double)),
+                                       nd.ctypes.data_as(I32P))
+        return w[:n].copy(), wt[:n].copy(), nd[:n].copy()
+
+
+# ---- oracle/_ref: the reference's own DBoW2 BowVector / FeatureVector (oracle/ref_dbow2.mk)
+REF_ROOT = "/root/reference"
+
+
+def ref_dbow2():
+    """The reference-built DBoW2 containers (oracle/_ref/libdbow2_ref.so, built from
+    /root/reference's sources by oracle/ref_dbow2.mk when the reference is present), or
+    None when neither the library nor the reference sources are available."""
+    import os
+    import subprocess
+    here = Path(__file__).resolve().parent
+    so = here / "_ref" / "libdbow2_ref.so"
+    if os.path.isdir(REF_ROOT + "/Thirdparty/DBoW2/DBoW2"):
+        subprocess.run(["make", "-s", "-f", str(here / "ref_dbow2.mk"), f"REF={REF_ROOT}"], check=True)
+    if not so.exists():
+        return None
+    L = C.CDLL(str(so))
+    U32P = C.POINTER(C.c_uint32)
+    L.dbow2_ref_frame.argtypes = [C.c_int, U32P, C.POINTER(C.c_double), U32P, C.c_int, C.c_int, U32P,
+                                  C.POINTER(C.c_double), U32P, I32P, U32P, C.POINTER(C.c_int)]
+    return L
+
+
+def ref_frame(L, word, weight, node, weighting: int, scoring: int):
+    """TemplatedVocabulary::transform's frame-level steps on the reference's BowVector /
+    FeatureVector: -> (bow_word, bow_value, fv_node, fv_off, fv_idx) like Vocab.transform."""
+    n = len(word)
+    w = np.ascontiguousarray(word, np.uint32)
+    wt = np.ascontiguousarray(weight, np.float64)
+    nd = np.ascontiguousarray(node, np.uint32)
+    cap = max(n, 1)
+    bw = np.zeros(cap, np.uint32)
+    bv = np.zeros(cap, np.float64)
+    fn = np.zeros(cap, np.uint32)
+    fo = np.zeros(cap + 1, np.int32)
+    fi = np.zeros(cap, np.uint32)
+    nf = C.c_int()
+    U32P = C.POINTER(C.c_uint32)
+    DP = C.POINTER(C.c_double)
+    nb = L.dbow2_ref_frame(n, w.ctypes.data_as(U32P), wt.ctypes.data_as(DP), nd.ctypes.data_as(U32P), int(weighting),
+                           int(scoring), bw.ctypes.data_as(U32P), bv.ctypes.data_as(DP), fn.ctypes.data_as(U32P),
+                           fo.ctypes.data_as(I32P), fi.ctypes.data_as(U32P), C.byref(nf))
+    nf = nf.value
+    return (bw[:nb].astype(np.int32), bv[:nb].copy(), fn[:nf].astype(np.int32), fo[:nf + 1].copy(),
+            fi[:fo[nf]].astype(np.int32))

@@ -134,6 +134,19 @@ static void transform_one(const ora_vocab* v, const uint8_t* f, int levelsup, in
     *weight = v->weight[final_id];
 }
 
+int ora_vocab_transform_features(const ora_vocab* v, const uint8_t* desc, int n, int levelsup, int32_t* word,
+                                 double* weight, int32_t* node) {
+    for (int i = 0; i < n; i++) {
+        int w, nid;
+        double wt;
+        transform_one(v, desc + (size_t)i * 32, levelsup, &w, &wt, &nid);
+        word[i] = w;
+        weight[i] = wt;
+        node[i] = nid;
+    }
+    return 0;
+}
+
 typedef struct {
     int key;  /* word or node id */
     int idx;  /* feature index */
@@ -197,7 +210,11 @@ int ora_vocab_transform(const ora_vocab* v, const uint8_t* desc, int n, int leve
     if (must) {
         double norm = 0.0;
         if (v->scoring == 1) {
-            for (int j = 0; j < nb; j++) norm += bow_value[j] * bow_value[j];
+            /* fused, as the reference builds it: g++ contracts C++ even under -std=c++11
+             * (contraction is off by default only for ISO C), and BowVector.cpp compiled
+             * with DBoW2's -O3 -march=native holds one vfmadd, in this loop
+             * (tests/test_vocab_ref.py runs that build) */
+            for (int j = 0; j < nb; j++) norm = fma(bow_value[j], bow_value[j], norm);
             norm = sqrt(norm);
         } else {
             for (int j = 0; j < nb; j++) norm += fabs(bow_value[j]);

@@ -37,6 +37,12 @@ void ora_vocab_free(ora_vocab* v);
 int ora_vocab_transform(const ora_vocab* v, const uint8_t* desc, int n, int levelsup, int32_t* bow_word,
                         double* bow_value, int* nbow, int32_t* fv_node, int32_t* fv_off, int32_t* fv_idx, int* nfv);
 
+/* transform(feature, word_id, weight, nid, levelsup) for each of n descriptors
+ * (TemplatedVocabulary.h:1220-1259): the per-feature tree walk the frame transform
+ * aggregates.  Returns 0. */
+int ora_vocab_transform_features(const ora_vocab* v, const uint8_t* desc, int n, int levelsup, int32_t* word,
+                                 double* weight, int32_t* node);
+
 #ifdef __cplusplus
 }
 #endif

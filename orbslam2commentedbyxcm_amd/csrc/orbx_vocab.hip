@@ -230,7 +230,9 @@ __global__ __launch_bounds__(kFrameThreads) void k_vocab_frame(const int32_t* __
         if (norm_kind == 1) {
             for (int p = 0; p < nb; p++) s = __dadd_rn(s, fabs(s_val[p]));
         } else if (norm_kind == 2) {
-            for (int p = 0; p < nb; p++) s = __dadd_rn(s, __dmul_rn(s_val[p], s_val[p]));
+            // fused like the reference's build (g++ -O3 -march=native contracts C++:
+            // BowVector::normalize's L2 loop is one vfmadd; tests/test_vocab_ref.py)
+            for (int p = 0; p < nb; p++) s = __fma_rn(s_val[p], s_val[p], s);
             s = sqrt(s);
         } else {
             s = accumulate ? (double)nb : 0.0;  // TF / TF_IDF without normalisation: / size()

@@ -4,6 +4,7 @@ cross-check the C oracle on small cases."""
 from __future__ import annotations
 
 import math
+from fractions import Fraction
 
 import numpy as np
 
@@ -158,9 +159,11 @@ def py_transform(tree: Tree, desc: np.ndarray, levelsup: int):
     must = tree.scoring != 5
     if must:
         if tree.scoring == 1:
+            # fused multiply-add (the reference's build contracts norm += v*v): the exact
+            # v*v + s, rounded once
             s = 0.0
             for w in words:
-                s += bow[w] * bow[w]
+                s = float(Fraction(bow[w]) * Fraction(bow[w]) + Fraction(s))
             s = math.sqrt(s)
         else:
             s = 0.0
