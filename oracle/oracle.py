@@ -114,6 +114,8 @@ def _load(path) -> C.CDLL:
     L.ora_set_trig_mode.restype = None
     L.ora_set_octree_tie_mode.argtypes = [C.c_int]
     L.ora_set_octree_tie_mode.restype = None
+    L.ora_set_contract_mode.argtypes = [C.c_int]
+    L.ora_set_contract_mode.restype = None
     L.ora_octree_ties.argtypes = [C.c_int]
     L.ora_octree_ties.restype = C.c_long
     return L
@@ -141,11 +143,13 @@ def level_sizes(p: Params, width: int, height: int):
 
 
 def extract(img: np.ndarray, p: Params | None = None, cap: int = 1 << 16, trig_mode: int = 0,
-            tie_mode: int = 0):
+            tie_mode: int = 0, contract_mode: int = 1):
     """ORBextractor::operator() on one u8 image -> (keypoints[n], descriptors[n,32], level_counts).
     trig_mode 1: rBRIEF rotation by glibc cosf / sinf (the reference's literal arithmetic,
     hazard H3) instead of the shipped correctly rounded values.  tie_mode 1: the octree's
-    final phase breaks size ties the other way (earlier-created node first, hazard H1)."""
+    final phase breaks size ties the other way (earlier-created node first, hazard H1).
+    contract_mode 0: the rBRIEF sample offsets unfused (the shipped form, 1, fuses them as
+    g++ -O3 -march=native builds the reference, hazard H4)."""
     p = p or params()
     img = np.ascontiguousarray(img, dtype=np.uint8)
     kps = np.zeros(cap, dtype=KEYPOINT_DTYPE)
@@ -156,6 +160,8 @@ def extract(img: np.ndarray, p: Params | None = None, cap: int = 1 << 16, trig_m
         L.ora_set_trig_mode(int(trig_mode))  # thread-local: this thread's next calls only
     if tie_mode:
         L.ora_set_octree_tie_mode(int(tie_mode))
+    if contract_mode != 1:
+        L.ora_set_contract_mode(int(contract_mode))
     try:
         n = L.ora_extract(C.byref(p), _u8(img), img.shape[1], img.shape[0], img.strides[0],
                           kps.ctypes.data, _u8(desc), cap, counts)
@@ -164,6 +170,8 @@ def extract(img: np.ndarray, p: Params | None = None, cap: int = 1 << 16, trig_m
             L.ora_set_trig_mode(0)
         if tie_mode:
             L.ora_set_octree_tie_mode(0)
+        if contract_mode != 1:
+            L.ora_set_contract_mode(1)
     if n < 0:
         raise RuntimeError("oracle capacity exceeded")
     return kps[:n].copy(), desc[:n].copy(), np.array(counts[:p.nlevels], dtype=np.int32)

@@ -423,6 +423,27 @@ void ora_cos_sin(float angle_deg, float* c, float* s) {
     *s = (float)sin((double)r);
 }
 
+/* Hazard H4 at descriptor level.  The reference is built by g++ -O3 -march=native
+ * (CMakeLists.txt:10-19), and g++ contracts a*b + c*d into fma(a, b, c*d) in C++ even
+ * under -std=c++11 (GCC keeps contraction off by default only for ISO C): the
+ * reference's own BowVector.cpp built with DBoW2's flags holds a vfmadd
+ * (tests/test_vocab_ref.py).  The sample offsets x*b + y*a and x*a - y*b
+ * (ORBextractor.cc:136-138) are such expressions, and GCC's FMA pass fuses the first
+ * product into the add: fma(x, b, y*a), fma(x, a, -(y*b)).  That is the shipped form
+ * (here and in k_describe).  ora_set_contract_mode(0) switches the calling thread to the
+ * unfused form, so the effect can be counted (tests/h4_contract_count.py: 3 of 257,543
+ * descriptors at configs[1]). */
+static _Thread_local int g_contract_mode = 1;
+
+void ora_set_contract_mode(int mode) { g_contract_mode = mode; }
+
+static inline float brief_u(float x, float y, float a, float b) {
+    return g_contract_mode ? fmaf(x, b, y * a) : x * b + y * a;
+}
+static inline float brief_v(float x, float y, float a, float b) {
+    return g_contract_mode ? fmaf(x, a, -(y * b)) : x * a - y * b;
+}
+
 /* computeOrbDescriptor, ORBextractor.cc:118-172 (pattern: cc:176-434) */
 void ora_orb_descriptor(const uint8_t* img, size_t stride, float x, float y, float angle_deg,
                         uint8_t* desc) {
@@ -437,8 +458,8 @@ void ora_orb_descriptor(const uint8_t* img, size_t stride, float x, float y, flo
             const int* p0 = pattern + 4 * j;       /* point 2j   : (x, y) */
             const int* p1 = pattern + 4 * j + 2;   /* point 2j+1 */
             float x0 = (float)p0[0], y0 = (float)p0[1], x1 = (float)p1[0], y1 = (float)p1[1];
-            int t0 = center[ora_cv_roundf(x0 * b + y0 * a) * step + ora_cv_roundf(x0 * a - y0 * b)];
-            int t1 = center[ora_cv_roundf(x1 * b + y1 * a) * step + ora_cv_roundf(x1 * a - y1 * b)];
+            int t0 = center[ora_cv_roundf(brief_u(x0, y0, a, b)) * step + ora_cv_roundf(brief_v(x0, y0, a, b))];
+            int t1 = center[ora_cv_roundf(brief_u(x1, y1, a, b)) * step + ora_cv_roundf(brief_v(x1, y1, a, b))];
             val |= (t0 < t1) << j;
         }
         desc[i] = (uint8_t)val;

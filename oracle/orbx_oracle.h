@@ -65,6 +65,7 @@ float ora_ic_angle(const uint8_t* img, size_t stride, float x, float y, const in
 void ora_cos_sin(float angle_deg, float* c, float* s);
 /* 0: (float)cos((double)r) (default); 1: cosf / sinf as ORBextractor.cc:123-125 (calling thread) */
 void ora_set_trig_mode(int mode);
+void ora_set_contract_mode(int mode); /* H4: 1 fused rBRIEF sample offsets (shipped), 0 unfused */
 void ora_set_octree_tie_mode(int mode);
 long ora_octree_ties(int reset);
 void ora_orb_descriptor(const uint8_t* img, size_t stride, float x, float y, float angle_deg,

@@ -26,6 +26,21 @@ enum { TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30 };
 /* ---------------------------------------------------------------- grid */
 
 /* Frame::PosInGrid, Frame.cc:558-567 */
+/* Hazard H4 in the matchers.  g++ -O3 -march=native (the reference's flags) contracts
+ * the projection and epipolar expressions -- GCC fuses the first product of a sum into an
+ * FMA -- and so does this restatement (and liborbx): u =
+ * fma(fx*xc, invzc, cx), ur = fma(-mbf, invzc, u), CheckDistEpipolarLine's
+ * fma(x, F00, y*F10) + F20, fma(a, x2, b*y2) + c, fma(a, a, b*b), the epipole test's
+ * fma(dx, dx, dy*dy), Fuse's chi-square fma(er, er, fma(ex, ex, ey*ey)).
+ * ora_set_match_contract_mode(0) switches the process to the unfused forms so the effect
+ * can be counted (tests/h4_match_contract_count.py). */
+static int g_mcontract = 1;  /* process-wide: cleared only by the exposure script */
+void ora_set_match_contract_mode(int mode) { g_mcontract = mode; }
+/* a*b + c */
+static inline float mad_(float a, float b, float c) { return g_mcontract ? fmaf(a, b, c) : a * b + c; }
+/* c - a*b */
+static inline float msub_(float c, float a, float b) { return g_mcontract ? fmaf(-a, b, c) : c - a * b; }
+
 static int pos_in_grid(const ora_frame* f, float inv_w, float inv_h, const ora_keypoint* kp, int* px, int* py) {
     *px = (int)roundf((kp->x - f->min_x) * inv_w);
     *py = (int)roundf((kp->y - f->min_y) * inv_h);
@@ -255,8 +270,8 @@ int ora_sbp_frame(const ora_frame* cur, int32_t* cur_mp, const ora_frame* last, 
         const float xc = x3Dc[0], yc = x3Dc[1];
         const float invzc = (float)(1.0 / x3Dc[2]);
         if (invzc < 0) continue;
-        const float u = cur->fx * xc * invzc + cur->cx;
-        const float v = cur->fy * yc * invzc + cur->cy;
+        const float u = mad_(cur->fx * xc, invzc, cur->cx);
+        const float v = mad_(cur->fy * yc, invzc, cur->cy);
         if (u < cur->min_x || u > cur->max_x) continue;
         if (v < cur->min_y || v > cur->max_y) continue;
         const int nLastOctave = last->keys[i].octave;
@@ -276,7 +291,7 @@ int ora_sbp_frame(const ora_frame* cur, int32_t* cur_mp, const ora_frame* last, 
             if (cur_mp[i2] >= 0)
                 if (mps->observations[cur_mp[i2]] > 0) continue;
             if (cur->u_right && cur->u_right[i2] > 0) {
-                const float ur = u - cur->bf * invzc;
+                const float ur = msub_(u, cur->bf, invzc);
                 const float er = fabsf(ur - cur->u_right[i2]);
                 if (er > radius) continue;
             }
@@ -353,8 +368,8 @@ void ora_is_in_frustum(const ora_frame* f, const ora_mappoints* mps, const int32
         project(T, P, Pc);
         if (Pc[2] < 0.0f) continue;
         const float invz = 1.0f / Pc[2];
-        const float u = f->fx * Pc[0] * invz + f->cx;
-        const float v = f->fy * Pc[1] * invz + f->cy;
+        const float u = mad_(f->fx * Pc[0], invz, f->cx);
+        const float v = mad_(f->fy * Pc[1], invz, f->cy);
         if (u < f->min_x || u > f->max_x) continue;
         if (v < f->min_y || v > f->max_y) continue;
         const float maxDistance = 1.2f * mps->max_distance[mp];
@@ -370,7 +385,7 @@ void ora_is_in_frustum(const ora_frame* f, const ora_mappoints* mps, const int32
         if (viewCos < viewingCosLimit) continue;
         in_view[mp] = 1;
         proj_x[mp] = u;
-        proj_xr[mp] = u - f->bf * invz;
+        proj_xr[mp] = msub_(u, f->bf, invz);
         proj_y[mp] = v;
         scale_level[mp] = predict_scale(mps->max_distance[mp], dist, f);
         view_cos[mp] = viewCos;
@@ -445,8 +460,8 @@ int ora_sbp_keyframe(const ora_frame* cur, int32_t* cur_mp, const ora_frame* kf,
         project(cur->Tcw, x3Dw, x3Dc);
         const float xc = x3Dc[0], yc = x3Dc[1];
         const float invzc = (float)(1.0 / x3Dc[2]);
-        const float u = cur->fx * xc * invzc + cur->cx;
-        const float v = cur->fy * yc * invzc + cur->cy;
+        const float u = mad_(cur->fx * xc, invzc, cur->cx);
+        const float v = mad_(cur->fy * yc, invzc, cur->cy);
         if (u < cur->min_x || u > cur->max_x) continue;
         if (v < cur->min_y || v > cur->max_y) continue;
         float PO[3];
@@ -531,8 +546,8 @@ int ora_sbp_sim3(const ora_frame* kf, const float* Scw, const int32_t* points, i
         const float invz = 1 / p3Dc[2];
         const float x = p3Dc[0] * invz;
         const float y = p3Dc[1] * invz;
-        const float u = kf->fx * x + kf->cx;
-        const float v = kf->fy * y + kf->cy;
+        const float u = mad_(kf->fx, x, kf->cx);
+        const float v = mad_(kf->fy, y, kf->cy);
         if (!(u >= kf->min_x && u < kf->max_x && v >= kf->min_y && v < kf->max_y)) continue;  /* IsInImage */
         const float maxDistance = 1.2f * mps->max_distance[mp];
         const float minDistance = 0.8f * mps->min_distance[mp];
@@ -577,11 +592,11 @@ int ora_sbp_sim3(const ora_frame* kf, const float* Scw, const int32_t* points, i
 /* ORBmatcher::CheckDistEpipolarLine, ORBmatcher.cc:186-213 */
 static int check_dist_epipolar_line(const ora_keypoint* kp1, const ora_keypoint* kp2, const float* F12,
                                     const float* sigma2) {
-    const float a = kp1->x * F12[0] + kp1->y * F12[3] + F12[6];
-    const float b = kp1->x * F12[1] + kp1->y * F12[4] + F12[7];
-    const float c = kp1->x * F12[2] + kp1->y * F12[5] + F12[8];
-    const float num = a * kp2->x + b * kp2->y + c;
-    const float den = a * a + b * b;
+    const float a = mad_(kp1->x, F12[0], kp1->y * F12[3]) + F12[6];
+    const float b = mad_(kp1->x, F12[1], kp1->y * F12[4]) + F12[7];
+    const float c = mad_(kp1->x, F12[2], kp1->y * F12[5]) + F12[8];
+    const float num = mad_(a, kp2->x, b * kp2->y) + c;
+    const float den = mad_(a, a, b * b);
     if (den == 0) return 0;
     const float dsqr = num * num / den;
     return dsqr < 3.84 * sigma2[kp2->octave];
@@ -603,8 +618,8 @@ int ora_search_for_triangulation(const ora_frame* kf1, const uint8_t* kf1_has_mp
     float C2[3];
     project(kf2->Tcw, Cw, C2);
     const float invz = 1.0f / C2[2];
-    const float ex = kf2->fx * C2[0] * invz + kf2->cx;
-    const float ey = kf2->fy * C2[1] * invz + kf2->cy;
+    const float ex = mad_(kf2->fx * C2[0], invz, kf2->cx);
+    const float ey = mad_(kf2->fy * C2[1], invz, kf2->cy);
 
     uint8_t* vbMatched2 = (uint8_t*)calloc((size_t)kf2->n + 1, 1);
     int32_t* vMatches12 = (int32_t*)malloc(sizeof(int32_t) * (size_t)(kf1->n + 1));
@@ -634,7 +649,7 @@ int ora_search_for_triangulation(const ora_frame* kf1, const uint8_t* kf1_has_mp
                     if (!bStereo1 && !bStereo2) {
                         const float distex = ex - kp2->x;
                         const float distey = ey - kp2->y;
-                        if (distex * distex + distey * distey < 100 * kf2->scale_factors[kp2->octave]) continue;
+                        if (mad_(distex, distex, distey * distey) < 100 * kf2->scale_factors[kp2->octave]) continue;
                     }
                     if (check_dist_epipolar_line(kp1, kp2, F12, kf2->level_sigma2)) {
                         bestIdx2 = idx2;
@@ -1096,11 +1111,11 @@ static int window_best(const ora_frame* kf, const ora_grid* g, int* cand, const 
         if (gate) {
             if (kf->u_right && kf->u_right[idx] >= 0) { /* cc:1137-1150 */
                 const float ex = u - kp->x, ey = v - kp->y, er = ur - kf->u_right[idx];
-                const float e2 = ex * ex + ey * ey + er * er;
+                const float e2 = mad_(er, er, mad_(ex, ex, ey * ey));
                 if ((double)(e2 * inv_sigma2[kpLevel]) > 7.8) continue;
             } else {
                 const float ex = u - kp->x, ey = v - kp->y;
-                const float e2 = ex * ex + ey * ey;
+                const float e2 = mad_(ex, ex, ey * ey);
                 if ((double)(e2 * inv_sigma2[kpLevel]) > 5.99) continue;
             }
         }
@@ -1136,9 +1151,9 @@ void ora_fuse(const ora_frame* kf, const int32_t* points, int npoints, const uin
         if (p3Dc[2] < 0.0f) continue;
         const float invz = 1 / p3Dc[2];
         const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
-        const float u = kf->fx * x + kf->cx, v = kf->fy * y + kf->cy;
+        const float u = mad_(kf->fx, x, kf->cx), v = mad_(kf->fy, y, kf->cy);
         if (!(u >= kf->min_x && u < kf->max_x && v >= kf->min_y && v < kf->max_y)) continue;
-        const float ur = u - kf->bf * invz;
+        const float ur = msub_(u, kf->bf, invz);
         const float maxDistance = 1.2f * mps->max_distance[mp], minDistance = 0.8f * mps->min_distance[mp];
         float PO[3];
         for (int c = 0; c < 3; c++) PO[c] = p3Dw[c] - Ow[c];
@@ -1182,7 +1197,7 @@ void ora_fuse_sim3(const ora_frame* kf, const float* Scw, const int32_t* points,
         if (p3Dc[2] < 0.0f) continue;
         const float invz = (float)(1.0 / p3Dc[2]);
         const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
-        const float u = kf->fx * x + kf->cx, v = kf->fy * y + kf->cy;
+        const float u = mad_(kf->fx, x, kf->cx), v = mad_(kf->fy, y, kf->cy);
         if (!(u >= kf->min_x && u < kf->max_x && v >= kf->min_y && v < kf->max_y)) continue;
         const float maxDistance = 1.2f * mps->max_distance[mp], minDistance = 0.8f * mps->min_distance[mp];
         float PO[3];
@@ -1220,7 +1235,7 @@ static void sim3_direction(const ora_frame* src, const int32_t* src_mp, const ui
         if (pd[2] < 0.0) continue;
         const float invz = (float)(1.0 / pd[2]);
         const float x = pd[0] * invz, y = pd[1] * invz;
-        const float u = dst->fx * x + dst->cx, v = dst->fy * y + dst->cy;
+        const float u = mad_(dst->fx, x, dst->cx), v = mad_(dst->fy, y, dst->cy);
         if (!(u >= dst->min_x && u < dst->max_x && v >= dst->min_y && v < dst->max_y)) continue;
         const float maxDistance = 1.2f * mps->max_distance[mp], minDistance = 0.8f * mps->min_distance[mp];
         const float dist3D = norm3(pd);

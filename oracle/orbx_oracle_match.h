@@ -102,6 +102,9 @@ void ora_compute_stereo_matches(const ora_frame* left, const ora_keypoint* keys_
                                 const uint8_t* const* levels_l, const uint8_t* const* levels_r, const int* level_w,
                                 const int* level_h, const float* inv_scale, float maxD, float* u_right, float* depth);
 
+/* H4: 1 (default) = the reference build's fused projection / epipolar forms, 0 = unfused */
+void ora_set_match_contract_mode(int mode);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1577,9 +1577,11 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     // the patch centre once.
     const uint32_t center = (uint32_t)(18 * 48 + 18 + (x - 18 - xb)) - (0x400000u * 48u + 0x4B400000u);
     const float kRound = 12582912.0f;  // 1.5 * 2^23
+    // the offsets fused as g++ -O3 -march=native builds the reference (hazard H4: GCC
+    // contracts C++ and fuses the first product, fma(x, b, y*a), fma(x, a, -(y*b)))
     auto sample = [&](float px, float py) -> int {
-        const uint32_t ry = __float_as_uint((px * b + py * a) + kRound);
-        const uint32_t rx = __float_as_uint((px * a - py * b) + kRound);
+        const uint32_t ry = __float_as_uint(fmaf(px, b, py * a) + kRound);
+        const uint32_t rx = __float_as_uint(fmaf(px, a, -(py * b)) + kRound);
         return bp[center + __umul24(ry, 48u) + rx];
     };
     const int* pat = (const int*)c_pattern + hl;

@@ -76,11 +76,12 @@ __global__ __launch_bounds__(256) void k_window_best(const BestProblem* __restri
                     if (pb.u_right && pb.u_right[idx] >= 0) {
                         const float ex = __fsub_rn(Q.u, kp.x), ey = __fsub_rn(Q.v, kp.y),
                                     er = __fsub_rn(Q.ur, pb.u_right[idx]);
-                        e2 = __fadd_rn(__fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey)), __fmul_rn(er, er));
+                        // fused like the reference's build (H4): fma(er, er, fma(ex, ex, ey*ey))
+                        e2 = __fmaf_rn(er, er, __fmaf_rn(ex, ex, __fmul_rn(ey, ey)));
                         if ((double)__fmul_rn(e2, pb.inv_sigma2[lv]) > 7.8) continue;
                     } else {
                         const float ex = __fsub_rn(Q.u, kp.x), ey = __fsub_rn(Q.v, kp.y);
-                        e2 = __fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey));
+                        e2 = __fmaf_rn(ex, ex, __fmul_rn(ey, ey));
                         if ((double)__fmul_rn(e2, pb.inv_sigma2[lv]) > 5.99) continue;
                     }
                 }

@@ -1682,13 +1682,14 @@ __global__ __launch_bounds__(256) void k_seq_build(SeqArgs A, ProjQuery* __restr
         for (int r = 0; r < 3; r++)
             x3Dc[r] = Tc[4 * r] * Xw[0] + Tc[4 * r + 1] * Xw[1] + Tc[4 * r + 2] * Xw[2] + Tc[4 * r + 3];
         const float invzc = (float)(1.0 / (double)x3Dc[2]);
-        const float u = A.fx * x3Dc[0] * invzc + A.cx;
-        const float v = A.fy * x3Dc[1] * invzc + A.cy;
+        // fused as g++ -O3 -march=native builds the reference (H4)
+        const float u = fmaf(A.fx * x3Dc[0], invzc, A.cx);
+        const float v = fmaf(A.fy * x3Dc[1], invzc, A.cy);
         if (!(invzc < 0) && !(u < A.min_x || u > A.max_x) && !(v < A.min_y || v > A.max_y)) {
             const int o = kp.octave;
             q.u = u;
             q.v = v;
-            q.ur = u - A.bf * invzc;
+            q.ur = fmaf(-A.bf, invzc, u);
             q.r = A.th * A.scale[o];
             q.er_max = q.r;
             if (bForward) {  // GetFeaturesInArea(u, v, radius, nLastOctave)
@@ -1784,9 +1785,9 @@ __global__ __launch_bounds__(kLocalThreads) void k_local_build(LocalArgs A, Proj
             in_view = !(Pc[2] < 0.0f);
             if (in_view) {
                 const float invz = 1.0f / Pc[2];
-                u = A.fx * Pc[0] * invz + A.cx;
-                v = A.fy * Pc[1] * invz + A.cy;
-                ur = u - A.bf * invz;
+                u = fmaf(A.fx * Pc[0], invz, A.cx);  // fused like the reference's build (H4)
+                v = fmaf(A.fy * Pc[1], invz, A.cy);
+                ur = fmaf(-A.bf, invz, u);
                 in_view = !(u < A.min_x || u > A.max_x) && !(v < A.min_y || v > A.max_y);
             }
             if (in_view) {
@@ -1936,9 +1937,11 @@ __device__ void score_tri(const TriProblem& pb, const TriQuery& Q, const uint8_t
     const unsigned long long q0 = d1[0], q1 = d1[1], q2 = d1[2], q3 = d1[3];
     // epipolar line of kp1 in KF2 (CheckDistEpipolarLine, ORBmatcher.cc:186-213)
     const float* F = pb.F12;
-    const float a = kp1.x * F[0] + kp1.y * F[3] + F[6];
-    const float b = kp1.x * F[1] + kp1.y * F[4] + F[7];
-    const float c = kp1.x * F[2] + kp1.y * F[5] + F[8];
+    // fused as g++ -O3 -march=native builds the reference: the first product of each
+    // sum goes into an FMA (H4)
+    const float a = fmaf(kp1.x, F[0], kp1.y * F[3]) + F[6];
+    const float b = fmaf(kp1.x, F[1], kp1.y * F[4]) + F[7];
+    const float c = fmaf(kp1.x, F[2], kp1.y * F[5]) + F[8];
     for (int p = Q.beg + lane; p < Q.end; p += 64) {
         const int idx2 = pb.fv2_idx[p];
         if (matched2[idx2] || pb.has_mp2[idx2]) continue;
@@ -1951,10 +1954,10 @@ __device__ void score_tri(const TriProblem& pb, const TriQuery& Q, const uint8_t
         if (!Q.stereo1 && !stereo2) {
             const float distex = pb.ex - kp2.x;
             const float distey = pb.ey - kp2.y;
-            if (distex * distex + distey * distey < 100 * pb.scale2[kp2.octave]) continue;
+            if (fmaf(distex, distex, distey * distey) < 100 * pb.scale2[kp2.octave]) continue;
         }
-        const float num = a * kp2.x + b * kp2.y + c;
-        const float den = a * a + b * b;
+        const float num = fmaf(a, kp2.x, b * kp2.y) + c;
+        const float den = fmaf(a, a, b * b);
         if (den == 0) continue;
         const float dsqr = num * num / den;
         if (!((double)dsqr < 3.84 * (double)pb.sigma2_2[kp2.octave])) continue;

@@ -491,8 +491,9 @@ int orbx_search_by_projection_frame(orbx_matcher* m, const orbx_frame_view* cur,
         const float xc = x3Dc[0], yc = x3Dc[1];
         const float invzc = (float)(1.0 / x3Dc[2]);
         if (invzc < 0) continue;
-        const float u = cur->fx * xc * invzc + cur->cx;
-        const float v = cur->fy * yc * invzc + cur->cy;
+        // fused as g++ -O3 -march=native builds the reference (H4)
+        const float u = std::fma(cur->fx * xc, invzc, cur->cx);
+        const float v = std::fma(cur->fy * yc, invzc, cur->cy);
         if (u < cur->min_x || u > cur->max_x) continue;
         if (v < cur->min_y || v > cur->max_y) continue;
         const int nLastOctave = last->keys[i].octave;
@@ -500,7 +501,7 @@ int orbx_search_by_projection_frame(orbx_matcher* m, const orbx_frame_view* cur,
         ProjQuery q{};
         q.u = u;
         q.v = v;
-        q.ur = u - cur->bf * invzc;
+        q.ur = std::fma(-cur->bf, invzc, u);
         q.r = radius;
         q.er_max = radius;
         if (bForward) {
@@ -553,8 +554,8 @@ int orbx_search_by_projection_keyframe(orbx_matcher* m, const orbx_frame_view* c
         float x3Dc[3];
         project(cur->Tcw, x3Dw, x3Dc);
         const float invzc = (float)(1.0 / x3Dc[2]);
-        const float u = cur->fx * x3Dc[0] * invzc + cur->cx;
-        const float v = cur->fy * x3Dc[1] * invzc + cur->cy;
+        const float u = std::fma(cur->fx * x3Dc[0], invzc, cur->cx);  // fused (H4)
+        const float v = std::fma(cur->fy * x3Dc[1], invzc, cur->cy);
         if (u < cur->min_x || u > cur->max_x) continue;
         if (v < cur->min_y || v > cur->max_y) continue;
         float PO[3];
@@ -619,8 +620,8 @@ int orbx_search_by_projection_sim3(orbx_matcher* m, const orbx_frame_view* kf, c
         project(T, p3Dw, p3Dc);
         if (p3Dc[2] < 0.0) continue;
         const float invz = 1 / p3Dc[2];
-        const float u = kf->fx * (p3Dc[0] * invz) + kf->cx;
-        const float v = kf->fy * (p3Dc[1] * invz) + kf->cy;
+        const float u = std::fma(kf->fx, p3Dc[0] * invz, kf->cx);  // fused (H4)
+        const float v = std::fma(kf->fy, p3Dc[1] * invz, kf->cy);
         if (!(u >= kf->min_x && u < kf->max_x && v >= kf->min_y && v < kf->max_y)) continue;  // IsInImage
         float PO[3];
         for (int c = 0; c < 3; c++) PO[c] = p3Dw[c] - Ow[c];
@@ -974,8 +975,8 @@ int orbx_search_for_triangulation(orbx_matcher* m, const orbx_frame_view* kf1, c
     centre(kf1->Tcw, Cw);
     project(kf2->Tcw, Cw, C2);
     const float invz = 1.0f / C2[2];
-    const float ex = kf2->fx * C2[0] * invz + kf2->cx;
-    const float ey = kf2->fy * C2[1] * invz + kf2->cy;
+    const float ex = std::fma(kf2->fx * C2[0], invz, kf2->cx);  // fused (H4)
+    const float ey = std::fma(kf2->fy * C2[1], invz, kf2->cy);
     // queries in the reference's visiting order: shared nodes ascending (cc:886-1019)
     std::vector<TriQuery> qs;
     int f1 = 0, f2 = 0;
@@ -1112,8 +1113,8 @@ int orbx_search_for_triangulation_batch_device(orbx_matcher* m, int nkf, const o
         centre(kfs[a].Tcw, Cw);
         project(kfs[b].Tcw, Cw, C2);
         const float invz = 1.0f / C2[2];
-        t.ex = cam->fx * C2[0] * invz + cam->cx;
-        t.ey = cam->fy * C2[1] * invz + cam->cy;
+        t.ex = std::fma(cam->fx * C2[0], invz, cam->cx);  // fused (H4)
+        t.ey = std::fma(cam->fy * C2[1], invz, cam->cy);
     }
     HIP_TRY(hipSetDevice(m->device));
     hipStream_t s = stream ? (hipStream_t)stream : m->stream;
@@ -1570,9 +1571,9 @@ int orbx_fuse(orbx_matcher* m, const orbx_frame_view* kf, const int32_t* points,
         if (p3Dc[2] < 0.0f) continue;
         const float invz = 1 / p3Dc[2];
         const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
-        const float u = kf->fx * x + kf->cx, v = kf->fy * y + kf->cy;
+        const float u = std::fma(kf->fx, x, kf->cx), v = std::fma(kf->fy, y, kf->cy);  // fused (H4)
         if (!in_image(kf, u, v)) continue;
-        const float ur = u - kf->bf * invz;
+        const float ur = std::fma(-kf->bf, invz, u);
         BestQuery q;
         if (!fuse_query(kf, mps, mp, Ow, u, v, ur, th, q)) continue;
         qs.push_back(q);
@@ -1615,7 +1616,7 @@ int orbx_fuse_sim3(orbx_matcher* m, const orbx_frame_view* kf, const float* Scw,
         if (p3Dc[2] < 0.0f) continue;
         const float invz = (float)(1.0 / p3Dc[2]);
         const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
-        const float u = kf->fx * x + kf->cx, v = kf->fy * y + kf->cy;
+        const float u = std::fma(kf->fx, x, kf->cx), v = std::fma(kf->fy, y, kf->cy);  // fused (H4)
         if (!in_image(kf, u, v)) continue;
         BestQuery q;
         if (!fuse_query(kf, mps, mp, Ow, u, v, 0.f, th, q)) continue;
@@ -1652,7 +1653,7 @@ int sim3_direction(orbx_matcher* m, const orbx_frame_view* src, const int32_t* s
         if (pd[2] < 0.0) continue;
         const float invz = (float)(1.0 / pd[2]);
         const float x = pd[0] * invz, y = pd[1] * invz;
-        const float u = dst->fx * x + dst->cx, v = dst->fy * y + dst->cy;
+        const float u = std::fma(dst->fx, x, dst->cx), v = std::fma(dst->fy, y, dst->cy);  // fused (H4)
         if (!in_image(dst, u, v)) continue;
         const float dist3D = norm3(pd);
         if (dist3D < 0.8f * mps->min_distance[mp] || dist3D > 1.2f * mps->max_distance[mp]) continue;

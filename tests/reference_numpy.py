@@ -204,13 +204,18 @@ def ic_angle(img: np.ndarray, x: int, y: int, umax) -> float:
 
 
 def orb_descriptor(blurred: np.ndarray, x: int, y: int, angle: float, pattern: np.ndarray) -> np.ndarray:
-    """computeOrbDescriptor (cc:118-172) with cos/sin rounded from double."""
+    """computeOrbDescriptor (cc:118-172) with cos/sin rounded from double and the sample
+    offsets fused (hazard H4)."""
     r = F32(angle) * F32(np.pi / 180.0)
     a, b = F32(np.cos(np.float64(r))), F32(np.sin(np.float64(r)))
     pts = pattern.reshape(512, 2).astype(np.float32)
     px, py = pts[:, 0], pts[:, 1]
-    ry = np.rint((px * b + py * a).astype(np.float32)).astype(np.int64)
-    rx = np.rint((px * a - py * b).astype(np.float32)).astype(np.int64)
+    # fused as g++ -O3 -march=native builds the reference (H4): fma(x, b, y*a) and
+    # fma(x, a, -(y*b)).  x*b is exact in double (|x| <= 15), y*a is rounded to float
+    # first, their double sum is exact, so one rounding to float32 is the fma's.
+    f64 = np.float64
+    ry = np.rint((px.astype(f64) * f64(b) + (py * a).astype(f64)).astype(np.float32)).astype(np.int64)
+    rx = np.rint((px.astype(f64) * f64(a) - (py * b).astype(f64)).astype(np.float32)).astype(np.int64)
     vals = blurred[y + ry, x + rx].astype(np.int64)
     bits = (vals[0::2] < vals[1::2]).astype(np.uint8)  # pair p -> bit p
     return np.packbits(bits, bitorder="little")
