@@ -352,6 +352,8 @@ def main():
     ap.add_argument("--lanes", type=int, default=2,
                     help="split the batch into this many contiguous chunks, each on its own extractor stream, so "
                          "one chunk's latency-bound kernels overlap another's")
+    ap.add_argument("--no-host-fed", action="store_true",
+                    help="skip the host-fed leg (frames uploaded from pinned host memory every step)")
     ap.add_argument("--no-local-map", action="store_true",
                     help="skip the second measurement of the step with TrackLocalMap's SearchLocalPoints")
     ap.add_argument("--selftest-launch", action="store_true", help=argparse.SUPPRESS)
@@ -474,6 +476,56 @@ def main():
                                             cy=CY, W=W, H=H, depth=DEPTH, th=TH))
         parity["bit_exact"] = parity["bit_exact"] and parity["octree_status_clean"]
 
+    # The same step fed from host memory: every step's 256 frames are uploaded from pinned
+    # host memory (double-buffered, on a copy stream beside the previous step's work) and
+    # the extraction lanes wait for their upload -- the PCIe-inclusive rate a caller whose
+    # frames arrive in host memory would see.  Not `value`.
+    host_fed = None
+    if match and not args.no_host_fed:
+        pl.set_timing(False)
+        h_frames = torch.from_numpy(frames_np).pin_memory()
+        d_buf = [torch.empty_like(d_frames) for _ in range(2)]
+        cs = torch.cuda.Stream(device=dev)
+        ev_up = [torch.cuda.Event() for _ in range(2)]
+
+        def hf_step(j):
+            b = pl.it % 2  # the pipeline's buffer of this step (nbuf 2) = the upload buffer
+            with torch.cuda.stream(cs):
+                if j >= 2:  # the extraction two steps back (pipeline buffer b) read d_buf[b]
+                    for c in range(pl.S):
+                        cs.wait_event(pl.ev_ex[b][c])
+                d_buf[b].copy_(h_frames, non_blocking=True)
+                ev_up[b].record(cs)
+            for c in range(pl.S):
+                pl.streams[c].wait_event(ev_up[b])
+            pl.step(d_buf[b], d_T)
+
+        if pl.nbuf_ok():
+            for j in range(max(args.warmup, 1)):
+                hf_step(j)
+            pl.drain(d_T)
+            sync()
+            barrier()
+            sync()
+            t0 = time.perf_counter()
+            for j in range(args.steps):
+                hf_step(j + 2)  # d_buf[b] was read by an extraction two steps back
+            pl.drain(d_T)
+            sync()
+            barrier()
+            sync()
+            el3 = time.perf_counter() - t0
+            if world > 1:
+                t = torch.tensor([el3], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                el3 = float(t.item())
+            host_fed = {"value": round(B * args.steps * world / el3, 2), "unit": "frames/s",
+                        "ms_per_step": round(el3 / args.steps * 1e3, 4),
+                        "upload_bytes_per_step": int(frames_np.nbytes),
+                        "upload_GBps": round(frames_np.nbytes * args.steps / el3 / 1e9, 2),
+                        "note": "frames uploaded from pinned host memory every step (copy stream, double-buffered, "
+                                "overlapped with the previous step's extraction and matching); results stay in HBM"}
+
     # The same step with TrackLocalMap (SearchLocalPoints against the MapPoints of the three
     # previous frames, after TrackWithMotionModel against the previous frame's MapPoints):
     # a second pipeline, timed the same way, checked the same way.
@@ -567,6 +619,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "with_local_map": local,
+            "host_fed": host_fed,
             "mean_keypoints_per_frame": round(mean_kps, 1),
             "mean_matches_per_pair": round(mean_matches, 1),
         }

@@ -222,6 +222,10 @@ class SequencePipeline:
             self._match(b)
             self.last = b
 
+    def nbuf_ok(self) -> bool:
+        """Two pipeline buffers (the layout an external double-buffered feeder pairs with)."""
+        return len(self.kps) == 2
+
     def drain(self, Tcw=None):
         if self.pipelined and self.pending is not None:
             self._match(self.pending)
