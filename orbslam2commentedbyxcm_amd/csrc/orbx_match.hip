@@ -169,15 +169,23 @@ constexpr int kNumCells = kGridCols * kGridRows;
 // levels around the predicted one) and the window radius grows with the octave
 // (th * scale[level]): at 5000 features x 12 levels a top-level window covers ~800
 // keypoints of which ~5 % are in the level range.  So the scan does not walk cells: a
-// grid column's keypoints are also listed bucketed by (octave, block of 8 grid rows)
-// -- orun, u16 entries position | (iy & 7) << 13 -- with bucket starts in bstart,
+// grid column's keypoints are also listed bucketed by (octave, block of kRowBlk grid rows)
+// -- orun, u16 entries position | (iy % kRowBlk) << 13 -- with bucket starts in bstart,
 // [ix][octave][block] (+ one sentinel).  A query visits, per column of its window and
 // per octave of its range, the buckets of the blocks its rows touch, and drops the rows
-// of the two end blocks outside the window (iy & 7 in the entry).  Octaves >= noct share
+// of the two end blocks outside the window (iy % kRowBlk in the entry).  Octaves >= noct share
 // the last bucket (the host sets noct above every keypoint's octave).
-constexpr int kRowBlk = 8;                    // grid rows per bucket block
+#ifndef ORBX_ROWBLK_LOG2
+// 4-row blocks (round 3): the end blocks of a small window carry fewer rows outside it.
+// Scoring alone configs[4] 707 -> 659 us, configs[1] 71.7 -> 66.8 us; 2-row blocks
+// 639 / 66.1 us but a slower sort and no pipelined gain (configs[4] 92.6-94.8k against
+// 95.4-95.8k frames/s for 4 rows, 93.9-95.4k for 8)
+#define ORBX_ROWBLK_LOG2 2
+#endif
+constexpr int kRowBlkLog2 = ORBX_ROWBLK_LOG2;
+constexpr int kRowBlk = 1 << kRowBlkLog2;     // grid rows per bucket block
 constexpr int kNumBlk = kGridRows / kRowBlk;  // 6
-static_assert(kGridRows % kRowBlk == 0, "row blocks tile the grid");
+static_assert(kGridRows % kRowBlk == 0 && kRowBlk <= 8, "row blocks tile the grid; 3 row bits in an orun entry");
 __host__ __device__ constexpr int bucket_table_len(int noct) { return kGridCols * noct * kNumBlk + 1; }
 
 struct SortedGrid {
@@ -195,7 +203,7 @@ __device__ __forceinline__ int sk_oct(unsigned k) { return (int)(k & 31u); }
 __device__ __forceinline__ int bucket_of(unsigned k, int ix, int noct) {
     const int iy = (int)(k >> 18) - ix * kGridRows;
     const int o = sk_oct(k) < noct ? sk_oct(k) : noct - 1;
-    return o * kNumBlk + (iy >> 3);
+    return o * kNumBlk + (iy >> kRowBlkLog2);
 }
 
 // colstart[c] = first sorted position whose grid column is >= c (c = 0..kGridCols;
@@ -247,18 +255,19 @@ __device__ void build_octave_runs(const unsigned* skey, const uint16_t* colstart
         atomicAdd(&cnt[ix * nb + bucket_of(k, ix, noct)], 1u);
     }
     __syncthreads();
-    const int per = (nb + 63) >> 6;  // consecutive buckets per lane, <= 3 (noct <= 32)
+    constexpr int kMaxPer = (32 * kNumBlk + 63) / 64;  // noct <= 32
+    const int per = (nb + 63) >> 6;  // consecutive buckets per lane, <= kMaxPer
     for (int ix = wave; ix < kGridCols; ix += kW) {
-        unsigned v[3], sum = 0;
+        unsigned v[kMaxPer], sum = 0;
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
+        for (int j = 0; j < kMaxPer; j++) {
             const int u = lane * per + j;
             v[j] = (j < per && u < nb) ? cnt[ix * nb + u] : 0u;
             sum += v[j];
         }
         unsigned run = colstart[ix] + wave_inclusive_sum(sum) - sum;
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
+        for (int j = 0; j < kMaxPer; j++) {
             const int u = lane * per + j;
             if (j < per && u < nb) {
                 cnt[ix * nb + u] = run;
@@ -273,7 +282,7 @@ __device__ void build_octave_runs(const unsigned* skey, const uint16_t* colstart
         const unsigned k = skey[p];
         const int ix = (int)(k >> 18) / kGridRows, iy = (int)(k >> 18) - ix * kGridRows;
         const unsigned slot = atomicAdd(&cnt[ix * nb + bucket_of(k, ix, noct)], 1u);
-        orun[slot] = (uint16_t)(p | ((iy & (kRowBlk - 1)) << 13));
+        orun[slot] = (uint16_t)(p | ((iy & (kRowBlk - 1)) << 13));  // 3 bits: kRowBlk <= 8
     }
 }
 
@@ -409,7 +418,8 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
             }
             const int noct = G.noct;
             const int blo = min(olo, noct - 1), bhi = olo > ohi ? -1 : min(ohi, noct - 1);
-            const int b0 = cr.y0 >> 3, b1 = cr.y1 >> 3, ylo = cr.y0 & 7, yhi = cr.y1 & 7;
+            const int b0 = cr.y0 >> kRowBlkLog2, b1 = cr.y1 >> kRowBlkLog2;
+            const int ylo = cr.y0 & (kRowBlk - 1), yhi = cr.y1 & (kRowBlk - 1);
             const int ncol = cr.x1 - cr.x0 + 1;
             // lanes per column: the most (up to 4 in a row, 16 in a wave) that still cover
             // every column in one pass; shifts, no division
