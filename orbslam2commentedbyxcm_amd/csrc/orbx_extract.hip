@@ -24,6 +24,7 @@ namespace orbx {
 const char* const kStageNames[kStages] = {"pyramid", "score_blur", "fast_cells", "octree", "describe", "total"};
 
 __constant__ __align__(16) int8_t c_pattern[1024];
+
 __constant__ int c_umax[16];
 // IC_Angle by rows: for a patch row v and the patch's start alignment d0 = (x-15) & 3,
 // c_icm[d0][|v|] holds 9 dwords of byte masks (1 where |u| <= umax[|v|]) and c_icw the
@@ -1458,114 +1459,162 @@ __device__ float fast_atan2(float y, float x) {
     return a;
 }
 
-// Two kept keypoint slots per wave (one per 32-lane half): IC_Angle on the level
-// (cc:59-106), rBRIEF on the blurred level (cc:118-172), coordinate scaling
-// (cc:1613-1622), output in the reference's level-major order.  Halving the waves halves
-// the per-keypoint cost of everything evaluated once per wave (fastAtan2, the sincos,
-// addressing); a lane's global loads (its IC row, its BRIEF patch rows) are issued
-// together, and the BRIEF gathers then read the LDS-staged patch.
-__global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ pyr,
-                                                  const uint8_t* __restrict__ blur, long long fb,
-                                                  const LevelGeom* __restrict__ lv, int L,
-                                                  const uint32_t* __restrict__ kept, int kept_pf,
-                                                  const int* __restrict__ kept_count,
-                                                  orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
-                                                  int cap, int* __restrict__ n_out, int nframes) {
-    __shared__ __align__(16) uint32_t s_bpatch[8][37 * 12];  // BRIEF patches, 48-byte rows
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int half = lane >> 5, hl = lane & 31;
-    int f, sb;
-    xcd_frame_block((kept_pf + 7) / 8, nframes, f, sb);
-    const int slot0 = sb * 8 + wave * 2;
-    if (slot0 >= kept_pf) return;  // whole wave
-    const int slot = slot0 + half;
-    const int* kc = kept_count + (size_t)f * L;
-    // level of this half's slot, its output base and the frame total
-    int l = 0;
-    while (l + 1 < L && slot >= lv[l + 1].out_off) l++;
-    int base = 0, total = 0;
-    for (int l2 = 0; l2 < L; l2++) {
-        const int c = kc[l2];
-        if (l2 < l) base += c;
-        total += c;
+// Per-level constants of the describe kernels and the frame's kept counts, staged in LDS
+// once per workgroup: a slot's level, output base and geometry are then LDS reads, not
+// the chain of dependent global loads (one per level passed) of a search over lv[].
+struct DescLevel {
+    int w, h, pitch;
+    uint32_t off;
+    int out_off, count;
+    float scale, kp_size;
+};
+
+__device__ __forceinline__ void stage_desc_levels(DescLevel* s, const LevelGeom* __restrict__ lv,
+                                                  const int* __restrict__ kc, int L) {
+    const int t = threadIdx.x;
+    if (t < L) {
+        const LevelGeom& g = lv[t];
+        DescLevel d;
+        d.w = g.w;
+        d.h = g.h;
+        d.pitch = g.pitch;
+        d.off = (uint32_t)g.off;
+        d.out_off = g.out_off;
+        d.count = kc[t];
+        d.scale = g.scale;
+        d.kp_size = g.kp_size;
+        s[t] = d;
     }
+    __syncthreads();
+}
+
+// Level l of kept slot `slot` (out_off is non-decreasing), the output index of the level's
+// first keypoint (base) and the frame's keypoint count (total): independent LDS reads.
+__device__ __forceinline__ void desc_level_of(const DescLevel* s, int L, int slot, int& l, int& base, int& total) {
+    l = 0;
+    base = 0;
+    total = 0;
+    for (int l2 = 0; l2 < L; l2++) {
+        const int c = s[l2].count;
+        total += c;
+        if (l2 + 1 < L && slot >= s[l2 + 1].out_off) {
+            base += c;
+            l = l2 + 1;
+        }
+    }
+}
+
+// Four kept keypoint slots per wave (one per 16-lane quarter): IC_Angle on the level
+// (cc:59-106), rBRIEF on the blurred level (cc:118-172), coordinate scaling
+// (cc:1613-1622), output in the reference's level-major order.  Everything evaluated
+// once per wave (fastAtan2, the double-precision sincos, the rounding constants) is
+// shared by four keypoints.  (Round 3: two per wave before, one per 32-lane half; four
+// take slightly longer alone -- configs[4] 0.654 -> 0.675 ms per launch -- but half the
+// waves leave the CUs to the other lane and the matcher: pipelined configs[4] 95.4-95.7k
+// -> 100.9-101.3k frames/s, configs[1] 215-218k -> 219.5k.)
+//   IC_Angle by rows: a lane reads rows v1 = ql - 15 and v2 = ql + 1 of the level (quarter
+//   lane 15 has no second row), 36 bytes from (x-15) & ~3 each, and two v_dot4_u32_u8 per
+//   dword against the circular mask and the (u + 15)-weighted mask give sum(I) and
+//   sum((u+15) I) over the row: m10 += sum((u+15) I) - 15 sum(I), m01 += v sum(I).
+//   The steered-BRIEF patch of the blurred level, rows y-18..y+18 (|rotated pattern
+//   point| <= 13*sqrt(2) < 18.5), 44 bytes from (x-18) & ~3, is staged in LDS as 111
+//   16-byte chunks (48-byte rows), seven per lane; all global loads are issued together,
+//   one round of latency.  Keypoints lie in [19, w-20] x [19, h-20] of their level, so
+//   every row exists; a row's last dword may reach 6 bytes past the level width (inside
+//   the pitch, or the buffers' slack for the very last row).
+//   A lane samples 16 of the 256 pairs (ql, 16 + ql, ..., 240 + ql); each pair step's
+//   ballot carries 16 descriptor bits per keypoint.
+__global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ pyr,
+                                                   const uint8_t* __restrict__ blur, long long fb,
+                                                   const LevelGeom* __restrict__ lv, int L,
+                                                   const uint32_t* __restrict__ kept, int kept_pf,
+                                                   const int* __restrict__ kept_count,
+                                                   orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                   int cap, int* __restrict__ n_out, int nframes) {
+    __shared__ __align__(16) uint32_t s_bpatch[16][37 * 12];  // BRIEF patches, 48-byte rows
+    __shared__ DescLevel s_lv[kMaxLevels];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int qt = lane >> 4, ql = lane & 15;
+    int f, sb;
+    xcd_frame_block((kept_pf + 15) / 16, nframes, f, sb);
+    const int slot0 = sb * 16 + wave * 4;
+    const int slot = slot0 + qt;
+    const uint32_t key_raw = kept[(size_t)f * kept_pf + min(slot, kept_pf - 1)];
+    stage_desc_levels(s_lv, lv, kept_count + (size_t)f * L, L);
+    if (slot0 >= kept_pf) return;  // whole wave; no barriers below
+    int l, base, total;
+    desc_level_of(s_lv, L, slot, l, base, total);
     if (slot0 == 0 && lane == 0) n_out[f] = total;
-    const LevelGeom& g = lv[l];
+    const DescLevel& g = s_lv[l];
     const int i = slot - g.out_off;
     const int o = base + i;
-    const bool valid = slot < kept_pf && i < kc[l] && o < cap;
-    if (__ballot(valid) == 0) return;  // both halves empty
-    const uint32_t key = valid ? kept[(size_t)f * kept_pf + slot] : 0u;
-    // an empty half samples the middle of its level (>= 23 px from every edge) and is masked
+    const bool valid = slot < kept_pf && i < g.count && o < cap;
+    if (__ballot(valid) == 0) return;  // all four quarters empty
+    const uint32_t key = valid ? key_raw : 0u;
+    // an empty quarter samples the middle of its level (>= 23 px from every edge) and is masked
     const int x = valid ? key_x(key) + kMinBorder : g.w / 2;
     const int y = valid ? key_y(key) + kMinBorder : g.h / 2;
     const int resp = key_resp(key);
     const int pitch = g.pitch;
     float lv_scale = g.scale, lv_size = g.kp_size;
     asm volatile("" : "+v"(lv_scale), "+v"(lv_size));
-    // IC_Angle (cc:59-106) by rows: lane hl < 31 loads patch row v = hl - 15 of the level,
-    // 36 bytes from (x-15) & ~3, and two v_dot4_u32_u8 per dword against the circular
-    // mask and the (u + 15)-weighted mask give sum(I) and sum((u+15) I) over the row:
-    // m10 += sum((u+15) I) - 15 sum(I), m01 += v sum(I).  The steered-BRIEF patch of the
-    // blurred level, rows y-18..y+18 (|rotated pattern point| <= 13*sqrt(2) < 18.5), 44
-    // bytes from (x-18) & ~3, is staged in LDS (48-byte rows as 111 16-byte chunks, four
-    // per lane; the patch loads are the kernel's largest cost: 37 row segments of
-    // separate cache lines per keypoint); all loads are issued together, one round of
-    // latency.
-    // Keypoints lie in [19, w-20] x [19, h-20] of their level, so every row exists; a
-    // row's last dword may reach 6 bytes past the level width (inside the pitch, or the
-    // buffers' slack for the very last row).
-    const int kp = wave * 2 + half;
+    const int kp = wave * 4 + qt;
     uint8_t* const bp = (uint8_t*)s_bpatch[kp];
     const int xs = (x - 15) & ~3, xb = (x - 18) & ~3;
     int m10, m01;
     {
-        const uint8_t* pframe = pyr + (size_t)f * fb;   // wave-uniform bases,
-        const uint8_t* bframe = blur + (size_t)f * fb;  // 32-bit offsets
-        const int v = min(hl, 30) - 15;
-        const int av = v < 0 ? -v : v;
+        const uint8_t* pframe = pyr + (size_t)f * fb;
+        const uint8_t* bframe = blur + (size_t)f * fb;
+        // rows v1 = ql - 15 (-15..0) and v2 = ql + 1 (1..15; quarter lane 15 has none)
+        const int v1 = ql - 15, v2 = min(ql + 1, 15);
         const int d0 = (x - 15) & 3;
-        const uint8_t* prow = pframe + (uint32_t)(g.off + (long long)(y + v) * pitch + xs);
-        const uint4 p0 = *(const uint4*)prow, p1 = *(const uint4*)(prow + 16);
-        const uint32_t p2 = *(const uint32_t*)(prow + 32);
-        // the patch's 37 x 3 16-byte chunks, chunk hl + 32 j (row c / 3, part c % 3):
-        // four load instructions per wave instead of six (37 rows on 32 lanes)
+        const uint8_t* prow1 = pframe + (uint32_t)(g.off + (long long)(y + v1) * pitch + xs);
+        const uint8_t* prow2 = pframe + (uint32_t)(g.off + (long long)(y + v2) * pitch + xs);
+        const uint4 p0 = *(const uint4*)prow1, p1 = *(const uint4*)(prow1 + 16);
+        const uint32_t p2 = *(const uint32_t*)(prow1 + 32);
+        const uint4 r0 = *(const uint4*)prow2, r1 = *(const uint4*)(prow2 + 16);
+        const uint32_t r2 = *(const uint32_t*)(prow2 + 32);
         const uint8_t* bpatch = bframe + (uint32_t)(g.off + (long long)(y - 18) * pitch + xb);
-        uint4 bch[4];
+        uint4 bch[7];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int c = min(hl + 32 * j, 110), row = (c * 171) >> 9;
+        for (int j = 0; j < 7; j++) {
+            const int c = min(ql + 16 * j, 110), row = (c * 171) >> 9;
             bch[j] = *(const uint4*)(bpatch + (uint32_t)(row * pitch + 16 * (c - 3 * row)));
         }
-        const uint4* cm = (const uint4*)c_icm[d0][av];
-        const uint4* cw = (const uint4*)c_icw[d0][av];
-        const uint4 m0 = cm[0], m1 = cm[1], m2 = cm[2], w0 = cw[0], w1 = cw[1], w2 = cw[2];
-        uint32_t cs = 0, ws = 0;
-        cs = __builtin_amdgcn_udot4(p0.x, m0.x, cs, false); ws = __builtin_amdgcn_udot4(p0.x, w0.x, ws, false);
-        cs = __builtin_amdgcn_udot4(p0.y, m0.y, cs, false); ws = __builtin_amdgcn_udot4(p0.y, w0.y, ws, false);
-        cs = __builtin_amdgcn_udot4(p0.z, m0.z, cs, false); ws = __builtin_amdgcn_udot4(p0.z, w0.z, ws, false);
-        cs = __builtin_amdgcn_udot4(p0.w, m0.w, cs, false); ws = __builtin_amdgcn_udot4(p0.w, w0.w, ws, false);
-        cs = __builtin_amdgcn_udot4(p1.x, m1.x, cs, false); ws = __builtin_amdgcn_udot4(p1.x, w1.x, ws, false);
-        cs = __builtin_amdgcn_udot4(p1.y, m1.y, cs, false); ws = __builtin_amdgcn_udot4(p1.y, w1.y, ws, false);
-        cs = __builtin_amdgcn_udot4(p1.z, m1.z, cs, false); ws = __builtin_amdgcn_udot4(p1.z, w1.z, ws, false);
-        cs = __builtin_amdgcn_udot4(p1.w, m1.w, cs, false); ws = __builtin_amdgcn_udot4(p1.w, w1.w, ws, false);
-        cs = __builtin_amdgcn_udot4(p2, m2.x, cs, false); ws = __builtin_amdgcn_udot4(p2, w2.x, ws, false);
-        const bool row_ok = hl < 31;
-        m10 = row_ok ? (int)ws - 15 * (int)cs : 0;
-        m01 = row_ok ? v * (int)cs : 0;
+        auto row_sums = [&](const uint4& a0, const uint4& a1, uint32_t a2, int av, uint32_t& cs, uint32_t& ws) {
+            const uint4* cm = (const uint4*)c_icm[d0][av];
+            const uint4* cw = (const uint4*)c_icw[d0][av];
+            const uint4 m0 = cm[0], m1 = cm[1], m2 = cm[2], w0 = cw[0], w1 = cw[1], w2 = cw[2];
+            cs = 0;
+            ws = 0;
+            cs = __builtin_amdgcn_udot4(a0.x, m0.x, cs, false); ws = __builtin_amdgcn_udot4(a0.x, w0.x, ws, false);
+            cs = __builtin_amdgcn_udot4(a0.y, m0.y, cs, false); ws = __builtin_amdgcn_udot4(a0.y, w0.y, ws, false);
+            cs = __builtin_amdgcn_udot4(a0.z, m0.z, cs, false); ws = __builtin_amdgcn_udot4(a0.z, w0.z, ws, false);
+            cs = __builtin_amdgcn_udot4(a0.w, m0.w, cs, false); ws = __builtin_amdgcn_udot4(a0.w, w0.w, ws, false);
+            cs = __builtin_amdgcn_udot4(a1.x, m1.x, cs, false); ws = __builtin_amdgcn_udot4(a1.x, w1.x, ws, false);
+            cs = __builtin_amdgcn_udot4(a1.y, m1.y, cs, false); ws = __builtin_amdgcn_udot4(a1.y, w1.y, ws, false);
+            cs = __builtin_amdgcn_udot4(a1.z, m1.z, cs, false); ws = __builtin_amdgcn_udot4(a1.z, w1.z, ws, false);
+            cs = __builtin_amdgcn_udot4(a1.w, m1.w, cs, false); ws = __builtin_amdgcn_udot4(a1.w, w1.w, ws, false);
+            cs = __builtin_amdgcn_udot4(a2, m2.x, cs, false); ws = __builtin_amdgcn_udot4(a2, w2.x, ws, false);
+        };
+        uint32_t cs1, ws1, cs2, ws2;
+        row_sums(p0, p1, p2, -v1, cs1, ws1);
+        row_sums(r0, r1, r2, v2, cs2, ws2);
+        const bool row2_ok = ql < 15;
+        m10 = ((int)ws1 - 15 * (int)cs1) + (row2_ok ? (int)ws2 - 15 * (int)cs2 : 0);
+        m01 = v1 * (int)cs1 + (row2_ok ? v2 * (int)cs2 : 0);
 #pragma unroll
-        for (int j = 0; j < 4; j++)
-            if (hl + 32 * j < 111) ((uint4*)bp)[hl + 32 * j] = bch[j];  // chunk c at byte 16 c
+        for (int j = 0; j < 7; j++)
+            if (ql + 16 * j < 111) ((uint4*)bp)[ql + 16 * j] = bch[j];  // chunk c at byte 16 c
     }
     wave_lds_fence();
 #pragma unroll
-    for (int o2 = 16; o2 > 0; o2 >>= 1) {  // within the 32-lane half
+    for (int o2 = 8; o2 > 0; o2 >>= 1) {  // within the 16-lane quarter
         m10 += __shfl_xor(m10, o2);
         m01 += __shfl_xor(m01, o2);
     }
     const float angle = fast_atan2((float)m01, (float)m10);
 
-    // steered BRIEF on the staged blurred patch: pairs hl, 32 + hl, ..., 224 + hl
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float rad = angle * factorPI;
     double cd, sd;
@@ -1584,42 +1633,44 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
         const uint32_t rx = __float_as_uint(fmaf(px, a, -(py * b)) + kRound);
         return bp[center + __umul24(ry, 48u) + rx];
     };
-    const int* pat = (const int*)c_pattern + hl;
-    int t0[8], t1[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const int q = pat[32 * k];
+    auto pair_test = [&](int q) -> bool {
         const float x0 = (float)(int8_t)(q & 0xff), y0 = (float)(int8_t)((q >> 8) & 0xff);
         const float x1 = (float)(int8_t)((q >> 16) & 0xff), y1 = (float)(int8_t)(q >> 24);
-        t0[k] = sample(x0, y0);
-        t1[k] = sample(x1, y1);
-    }
+        return sample(x0, y0) < sample(x1, y1);
+    };
+    const int* pat = (const int*)c_pattern + ql;
+    // descriptor word w (pairs 32 w .. 32 w + 31) = this quarter's 16 bits of the ballots
+    // of pair steps 2 w and 2 w + 1; lane ql < 2 stores words 4 ql .. 4 ql + 3
+    const int qsh = 16 * (qt & 1);
     uint32_t words[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const unsigned long long bits = __ballot(t0[k] < t1[k]);
-        words[k] = half ? (uint32_t)(bits >> 32) : (uint32_t)bits;  // descriptor bytes 4k..4k+3
+    for (int w = 0; w < 8; w++) {
+        const unsigned long long ba = __ballot(pair_test(pat[16 * (2 * w)]));
+        const unsigned long long bb = __ballot(pair_test(pat[16 * (2 * w + 1)]));
+        const uint32_t la = (qt & 2) ? (uint32_t)(ba >> 32) : (uint32_t)ba;
+        const uint32_t lb = (qt & 2) ? (uint32_t)(bb >> 32) : (uint32_t)bb;
+        words[w] = ((la >> qsh) & 0xffffu) | ((lb >> qsh) << 16);
     }
-    if (valid && hl < 2) {
+    if (valid && ql < 2) {
         uint4* d = (uint4*)(desc + ((size_t)f * cap + o) * 32);
-        d[hl] = hl == 0 ? make_uint4(words[0], words[1], words[2], words[3])
+        d[ql] = ql == 0 ? make_uint4(words[0], words[1], words[2], words[3])
                         : make_uint4(words[4], words[5], words[6], words[7]);
     }
-    if (valid && hl == 0) {
+    if (valid && ql == 0) {
         float fx = (float)x, fy = (float)y;
         if (l != 0) {
             fx = fx * lv_scale;
             fy = fy * lv_scale;
         }
-        orbx_keypoint kp;
-        kp.x = fx;
-        kp.y = fy;
-        kp.size = lv_size;
-        kp.angle = angle;
-        kp.response = (float)resp;
-        kp.octave = l;
-        kp.class_id = -1;
-        kps[(size_t)f * cap + o] = kp;
+        orbx_keypoint kpo;
+        kpo.x = fx;
+        kpo.y = fy;
+        kpo.size = lv_size;
+        kpo.angle = angle;
+        kpo.response = (float)resp;
+        kpo.octave = l;
+        kpo.class_id = -1;
+        kps[(size_t)f * cap + o] = kpo;
     }
 }
 
@@ -1683,7 +1734,7 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     if (ev) (void)hipEventRecord(ev[4], stream);
     if (stage_ev && stage_after == 4) (void)hipEventRecord(stage_ev, stream);
     {
-        dim3 grid(((plan.kept_per_frame + 7) / 8) * batch);
+        dim3 grid(((plan.kept_per_frame + 15) / 16) * batch);
         hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, stream, db.pyr, db.blur, fb, db.lv, L, db.kept,
                            plan.kept_per_frame, db.kept_count, (orbx_keypoint*)kps, desc, cap, n_per_frame, batch);
     }
