@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <type_traits>
 
 #include "orbx_kernels.h"
@@ -23,7 +24,10 @@ namespace orbx {
 
 const char* const kStageNames[kStages] = {"pyramid", "score_blur", "fast_cells", "octree", "describe", "total"};
 
-__constant__ __align__(16) int8_t c_pattern[1024];
+// the 256 rBRIEF point pairs (x0, y0, x1, y1 as int8, one int per pair), ordered
+// lane-major for k_describe: c_pattern[ql][k] = pair ql + 16 k, so quarter lane ql's
+// 16 pairs are four 16-byte loads
+__constant__ __align__(16) int c_pattern[16][16];
 
 __constant__ int c_umax[16];
 // IC_Angle by rows: for a patch row v and the patch's start alignment d0 = (x-15) & 3,
@@ -37,7 +41,10 @@ static const int8_t kPatternHost[1024] = {
 };
 
 hipError_t upload_constants(const OrbParams& prm) {
-    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), kPatternHost, sizeof(kPatternHost));
+    int patq[16][16];
+    for (int ql = 0; ql < 16; ql++)
+        for (int k = 0; k < 16; k++) memcpy(&patq[ql][k], kPatternHost + 4 * (ql + 16 * k), 4);
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), patq, sizeof(patq));
     if (e != hipSuccess) return e;
     uint32_t icm[4][16][12] = {}, icw[4][16][12] = {};
     for (int d0 = 0; d0 < 4; d0++)
@@ -1638,15 +1645,23 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
         const float x1 = (float)(int8_t)((q >> 16) & 0xff), y1 = (float)(int8_t)(q >> 24);
         return sample(x0, y0) < sample(x1, y1);
     };
-    const int* pat = (const int*)c_pattern + ql;
+    int pat[16];
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+        const int4 p4 = ((const int4*)c_pattern[ql])[v];
+        pat[4 * v] = p4.x;
+        pat[4 * v + 1] = p4.y;
+        pat[4 * v + 2] = p4.z;
+        pat[4 * v + 3] = p4.w;
+    }
     // descriptor word w (pairs 32 w .. 32 w + 31) = this quarter's 16 bits of the ballots
     // of pair steps 2 w and 2 w + 1; lane ql < 2 stores words 4 ql .. 4 ql + 3
     const int qsh = 16 * (qt & 1);
     uint32_t words[8];
 #pragma unroll
     for (int w = 0; w < 8; w++) {
-        const unsigned long long ba = __ballot(pair_test(pat[16 * (2 * w)]));
-        const unsigned long long bb = __ballot(pair_test(pat[16 * (2 * w + 1)]));
+        const unsigned long long ba = __ballot(pair_test(pat[2 * w]));
+        const unsigned long long bb = __ballot(pair_test(pat[2 * w + 1]));
         const uint32_t la = (qt & 2) ? (uint32_t)(ba >> 32) : (uint32_t)ba;
         const uint32_t lb = (qt & 2) ? (uint32_t)(bb >> 32) : (uint32_t)bb;
         words[w] = ((la >> qsh) & 0xffffu) | ((lb >> qsh) << 16);

@@ -189,7 +189,7 @@ static_assert(kGridRows % kRowBlk == 0 && kRowBlk <= 8, "row blocks tile the gri
 __host__ __device__ constexpr int bucket_table_len(int noct) { return kGridCols * noct * kNumBlk + 1; }
 
 struct SortedGrid {
-    const unsigned* skey;     // (cell << 18) | (index << 5) | octave, ascending
+    const unsigned* skey;     // (cell << 18) | (index << 5) | octave, ascending; bit 31: see kKeyBlocked
     const uint16_t* bstart;   // bucket starts into orun, [ix][octave][block], + sentinel
     const uint16_t* orun;     // sorted positions bucketed by (column, octave, row block)
     const float2* sxy;        // x, y
@@ -198,6 +198,10 @@ struct SortedGrid {
 };
 __device__ __forceinline__ int sk_idx(unsigned k) { return (int)((k >> 5) & 0x1fffu); }
 __device__ __forceinline__ int sk_oct(unsigned k) { return (int)(k & 31u); }
+// Bit 31 of a sorted key (above every cell, kNoCell included): the keypoint is blocked by
+// its claim before the search (kp_blocked).  Set only by the split scoring kernel, which
+// then holds no claims array in LDS; the published grid has it cleared.
+constexpr unsigned kKeyBlocked = 0x80000000u;
 
 // bucket of the keypoint with sorted key k in grid column ix: octave-major, then block
 __device__ __forceinline__ int bucket_of(unsigned k, int ix, int noct) {
@@ -460,7 +464,9 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
                                 __popcll(q2 ^ ((unsigned long long)b4.y << 32 | b4.x)) +
                                 __popcll(q3 ^ ((unsigned long long)b4.w << 32 | b4.z));
                         } else {
-                            const int i = sk_idx(G.skey[p]);
+                            const unsigned kk = G.skey[p];
+                            if (kk & kKeyBlocked) continue;
+                            const int i = sk_idx(kk);
                             if (Q.er_max >= 0.f && pb.u_right) {
                                 const float ur = pb.u_right[i];
                                 if (ur > 0 && fabsf(Q.ur - ur) > Q.er_max) continue;
@@ -600,7 +606,9 @@ struct ProjLds {
         orun = align16(bstart + (size_t)bucket_table_len(noct) * 2);
         sxy = align16(orun + (size_t)n * 2);
         sfmp = sxy + (size_t)n * 8;
-        owner = sfmp + (size_t)n * 4;  // the replay's owner map (none without the replay)
+        // the claims and the replay's owner map (neither without the replay: the split
+        // scoring keeps a keypoint's initial claim as bit 31 of its sorted key)
+        owner = sfmp + (replay ? (size_t)n * 4 : 0);
         // keypoint angles in sorted order (the rotation bins), with the LDS-resident query
         // state only; the lean form reads them from the keypoints after the replay
         sang = owner + (replay ? (size_t)n * 4 : 0);
@@ -1253,6 +1261,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
                                                               unsigned long long* __restrict__ scratch,
                                                               const long long* __restrict__ scratch_off,
                                                               unsigned char* __restrict__ grids, int gcap) {
+    static_assert(!SPLIT || !DLDS, "the split scoring tests the initial claims through the sorted keys only");
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_hist[kHistoLength];
     const ProjProblem pb = probs[blockIdx.x];
@@ -1298,11 +1307,16 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     build_octave_runs<NT>(skey, colstart, P.noct, bstart, orun, (unsigned*)(smem + L.sxy));
     __syncthreads();
     for (int p = tid; p < n; p += NT) {
-        const int i = sk_idx(skey[p]);
+        const unsigned k = skey[p];
+        const int i = sk_idx(k);
         const orbx_keypoint& kp = pb.keys[i];
         sxy[p] = make_float2(kp.x, kp.y);
-        sfmp[p] = pb.frame_mp[i];
-        if (!SPLIT) owner[p] = 0x7fffffff;
+        if (SPLIT) {
+            if (kp_blocked(pb.frame_mp[i], P)) skey[p] = k | kKeyBlocked;
+        } else {
+            sfmp[p] = pb.frame_mp[i];
+            owner[p] = 0x7fffffff;
+        }
         if (QLDS) sang[p] = kp.angle;
     }
     if (DLDS) {
@@ -1330,7 +1344,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
             if (qb + kStep < nq) nxt = load_query(pb, min(q + kStep, nq - 1));  // prefetch
             const int mp = q < nq ? cur.q.mp : -1;
             unsigned e[kTopK];
-            score_groupk<KR>(pb, P, cur, mp >= 0, G, sfmp, e);
+            score_groupk<KR>(pb, P, cur, mp >= 0, G, SPLIT ? nullptr : sfmp, e);
             if ((lane & (KR - 1)) == 0 && q < nq) {
 #pragma unroll
                 for (int v = 0; v < kListVec; v++)
@@ -1350,7 +1364,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
         unsigned char* gb = grids + (size_t)blockIdx.x * gl.total;
         const int nb = bucket_table_len(P.noct);
         for (int p = tid; p < n; p += NT) {
-            ((unsigned*)(gb + gl.skey))[p] = skey[p];
+            ((unsigned*)(gb + gl.skey))[p] = skey[p] & ~kKeyBlocked;
             ((uint16_t*)(gb + gl.orun))[p] = orun[p];
             ((float2*)(gb + gl.sxy))[p] = sxy[p];
             ((float*)(gb + gl.sang))[p] = pb.keys[sk_idx(skey[p])].angle;

@@ -6,8 +6,7 @@ set -o pipefail
 mkdir -p gpurun_out
 VARIANTS=${VARIANTS:-"a b c"}
 for v in ${PAR:-}; do
-  ORBX_LIB=$PWD/orbslam2commentedbyxcm_amd/_ab/liborbx_$v.so timeout -k 10 600 python -u -m pytest tests/test_gpu_extract.py \
-      tests/test_gpu_pipeline.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r3w_pytest_$v.log 2>&1
+  ORBX_LIB=$PWD/orbslam2commentedbyxcm_amd/_ab/liborbx_$v.so timeout -k 10 600 python -u -m pytest ${TESTS:-tests/test_gpu_extract.py tests/test_gpu_pipeline.py} -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r3w_pytest_$v.log 2>&1
   rc=$?; echo "parity $v"; tail -1 gpurun_out/r3w_pytest_$v.log
   if [ $rc -ne 0 ]; then exit $rc; fi
 done
