@@ -1511,6 +1511,14 @@ __device__ __forceinline__ void desc_level_of(const DescLevel* s, int L, int slo
     }
 }
 
+// k_describe's staging form by keypoint slots per frame.  Direct-to-LDS staging (more
+// describe waves per SIMD) is the faster kernel, alone and in the pipelined configs[1]
+// step (222.1-223.8k -> 226.4-227.7k frames/s), but at 5000 features, where the matcher
+// beside the extraction sets the step, the extra waves cost the matcher more than they
+// save (configs[4] 100.6-100.9k -> 94.1-95.1k; capping them by LDS gives both back):
+// register staging above this many slots.
+constexpr int kDescGldsMaxSlots = 3000;
+
 // Four kept keypoint slots per wave (one per 16-lane quarter): IC_Angle on the level
 // (cc:59-106), rBRIEF on the blurred level (cc:118-172), coordinate scaling
 // (cc:1613-1622), output in the reference's level-major order.  Everything evaluated
@@ -1525,12 +1533,15 @@ __device__ __forceinline__ void desc_level_of(const DescLevel* s, int L, int slo
 //   sum((u+15) I) over the row: m10 += sum((u+15) I) - 15 sum(I), m01 += v sum(I).
 //   The steered-BRIEF patch of the blurred level, rows y-18..y+18 (|rotated pattern
 //   point| <= 13*sqrt(2) < 18.5), 44 bytes from (x-18) & ~3, is staged in LDS as 111
-//   16-byte chunks (48-byte rows), seven per lane; all global loads are issued together,
-//   one round of latency.  Keypoints lie in [19, w-20] x [19, h-20] of their level, so
+//   16-byte chunks (48-byte rows); all global loads are issued together, one round of
+//   latency.  GLDS: the chunks go straight to LDS (global_load_lds_dwordx4, no VGPR
+//   destinations: 76 instead of 102 VGPRs, five waves per SIMD instead of four); else
+//   through registers, seven chunks per lane.  Keypoints lie in [19, w-20] x [19, h-20] of their level, so
 //   every row exists; a row's last dword may reach 6 bytes past the level width (inside
 //   the pitch, or the buffers' slack for the very last row).
 //   A lane samples 16 of the 256 pairs (ql, 16 + ql, ..., 240 + ql); each pair step's
 //   ballot carries 16 descriptor bits per keypoint.
+template <bool GLDS>
 __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ pyr,
                                                    const uint8_t* __restrict__ blur, long long fb,
                                                    const LevelGeom* __restrict__ lv, int L,
@@ -1582,11 +1593,40 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
         const uint4 r0 = *(const uint4*)prow2, r1 = *(const uint4*)(prow2 + 16);
         const uint32_t r2 = *(const uint32_t*)(prow2 + 32);
         const uint8_t* bpatch = bframe + (uint32_t)(g.off + (long long)(y - 18) * pitch + xb);
-        uint4 bch[7];
+        if constexpr (GLDS) {
+        // the four BRIEF patches go straight to LDS (global_load_lds_dwordx4: no VGPR
+        // destinations, so more waves fit a SIMD): patch by patch, the whole wave loads
+        // its 111 chunks (lane L chunks L and 64 + L), from the patch base of quarter q
+        // read off lane 16 q; an LDS-DMA piece lands at base + 16 x lane
+        {
+            const uint64_t mybase = (uint64_t)(uintptr_t)bpatch;
+            uint8_t* const wbp = (uint8_t*)s_bpatch[wave * 4];
 #pragma unroll
-        for (int j = 0; j < 7; j++) {
-            const int c = min(ql + 16 * j, 110), row = (c * 171) >> 9;
-            bch[j] = *(const uint4*)(bpatch + (uint32_t)(row * pitch + 16 * (c - 3 * row)));
+            for (int q = 0; q < 4; q++) {
+                const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)mybase, 16 * q);
+                const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(mybase >> 32), 16 * q);
+                const int sp = __builtin_amdgcn_readlane(pitch, 16 * q);
+                const uint8_t* qb = (const uint8_t*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+#pragma unroll
+                for (int jj = 0; jj < 2; jj++) {
+                    const int c = 64 * jj + lane;
+                    if (c < 111) {
+                        const int row = (c * 171) >> 9;
+                        __builtin_amdgcn_global_load_lds((const void*)(qb + (uint32_t)(row * sp + 16 * (c - 3 * row))),
+                                                         (__attribute__((address_space(3))) void*)(wbp + q * (int)sizeof(s_bpatch[0]) + 1024 * jj),
+                                                         16, 0, 0);
+                    }
+                }
+            }
+        }
+        }
+        uint4 bch[7];
+        if constexpr (!GLDS) {
+#pragma unroll
+            for (int j = 0; j < 7; j++) {
+                const int c = min(ql + 16 * j, 110), row = (c * 171) >> 9;
+                bch[j] = *(const uint4*)(bpatch + (uint32_t)(row * pitch + 16 * (c - 3 * row)));
+            }
         }
         auto row_sums = [&](const uint4& a0, const uint4& a1, uint32_t a2, int av, uint32_t& cs, uint32_t& ws) {
             const uint4* cm = (const uint4*)c_icm[d0][av];
@@ -1610,9 +1650,13 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
         const bool row2_ok = ql < 15;
         m10 = ((int)ws1 - 15 * (int)cs1) + (row2_ok ? (int)ws2 - 15 * (int)cs2 : 0);
         m01 = v1 * (int)cs1 + (row2_ok ? v2 * (int)cs2 : 0);
+        if constexpr (GLDS) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA pieces have landed
+        } else {
 #pragma unroll
-        for (int j = 0; j < 7; j++)
-            if (ql + 16 * j < 111) ((uint4*)bp)[ql + 16 * j] = bch[j];  // chunk c at byte 16 c
+            for (int j = 0; j < 7; j++)
+                if (ql + 16 * j < 111) ((uint4*)bp)[ql + 16 * j] = bch[j];  // chunk c at byte 16 c
+        }
     }
     wave_lds_fence();
 #pragma unroll
@@ -1750,7 +1794,8 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     if (stage_ev && stage_after == 4) (void)hipEventRecord(stage_ev, stream);
     {
         dim3 grid(((plan.kept_per_frame + 15) / 16) * batch);
-        hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, stream, db.pyr, db.blur, fb, db.lv, L, db.kept,
+        auto kern = plan.kept_per_frame <= kDescGldsMaxSlots ? k_describe<true> : k_describe<false>;
+        hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, db.pyr, db.blur, fb, db.lv, L, db.kept,
                            plan.kept_per_frame, db.kept_count, (orbx_keypoint*)kps, desc, cap, n_per_frame, batch);
     }
     if (ev) (void)hipEventRecord(ev[5], stream);

@@ -10,14 +10,14 @@ for v in ${PAR:-}; do
   rc=$?; echo "parity $v"; tail -1 gpurun_out/r3w_pytest_$v.log
   if [ $rc -ne 0 ]; then exit $rc; fi
 done
-for w in tum5k tum; do
+for w in ${WLS:-tum5k tum}; do
   for v in $VARIANTS; do
     ORBX_LIB=$PWD/orbslam2commentedbyxcm_amd/_ab/liborbx_$v.so timeout -k 10 200 python bench.py --workload $w --lanes 1 --no-pipeline \
         --no-cpu-baseline --no-local-map --no-host-fed --steps 20 --parity-frames 0 > gpurun_out/r3w.json 2>gpurun_out/r3w.err || exit 1
     python3 -c "import json; d=json.load(open('gpurun_out/r3w.json')); s=d['roofline']['stage_ms']; print('iso $w $v', {k: round(x, 4) for k, x in s.items()}, flush=True)" || exit 1
   done
 done
-for w in tum5k tum; do
+for w in ${WLS:-tum5k tum}; do
   for i in 1 2; do
     for v in $VARIANTS; do
       ORBX_LIB=$PWD/orbslam2commentedbyxcm_amd/_ab/liborbx_$v.so timeout -k 10 200 python bench.py --workload $w \
