@@ -133,6 +133,16 @@ def rocprof_mean_ms(stage: str, workload: str):
     return (None if tot is None else tot * 1e-6), files[-1].name
 
 
+def dominant_stage(event_ms: dict, workload: str) -> str:
+    """The stage whose kernels run longest per launch: by the committed kernel trace of
+    this workload's bench when it covers every stage, else by the HIP-event times (which,
+    pipelined, also hold the time a kernel waited for CUs held by other streams)."""
+    prof = {k: rocprof_mean_ms(k, workload)[0] for k in event_ms}
+    if all(v is not None for v in prof.values()):
+        return max(prof, key=prof.get)
+    return max(event_ms, key=event_ms.get)
+
+
 def pmc_valu(stage: str):
     """VALU wave-instructions per launch of `stage` from the newest profiles/*_pmc_valu.json
     (tools/pmc_valu.sh + tools/pmc_valu.py), or (None, None)."""
@@ -448,13 +458,13 @@ def main():
     # whichever is longer: a lane's extraction (its longest stage is reported) or the
     # matcher (configs[4]: its launch is then the critical path).
     kernels = {k: v for k, v in stage_ms.items() if k not in ("total", "match")}
-    dom = max(kernels, key=kernels.get)
+    wl = "tum5k" if c5 else "tum"
+    dom = dominant_stage(kernels, wl)
     if match and pipeline and stage_ms.get("match", 0.0) > stage_ms.get("total", 0.0):
         dom = "match"
     # frames per launch: a lane's batch for extraction stages, every pair for the matcher
     per_launch = (B - 1) if dom == "match" else (pl.bounds[0][1] - pl.bounds[0][0])
     achieved = bytes_pf[dom] * per_launch / (stage_ms[dom] * 1e-3) / 1e9
-    wl = "tum5k" if c5 else "tum"
     prof = profile_fields(dom, bytes_pf[dom] * per_launch, stage_ms[dom], wl)
     valu, valu_src = pmc_valu(dom) if not c5 else (None, None)
     issue = None

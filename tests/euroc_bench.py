@@ -302,7 +302,7 @@ def main(argv=None):
         n_mean = float(np.concatenate([res["nl"], res["nr"]]).mean())
         bytes_pf = bench.stage_bytes(pl.W, pl.H, n_mean)
         kern = {k: v for k, v in stage_ms.items() if k in bytes_pf and k != "total"}
-        dom = max(kern, key=kern.get)
+        dom = bench.dominant_stage(kern, "euroc")
         achieved = bytes_pf[dom] * B / (stage_ms[dom] * 1e-3) / 1e9
         slab_mb = pl.lay.nbytes / 1e6
         out = {

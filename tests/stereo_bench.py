@@ -248,7 +248,7 @@ def main(argv=None):
     n_mean = float(np.concatenate([nl, nr]).mean())
     bytes_pf = bench.stage_bytes(W, H, n_mean)
     kern = {s: v for s, v in stage_ms.items() if s not in ("total", "stereo")}
-    dom = max(kern, key=kern.get)
+    dom = bench.dominant_stage(kern, "kitti")
     achieved = bytes_pf[dom] * B / (stage_ms[dom] * 1e-3) / 1e9
     cpu = None
     if not args.no_cpu_baseline:
