@@ -66,6 +66,25 @@ def test_profile_fields_read_the_workload_trace(tmp_path, monkeypatch):
     assert bench.profile_fields("score_blur", 1.0, 0.3, "kitti")["rocprof_mean_ms"] is None
 
 
+def test_dominant_stage_prefers_the_kernel_trace(tmp_path, monkeypatch):
+    """Pipelined HIP-event times hold queueing beside the other streams, so the roofline's
+    kernel is the longest one in the workload's kernel trace when that covers every stage
+    (here describe's events are longest but its kernel is not), and the events decide
+    otherwise."""
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    hdr = '"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"\n'
+    (prof / "r03e_tum_kernel_stats.csv").write_text(
+        hdr + '"orbx::k_level_tiles(unsigned char const*)",50,1,316000.0,1,1,1,1\n'
+        '"void orbx::k_describe<true>(unsigned char const*)",50,1,263000.0,1,1,1,1\n')
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    ev = {"score_blur": 0.314, "describe": 0.313}
+    ev2 = {"score_blur": 0.30, "describe": 0.31}
+    assert bench.dominant_stage(ev2, "tum") == "score_blur"
+    assert bench.dominant_stage(ev, "kitti") == "score_blur"  # no trace: events
+    assert bench.dominant_stage({**ev2, "pyramid": 0.1}, "tum") == "describe"  # pyramid not in the trace
+
+
 def test_newest_profile_is_highest_tag():
     files = bench.newest_profiles("*_pmc_traffic.json")
     assert files, "no PMC traffic summary under profiles/"
