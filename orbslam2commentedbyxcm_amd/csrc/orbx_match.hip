@@ -390,6 +390,12 @@ __device__ __forceinline__ QueryReg shfl_query(const QueryReg& x, int src) {
 // row (out = kNoEntry).  Must be called with the whole wave active.
 // K = 64: one query per wave, all lanes over its window (the replay's re-scoring of a
 // query whose list ran out, a single query on the critical path).
+#ifndef ORBX_SCORE_PAIR
+// two bucket entries per scan step with descriptors from global memory (round 3): the
+// configs[4] matcher alone 1.114 -> 1.047 ms, the drop-in rows a11-a14 1-3 % faster,
+// pipelined steps unchanged (within noise)
+#define ORBX_SCORE_PAIR 1
+#endif
 template <int K>
 __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const QueryReg& QR, bool valid,
                              const SortedGrid& G, const int* sfmp, unsigned out[kTopK]) {
@@ -443,6 +449,56 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
                     // first / last block also hold rows outside the window
                     const uint16_t* bt = G.bstart + (ix * noct + o) * kNumBlk;
                     const int s0 = bt[b0], e0 = bt[b0 + 1], s1 = bt[b1], e1 = bt[b1 + 1];
+#if ORBX_SCORE_PAIR
+                    if (!G.sdesc) {
+                        // two entries per step (a and a + lpc): their LDS chains (entry,
+                        // position, key) and descriptor loads are independent, so they overlap
+                        auto test = [&](int a, int ent, float2 kp, unsigned kk, int p) {
+                            const int yr = ent >> 13;
+                            if ((a < e0 && yr < ylo) || (a >= s1 && yr > yhi)) return false;
+                            if (!(fabsf(kp.x - Q.u) < Q.r && fabsf(kp.y - Q.v) < Q.r)) return false;
+                            if (sfmp && kp_blocked(sfmp[p], P)) return false;
+                            return (kk & kKeyBlocked) == 0u;
+                        };
+                        for (int a = s0 + sub; a < e1; a += 2 * lpc) {
+                            const int a2 = a + lpc;
+                            const bool h2 = a2 < e1;
+                            const int entA = G.orun[a], entB = G.orun[h2 ? a2 : a];
+                            const int pA = entA & 0x1fff, pB = entB & 0x1fff;
+                            const float2 kA = G.sxy[pA], kB = G.sxy[pB];
+                            const unsigned kkA = G.skey[pA], kkB = G.skey[pB];
+                            const bool okA = test(a, entA, kA, kkA, pA);
+                            const bool okB = h2 && test(a2, entB, kB, kkB, pB);
+                            if (!okA && !okB) continue;
+                            const int iA = sk_idx(kkA), iB = sk_idx(okB ? kkB : kkA);
+                            const unsigned long long* tA = (const unsigned long long*)(pb.desc + (size_t)iA * 32);
+                            const unsigned long long* tB = (const unsigned long long*)(pb.desc + (size_t)iB * 32);
+                            const unsigned long long xA0 = tA[0], xA1 = tA[1], xA2 = tA[2], xA3 = tA[3];
+                            const unsigned long long xB0 = tB[0], xB1 = tB[1], xB2 = tB[2], xB3 = tB[3];
+                            float urA = 0.f, urB = 0.f;
+                            if (Q.er_max >= 0.f && pb.u_right) {
+                                urA = pb.u_right[iA];
+                                urB = pb.u_right[iB];
+                            }
+                            auto take = [&](bool ok, float ur, int p, unsigned long long x0, unsigned long long x1,
+                                            unsigned long long x2, unsigned long long x3) {
+                                if (!ok || (ur > 0 && fabsf(Q.ur - ur) > Q.er_max)) return;
+                                const int d = __popcll(q0 ^ x0) + __popcll(q1 ^ x1) + __popcll(q2 ^ x2) + __popcll(q3 ^ x3);
+                                const unsigned key = ((unsigned)d << 13) | (unsigned)p;
+                                seen++;
+                                if (key < k[KL - 1]) {
+#pragma unroll
+                                    for (int i = KL - 1; i > 0; i--)
+                                        k[i] = key < k[i - 1] ? k[i - 1] : (key < k[i] ? key : k[i]);
+                                    k[0] = key < k[0] ? key : k[0];
+                                }
+                            };
+                            take(okA, urA, pA, xA0, xA1, xA2, xA3);
+                            take(okB, urB, pB, xB0, xB1, xB2, xB3);
+                        }
+                        continue;
+                    }
+#endif
                     for (int a = s0 + sub; a < e1; a += lpc) {
                         const int ent = G.orun[a];
                         const int p = ent & 0x1fff, yr = ent >> 13;
