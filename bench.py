@@ -79,8 +79,10 @@ def stage_bytes(W, H, n_kps, nlevels=8, scale=1.2):
         "fast_cells": sum((w - 38) * (h - 38) for (w, h) in lv),
         # candidates in, kept keypoints out (4 B each)
         "octree": 8 * n_kps,
-        # 28 B keypoint + 32 B descriptor out per keypoint (patch reads hit L2)
-        "describe": 60 * n_kps,
+        # 28 B keypoint + 32 B descriptor out per keypoint, and the pixels it samples: the
+        # IC_Angle disc of the level (749 px, umax of ORBextractor.cc:519-549) and the 512
+        # rBRIEF points of the blurred level per keypoint, at most both images of every level
+        "describe": 60 * n_kps + min(n_kps * (749 + 512), 2 * P),
         # matching: query + candidate descriptors and keypoints read once, 4 B assignment out
         "match": (32 + 28) * 2 * n_kps + 4 * n_kps,
         # SURVEY.md §8(d) canonical whole-extraction figure
