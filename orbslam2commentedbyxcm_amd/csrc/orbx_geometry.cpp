@@ -209,7 +209,10 @@ bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
         const float s = prm.inv_scale[l];
         g.w = cv_roundf((float)W * s);                 // cc:1643
         g.h = cv_roundf((float)H * s);
-        if (g.w < 2 * kEdge + 8 || g.h < 2 * kEdge + 8) { plan.why = "pyramid level too small"; return false; }
+        // below 33 px the reference's DistributeOctTree divides by a zero or negative
+        // border-trimmed size (ORBextractor.cc:674-676: nIni = round(width / height),
+        // vpIniNodes.resize(nIni)), so such frames are refused rather than given a meaning
+        if (g.w < kMinLevelSide || g.h < kMinLevelSide) { plan.why = "pyramid level under 33 px"; return false; }
         if (g.w - 2 * kMinBorder >= 4096 || g.h - 2 * kMinBorder >= 4096) { plan.why = "frame too large"; return false; }
         g.pitch = (g.w + 63) & ~63;
         g.off = off;
@@ -226,13 +229,15 @@ bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
         const float height = (float)(maxBorderY - minBorderY);
         const int nCols = (int)(width / 30.f);
         const int nRows = (int)(height / 30.f);
-        if (nCols <= 0 || nRows <= 0) { plan.why = "level narrower than one FAST cell"; return false; }
-        const int wCell = (int)std::ceil(width / nCols);
-        const int hCell = (int)std::ceil(height / nRows);
+        // a level narrower or shorter than one 30-px FAST cell (under 62 px) has no cells:
+        // the reference's cell loops run zero times and the level keeps no keypoints
+        const bool no_cells = nCols <= 0 || nRows <= 0;
+        const int wCell = no_cells ? 0 : (int)std::ceil(width / nCols);
+        const int hCell = no_cells ? 0 : (int)std::ceil(height / nRows);
         g.cell_first = cell_first;
         g.key_off = key_off;
         int level_cap = 0;
-        for (int i = 0; i < nRows; i++) {
+        for (int i = 0; i < (no_cells ? 0 : nRows); i++) {
             const float iniY = (float)(minBorderY + i * hCell);
             float maxY = iniY + hCell + 6;
             if (iniY >= maxBorderY - 3) continue;
@@ -270,6 +275,8 @@ bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
         // octree roots, cc:674-699
         const int minX = minBorderX, maxX = maxBorderX, minY = minBorderY, maxY = maxBorderY;
         g.nIni = (int)std::round((float)(maxX - minX) / (maxY - minY));
+        // a level without keypoints never reads its root nodes (DistributeOctTree of no keys)
+        if (level_cap == 0) g.nIni = std::min(std::max(g.nIni, 1), kMaxIni);
         if (g.nIni < 1 || g.nIni > kMaxIni) { plan.why = "aspect ratio outside octree support"; return false; }
         g.hX = (float)(maxX - minX) / g.nIni;
         for (int i = 0; i <= g.nIni; i++) g.ini_x0[i] = (int)(g.hX * (float)i);

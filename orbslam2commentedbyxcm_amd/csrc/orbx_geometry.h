@@ -14,6 +14,7 @@
 namespace orbx {
 
 constexpr int kMaxLevels = 32;
+constexpr int kMinLevelSide = 33;  // smallest pyramid level side make_plan accepts
 constexpr int kEdge = 19;        // EDGE_THRESHOLD, ORBextractor.cc:46
 constexpr int kMinBorder = 16;   // EDGE_THRESHOLD - 3, ORBextractor.cc:1032
 constexpr int kMaxIni = 16;      // octree root nodes supported per level
