@@ -473,3 +473,28 @@ def test_search_for_triangulation_batch_device_rejects(orbx_built):
         m.SearchForTriangulationBatchDevice([rec], cam, np.array([[0, 1]]), np.zeros((1, 3, 3)), 8, z, z, z)
     with pytest.raises(L.OrbxError):
         m.SearchForTriangulationBatchDevice([rec], cam, np.array([[0, 0]]), np.zeros((1, 3, 3)), 9000, z, z, z)
+
+
+def test_search_by_projection_without_queries(oracle, orbx_built):
+    """No query survives (every last-frame MapPoint absent or an outlier; every KeyFrame
+    MapPoint already found): 0 matches, the current assignment untouched, as the oracle."""
+    A, B = S.two_views(oracle, 0)
+    mps = S.with_depth_info(S.mappoints_from(A, 0), A, 0)
+    cur0 = np.full(len(B.keys), -1, np.int32)
+    cur0[::7] = 3
+    m = ORBmatcher(0.9, True)
+    none_mp = np.full(len(A.keys), -1, np.int32)
+    cur = cur0.copy()
+    assert m.SearchByProjectionFrame(B, cur, A, none_mp, mps, 15.0, True) == 0
+    assert np.array_equal(cur, cur0)
+    all_out = np.ones(len(A.keys), np.uint8)
+    last_mp = np.arange(len(A.keys), dtype=np.int32)
+    cur = cur0.copy()
+    n = m.SearchByProjectionFrame(B, cur, A, last_mp, mps, 15.0, True, last_outlier=all_out)
+    cur_ref = cur0.copy()
+    assert n == oracle.sbp_frame(B, cur_ref, A, last_mp, mps, 15.0, True, True, last_outlier=all_out) == 0
+    assert np.array_equal(cur, cur0) and np.array_equal(cur_ref, cur0)
+    cur = cur0.copy()
+    found = np.ones(len(A.keys), np.uint8)
+    assert m.SearchByProjectionKeyFrame(B, cur, A, last_mp, mps, 10.0, 100, already_found=found) == 0
+    assert np.array_equal(cur, cur0)
