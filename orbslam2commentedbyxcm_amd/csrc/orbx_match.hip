@@ -2007,49 +2007,66 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
 
 // One query of SearchForTriangulation = one unmatched KF1 keypoint inside a vocabulary
 // node shared with KF2 (ORBmatcher.cc:886-1019), in the reference's visiting order.
+// K lanes per query (K = 16: four queries per wave, a shared node's list holds a few
+// to a few tens of KF2 keypoints; K = 64: the whole wave on one query).  Returns the
+// group's best as a 32-bit key dist << 26 | (2^26 - 1 - offset in the node list): the
+// minimum is the smallest distance, the last position on ties (the reference replaces
+// its best on dist <= bestDist); 0xffffffff = none.  `valid` false: no query for this
+// group.  Must be called with the whole wave active.
+template <int K>
+__device__ unsigned score_tri_group(const TriProblem& pb, const TriQuery& Q, bool valid, const uint8_t* matched2) {
+    static_assert(K == 16 || K == 64, "a DPP row or a wave");
+    const int r = threadIdx.x & (K - 1);
+    unsigned best = 0xffffffffu;
+    if (valid && Q.beg < Q.end) {  // empty range: no shared node (batched tables: filtered queries)
+        const orbx_keypoint kp1 = pb.keys1[Q.idx1];
+        const unsigned long long* d1 = (const unsigned long long*)(pb.desc1 + (size_t)Q.idx1 * 32);
+        const unsigned long long q0 = d1[0], q1 = d1[1], q2 = d1[2], q3 = d1[3];
+        // epipolar line of kp1 in KF2 (CheckDistEpipolarLine, ORBmatcher.cc:186-213)
+        const float* F = pb.F12;
+        // fused as g++ -O3 -march=native builds the reference: the first product of each
+        // sum goes into an FMA (H4)
+        const float a = fmaf(kp1.x, F[0], kp1.y * F[3]) + F[6];
+        const float b = fmaf(kp1.x, F[1], kp1.y * F[4]) + F[7];
+        const float c = fmaf(kp1.x, F[2], kp1.y * F[5]) + F[8];
+        for (int p = Q.beg + r; p < Q.end; p += K) {
+            const int idx2 = pb.fv2_idx[p];
+            if (matched2[idx2] || pb.has_mp2[idx2]) continue;
+            const bool stereo2 = pb.u_right2 && pb.u_right2[idx2] >= 0;
+            if (pb.only_stereo && !stereo2) continue;
+            const unsigned long long* t = (const unsigned long long*)(pb.desc2 + (size_t)idx2 * 32);
+            const int dist = __popcll(q0 ^ t[0]) + __popcll(q1 ^ t[1]) + __popcll(q2 ^ t[2]) + __popcll(q3 ^ t[3]);
+            if (dist > 50) continue;  // TH_LOW; the running bestDist bound is applied by the key order
+            const orbx_keypoint kp2 = pb.keys2[idx2];
+            if (!Q.stereo1 && !stereo2) {
+                const float distex = pb.ex - kp2.x;
+                const float distey = pb.ey - kp2.y;
+                if (fmaf(distex, distex, distey * distey) < 100 * pb.scale2[kp2.octave]) continue;
+            }
+            const float num = fmaf(a, kp2.x, b * kp2.y) + c;
+            const float den = fmaf(a, a, b * b);
+            if (den == 0) continue;
+            const float dsqr = num * num / den;
+            if (!((double)dsqr < 3.84 * (double)pb.sigma2_2[kp2.octave])) continue;
+            const unsigned key = ((unsigned)dist << 26) | (0x3ffffffu - (unsigned)(p - Q.beg));
+            best = key < best ? key : best;
+        }
+    }
+    if (K == 16) return row_min_u32(best);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = umin_(best, (unsigned)__shfl_xor((int)best, o));
+    return best;
+}
+
+// The 64-bit form the commit reads: dist << 32 | (0xffffffff - offset), or kNoKey.
+__device__ __forceinline__ unsigned long long tri_key64(unsigned k32) {
+    if (k32 == 0xffffffffu) return kNoKey;
+    return ((unsigned long long)(k32 >> 26) << 32) | (0xffffffffu - (0x3ffffffu - (k32 & 0x3ffffffu)));
+}
+
 __device__ void score_tri(const TriProblem& pb, const TriQuery& Q, const uint8_t* matched2,
                           unsigned long long& best) {
-    const int lane = threadIdx.x & 63;
-    best = kNoKey;
-    if (Q.beg >= Q.end) return;  // no shared node (batched tables: filtered queries), wave-uniform
-    const orbx_keypoint kp1 = pb.keys1[Q.idx1];
-    const unsigned long long* d1 = (const unsigned long long*)(pb.desc1 + (size_t)Q.idx1 * 32);
-    const unsigned long long q0 = d1[0], q1 = d1[1], q2 = d1[2], q3 = d1[3];
-    // epipolar line of kp1 in KF2 (CheckDistEpipolarLine, ORBmatcher.cc:186-213)
-    const float* F = pb.F12;
-    // fused as g++ -O3 -march=native builds the reference: the first product of each
-    // sum goes into an FMA (H4)
-    const float a = fmaf(kp1.x, F[0], kp1.y * F[3]) + F[6];
-    const float b = fmaf(kp1.x, F[1], kp1.y * F[4]) + F[7];
-    const float c = fmaf(kp1.x, F[2], kp1.y * F[5]) + F[8];
-    for (int p = Q.beg + lane; p < Q.end; p += 64) {
-        const int idx2 = pb.fv2_idx[p];
-        if (matched2[idx2] || pb.has_mp2[idx2]) continue;
-        const bool stereo2 = pb.u_right2 && pb.u_right2[idx2] >= 0;
-        if (pb.only_stereo && !stereo2) continue;
-        const unsigned long long* t = (const unsigned long long*)(pb.desc2 + (size_t)idx2 * 32);
-        const int dist = __popcll(q0 ^ t[0]) + __popcll(q1 ^ t[1]) + __popcll(q2 ^ t[2]) + __popcll(q3 ^ t[3]);
-        if (dist > 50) continue;  // TH_LOW; the running bestDist bound is applied by the key order
-        const orbx_keypoint kp2 = pb.keys2[idx2];
-        if (!Q.stereo1 && !stereo2) {
-            const float distex = pb.ex - kp2.x;
-            const float distey = pb.ey - kp2.y;
-            if (fmaf(distex, distex, distey * distey) < 100 * pb.scale2[kp2.octave]) continue;
-        }
-        const float num = fmaf(a, kp2.x, b * kp2.y) + c;
-        const float den = fmaf(a, a, b * b);
-        if (den == 0) continue;
-        const float dsqr = num * num / den;
-        if (!((double)dsqr < 3.84 * (double)pb.sigma2_2[kp2.octave])) continue;
-        // accepted candidates replace the best on dist <= bestDist: min distance, last position
-        const unsigned long long key = ((unsigned long long)dist << 32) | (0xffffffffu - (unsigned)(p - Q.beg));
-        best = key < best ? key : best;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long ob = __shfl_xor(best, o);
-        best = ob < best ? ob : best;
-    }
+    best = tri_key64(score_tri_group<64>(pb, Q, true, matched2));
 }
 
 // 16 waves score the queries (each scan is a chain of dependent gathers); wave 0 then
@@ -2073,10 +2090,12 @@ __global__ __launch_bounds__(kTriThreads) void k_triangulation(const TriProblem*
     if (tid < kHistoLength) s_hist[tid] = 0;
     __syncthreads();
     unsigned long long* keys = scratch + pb.scratch_off;
-    for (int q = wave; q < pb.nq; q += kTriThreads / 64) {  // candidate scans: all waves
-        unsigned long long best;
-        score_tri(pb, pb.q[q], matched2, best);
-        if (lane == 0) keys[q] = best;
+    // candidate scans: all waves, four queries per wave (16-lane rows)
+    for (int q0 = wave * 4; q0 < pb.nq; q0 += kTriThreads / 16) {
+        const int q = q0 + (lane >> 4);
+        const bool valid = q < pb.nq;
+        const unsigned best = score_tri_group<16>(pb, pb.q[valid ? q : q0], valid, matched2);
+        if (valid && (lane & 15) == 0) keys[q] = tri_key64(best);
     }
     __syncthreads();
     if (wave == 0) {
