@@ -2338,7 +2338,7 @@ hipError_t launch_triangulation_batch(const TriBatch& tb, unsigned long long* sc
 
 // Frame::ComputeStereoMatches (Frame.cc:673-885) for B left/right pairs, three launches:
 //   k_stereo_rows     vRowIndices (cc:693-708) of each pair as a CSR over image rows;
-//   k_stereo          one wave per left keypoint: row-band Hamming search, 11x11 SAD over
+//   k_stereo          a 16-lane row per left keypoint: row-band Hamming search, 11x11 SAD over
 //                     shifts -5..5 on the pyramid level, parabola fit (cc:720-866);
 //   k_stereo_outlier  this fork's outlier pass, which sits inside the iL loop
 //                     (cc:868-884, hazard H8): after every iteration that reaches it,
@@ -2418,20 +2418,39 @@ __global__ __launch_bounds__(kStereoRowThreads) void k_stereo_rows(StereoBatch s
 }
 
 // One wave per left keypoint of pair blockIdx.y.
+// k_stereo: four left keypoints per wave (16-lane rows; round 3, one per wave before:
+// KITTI 55.5-55.7k -> 57.9-58.3k stereo frames/s, EuRoC +7 %).  A row
+// band holds tens of right keypoints and the SAD window 121 pixels, so a whole wave per
+// keypoint left most lanes idle in the band scan's last pass and the SAD's second; here
+// a row's 16 lanes share the band scan (key dist << 23 | iR: the smallest distance, then
+// the first right keypoint of the row list, as the reference's strict <) and each SAD
+// (the 11 shifts' sums by DPP row reductions).  Rows whose keypoint stops early (empty
+// band, no match, out-of-image window, border shift, |deltaR| > 1) carry their result
+// along with the wave; lane 0 of a row writes it.
+__device__ __forceinline__ unsigned row_sum_u32(unsigned v) {
+    v += (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false);
+    return v;
+}
+
 __global__ __launch_bounds__(256) void k_stereo(StereoBatch sb) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int gl = lane & 15;
     const int b = blockIdx.y;
-    const int iL = blockIdx.x * 4 + wave;
+    const int base = (blockIdx.x * 4 + wave) * 4;
+    const int iL = base + (lane >> 4);
     const int nl = min(sb.n_l[b], sb.cap);
-    if (iL >= nl) return;
+    if (base >= nl) return;  // whole wave
+    const bool valid = iL < nl;
     StereoResult res;
     res.reach_sort = 0;
     res.pushed = 0;
     res.dist = 0;
     res.u_right = -1.f;
     res.depth = -1.f;
-    StereoResult* out = sb.res + (size_t)b * sb.cap + iL;
-    const orbx_keypoint kpL = sb.keys_l[(size_t)b * sb.cap + iL];
+    const orbx_keypoint kpL = sb.keys_l[(size_t)b * sb.cap + (valid ? iL : base)];
     const int levelL = kpL.octave;
     const float vL = kpL.y, uL = kpL.x;
     const int row = (int)vL;
@@ -2439,71 +2458,82 @@ __global__ __launch_bounds__(256) void k_stereo(StereoBatch sb) {
     const int cbeg = row >= 0 && row < sb.rows ? roff[row] : 0;
     const int cend = row >= 0 && row < sb.rows ? min(roff[row + 1], sb.band_cap) : 0;
     const float minD = 0.f;
-    if (cend == cbeg || uL - minD < 0) {  // cc:727-735
-        if (lane == 0) *out = res;
-        return;
-    }
+    const bool scan = valid && cend != cbeg && uL - minD >= 0;  // cc:727-735
     const float minU = uL - sb.max_d, maxU = uL - minD;
     const int32_t* ridx = sb.row_idx + (size_t)b * sb.band_cap;
     const orbx_keypoint* kr = sb.keys_r + (size_t)b * sb.cap;
     const uint8_t* dr = sb.desc_r + (size_t)b * sb.cap * 32;
-    const unsigned long long* dl = (const unsigned long long*)(sb.desc_l + ((size_t)b * sb.cap + iL) * 32);
-    const unsigned long long q0 = dl[0], q1 = dl[1], q2 = dl[2], q3 = dl[3];
-    unsigned long long best = kNoKey;
-    for (int p = cbeg + lane; p < cend; p += 64) {
-        const int iR = ridx[p];
-        const orbx_keypoint kpR = kr[iR];
-        if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
-        const float uR = kpR.x;
-        if (uR >= minU && uR <= maxU) {
-            const unsigned long long* t = (const unsigned long long*)(dr + (size_t)iR * 32);
-            const int d = __popcll(q0 ^ t[0]) + __popcll(q1 ^ t[1]) + __popcll(q2 ^ t[2]) + __popcll(q3 ^ t[3]);
-            const unsigned long long key = ((unsigned long long)d << 32) | (unsigned)iR;
-            best = key < best ? key : best;
+    unsigned best = 0xffffffffu;
+    if (scan) {
+        const unsigned long long* dl = (const unsigned long long*)(sb.desc_l + ((size_t)b * sb.cap + iL) * 32);
+        const unsigned long long q0 = dl[0], q1 = dl[1], q2 = dl[2], q3 = dl[3];
+        for (int p = cbeg + gl; p < cend; p += 16) {
+            const int iR = ridx[p];
+            const orbx_keypoint kpR = kr[iR];
+            if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
+            const float uR = kpR.x;
+            if (uR >= minU && uR <= maxU) {
+                const unsigned long long* t = (const unsigned long long*)(dr + (size_t)iR * 32);
+                const int d = __popcll(q0 ^ t[0]) + __popcll(q1 ^ t[1]) + __popcll(q2 ^ t[2]) + __popcll(q3 ^ t[3]);
+                best = umin_(best, ((unsigned)d << 23) | (unsigned)iR);
+            }
         }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long ob = __shfl_xor(best, o);
-        best = ob < best ? ob : best;
-    }
-    res.reach_sort = 1;
-    const int bestDist = best == kNoKey ? 100 : (int)(best >> 32);  // starts at TH_HIGH, strict <
-    if (bestDist < 75) {                                             // thOrbDist = (TH_HIGH + TH_LOW) / 2
-        const int bestIdxR = (int)(best & 0xffffffffu);
+    best = row_min_u32(best);
+    if (scan) res.reach_sort = 1;
+    const int bestDist = best == 0xffffffffu ? 100 : (int)(best >> 23);  // starts at TH_HIGH, strict <
+    bool sad = scan && bestDist < 75;                                     // thOrbDist = (TH_HIGH + TH_LOW) / 2
+    const int w = 5, L = 5;
+    float scaleduL = 0.f, scaledvL = 0.f, scaleduR0 = 0.f;
+    if (sad) {
+        const int bestIdxR = (int)(best & 0x7fffffu);
         const float uR0 = kr[bestIdxR].x;
         const float scaleFactor = sb.inv_scale[levelL];
-        const float scaleduL = roundf(kpL.x * scaleFactor);
-        const float scaledvL = roundf(kpL.y * scaleFactor);
-        const float scaleduR0 = roundf(uR0 * scaleFactor);
-        const int w = 5, L = 5;
+        scaleduL = roundf(kpL.x * scaleFactor);
+        scaledvL = roundf(kpL.y * scaleFactor);
+        scaleduR0 = roundf(uR0 * scaleFactor);
         const float iniu = scaleduR0 + L - w;
         const float endu = scaleduR0 + L + w + 1;
         if (iniu < 0 || endu >= sb.level_w[levelL]) {  // cc:810-811
             res.reach_sort = 0;
-            if (lane == 0) *out = res;
-            return;
+            sad = false;
         }
-        const int pitch = sb.level_pitch[levelL];
-        const uint8_t* IL = sb.pyr_l + (size_t)b * sb.fb_l + sb.level_off[levelL];
-        const uint8_t* IR = sb.pyr_r + (size_t)b * sb.fb_r + sb.level_off[levelL];
+    }
+    float vd[11];
+    int bestDistS = 0x7fffffff, bestincR = 0;
+    {
+        const int pitch = sad ? sb.level_pitch[levelL] : 0;
+        const uint8_t* IL = sb.pyr_l + (size_t)b * sb.fb_l + (sad ? sb.level_off[levelL] : 0);
+        const uint8_t* IR = sb.pyr_r + (size_t)b * sb.fb_r + (sad ? sb.level_off[levelL] : 0);
         const int yl0 = (int)scaledvL - w, xl0 = (int)scaleduL - w;
-        const int cl = IL[(size_t)(yl0 + w) * pitch + xl0 + w];
-        float vd[11];
-        int bestDistS = 0x7fffffff, bestincR = 0;
+        int cl = 0;
+        int a8[8];
+        if (sad) {
+            cl = IL[(size_t)(yl0 + w) * pitch + xl0 + w];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int k = gl + 16 * j;
+                const int yy = k / 11, xx = k - yy * 11;
+                a8[j] = k < 121 ? (int)IL[(size_t)(yl0 + yy) * pitch + xl0 + xx] - cl : 0;
+            }
+        }
 #pragma unroll
         for (int incR = -L; incR <= L; incR++) {
-            const int xr0 = (int)(scaleduR0 + incR - w);
-            const int cr = IR[(size_t)(yl0 + w) * pitch + xr0 + w];
             int acc = 0;
-            for (int k = lane; k < 121; k += 64) {
-                const int yy = k / 11, xx = k - yy * 11;
-                const int a = (int)IL[(size_t)(yl0 + yy) * pitch + xl0 + xx] - cl;
-                const int c = (int)IR[(size_t)(yl0 + yy) * pitch + xr0 + xx] - cr;
-                acc += a > c ? a - c : c - a;
-            }
+            if (sad) {
+                const int xr0 = (int)(scaleduR0 + incR - w);
+                const int cr = IR[(size_t)(yl0 + w) * pitch + xr0 + w];
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+                for (int j = 0; j < 8; j++) {
+                    const int k = gl + 16 * j;
+                    if (k < 121) {
+                        const int yy = k / 11, xx = k - yy * 11;
+                        const int c = (int)IR[(size_t)(yl0 + yy) * pitch + xr0 + xx] - cr;
+                        acc += a8[j] > c ? a8[j] - c : c - a8[j];
+                    }
+                }
+            }
+            acc = (int)row_sum_u32((unsigned)acc);
             const float dist = (float)acc;  // cv::norm(IL, IR, NORM_L1) on integer-valued floats
             if (dist < (float)bestDistS) {
                 bestDistS = (int)dist;
@@ -2511,11 +2541,12 @@ __global__ __launch_bounds__(256) void k_stereo(StereoBatch sb) {
             }
             vd[L + incR] = dist;
         }
-        if (bestincR == -L || bestincR == L) {  // cc:834-835
-            res.reach_sort = 0;
-            if (lane == 0) *out = res;
-            return;
-        }
+    }
+    if (sad && (bestincR == -L || bestincR == L)) {  // cc:834-835
+        res.reach_sort = 0;
+        sad = false;
+    }
+    if (sad) {
         float dist1 = vd[0], dist2 = vd[0], dist3 = vd[0];
 #pragma unroll
         for (int k = 0; k < 11; k++) {
@@ -2526,24 +2557,24 @@ __global__ __launch_bounds__(256) void k_stereo(StereoBatch sb) {
         const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
         if (deltaR < -1 || deltaR > 1) {  // cc:845-846
             res.reach_sort = 0;
-            if (lane == 0) *out = res;
-            return;
-        }
-        float bestuR = sb.scale[levelL] * (scaleduR0 + (float)bestincR + deltaR);
-        float disparity = (uL - bestuR);
-        if (disparity >= minD && disparity < sb.max_d) {
-            if (disparity <= 0) {
-                disparity = 0.01f;
-                bestuR = (float)((double)uL - 0.01);
+        } else {
+            float bestuR = sb.scale[levelL] * (scaleduR0 + (float)bestincR + deltaR);
+            float disparity = (uL - bestuR);
+            if (disparity >= minD && disparity < sb.max_d) {
+                if (disparity <= 0) {
+                    disparity = 0.01f;
+                    bestuR = (float)((double)uL - 0.01);
+                }
+                res.depth = sb.bf / disparity;
+                res.u_right = bestuR;
+                res.pushed = 1;
+                res.dist = bestDistS;
             }
-            res.depth = sb.bf / disparity;
-            res.u_right = bestuR;
-            res.pushed = 1;
-            res.dist = bestDistS;
         }
     }
-    if (lane == 0) *out = res;
+    if (valid && gl == 0) sb.res[(size_t)b * sb.cap + iL] = res;
 }
+
 
 // The in-loop outlier pass (cc:868-884) of one pair per 1024-thread workgroup.
 //
@@ -2731,7 +2762,7 @@ hipError_t launch_stereo(const StereoBatch& sb, int batch, hipStream_t stream) {
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k_stereo_rows, dim3(batch), dim3(kStereoRowThreads), rows_lds, stream, sb);
-    hipLaunchKernelGGL(k_stereo, dim3((sb.cap + 3) / 4, batch), dim3(256), 0, stream, sb);
+    hipLaunchKernelGGL(k_stereo, dim3((sb.cap + 15) / 16, batch), dim3(256), 0, stream, sb);
     int n2 = kSortThreads;
     while (n2 < sb.cap) n2 <<= 1;
     const size_t lds = stereo_outlier_lds(sb.cap);
