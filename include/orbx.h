@@ -84,7 +84,11 @@ int orbx_extractor_max_keypoints(orbx_extractor* ex, int width, int height, int*
  * the reference order (level-major, octree-list order), coordinates scaled to level
  * 0; descriptors n x 32 bytes.  Returns ORBX_EMPTY (outputs untouched) for an empty
  * image, ORBX_ERR_CAPACITY if more than `cap` keypoints were found (*n_out then
- * holds the required count). */
+ * holds the required count).  Frame size: pyramid levels under 62 px on a side hold no
+ * FAST cell and keep no keypoints, as in the reference (ORBextractor.cc:1047-1085); a
+ * frame with a level under 33 px returns ORBX_ERR_UNSUPPORTED (the reference's
+ * DistributeOctTree divides by a zero or negative size there, cc:674-676), as do
+ * levels over 4096 px and aspect ratios beyond 16 octree roots. */
 int orbx_extract(orbx_extractor* ex, const uint8_t* img, int width, int height, size_t stride,
                  orbx_keypoint* kps, uint8_t* desc, int cap, int* n_out);
 
