@@ -120,11 +120,15 @@ def newest_profiles(pattern: str):
 
 def rocprof_mean_ms(stage: str, workload: str):
     """Mean duration (ms) per launch of `stage`'s kernels in the newest committed kernel
-    trace of this workload's bench (profiles/<tag>_<workload>_kernel_stats.csv: rocprofv3
-    --kernel-trace --stats of the command the driver runs, tools/prof_bench.sh), the
-    profile-side check of the HIP-event time, or (None, None)."""
+    trace of this workload's bench (rocprofv3 --kernel-trace --stats of the command the
+    driver runs, tools/prof_bench.sh): over the timed steps' launches
+    (profiles/<tag>_<workload>_kernel_stats_timed.csv) when there is one, else over the
+    whole trace (<tag>_<workload>_kernel_stats.csv) -- the profile-side check of the
+    HIP-event time -- or (None, None)."""
     import csv
-    files = newest_profiles(f"*_{workload}_kernel_stats.csv")
+    # the timed steps' launches only (tools/prof_collect.py) when committed: the trace's
+    # later legs (TrackLocalMap, host-fed) run the same kernels beside other work
+    files = newest_profiles(f"*_{workload}_kernel_stats_timed.csv") or newest_profiles(f"*_{workload}_kernel_stats.csv")
     if not files:
         return None, None
     ks = {}

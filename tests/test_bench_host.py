@@ -141,3 +141,48 @@ def test_h3_flip_count_runs(oracle):
     r = h3_flip_count.count_flips(synth.frames(3, first_seed=90), threads=3)
     assert r["keypoints_identical_all_frames"] and r["keypoints"] > 2000
     assert r["descriptors_differing"] <= r["keypoints"] // 100
+
+
+def test_rocprof_mean_prefers_the_timed_steps(tmp_path, monkeypatch):
+    """tools/prof_collect.py's statistics over the timed steps' launches win over the
+    whole trace's (whose later legs run the kernels beside other work)."""
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    hdr = '"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"\n'
+    (prof / "r03g_tum5k_kernel_stats.csv").write_text(hdr + '"orbx::k_pyramid<true>(x)",150,1,408000.0,1,1,1,1\n')
+    (prof / "r03g_tum5k_kernel_stats_timed.csv").write_text(hdr + '"orbx::k_pyramid<true>(x)",40,1,587000.0,1,1,1,1\n')
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    ms, src = bench.rocprof_mean_ms("pyramid", "tum5k")
+    assert src == "r03g_tum5k_kernel_stats_timed.csv" and abs(ms - 0.587) < 1e-9
+
+
+def test_prof_collect_timed_window(tmp_path):
+    """The timed steps are the first leg's last lanes x steps pyramid launches; kernels
+    from the first of them up to the next leg's first pyramid launch are counted."""
+    import csv
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("prof_collect", ROOT / "tools" / "prof_collect.py")
+    pc = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(pc)
+    rows, t = [], 0
+    def add(name, dur):
+        nonlocal t
+        rows.append({"Start_Timestamp": t, "End_Timestamp": t + dur, "Kernel_Name": name})
+        t += dur
+    for step in range(6):          # leg 1: 2 warmup + 4 timed steps, 2 lanes
+        for lane in range(2):
+            add("void orbx::k_pyramid<true>(a)", 100 if step >= 2 else 999)
+            add("orbx::k_describe(a)", 50)
+    t += 50_000_000                # the next leg starts 50 ms later
+    for step in range(3):
+        add("void orbx::k_pyramid<true>(a)", 7777)
+    trace = tmp_path / "trace.csv"
+    with open(trace, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Start_Timestamp", "End_Timestamp", "Kernel_Name"])
+        w.writeheader()
+        w.writerows(rows)
+    out = tmp_path / "timed.csv"
+    pc.timed_stats(str(trace), 4, out)
+    got = {r["Name"]: (int(r["Calls"]), float(r["AverageNs"])) for r in csv.DictReader(open(out))}
+    assert got["void orbx::k_pyramid<true>(a)"] == (8, 100.0)
+    assert got["orbx::k_describe(a)"] == (8, 50.0)
