@@ -144,11 +144,14 @@ __global__ __launch_bounds__(256) ORBX_PZ_ATTR void k_pyramid(const uint8_t* __r
                                                  int vec4, uint8_t* __restrict__ pyr, long long fb,
                                                  const LevelGeom* __restrict__ lv, int L,
                                                  const int16_t* __restrict__ rtab, int pz_off, int tiles_pf,
-                                                 int nframes, int lds_a) {
+                                                 int nframes, int lds_a, int* __restrict__ status) {
     extern __shared__ __align__(16) uint8_t s_pz[];
     int f, tile;
     xcd_frame_block(tiles_pf, nframes, f, tile);
     const int tid = threadIdx.x;
+    // the frame's status word starts clean here (k_octree ORs into it later on this stream):
+    // no separate memset launch ahead of every extraction
+    if (tile == 0 && tid == 0) status[f] = 0;
     const int16_t* R = rtab + pz_off + (size_t)tile * L * 8;
     uint8_t* const frame = pyr + (size_t)f * fb;
     // LDS rows of a level hold its needed columns widened to whole quads, [x0 & ~3, ...)
@@ -1743,7 +1746,6 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     const long long fb = plan.pyr_frame_bytes;
     const int ncells = (int)plan.cells.size();
     if (ev) (void)hipEventRecord(ev[0], stream);
-    (void)hipMemsetAsync(db.status, 0, sizeof(int) * (size_t)batch, stream);
     {
         const int vec4 = ((uintptr_t)d_imgs % 4 == 0) && (stride % 4 == 0) && (frame_pitch % 4 == 0);
         const size_t lds = (size_t)plan.pz_lds_a + plan.pz_lds_b;
@@ -1753,7 +1755,8 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
             if (e != hipSuccess) return e;
         }
         hipLaunchKernelGGL(kern, dim3(plan.pz_tiles * batch), dim3(256), lds, stream, d_imgs, frame_pitch, stride,
-                           vec4, db.pyr, fb, db.lv, L, db.rtab, plan.pz_off, plan.pz_tiles, batch, plan.pz_lds_a);
+                           vec4, db.pyr, fb, db.lv, L, db.rtab, plan.pz_off, plan.pz_tiles, batch, plan.pz_lds_a,
+                           db.status);
     }
     if (ev) (void)hipEventRecord(ev[1], stream);
     if (stage_ev && stage_after == 1) (void)hipEventRecord(stage_ev, stream);
