@@ -1521,6 +1521,13 @@ __device__ __forceinline__ void desc_level_of(const DescLevel* s, int L, int slo
 // save (configs[4] 100.6-100.9k -> 94.1-95.1k; capping them by LDS gives both back):
 // register staging above this many slots.
 constexpr int kDescGldsMaxSlots = 3000;
+#ifndef ORBX_DESC_DMA
+// the LDS-DMA form below kDescGldsMaxSlots: 1 = 16-byte pieces into 48-byte rows (five
+// workgroups a CU), 2 = 4-byte pieces into 40-byte rows (24.7 KB, six a CU: configs[1]
+// pipelined 222.3-224.0k -> 224.5-225.0k frames/s over three interleaved pairs, alone
+// 0.209 -> 0.218 ms; KITTI unchanged)
+#define ORBX_DESC_DMA 2
+#endif
 
 // Four kept keypoint slots per wave (one per 16-lane quarter): IC_Angle on the level
 // (cc:59-106), rBRIEF on the blurred level (cc:118-172), coordinate scaling
@@ -1537,14 +1544,14 @@ constexpr int kDescGldsMaxSlots = 3000;
 //   The steered-BRIEF patch of the blurred level, rows y-18..y+18 (|rotated pattern
 //   point| <= 13*sqrt(2) < 18.5), 44 bytes from (x-18) & ~3, is staged in LDS as 111
 //   16-byte chunks (48-byte rows); all global loads are issued together, one round of
-//   latency.  GLDS: the chunks go straight to LDS (global_load_lds_dwordx4, no VGPR
-//   destinations: 76 instead of 102 VGPRs, five waves per SIMD instead of four); else
-//   through registers, seven chunks per lane.  Keypoints lie in [19, w-20] x [19, h-20] of their level, so
+//   latency.  STAGE 1 / 2: the patch goes straight to LDS (global_load_lds_dwordx4 /
+//   _dword, no VGPR destinations: 76-78 instead of 102 VGPRs, five / six waves per SIMD
+//   instead of four); STAGE 0: through registers, seven chunks per lane.  Keypoints lie in [19, w-20] x [19, h-20] of their level, so
 //   every row exists; a row's last dword may reach 6 bytes past the level width (inside
 //   the pitch, or the buffers' slack for the very last row).
 //   A lane samples 16 of the 256 pairs (ql, 16 + ql, ..., 240 + ql); each pair step's
 //   ballot carries 16 descriptor bits per keypoint.
-template <bool GLDS>
+template <int STAGE>  // 0: registers, 1: 16-byte LDS-DMA, 2: 4-byte LDS-DMA into 40-byte rows
 __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ pyr,
                                                    const uint8_t* __restrict__ blur, long long fb,
                                                    const LevelGeom* __restrict__ lv, int L,
@@ -1552,7 +1559,10 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
                                                    const int* __restrict__ kept_count,
                                                    orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                    int cap, int* __restrict__ n_out, int nframes) {
-    __shared__ __align__(16) uint32_t s_bpatch[16][37 * 12];  // BRIEF patches, 48-byte rows
+    // BRIEF patches: 37 rows of 48 bytes (16-byte chunks), or of 40 bytes -- the 37
+    // columns x-18..x+18 from (x-18) & ~3 -- for the 4-byte DMA (six workgroups a CU)
+    constexpr int kPP = STAGE == 2 ? 40 : 48;
+    __shared__ __align__(16) uint32_t s_bpatch[16][37 * kPP / 4];
     __shared__ DescLevel s_lv[kMaxLevels];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int qt = lane >> 4, ql = lane & 15;
@@ -1596,7 +1606,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
         const uint4 r0 = *(const uint4*)prow2, r1 = *(const uint4*)(prow2 + 16);
         const uint32_t r2 = *(const uint32_t*)(prow2 + 32);
         const uint8_t* bpatch = bframe + (uint32_t)(g.off + (long long)(y - 18) * pitch + xb);
-        if constexpr (GLDS) {
+        if constexpr (STAGE == 1) {
         // the four BRIEF patches go straight to LDS (global_load_lds_dwordx4: no VGPR
         // destinations, so more waves fit a SIMD): patch by patch, the whole wave loads
         // its 111 chunks (lane L chunks L and 64 + L), from the patch base of quarter q
@@ -1623,8 +1633,30 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
             }
         }
         }
+        if constexpr (STAGE == 2) {
+            // 4-byte pieces: patch q's 370 dwords (37 rows x 10), lane L dword L + 64 j
+            const uint64_t mybase = (uint64_t)(uintptr_t)bpatch;
+            uint8_t* const wbp = (uint8_t*)s_bpatch[wave * 4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)mybase, 16 * q);
+                const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(mybase >> 32), 16 * q);
+                const int sp = __builtin_amdgcn_readlane(pitch, 16 * q);
+                const uint8_t* qb = (const uint8_t*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+#pragma unroll
+                for (int jj = 0; jj < 6; jj++) {
+                    const int c = 64 * jj + lane;
+                    if (c < 370) {
+                        const int row = (c * 205) >> 11;  // c / 10 for c < 370
+                        __builtin_amdgcn_global_load_lds((const void*)(qb + (uint32_t)(row * sp + 4 * (c - 10 * row))),
+                                                         (__attribute__((address_space(3))) void*)(wbp + q * (int)sizeof(s_bpatch[0]) + 256 * jj),
+                                                         4, 0, 0);
+                    }
+                }
+            }
+        }
         uint4 bch[7];
-        if constexpr (!GLDS) {
+        if constexpr (STAGE == 0) {
 #pragma unroll
             for (int j = 0; j < 7; j++) {
                 const int c = min(ql + 16 * j, 110), row = (c * 171) >> 9;
@@ -1653,7 +1685,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
         const bool row2_ok = ql < 15;
         m10 = ((int)ws1 - 15 * (int)cs1) + (row2_ok ? (int)ws2 - 15 * (int)cs2 : 0);
         m01 = v1 * (int)cs1 + (row2_ok ? v2 * (int)cs2 : 0);
-        if constexpr (GLDS) {
+        if constexpr (STAGE != 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA pieces have landed
         } else {
 #pragma unroll
@@ -1678,14 +1710,14 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     // even, like rint): 0x4B400000 + cvRound(v).  The row offset is one v_mul_u32_u24,
     // which reads only the low 24 bits (0x400000 + cvRound(y)); the constants come off
     // the patch centre once.
-    const uint32_t center = (uint32_t)(18 * 48 + 18 + (x - 18 - xb)) - (0x400000u * 48u + 0x4B400000u);
+    const uint32_t center = (uint32_t)(18 * kPP + 18 + (x - 18 - xb)) - (0x400000u * (uint32_t)kPP + 0x4B400000u);
     const float kRound = 12582912.0f;  // 1.5 * 2^23
     // the offsets fused as g++ -O3 -march=native builds the reference (hazard H4: GCC
     // contracts C++ and fuses the first product, fma(x, b, y*a), fma(x, a, -(y*b)))
     auto sample = [&](float px, float py) -> int {
         const uint32_t ry = __float_as_uint(fmaf(px, b, py * a) + kRound);
         const uint32_t rx = __float_as_uint(fmaf(px, a, -(py * b)) + kRound);
-        return bp[center + __umul24(ry, 48u) + rx];
+        return bp[center + __umul24(ry, (uint32_t)kPP) + rx];
     };
     auto pair_test = [&](int q) -> bool {
         const float x0 = (float)(int8_t)(q & 0xff), y0 = (float)(int8_t)((q >> 8) & 0xff);
@@ -1797,7 +1829,7 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     if (stage_ev && stage_after == 4) (void)hipEventRecord(stage_ev, stream);
     {
         dim3 grid(((plan.kept_per_frame + 15) / 16) * batch);
-        auto kern = plan.kept_per_frame <= kDescGldsMaxSlots ? k_describe<true> : k_describe<false>;
+        auto kern = plan.kept_per_frame <= kDescGldsMaxSlots ? k_describe<ORBX_DESC_DMA> : k_describe<0>;
         hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, db.pyr, db.blur, fb, db.lv, L, db.kept,
                            plan.kept_per_frame, db.kept_count, (orbx_keypoint*)kps, desc, cap, n_per_frame, batch);
     }
