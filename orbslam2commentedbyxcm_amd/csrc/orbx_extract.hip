@@ -1779,16 +1779,26 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     const int ncells = (int)plan.cells.size();
     if (ev) (void)hipEventRecord(ev[0], stream);
     {
-        const int vec4 = ((uintptr_t)d_imgs % 4 == 0) && (stride % 4 == 0) && (frame_pitch % 4 == 0);
-        const size_t lds = (size_t)plan.pz_lds_a + plan.pz_lds_b;
+        // one launch per pyramid segment (orbx_geometry.h): the first reads the input
+        // frames, a later one its input level from the pyramid the previous one wrote
         auto kern = plan.pz_win ? k_pyramid<true> : k_pyramid<false>;
-        if (lds > 64 * 1024) {
-            hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        size_t lds_max = 0;
+        for (int s = 0; s < plan.pz_nseg; s++)
+            lds_max = std::max(lds_max, (size_t)plan.pz[s].lds_a + plan.pz[s].lds_b);
+        if (lds_max > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(kern, dim3(plan.pz_tiles * batch), dim3(256), lds, stream, d_imgs, frame_pitch, stride,
-                           vec4, db.pyr, fb, db.lv, L, db.rtab, plan.pz_off, plan.pz_tiles, batch, plan.pz_lds_a,
-                           db.status);
+        for (int s = 0; s < plan.pz_nseg; s++) {
+            const PzSeg& sg = plan.pz[s];
+            const LevelGeom& g0 = plan.lv[sg.l0];
+            const uint8_t* in = s == 0 ? d_imgs : db.pyr + g0.off;
+            const size_t fp = s == 0 ? frame_pitch : (size_t)fb, st = s == 0 ? stride : (size_t)g0.pitch;
+            const int vec4 = ((uintptr_t)in % 4 == 0) && (st % 4 == 0) && (fp % 4 == 0);
+            hipLaunchKernelGGL(kern, dim3(sg.tiles * batch), dim3(256), (size_t)sg.lds_a + sg.lds_b, stream, in, fp, st,
+                               vec4, db.pyr, fb, db.lv + sg.l0, sg.nl, db.rtab, sg.off, sg.tiles, batch, sg.lds_a,
+                               db.status);
+        }
     }
     if (ev) (void)hipEventRecord(ev[1], stream);
     if (stage_ev && stage_after == 1) (void)hipEventRecord(stage_ev, stream);

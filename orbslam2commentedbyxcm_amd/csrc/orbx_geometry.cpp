@@ -110,49 +110,47 @@ static void resize_tables(int sw, int sh, int dw, int dh, int16_t* xtab, int16_t
 // resize tables' source footprints (the tables are monotone, so a range of columns
 // maps to [t(first).s0, t(last).s1]): the halo is 0 on the left / top and about
 // 1 + 1.2 * (halo of the level above) on the right / bottom.
-static bool pyramid_tiles(Plan& plan) {
-    const int L = plan.L;
-    // ORBX_PZ_TILE=WxH overrides the level-0 tile size (tuning; the output is the same)
-    int tw = kPzTW, th = kPzTH;
-    if (const char* e = std::getenv("ORBX_PZ_TILE")) {
-        int a = 0, b = 0;
-        if (std::sscanf(e, "%dx%d", &a, &b) == 2 && a >= 16 && b >= 16) { tw = a; th = b; }
-    }
-    const int nx = (plan.W + tw - 1) / tw, ny = (plan.H + th - 1) / th;
-    plan.pz_nx = nx;
-    plan.pz_ny = ny;
-    plan.pz_tiles = nx * ny;
-    plan.pz_off = (int)plan.rtab.size();
-    plan.rtab.resize(plan.rtab.size() + (size_t)nx * ny * L * 8);
-    // owned boundaries per level: bx[l][0..nx], by[l][0..ny]
-    std::vector<std::vector<int>> bx(L, std::vector<int>(nx + 1)), by(L, std::vector<int>(ny + 1));
-    for (int j = 0; j <= nx; j++) bx[0][j] = (int)(((long long)j * plan.W) / nx);
-    for (int i = 0; i <= ny; i++) by[0][i] = (int)(((long long)i * plan.H) / ny);
-    for (int l = 1; l < L; l++) {
-        const LevelGeom& g = plan.lv[l];
+// One segment: levels s.l0 .. s.l0 + s.nl - 1, tiled over level s.l0 (owned by the
+// segment only when s.l0 == 0: a later segment's input level is already in HBM).
+static bool pyramid_segment(Plan& plan, PzSeg& s, int tw, int th) {
+    const int l0 = s.l0, n = s.nl;
+    const LevelGeom& g0 = plan.lv[l0];
+    const int nx = (g0.w + tw - 1) / tw, ny = (g0.h + th - 1) / th;
+    s.nx = nx;
+    s.ny = ny;
+    s.tiles = nx * ny;
+    s.off = (int)plan.rtab.size();
+    plan.rtab.resize(plan.rtab.size() + (size_t)nx * ny * n * 8);
+    // owned boundaries per segment level: bx[k][0..nx], by[k][0..ny] (level l0 + k)
+    std::vector<std::vector<int>> bx(n, std::vector<int>(nx + 1)), by(n, std::vector<int>(ny + 1));
+    for (int j = 0; j <= nx; j++) bx[0][j] = (int)(((long long)j * g0.w) / nx);
+    for (int i = 0; i <= ny; i++) by[0][i] = (int)(((long long)i * g0.h) / ny);
+    for (int k = 1; k < n; k++) {
+        const LevelGeom& g = plan.lv[l0 + k];
         const int16_t* xt = plan.rtab.data() + g.xtab_off;
         const int16_t* yt = plan.rtab.data() + g.ytab_off;
         for (int j = 0; j <= nx; j++) {
-            int c = j == 0 ? 0 : bx[l][j - 1];
-            while (c < g.w && (j == nx || xt[4 * c] < bx[l - 1][j])) c++;
-            bx[l][j] = c;
+            int c = j == 0 ? 0 : bx[k][j - 1];
+            while (c < g.w && (j == nx || xt[4 * c] < bx[k - 1][j])) c++;
+            bx[k][j] = c;
         }
         for (int i = 0; i <= ny; i++) {
-            int r = i == 0 ? 0 : by[l][i - 1];
-            while (r < g.h && (i == ny || yt[4 * r] < by[l - 1][i])) r++;
-            by[l][i] = r;
+            int r = i == 0 ? 0 : by[k][i - 1];
+            while (r < g.h && (i == ny || yt[4 * r] < by[k - 1][i])) r++;
+            by[k][i] = r;
         }
     }
     for (int ty = 0; ty < ny; ty++)
         for (int tx = 0; tx < nx; tx++) {
-            int16_t* R = plan.rtab.data() + plan.pz_off + (size_t)(ty * nx + tx) * L * 8;
+            int16_t* R = plan.rtab.data() + s.off + (size_t)(ty * nx + tx) * n * 8;
             int nx0 = 0, ny0 = 0, nx1 = 0, ny1 = 0;  // needed rectangle of level l + 1
-            for (int l = L - 1; l >= 0; l--) {
-                const LevelGeom& g = plan.lv[l];
-                const int ox0 = bx[l][tx], ox1 = bx[l][tx + 1], oy0 = by[l][ty], oy1 = by[l][ty + 1];
+            for (int k = n - 1; k >= 0; k--) {
+                const int l = l0 + k;
+                int ox0 = bx[k][tx], ox1 = bx[k][tx + 1], oy0 = by[k][ty], oy1 = by[k][ty + 1];
+                if (k == 0 && l0 > 0) ox0 = ox1 = oy0 = oy1 = 0;  // the input level: not owned here
                 int x0 = ox0, x1 = ox1, y0 = oy0, y1 = oy1;
                 bool any = ox1 > ox0 && oy1 > oy0;
-                if (l + 1 < L && nx1 > nx0 && ny1 > ny0) {
+                if (k + 1 < n && nx1 > nx0 && ny1 > ny0) {
                     const LevelGeom& u = plan.lv[l + 1];
                     const int16_t* xt = plan.rtab.data() + u.xtab_off;
                     const int16_t* yt = plan.rtab.data() + u.ytab_off;
@@ -169,17 +167,44 @@ static bool pyramid_tiles(Plan& plan) {
                 if (!any) x0 = x1 = y0 = y1 = 0;
                 const int16_t r[8] = {(int16_t)x0, (int16_t)y0, (int16_t)x1, (int16_t)y1,
                                       (int16_t)ox0, (int16_t)oy0, (int16_t)ox1, (int16_t)oy1};
-                std::memcpy(R + 8 * l, r, sizeof(r));
+                std::memcpy(R + 8 * k, r, sizeof(r));
                 // LDS holds the needed columns widened to whole 4-byte quads
                 // (+ 16: k_pyramid<true> reads a row's source window as three dwords, which
                 // can reach 8 bytes past the last row's last quad)
                 const int bytes = any ? 4 * ((x1 - (x0 & ~3) + 3) / 4) * (y1 - y0) : 0;
-                int& buf = (l & 1) ? plan.pz_lds_b : plan.pz_lds_a;
+                int& buf = (k & 1) ? s.lds_b : s.lds_a;
                 buf = std::max(buf, ((bytes + 15) & ~15) + 16);
                 nx0 = x0; nx1 = x1; ny0 = y0; ny1 = y1;
             }
         }
-    if (plan.pz_lds_a + plan.pz_lds_b > kPzMaxLds) { plan.why = "pyramid tile exceeds LDS (scale factor too large)"; return false; }
+    if (s.lds_a + s.lds_b > kPzMaxLds) { plan.why = "pyramid tile exceeds LDS (scale factor too large)"; return false; }
+    return true;
+}
+
+static bool pyramid_tiles(Plan& plan) {
+    const int L = plan.L;
+    // ORBX_PZ_TILE=WxH / ORBX_PZ_TILE2=WxH override the first / later segments' tile size,
+    // ORBX_PZ_SEG=n the levels per segment (0: one segment); tuning, the output is the same
+    int tw = kPzTW, th = kPzTH, tw2 = kPzTW2, th2 = kPzTH2, seg = kPzSegLevels;
+    auto tile_env = [](const char* name, int& w, int& h) {
+        int a = 0, b = 0;
+        if (const char* e = std::getenv(name))
+            if (std::sscanf(e, "%dx%d", &a, &b) == 2 && a >= 16 && b >= 16) { w = a; h = b; }
+    };
+    tile_env("ORBX_PZ_TILE", tw, th);
+    tile_env("ORBX_PZ_TILE2", tw2, th2);
+    if (const char* e = std::getenv("ORBX_PZ_SEG")) seg = std::atoi(e);
+    if (seg < 2 || seg > L) seg = L;
+    plan.pz_nseg = 0;
+    for (int l0 = 0;;) {
+        PzSeg& s = plan.pz[plan.pz_nseg++];
+        s = PzSeg{};
+        s.l0 = l0;
+        s.nl = std::min(seg, L - l0);
+        if (!pyramid_segment(plan, s, l0 == 0 ? tw : tw2, l0 == 0 ? th : th2)) return false;
+        if (l0 + s.nl >= L) break;
+        l0 += s.nl - 1;
+    }
     // k_pyramid<true> needs the source bytes of any 4 consecutive output columns (sx0 of the
     // first .. sx1 of the last) within 8 bytes: scale factors up to about 2
     // (ORBX_PZ_BYTE=1 forces the byte-read form: tuning, the output is the same)

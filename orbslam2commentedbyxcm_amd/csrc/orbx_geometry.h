@@ -84,8 +84,25 @@ struct CellGeom {
 // plus the source footprint of its needed rectangle at level l + 1, so levels chain
 // inside LDS with a small recomputed right / bottom halo.  Per (tile, level) the table
 // holds 8 int16: needed x0, y0, x1, y1 and owned x0, y0, x1, y1 (ends exclusive).
+// Deep pyramids are built in segments of at most kPzSegLevels levels, one launch each:
+// a segment after the first takes its input level (the previous segment's last, already
+// in HBM) as its "level 0" and owns none of it.  Each segment's halo then grows over at
+// most kPzSegLevels - 1 resizes instead of L - 1 (12 levels: ~32 px of recomputed
+// right / bottom halo per 128 x 96 level-0 tile and 35 KB of LDS, against ~13 px and
+// 27 KB for 8), at the price of re-reading one small level.  Later segments tile their
+// input level by kPzTW2 x kPzTH2.
 constexpr int kPzTW = 128, kPzTH = 96;
+constexpr int kPzTW2 = 64, kPzTH2 = 48;
+constexpr int kPzSegLevels = 8;
+constexpr int kPzMaxSegs = kMaxLevels;
 constexpr int kPzMaxLds = 150 * 1024;
+
+struct PzSeg {
+    int l0 = 0, nl = 0;           // input level and level count (l0 .. l0 + nl - 1)
+    int nx = 0, ny = 0, tiles = 0;  // tile grid over level l0
+    int off = 0;                  // offset (int16 units) of the tile rectangles in rtab
+    int lds_a = 0, lds_b = 0;     // LDS ping / pong buffers (even / odd levels of the segment), bytes
+};
 
 struct Plan {
     int W = 0, H = 0, L = 0;
@@ -98,10 +115,8 @@ struct Plan {
     int keys_per_frame = 0;         // candidate key capacity per frame
     int kept_per_frame = 0;         // sum of ncap
     int tiles_total = 0;            // blur tiles per frame
-    int pz_tiles = 0;               // k_pyramid tiles per frame (pz_nx x pz_ny)
-    int pz_nx = 0, pz_ny = 0;
-    int pz_off = 0;                 // offset (int16 units) of the tile rectangles in rtab
-    int pz_lds_a = 0, pz_lds_b = 0; // LDS ping / pong buffers (even / odd levels), bytes
+    int pz_nseg = 0;                // k_pyramid segments (launches)
+    PzSeg pz[kPzMaxSegs];
     bool pz_win = false;            // k_pyramid<true>: every 4 columns' resize taps span <= 8 source bytes
     int fc_wr = 0, fc_wc = 0;       // largest FAST detection window (rows, cols)
     int max_ncap = 0;
