@@ -98,15 +98,25 @@ STAGE_KERNELS = {"pyramid": ["orbx::k_pyramid"], "score_blur": ["orbx::k_level_t
                  "match": ["orbx::k_seq_build", "orbx::k_proj_search", "orbx::k_seq_commit"]}
 
 
-def _stage_sum(ks: dict, stage: str, field: str):
+def _stage_sum(ks: dict, stage: str, field: str, count: str = None):
     """Sum of `field` over the kernels of `stage` (a name matches its STAGE_KERNELS entry
-    or that entry plus template arguments); None unless every entry matches one."""
+    or that entry plus template arguments); None unless every entry matches one.
+    count: the per-kernel launch-count field; an extraction stage's per-launch value is
+    then scaled by its launches per extraction (k_level_tiles runs once per extraction;
+    k_pyramid once per pyramid segment: 2 at configs[4]'s 12 levels)."""
+    def per_ex(k):
+        if not count or stage == "match":
+            return 1
+        anchor = [v for n, v in ks.items() if n == "orbx::k_level_tiles"]
+        if not anchor or not anchor[0].get(count) or not ks[k].get(count):
+            return 1
+        return max(1, round(ks[k][count] / anchor[0][count]))
     tot = 0
     for name in STAGE_KERNELS.get(stage, []):
         hits = [k for k in ks if k == name or k.startswith(name + "<")]
         if not hits:
             return None
-        tot += sum(ks[k][field] for k in hits)
+        tot += sum(ks[k][field] * per_ex(k) for k in hits)
     return tot if STAGE_KERNELS.get(stage) else None
 
 
@@ -134,8 +144,8 @@ def rocprof_mean_ms(stage: str, workload: str):
     ks = {}
     for r in csv.DictReader(open(files[-1])):
         name = r["Name"].split("(")[0].replace("void ", "")
-        ks[name] = {"avg_ns": float(r["AverageNs"])}
-    tot = _stage_sum(ks, stage, "avg_ns")
+        ks[name] = {"avg_ns": float(r["AverageNs"]), "calls": int(r["Calls"])}
+    tot = _stage_sum(ks, stage, "avg_ns", "calls")
     return (None if tot is None else tot * 1e-6), files[-1].name
 
 
@@ -172,7 +182,7 @@ def pmc_traffic(stage: str, workload: str = "tum"):
     if not files:
         return None, None
     ks = json.loads(files[-1].read_text())["kernels"]
-    tot = _stage_sum(ks, stage, "traffic_bytes")
+    tot = _stage_sum(ks, stage, "traffic_bytes", "dispatches")
     return (None if tot is None else int(tot)), files[-1].name
 
 

@@ -186,3 +186,53 @@ def test_prof_collect_timed_window(tmp_path):
     got = {r["Name"]: (int(r["Calls"]), float(r["AverageNs"])) for r in csv.DictReader(open(out))}
     assert got["void orbx::k_pyramid<true>(a)"] == (8, 100.0)
     assert got["orbx::k_describe(a)"] == (8, 50.0)
+
+
+def test_prof_collect_timed_window_pyramid_segments(tmp_path):
+    """A 12-level pyramid is two k_pyramid launches per extraction (one per segment): the
+    timed window still spans the last `steps` steps, found from the k_pyramid /
+    k_level_tiles launch ratio."""
+    import csv
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("prof_collect", ROOT / "tools" / "prof_collect.py")
+    pc = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(pc)
+    rows, t = [], 0
+
+    def add(name, dur):
+        nonlocal t
+        rows.append({"Start_Timestamp": t, "End_Timestamp": t + dur, "Kernel_Name": name})
+        t += dur
+    for step in range(6):          # 2 warmup + 4 timed steps, 2 lanes, 2 segments
+        for lane in range(2):
+            add("void orbx::k_pyramid<true>(a)", 100 if step >= 2 else 999)
+            add("void orbx::k_pyramid<true>(a)", 20 if step >= 2 else 999)
+            add("orbx::k_level_tiles(a)", 70 if step >= 2 else 999)
+    trace = tmp_path / "trace.csv"
+    with open(trace, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Start_Timestamp", "End_Timestamp", "Kernel_Name"])
+        w.writeheader()
+        w.writerows(rows)
+    out = tmp_path / "timed.csv"
+    pc.timed_stats(str(trace), 4, out)
+    got = {r["Name"]: (int(r["Calls"]), float(r["AverageNs"])) for r in csv.DictReader(open(out))}
+    assert got["void orbx::k_pyramid<true>(a)"] == (16, 60.0)
+    assert got["orbx::k_level_tiles(a)"] == (8, 70.0)
+
+
+def test_stage_sum_counts_pyramid_segments(tmp_path, monkeypatch):
+    """The pyramid stage per extraction is k_pyramid's mean launch x its launches per
+    extraction (k_pyramid calls / k_level_tiles calls), in the trace and PMC summaries."""
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    hdr = '"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"\n'
+    (prof / "r09_tum5k_kernel_stats_timed.csv").write_text(
+        hdr + '"void orbx::k_pyramid<true>(x)",80,1,300000.0,1,1,1,1\n"orbx::k_level_tiles(x)",40,1,1,1,1,1,1\n')
+    (prof / "r09_tum5k_pmc_traffic.json").write_text(json.dumps({"kernels": {
+        "orbx::k_pyramid<true>": {"traffic_bytes": 1000, "dispatches": 6},
+        "orbx::k_level_tiles": {"traffic_bytes": 5, "dispatches": 3}}}))
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    ms, _ = bench.rocprof_mean_ms("pyramid", "tum5k")
+    assert abs(ms - 0.6) < 1e-9
+    assert bench.pmc_traffic("pyramid", "tum5k")[0] == 2000
+    assert bench.pmc_traffic("score_blur", "tum5k")[0] == 5

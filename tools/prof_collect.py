@@ -19,17 +19,24 @@ ROOT = Path(__file__).resolve().parents[1]
 
 def timed_stats(trace_csv: str, steps: int, out: Path, lanes: int = 2, gap_ms: float = 5.0) -> None:
     """Per-kernel statistics over the timed steps of the bench's first leg: every step
-    launches k_pyramid `lanes` times (two lanes, or the left and right extractors); that
+    launches k_pyramid `lanes` x segments times (two lanes, or the left and right
+    extractors; one launch per pyramid segment); that
     leg ends at the first pause of more than gap_ms between pyramid launches after its
-    last 2 * steps launches could have begun (or at the trace's end), and its timed steps
-    are its last lanes * steps pyramid launches.  Kernels that start from the first of
+    last launches could have begun (or at the trace's end), and its timed steps are its
+    last lanes * segments * steps pyramid launches.  Kernels that start from the first of
     them up to the next leg's first pyramid launch are counted."""
     ev = []
     for r in csv.DictReader(open(trace_csv)):
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     ev.sort()
-    pyr = [e for e in ev if e[2].split("(")[0].replace("void ", "").startswith("orbx::k_pyramid")]
-    n = lanes * steps
+    def is_(e, k):
+        return e[2].split("(")[0].replace("void ", "").startswith(k)
+    pyr = [e for e in ev if is_(e, "orbx::k_pyramid")]
+    # a deep pyramid is built in segments, one k_pyramid launch each (configs[4]'s 12
+    # levels: 2): launches per extraction = k_pyramid / k_level_tiles launches (one each)
+    nlt = sum(1 for e in ev if is_(e, "orbx::k_level_tiles"))
+    nseg = max(1, round(len(pyr) / nlt)) if nlt else 1
+    n = lanes * nseg * steps
     if len(pyr) < n:
         return
     end = len(pyr) - 1
