@@ -254,7 +254,7 @@ namespace {
 // Upload one frame view + queries and run k_proj_search for a single problem.
 int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const std::vector<ProjQuery>& qs,
              const std::vector<uint8_t>& qdesc, const orbx_mappoints* mps, const ProjParams& base_params,
-             int* nmatches) {
+             int* nmatches, int replay_rt = 0) {
     const int n = f->n, nq = (int)qs.size();
     if (nq == 0 || n == 0) {
         if (nmatches) *nmatches = 0;
@@ -351,8 +351,10 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
     if (mapped) {
         // inputs copied in by k_stage_copy (no DMA), results written to mapped memory
         const size_t staged = m->arena.take_staged();
-        HIP_TRY(launch_seq_split(d_prob, 1, P, d_grid, gcap, d_scr, d_off, s, 0, 0, m->arena.host_dev, m->arena.base,
-                                 staged));
+        // replay width: the row's (replay_rt) unless ORBX_REPLAY_THREADS overrides it
+        static const bool rt_env = getenv("ORBX_REPLAY_THREADS") != nullptr;
+        HIP_TRY(launch_seq_split(d_prob, 1, P, d_grid, gcap, d_scr, d_off, s, 0, rt_env ? 0 : replay_rt,
+                                 m->arena.host_dev, m->arena.base, staged));
     } else {
         HIP_TRY(m->arena.flush(s));
         HIP_TRY(launch_proj_search(d_prob, 1, P, d_scr, d_off, n, nq, s));
@@ -582,7 +584,9 @@ int orbx_search_by_projection_keyframe(orbx_matcher* m, const orbx_frame_view* c
     P.accept_th = orb_dist;
     P.ratio_mode = 0;
     P.check_ori = m->check_ori;
-    return run_proj(m, cur, cur_mp, qs, qd, mps, P, nmatches);
+    // a 1024-thread replay: this row's conflict chains are short (r03 rows: 29 one-wave
+    // iterations against a12's 109), so a wider fixpoint finishes sooner
+    return run_proj(m, cur, cur_mp, qs, qd, mps, P, nmatches, 1024);
 }
 
 // ORBmatcher::SearchByProjection(KeyFrame*, cv::Mat Scw, const vector<MapPoint*>&,
@@ -651,7 +655,8 @@ int orbx_search_by_projection_sim3(orbx_matcher* m, const orbx_frame_view* kf, c
     P.accept_th = TH_LOW;
     P.ratio_mode = 0;
     P.check_ori = 0;
-    return run_proj(m, kf, matched, qs, qd, mps, P, nmatches);
+    // short conflict chains (accept <= TH_LOW; 17 one-wave iterations): 1024-thread replay
+    return run_proj(m, kf, matched, qs, qd, mps, P, nmatches, 1024);
 }
 
 // Batched SearchByProjection(CurrentFrame, LastFrame, th, bMono) over a device
