@@ -425,7 +425,7 @@ def main():
                           matcher_mode=None if "ORBX_MATCH_MODE" not in os.environ
                           else int(os.environ["ORBX_MATCH_MODE"]),
                           match_after_stage=int(os.environ.get("ORBX_MATCH_AFTER", "0")),
-                          lane_offset_stage=int(os.environ.get("ORBX_LANE_OFFSET", "2")),
+                          lane_offset_stage=int(os.environ["ORBX_LANE_OFFSET"]) if "ORBX_LANE_OFFSET" in os.environ else None,
                           match_cu_stride=int(os.environ.get("ORBX_MATCH_CUSTRIDE", "1")),
                           match_priority=int(os.environ.get("ORBX_MATCH_STREAM_PRIO", "0")))
     S = pl.S
@@ -628,6 +628,7 @@ def main():
                                    "against its predecessor" + ("" if match else " (match disabled)"),
                        "frames_per_gpu_step": B, "global_batch": B * world, "width": W, "height": H,
                        "parallelism": f"frame-sharded x{world}", "lanes_per_gpu": S,
+                       "lane_offset_stage": pl.lane_offset_stage,
                        "pipelined_match": pipeline,
                        "match_cu_stride": match_cu},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

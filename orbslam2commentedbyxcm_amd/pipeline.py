@@ -34,7 +34,7 @@ class SequencePipeline:
                  fy: float = 500.0, cx: float = 320.0, cy: float = 240.0, depth: float = 5.0, th: float = 15.0,
                  nnratio: float = 0.9, check_ori: bool = True, match_stream=None,
                  nbuf: int = 2, matcher_mode: int | None = None, match_after_stage: int = 0,
-                 lane_offset_stage: int = 2, match_cu_stride: int = 1,
+                 lane_offset_stage: int | None = None, match_cu_stride: int = 1,
                  match_priority: int = 0, on_matched=None, local_map: bool = False, local_window: int = 3,
                  local_th: float = 1.0):
         import torch
@@ -117,7 +117,14 @@ class SequencePipeline:
         # it, so the lanes run out of phase (one lane's latency-bound stages beside the
         # other's issue-bound ones) instead of in step.  Default 2 (after the blur + FAST
         # strength stage): 193.6-197.4k frames/s against 192.8-194.3k in step, extraction
-        # alone 216.5k against 210.8k (profiles/r02_l_lane_offset_ab.log)
+        # alone 216.5k against 210.8k (profiles/r02_l_lane_offset_ab.log).  None: 2, or 4
+        # (after the octree) for pyramids deeper than 8 levels, whose longer matcher runs
+        # best beside one lane's describe and the other's first stages (configs[4]
+        # 99.8-101.0k -> 105.7-106.0k frames/s; configs[1] with 4: 214.5-215.4k against
+        # 224.4-225.1k with 2; tools/g_r3zy.sh, tools/g_r3zz.sh)
+        if lane_offset_stage is None:
+            lane_offset_stage = 4 if int(params[2]) > 8 else 2
+        self.lane_offset_stage = int(lane_offset_stage)
         self.lane_ev = [e.set_stage_event(lane_offset_stage) for e in self.exs] \
             if (lane_offset_stage and not match_after_stage and self.S > 1) else None
         # on_matched(b): called right after a batch's matching is enqueued on self.ms and

@@ -39,7 +39,7 @@ def _run(B, lanes, pipelined, steps, seed=1000, matcher_mode=None, lane_offset=2
                          [(256, 2, True, 2, None, 2, 0), (16, 1, False, 1, None, 2, 0), (8, 2, True, 3, None, 2, 0),
                           (12, 2, False, 2, None, 2, 0), (256, 2, False, 1, None, 2, 0), (256, 2, True, 2, 2, 2, 0),
                           (13, 2, True, 3, 2, 2, 0), (256, 2, True, 2, 4, 0, 0), (24, 3, True, 3, 0, 1, 0),
-                          (16, 2, True, 3, None, 0, 2)])
+                          (16, 2, True, 3, None, 0, 2), (16, 2, True, 3, None, 4, 0)])
 def test_sequence_pipeline_matches_oracle(oracle, orbx_built, B, lanes, pipelined, steps, mode, offset, after):
     """Every frame and pair of the newest batch == the oracle, over matcher footprints
     (None = the default lean split), lanes in step (offset 0) or out of phase, and the
