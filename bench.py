@@ -429,6 +429,7 @@ def main():
                           match_cu_stride=int(os.environ.get("ORBX_MATCH_CUSTRIDE", "1")),
                           match_priority=int(os.environ.get("ORBX_MATCH_STREAM_PRIO", "0")))
     S = pl.S
+    lane_off = pl.lane_offset_stage
     d_frames = torch.from_numpy(frames_np).to(dev)
     d_T = torch.from_numpy(T).to(dev)
     torch.cuda.synchronize(dev)  # uploads on torch's stream finish before the extractor streams read them
@@ -628,7 +629,7 @@ def main():
                                    "against its predecessor" + ("" if match else " (match disabled)"),
                        "frames_per_gpu_step": B, "global_batch": B * world, "width": W, "height": H,
                        "parallelism": f"frame-sharded x{world}", "lanes_per_gpu": S,
-                       "lane_offset_stage": pl.lane_offset_stage,
+                       "lane_offset_stage": lane_off,
                        "pipelined_match": pipeline,
                        "match_cu_stride": match_cu},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
