@@ -34,6 +34,7 @@ import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
+SRC_ROOT = ROOT  # the sources source_hash() covers (ROOT may be redirected by tests)
 sys.path.insert(0, str(ROOT))
 
 # The pipelined step keeps three HIP streams busy at once (two extraction lanes and the
@@ -159,26 +160,60 @@ def dominant_stage(event_ms: dict, workload: str) -> str:
     return max(event_ms, key=event_ms.get)
 
 
-def pmc_valu(stage: str):
-    """VALU wave-instructions per launch of `stage` from the newest profiles/*_pmc_valu.json
-    (tools/pmc_valu.sh + tools/pmc_valu.py), or (None, None)."""
-    files = newest_profiles("*_pmc_valu.json")
+OTHER_WORKLOADS = ("_tum5k_", "_kitti_", "_euroc_")
+
+
+def workload_profiles(kind: str, workload: str):
+    """profiles/*_<kind> files of this workload's bench, oldest first: configs[1] ("tum")
+    files are tagged <tag>_tum_<kind> or carry no workload tag (older passes), the others
+    <tag>_<workload>_<kind>."""
+    if workload == "tum":
+        return [f for f in newest_profiles(f"*_{kind}") if not any(w in f.name for w in OTHER_WORKLOADS)]
+    return newest_profiles(f"*_{workload}_{kind}")
+
+
+def source_hash() -> str:
+    """Hash of the code a profile measures: the HIP / C++ sources of liborbx.so and the
+    C ABI header (file names and bytes).  Every bench line carries it, so a committed
+    profile (whose bench line records the hash it ran with) can be told stale."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = SRC_ROOT / "orbslam2commentedbyxcm_amd" / "csrc"
+    for f in sorted(list(csrc.iterdir()) + [SRC_ROOT / "include" / "orbx.h"]):
+        if f.is_file():
+            h.update(f.name.encode() + b"\0" + f.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def profile_hash(f: Path):
+    """The source_hash a committed profile summary was taken at (None: not recorded)."""
+    try:
+        if f.suffix == ".json":
+            return json.loads(f.read_text()).get("source_hash")
+        side = f.with_name(f.name.replace("_kernel_stats_timed.csv", "_prof_bench.json")
+                           .replace("_kernel_stats.csv", "_prof_bench.json"))
+        return json.loads(side.read_text()).get("source_hash") if side.exists() else None
+    except (OSError, ValueError):
+        return None
+
+
+def pmc_valu(stage: str, workload: str = "tum"):
+    """VALU wave-instructions per launch of `stage` from the newest VALU summary of this
+    workload's bench (profiles/<tag>_<workload>_pmc_valu.json, tools/pmc_valu.sh +
+    tools/pmc_valu.py), or (None, None)."""
+    files = workload_profiles("pmc_valu.json", workload)
     if not files:
         return None, None
     ks = json.loads(files[-1].read_text())["kernels"]
-    tot = _stage_sum(ks, stage, "sq_insts_valu")
+    tot = _stage_sum(ks, stage, "sq_insts_valu", "dispatches")
     return (None if tot is None else int(tot)), files[-1].name
 
 
 def pmc_traffic(stage: str, workload: str = "tum"):
     """HBM bytes per launch of `stage` from the newest committed PMC summary of this
     workload's bench (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from
-    separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes; configs[1] files carry no workload
-    tag, the others <tag>_<workload>_pmc_traffic.json), or (None, None)."""
-    files = newest_profiles(f"*_{workload}_pmc_traffic.json")
-    if workload == "tum":
-        files = [f for f in newest_profiles("*_pmc_traffic.json")
-                 if not any(w in f.name for w in ("_tum5k_", "_kitti_", "_euroc_"))]
+    separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes), or (None, None)."""
+    files = workload_profiles("pmc_traffic.json", workload)
     if not files:
         return None, None
     ks = json.loads(files[-1].read_text())["kernels"]
@@ -192,8 +227,14 @@ def profile_fields(dom: str, algorithmic_bytes: float, event_ms: float, workload
     HBM peak recomputed from that mean (the profile-side check of the HIP-event `frac`)."""
     traffic, traffic_src = pmc_traffic(dom, workload)
     prof_ms, prof_src = rocprof_mean_ms(dom, workload)
+    cur = source_hash()
+    src_hash = {n: profile_hash(ROOT / "profiles" / n) for n in (traffic_src, prof_src) if n}
     return {"traffic": traffic, "traffic_unit": "bytes per launch (PMC FETCH_SIZEx2 + WRITE_SIZE)",
             "traffic_source": traffic_src, "kernels": STAGE_KERNELS.get(dom),
+            # a profile taken at other sources than this run's (or with no hash recorded)
+            # may not describe the code measured here
+            "profile_source_hash": src_hash,
+            "profiles_stale": any(h != cur for h in src_hash.values()),
             "event_ms": round(event_ms, 4),
             "rocprof_mean_ms": None if prof_ms is None else round(prof_ms, 4), "rocprof_source": prof_src,
             "frac_rocprof": None if not prof_ms else
@@ -429,7 +470,7 @@ def main():
                           match_cu_stride=int(os.environ.get("ORBX_MATCH_CUSTRIDE", "1")),
                           match_priority=int(os.environ.get("ORBX_MATCH_STREAM_PRIO", "0")))
     S = pl.S
-    lane_off = pl.lane_offset_stage
+    lane_off = pl.lane_offset_stage if pl.lane_ev is not None else None  # None: no offset applied
     d_frames = torch.from_numpy(frames_np).to(dev)
     d_T = torch.from_numpy(T).to(dev)
     torch.cuda.synchronize(dev)  # uploads on torch's stream finish before the extractor streams read them
@@ -483,12 +524,13 @@ def main():
     per_launch = (B - 1) if dom == "match" else (pl.bounds[0][1] - pl.bounds[0][0])
     achieved = bytes_pf[dom] * per_launch / (stage_ms[dom] * 1e-3) / 1e9
     prof = profile_fields(dom, bytes_pf[dom] * per_launch, stage_ms[dom], wl)
-    valu, valu_src = pmc_valu(dom) if not c5 else (None, None)
+    valu, valu_src = pmc_valu(dom, wl)
     issue = None
     if valu:
         rate = valu / (stage_ms[dom] * 1e-3) / 1e9
         issue = {"bound": "valu", "achieved": round(rate, 1), "peak": VALU_PEAK_GIPS, "unit": "G wave-instr/s",
                  "frac": round(rate / VALU_PEAK_GIPS, 4), "valu_per_launch": valu, "source": valu_src,
+                 "source_stale": profile_hash(ROOT / "profiles" / valu_src) != source_hash(),
                  "note": "SQ_INSTS_VALU per launch / stage time; peak = 1024 SIMDs x 2.4 GHz / 2 cycles",
                  "frac_all_lanes": round(rate * S / VALU_PEAK_GIPS, 4)}
 
@@ -622,6 +664,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
+            "source_hash": source_hash(),
             "config": {"workload": f"{'configs[4]' if c5 else 'configs[1]'}: {B} synthetic 640x480 gray frames per GPU "
                                    f"(views of one textured canvas along a random walk), nFeatures={prm[0]}, scale 1.2, "
                                    f"{prm[2]} levels, FAST 20/7; step = "

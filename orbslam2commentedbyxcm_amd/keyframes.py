@@ -29,7 +29,8 @@ keyframes whose views overlap most, then the baseline skip) depends only on the 
 is made once on the host, as LocalMapping does per keyframe.
 
 tests/euroc_bench.py (bench.py --workload euroc) times this object;
-tests/test_gpu_keyframes.py checks its output against the CPU parity oracle, and
+tests/test_gpu_keyframes.py checks its output against the CPU parity oracle (also through
+a one-rank RCCL group with collective=True, the all_gather_into_tensor path), and
 tests/test_distributed.py covers the layout, the plan and the gather at world size 2 on
 gloo.
 """
@@ -169,15 +170,18 @@ def stream_poses(off: np.ndarray, fx: float, fy: float, depth: float) -> np.ndar
     return T
 
 
-def gather_slabs(slab, gathered, group=None) -> None:
+def gather_slabs(slab, gathered, group=None, force: bool = False) -> None:
     """Every rank's slab into `gathered` (world x slab bytes), rank order.  RCCL:
-    one all_gather_into_tensor, device to device.  gloo (the CPU tests, and the
+    one all_gather_into_tensor, device to device, enqueued behind the current stream's
+    work (ProcessGroupNCCL's stream waits on it, and the current stream waits on the
+    collective before anything enqueued after it).  gloo (the CPU tests, and the
     several-ranks-on-one-GPU rehearsal): all_gather, staged through host memory for
-    device tensors."""
+    device tensors.  World size 1 is a device copy unless `force`, which issues the
+    collective anyway (the one-GPU hardware test of the RCCL path)."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
-    if world == 1:
+    if world == 1 and not force:
         if gathered.data_ptr() != slab.data_ptr():
             gathered.copy_(slab)
         return
@@ -196,7 +200,7 @@ class StereoKeyFramePipeline:
 
     def __init__(self, batch: int, rank: int = 0, world: int = 1, device: int = 0, nn: int = 10, seq_seed: int = 3,
                  vocab_text: bytes | None = None, settings: dict | None = None, group=None, windows: int = 1,
-                 on_step_done=None):
+                 on_step_done=None, collective: bool = False):
         import torch
 
         from . import synth
@@ -206,6 +210,11 @@ class StereoKeyFramePipeline:
 
         s = dict(EUROC if settings is None else settings)
         self.s, self.B, self.rank, self.world, self.group = s, int(batch), int(rank), int(world), group
+        # collective: the slab exchange runs through the process group even at world size 1
+        # (a one-rank RCCL all_gather_into_tensor into its own gathered buffers), so the
+        # N-GPU data path -- collective, gathered buffers, keyframe tables into them -- is
+        # the one under test on a single GPU; world > 1 always exchanges
+        self.collective = self.world > 1 or bool(collective)
         self.W, self.H = s["width"], s["height"]
         self.dev = torch.device("cuda", device)
         self.mb = s["bf"] / s["fx"]
@@ -262,7 +271,7 @@ class StereoKeyFramePipeline:
         # one gathered buffer per set: step j+1's all-gather (set k') must not overwrite the
         # neighbours step j's triangulation (set k) is reading on the other stream
         self.gathered = [torch.zeros(self.world * self.lay.nbytes, **u8) for _ in range(2)] \
-            if self.world > 1 else None
+            if self.collective else None
         self.plan = plan_neighbours(self.poses, self.rank, self.world, self.B, nn, self.mb, s)
         P = max(len(self.plan.pairs), 1)
         self.m12 = [torch.empty((P, self.cap), **i32) for _ in range(2)]
@@ -295,7 +304,7 @@ class StereoKeyFramePipeline:
         torch.cuda.synchronize(self.dev)
         # the keyframe tables are fixed per buffer: build the ctypes arrays once
         from .matcher import keyframe_table
-        bufs = self.gathered if self.world > 1 else self.slabs
+        bufs = self.gathered if self.collective else self.slabs
         self._tabs = [keyframe_table(self.lay.records(b.data_ptr(), self.world, self._rec_poses)) for b in bufs]
 
     def close(self):
@@ -345,8 +354,8 @@ class StereoKeyFramePipeline:
         with torch.cuda.stream(ms):
             # Tracking::CreateNewKeyFrame: a MapPoint for every stereo point closer than mThDepth
             torch.logical_and(v["u_right"] >= 0, rt["depth"] < self.th_depth, out=v["has_mp"].view(torch.bool))
-            if self.world > 1:
-                gather_slabs(self.slabs[k], self.gathered[k], self.group)
+            if self.collective:
+                gather_slabs(self.slabs[k], self.gathered[k], self.group, force=True)
         self.ev_s[k].record(ms)
         ts = self.ts
         ts.wait_event(self.ev_s[k])
@@ -383,7 +392,7 @@ class StereoKeyFramePipeline:
 
     def results(self, k=None) -> dict:
         """Device tensors of set k (default: the newest step's): every field the step
-        writes, the triangulation outputs and (world > 1) the gathered buffer."""
+        writes, the triangulation outputs and (collective) the gathered buffer."""
         k = self.last if k is None else k
         v, rt = self.sv[k], self.right[k]
         P = len(self.plan.pairs)
@@ -391,7 +400,7 @@ class StereoKeyFramePipeline:
              "ur": v["u_right"], "depth": rt["depth"], "has_mp": v["has_mp"], "fv_node": v["fv_node"],
              "fv_off": v["fv_off"], "fv_idx": v["fv_idx"], "nfv": v["nfv"], "tri_n": self.tri_n[k][:P],
              "tri_pairs": self.tri_pairs[k][:P]}
-        if self.world > 1:
+        if self.collective:
             r["gathered"] = self.gathered[k]
         return r
 

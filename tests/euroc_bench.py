@@ -127,7 +127,7 @@ def check(pl, ok: OracleKeyFrames, res: dict, nlocal: int, threads: int) -> dict
         if not good:
             bad_kf.append(g)
     bad_gathered = []
-    if world > 1:  # the neighbours as this rank received them over RCCL
+    if pl.collective:  # the neighbours as this rank received them over RCCL
         buf = res["gathered"]
         for h in sorted(need):
             q, i = h % world, h // world
@@ -150,7 +150,7 @@ def check(pl, ok: OracleKeyFrames, res: dict, nlocal: int, threads: int) -> dict
             bad_pairs.append(p)
         assert record_index(int(plan.kf1_window[p]), world, B) == plan.pairs[p, 0]
     return {"keyframes_checked": len(local_g), "keyframes_mismatched": len(bad_kf), "first_bad_keyframes": bad_kf[:8],
-            "gathered_neighbours_checked": len(need) if world > 1 else 0,
+            "gathered_neighbours_checked": len(need) if pl.collective else 0,
             "gathered_mismatched": len(bad_gathered), "first_bad_gathered": bad_gathered[:8],
             "pairs_checked": len(sel), "pairs_mismatched": len(bad_pairs), "first_bad_pairs": bad_pairs[:8],
             "mean_triangulation_matches_ref": float(np.mean(npairs)) if npairs else 0.0,
@@ -224,6 +224,9 @@ def main(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--parity-frames", type=int, default=-1,
                     help="rank 0 keyframes to check (-1: all at world 1, 16 at world > 1; 0: none)")
+    ap.add_argument("--collective", action="store_true",
+                    help="exchange the slabs through an RCCL process group even at --gpus 1 (a one-rank "
+                         "all_gather_into_tensor into gathered buffers: the N-GPU data path on one GPU)")
     args, _ = ap.parse_known_args(argv)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -238,7 +241,17 @@ def main(argv=None):
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    collective = world > 1 or args.collective
+    if collective:
+        if world == 1:  # a one-rank group (env rendezvous: 127.0.0.1, a free port)
+            import socket
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                with socket.socket() as sk:
+                    sk.bind(("127.0.0.1", 0))
+                    os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=dev)
     s = EUROC
     # the vocabulary's level-1 centres come from the stream's first left view (same on every rank)
@@ -249,7 +262,8 @@ def main(argv=None):
     t0 = time.perf_counter()
     text = synth.vocabulary_text(7, 10, 6, 0, 0, centres=d0)
     gen_s = time.perf_counter() - t0
-    pl = StereoKeyFramePipeline(B, rank, world, device=local_rank, nn=args.nn, vocab_text=text)
+    pl = StereoKeyFramePipeline(B, rank, world, device=local_rank, nn=args.nn, vocab_text=text,
+                                collective=collective)
 
     def barrier():
         if world > 1:
@@ -319,6 +333,7 @@ def main(argv=None):
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
+            "source_hash": __import__("bench").source_hash(),
             "config": {"workload": f"configs[3]: {B} stereo keyframes per GPU per step (keyframe g of the {B * world}-"
                                    f"keyframe window on rank g % {world}), synthetic rectified 752x480 views of a "
                                    f"textured plane at {pl.depth:.2f} m, EuRoC calibration, nFeatures=1200, scale 1.2, "
@@ -328,6 +343,8 @@ def main(argv=None):
                                    f"keyframe vs its nn={args.nn} stream neighbours passing the baseline test",
                        "keyframes_per_gpu_step": B, "global_batch": B * world, "width": pl.W, "height": pl.H,
                        "parallelism": f"frame-sharded x{world} + all-gather", "slab_mb_per_rank": round(slab_mb, 2),
+                       "slab_exchange": ("rccl all_gather_into_tensor" if collective else "none (world 1: slabs read in "
+                                         "place)"),
                        "allgather_mb_per_rank_step": round(slab_mb * world, 2),
                        "triangulation_pairs_per_step": tot_pairs, "baseline_skipped_per_step": tot_skipped,
                        "triangulation_matches_per_step": tot_matches},
@@ -344,7 +361,7 @@ def main(argv=None):
             "mean_stereo_matches_per_keyframe": round(float((res["ur"] >= 0).sum(axis=1).mean()), 1),
             "vocabulary_generate_s": round(gen_s, 2),
         }
-    if world > 1:
+    if collective:
         dist.barrier()
         dist.destroy_process_group()
     if out is not None:

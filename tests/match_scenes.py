@@ -228,3 +228,29 @@ def posed_sequence(seed, n):
     imgs, _ = synth.plane_views(seed, rels, 640, 480, FX, FY, CX, CY, Z0)
     T = np.stack([_world_pose(r)[:3, :4].reshape(12) for r in rels]).astype(np.float32)
     return imgs, rels, T
+
+
+def posed_walk(seed, n, max_roll=40.0):
+    """n views of one plane along a seeded random walk with a full rotation in every Tcw
+    (the bench-shaped posed batch): per frame the roll about the optical axis turns by 5-14
+    degrees either way (so the rotation histogram's dominant 12-degree bin is rarely bin
+    0; bounded by max_roll), the tilts about x / y by up to +-0.6 degrees
+    (bounded by 3), the centre by up to 0.03 sideways and 0.06 along the axis (bounded by
+    0.3 / 0.4).  Returns (views (n, 480, 640) u8, relative poses, world Tcw (n, 12) f32)."""
+    g = np.random.default_rng(seed + 91)
+    roll, tx, ty = 0.0, 0.0, 0.0
+    c = np.zeros(3)
+    rels = []
+    for k in range(n):
+        if k:
+            step = g.uniform(5.0, 14.0) * (1 if g.random() < 0.5 else -1)
+            if abs(roll + step) > max_roll:
+                step = -step
+            roll += step
+            tx = float(np.clip(tx + g.uniform(-0.6, 0.6), -3.0, 3.0))
+            ty = float(np.clip(ty + g.uniform(-0.6, 0.6), -3.0, 3.0))
+            c = np.clip(c + g.uniform([-0.03, -0.03, -0.06], [0.03, 0.03, 0.06]), [-0.3, -0.3, -0.4], [0.3, 0.3, 0.4])
+        rels.append(_rel([("z", roll), ("x", tx), ("y", ty)], c.copy()))
+    imgs, _ = synth.plane_views(seed, rels, 640, 480, FX, FY, CX, CY, Z0)
+    T = np.stack([_world_pose(r)[:3, :4].reshape(12) for r in rels]).astype(np.float32)
+    return imgs, rels, T

@@ -268,6 +268,7 @@ def main(argv=None):
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
+        "source_hash": __import__("bench").source_hash(),
         "config": {"workload": f"configs[2]: {B} synthetic 1241x376 stereo pairs per step ({len(pairs)} distinct), "
                                f"nFeatures=2000, scale 1.2, 8 levels, FAST 20/7; step = extract L and R on two "
                                f"extractors + Frame::ComputeStereoMatches of every pair (bf {BF}, maxD = fx)",

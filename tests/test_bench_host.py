@@ -236,3 +236,30 @@ def test_stage_sum_counts_pyramid_segments(tmp_path, monkeypatch):
     assert abs(ms - 0.6) < 1e-9
     assert bench.pmc_traffic("pyramid", "tum5k")[0] == 2000
     assert bench.pmc_traffic("score_blur", "tum5k")[0] == 5
+
+
+def test_pmc_valu_reads_the_workload_file(tmp_path, monkeypatch):
+    """The issue figure comes from the newest VALU summary of the bench's own workload
+    (configs[1]: <tag>_tum_ or untagged files, never another workload's), and a summary
+    taken at other sources than the running code is flagged stale."""
+    import json
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+
+    def put(name, valu, h):
+        (prof / name).write_text(json.dumps({"source_hash": h, "kernels": {
+            "orbx::k_level_tiles": {"sq_insts_valu": valu, "dispatches": 4}}}))
+    put("r03c_pmc_valu.json", 100, "x")
+    put("r04a_tum5k_pmc_valu.json", 900, "y")
+    put("r04a_tum_pmc_valu.json", 200, bench.source_hash())
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    assert bench.pmc_valu("score_blur", "tum") == (200, "r04a_tum_pmc_valu.json")
+    assert bench.pmc_valu("score_blur", "tum5k") == (900, "r04a_tum5k_pmc_valu.json")
+    assert bench.pmc_valu("score_blur", "kitti") == (None, None)
+    assert bench.profile_hash(prof / "r04a_tum_pmc_valu.json") == bench.source_hash()
+    assert bench.profile_hash(prof / "r04a_tum5k_pmc_valu.json") != bench.source_hash()
+
+
+def test_source_hash_tracks_the_sources():
+    h = bench.source_hash()
+    assert len(h) == 16 and h == bench.source_hash()

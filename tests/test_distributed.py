@@ -190,7 +190,7 @@ def test_neighbour_plan(world, batch):
     del seq
 
 
-def _slab_worker(rank, world, port, outdir):
+def _slab_worker(rank, world, port, outdir, force=False):
     import torch
     import torch.distributed as dist
 
@@ -206,7 +206,7 @@ def _slab_worker(rank, world, port, outdir):
             v["n"][i] = 100 * rank + i
             v["fv_off"][i] = torch.arange(51, dtype=torch.int32) + rank
         gathered = torch.zeros(world * lay.nbytes, dtype=torch.uint8)
-        gather_slabs(slab, gathered)
+        gather_slabs(slab, gathered, force=force)
         buf = gathered.numpy()
         ok = True
         for q in range(world):
@@ -227,3 +227,13 @@ def test_gather_slabs_gloo_world2(tmp_path):
     world = 2
     mp.spawn(_slab_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     assert all(open(tmp_path / f"s{r}").read().strip() == "1" for r in range(world))
+
+
+def test_gather_slabs_forced_world1(tmp_path):
+    """collective=True at world size 1: the exchange goes through the process group's
+    all_gather (gloo here; RCCL's all_gather_into_tensor on the GPU test) and lands the
+    slab in the gathered buffer."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_slab_worker, args=(1, _free_port(), str(tmp_path), True), nprocs=1, join=True)
+    assert open(tmp_path / "s0").read().strip() == "1"

@@ -52,10 +52,11 @@ def test_keyframe_pipeline_matches_oracle(oracle, orbx_built, B, nn, steps, wind
         assert (res["ur"] >= 0).sum() > 50 * B
 
 
-def _rank(rank, world, port, outdir):
+def _rank(rank, world, port, outdir, backend="gloo", B=6, steps=4):
     import json
     import os
 
+    import torch
     import torch.distributed as dist
 
     import euroc_bench as E
@@ -64,21 +65,25 @@ def _rank(rank, world, port, outdir):
     from orbslam2commentedbyxcm_amd.keyframes import StereoKeyFramePipeline
 
     # several ranks on the one GPU of the test box: gloo carries the slab exchange (the
-    # RCCL all_gather_into_tensor needs one GPU per rank); everything else is the N-GPU path
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    # RCCL all_gather_into_tensor needs one GPU per rank); everything else is the N-GPU path.
+    # backend "nccl" (world 1): the RCCL collective itself, forced at one rank
+    kw = {"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}
+    dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world, **kw)
     try:
-        pl = StereoKeyFramePipeline(6, rank, world, device=0, nn=4, vocab_text=synth.vocabulary_text(11, 8, 6, 0, 0),
-                                    windows=2)
-        snaps = _run_snapshots(pl, 4)
+        pl = StereoKeyFramePipeline(B, rank, world, device=0, nn=4, vocab_text=synth.vocabulary_text(11, 8, 6, 0, 0),
+                                    windows=2, collective=True)
+        assert pl.collective and pl.gathered is not None
+        snaps = _run_snapshots(pl, steps)
         O.build()
         oks = {}
         steps = []
         for j, (w, res) in enumerate(snaps):
             ok = oks.setdefault(w, E.OracleKeyFrames(O, pl, O.Vocab(pl.vocab_text), window=w))
-            r = E.check(pl, ok, res, 6, 4)
+            r = E.check(pl, ok, res, B, 4)
             r["window"] = w
             steps.append(r)
-        out = {"pairs": len(pl.plan.pairs), "status": pl.status(), "steps": steps}
+        out = {"pairs": len(pl.plan.pairs), "status": pl.status(), "steps": steps,
+               "backend": dist.get_backend()}
         with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
             json.dump(out, f)
         dist.barrier()
@@ -106,3 +111,27 @@ def test_keyframe_pipeline_world2_gloo_on_one_gpu(orbx_built, tmp_path):
         for j, st in enumerate(out["steps"]):
             assert st["window"] == j % 2 and st["bit_exact"], (r, j, st)
             assert st["gathered_neighbours_checked"] > 6 and st["pairs_checked"] == out["pairs"] > 6, (r, j, st)
+
+
+def test_keyframe_pipeline_rccl_allgather_world1(orbx_built, tmp_path):
+    """The RCCL branch of gather_slabs on hardware: a one-rank nccl (RCCL) group with the
+    exchange forced (collective=True), so every step's slab goes through
+    all_gather_into_tensor into that set's gathered buffer and the triangulation reads its
+    neighbours from there.  Six pipelined steps over two alternating keyframe windows with
+    no host synchronisation between them (the RCCL enqueue is asynchronous: it is ordered
+    only by the matcher stream it is issued on, and the triangulation stream waits on that
+    stream's event); every step's keyframes, gathered copies and pair lists vs the oracle."""
+    import json
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_rank, args=(1, port, str(tmp_path), "nccl", 8, 6), nprocs=1, join=True)
+    out = json.loads(open(tmp_path / "r0.json").read())
+    assert out["backend"] == "nccl" and out["status"] and len(out["steps"]) == 6, out
+    for j, st in enumerate(out["steps"]):
+        assert st["window"] == j % 2 and st["bit_exact"], (j, st)
+        assert st["gathered_neighbours_checked"] >= 8 and st["pairs_checked"] == out["pairs"] > 8, (j, st)

@@ -196,3 +196,59 @@ def test_sequence_pipeline_local_map_c5_large_local_map(oracle, orbx_built):
     assert r["bit_exact"], r
     assert r["mean_local_matches_ref"] > 50, r
     pl.close()
+
+
+def test_sequence_pipeline_configs4_bench_shape(oracle, orbx_built):
+    """configs[4]'s bench shape exactly: B = 256 in two 128-frame lanes, 5000 features x 12
+    levels (two pyramid segments), the default lane offset for deep pyramids (4: lane 1
+    starts after lane 0's octree), the lean split matcher, pipelined; every frame and every
+    pair of the newest batch against the oracle."""
+    prm = (5000, 1.2, 12, 20, 7)
+    import torch
+
+    frames, off = synth.sequence(1000, 256)
+    T = sequence_poses(off)
+    pl = SequencePipeline(256, 640, 480, lanes=2, pipelined=True, params=prm)
+    assert pl.lane_offset_stage == 4 and pl.lane_ev is not None and pl.S == 2
+    d_frames = torch.from_numpy(frames).to(pl.dev)
+    d_T = torch.from_numpy(T).to(pl.dev)
+    torch.cuda.synchronize()
+    pl.run(d_frames, d_T, 3)
+    torch.cuda.synchronize()
+    res = pl.host_results()
+    assert not pl.status().any()
+    r = checks.check_sequence(frames, T, res, pl.sf, params=prm)
+    assert r["frames_checked"] == 256 and r["pairs_checked"] == 255
+    assert r["frames_mismatched"] == 0 and r["pairs_mismatched"] == 0, r
+    assert r["mean_matches_per_pair_ref"] > 1000, r
+    pl.close()
+
+
+def test_sequence_pipeline_posed_b256(oracle, orbx_built):
+    """The headline pipeline (B = 256, two lanes, pipelined) on a posed batch: every Tcw a
+    full rotation, the camera rolling 5-14 degrees between frames, so the rotation
+    histogram of every pair (ORBmatcher.cc:1750-1786) has its dominant bin off zero on most
+    pairs; every frame and pair against the oracle."""
+    import torch
+
+    import match_scenes as S
+
+    imgs, _, T = S.posed_walk(40, 256)
+    pl = SequencePipeline(256, 640, 480, lanes=2, pipelined=True, depth=S.Z0)
+    d_frames = torch.from_numpy(imgs).to(pl.dev)
+    d_T = torch.from_numpy(T).to(pl.dev)
+    torch.cuda.synchronize()
+    pl.run(d_frames, d_T, 2)
+    torch.cuda.synchronize()
+    res = pl.host_results()
+    assert not pl.status().any()
+    r = checks.check_sequence(imgs, T, res, pl.sf, depth=S.Z0)
+    assert r["frames_mismatched"] == 0 and r["pairs_mismatched"] == 0, r
+    assert r["mean_matches_per_pair_ref"] > 300, r
+    dom = []
+    for b in range(1, 256):
+        n0, n1 = int(res["n"][b - 1]), int(res["n"][b])
+        h = S.rotation_bins(res["kps"][b - 1][:n0], res["kps"][b][:n1], res["mp"][b][:n1])
+        dom.append(int(np.argmax(h)))
+    assert sum(d != 0 for d in dom) > 200, dom
+    pl.close()

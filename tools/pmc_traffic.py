@@ -30,6 +30,18 @@ def per_kernel(pattern, counter):
     return {k: sum(v) / len(v) for k, v in out.items()}, {k: len(v) for k, v in out.items()}
 
 
+def bench_source_hash(*logs):
+    """The source_hash of the bench line a profiled run printed (its last JSON line)."""
+    for log in logs:
+        try:
+            for line in reversed(Path(log).read_text().splitlines()):
+                if line.startswith("{"):
+                    return json.loads(line).get("source_hash")
+        except (OSError, ValueError):
+            continue
+    return None
+
+
 def main():
     tag = sys.argv[1]
     base = ROOT / "gpurun_out"
@@ -43,6 +55,7 @@ def main():
                   "dispatches": nf.get(k, 0)}
     out = ROOT / "profiles" / f"{tag}_pmc_traffic.json"
     out.write_text(json.dumps({"units": "bytes per launch (FETCH_SIZE x2 x1024 + WRITE_SIZE x1024)",
+                               "source_hash": bench_source_hash(base / f"{tag}_fetch.log", base / f"{tag}_write.log"),
                                "kernels": res}, indent=1))
     for k, v in res.items():
         print(f"{k:40s} read {v['read_bytes']/1e6:10.2f} MB  write {v['write_bytes']/1e6:10.2f} MB  "
