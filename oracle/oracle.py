@@ -108,6 +108,8 @@ def _load(path) -> C.CDLL:
                                            C.c_int, C.c_void_p, C.c_int]
     L.ora_pyramid.argtypes = [C.POINTER(Params), u8p, C.c_int, C.c_int, C.c_size_t, C.POINTER(u8p)]
     L.ora_level_candidates.argtypes = [C.POINTER(Params), u8p, C.c_int, C.c_int, C.c_void_p, C.c_int]
+    L.ora_level_candidates_cells.argtypes = [C.POINTER(Params), u8p, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                             C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_int)]
     L.ora_level_size.argtypes = [C.POINTER(Params), C.c_int, C.c_int, C.c_int,
                                     C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.ora_set_trig_mode.argtypes = [C.c_int]
@@ -195,6 +197,20 @@ def level_candidates(level: np.ndarray, p: Params | None = None, cap: int = 1 <<
     if n < 0:
         raise RuntimeError("capacity")
     return out[:n].copy()
+
+
+def level_candidates_cells(level: np.ndarray, p: Params | None = None, cap: int = 1 << 18):
+    """level_candidates plus the FAST output count of every visited cell, in visit order."""
+    p = p or params()
+    level = np.ascontiguousarray(level)
+    out = np.zeros(cap, dtype=KEYPOINT_DTYPE)
+    cc = np.zeros(1 << 14, dtype=np.int32)
+    nc = C.c_int(0)
+    n = lib().ora_level_candidates_cells(C.byref(p), _u8(level), level.shape[1], level.shape[0], out.ctypes.data,
+                                         cap, cc.ctypes.data_as(C.POINTER(C.c_int)), len(cc), C.byref(nc))
+    if n < 0:
+        raise RuntimeError("capacity")
+    return out[:n].copy(), cc[:nc.value].copy()
 
 
 def distribute_octree(keys: np.ndarray, minX, maxX, minY, maxY, N):

@@ -718,8 +718,23 @@ int ora_pyramid(const ora_params* p, const uint8_t* img, int W, int H, size_t st
 }
 
 /* ComputeKeyPointsOctTree cell loop, ORBextractor.cc:1025-1122 */
+static int level_candidates(const ora_params* p, const uint8_t* level, int w, int h, ora_keypoint* out,
+                            int cap, int* cell_counts, int cell_cap, int* ncells);
+
 int ora_level_candidates(const ora_params* p, const uint8_t* level, int w, int h, ora_keypoint* out,
                          int cap) {
+    return level_candidates(p, level, w, h, out, cap, NULL, 0, NULL);
+}
+
+/* The same, plus the FAST output count of every visited cell in visit order (test
+ * infrastructure for the H1 allocator measurement, tests/h1_glibc_measure.py). */
+int ora_level_candidates_cells(const ora_params* p, const uint8_t* level, int w, int h, ora_keypoint* out,
+                               int cap, int* cell_counts, int cell_cap, int* ncells) {
+    return level_candidates(p, level, w, h, out, cap, cell_counts, cell_cap, ncells);
+}
+
+static int level_candidates(const ora_params* p, const uint8_t* level, int w, int h, ora_keypoint* out,
+                            int cap, int* cell_counts, int cell_cap, int* ncells) {
     const float Wc = 30;
     const int minBorderX = EDGE_THRESHOLD - 3;
     const int minBorderY = minBorderX;
@@ -749,6 +764,10 @@ int ora_level_candidates(const ora_params* p, const uint8_t* level, int w, int h
             int nc = ora_fast_detect(sub, rows, cols, (size_t)w, p->ini_th_fast, cell, 64 * 64);
             if (nc == 0) nc = ora_fast_detect(sub, rows, cols, (size_t)w, p->min_th_fast, cell, 64 * 64);
             if (nc < 0) return -1;
+            if (ncells) {
+                if (*ncells >= cell_cap) return -1;
+                cell_counts[(*ncells)++] = nc;
+            }
             for (int k = 0; k < nc; k++) {
                 if (nout >= cap) return -1;
                 out[nout] = cell[k];

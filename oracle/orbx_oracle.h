@@ -80,6 +80,8 @@ int ora_pyramid(const ora_params* p, const uint8_t* img, int W, int H, size_t st
 /* Per-level FAST candidates (vToDistributeKeys, coordinates relative to minBorder). */
 int ora_level_candidates(const ora_params* p, const uint8_t* level, int w, int h, ora_keypoint* out,
                          int cap);
+int ora_level_candidates_cells(const ora_params* p, const uint8_t* level, int w, int h, ora_keypoint* out,
+                               int cap, int* cell_counts, int cell_cap, int* ncells);
 
 /* Full ORBextractor::operator() (ORBextractor.cc:1513-1629).  Returns the keypoint
  * count (>=0), or -1 if cap is too small.  level_counts (nullable) receives the

@@ -5,9 +5,10 @@
 
 The shared library lands next to this file so that it travels with the repository
 snapshot to the GPU box (it is git-ignored, not gpurun-ignored).  Every translation
-unit is compiled with -ffp-contract=off: the reference is built -std=c++11 (ISO),
-under which GCC does not contract a*b+c into FMA, and the descriptor / fastAtan2
-float expressions must round identically (hazard H4).
+unit is compiled with -ffp-contract=off, and fuses exactly where the reference's g++
+-O3 -march=native build fuses, with explicit fma (g++ contracts C++ even under
+-std=c++11; measured on the reference's own BowVector.cpp): the descriptor / fastAtan2 /
+projection float expressions must round identically (hazard H4).
 """
 from __future__ import annotations
 
@@ -96,6 +97,10 @@ def clean() -> None:
 
 
 if __name__ == "__main__":
+    if "--variant" in sys.argv:  # python -m orbslam2commentedbyxcm_amd.build --variant TAG -DNAME=V ...
+        i = sys.argv.index("--variant")
+        print(build_variant(sys.argv[i + 1], [a[2:] for a in sys.argv[i + 2:] if a.startswith("-D")]))
+        sys.exit(0)
     if "--clean" in sys.argv:
         clean()
     build(verbose=True)

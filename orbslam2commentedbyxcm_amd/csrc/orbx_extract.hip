@@ -1521,6 +1521,9 @@ __device__ __forceinline__ void desc_level_of(const DescLevel* s, int L, int slo
 // save (configs[4] 100.6-100.9k -> 94.1-95.1k; capping them by LDS gives both back):
 // register staging above this many slots.
 constexpr int kDescGldsMaxSlots = 3000;
+#ifndef ORBX_ABL_DESC
+#define ORBX_ABL_DESC 0  // timing ablations of k_describe (tools/ab_lib.sh); 0 in every shipped build
+#endif
 #ifndef ORBX_DESC_DMA
 // the LDS-DMA form below kDescGldsMaxSlots: 1 = 16-byte pieces into 48-byte rows (five
 // workgroups a CU), 2 = 4-byte pieces into 40-byte rows (24.7 KB, six a CU: configs[1]
@@ -1576,6 +1579,9 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     int l, base, total;
     desc_level_of(s_lv, L, slot, l, base, total);
     if (slot0 == 0 && lane == 0) n_out[f] = total;
+#if ORBX_ABL_DESC == 2  // timing ablation only: no describe work at all
+    return;
+#endif
     const DescLevel& g = s_lv[l];
     const int i = slot - g.out_off;
     const int o = base + i;
@@ -1601,12 +1607,18 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
         const int d0 = (x - 15) & 3;
         const uint8_t* prow1 = pframe + (uint32_t)(g.off + (long long)(y + v1) * pitch + xs);
         const uint8_t* prow2 = pframe + (uint32_t)(g.off + (long long)(y + v2) * pitch + xs);
+#if ORBX_ABL_DESC == 1  // timing ablation only: no staging loads (garbage patch, constant rows)
+        const uint4 p0 = make_uint4(x, y, x ^ y, 7), p1 = p0, r0 = make_uint4(y, x, 3, x + y), r1 = r0;
+        const uint32_t p2 = (uint32_t)x, r2 = (uint32_t)y;
+        (void)prow1; (void)prow2;
+#else
         const uint4 p0 = *(const uint4*)prow1, p1 = *(const uint4*)(prow1 + 16);
         const uint32_t p2 = *(const uint32_t*)(prow1 + 32);
         const uint4 r0 = *(const uint4*)prow2, r1 = *(const uint4*)(prow2 + 16);
         const uint32_t r2 = *(const uint32_t*)(prow2 + 32);
+#endif
         const uint8_t* bpatch = bframe + (uint32_t)(g.off + (long long)(y - 18) * pitch + xb);
-        if constexpr (STAGE == 1) {
+        if constexpr (STAGE == 1 && ORBX_ABL_DESC != 1) {
         // the four BRIEF patches go straight to LDS (global_load_lds_dwordx4: no VGPR
         // destinations, so more waves fit a SIMD): patch by patch, the whole wave loads
         // its 111 chunks (lane L chunks L and 64 + L), from the patch base of quarter q
@@ -1633,7 +1645,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
             }
         }
         }
-        if constexpr (STAGE == 2) {
+        if constexpr (STAGE == 2 && ORBX_ABL_DESC != 1) {
             // 4-byte pieces: patch q's 370 dwords (37 rows x 10), lane L dword L + 64 j
             const uint64_t mybase = (uint64_t)(uintptr_t)bpatch;
             uint8_t* const wbp = (uint8_t*)s_bpatch[wave * 4];
@@ -1660,7 +1672,11 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
 #pragma unroll
             for (int j = 0; j < 7; j++) {
                 const int c = min(ql + 16 * j, 110), row = (c * 171) >> 9;
+#if ORBX_ABL_DESC == 1
+                bch[j] = make_uint4(row, c, x, y);
+#else
                 bch[j] = *(const uint4*)(bpatch + (uint32_t)(row * pitch + 16 * (c - 3 * row)));
+#endif
             }
         }
         auto row_sums = [&](const uint4& a0, const uint4& a1, uint32_t a2, int av, uint32_t& cs, uint32_t& ws) {
