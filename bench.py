@@ -482,11 +482,26 @@ def main():
         if world > 1:
             dist.barrier()
 
+    # The warmup steps record every stage boundary (HIP events on each lane's stream and
+    # the matcher's): the stage table and the dominant stage come from them.  The timed
+    # steps then record only the dominant stage's two events per launch (a ring of event
+    # sets, read back after the loop, no synchronisation inside it): every recorded event
+    # costs the pipelined step ~0.2 % (tools/timing_ab.py: all stages' events 1.3-1.6 %).
+    wl = "tum5k" if c5 else "tum"
+    pl.set_timing(True)
     pl.run(d_frames, d_T, max(args.warmup, 1))
     sync()
-    # Per-stage HIP events on the extractor's stream, recorded inside the timed loop
-    # (a ring of event sets; read back after the loop, no synchronisation inside it).
-    pl.set_timing(True)
+    stage_ms = pl.stage_times()  # warmup steps, every stage
+    kernels = {k: v for k, v in stage_ms.items() if k not in ("total", "match")}
+    # Dominant kernel: the longest stage on the critical path.  Pipelined, the matcher
+    # runs beside the next batch's extraction on its own stream, so the step is set by
+    # whichever is longer: a lane's extraction (its longest stage is reported) or the
+    # matcher (configs[4]: its launch is then the critical path).
+    dom = dominant_stage(kernels, wl)
+    if match and pipeline and stage_ms.get("match", 0.0) > stage_ms.get("total", 0.0):
+        dom = "match"
+    # ORBX_BENCH_ALL_EVENTS=1 (A/B knob): every stage's events in the timed steps too
+    pl.set_timing(True, stage=None if os.environ.get("ORBX_BENCH_ALL_EVENTS") else dom)
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -508,26 +523,17 @@ def main():
     mean_kps = float(n_host.mean())
     mean_matches = float(res["nm"][1:].mean()) if match and B > 1 else 0.0
 
-    stage_ms = pl.stage_times()  # HIP events, mean over the lanes' launches
+    dom_ms = pl.stage_times()[dom]  # HIP events over the timed steps, mean over the lanes' launches
     pl.set_timing(False)
     bytes_pf = stage_bytes(W, H, mean_kps, nlevels=prm[2], scale=prm[1])
-    # Dominant kernel: the longest stage on the critical path.  Pipelined, the matcher
-    # runs beside the next batch's extraction on its own stream, so the step is set by
-    # whichever is longer: a lane's extraction (its longest stage is reported) or the
-    # matcher (configs[4]: its launch is then the critical path).
-    kernels = {k: v for k, v in stage_ms.items() if k not in ("total", "match")}
-    wl = "tum5k" if c5 else "tum"
-    dom = dominant_stage(kernels, wl)
-    if match and pipeline and stage_ms.get("match", 0.0) > stage_ms.get("total", 0.0):
-        dom = "match"
     # frames per launch: a lane's batch for extraction stages, every pair for the matcher
     per_launch = (B - 1) if dom == "match" else (pl.bounds[0][1] - pl.bounds[0][0])
-    achieved = bytes_pf[dom] * per_launch / (stage_ms[dom] * 1e-3) / 1e9
-    prof = profile_fields(dom, bytes_pf[dom] * per_launch, stage_ms[dom], wl)
+    achieved = bytes_pf[dom] * per_launch / (dom_ms * 1e-3) / 1e9
+    prof = profile_fields(dom, bytes_pf[dom] * per_launch, dom_ms, wl)
     valu, valu_src = pmc_valu(dom, wl)
     issue = None
     if valu:
-        rate = valu / (stage_ms[dom] * 1e-3) / 1e9
+        rate = valu / (dom_ms * 1e-3) / 1e9
         issue = {"bound": "valu", "achieved": round(rate, 1), "peak": VALU_PEAK_GIPS, "unit": "G wave-instr/s",
                  "frac": round(rate / VALU_PEAK_GIPS, 4), "valu_per_launch": valu, "source": valu_src,
                  "source_stale": profile_hash(ROOT / "profiles" / valu_src) != source_hash(),
@@ -680,8 +686,11 @@ def main():
                          "algorithmic_bytes_per_launch": int(bytes_pf[dom] * per_launch),
                          "units_per_launch": per_launch,
                          "event_ms_note": "HIP events on the launching stream around the stage, mean over the timed "
-                                          "steps and the lanes",
-                         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()}, "issue": issue,
+                                          "steps and the lanes (the timed steps record only this stage's events)",
+                         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
+                         "stage_ms_note": "every stage's HIP-event ms over the warmup steps (all boundaries recorded "
+                                          "there; used to pick the dominant stage when no kernel trace is committed)",
+                         "issue": issue,
                          # the S lanes launch the same kernel on S streams at once, so a
                          # launch's duration is shared with S - 1 concurrent launches
                          "concurrent_launches": S,

@@ -156,7 +156,10 @@ int orbx_extractor_set_node_capacity(orbx_extractor* ex, int cap);
 /* Per-stage HIP-event timing (ms) of extraction calls, averaged over the (up to 64)
  * most recent calls made since orbx_extractor_set_timing(ex, 1), which also resets the
  * average.  Events are recorded on the launch stream between the stages, so a timed
- * loop is measured without synchronising inside it.  Names are static strings. */
+ * loop is measured without synchronising inside it.  Names are static strings.
+ * enable = 2 + s (s = 0 pyramid .. 4 describe) records only stage s's two boundary events
+ * (each recorded event costs the pipelined step ~0.2 %: bench.py times one stage live);
+ * stage_times then returns that stage alone. */
 int orbx_extractor_set_timing(orbx_extractor* ex, int enable);
 int orbx_extractor_stage_times(orbx_extractor* ex, int max_stages, const char** names, float* ms,
                                int* n_stages);
@@ -240,6 +243,12 @@ typedef struct {
 } orbx_track;
 
 typedef struct orbx_matcher orbx_matcher;
+
+/* Failure of the sequential replay (every SearchByProjection form): its fixpoint has an
+ * iteration guard that no valid input reaches.  The single-call forms below then return
+ * ORBX_ERR_STATE (the MapPoint output is partial); the batched device forms
+ * (orbx_match_sequence_device(_ex), orbx_search_local_points_device) write -1 into that
+ * frame's nmatches entry, which a caller must treat as a failed frame, never as a count. */
 
 /* ORBmatcher::ORBmatcher(nnratio, checkOri) (ORBmatcher.h:57), bound to HIP device
  * `device` with its own stream and scratch buffers. */
@@ -363,7 +372,9 @@ typedef struct {
     int nlevels;
     const float* scale_factors;   /* host: mvScaleFactors (nlevels) */
     const int32_t* local_off;     /* host: [B + 1] */
-    const int32_t* local_ids;     /* device: local map MapPoint ids, frame after frame */
+    const int32_t* local_ids;     /* device: local map MapPoint ids, frame after frame; ids (here and in
+                                     frame_mp) must be < mps->n: an id outside the table is treated as
+                                     a NULL entry (never read out of bounds) */
     float th;                     /* 1; 3 for RGB-D; 5 right after a relocalisation (Tracking.cc:1320-1331) */
     float viewing_cos_limit;      /* 0.5 (Tracking.cc:1314) */
     int32_t* frame_mp;            /* [B][cap] in/out */

@@ -63,6 +63,7 @@ struct orbx_extractor {
     // measured without synchronising inside it; stage_times averages the ring.
     static constexpr int kRing = 64;
     bool timing = false;
+    int timing_stage = -1;  // -1: every stage boundary; s >= 0: only stage s's two events
     hipEvent_t ev[kRing][kStages + 1] = {};
     long long ncalls = 0;
     // host-API staging
@@ -92,7 +93,8 @@ namespace {
 
 void free_buffers(DeviceBuffers& db) {
     void* ptrs[] = {db.lv, db.cells, db.rtab, db.pyr, db.blur, db.score, db.slots, db.cell_count,
-                    db.keys, db.key_node, db.kept, db.kept_count, db.status, db.oct_stamps};
+                    db.keys, db.key_node, db.kept, db.kept_count, db.status, db.oct_stamps, db.dt_list,
+                    db.dt_tile};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     db = DeviceBuffers();
@@ -128,6 +130,8 @@ int prepare(orbx_extractor* ex, int W, int H, int batch) {
     HIP_TRY(dalloc(&db.key_node, B * (size_t)p.keys_per_frame));
     HIP_TRY(dalloc(&db.kept, B * (size_t)p.kept_per_frame));
     HIP_TRY(dalloc(&db.kept_count, B * (size_t)p.L));
+    HIP_TRY(dalloc(&db.dt_list, B * (size_t)p.kept_per_frame));
+    HIP_TRY(dalloc(&db.dt_tile, B * (size_t)p.tiles_total));
     HIP_TRY(dalloc(&db.status, B));
     if (getenv("ORBX_OCT_STAMPS")) HIP_TRY(dalloc(&db.oct_stamps, B * (size_t)p.L * 8));
     HIP_TRY(hipMemcpyAsync(db.lv, p.lv, sizeof(LevelGeom) * kMaxLevels, hipMemcpyHostToDevice, ex->stream));
@@ -153,11 +157,17 @@ int run_device(orbx_extractor* ex, int batch, const uint8_t* d_imgs, size_t fram
     int rc = prepare(ex, W, H, batch);
     if (rc != ORBX_OK) return rc;
     hipEvent_t* ev = nullptr;
+    hipEvent_t sel[kStages + 1] = {};
     if (ex->timing) {
         hipEvent_t* slot = ex->ev[ex->ncalls % orbx_extractor::kRing];
         for (int i = 0; i <= kStages; i++)
             if (!slot[i]) HIP_TRY(hipEventCreate(&slot[i]));
         ev = slot;
+        if (ex->timing_stage >= 0) {  // only the timed stage's boundaries are recorded
+            sel[ex->timing_stage] = slot[ex->timing_stage];
+            sel[ex->timing_stage + 1] = slot[ex->timing_stage + 1];
+            ev = sel;
+        }
     }
     hipError_t e = launch_extract(ex->plan, ex->db, batch, d_imgs, frame_pitch, stride, d_kps, d_desc, cap, d_n,
                                   stream, ev, ex->stage_ev, ex->stage_after);
@@ -454,7 +464,9 @@ int orbx_extractor_set_node_capacity(orbx_extractor* ex, int cap) {
 
 int orbx_extractor_set_timing(orbx_extractor* ex, int enable) {
     if (!ex) return fail(ORBX_ERR_ARG, "null extractor");
+    if (enable < 0 || enable > 1 + kStages - 1) return fail(ORBX_ERR_ARG, "timing: 0, 1 or 2 + stage (0..4)");
     ex->timing = enable != 0;
+    ex->timing_stage = enable >= 2 ? enable - 2 : -1;
     ex->ncalls = 0;
     return ORBX_OK;
 }
@@ -464,6 +476,23 @@ int orbx_extractor_stage_times(orbx_extractor* ex, int max_stages, const char** 
     if (ex->ncalls == 0) return fail(ORBX_ERR_STATE, "no timed extraction yet");
     const long long last = ex->ncalls - 1;
     const int nslots = ex->ncalls < orbx_extractor::kRing ? (int)ex->ncalls : orbx_extractor::kRing;
+    if (ex->timing_stage >= 0) {  // one stage timed
+        const int st = ex->timing_stage;
+        HIP_TRY(hipEventSynchronize(ex->ev[last % orbx_extractor::kRing][st + 1]));
+        double sum = 0.0;
+        for (int k = 0; k < nslots; k++) {
+            hipEvent_t* e = ex->ev[(last - k) % orbx_extractor::kRing];
+            float t = 0.f;
+            HIP_TRY(hipEventElapsedTime(&t, e[st], e[st + 1]));
+            sum += t;
+        }
+        if (max_stages >= 1) {
+            if (names) names[0] = kStageNames[st];
+            if (ms) ms[0] = (float)(sum / nslots);
+        }
+        if (n_stages) *n_stages = max_stages >= 1 ? 1 : 0;
+        return ORBX_OK;
+    }
     HIP_TRY(hipEventSynchronize(ex->ev[last % orbx_extractor::kRing][kStages - 1]));
     int n = kStages < max_stages ? kStages : max_stages;
     for (int i = 0; i < n; i++) {

@@ -986,7 +986,9 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
                                                 uint32_t* __restrict__ keys, int* __restrict__ key_node,
                                                 int keys_pf, uint32_t* __restrict__ kept, int kept_pf,
                                                 int* __restrict__ kept_count, int* __restrict__ status,
-                                                int NC, int nframes, unsigned long long* __restrict__ stamps) {
+                                                int NC, int nframes, unsigned long long* __restrict__ stamps,
+                                                uint16_t* __restrict__ dt_list, uint32_t* __restrict__ dt_tile,
+                                                int tiles_pf) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_tmp[8];
     __shared__ int s_scal[16];
@@ -1098,6 +1100,8 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
             atomicOr(&status[f], kStatusNodeOverflow);
             kept_count[(size_t)f * L + l] = 0;
         }
+        if (dt_list)
+            for (int t = tid; t < g.tiles_x * g.tiles_y; t += 256) dt_tile[(size_t)f * tiles_pf + g.tile_first + t] = 0u;
         return;
     }
 
@@ -1431,6 +1435,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
         out[j] = K[k];
     }
     if (tid == 0) {
+        s_scal[7] = outn;
         kept_count[(size_t)f * L + l] = outn;
         if (size > g.ncap) atomicOr(&status[f], kStatusNodeOverflow);
         if (st) {
@@ -1441,6 +1446,34 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
     };
     if (n <= kOctKeysReg) tail(std::true_type{});
     else tail(std::false_type{});
+
+    // k_describe_tiles' bins: the kept slots of every level tile (k_level_tiles' 64 x 48
+    // grid), counted, then listed tile after tile (any order inside a tile: each slot's
+    // output position is its own).  The node arrays sa / sb are free now; the host checks
+    // that a level's tiles fit in NC entries.
+    if (dt_list) {
+        const int ntl = g.tiles_x * g.tiles_y;
+        int* const tcnt = sa;
+        int* const tnum = sb;
+        auto tile_of = [&](uint32_t kk) {
+            return (int)((key_y(kk) + kMinBorder) / kLtTH) * g.tiles_x + ((key_x(kk) + kMinBorder) >> 6);
+        };
+        for (int t = tid; t < ntl; t += 256) tcnt[t] = 0;
+        __syncthreads();  // also publishes s_scal[7] and the kept slots written above
+        const int outn = s_scal[7];
+        const uint32_t* out = kept + (size_t)f * kept_pf + g.out_off;
+        for (int j = tid; j < outn; j += 256) atomicAdd(&tcnt[tile_of(out[j])], 1);
+        __syncthreads();
+        for (int t = tid; t < ntl; t += 256) tnum[t] = tcnt[t];
+        __syncthreads();
+        block_exscan(tcnt, ntl, s_tmp);
+        __syncthreads();
+        uint32_t* dtt = dt_tile + (size_t)f * tiles_pf + g.tile_first;
+        for (int t = tid; t < ntl; t += 256) dtt[t] = ((uint32_t)tcnt[t] << 16) | (uint32_t)tnum[t];
+        __syncthreads();
+        uint16_t* dl = dt_list + (size_t)f * kept_pf + g.out_off;
+        for (int j = tid; j < outn; j += 256) dl[atomicAdd(&tcnt[tile_of(out[j])], 1)] = (uint16_t)j;
+    }
 }
 
 // ------------------------------------------------------------------ angle + descriptor
@@ -1784,6 +1817,186 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     }
 }
 
+// Tile-major describe (dense frames: configs[4]'s 5000 keypoints, ~16 per level tile).
+// One workgroup per level tile of k_level_tiles' 64 x 48 grid: the tile plus an 18-px
+// halo of the level (rows Y0-18 .. Y0+65, 128 columns from (X0-18) & ~15) is staged in
+// LDS once, raw and blurred, in 16-byte row loads, and every kept keypoint the octree
+// binned into the tile is described from there: IC_Angle's rows (cc:59-106) and the
+// rBRIEF samples (cc:118-172) become LDS reads, instead of each keypoint staging its own
+// 37 x 37 blurred patch and 31 raw rows (k_describe: ~2.6 KB per keypoint, 6x a dense
+// frame's two images).  Four keypoints per wave as in k_describe, 16 per round.
+constexpr int kDtP = 128;               // staged row pitch (bytes)
+constexpr int kDtRows = kLtTH + 36;     // tile rows + 18-px halo above and below
+__global__ __launch_bounds__(256) void k_describe_tiles(const uint8_t* __restrict__ pyr,
+                                                         const uint8_t* __restrict__ blur, long long fb,
+                                                         const LevelGeom* __restrict__ lv, int L,
+                                                         const uint32_t* __restrict__ kept, int kept_pf,
+                                                         const int* __restrict__ kept_count,
+                                                         const uint16_t* __restrict__ dt_list,
+                                                         const uint32_t* __restrict__ dt_tile, int tiles_pf,
+                                                         orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                         int cap, int* __restrict__ n_out, int nframes) {
+    __shared__ __align__(16) uint8_t s_raw[kDtRows][kDtP];
+    __shared__ __align__(16) uint8_t s_blr[kDtRows][kDtP];
+    int f, tile;
+    xcd_frame_block(tiles_pf, nframes, f, tile);
+    const int tid = threadIdx.x;
+    const int* kc = kept_count + (size_t)f * L;
+    if (tile == 0 && tid == 0) {
+        int tot = 0;
+        for (int l2 = 0; l2 < L; l2++) tot += kc[l2];
+        n_out[f] = tot;
+    }
+    const uint32_t td = dt_tile[(size_t)f * tiles_pf + tile];
+    const int cnt = (int)(td & 0xffffu), start = (int)(td >> 16);
+    if (cnt == 0) return;  // whole workgroup, before any barrier
+    int l = 0;
+    while (l + 1 < L && tile >= lv[l + 1].tile_first) l++;
+    const LevelGeom& g = lv[l];
+    int base = 0;  // output index of the level's first keypoint
+    for (int l2 = 0; l2 < l; l2++) base += kc[l2];
+    const int t = tile - g.tile_first;
+    const int ty = t / g.tiles_x;
+    const int X0 = (t - ty * g.tiles_x) * kLtTW, Y0 = ty * kLtTH;
+    const int Xs = max(0, (X0 - 18) & ~15), Ys = max(0, Y0 - 18);
+    const int nrows = min(g.h, Y0 + kLtTH + 18) - Ys;
+    const int nch = (min(g.w, X0 + kLtTW + 18) - Xs + 15) >> 4;  // 16-byte chunks per row (<= 8)
+    {
+        // all loads of a thread issued before its LDS stores; chunks past the level's
+        // right edge are not loaded (nothing samples them)
+        constexpr int kPer = (kDtRows * (kDtP / 16) + 255) / 256;
+        const uint8_t* pr = pyr + (size_t)f * fb + g.off + (size_t)Ys * g.pitch + Xs;
+        const uint8_t* br = blur + (size_t)f * fb + g.off + (size_t)Ys * g.pitch + Xs;
+        // (a thread past the region loads and stores the region's last chunk again)
+        uint4 a[kPer], b[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int i = tid + 256 * k;
+            const int r = min(i >> 3, nrows - 1), c = min(i & 7, nch - 1);
+            const uint32_t o = (uint32_t)(r * g.pitch + 16 * c);
+            a[k] = *(const uint4*)(pr + o);
+            b[k] = *(const uint4*)(br + o);
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int i = tid + 256 * k;
+            const int r = min(i >> 3, nrows - 1), c = min(i & 7, nch - 1);
+            *(uint4*)&s_raw[r][16 * c] = a[k];
+            *(uint4*)&s_blr[r][16 * c] = b[k];
+        }
+    }
+    __syncthreads();
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int qt = lane >> 4, ql = lane & 15;
+    const uint32_t* kl = kept + (size_t)f * kept_pf + g.out_off;
+    const uint16_t* dl = dt_list + (size_t)f * kept_pf + g.out_off + start;
+    float lv_scale = g.scale, lv_size = g.kp_size;
+    for (int s0 = wave * 4; s0 < cnt; s0 += 16) {  // wave-uniform; no barriers below
+        const int s = s0 + qt;
+        const bool in = s < cnt;
+        const int j = in ? dl[s] : 0;
+        const int o = base + j;
+        const bool valid = in && o < cap;
+        const uint32_t key = kl[j];
+        // an empty quarter samples the tile's first keypoint and is masked
+        const int x = key_x(valid ? key : kl[dl[0]]) + kMinBorder;
+        const int y = key_y(valid ? key : kl[dl[0]]) + kMinBorder;
+        const int resp = key_resp(key);
+        // IC_Angle: rows v1 = ql - 15 and v2 = ql + 1 (quarter lane 15 has none), 36 bytes
+        // from (x - 15) & ~3 as nine dword LDS reads each
+        const int v1 = ql - 15, v2 = min(ql + 1, 15);
+        const int d0 = (x - 15) & 3;
+        const int cs0 = ((x - 15) & ~3) - Xs;
+        auto row_sums = [&](int rr, int av, uint32_t& cs, uint32_t& ws) {
+            const uint32_t* rp = (const uint32_t*)&s_raw[rr][cs0];
+            const uint4* cm4 = (const uint4*)c_icm[d0][av];
+            const uint4* cw4 = (const uint4*)c_icw[d0][av];
+            const uint4 m0 = cm4[0], m1 = cm4[1], m2 = cm4[2], w0 = cw4[0], w1 = cw4[1], w2 = cw4[2];
+            const uint32_t cm[9] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w, m2.x};
+            const uint32_t cw[9] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x};
+            cs = 0;
+            ws = 0;
+#pragma unroll
+            for (int k = 0; k < 9; k++) {
+                const uint32_t d = rp[k];
+                cs = __builtin_amdgcn_udot4(d, cm[k], cs, false);
+                ws = __builtin_amdgcn_udot4(d, cw[k], ws, false);
+            }
+        };
+        uint32_t cs1, ws1, cs2, ws2;
+        row_sums(y + v1 - Ys, -v1, cs1, ws1);
+        row_sums(y + v2 - Ys, v2, cs2, ws2);
+        const bool row2_ok = ql < 15;
+        int m10 = ((int)ws1 - 15 * (int)cs1) + (row2_ok ? (int)ws2 - 15 * (int)cs2 : 0);
+        int m01 = v1 * (int)cs1 + (row2_ok ? v2 * (int)cs2 : 0);
+#pragma unroll
+        for (int o2 = 8; o2 > 0; o2 >>= 1) {  // within the 16-lane quarter
+            m10 += __shfl_xor(m10, o2);
+            m01 += __shfl_xor(m01, o2);
+        }
+        const float angle = fast_atan2((float)m01, (float)m10);
+        const float factorPI = (float)(3.14159265358979323846 / 180.f);
+        const float rad = angle * factorPI;
+        double cd, sd;
+        sincos_0_2pi((double)rad, cd, sd);  // == (float)cos/sin((double)rad) (orbx_sincos.h)
+        const float ca = (float)cd, sb = (float)sd;
+        // cvRound by the 1.5 * 2^23 bias, as in k_describe, over the staged blurred tile
+        const uint8_t* bp = &s_blr[0][0];
+        const uint32_t center = (uint32_t)((y - Ys) * kDtP + (x - Xs)) - (0x400000u * (uint32_t)kDtP + 0x4B400000u);
+        const float kRound = 12582912.0f;
+        auto sample = [&](float px, float py) -> int {  // fused like the reference's build (H4)
+            const uint32_t ry = __float_as_uint(fmaf(px, sb, py * ca) + kRound);
+            const uint32_t rx = __float_as_uint(fmaf(px, ca, -(py * sb)) + kRound);
+            return bp[center + __umul24(ry, (uint32_t)kDtP) + rx];
+        };
+        auto pair_test = [&](int q) -> bool {
+            const float x0 = (float)(int8_t)(q & 0xff), y0 = (float)(int8_t)((q >> 8) & 0xff);
+            const float x1 = (float)(int8_t)((q >> 16) & 0xff), y1 = (float)(int8_t)(q >> 24);
+            return sample(x0, y0) < sample(x1, y1);
+        };
+        int pat[16];
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            const int4 p4 = ((const int4*)c_pattern[ql])[v];
+            pat[4 * v] = p4.x;
+            pat[4 * v + 1] = p4.y;
+            pat[4 * v + 2] = p4.z;
+            pat[4 * v + 3] = p4.w;
+        }
+        const int qsh = 16 * (qt & 1);
+        uint32_t words[8];
+#pragma unroll
+        for (int w = 0; w < 8; w++) {
+            const unsigned long long ba = __ballot(pair_test(pat[2 * w]));
+            const unsigned long long bb = __ballot(pair_test(pat[2 * w + 1]));
+            const uint32_t la = (qt & 2) ? (uint32_t)(ba >> 32) : (uint32_t)ba;
+            const uint32_t lb = (qt & 2) ? (uint32_t)(bb >> 32) : (uint32_t)bb;
+            words[w] = ((la >> qsh) & 0xffffu) | ((lb >> qsh) << 16);
+        }
+        if (valid && ql < 2) {
+            uint4* d = (uint4*)(desc + ((size_t)f * cap + o) * 32);
+            d[ql] = ql == 0 ? make_uint4(words[0], words[1], words[2], words[3])
+                            : make_uint4(words[4], words[5], words[6], words[7]);
+        }
+        if (valid && ql == 0) {
+            float fx = (float)x, fy = (float)y;
+            if (l != 0) {
+                fx = fx * lv_scale;
+                fy = fy * lv_scale;
+            }
+            orbx_keypoint kpo;
+            kpo.x = fx;
+            kpo.y = fy;
+            kpo.size = lv_size;
+            kpo.angle = angle;
+            kpo.response = (float)resp;
+            kpo.octave = l;
+            kpo.class_id = -1;
+            kps[(size_t)f * cap + o] = kpo;
+        }
+    }
+}
+
 // ------------------------------------------------------------------ host launch
 
 hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, const uint8_t* d_imgs,
@@ -1793,8 +2006,11 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     const int L = plan.L;
     const long long fb = plan.pyr_frame_bytes;
     const int ncells = (int)plan.cells.size();
-    if (ev) (void)hipEventRecord(ev[0], stream);
-    {
+    // ORBX_DUP_STAGE=k (measurement knob): launch stage k (1 pyramid .. 5 describe) twice --
+    // every stage is idempotent -- so a pipelined run prices that stage's marginal cost
+    static const int dup = getenv("ORBX_DUP_STAGE") ? atoi(getenv("ORBX_DUP_STAGE")) : 0;
+    if (ev && ev[0]) (void)hipEventRecord(ev[0], stream);
+    for (int rep = 0; rep < (dup == 1 ? 2 : 1); rep++) {
         // one launch per pyramid segment (orbx_geometry.h): the first reads the input
         // frames, a later one its input level from the pyramid the previous one wrote
         auto kern = plan.pz_win ? k_pyramid<true> : k_pyramid<false>;
@@ -1816,27 +2032,27 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
                                db.status);
         }
     }
-    if (ev) (void)hipEventRecord(ev[1], stream);
+    if (ev && ev[1]) (void)hipEventRecord(ev[1], stream);
     if (stage_ev && stage_after == 1) (void)hipEventRecord(stage_ev, stream);
-    {
+    for (int rep = 0; rep < (dup == 2 ? 2 : 1); rep++) {
         dim3 grid(plan.tiles_total * batch);
         int tq = plan.prm.ini_th < plan.prm.min_th ? plan.prm.ini_th : plan.prm.min_th;
         tq = tq < 0 ? 0 : (tq > 255 ? 255 : tq);
         hipLaunchKernelGGL(k_level_tiles, grid, dim3(256), 0, stream, db.pyr, db.blur, db.score, fb, db.lv, L,
                            plan.tiles_total, batch, tq);
     }
-    if (ev) (void)hipEventRecord(ev[2], stream);
+    if (ev && ev[2]) (void)hipEventRecord(ev[2], stream);
     if (stage_ev && stage_after == 2) (void)hipEventRecord(stage_ev, stream);
-    {
+    for (int rep = 0; rep < (dup == 3 ? 2 : 1); rep++) {
         dim3 grid(((ncells + 3) / 4) * batch);
         const size_t fc_lds = 4 * (size_t)((((plan.fc_wr + 2) * kFcStride + 2 * plan.fc_wr * plan.fc_wc) + 15) & ~15);
         hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), fc_lds, stream, db.score, fb, db.cells, ncells,
                            plan.prm.ini_th, plan.prm.min_th, db.slots, plan.slots_per_frame, db.cell_count, batch,
                            plan.fc_wr, plan.fc_wc);
     }
-    if (ev) (void)hipEventRecord(ev[3], stream);
+    if (ev && ev[3]) (void)hipEventRecord(ev[3], stream);
     if (stage_ev && stage_after == 3) (void)hipEventRecord(stage_ev, stream);
-    {
+    for (int rep = 0; rep < (dup == 4 ? 2 : 1); rep++) {
         const int NC = (plan.max_ncap + 63) & ~63;
         const size_t lds = (size_t)NC * kOctNodeBytes;
         // int16 node ids / ranks, and one workgroup's LDS (beside its static arrays)
@@ -1849,17 +2065,24 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
         dim3 grid(L * batch);
         hipLaunchKernelGGL(k_octree, grid, dim3(256), lds, stream, db.lv, L, db.slots, plan.slots_per_frame,
                            db.cells, db.cell_count, ncells, db.keys, db.key_node, plan.keys_per_frame,
-                           db.kept, plan.kept_per_frame, db.kept_count, db.status, NC, batch, db.oct_stamps);
+                           db.kept, plan.kept_per_frame, db.kept_count, db.status, NC, batch, db.oct_stamps,
+                           plan.desc_tiles ? db.dt_list : nullptr, db.dt_tile, plan.tiles_total);
     }
-    if (ev) (void)hipEventRecord(ev[4], stream);
+    if (ev && ev[4]) (void)hipEventRecord(ev[4], stream);
     if (stage_ev && stage_after == 4) (void)hipEventRecord(stage_ev, stream);
-    {
-        dim3 grid(((plan.kept_per_frame + 15) / 16) * batch);
-        auto kern = plan.kept_per_frame <= kDescGldsMaxSlots ? k_describe<ORBX_DESC_DMA> : k_describe<0>;
-        hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, db.pyr, db.blur, fb, db.lv, L, db.kept,
-                           plan.kept_per_frame, db.kept_count, (orbx_keypoint*)kps, desc, cap, n_per_frame, batch);
+    for (int rep = 0; rep < (dup == 5 ? 2 : 1); rep++) {
+        if (plan.desc_tiles) {
+            hipLaunchKernelGGL(k_describe_tiles, dim3(plan.tiles_total * batch), dim3(256), 0, stream, db.pyr,
+                               db.blur, fb, db.lv, L, db.kept, plan.kept_per_frame, db.kept_count, db.dt_list,
+                               db.dt_tile, plan.tiles_total, (orbx_keypoint*)kps, desc, cap, n_per_frame, batch);
+        } else {
+            dim3 grid(((plan.kept_per_frame + 15) / 16) * batch);
+            auto kern = plan.kept_per_frame <= kDescGldsMaxSlots ? k_describe<ORBX_DESC_DMA> : k_describe<0>;
+            hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, db.pyr, db.blur, fb, db.lv, L, db.kept,
+                               plan.kept_per_frame, db.kept_count, (orbx_keypoint*)kps, desc, cap, n_per_frame, batch);
+        }
     }
-    if (ev) (void)hipEventRecord(ev[5], stream);
+    if (ev && ev[5]) (void)hipEventRecord(ev[5], stream);
     return hipGetLastError();
 }
 

@@ -337,6 +337,18 @@ bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
     plan.keys_per_frame = key_off;
     plan.kept_per_frame = out_off;
     plan.tiles_total = tile_first;
+    {
+        // k_describe_tiles (ORBX_DESC_TILES=1; measured slower than k_describe, DESIGN.md
+        // section 4 item 5): k_octree bins each level's kept slots into its tiles with
+        // NC-entry LDS counters and 16-bit list offsets
+        const int NC = (plan.max_ncap + 63) & ~63;
+        bool fits = true;
+        for (int l = 0; l < plan.L; l++)
+            fits = fits && plan.lv[l].tiles_x * plan.lv[l].tiles_y <= NC && plan.lv[l].ncap < 65536;
+        const char* e = getenv("ORBX_DESC_TILES");
+        const int mode = e ? atoi(e) : -1;
+        plan.desc_tiles = fits && mode == 1;
+    }
     plan.rtab.resize(plan.rtab.size() + 64, 0);  // k_pyramid reads row taps in batches of 8 rows
     plan.ok = true;
     return true;

@@ -19,6 +19,7 @@ constexpr int kEdge = 19;        // EDGE_THRESHOLD, ORBextractor.cc:46
 constexpr int kMinBorder = 16;   // EDGE_THRESHOLD - 3, ORBextractor.cc:1032
 constexpr int kMaxIni = 16;      // octree root nodes supported per level
 constexpr int kCellMax = 64;     // max detection-window width/height of a FAST cell
+
 #ifndef ORBX_LT_TH
 #define ORBX_LT_TH 48
 #endif
@@ -120,6 +121,10 @@ struct Plan {
     bool pz_win = false;            // k_pyramid<true>: every 4 columns' resize taps span <= 8 source bytes
     int fc_wr = 0, fc_wc = 0;       // largest FAST detection window (rows, cols)
     int max_ncap = 0;
+    // describe in level-tile order (k_describe_tiles, bins from k_octree) instead of
+    // keypoint by keypoint: ORBX_DESC_TILES=1, when every level's tiles fit the octree's
+    // NC-entry LDS arrays (a measured alternative, slower at configs[1] and [4])
+    bool desc_tiles = false;
     int max_key_cap = 0;
     bool ok = false;
     const char* why = nullptr;

@@ -24,6 +24,8 @@ struct DeviceBuffers {
     int* key_node = nullptr;         // [B][keys_per_frame] octree node of each candidate
     uint32_t* kept = nullptr;        // [B][kept_per_frame] kept keypoints (octree list order)
     int* kept_count = nullptr;       // [B][L]
+    uint16_t* dt_list = nullptr;     // [B][kept_per_frame] kept slots listed tile after tile (k_describe_tiles)
+    uint32_t* dt_tile = nullptr;     // [B][tiles_total] per level tile: list start << 16 | count
     int* status = nullptr;           // [B] error flags
     unsigned long long* oct_stamps = nullptr;  // [B][L][8] k_octree phase stamps (ORBX_OCT_STAMPS)
 };

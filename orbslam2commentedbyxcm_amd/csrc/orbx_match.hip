@@ -1822,7 +1822,9 @@ __global__ __launch_bounds__(kLocalThreads) void k_local_build(LocalArgs A, Proj
     for (int i = tid; i < n; i += kLocalThreads) {
         const int mp = fmp[i];
         if (mp < 0) continue;
-        if (A.bad && A.bad[mp]) {  // Tracking.cc:1288-1290
+        // an id outside the MapPoint table (a caller error) is dropped like a NULL entry:
+        // never read past the table (orbx.h, orbx_search_local_points_device)
+        if ((unsigned)mp >= (unsigned)A.nmp || (A.bad && A.bad[mp])) {  // Tracking.cc:1288-1290
             fmp[i] = -1;
             continue;
         }
@@ -1843,7 +1845,7 @@ __global__ __launch_bounds__(kLocalThreads) void k_local_build(LocalArgs A, Proj
         const int mp = A.local_ids[j];
         ProjQuery q{};
         q.mp = -1;
-        bool in_view = !(A.bad && A.bad[mp]);
+        bool in_view = (unsigned)mp < (unsigned)A.nmp && !(A.bad && A.bad[mp]);
         if (in_view) {  // pMP->mnLastFrameSeen == mCurrentFrame.mnId (Tracking.cc:1306-1307)
             unsigned h = local_hash(mp, mask);
             while (true) {

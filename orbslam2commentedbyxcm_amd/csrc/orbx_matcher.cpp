@@ -58,7 +58,7 @@ struct Arena {
         cap = 0;
         bytes = (bytes + 15) & ~(size_t)15;
         hipError_t e = hipMalloc((void**)&base, bytes);
-        if (e == hipSuccess) e = hipHostMalloc((void**)&host, bytes, hipHostMallocMapped);
+        if (e == hipSuccess) e = hipHostMalloc((void**)&host, bytes, hipHostMallocMapped | hipHostMallocCoherent);
         if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&host_dev, host, 0);
         if (e == hipSuccess) cap = bytes;
         return e;
@@ -339,7 +339,10 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
         if (m->hmp) (void)hipHostFree(m->hmp);
         m->hmp = m->hmp_dev = nullptr;
         m->hmp_cap = 0;
-        HIP_TRY(hipHostMalloc((void**)&m->hmp, sizeof(int32_t) * ((size_t)n + 1), hipHostMallocMapped));
+        // coherent explicitly: the kernel's stores must be visible to the memcpy after the
+        // stream synchronise whatever the runtime's default coherence setting
+        HIP_TRY(hipHostMalloc((void**)&m->hmp, sizeof(int32_t) * ((size_t)n + 1),
+                              hipHostMallocMapped | hipHostMallocCoherent));
         HIP_TRY(hipHostGetDevicePointer((void**)&m->hmp_dev, m->hmp, 0));
         m->hmp_cap = (size_t)n + 1;
     }
@@ -382,6 +385,8 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
                 (double)(h[2] - h[1]) * 0.01, (double)(h[4] - h[2]) * 0.01, (double)(h[10] - h[4]) * 0.01,
                 (double)(h[11] - h[10]) * 0.01, (double)(h[3] - h[13]) * 0.01, h[7], h[5]);
     }
+    if (nm < 0)  // the replay's iteration guard fired: frame_mp is partial, never report it as matches
+        return fail(ORBX_ERR_STATE, "SearchByProjection replay did not converge (iteration guard)");
     if (nmatches) *nmatches = nm;
     return ORBX_OK;
 }

@@ -158,8 +158,13 @@ class ORBextractor:
         """Test hook: cap the octree node capacity per level (0 = the guaranteed bound)."""
         L.check(L.lib().orbx_extractor_set_node_capacity(self._h, int(cap)))
 
-    def set_timing(self, enable: bool = True) -> None:
-        L.check(L.lib().orbx_extractor_set_timing(self._h, 1 if enable else 0))
+    STAGES = ("pyramid", "score_blur", "fast_cells", "octree", "describe")
+
+    def set_timing(self, enable: bool = True, stage: str | None = None) -> None:
+        """HIP-event stage timing of the following calls (all stage boundaries, or only
+        `stage`'s two when given: fewer events in a timed loop)."""
+        v = 0 if not enable else (1 if stage is None else 2 + self.STAGES.index(stage))
+        L.check(L.lib().orbx_extractor_set_timing(self._h, v))
 
     def stage_times(self) -> dict:
         names = (C.c_char_p * 16)()

@@ -133,6 +133,7 @@ class SequencePipeline:
         # buffer is overwritten
         self.on_matched = on_matched
         self._timing = False
+        self._ext_timed = self._match_timed = False
         self.it = 0            # extractions issued
         self.pending = None    # buffer extracted but not yet matched (pipelined)
         self.last = None       # buffer holding the newest complete result
@@ -270,21 +271,30 @@ class SequencePipeline:
         """Octree status words of every frame of the newest extraction (0 = complete)."""
         return np.concatenate([e.status(b1 - b0) for e, (b0, b1) in zip(self.exs, self.bounds)])
 
-    def set_timing(self, enable: bool):
+    def set_timing(self, enable: bool, stage: str | None = None):
+        """HIP-event timing of the following steps: every stage of every lane and the
+        matcher, or (stage given) only that stage's launches -- an extraction stage's two
+        boundary events per lane, or the matcher's ("match")."""
+        ext = enable and stage != "match"
         for e in self.exs:
-            e.set_timing(enable)
+            e.set_timing(ext, None if stage == "match" else stage)
+        self._match_timed = bool(enable) and self.match and stage in (None, "match")
         if self.match:
-            self.matcher.set_timing(enable)
+            self.matcher.set_timing(self._match_timed)
+        self._ext_timed = bool(ext)
         self._timing = bool(enable)
         if enable and self.local_map:
             self._lt = []
 
     def stage_times(self) -> dict:
         """HIP-event stage times (ms per launch) averaged over the lanes' extractors (each
-        lane's launches time its own frames), plus the matcher's ("match")."""
-        per = [e.stage_times() for e in self.exs]
-        out = {k: sum(p[k] for p in per) / len(per) for k in per[0]}
-        if self.match:
+        lane's launches time its own frames), plus the matcher's ("match"): the stages
+        set_timing selected."""
+        out = {}
+        if self._ext_timed:
+            per = [e.stage_times() for e in self.exs]
+            out = {k: sum(p[k] for p in per) / len(per) for k in per[0]}
+        if self._match_timed:
             out["match"] = self.matcher.last_ms()
         if self.local_map and self._lt:
             out["local_map"] = sum(a.elapsed_time(b) for a, b in self._lt) / len(self._lt)

@@ -78,3 +78,30 @@ def test_other_configs_match_oracle(oracle, orbx_built, cfg):
     kps, desc = ex(img)
     kr, dr, _ = oracle.extract(img, oracle.params(nf, sf, nl, 20, 7))
     _cmp(kps, desc, kr, dr)
+
+
+@pytest.mark.parametrize("prm,size,B", [((1000, 1.2, 8, 20, 7), (640, 480), 8), ((5000, 1.2, 12, 20, 7), (640, 480), 8),
+                                        ((2000, 1.2, 8, 20, 7), (1241, 376), 4)])
+def test_describe_tiles_form_matches_oracle(oracle, orbx_built, monkeypatch, prm, size, B):
+    """The tile-major describe (ORBX_DESC_TILES=1: k_octree bins the kept slots by level
+    tile, k_describe_tiles stages each tile once) gives the same keypoints and
+    descriptors; the setting is read when an extractor plans a frame size."""
+    import torch
+
+    from oracle import checks
+    monkeypatch.setenv("ORBX_DESC_TILES", "1")
+    W, H = size
+    frames = synth.frames(B, W, H, first_seed=40)
+    ex = ORBextractor(*prm)
+    cap = ex.max_keypoints(W, H)
+    dev = torch.device("cuda", 0)
+    kps = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)
+    desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
+    n = torch.empty((B,), dtype=torch.int32, device=dev)
+    ex.extract_batch_device(torch.from_numpy(frames).to(dev), kps, desc, n)
+    torch.cuda.synchronize()
+    assert not ex.status().any()
+    from orbslam2commentedbyxcm_amd import _lib as L
+    k = kps.cpu().numpy().view(np.uint8).reshape(B, cap, 28).view(L.KEYPOINT_DTYPE).reshape(B, cap)
+    ref = checks.extract_all(frames, params=prm)
+    assert checks.compare_extraction(ref, k, desc.cpu().numpy(), n.cpu().numpy()) == []

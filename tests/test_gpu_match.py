@@ -498,3 +498,19 @@ def test_search_by_projection_without_queries(oracle, orbx_built):
     found = np.ones(len(A.keys), np.uint8)
     assert m.SearchByProjectionKeyFrame(B, cur, A, last_mp, mps, 10.0, 100, already_found=found) == 0
     assert np.array_equal(cur, cur0)
+
+
+def test_one_matcher_growing_frames(oracle, orbx_built):
+    """One drop-in matcher reused on frames of growing size: the host-mapped result buffer
+    (coherent) is reallocated for the larger frame, and every call matches the oracle."""
+    m = ORBmatcher(0.9, True)
+    for seed, prm in ((0, S.C1), (7, (2000, 1.2, 8, 20, 7)), (8, (3000, 1.2, 8, 20, 7)), (1, S.C1)):
+        A, B = S.two_views(oracle, seed, prm=prm)
+        mps = S.mappoints_from(A, seed)
+        last_mp = np.arange(len(A.keys), dtype=np.int32)
+        cur_gpu = np.full(len(B.keys), -1, np.int32)
+        n_gpu = m.SearchByProjectionFrame(B, cur_gpu, A, last_mp, mps, 15.0, True)
+        cur_ref = np.full(len(B.keys), -1, np.int32)
+        n_ref = oracle.sbp_frame(B, cur_ref, A, last_mp, mps, 15.0, True, True)
+        assert n_gpu == n_ref and n_ref > 300, (seed, n_gpu, n_ref)
+        assert np.array_equal(cur_gpu, cur_ref), (seed, np.nonzero(cur_gpu != cur_ref)[0][:10])
