@@ -468,7 +468,8 @@ def main():
                           match_after_stage=int(os.environ.get("ORBX_MATCH_AFTER", "0")),
                           lane_offset_stage=int(os.environ["ORBX_LANE_OFFSET"]) if "ORBX_LANE_OFFSET" in os.environ else None,
                           match_cu_stride=int(os.environ.get("ORBX_MATCH_CUSTRIDE", "1")),
-                          match_priority=int(os.environ.get("ORBX_MATCH_STREAM_PRIO", "0")))
+                          match_priority=int(os.environ.get("ORBX_MATCH_STREAM_PRIO", "0")),
+                          level0_in_place=os.environ.get("ORBX_L0_COPY") != "1")
     S = pl.S
     lane_off = pl.lane_offset_stage if pl.lane_ev is not None else None  # None: no offset applied
     d_frames = torch.from_numpy(frames_np).to(dev)

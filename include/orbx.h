@@ -153,6 +153,16 @@ int orbx_extractor_status_device(orbx_extractor* ex, const int32_t** d_status);
  * draining the whole device; takes effect at the next extraction. */
 int orbx_extractor_set_node_capacity(orbx_extractor* ex, int cap);
 
+/* Level 0 of the pyramid is the input image (ORBextractor.cc:1688-1690).  With enable = 1,
+ * orbx_extract_batch_device reads it in place from the caller's device frames instead of
+ * copying it into the extractor's pyramid (when the frames are 16-byte aligned, their
+ * frame pitch a multiple of 16 and their row stride a multiple of 64; otherwise it is
+ * copied as before).  The frames must then stay unchanged while the pyramid is in use:
+ * orbx_pyramid_level(_device) returns level 0 from them, and the stereo matchers, which
+ * read the pyramid's own layout, refuse the extractor (ORBX_ERR_STATE).  For the
+ * monocular front end (Frame's monocular constructor never reads mvImagePyramid). */
+int orbx_extractor_set_level0_in_place(orbx_extractor* ex, int enable);
+
 /* Per-stage HIP-event timing (ms) of extraction calls, averaged over the (up to 64)
  * most recent calls made since orbx_extractor_set_timing(ex, 1), which also resets the
  * average.  Events are recorded on the launch stream between the stages, so a timed

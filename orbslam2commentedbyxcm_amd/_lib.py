@@ -47,7 +47,7 @@ EXPORTED = [
     "orbx_compute_image_bounds", "orbx_assign_features_to_grid", "orbx_assign_features_to_grid_device",
     "orbx_fuse", "orbx_fuse_sim3", "orbx_search_by_sim3", "orbx_compute_distinctive_descriptors",
     "orbx_compute_distinctive_descriptors_device", "orbx_extractor_status", "orbx_extractor_status_device",
-    "orbx_extractor_set_node_capacity", "orbx_compute_stereo_matches_batch_device",
+    "orbx_extractor_set_node_capacity", "orbx_extractor_set_level0_in_place", "orbx_compute_stereo_matches_batch_device",
     "orbx_search_for_triangulation_batch_device", "orbx_match_sequence_device_ex",
     "orbx_search_local_points_device", "orbx_create_mappoints_device",
 ]
@@ -139,6 +139,7 @@ def lib() -> C.CDLL:
     L.orbx_extractor_status.argtypes = [vp, C.c_int, ip, ip]
     L.orbx_extractor_status_device.argtypes = [vp, C.POINTER(vp)]
     L.orbx_extractor_set_node_capacity.argtypes = [vp, C.c_int]
+    L.orbx_extractor_set_level0_in_place.argtypes = [vp, C.c_int]
     L.orbx_extractor_set_timing.argtypes = [vp, C.c_int]
     L.orbx_extractor_stage_times.argtypes = [vp, C.c_int, C.POINTER(C.c_char_p), fp, ip]
     L.orbx_pyramid_level.argtypes = [vp, C.c_int, C.c_int, u8p, C.c_size_t, ip, ip]

@@ -62,6 +62,11 @@ struct orbx_extractor {
     // Stage timing: a ring of event sets, one per timed call, so a whole timed loop is
     // measured without synchronising inside it; stage_times averages the ring.
     static constexpr int kRing = 64;
+    // orbx_extractor_set_level0_in_place: level 0 stays in the caller's device frames (no
+    // copy into the pyramid) when they are aligned for it; l0_* describe the last call's
+    bool l0_in_place = false;
+    const uint8_t* l0 = nullptr;
+    size_t l0_fp = 0, l0_pitch = 0;
     bool timing = false;
     int timing_stage = -1;  // -1: every stage boundary; s >= 0: only stage s's two events
     hipEvent_t ev[kRing][kStages + 1] = {};
@@ -169,8 +174,13 @@ int run_device(orbx_extractor* ex, int batch, const uint8_t* d_imgs, size_t fram
             ev = sel;
         }
     }
+    const bool inplace = ex->l0_in_place && !ex->plan.desc_tiles && (uintptr_t)d_imgs % 16 == 0 && stride % 64 == 0 &&
+                         frame_pitch % 16 == 0;
     hipError_t e = launch_extract(ex->plan, ex->db, batch, d_imgs, frame_pitch, stride, d_kps, d_desc, cap, d_n,
-                                  stream, ev, ex->stage_ev, ex->stage_after);
+                                  stream, ev, ex->stage_ev, ex->stage_after, inplace);
+    ex->l0 = inplace ? d_imgs : nullptr;
+    ex->l0_fp = frame_pitch;
+    ex->l0_pitch = stride;
     if (e != hipSuccess) return hip_fail(e, "launch_extract");
     if (ex->db.oct_stamps) {  // diagnostics: per-level k_octree phase times (us) to stderr
         const int L = ex->plan.L;
@@ -287,6 +297,7 @@ int ensure_host_staging(orbx_extractor* ex, size_t in_bytes, size_t out_slots, i
 int orbx::extractor_pyramid(orbx_extractor* ex, PyrView* v) {
     if (!ex || !v) return fail(ORBX_ERR_ARG, "null argument");
     if (!ex->have_pyramid) return fail(ORBX_ERR_STATE, "no extraction yet");
+    if (ex->l0) return fail(ORBX_ERR_STATE, "pyramid level 0 was read in place (orbx_extractor_set_level0_in_place)");
     const Plan& p = ex->plan;
     v->base = ex->db.pyr;
     v->frame_bytes = p.pyr_frame_bytes;
@@ -448,6 +459,12 @@ int orbx_extractor_status_device(orbx_extractor* ex, const int32_t** d_status) {
     return ORBX_OK;
 }
 
+int orbx_extractor_set_level0_in_place(orbx_extractor* ex, int enable) {
+    if (!ex) return fail(ORBX_ERR_ARG, "null extractor");
+    ex->l0_in_place = enable != 0;
+    return ORBX_OK;
+}
+
 int orbx_extractor_set_node_capacity(orbx_extractor* ex, int cap) {
     if (!ex || cap < 0) return fail(ORBX_ERR_ARG, "bad argument");
     HIP_TRY(hipSetDevice(ex->device));
@@ -588,8 +605,13 @@ int orbx_pyramid_level_device(orbx_extractor* ex, int frame, int level, const ui
     if (!ex || !ex->have_pyramid) return fail(ORBX_ERR_STATE, "no extraction yet");
     if (frame < 0 || frame >= ex->last_batch || level < 0 || level >= ex->plan.L) return fail(ORBX_ERR_ARG, "range");
     const LevelGeom& g = ex->plan.lv[level];
-    if (d_ptr) *d_ptr = ex->db.pyr + (size_t)frame * ex->plan.pyr_frame_bytes + g.off;
-    if (pitch) *pitch = (size_t)g.pitch;
+    if (level == 0 && ex->l0) {  // level 0 read in place: the caller's frame
+        if (d_ptr) *d_ptr = ex->l0 + (size_t)frame * ex->l0_fp;
+        if (pitch) *pitch = ex->l0_pitch;
+    } else {
+        if (d_ptr) *d_ptr = ex->db.pyr + (size_t)frame * ex->plan.pyr_frame_bytes + g.off;
+        if (pitch) *pitch = (size_t)g.pitch;
+    }
     if (w) *w = g.w;
     if (h) *h = g.h;
     return ORBX_OK;

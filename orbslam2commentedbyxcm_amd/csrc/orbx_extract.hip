@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256) ORBX_PZ_ATTR void k_pyramid(const uint8_t* __r
                                                  int vec4, uint8_t* __restrict__ pyr, long long fb,
                                                  const LevelGeom* __restrict__ lv, int L,
                                                  const int16_t* __restrict__ rtab, int pz_off, int tiles_pf,
-                                                 int nframes, int lds_a, int* __restrict__ status) {
+                                                 int nframes, int lds_a, int* __restrict__ status, int l0_store) {
     extern __shared__ __align__(16) uint8_t s_pz[];
     int f, tile;
     xcd_frame_block(tiles_pf, nframes, f, tile);
@@ -190,7 +190,9 @@ __global__ __launch_bounds__(256) ORBX_PZ_ATTR void k_pyramid(const uint8_t* __r
                             if (r < hn) {
                                 *(uint32_t*)&s_pz[r * ostride + 4 * qq] = v[k];
                                 const int y = y0 + r;
-                                if (own_x && y >= oy0 && y < oy1)
+                                // l0_store 0: level 0 is read in place from the input by the
+                                // later stages (orbx_extractor_set_level0_in_place)
+                                if (l0_store && own_x && y >= oy0 && y < oy1)
                                     store_owned_quad(frame + g.off + (size_t)y * g.pitch + x, x, ox0, ox1, v[k]);
                             }
                         }
@@ -462,7 +464,8 @@ __device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
 __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                      uint8_t* __restrict__ score, long long fb,
                                                      const LevelGeom* __restrict__ lv, int L, int tiles_pf,
-                                                     int nframes, int tq) {
+                                                     int nframes, int tq, const uint8_t* __restrict__ l0,
+                                                     long long l0_fp, int l0_pitch) {
     __shared__ __align__(16) uint8_t s_in[kTH + 6][kSW];
     __shared__ __align__(16) uint8_t s_m[kTH][kTW];
     // the survivor list (+ per-lane dump slots for branch-free appends) and, after the
@@ -484,7 +487,10 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
     const int t = tile - g.tile_first;
     const int ty = t / g.tiles_x;
     const int X0 = (t - ty * g.tiles_x) * kTW, Y0 = ty * kTH;
-    const uint8_t* img = pyr + (size_t)f * fb + g.off;
+    // level 0 from the input frame itself when it is read in place (l0 != null)
+    const bool in0 = l == 0 && l0 != nullptr;
+    const uint8_t* img = in0 ? l0 + (size_t)f * l0_fp : pyr + (size_t)f * fb + g.off;
+    const int ipitch = in0 ? l0_pitch : g.pitch;
     // ---- stage rows Y0-3 .. Y0+kTH+2, columns X0-16 .. X0+79 (REFLECT_101 at the ROI
     // edges) as 16-byte loads (pitch and level offsets are multiples of 64); all loads
     // of a thread are issued before the LDS stores: no per-load round trip
@@ -498,8 +504,8 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
             const int r = i / kRow, cu = i - r * kRow;
             // edge tile: the start column clamped into the row (a load holding an in-range
             // column never clamps: X0 and pitch are multiples of 64)
-            const int col = edge ? min(max(X0 - kSX + kLU * cu, 0), g.pitch - kLU) : X0 - kSX + kLU * cu;
-            v[k] = *(const lt_load_t*)(img + (size_t)reflect101(Y0 + r - 3, g.h) * g.pitch + col);
+            const int col = edge ? min(max(X0 - kSX + kLU * cu, 0), ipitch - kLU) : X0 - kSX + kLU * cu;
+            v[k] = *(const lt_load_t*)(img + (size_t)reflect101(Y0 + r - 3, g.h) * ipitch + col);
         }
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
@@ -1594,7 +1600,8 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
                                                    const uint32_t* __restrict__ kept, int kept_pf,
                                                    const int* __restrict__ kept_count,
                                                    orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
-                                                   int cap, int* __restrict__ n_out, int nframes) {
+                                                   int cap, int* __restrict__ n_out, int nframes,
+                                                   const uint8_t* __restrict__ l0, long long l0_fp, int l0_pitch) {
     // BRIEF patches: 37 rows of 48 bytes (16-byte chunks), or of 40 bytes -- the 37
     // columns x-18..x+18 from (x-18) & ~3 -- for the 4-byte DMA (six workgroups a CU)
     constexpr int kPP = STAGE == 2 ? 40 : 48;
@@ -1633,13 +1640,16 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     const int xs = (x - 15) & ~3, xb = (x - 18) & ~3;
     int m10, m01;
     {
-        const uint8_t* pframe = pyr + (size_t)f * fb;
         const uint8_t* bframe = blur + (size_t)f * fb;
+        // the IC rows' level: level 0 from the input frame when it is read in place
+        const bool in0 = l == 0 && l0 != nullptr;
+        const uint8_t* plevel = in0 ? l0 + (size_t)f * l0_fp : pyr + (size_t)f * fb + g.off;
+        const int rpitch = in0 ? l0_pitch : pitch;
         // rows v1 = ql - 15 (-15..0) and v2 = ql + 1 (1..15; quarter lane 15 has none)
         const int v1 = ql - 15, v2 = min(ql + 1, 15);
         const int d0 = (x - 15) & 3;
-        const uint8_t* prow1 = pframe + (uint32_t)(g.off + (long long)(y + v1) * pitch + xs);
-        const uint8_t* prow2 = pframe + (uint32_t)(g.off + (long long)(y + v2) * pitch + xs);
+        const uint8_t* prow1 = plevel + (uint32_t)((y + v1) * rpitch + xs);
+        const uint8_t* prow2 = plevel + (uint32_t)((y + v2) * rpitch + xs);
 #if ORBX_ABL_DESC == 1  // timing ablation only: no staging loads (garbage patch, constant rows)
         const uint4 p0 = make_uint4(x, y, x ^ y, 7), p1 = p0, r0 = make_uint4(y, x, 3, x + y), r1 = r0;
         const uint32_t p2 = (uint32_t)x, r2 = (uint32_t)y;
@@ -2002,7 +2012,12 @@ __global__ __launch_bounds__(256) void k_describe_tiles(const uint8_t* __restric
 hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, const uint8_t* d_imgs,
                           size_t frame_pitch, size_t stride, void* kps, uint8_t* desc, int cap,
                           int* n_per_frame, hipStream_t stream, hipEvent_t* ev, hipEvent_t stage_ev,
-                          int stage_after) {
+                          int stage_after, bool l0_in_place) {
+    // level 0 read in place by k_level_tiles / k_describe (their 16-byte row loads need
+    // 16-byte aligned frames and 64-byte aligned rows), not copied into the pyramid
+    const uint8_t* l0 = l0_in_place ? d_imgs : nullptr;
+    const long long l0_fp = (long long)frame_pitch;
+    const int l0_pitch = (int)stride;
     const int L = plan.L;
     const long long fb = plan.pyr_frame_bytes;
     const int ncells = (int)plan.cells.size();
@@ -2029,7 +2044,7 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
             const int vec4 = ((uintptr_t)in % 4 == 0) && (st % 4 == 0) && (fp % 4 == 0);
             hipLaunchKernelGGL(kern, dim3(sg.tiles * batch), dim3(256), (size_t)sg.lds_a + sg.lds_b, stream, in, fp, st,
                                vec4, db.pyr, fb, db.lv + sg.l0, sg.nl, db.rtab, sg.off, sg.tiles, batch, sg.lds_a,
-                               db.status);
+                               db.status, (s == 0 && l0) ? 0 : 1);
         }
     }
     if (ev && ev[1]) (void)hipEventRecord(ev[1], stream);
@@ -2039,7 +2054,7 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
         int tq = plan.prm.ini_th < plan.prm.min_th ? plan.prm.ini_th : plan.prm.min_th;
         tq = tq < 0 ? 0 : (tq > 255 ? 255 : tq);
         hipLaunchKernelGGL(k_level_tiles, grid, dim3(256), 0, stream, db.pyr, db.blur, db.score, fb, db.lv, L,
-                           plan.tiles_total, batch, tq);
+                           plan.tiles_total, batch, tq, l0, l0_fp, l0_pitch);
     }
     if (ev && ev[2]) (void)hipEventRecord(ev[2], stream);
     if (stage_ev && stage_after == 2) (void)hipEventRecord(stage_ev, stream);
@@ -2079,7 +2094,8 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
             dim3 grid(((plan.kept_per_frame + 15) / 16) * batch);
             auto kern = plan.kept_per_frame <= kDescGldsMaxSlots ? k_describe<ORBX_DESC_DMA> : k_describe<0>;
             hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, db.pyr, db.blur, fb, db.lv, L, db.kept,
-                               plan.kept_per_frame, db.kept_count, (orbx_keypoint*)kps, desc, cap, n_per_frame, batch);
+                               plan.kept_per_frame, db.kept_count, (orbx_keypoint*)kps, desc, cap, n_per_frame, batch,
+                               l0, l0_fp, l0_pitch);
         }
     }
     if (ev && ev[5]) (void)hipEventRecord(ev[5], stream);

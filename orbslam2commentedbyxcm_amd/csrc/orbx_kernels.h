@@ -61,7 +61,7 @@ hipError_t upload_constants(const OrbParams& prm);
 hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, const uint8_t* d_imgs,
                           size_t frame_pitch, size_t stride, void* kps, uint8_t* desc, int cap,
                           int* n_per_frame, hipStream_t stream, hipEvent_t* ev,
-                          hipEvent_t stage_ev = nullptr, int stage_after = 0);
+                          hipEvent_t stage_ev = nullptr, int stage_after = 0, bool l0_in_place = false);
 
 // dist[i*nb+j] = Hamming(a_i, b_j)
 hipError_t launch_hamming_matrix(const uint8_t* a, int na, const uint8_t* b, int nb, int32_t* dist,

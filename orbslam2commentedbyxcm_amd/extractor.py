@@ -158,6 +158,11 @@ class ORBextractor:
         """Test hook: cap the octree node capacity per level (0 = the guaranteed bound)."""
         L.check(L.lib().orbx_extractor_set_node_capacity(self._h, int(cap)))
 
+    def set_level0_in_place(self, enable: bool = True) -> None:
+        """orbx_extractor_set_level0_in_place: level 0 read from the caller's device frames
+        (monocular front end; the frames must stay unchanged while the pyramid is used)."""
+        L.check(L.lib().orbx_extractor_set_level0_in_place(self._h, 1 if enable else 0))
+
     STAGES = ("pyramid", "score_blur", "fast_cells", "octree", "describe")
 
     def set_timing(self, enable: bool = True, stage: str | None = None) -> None:

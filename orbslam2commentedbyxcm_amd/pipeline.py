@@ -36,7 +36,7 @@ class SequencePipeline:
                  nbuf: int = 2, matcher_mode: int | None = None, match_after_stage: int = 0,
                  lane_offset_stage: int | None = None, match_cu_stride: int = 1,
                  match_priority: int = 0, on_matched=None, local_map: bool = False, local_window: int = 3,
-                 local_th: float = 1.0):
+                 local_th: float = 1.0, level0_in_place: bool = True):
         import torch
 
         self.B, self.W, self.H = int(batch), int(width), int(height)
@@ -60,6 +60,10 @@ class SequencePipeline:
             self._own_ms = stream_create(device, max(1, int(match_cu_stride)), int(match_priority))
             self.ms = torch.cuda.ExternalStream(self._own_ms, device=self.dev)
         self.exs = [ORBextractor(*params, device=device) for _ in range(self.S)]
+        # the monocular front end never reads mvImagePyramid: level 0 stays in the batch's
+        # frames (no copy into the pyramid; orbx_extractor_set_level0_in_place)
+        for e in self.exs:
+            e.set_level0_in_place(level0_in_place)
         self.matcher = ORBmatcher(nnratio, check_ori, device=device)
         # matcher_mode: orbx_matcher_set_footprint.  Default 5 (lean split: one 1024-thread
         # workgroup per problem sorts and scores with only the grid and the claims in LDS,

@@ -105,3 +105,40 @@ def test_describe_tiles_form_matches_oracle(oracle, orbx_built, monkeypatch, prm
     k = kps.cpu().numpy().view(np.uint8).reshape(B, cap, 28).view(L.KEYPOINT_DTYPE).reshape(B, cap)
     ref = checks.extract_all(frames, params=prm)
     assert checks.compare_extraction(ref, k, desc.cpu().numpy(), n.cpu().numpy()) == []
+
+
+def test_level0_in_place(oracle, orbx_built):
+    """orbx_extractor_set_level0_in_place: the device batch reads level 0 from the caller's
+    frames (bit-exact output; mvImagePyramid level 0 is then the caller's frame, the other
+    levels the extractor's own), an unaligned stride falls back to the copy, and the stereo
+    matcher refuses an extractor whose level 0 was read in place."""
+    import torch
+
+    from oracle import checks
+    from orbslam2commentedbyxcm_amd import OrbxError
+    from orbslam2commentedbyxcm_amd.matcher import ORBmatcher
+    B = 4
+    frames = synth.frames(B, 640, 480, first_seed=60)
+    ex = ORBextractor(1000, 1.2, 8, 20, 7)
+    ex.set_level0_in_place(True)
+    cap = ex.max_keypoints(640, 480)
+    dev = torch.device("cuda", 0)
+    d_frames = torch.from_numpy(frames).to(dev)
+    kps = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)
+    desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
+    n = torch.empty((B,), dtype=torch.int32, device=dev)
+    ex.extract_batch_device(d_frames, kps, desc, n)
+    torch.cuda.synchronize()
+    from orbslam2commentedbyxcm_amd import _lib as L
+    k = kps.cpu().numpy().view(np.uint8).reshape(B, cap, 28).view(L.KEYPOINT_DTYPE).reshape(B, cap)
+    ref = checks.extract_all(frames)
+    assert checks.compare_extraction(ref, k, desc.cpu().numpy(), n.cpu().numpy()) == []
+    pyr = oracle.pyramid(frames[0], oracle.params(1000, 1.2, 8, 20, 7))
+    for lv in (0, 3):
+        assert np.array_equal(ex.pyramid_level(lv, frame=0), pyr[lv])
+    ex2 = ORBextractor(1000, 1.2, 8, 20, 7)
+    with pytest.raises(OrbxError):
+        ORBmatcher(0.6, True).ComputeStereoMatchesBatchDevice(
+            ex, ex2, kps, desc, n, kps, desc, n, 100.0, 500.0,
+            torch.empty((B, cap), dtype=torch.float32, device=dev),
+            torch.empty((B, cap), dtype=torch.float32, device=dev))
