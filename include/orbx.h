@@ -229,7 +229,8 @@ typedef struct {
 
 /* MapPoint fields, indexed by MapPoint id (the ids stand in for MapPoint*).  Fields a
  * call does not read may be NULL: max/min_distance and normal are read only by the
- * KeyFrame / Sim3 projections (a13, a14). */
+ * KeyFrame / Sim3 projections (a13, a14).  n < 2^30 for the projection searches (their
+ * claims carry a flag in bit 30; larger tables fail with ORBX_ERR_ARG). */
 typedef struct {
     int n;
     const float* pos;            /* GetWorldPos(), n x 3 (may be NULL where unused) */

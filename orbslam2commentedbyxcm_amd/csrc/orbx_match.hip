@@ -131,6 +131,18 @@ __device__ __forceinline__ bool kp_blocked(int fmp, const ProjParams& P) {
     return P.blocked_mode == 1 || P.mp_obs[fmp] > 0;
 }
 
+// Claim words: the search's claims (sfmp, the grid's claims) and its queries' MapPoints
+// (qmp) carry whether the MapPoint's claim blocks a keypoint as bit 30 (set: it does not,
+// a11 / a12's Observations() == 0), so the replay and the re-scoring test a claim with
+// one LDS read instead of a dependent Observations() load (MapPoint ids < 2^30, checked
+// by the host).  -1: no claim.
+constexpr int kClaimFree = 1 << 30;
+__device__ __forceinline__ int claim_word(int fmp, const ProjParams& P) {
+    return fmp >= 0 && !kp_blocked(fmp, P) ? fmp | kClaimFree : fmp;
+}
+__device__ __forceinline__ bool claim_blocks(int w) { return w >= 0 && !(w & kClaimFree); }
+__device__ __forceinline__ int claim_mp(int w) { return w >= 0 ? w & ~kClaimFree : w; }
+
 struct CellRange {
     int x0, x1, y0, y1;
     bool empty;
@@ -457,7 +469,7 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
                             const int yr = ent >> 13;
                             if ((a < e0 && yr < ylo) || (a >= s1 && yr > yhi)) return false;
                             if (!(fabsf(kp.x - Q.u) < Q.r && fabsf(kp.y - Q.v) < Q.r)) return false;
-                            if (sfmp && kp_blocked(sfmp[p], P)) return false;
+                            if (sfmp && claim_blocks(sfmp[p])) return false;
                             return (kk & kKeyBlocked) == 0u;
                         };
                         for (int a = s0 + sub; a < e1; a += 2 * lpc) {
@@ -507,7 +519,7 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
                         const float distx = kp.x - Q.u;
                         const float disty = kp.y - Q.v;
                         if (!(fabsf(distx) < Q.r && fabsf(disty) < Q.r)) continue;
-                        if (sfmp && kp_blocked(sfmp[p], P)) continue;  // null: nothing claimed yet
+                        if (sfmp && claim_blocks(sfmp[p])) continue;  // null: nothing claimed yet
                         int d;
                         if (G.sdesc) {
                             if (Q.er_max >= 0.f && pb.u_right) {
@@ -715,10 +727,10 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
     // no lane changes (Jacobi iteration: after t iterations the first t lanes are final,
     // so it converges, and its fixpoint is the sequential result).  A chunk with k
     // independent conflicts then costs one iteration plus the longest dependency chain,
-    // not k rounds.  Sequence points stop the commit: a lane whose list ran out (it is
-    // re-scored against the committed claims) and a lane accepting a MapPoint whose claim
-    // does not block (a11: Observations() == 0) -- it commits alone after the lanes
-    // before it.
+    // not k rounds.  A lane whose list ran out stops the commit (it is re-scored against
+    // the committed claims); a lane accepting a MapPoint whose claim does not block (a11:
+    // Observations() == 0) does not -- later lanes ignore its proposal, and the commit
+    // keeps the last claim of a keypoint.
     const int lastp = pb.n > 0 ? pb.n - 1 : 0;
     int guard = 0;
     // a chunk's lists, MapPoints and queries (the latter for a re-scoring) are loaded
@@ -778,20 +790,9 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
         // one batch of independent LDS reads, and Observations() loads for a11)
         unsigned cblk = 0;
         if (mp >= 0) {
-            bself = P.blocked_mode == 1 || P.mp_obs[mp] > 0;
-            int fm[kTopK];
+            bself = claim_blocks(mp);
 #pragma unroll
-            for (int j = 0; j < kTopK; j++) fm[j] = sfmp[oa[j]];
-            if (P.blocked_mode == 1) {
-#pragma unroll
-                for (int j = 0; j < kTopK; j++) cblk |= (fm[j] >= 0 ? 1u : 0u) << j;
-            } else {
-                int ob[kTopK];
-#pragma unroll
-                for (int j = 0; j < kTopK; j++) ob[j] = P.mp_obs[fm[j] >= 0 ? fm[j] : 0];
-#pragma unroll
-                for (int j = 0; j < kTopK; j++) cblk |= (fm[j] >= 0 && ob[j] > 0 ? 1u : 0u) << j;
-            }
+            for (int j = 0; j < kTopK; j++) cblk |= (claim_blocks(sfmp[oa[j]]) ? 1u : 0u) << j;
         }
         // a lane's choice given the blocked entries bm: c1 (its best free entry), whether
         // it accepts c1, and whether its list ran out (exhausted: unlisted candidates may
@@ -848,15 +849,24 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
             if (act) eval(cblk | sb);
             if (__ballot(act && sig() != old)) continue;
             // fixpoint: every active lane's choice is the sequential one up to the first
-            // sequence point f
-            const bool nbl = act && acc && !bself;
-            const unsigned long long sm = __ballot(act && (exh || nbl));
+            // exhausted lane f
+            const unsigned long long sm = __ballot(act && exh);
             const int f = sm ? __ffsll((long long)sm) - 1 : 64;
-            const bool fnb = f < 64 && __builtin_amdgcn_readlane((int)nbl, f);
-            const int lim = fnb ? f + 1 : f;  // lanes below lim commit
-            const bool com = act && acc && lane < lim;
+            const bool com = act && acc && lane < f;
             const unsigned long long comm = __ballot(com);
-            if (com) sfmp[ent_pos(c1)] = mp;
+            // Blocking claims are unique (a later lane saw them).  A non-blocking claim
+            // (a11: Observations() == 0) may be taken again by a later lane of the same
+            // commit, which then keeps the keypoint (ORBmatcher.cc:117-119, 167): it is
+            // written only by the last lane claiming its keypoint (owner map: the lowest
+            // 63 - lane, in order: atomics, reads, reset).
+            if (com && bself) sfmp[ent_pos(c1)] = mp;
+            if (__ballot(com && !bself)) {
+                const int pp = com ? ent_pos(c1) : 0;
+                if (com) atomicMin(&owner[pp], 63 - lane);
+                const int lo = owner[pp];
+                if (com) owner[pp] = 0x7fffffff;
+                if (com && !bself && lo == 63 - lane) sfmp[pp] = mp;
+            }
             nmatch += __popcll(comm);
             if (P.check_ori) {
                 // the match is recorded with its query; the rotation bins are computed
@@ -874,9 +884,9 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
             // the committed lanes' claims, for the lanes after them: the entries a lane
             // below f proposed (blocking proposals only reach the owner map)
 #pragma unroll
-            for (int j = 0; j < kTopK; j++) cblk |= (act && lane >= lim ? (unsigned)(ow[j] - f) >> 31 : 0u) << j;
-            start = lim;
-            if (!fnb) {
+            for (int j = 0; j < kTopK; j++) cblk |= (act && lane >= f ? (unsigned)(ow[j] - f) >> 31 : 0u) << j;
+            start = f;
+            {
                 // lane f's list ran out: re-score it against the current claims.  Any list
                 // that is exact against the claims of some moment stays valid later
                 // (claims only ever block more keypoints), so the other exhausted lanes
@@ -1073,20 +1083,9 @@ __device__ void proj_replay_block(const ProjProblem& pb, const ProjParams& P, co
         bool bself = false;
         unsigned cblk = 0;
         if (mp >= 0) {
-            bself = P.blocked_mode == 1 || P.mp_obs[mp] > 0;
-            int fm[kTopK];
+            bself = claim_blocks(mp);
 #pragma unroll
-            for (int j = 0; j < kTopK; j++) fm[j] = sfmp[oa[j]];
-            if (P.blocked_mode == 1) {
-#pragma unroll
-                for (int j = 0; j < kTopK; j++) cblk |= (fm[j] >= 0 ? 1u : 0u) << j;
-            } else {
-                int ob[kTopK];
-#pragma unroll
-                for (int j = 0; j < kTopK; j++) ob[j] = P.mp_obs[fm[j] >= 0 ? fm[j] : 0];
-#pragma unroll
-                for (int j = 0; j < kTopK; j++) cblk |= (fm[j] >= 0 && ob[j] > 0 ? 1u : 0u) << j;
-            }
+            for (int j = 0; j < kTopK; j++) cblk |= (claim_blocks(sfmp[oa[j]]) ? 1u : 0u) << j;
         }
         unsigned c1 = kNoEntry;
         bool exh = false, acc = false;
@@ -1132,29 +1131,40 @@ __device__ void proj_replay_block(const ProjProblem& pb, const ProjParams& P, co
                 sb |= ((ow[j] >> 10) == it && (int)(1023u - (ow[j] & 1023u)) < tid ? 1u : 0u) << j;
             if (act) eval(cblk | sb);
             if (__syncthreads_or(act && sig() != old)) continue;
-            // fixpoint: the first sequence point f (exhausted, or a non-blocking acceptor)
-            const bool nbl = act && acc && !bself;
-            int key = act && (exh || nbl) ? 2 * tid + (exh ? 0 : 1) : 0x7fffffff;
+            // fixpoint: the first exhausted thread f stops the commit (a non-blocking
+            // acceptor does not: see proj_replay)
+            int key = act && exh ? tid : 0x7fffffff;
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) key = min(key, __shfl_xor(key, o));
             if (lane == 0 && key != 0x7fffffff) atomicMin(&s_key, key);
             __syncthreads();
             const int K = s_key;
-            const int f = K == 0x7fffffff ? RT : (K >> 1);
-            const bool fnb = K != 0x7fffffff && (K & 1);
-            const int lim = fnb ? f + 1 : f;  // threads below lim commit
-            const bool com = act && acc && tid < lim;
-            if (com) sfmp[ent_pos(c1)] = mp;
+            const int f = K == 0x7fffffff ? RT : K;
+            const bool com = act && acc && tid < f;
+            if (com && bself) sfmp[ent_pos(c1)] = mp;  // unique
             const unsigned long long cm = __ballot(com);
-            if (lane == 0) s_wc[wave] = __popcll(cm);
+            const bool wnb = __ballot(com && !bself) != 0;
+            if (lane == 0) s_wc[wave] = __popcll(cm) | (wnb ? 1 << 16 : 0);
             __syncthreads();
             if (tid == 0) s_key = 0x7fffffff;  // read by every thread before the barrier above
-            int tot = 0, woff = 0;
+            int tot = 0, woff = 0, nb = 0;
 #pragma unroll
             for (int w = 0; w < kW; w++) {
-                const int c = s_wc[w];
+                const int c = s_wc[w] & 0xffff;
+                nb |= s_wc[w] >> 16;
                 woff += w < wave ? c : 0;
                 tot += c;
+            }
+            const unsigned itf = it;
+            if (nb) {
+                // non-blocking claims: only the last committed thread claiming a keypoint
+                // writes it (a fresh tag iteration, highest thread wins)
+                it++;
+                const unsigned tag = (it << 10) | (unsigned)tid;
+                if (com) atomicMax(&owner[ent_pos(c1)], tag);
+                __syncthreads();
+                if (com && !bself && owner[ent_pos(c1)] == tag) sfmp[ent_pos(c1)] = mp;
+                __syncthreads();  // publishes sfmp for the re-scoring and the next chunk
             }
             if (P.check_ori && com) {
                 const int r = nrec + woff + __popcll(cm & below);
@@ -1165,13 +1175,13 @@ __device__ void proj_replay_block(const ProjProblem& pb, const ProjParams& P, co
             if (P.check_ori) nrec += tot;
             if (f >= RT) break;
             // the committed threads' claims, for the threads after them
-            if (act && tid >= lim) {
+            if (act && tid >= f) {
 #pragma unroll
                 for (int j = 0; j < kTopK; j++)
-                    cblk |= ((ow[j] >> 10) == it && (int)(1023u - (ow[j] & 1023u)) < f ? 1u : 0u) << j;
+                    cblk |= ((ow[j] >> 10) == itf && (int)(1023u - (ow[j] & 1023u)) < f ? 1u : 0u) << j;
             }
-            start = lim;
-            if (!fnb) {
+            start = f;
+            {
                 // every exhausted list at or after f, against the current claims (sfmp is
                 // published by the barrier above)
                 unsigned long long X = __ballot(act && exh && tid >= f);
@@ -1370,7 +1380,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
         if (SPLIT) {
             if (kp_blocked(pb.frame_mp[i], P)) skey[p] = k | kKeyBlocked;
         } else {
-            sfmp[p] = pb.frame_mp[i];
+            sfmp[p] = claim_word(pb.frame_mp[i], P);
             owner[p] = 0x7fffffff;
         }
         if (QLDS) sang[p] = kp.angle;
@@ -1405,7 +1415,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
 #pragma unroll
                 for (int v = 0; v < kListVec; v++)
                     qk[kListVec * q + v] = make_uint4(e[4 * v], e[4 * v + 1], e[4 * v + 2], e[4 * v + 3]);
-                qmp[q] = mp;
+                qmp[q] = claim_word(mp, P);
                 qang[q] = cur.q.angle;
             }
             cur = nxt;
@@ -1434,7 +1444,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     proj_replay(pb, P, G, sfmp, owner, (unsigned*)(smem + L.elist), qk, qmp, qang, mlist, mbin, s_hist,
                 [&](int tpos) { return QLDS ? sang[tpos] : pb.keys[sk_idx(skey[tpos])].angle; }, st);
     wave_lds_fence();
-    for (int p = lane; p < n; p += 64) pb.frame_mp[sk_idx(skey[p])] = sfmp[p];
+    for (int p = lane; p < n; p += 64) pb.frame_mp[sk_idx(skey[p])] = claim_mp(sfmp[p]);
     if (st && lane == 0) st[4] = wall_clock64();
 }
 
@@ -1477,7 +1487,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage_copy(const uint4* __res
 }
 
 template <int kSeqGridThreads>  // (shadows the batch default of the same name)
-__global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem* probs, unsigned char* grids,
+__global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem* probs, ProjParams P, unsigned char* grids,
                                                               int cap, int noct, unsigned long long* stamps) {
     extern __shared__ __align__(16) unsigned char smem[];
     // diagnostics (one problem): words 0, 1, 2, 4, 10, 11 of its stamp row
@@ -1506,7 +1516,7 @@ __global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem*
         gkey[p] = k;
         sxy[p] = make_float2(kp.x, kp.y);
         sang[p] = kp.angle;
-        gfmp[p] = pb.frame_mp[i];
+        gfmp[p] = claim_word(pb.frame_mp[i], P);
     }
     for (int t = tid; t < 2 * n; t += kSeqGridThreads) {
         const int i = sk_idx(skey[t >> 1]);
@@ -1552,7 +1562,7 @@ __global__ __launch_bounds__(kSeqScoreThreads) void k_seq_score(const ProjProble
 #pragma unroll
         for (int v = 0; v < kListVec; v++)
             qk[kListVec * q + v] = make_uint4(e[4 * v], e[4 * v + 1], e[4 * v + 2], e[4 * v + 3]);
-        qmp[q] = mp;
+        qmp[q] = claim_word(mp, P);
         qang[q] = cur.q.angle;
     }
 }
@@ -1583,7 +1593,7 @@ __global__ __launch_bounds__(RT) void k_seq_commit(const ProjProblem* __restrict
     int* sfmp = (int*)(elist + kTopK * RT);
     int* owner = sfmp + n;
     for (int p = tid; p < n; p += RT) {
-        sfmp[p] = pb.frame_mp[sk_idx(G.skey[p])];
+        sfmp[p] = claim_word(pb.frame_mp[sk_idx(G.skey[p])], P);
         owner[p] = RT == 64 ? 0x7fffffff : 0;
     }
     if (tid < kHistoLength) s_hist[tid] = 0;
@@ -1602,7 +1612,7 @@ __global__ __launch_bounds__(RT) void k_seq_commit(const ProjProblem* __restrict
                               [&](int tpos) { return gang[tpos]; }, st);
     __syncthreads();
     int32_t* out = P.out_mp ? P.out_mp : pb.frame_mp;
-    for (int p = tid; p < n; p += RT) out[sk_idx(G.skey[p])] = sfmp[p];
+    for (int p = tid; p < n; p += RT) out[sk_idx(G.skey[p])] = claim_mp(sfmp[p]);
 }
 
 size_t seq_grid_bytes(int cap, int noct) { return SeqGridLayout(cap, noct).total; }
@@ -1681,11 +1691,11 @@ hipError_t launch_seq_split(const ProjProblem* d_probs, int nprob, const ProjPar
         if (ce != hipSuccess) return ce;
     }
     if (wide)
-        hipLaunchKernelGGL(k_seq_grid<1024>, dim3(nprob), dim3(1024), lds_grid, stream, d_probs, grids, cap, P.noct,
+        hipLaunchKernelGGL(k_seq_grid<1024>, dim3(nprob), dim3(1024), lds_grid, stream, d_probs, P, grids, cap, P.noct,
                            P.stamps);
     else
         hipLaunchKernelGGL(k_seq_grid<kSeqGridThreads>, dim3(nprob), dim3(kSeqGridThreads), lds_grid, stream, d_probs,
-                           grids, cap, P.noct, P.stamps);
+                           P, grids, cap, P.noct, P.stamps);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int qblocks = (qcap + kSeqScoreQ - 1) / kSeqScoreQ;

@@ -42,6 +42,7 @@ int fail(int code, const char* what) {
 constexpr int kNumCellsHost = kGridCols * kGridRows;
 constexpr int TH_HIGH = 100;  // ORBmatcher.cc:38
 constexpr int TH_LOW = 50;    // ORBmatcher.cc:39
+constexpr long long kMaxMapPointIds = 1ll << 30;  // the searches carry a flag in bit 30 of a claim
 
 // Grow-only device arena, reset per call.
 struct Arena {
@@ -260,6 +261,7 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
         if (nmatches) *nmatches = 0;
         return ORBX_OK;
     }
+    if (mps->n < 0 || mps->n >= kMaxMapPointIds) return fail(ORBX_ERR_ARG, "MapPoint table of 2^30 or more");
     const auto t_stage0 = std::chrono::steady_clock::now();
     HIP_TRY(hipSetDevice(m->device));
     const int nobs = mps->n;
@@ -704,6 +706,7 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
     if (batch == 0) return ORBX_OK;
     if (!sq->kps || !sq->desc || !sq->n || !sq->Tcw || !sq->cur_mp || !sq->nmatches)
         return fail(ORBX_ERR_ARG, "null buffer");
+    if ((long long)batch * cap >= kMaxMapPointIds) return fail(ORBX_ERR_ARG, "batch x cap MapPoint ids >= 2^30");
     if (!sq->mono && !(sq->b > 0.f)) return fail(ORBX_ERR_ARG, "stereo / RGB-D sequence needs the baseline mb > 0");
     int32_t* d_cur_mp = sq->cur_mp;
     int32_t* d_nmatches = sq->nmatches;
@@ -773,7 +776,8 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
     P.noct = nlevels;  // the extractor's keypoints have octave < nlevels
     // ORBX_MATCH_STAMPS=1: per-phase wall-clock breakdown of the search kernel to stderr
     // (diagnostics only; synchronises the stream).
-    const bool stamps = !grids && getenv("ORBX_MATCH_STAMPS") != nullptr;  // k_proj_search phases only
+    // (split launches: the commit kernel's replay only)
+    const bool stamps = (!grids || split) && getenv("ORBX_MATCH_STAMPS") != nullptr;
     unsigned long long* d_st = nullptr;
     if (stamps) {
         HIP_TRY(hipMalloc(&d_st, sizeof(unsigned long long) * kStampWords * npairs));
@@ -795,6 +799,24 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
         HIP_TRY(hipStreamSynchronize(s));
         HIP_TRY(hipMemcpy(h.data(), d_st, h.size() * 8, hipMemcpyDeviceToHost));
         HIP_TRY(hipFree(d_st));
+        if (split) {
+            double cm = 0, cmx = 0, resc = 0, nq = 0, nit = 0, itmx = 0;
+            for (int p = 0; p < npairs; p++) {
+                const unsigned long long* r = &h[(size_t)kStampWords * p];
+                const double d = (double)(r[3] - r[13]) * 0.01;
+                cm += d;
+                cmx = d > cmx ? d : cmx;
+                resc += (double)r[5];
+                nq += (double)r[6];
+                nit += (double)r[7];
+                itmx = (double)r[7] > itmx ? (double)r[7] : itmx;
+            }
+            fprintf(stderr,
+                    "[orbx seq stamps] pairs=%d | commit mean/max %.1f/%.1f us | %.1f queries, %.1f re-scored, replay "
+                    "iterations mean/max %.1f/%.0f\n",
+                    npairs, cm / npairs, cmx, nq / npairs, resc / npairs, nit / npairs, itmx);
+            return ORBX_OK;
+        }
         double ph[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0}, resc = 0, nq = 0, nit = 0, tres = 0, tfirst = 0;
         double tbit = 0, tfill = 0, tbuild = 0, rtrunc = 0;
         unsigned long long t0 = ~0ull, t1 = 0;
@@ -840,6 +862,7 @@ int orbx_search_local_points_device(orbx_matcher* m, const orbx_mappoints_device
     if (!lm->kps || !lm->desc || !lm->n || !lm->Tcw || !lm->frame_mp || !lm->nmatches || !mps->pos || !mps->desc ||
         !mps->normal || !mps->max_distance || !mps->min_distance || !mps->observations)
         return fail(ORBX_ERR_ARG, "null buffer");
+    if (mps->n < 0 || mps->n >= kMaxMapPointIds) return fail(ORBX_ERR_ARG, "MapPoint table of 2^30 or more");
     int maxnq = 0;
     for (int b = 0; b < B; b++) {
         const int c = lm->local_off[b + 1] - lm->local_off[b];

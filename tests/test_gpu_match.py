@@ -102,6 +102,26 @@ def test_search_by_projection_local(oracle, orbx_built, seed, th, nnratio):
     assert np.array_equal(fg, fr), np.nonzero(fg != fr)[0][:10]
 
 
+@pytest.mark.parametrize("zero_frac,reps", [(0.5, 1), (1.0, 1), (0.5, 3), (1.0, 4)])
+def test_search_by_projection_local_nonblocking(oracle, orbx_built, zero_frac, reps):
+    """MapPoints with Observations() == 0 do not block a keypoint (ORBmatcher.cc:117-119):
+    later queries of the same replay commit take it again and the last one keeps it.  Each
+    MapPoint queried `reps` times makes such re-claims dense."""
+    A, B = S.two_views(oracle, 4)
+    mps = S.mappoints_from(A, 4, obs_zero_frac=zero_frac)
+    trk = S.local_track(A, B, mps, 4)
+    rng = np.random.default_rng(5)
+    queries = np.concatenate([rng.permutation(len(A.keys)) for _ in range(reps)]).astype(np.int32)
+    f0 = np.full(len(B.keys), -1, np.int32)
+    m = ORBmatcher(0.8, False)
+    fg = f0.copy()
+    ng = m.SearchByProjectionLocal(B, fg, queries, mps, trk, 3.0)
+    fr = f0.copy()
+    nr = oracle.sbp_local(B, fr, queries, mps, trk, 3.0, 0.8)
+    assert ng == nr and nr > 50
+    assert np.array_equal(fg, fr), np.nonzero(fg != fr)[0][:10]
+
+
 @pytest.mark.parametrize("seed,stereo,only_stereo,check_ori", [(0, False, False, False), (1, True, False, False),
                                                                 (2, True, True, False), (3, False, False, True)])
 def test_search_for_triangulation(oracle, orbx_built, seed, stereo, only_stereo, check_ori):
