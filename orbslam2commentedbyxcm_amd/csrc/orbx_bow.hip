@@ -21,6 +21,7 @@
 
 #include <climits>
 
+#include "orbx_gmem.h"
 #include "orbx_kernels.h"
 
 namespace orbx {
@@ -77,14 +78,16 @@ struct Desc {
 };
 
 __device__ __forceinline__ Desc load_desc(const uint8_t* p) {
-    const unsigned long long* q = (const unsigned long long*)p;
-    return Desc{q[0], q[1], q[2], q[3]};
+    const ulonglong2* q = (const ulonglong2*)p;
+    const ulonglong2 a = ldg(q), b = ldg(q + 1);
+    return Desc{a.x, a.y, b.x, b.y};
 }
 
 // DescriptorDistance, ORBmatcher.cc:1983-2003
 __device__ __forceinline__ int hamming(const Desc& x, const uint8_t* p) {
-    const unsigned long long* q = (const unsigned long long*)p;
-    return __popcll(x.a ^ q[0]) + __popcll(x.b ^ q[1]) + __popcll(x.c ^ q[2]) + __popcll(x.d ^ q[3]);
+    const ulonglong2* q = (const ulonglong2*)p;
+    const ulonglong2 a = ldg(q), b = ldg(q + 1);
+    return __popcll(x.a ^ a.x) + __popcll(x.b ^ a.y) + __popcll(x.c ^ b.x) + __popcll(x.d ^ b.y);
 }
 
 // rotHist bin of a match (ORBmatcher.cc:363-371)
@@ -145,17 +148,17 @@ __global__ __launch_bounds__(kBowThreads) void k_bow(const BowProblem* __restric
     __syncthreads();
     const int acc_th = pb.kf_kf ? kThLow - 1 : kThLow;  // KF->KF: bestDist1 < TH_LOW; KF->F: <= TH_LOW
     for (int nd = wave; nd < pb.nnodes; nd += kBowWaves) {
-        const BowNode N = pb.nodes[nd];
+        const BowNode N = ldg(pb.nodes + nd);
         const int ncand = N.c_end - N.c_beg;
         for (int q = N.q_beg; q < N.q_end; q++) {
-            const int idx1 = pb.q_idx1[q];
+            const int idx1 = ldg(pb.q_idx1 + q);
             const Desc d1 = load_desc(pb.desc1 + (size_t)idx1 * 32);
             // lane-local best two of (dist << 16 | node-list position); ties go to the
             // earlier position like the reference's strict '<' updates
             unsigned k1 = 0xffffffffu, k2 = 0xffffffffu;
             for (int p = lane; p < ncand; p += 64) {
-                const int idx2 = pb.fv2_idx[N.c_beg + p];
-                if (claimed2[idx2] || (pb.avail2 && !pb.avail2[idx2])) continue;
+                const int idx2 = ldg(pb.fv2_idx + N.c_beg + p);
+                if (claimed2[idx2] || (pb.avail2 && !ldg(pb.avail2 + idx2))) continue;
                 const int dist = hamming(d1, pb.desc2 + (size_t)idx2 * 32);
                 if (dist >= 256) continue;  // never below the initial bestDist 256
                 const unsigned key = (unsigned)dist << 16 | (unsigned)p;
@@ -254,16 +257,16 @@ __device__ void init_scan(const InitProblem& pb, int i1, const int* md, unsigned
 #pragma unroll
     for (int k = 0; k < K; k++) l[k] = kNone;
     seen = 0;
-    const float x = pb.prev[2 * i1], y = pb.prev[2 * i1 + 1];
+    const float x = ldg(pb.prev + 2 * i1), y = ldg(pb.prev + 2 * i1 + 1);
     const Window w = init_window(pb, x, y);
     if (w.empty) return;
     const Desc d1 = load_desc(pb.desc1 + (size_t)i1 * 32);
     int rank0 = 0;
     for (int ix = w.x0; ix <= w.x1; ix++) {
-        const int a = pb.cell_start[ix * kGridRows + w.y0], b = pb.cell_start[ix * kGridRows + w.y1 + 1];
+        const int a = ldg(pb.cell_start + ix * kGridRows + w.y0), b = ldg(pb.cell_start + ix * kGridRows + w.y1 + 1);
         for (int p = a + lane; p < b; p += 64) {
-            const int i2 = pb.cell_idx[p];
-            const orbx_keypoint kp = pb.keys2[i2];
+            const int i2 = ldg(pb.cell_idx + p);
+            const orbx_keypoint kp = ldg(pb.keys2 + i2);
             if (kp.octave != 0) continue;  // minLevel = maxLevel = level1 = 0
             const float distx = kp.x - x, disty = kp.y - y;
             if (!(fabsf(distx) < pb.r && fabsf(disty) < pb.r)) continue;

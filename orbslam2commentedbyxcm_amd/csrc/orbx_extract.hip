@@ -181,9 +181,10 @@ __global__ __launch_bounds__(256) ORBX_PZ_ATTR void k_pyramid(const uint8_t* __r
                             } else if (x + 8 <= g.w) {
                                 // an unaligned row (e.g. 1241-byte KITTI rows): the two aligned
                                 // dwords around the quad, funnel-shifted (both inside the row)
-                                const uintptr_t pa = (uintptr_t)p;
-                                const uint32_t* q = (const uint32_t*)(pa & ~(uintptr_t)3);
-                                const int sh = (int)(pa & 3);
+                                // (pointer arithmetic, not an integer round trip: the loads
+                                // stay global, not flat)
+                                const int sh = (int)((uintptr_t)p & 3);
+                                const uint32_t* q = (const uint32_t*)(p - sh);
                                 const uint32_t lo = q[0], hi = q[sh ? 1 : 0];
                                 v[k] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
                             } else {

@@ -13,6 +13,7 @@
 #include <type_traits>
 
 #include "orbx_block_sort.h"
+#include "orbx_gmem.h"
 #include "orbx_kernels.h"
 
 namespace orbx {
@@ -358,10 +359,10 @@ static_assert(sizeof(ProjQuery) == 48, "ProjQuery layout");
 
 __device__ __forceinline__ QueryReg load_query(const ProjProblem& pb, int q) {
     QueryReg r;
-    r.q = pb.q[q];
+    r.q = ldg(pb.q + q);
     const uint4* d = (const uint4*)(pb.qdesc + (size_t)q * 32);
-    r.d0 = d[0];
-    r.d1 = d[1];
+    r.d0 = ldg(d);
+    r.d1 = ldg(d + 1);
     return r;
 }
 
@@ -483,14 +484,15 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
                             const bool okB = h2 && test(a2, entB, kB, kkB, pB);
                             if (!okA && !okB) continue;
                             const int iA = sk_idx(kkA), iB = sk_idx(okB ? kkB : kkA);
-                            const unsigned long long* tA = (const unsigned long long*)(pb.desc + (size_t)iA * 32);
-                            const unsigned long long* tB = (const unsigned long long*)(pb.desc + (size_t)iB * 32);
-                            const unsigned long long xA0 = tA[0], xA1 = tA[1], xA2 = tA[2], xA3 = tA[3];
-                            const unsigned long long xB0 = tB[0], xB1 = tB[1], xB2 = tB[2], xB3 = tB[3];
+                            const ulonglong2* tA = (const ulonglong2*)(pb.desc + (size_t)iA * 32);
+                            const ulonglong2* tB = (const ulonglong2*)(pb.desc + (size_t)iB * 32);
+                            const ulonglong2 yA0 = ldg(tA), yA1 = ldg(tA + 1), yB0 = ldg(tB), yB1 = ldg(tB + 1);
+                            const unsigned long long xA0 = yA0.x, xA1 = yA0.y, xA2 = yA1.x, xA3 = yA1.y;
+                            const unsigned long long xB0 = yB0.x, xB1 = yB0.y, xB2 = yB1.x, xB3 = yB1.y;
                             float urA = 0.f, urB = 0.f;
                             if (Q.er_max >= 0.f && pb.u_right) {
-                                urA = pb.u_right[iA];
-                                urB = pb.u_right[iB];
+                                urA = ldg(pb.u_right + iA);
+                                urB = ldg(pb.u_right + iB);
                             }
                             auto take = [&](bool ok, float ur, int p, unsigned long long x0, unsigned long long x1,
                                             unsigned long long x2, unsigned long long x3) {
@@ -523,7 +525,7 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
                         int d;
                         if (G.sdesc) {
                             if (Q.er_max >= 0.f && pb.u_right) {
-                                const float ur = pb.u_right[sk_idx(G.skey[p])];
+                                const float ur = ldg(pb.u_right + sk_idx(G.skey[p]));
                                 if (ur > 0 && fabsf(Q.ur - ur) > Q.er_max) continue;
                             }
                             const uint4 a4 = G.sdesc[2 * p], b4 = G.sdesc[2 * p + 1];
@@ -536,12 +538,12 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
                             if (kk & kKeyBlocked) continue;
                             const int i = sk_idx(kk);
                             if (Q.er_max >= 0.f && pb.u_right) {
-                                const float ur = pb.u_right[i];
+                                const float ur = ldg(pb.u_right + i);
                                 if (ur > 0 && fabsf(Q.ur - ur) > Q.er_max) continue;
                             }
-                            const unsigned long long* tt = (const unsigned long long*)(pb.desc + (size_t)i * 32);
-                            d = __popcll(q0 ^ tt[0]) + __popcll(q1 ^ tt[1]) + __popcll(q2 ^ tt[2]) +
-                                __popcll(q3 ^ tt[3]);
+                            const ulonglong2* tt = (const ulonglong2*)(pb.desc + (size_t)i * 32);
+                            const ulonglong2 t0 = ldg(tt), t1 = ldg(tt + 1);
+                            d = __popcll(q0 ^ t0.x) + __popcll(q1 ^ t0.y) + __popcll(q2 ^ t1.x) + __popcll(q3 ^ t1.y);
                         }
                         const unsigned key = ((unsigned)d << 13) | (unsigned)p;
                         seen++;
@@ -630,7 +632,7 @@ __device__ void grid_sort(const ProjProblem& pb, unsigned* skey, unsigned* cnt) 
     for (int c = tid; c <= kNumCells; c += NT) cnt[c] = 0u;
     __syncthreads();
     for (int i = tid; i < n; i += NT) {
-        const orbx_keypoint& kp = pb.keys[i];
+        const orbx_keypoint kp = ldg(pb.keys + i);
         const int px = (int)roundf((kp.x - pb.min_x) * pb.inv_w);
         const int py = (int)roundf((kp.y - pb.min_y) * pb.inv_h);
         const bool in = !(px < 0 || px >= kGridCols || py < 0 || py >= kGridRows);
@@ -639,7 +641,7 @@ __device__ void grid_sort(const ProjProblem& pb, unsigned* skey, unsigned* cnt) 
     __syncthreads();
     block_exscan_u32<NT>(cnt, kNumCells + 1);
     for (int i = tid; i < n; i += NT) {
-        const orbx_keypoint& kp = pb.keys[i];
+        const orbx_keypoint kp = ldg(pb.keys + i);
         const int px = (int)roundf((kp.x - pb.min_x) * pb.inv_w);
         const int py = (int)roundf((kp.y - pb.min_y) * pb.inv_h);
         const bool in = !(px < 0 || px >= kGridCols || py < 0 || py >= kGridRows);
@@ -715,7 +717,8 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
     const int lane = threadIdx.x & 63;
     const int nq = pb.nq;
     int nmatch = 0, nrec = 0, nrescore = 0, niter = 0, ntrunc = 0;
-    unsigned long long t_res = 0, t_first = 0;  // diagnostics (stamps): re-scoring, chunk loads + first round
+    // diagnostics (stamps): re-scoring, chunk loads + first round, chunk loads alone
+    unsigned long long t_res = 0, t_first = 0, t_load = 0;
     const float factor = kHistoLength / 360.0f;
     const int need = P.ratio_mode ? 2 : 1;
     const unsigned long long below = (1ull << lane) - 1;
@@ -738,20 +741,23 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
     uint4 nx_l[kListVec];
     int nx_mp = -1;
     QueryReg nx_q;
+    // Unconditional loads (a clamped index; nx_ok marks the real ones): a load under a
+    // per-lane branch makes the compiler merge its registers at the join, which waits for
+    // the data at once and turns the prefetch into a stall.
+    bool nx_ok = false;
     auto fetch = [&](int qn) {
-        nx_mp = -1;
-        if (qn < nq) {
-            nx_q = load_query(pb, qn);
-            nx_mp = qmp[qn];
+        const int qc = min(qn, nq - 1);  // nq >= 1 wherever fetch runs
+        nx_ok = qn < nq;
+        nx_q = load_query(pb, qc);
+        nx_mp = qmp[qc];
 #pragma unroll
-            for (int v = 0; v < kListVec; v++) nx_l[v] = qk[kListVec * qn + v];
-        }
+        for (int v = 0; v < kListVec; v++) nx_l[v] = qk[kListVec * qc + v];
     };
-    fetch(lane);
+    if (nq > 0) fetch(lane);
     for (int base = 0; base < nq && guard >= 0; base += 64) {
         const int q = base + lane;
         const unsigned long long t_chunk = st ? wall_clock64() : 0;
-        int mp = nx_mp;
+        int mp = nx_ok ? nx_mp : -1;
         unsigned e[kTopK];
 #pragma unroll
         for (int v = 0; v < kListVec; v++) {
@@ -824,6 +830,7 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
         // what later lanes and the commit see of a lane's choice
         auto sig = [&]() { return exh ? kTrunc : (acc ? c1 : kNoEntry); };
         if (mp >= 0) eval(cblk);
+        if (st) t_load += wall_clock64() - t_chunk;
         int start = 0;
         int ow[kTopK];
         bool first = true;
@@ -940,6 +947,7 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
         }
         wave_lds_fence();
     }
+    if (st && lane == 0) st[15] = wall_clock64();
     if (guard < 0) nmatch = -1;  // a broken fixpoint (never observed): fail the parity check loudly
     // the match list (global scratch in some modes) is read back by other lanes below
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -998,6 +1006,7 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
         st[7] = niter;
         st[8] = t_res;
         st[9] = t_first;
+        st[14] = t_load;
     }
 }
 
@@ -1034,16 +1043,19 @@ __device__ void proj_replay_block(const ProjProblem& pb, const ProjParams& P, co
     uint4 nx_l[kListVec];
     int nx_mp = -1;
     QueryReg nx_q;
+    // Unconditional loads (a clamped index; nx_ok marks the real ones): a load under a
+    // per-lane branch makes the compiler merge its registers at the join, which waits for
+    // the data at once and turns the prefetch into a stall.
+    bool nx_ok = false;
     auto fetch = [&](int qn) {
-        nx_mp = -1;
-        if (qn < nq) {
-            nx_q = load_query(pb, qn);
-            nx_mp = qmp[qn];
+        const int qc = min(qn, nq - 1);  // nq >= 1 wherever fetch runs
+        nx_ok = qn < nq;
+        nx_q = load_query(pb, qc);
+        nx_mp = qmp[qc];
 #pragma unroll
-            for (int v = 0; v < kListVec; v++) nx_l[v] = qk[kListVec * qn + v];
-        }
+        for (int v = 0; v < kListVec; v++) nx_l[v] = qk[kListVec * qc + v];
     };
-    fetch(tid);
+    if (nq > 0) fetch(tid);
     __syncthreads();
     for (int base = 0; base < nq && !broken; base += RT) {
         if (it > (1u << 20)) {  // keep iteration << 10 in 31 bits: restart the tags
@@ -1052,7 +1064,7 @@ __device__ void proj_replay_block(const ProjProblem& pb, const ProjParams& P, co
             __syncthreads();
         }
         const int q = base + tid;
-        const int mp = nx_mp;
+        const int mp = nx_ok ? nx_mp : -1;
         unsigned e[kTopK];
 #pragma unroll
         for (int v = 0; v < kListVec; v++) {
@@ -1375,12 +1387,12 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     for (int p = tid; p < n; p += NT) {
         const unsigned k = skey[p];
         const int i = sk_idx(k);
-        const orbx_keypoint& kp = pb.keys[i];
+        const orbx_keypoint kp = ldg(pb.keys + i);
         sxy[p] = make_float2(kp.x, kp.y);
         if (SPLIT) {
-            if (kp_blocked(pb.frame_mp[i], P)) skey[p] = k | kKeyBlocked;
+            if (kp_blocked(ldg(pb.frame_mp + i), P)) skey[p] = k | kKeyBlocked;
         } else {
-            sfmp[p] = claim_word(pb.frame_mp[i], P);
+            sfmp[p] = claim_word(ldg(pb.frame_mp + i), P);
             owner[p] = 0x7fffffff;
         }
         if (QLDS) sang[p] = kp.angle;
@@ -1388,7 +1400,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     if (DLDS) {
         for (int t = tid; t < 2 * n; t += NT) {
             const int i = sk_idx(skey[t >> 1]);
-            sdesc[t] = ((const uint4*)(pb.desc + (size_t)i * 32))[t & 1];
+            sdesc[t] = ldg((const uint4*)(pb.desc + (size_t)i * 32) + (t & 1));
         }
     }
     __syncthreads();
@@ -1433,7 +1445,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
             ((unsigned*)(gb + gl.skey))[p] = skey[p] & ~kKeyBlocked;
             ((uint16_t*)(gb + gl.orun))[p] = orun[p];
             ((float2*)(gb + gl.sxy))[p] = sxy[p];
-            ((float*)(gb + gl.sang))[p] = pb.keys[sk_idx(skey[p])].angle;
+            ((float*)(gb + gl.sang))[p] = ldg(&pb.keys[sk_idx(skey[p])].angle);
         }
         for (int t = tid; t < nb; t += NT) ((uint16_t*)(gb + gl.bstart))[t] = bstart[t];
         return;
@@ -1442,7 +1454,7 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     // wave slots go back to whatever runs beside this kernel for the rest of its life.
     if (wave != 0) return;
     proj_replay(pb, P, G, sfmp, owner, (unsigned*)(smem + L.elist), qk, qmp, qang, mlist, mbin, s_hist,
-                [&](int tpos) { return QLDS ? sang[tpos] : pb.keys[sk_idx(skey[tpos])].angle; }, st);
+                [&](int tpos) { return QLDS ? sang[tpos] : ldg(&pb.keys[sk_idx(skey[tpos])].angle); }, st);
     wave_lds_fence();
     for (int p = lane; p < n; p += 64) pb.frame_mp[sk_idx(skey[p])] = claim_mp(sfmp[p]);
     if (st && lane == 0) st[4] = wall_clock64();
@@ -1512,15 +1524,15 @@ __global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem*
     for (int p = tid; p < n; p += kSeqGridThreads) {
         const unsigned k = skey[p];
         const int i = sk_idx(k);
-        const orbx_keypoint& kp = pb.keys[i];
+        const orbx_keypoint kp = ldg(pb.keys + i);
         gkey[p] = k;
         sxy[p] = make_float2(kp.x, kp.y);
         sang[p] = kp.angle;
-        gfmp[p] = claim_word(pb.frame_mp[i], P);
+        gfmp[p] = claim_word(ldg(pb.frame_mp + i), P);
     }
     for (int t = tid; t < 2 * n; t += kSeqGridThreads) {
         const int i = sk_idx(skey[t >> 1]);
-        sdesc[t] = ((const uint4*)(pb.desc + (size_t)i * 32))[t & 1];
+        sdesc[t] = ldg((const uint4*)(pb.desc + (size_t)i * 32) + (t & 1));
     }
     if (st) st[4] = wall_clock64();
     build_colstart<kSeqGridThreads>(skey, n, colstart);
@@ -1593,7 +1605,7 @@ __global__ __launch_bounds__(RT) void k_seq_commit(const ProjProblem* __restrict
     int* sfmp = (int*)(elist + kTopK * RT);
     int* owner = sfmp + n;
     for (int p = tid; p < n; p += RT) {
-        sfmp[p] = claim_word(pb.frame_mp[sk_idx(G.skey[p])], P);
+        sfmp[p] = claim_word(ldg(pb.frame_mp + sk_idx(G.skey[p])), P);
         owner[p] = RT == 64 ? 0x7fffffff : 0;
     }
     if (tid < kHistoLength) s_hist[tid] = 0;
@@ -2031,9 +2043,10 @@ __device__ unsigned score_tri_group(const TriProblem& pb, const TriQuery& Q, boo
     const int r = threadIdx.x & (K - 1);
     unsigned best = 0xffffffffu;
     if (valid && Q.beg < Q.end) {  // empty range: no shared node (batched tables: filtered queries)
-        const orbx_keypoint kp1 = pb.keys1[Q.idx1];
-        const unsigned long long* d1 = (const unsigned long long*)(pb.desc1 + (size_t)Q.idx1 * 32);
-        const unsigned long long q0 = d1[0], q1 = d1[1], q2 = d1[2], q3 = d1[3];
+        const orbx_keypoint kp1 = ldg(pb.keys1 + Q.idx1);
+        const ulonglong2* d1 = (const ulonglong2*)(pb.desc1 + (size_t)Q.idx1 * 32);
+        const ulonglong2 e0 = ldg(d1), e1 = ldg(d1 + 1);
+        const unsigned long long q0 = e0.x, q1 = e0.y, q2 = e1.x, q3 = e1.y;
         // epipolar line of kp1 in KF2 (CheckDistEpipolarLine, ORBmatcher.cc:186-213)
         const float* F = pb.F12;
         // fused as g++ -O3 -march=native builds the reference: the first product of each
@@ -2042,24 +2055,25 @@ __device__ unsigned score_tri_group(const TriProblem& pb, const TriQuery& Q, boo
         const float b = fmaf(kp1.x, F[1], kp1.y * F[4]) + F[7];
         const float c = fmaf(kp1.x, F[2], kp1.y * F[5]) + F[8];
         for (int p = Q.beg + r; p < Q.end; p += K) {
-            const int idx2 = pb.fv2_idx[p];
-            if (matched2[idx2] || pb.has_mp2[idx2]) continue;
-            const bool stereo2 = pb.u_right2 && pb.u_right2[idx2] >= 0;
+            const int idx2 = ldg(pb.fv2_idx + p);
+            if (matched2[idx2] || ldg(pb.has_mp2 + idx2)) continue;
+            const bool stereo2 = pb.u_right2 && ldg(pb.u_right2 + idx2) >= 0;
             if (pb.only_stereo && !stereo2) continue;
-            const unsigned long long* t = (const unsigned long long*)(pb.desc2 + (size_t)idx2 * 32);
-            const int dist = __popcll(q0 ^ t[0]) + __popcll(q1 ^ t[1]) + __popcll(q2 ^ t[2]) + __popcll(q3 ^ t[3]);
+            const ulonglong2* t = (const ulonglong2*)(pb.desc2 + (size_t)idx2 * 32);
+            const ulonglong2 t0 = ldg(t), t1 = ldg(t + 1);
+            const int dist = __popcll(q0 ^ t0.x) + __popcll(q1 ^ t0.y) + __popcll(q2 ^ t1.x) + __popcll(q3 ^ t1.y);
             if (dist > 50) continue;  // TH_LOW; the running bestDist bound is applied by the key order
-            const orbx_keypoint kp2 = pb.keys2[idx2];
+            const orbx_keypoint kp2 = ldg(pb.keys2 + idx2);
             if (!Q.stereo1 && !stereo2) {
                 const float distex = pb.ex - kp2.x;
                 const float distey = pb.ey - kp2.y;
-                if (fmaf(distex, distex, distey * distey) < 100 * pb.scale2[kp2.octave]) continue;
+                if (fmaf(distex, distex, distey * distey) < 100 * ldg(pb.scale2 + kp2.octave)) continue;
             }
             const float num = fmaf(a, kp2.x, b * kp2.y) + c;
             const float den = fmaf(a, a, b * b);
             if (den == 0) continue;
             const float dsqr = num * num / den;
-            if (!((double)dsqr < 3.84 * (double)pb.sigma2_2[kp2.octave])) continue;
+            if (!((double)dsqr < 3.84 * (double)ldg(pb.sigma2_2 + kp2.octave))) continue;
             const unsigned key = ((unsigned)dist << 26) | (0x3ffffffu - (unsigned)(p - Q.beg));
             best = key < best ? key : best;
         }
@@ -2106,7 +2120,7 @@ __global__ __launch_bounds__(kTriThreads) void k_triangulation(const TriProblem*
     for (int q0 = wave * 4; q0 < pb.nq; q0 += kTriThreads / 16) {
         const int q = q0 + (lane >> 4);
         const bool valid = q < pb.nq;
-        const unsigned best = score_tri_group<16>(pb, pb.q[valid ? q : q0], valid, matched2);
+        const unsigned best = score_tri_group<16>(pb, ldg(pb.q + (valid ? q : q0)), valid, matched2);
         if (valid && (lane & 15) == 0) keys[q] = tri_key64(best);
     }
     __syncthreads();
@@ -2123,14 +2137,14 @@ __global__ __launch_bounds__(kTriThreads) void k_triangulation(const TriProblem*
             unsigned long long l_best = kNoKey;
             float l_a1 = 0.f, l_a2 = 0.f;
             if (ql < pb.nq) {
-                const TriQuery Q = pb.q[ql];
+                const TriQuery Q = ldg(pb.q + ql);
                 l_idx1 = Q.idx1;
                 l_best = keys[ql];
                 if (l_best != kNoKey) {
-                    l_idx2 = pb.fv2_idx[Q.beg + (int)(0xffffffffu - (unsigned)(l_best & 0xffffffffu))];
-                    l_a2 = pb.keys2[l_idx2].angle;
+                    l_idx2 = ldg(pb.fv2_idx + Q.beg + (int)(0xffffffffu - (unsigned)(l_best & 0xffffffffu)));
+                    l_a2 = ldg(&pb.keys2[l_idx2].angle);
                 }
-                if (Q.idx1 >= 0) l_a1 = pb.keys1[Q.idx1].angle;
+                if (Q.idx1 >= 0) l_a1 = ldg(&pb.keys1[Q.idx1].angle);
             }
             // Rounds over the chunk: a lane's pre-scored best is still its answer unless an
             // earlier query took that keypoint (vbMatched2) or an earlier lane of this round
@@ -2168,12 +2182,12 @@ __global__ __launch_bounds__(kTriThreads) void k_triangulation(const TriProblem*
                 if (f >= 64) break;
                 wave_lds_fence();
                 // query q0 + f: re-score against the current claims, commit alone
-                const TriQuery Q = pb.q[q0 + f];
+                const TriQuery Q = ldg(pb.q + q0 + f);
                 unsigned long long best;
                 score_tri(pb, Q, matched2, best);
                 const int idx1 = __builtin_amdgcn_readlane(l_idx1, f);
                 const int idx2 = best != kNoKey
-                                     ? pb.fv2_idx[Q.beg + (int)(0xffffffffu - (unsigned)(best & 0xffffffffu))]
+                                     ? ldg(pb.fv2_idx + Q.beg + (int)(0xffffffffu - (unsigned)(best & 0xffffffffu)))
                                      : -1;
                 if (lane == f) l_idx2 = -1;  // resolved
                 if (idx2 >= 0) {

@@ -382,10 +382,12 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
         HIP_TRY(hipFree(d_st));
         auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
         fprintf(stderr, "[orbx call] n=%d nq=%d | host staging %.1f us, enqueue %.1f us, wait %.1f us | grid: start %.1f, "
-                "sort %.1f, writes %.1f, colstart %.1f, runs %.1f us | replay %.1f us, %llu iterations, %llu re-scored\n",
+                "sort %.1f, writes %.1f, colstart %.1f, runs %.1f us | replay %.1f us, %llu iterations, %llu re-scored "
+                "(%.1f us), chunk loads %.1f + first rounds %.1f us, after the loop %.1f us\n",
                 n, nq, us(t_stage0, t_flush), us(t_flush, t_enq), us(t_enq, t_done), (double)(h[1] - h[0]) * 0.01,
                 (double)(h[2] - h[1]) * 0.01, (double)(h[4] - h[2]) * 0.01, (double)(h[10] - h[4]) * 0.01,
-                (double)(h[11] - h[10]) * 0.01, (double)(h[3] - h[13]) * 0.01, h[7], h[5]);
+                (double)(h[11] - h[10]) * 0.01, (double)(h[3] - h[13]) * 0.01, h[7], h[5], (double)h[8] * 0.01,
+                (double)h[14] * 0.01, (double)(h[9] - h[14]) * 0.01, h[15] ? (double)(h[3] - h[15]) * 0.01 : 0.0);
     }
     if (nm < 0)  // the replay's iteration guard fired: frame_mp is partial, never report it as matches
         return fail(ORBX_ERR_STATE, "SearchByProjection replay did not converge (iteration guard)");
@@ -776,8 +778,8 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
     P.noct = nlevels;  // the extractor's keypoints have octave < nlevels
     // ORBX_MATCH_STAMPS=1: per-phase wall-clock breakdown of the search kernel to stderr
     // (diagnostics only; synchronises the stream).
-    // (split launches: the commit kernel's replay only)
-    const bool stamps = (!grids || split) && getenv("ORBX_MATCH_STAMPS") != nullptr;
+    // (with grids -- the split launches and the lean form -- the commit kernel's replay only)
+    const bool stamps = getenv("ORBX_MATCH_STAMPS") != nullptr;
     unsigned long long* d_st = nullptr;
     if (stamps) {
         HIP_TRY(hipMalloc(&d_st, sizeof(unsigned long long) * kStampWords * npairs));
@@ -799,10 +801,14 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
         HIP_TRY(hipStreamSynchronize(s));
         HIP_TRY(hipMemcpy(h.data(), d_st, h.size() * 8, hipMemcpyDeviceToHost));
         HIP_TRY(hipFree(d_st));
-        if (split) {
-            double cm = 0, cmx = 0, resc = 0, nq = 0, nit = 0, itmx = 0;
+        if (grids) {
+            double cm = 0, cmx = 0, resc = 0, nq = 0, nit = 0, itmx = 0, sc = 0, gr = 0;
             for (int p = 0; p < npairs; p++) {
                 const unsigned long long* r = &h[(size_t)kStampWords * p];
+                if (!split) {  // the lean form's search kernel: grid, then scoring
+                    gr += (double)(r[1] - r[0]) * 0.01;
+                    sc += (double)(r[2] - r[1]) * 0.01;
+                }
                 const double d = (double)(r[3] - r[13]) * 0.01;
                 cm += d;
                 cmx = d > cmx ? d : cmx;
@@ -812,9 +818,9 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
                 itmx = (double)r[7] > itmx ? (double)r[7] : itmx;
             }
             fprintf(stderr,
-                    "[orbx seq stamps] pairs=%d | commit mean/max %.1f/%.1f us | %.1f queries, %.1f re-scored, replay "
-                    "iterations mean/max %.1f/%.0f\n",
-                    npairs, cm / npairs, cmx, nq / npairs, resc / npairs, nit / npairs, itmx);
+                    "[orbx seq stamps] pairs=%d | grid %.1f, scoring %.1f us | commit mean/max %.1f/%.1f us | %.1f "
+                    "queries, %.1f re-scored, replay iterations mean/max %.1f/%.0f\n",
+                    npairs, gr / npairs, sc / npairs, cm / npairs, cmx, nq / npairs, resc / npairs, nit / npairs, itmx);
             return ORBX_OK;
         }
         double ph[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0}, resc = 0, nq = 0, nit = 0, tres = 0, tfirst = 0;
