@@ -1034,7 +1034,10 @@ __device__ void proj_replay_block(const ProjProblem& pb, const ProjParams& P, co
     const int need = P.ratio_mode ? 2 : 1;
     const unsigned long long below = (1ull << lane) - 1;
     const float factor = kHistoLength / 360.0f;
-    int nmatch = 0, nrec = 0, nrescore = 0, niter = 0;  // block-uniform
+    int nmatch = 0, nrec = 0, nrescore = 0, niter = 0, nstop = 0;  // block-uniform
+    // diagnostics (stamps, thread 0's clock): chunk loads, fixpoint rounds, commits, re-scoring
+    unsigned long long t_load = 0, t_round = 0, t_commit = 0, t_res = 0, tc = 0;
+    const bool clk = st && tid == 0;
     unsigned it = 0;
     long long guard = 0;
     bool broken = false;
@@ -1064,6 +1067,7 @@ __device__ void proj_replay_block(const ProjProblem& pb, const ProjParams& P, co
             __syncthreads();
         }
         const int q = base + tid;
+        if (clk) tc = wall_clock64();
         const int mp = nx_ok ? nx_mp : -1;
         unsigned e[kTopK];
 #pragma unroll
@@ -1121,6 +1125,11 @@ __device__ void proj_replay_block(const ProjProblem& pb, const ProjParams& P, co
         };
         auto sig = [&]() { return exh ? kTrunc : (acc ? c1 : kNoEntry); };
         if (mp >= 0) eval(cblk);
+        if (clk) {
+            const unsigned long long t = wall_clock64();
+            t_load += t - tc;
+            tc = t;
+        }
         int start = 0;
         unsigned ow[kTopK];
         while (true) {
@@ -1143,6 +1152,11 @@ __device__ void proj_replay_block(const ProjProblem& pb, const ProjParams& P, co
                 sb |= ((ow[j] >> 10) == it && (int)(1023u - (ow[j] & 1023u)) < tid ? 1u : 0u) << j;
             if (act) eval(cblk | sb);
             if (__syncthreads_or(act && sig() != old)) continue;
+            if (clk) {
+                const unsigned long long t = wall_clock64();
+                t_round += t - tc;
+                tc = t;
+            }
             // fixpoint: the first exhausted thread f stops the commit (a non-blocking
             // acceptor does not: see proj_replay)
             int key = act && exh ? tid : 0x7fffffff;
@@ -1185,7 +1199,13 @@ __device__ void proj_replay_block(const ProjProblem& pb, const ProjParams& P, co
             }
             nmatch += tot;
             if (P.check_ori) nrec += tot;
+            if (clk) {
+                const unsigned long long t = wall_clock64();
+                t_commit += t - tc;
+                tc = t;
+            }
             if (f >= RT) break;
+            nstop++;
             // the committed threads' claims, for the threads after them
             if (act && tid >= f) {
 #pragma unroll
@@ -1235,6 +1255,12 @@ __device__ void proj_replay_block(const ProjProblem& pb, const ProjParams& P, co
                         for (int r = 0; r < 4 && X; r++) X &= X - 1;
                     }
                 }
+            }
+            if (st) __syncthreads();  // diagnostics: every wave's re-scoring done before the clock
+            if (clk) {
+                const unsigned long long t = wall_clock64();
+                t_res += t - tc;
+                tc = t;
             }
         }
         __syncthreads();
@@ -1291,6 +1317,11 @@ __device__ void proj_replay_block(const ProjProblem& pb, const ProjParams& P, co
         st[5] = nrescore;
         st[6] = nq;
         st[7] = niter;
+        st[8] = t_res;
+        st[9] = t_round;
+        st[12] = nstop;
+        st[14] = t_load;
+        st[15] = t_commit;
     }
     __syncthreads();
 }

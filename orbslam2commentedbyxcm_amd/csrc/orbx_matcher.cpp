@@ -803,6 +803,7 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
         HIP_TRY(hipFree(d_st));
         if (grids) {
             double cm = 0, cmx = 0, resc = 0, nq = 0, nit = 0, itmx = 0, sc = 0, gr = 0;
+            double tl = 0, tr = 0, tcm = 0, trs = 0, nst = 0;
             for (int p = 0; p < npairs; p++) {
                 const unsigned long long* r = &h[(size_t)kStampWords * p];
                 if (!split) {  // the lean form's search kernel: grid, then scoring
@@ -810,6 +811,11 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
                     sc += (double)(r[2] - r[1]) * 0.01;
                 }
                 const double d = (double)(r[3] - r[13]) * 0.01;
+                tl += (double)r[14] * 0.01;
+                tr += (double)r[9] * 0.01;
+                tcm += (double)r[15] * 0.01;
+                trs += (double)r[8] * 0.01;
+                nst += (double)r[12];
                 cm += d;
                 cmx = d > cmx ? d : cmx;
                 resc += (double)r[5];
@@ -819,8 +825,10 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
             }
             fprintf(stderr,
                     "[orbx seq stamps] pairs=%d | grid %.1f, scoring %.1f us | commit mean/max %.1f/%.1f us | %.1f "
-                    "queries, %.1f re-scored, replay iterations mean/max %.1f/%.0f\n",
-                    npairs, gr / npairs, sc / npairs, cm / npairs, cmx, nq / npairs, resc / npairs, nit / npairs, itmx);
+                    "queries, %.1f re-scored, replay iterations mean/max %.1f/%.0f | chunk loads %.1f, rounds %.1f, "
+                    "commits %.1f, re-scoring %.1f us, %.1f stops\n",
+                    npairs, gr / npairs, sc / npairs, cm / npairs, cmx, nq / npairs, resc / npairs, nit / npairs, itmx,
+                    tl / npairs, tr / npairs, tcm / npairs, trs / npairs, nst / npairs);
             return ORBX_OK;
         }
         double ph[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0}, resc = 0, nq = 0, nit = 0, tres = 0, tfirst = 0;
