@@ -391,6 +391,33 @@ __device__ __forceinline__ QueryReg shfl_query(const QueryReg& x, int src) {
     return r;
 }
 
+#ifndef ORBX_MED3_INSERT
+#define ORBX_MED3_INSERT 1
+#endif
+// v_med3_u32 (no integer builtin; max(a, min(b, c)) is not matched to it)
+__device__ __forceinline__ unsigned med3_u32(unsigned a, unsigned b, unsigned c) {
+    unsigned d;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+// Insert key into the ascending list k[0..L) (keys distinct), dropping the largest.  With
+// k[i-1] <= k[i] the new k[i] is max(k[i-1], min(key, k[i])) = med3(k[i-1], key, k[i]):
+// one instruction per entry, top down, branch-free (a key above k[L-1] changes nothing).
+template <int L>
+__device__ __forceinline__ void sorted_insert(unsigned (&k)[L], unsigned key) {
+#if ORBX_MED3_INSERT
+#pragma unroll
+    for (int i = L - 1; i > 0; i--) k[i] = med3_u32(k[i - 1], key, k[i]);
+    k[0] = key < k[0] ? key : k[0];
+#else
+    if (key < k[L - 1]) {  // top down (reads k[i-1] first)
+#pragma unroll
+        for (int i = L - 1; i > 0; i--) k[i] = key < k[i - 1] ? k[i - 1] : (key < k[i] ? key : k[i]);
+        k[0] = key < k[0] ? key : k[0];
+    }
+#endif
+}
+
 // The kTopK best candidates of a query (GetFeaturesInArea + the overload's filters)
 // against the current claims sfmp, as entries (kNoEntry = no more candidates, kTrunc =
 // more candidates exist than listed).  One 16-lane row per query, four queries per wave:
@@ -500,12 +527,7 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
                                 const int d = __popcll(q0 ^ x0) + __popcll(q1 ^ x1) + __popcll(q2 ^ x2) + __popcll(q3 ^ x3);
                                 const unsigned key = ((unsigned)d << 13) | (unsigned)p;
                                 seen++;
-                                if (key < k[KL - 1]) {
-#pragma unroll
-                                    for (int i = KL - 1; i > 0; i--)
-                                        k[i] = key < k[i - 1] ? k[i - 1] : (key < k[i] ? key : k[i]);
-                                    k[0] = key < k[0] ? key : k[0];
-                                }
+                                sorted_insert<KL>(k, key);
                             };
                             take(okA, urA, pA, xA0, xA1, xA2, xA3);
                             take(okB, urB, pB, xB0, xB1, xB2, xB3);
@@ -547,11 +569,7 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
                         }
                         const unsigned key = ((unsigned)d << 13) | (unsigned)p;
                         seen++;
-                        if (key < k[KL - 1]) {  // sorted insert, top down (reads k[i-1] first)
-#pragma unroll
-                            for (int i = KL - 1; i > 0; i--) k[i] = key < k[i - 1] ? k[i - 1] : (key < k[i] ? key : k[i]);
-                            k[0] = key < k[0] ? key : k[0];
-                        }
+                        sorted_insert<KL>(k, key);
                     }
                 }
             }
