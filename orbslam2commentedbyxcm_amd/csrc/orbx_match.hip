@@ -447,6 +447,9 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
 #pragma unroll
     for (int i = 0; i < KL; i++) k[i] = kNoEntry;
     int seen = 0;
+#if ORBX_SCORE_COUNT
+    unsigned long long n_pair = 0, n_step = 0, n_ok = 0;
+#endif
     if (valid) {
         const CellRange cr = cell_range(pb, Q.u, Q.v, Q.r);
         if (!cr.empty) {
@@ -489,6 +492,9 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
                     // first / last block also hold rows outside the window
                     const uint16_t* bt = G.bstart + (ix * noct + o) * kNumBlk;
                     const int s0 = bt[b0], e0 = bt[b0 + 1], s1 = bt[b1], e1 = bt[b1 + 1];
+#if ORBX_SCORE_COUNT
+                    n_pair++;
+#endif
 #if ORBX_SCORE_PAIR
                     if (!G.sdesc) {
                         // two entries per step (a and a + lpc): their LDS chains (entry,
@@ -509,6 +515,10 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
                             const unsigned kkA = G.skey[pA], kkB = G.skey[pB];
                             const bool okA = test(a, entA, kA, kkA, pA);
                             const bool okB = h2 && test(a2, entB, kB, kkB, pB);
+#if ORBX_SCORE_COUNT
+                            n_step++;
+                            n_ok += (okA ? 1 : 0) + (okB ? 1 : 0);
+#endif
                             if (!okA && !okB) continue;
                             const int iA = sk_idx(kkA), iB = sk_idx(okB ? kkB : kkA);
                             const ulonglong2* tA = (const ulonglong2*)(pb.desc + (size_t)iA * 32);
@@ -575,6 +585,15 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
             }
         }
     }
+#if ORBX_SCORE_COUNT
+    if (P.stamps && valid) {
+        unsigned long long* sc = P.stamps + kStampWords * (size_t)blockIdx.x;
+        atomicAdd(sc + 16, n_pair);
+        atomicAdd(sc + 17, n_step);
+        atomicAdd(sc + 18, n_ok);
+        if (r == 0) atomicAdd(sc + 19, 1ull);
+    }
+#endif
     // Group top-kTopK: keys are unique (distinct positions), so one lane pops each minimum.
     const int rsh = K == 64 ? 0 : (threadIdx.x & (63 & ~(K - 1)));  // first lane of this group
     const unsigned long long gmask = K == 64 ? ~0ull : ((1ull << K) - 1);

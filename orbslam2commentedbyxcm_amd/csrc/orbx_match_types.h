@@ -52,7 +52,10 @@ struct ProjProblem {
 // the candidate list (ORBX_TOPK u32) + mp, angle, match list, bin
 constexpr int kProjScratchWords = ORBX_TOPK / 2 + 2;
 
-constexpr int kStampWords = 16;  // ProjParams::stamps words per problem
+#ifndef ORBX_SCORE_COUNT
+#define ORBX_SCORE_COUNT 0  // diagnostics build: the scoring loop's visit counts in stamp words 16-19
+#endif
+constexpr int kStampWords = ORBX_SCORE_COUNT ? 20 : 16;  // ProjParams::stamps words per problem
 
 // Call-level semantics of the SearchByProjection overload being executed.
 struct ProjParams {

@@ -823,6 +823,21 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
                 nit += (double)r[7];
                 itmx = (double)r[7] > itmx ? (double)r[7] : itmx;
             }
+#if ORBX_SCORE_COUNT
+            {
+                double a = 0, b = 0, c = 0, n = 0;
+                for (int p = 0; p < npairs; p++) {
+                    const unsigned long long* r = &h[(size_t)kStampWords * p];
+                    a += (double)r[16];
+                    b += (double)r[17];
+                    c += (double)r[18];
+                    n += (double)r[19];
+                }
+                fprintf(stderr, "[orbx score counts] per scored query: %.1f (column, octave) visits, %.1f entry steps, "
+                        "%.1f candidates in the window (summed over the query's lanes; %.0f queries)\n",
+                        a / n, b / n, c / n, n);
+            }
+#endif
             fprintf(stderr,
                     "[orbx seq stamps] pairs=%d | grid %.1f, scoring %.1f us | commit mean/max %.1f/%.1f us | %.1f "
                     "queries, %.1f re-scored, replay iterations mean/max %.1f/%.0f | chunk loads %.1f, rounds %.1f, "
