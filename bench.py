@@ -122,11 +122,23 @@ def _stage_sum(ks: dict, stage: str, field: str, count: str = None):
 
 
 def newest_profiles(pattern: str):
-    """profiles/ files matching `pattern` (vocabulary runs excluded), oldest first by the
-    numbers in their tags (r01v9 < r01v10)."""
+    """profiles/ files matching `pattern` (vocabulary runs excluded), oldest first: the
+    ones taken at the current source_hash() last, each group by the numbers in its tags
+    (r01v9 < r01v10) -- a pass at HEAD wins whatever its letter (r04f after r04n)."""
     import re
     files = [f for f in (ROOT / "profiles").glob(pattern) if "vocab" not in f.name]
-    return sorted(files, key=lambda f: ([int(x) for x in re.findall(r"\d+", f.name)], f.name))
+    cur = _current_source_hash()
+    return sorted(files, key=lambda f: (profile_hash(f) == cur, [int(x) for x in re.findall(r"\d+", f.name)], f.name))
+
+
+_SRC_HASH = None
+
+
+def _current_source_hash() -> str:
+    global _SRC_HASH
+    if _SRC_HASH is None:
+        _SRC_HASH = source_hash()
+    return _SRC_HASH
 
 
 def rocprof_mean_ms(stage: str, workload: str):

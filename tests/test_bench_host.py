@@ -92,6 +92,20 @@ def test_newest_profile_is_highest_tag():
     assert "orbx::k_level_tiles" in data["kernels"]
 
 
+def test_newest_profiles_prefer_the_current_source(tmp_path, monkeypatch):
+    """A pass taken at the code's current source hash counts as newest whatever its tag's
+    letter; without one, the tags' numbers and names decide."""
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    for tag, h in (("r04n", "old"), ("r04f", "cur")):
+        (prof / f"{tag}_tum_pmc_traffic.json").write_text(json.dumps({"source_hash": h, "kernels": {}}))
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    monkeypatch.setattr(bench, "_SRC_HASH", "cur")
+    assert [f.name for f in bench.newest_profiles("*_pmc_traffic.json")][-1] == "r04f_tum_pmc_traffic.json"
+    monkeypatch.setattr(bench, "_SRC_HASH", "other")
+    assert [f.name for f in bench.newest_profiles("*_pmc_traffic.json")][-1] == "r04n_tum_pmc_traffic.json"
+
+
 def test_gpus_flag_launches_that_many_ranks():
     """bench.py --gpus 2 with no launcher starts two ranks itself (the path the driver's
     N>1 runs take when WORLD_SIZE is unset); each joins the group (gloo here)."""
