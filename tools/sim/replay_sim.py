@@ -1,7 +1,9 @@
 """Simulation of SearchByProjection's sequential claim replay (H5) and of two parallel
-forms, on random candidate lists: the chunked Jacobi fixpoint k_seq_commit / proj_replay
-ship (64 queries per chunk) and a sliding-window form (lanes retire as soon as every
-earlier lane is certified, and take the next query).  Checks both against the
+forms, on random candidate lists: the chunked Jacobi fixpoint of k_seq_commit /
+proj_replay (64 queries per chunk; round 3 with non-blocking acceptances as sequence
+points, round 4 without, its claims written as the kernel writes them) and a
+sliding-window form (lanes retire as soon as every earlier lane is certified, and take
+the next query).  Checks both against the
 sequential loop and counts iterations.  TEST / DESIGN TOOLING ONLY.
 
     python tools/sim/replay_sim.py [--scenes 300] [--seed 0]
@@ -57,6 +59,16 @@ def sequential(qs, bself, ratio):
         if a is not None and bself[q]:
             blocked.add(a[1])
     return out
+
+
+def final_claims(qs, out):
+    """The keypoint -> query map the reference leaves in F.mvpMapPoints: every acceptance
+    writes its keypoint, so the last one in query order keeps it (ORBmatcher.cc:167)."""
+    m = {}
+    for q, a in enumerate(out):
+        if a is not None:
+            m[a[1]] = q
+    return m
 
 
 class Lane:
@@ -199,13 +211,66 @@ def chunked(qs, bself, ratio, W=64):
     return out, iters
 
 
+def chunked_nb(qs, bself, ratio, W=64):
+    """The round-4 form: like chunked, but a non-blocking acceptance does not stop the
+    commit; the claims are written as the kernel writes them -- blocking ones directly,
+    a non-blocking one only when no later lane of the same commit claims its keypoint.
+    Returns (acceptances, final keypoint -> query map, iterations)."""
+    nq = len(qs)
+    committed = set()
+    out = [None] * nq
+    claims = {}
+    iters = 0
+    for base in range(0, nq, W):
+        qrange = list(range(base, min(nq, base + W)))
+        lanes = {q: Lane(q, qs, committed) for q in qrange}
+        start = base
+        while start < qrange[-1] + 1:
+            changed = True
+            prop = {}
+            while changed:
+                iters += 1
+                owner = {}
+                for q, p in prop.items():
+                    if p is not None and (p not in owner or q < owner[p]):
+                        owner[p] = q
+                changed, newprop = False, {}
+                for q in range(start, qrange[-1] + 1):
+                    L = lanes[q]
+                    blocked = committed | {p for p, o in owner.items() if o < q}
+                    s = evaluate(L, blocked, ratio)
+                    if s != L.sig:
+                        changed = True
+                    L.sig = s
+                    newprop[q] = s[1] if (s not in (NONE, TRUNC) and bself[q]) else None
+                prop = newprop
+            f = next((q for q in range(start, qrange[-1] + 1) if lanes[q].sig is TRUNC), qrange[-1] + 1)
+            com = [q for q in range(start, f) if lanes[q].sig is not NONE]
+            last = {}
+            for q in com:  # the dedup pass: the highest committing lane per keypoint
+                last[lanes[q].sig[1]] = q
+            for q in com:
+                out[q] = lanes[q].sig
+                p = lanes[q].sig[1]
+                if bself[q]:
+                    committed.add(p)
+                    claims[p] = q
+                elif last[p] == q:
+                    claims[p] = q
+            if f <= qrange[-1]:
+                lanes[f].relist(qs, committed)
+                lanes[f].sig = None
+            start = f
+    return out, claims, iters
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scenes", type=int, default=300)
     ap.add_argument("--seed", type=int, default=0)
     a = ap.parse_args()
     rng = random.Random(a.seed)
-    tot_s = tot_c = 0
+    tot_s = tot_c = tot_n = 0
     for i in range(a.scenes):
         nq = rng.choice([64, 200, 1000])
         ratio = rng.random() < 0.5
@@ -214,12 +279,15 @@ def main():
         ref = sequential(qs, bself, ratio)
         s, it_s = sliding(qs, bself, ratio)
         c, it_c = chunked(qs, bself, ratio)
+        n, cl, it_n = chunked_nb(qs, bself, ratio)
         assert s == ref, ("sliding", i)
         assert c == ref, ("chunked", i)
+        assert n == ref and cl == final_claims(qs, ref), ("chunked_nb", i)
         tot_s += it_s
         tot_c += it_c
-    print(f"{a.scenes} scenes: all equal to the sequential loop; iterations chunked {tot_c}, sliding {tot_s} "
-          f"({tot_c / max(tot_s, 1):.2f}x fewer)")
+        tot_n += it_n
+    print(f"{a.scenes} scenes: all equal to the sequential loop; iterations chunked (round 3) {tot_c}, "
+          f"chunked with non-blocking commits (round 4) {tot_n}, sliding {tot_s}")
 
 
 if __name__ == "__main__":
