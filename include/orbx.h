@@ -341,6 +341,10 @@ typedef struct {
     int global_ids;               /* 0: MapPoint id = LastFrame keypoint index i; 1: id = (b-1)*cap + i */
     int32_t* cur_mp;              /* [B][cap] out: CurrentFrame.mvpMapPoints as MapPoint ids, -1 */
     int32_t* nmatches;            /* [B] out (frame 0: 0) */
+    const int32_t* mp_obs;        /* [B*cap] Observations() per MapPoint id (device; needs global_ids), or
+                                     NULL: every MapPoint has Observations() > 0.  A claim by a MapPoint
+                                     with 0 observations (UpdateLastFrame's temporal points) does not
+                                     block the keypoint (ORBmatcher.cc:1716-1718) */
 } orbx_sequence;
 int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* seq, void* stream);
 
@@ -601,6 +605,22 @@ int orbx_create_mappoints_device(int batch, const orbx_keypoint* d_kps, const in
                                  float cx, float cy, const float* scale_factors, int nlevels, float* d_pos,
                                  float* d_normal, float* d_max_distance, float* d_min_distance,
                                  int32_t* d_observations, uint8_t* d_bad, void* stream);
+
+/* Tracking::UpdateLastFrame (Tracking.cc:893-954) for B stereo / RGB-D LastFrames in HBM
+ * (none of them the last keyframe): the keypoints with mvDepth > 0 are visited nearest
+ * first (pairs (depth, index) ascending); one without a MapPoint, or whose MapPoint has
+ * Observations() < 1, gets a temporal MapPoint at Frame::UnprojectStereo(i) (Frame.cc:
+ * 912-927) with Observations() 0; the walk ends after the first point beyond th_depth
+ * (mThDepth = mbf * ThDepth / fx) once more than 100 points were visited.  In: d_obs_in
+ * [B][cap] Observations() of LastFrame.mvpMapPoints (-1 = NULL) and d_pos_in [B][cap][3]
+ * their world positions, or both NULL (no MapPoints).  Out: d_mp_obs [B][cap] (-1 = none),
+ * d_mp_pos [B][cap][3], d_has_mp [B][cap] -- the orbx_sequence mp_obs / mp_pos / has_mp
+ * inputs of the following TrackWithMotionModel search (global ids b*cap + i).  The outputs
+ * may alias the inputs.  Asynchronous. */
+int orbx_update_last_frame_device(int batch, const orbx_keypoint* d_kps, const int32_t* d_n, int cap,
+                                  const float* d_depth, const float* d_Tcw, float fx, float fy, float cx, float cy,
+                                  float th_depth, const int32_t* d_obs_in, const float* d_pos_in, int32_t* d_mp_obs,
+                                  float* d_mp_pos, uint8_t* d_has_mp, void* stream);
 
 /* ---- DBoW2 vocabulary (TemplatedVocabulary<FORB::TDescriptor, FORB>, §8(f) rank 1) ----
  * The tree lives in HBM as its CSR edge list.  Scoring / weighting

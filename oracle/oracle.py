@@ -415,6 +415,24 @@ def create_mappoints(F, depth=None, const_depth=0.0):
     return out
 
 
+def update_last_frame(F, depth, th_depth, mp_obs=None, pos=None):
+    """Tracking::UpdateLastFrame (Tracking.cc:893-954) for a stereo LastFrame: temporal
+    MapPoints at UnprojectStereo for the nearest keypoints with depth.  mp_obs (n,) i32:
+    Observations() of each keypoint's MapPoint (-1 = NULL, default all NULL); pos (n, 3):
+    their world positions.  -> (mp_obs, pos, created), new arrays (temporal points get 0)."""
+    keep = []
+    f = _frame(F, keep)
+    n = len(F.keys)
+    obs = np.full(n, -1, np.int32) if mp_obs is None else np.array(mp_obs, np.int32, copy=True)
+    p = np.zeros((n, 3), np.float32) if pos is None else np.array(pos, np.float32, copy=True).reshape(n, 3)
+    d = np.ascontiguousarray(depth, np.float32)
+    L = lib()
+    L.ora_update_last_frame.argtypes = [C.c_void_p, F32P, C.c_float, I32P, F32P]
+    created = L.ora_update_last_frame(C.addressof(f), d.ctypes.data_as(F32P), float(th_depth),
+                                      obs.ctypes.data_as(I32P), p.ctypes.data_as(F32P))
+    return obs, p, created
+
+
 def search_local_points(F, frame_mp, local_ids, mps, th, nnratio=0.8, viewing_cos_limit=0.5):
     """Tracking::SearchLocalPoints (Tracking.cc:1280-1336) for one Frame, restated over the
     oracle's IsInFrustum and SearchByProjection(F, vpMapPoints, th): frame_mp (MapPoint ids)

@@ -433,6 +433,61 @@ void ora_create_mappoints(const ora_frame* f, const float* depth, float const_de
     }
 }
 
+/* Tracking::UpdateLastFrame (Tracking.cc:893-954), after SetPose, for a stereo / RGB-D
+ * LastFrame that is not the last keyframe: the pairs (mvDepth[i], i) with depth > 0 are
+ * sorted ascending (std::sort of pair<float,int>: depth, then index) and visited in order;
+ * a keypoint without a MapPoint, or whose MapPoint has Observations() < 1, gets a new
+ * temporal MapPoint at Frame::UnprojectStereo(i) (created without AddObservation, so its
+ * Observations() is 0); every visited point counts, and the walk stops after the first
+ * point deeper than th_depth (mThDepth) once more than 100 have been visited (cc:951-952).
+ * mp_obs[i]: in, Observations() of keypoint i's MapPoint (-1 = NULL); out, 0 where a
+ * temporal point was made.  pos[3i..3i+2]: in, that MapPoint's GetWorldPos(); out, the
+ * temporal point's.  Returns the number of temporal points. */
+typedef struct {
+    float z;
+    int i;
+} depth_idx;
+
+static int cmp_depth_idx(const void* a, const void* b) {
+    const depth_idx* x = (const depth_idx*)a;
+    const depth_idx* y = (const depth_idx*)b;
+    if (x->z < y->z) return -1;
+    if (x->z > y->z) return 1;
+    return (x->i > y->i) - (x->i < y->i);
+}
+
+int ora_update_last_frame(const ora_frame* f, const float* depth, float th_depth, int32_t* mp_obs, float* pos) {
+    depth_idx* v = (depth_idx*)malloc(sizeof(depth_idx) * (size_t)(f->n + 1));
+    int m = 0;
+    for (int i = 0; i < f->n; i++)
+        if (depth[i] > 0) {
+            v[m].z = depth[i];
+            v[m].i = i;
+            m++;
+        }
+    qsort(v, (size_t)m, sizeof(depth_idx), cmp_depth_idx);
+    const float* T = f->Tcw;
+    const float invfx = 1.0f / f->fx, invfy = 1.0f / f->fy;
+    float Ow[3];
+    for (int r = 0; r < 3; r++) Ow[r] = -(T[r] * T[3] + T[4 + r] * T[7] + T[8 + r] * T[11]);
+    int nPoints = 0, created = 0;
+    for (int j = 0; j < m; j++) {
+        const int i = v[j].i;
+        if (mp_obs[i] < 1) { /* !pMP || pMP->Observations() < 1 */
+            const float z = depth[i];
+            const float x = (f->keys[i].x - f->cx) * z * invfx;
+            const float y = (f->keys[i].y - f->cy) * z * invfy;
+            for (int r = 0; r < 3; r++) pos[3 * i + r] = T[r] * x + T[4 + r] * y + T[8 + r] * z + Ow[r];
+            mp_obs[i] = 0;
+            created++;
+        }
+        nPoints++;
+        if (v[j].z > th_depth && nPoints > 100) break;
+    }
+    free(v);
+    return created;
+}
+
 /* ---------------------------------------------------------------- a13 */
 
 /* ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>&

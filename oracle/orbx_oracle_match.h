@@ -68,6 +68,8 @@ void ora_is_in_frustum(const ora_frame* f, const ora_mappoints* mps, const int32
                        int32_t* scale_level, float* view_cos);
 void ora_create_mappoints(const ora_frame* f, const float* depth, float const_depth, float* pos, float* normal,
                           float* max_distance, float* min_distance, uint8_t* valid);
+/* Tracking::UpdateLastFrame (Tracking.cc:893-954): temporal MapPoints of a stereo LastFrame */
+int ora_update_last_frame(const ora_frame* f, const float* depth, float th_depth, int32_t* mp_obs, float* pos);
 int ora_sbp_frame(const ora_frame* cur, int32_t* cur_mp, const ora_frame* last, const int32_t* last_mp,
                   const uint8_t* last_outlier, const ora_mappoints* mps, float th, int bMono, int check_ori);
 int ora_sbp_keyframe(const ora_frame* cur, int32_t* cur_mp, const ora_frame* kf, const int32_t* kf_mp,

@@ -49,7 +49,7 @@ EXPORTED = [
     "orbx_compute_distinctive_descriptors_device", "orbx_extractor_status", "orbx_extractor_status_device",
     "orbx_extractor_set_node_capacity", "orbx_extractor_set_level0_in_place", "orbx_compute_stereo_matches_batch_device",
     "orbx_search_for_triangulation_batch_device", "orbx_match_sequence_device_ex",
-    "orbx_search_local_points_device", "orbx_create_mappoints_device",
+    "orbx_search_local_points_device", "orbx_create_mappoints_device", "orbx_update_last_frame_device",
 ]
 
 
@@ -71,7 +71,7 @@ class Sequence(C.Structure):
                 ("bf", C.c_float), ("b", C.c_float), ("min_x", C.c_float), ("max_x", C.c_float),
                 ("min_y", C.c_float), ("max_y", C.c_float), ("nlevels", C.c_int),
                 ("scale_factors", C.POINTER(C.c_float)), ("th", C.c_float), ("mono", C.c_int),
-                ("global_ids", C.c_int), ("cur_mp", C.c_void_p), ("nmatches", C.c_void_p)]
+                ("global_ids", C.c_int), ("cur_mp", C.c_void_p), ("nmatches", C.c_void_p), ("mp_obs", C.c_void_p)]
 
 
 class MapPointsDevice(C.Structure):
@@ -169,6 +169,8 @@ def lib() -> C.CDLL:
     L.orbx_search_local_points_device.argtypes = [vp, C.POINTER(MapPointsDevice), C.POINTER(LocalMapBatch), vp]
     L.orbx_create_mappoints_device.argtypes = [C.c_int, vp, vp, C.c_int, vp, C.c_float, vp, C.c_float, C.c_float,
                                                C.c_float, C.c_float, fp, C.c_int, vp, vp, vp, vp, vp, vp, vp]
+    L.orbx_update_last_frame_device.argtypes = [C.c_int, vp, vp, C.c_int, vp, vp, C.c_float, C.c_float, C.c_float,
+                                                C.c_float, C.c_float, vp, vp, vp, vp, vp, vp]
     L.orbx_search_by_projection_keyframe.argtypes = [vp, vp, i32p, vp, i32p, u8p, vp, C.c_float, C.c_int, ip]
     L.orbx_search_by_projection_sim3.argtypes = [vp, vp, fp, i32p, C.c_int, i32p, vp, C.c_int, ip]
     L.orbx_search_by_bow_frame.argtypes = [vp, vp, i32p, i32p, i32p, i32p, C.c_int, vp, i32p, i32p, i32p, C.c_int,

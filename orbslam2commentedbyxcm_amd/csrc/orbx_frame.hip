@@ -190,6 +190,114 @@ __global__ __launch_bounds__(256) void k_create_mappoints(MapPointArgs A, int to
     A.bad[id] = 0;
 }
 
+// Tracking::UpdateLastFrame (Tracking.cc:893-954) for B stereo LastFrames, one 256-thread
+// workgroup per frame.  The reference sorts (mvDepth[i], i) for depth > 0 and visits the
+// pairs in order, giving a keypoint without a MapPoint (or with Observations() < 1) a
+// temporal MapPoint at UnprojectStereo(i), until it has visited more than 100 points and the
+// current one lies beyond mThDepth.  With c points at depth <= th_depth among m with depth,
+// the visited set is therefore the K = min(m, max(c, 100) + 1) smallest (depth, index)
+// pairs: every point within th_depth, plus the nearest kb = K - c beyond it -- one (the
+// minimum key) when c >= 100, and otherwise ranked by counting.  No sort is needed.
+// Keys (float bits of depth << 32 | index) order like the pairs: depths are positive.
+struct LastFrameArgs {
+    const orbx_keypoint* kps;
+    const int32_t* n;
+    int cap;
+    const float* depth;      // [B][cap] mvDepth
+    const float* Tcw;        // [B][12]
+    float fx, fy, cx, cy;
+    float th_depth;          // mThDepth
+    const int32_t* obs_in;   // [B][cap] Observations() of LastFrame's MapPoints (-1 = NULL) or null
+    const float* pos_in;     // [B][cap][3] their GetWorldPos() (read where obs_in >= 0)
+    int32_t* mp_obs;         // [B][cap] out (-1 = no MapPoint; 0 = temporal)
+    float* mp_pos;           // [B][cap][3] out
+    uint8_t* has_mp;         // [B][cap] out
+};
+
+constexpr int kLastFrameThreads = 256;
+
+__global__ __launch_bounds__(kLastFrameThreads) void k_update_last_frame(LastFrameArgs A) {
+    const int b = blockIdx.x;
+    const int t = threadIdx.x;
+    const int n = A.n[b] < A.cap ? A.n[b] : A.cap;
+    const size_t base = (size_t)b * A.cap;
+    const float* dep = A.depth + base;
+    __shared__ int s_c, s_m;
+    __shared__ unsigned long long s_min;
+    if (t == 0) {
+        s_c = 0;
+        s_m = 0;
+        s_min = ~0ull;
+    }
+    __syncthreads();
+    int c = 0, m = 0;
+    unsigned long long mn = ~0ull;
+    for (int i = t; i < n; i += kLastFrameThreads) {
+        const float z = dep[i];
+        if (z > 0) {
+            m++;
+            if (z <= A.th_depth) {
+                c++;
+            } else {
+                const unsigned long long k = (unsigned long long)__float_as_uint(z) << 32 | (unsigned)i;
+                mn = k < mn ? k : mn;
+            }
+        }
+    }
+    if (c) atomicAdd(&s_c, c);
+    if (m) atomicAdd(&s_m, m);
+    if (mn != ~0ull) atomicMin(&s_min, mn);
+    __syncthreads();
+    const int C = s_c, M = s_m;
+    const int K = M < (C > 100 ? C : 100) + 1 ? M : (C > 100 ? C : 100) + 1;
+    const int kb = K - C;  // beyond-threshold points visited
+    const float* T = A.Tcw + 12 * (size_t)b;
+    const float invfx = 1.0f / A.fx, invfy = 1.0f / A.fy;
+    float Ow[3];
+    for (int r = 0; r < 3; r++) Ow[r] = -(T[r] * T[3] + T[4 + r] * T[7] + T[8 + r] * T[11]);
+    for (int i = t; i < A.cap; i += kLastFrameThreads) {
+        int obs = -1;
+        float p[3] = {0.f, 0.f, 0.f};
+        if (i < n) {
+            if (A.obs_in) {
+                obs = A.obs_in[base + i];
+                if (obs >= 0)
+                    for (int r = 0; r < 3; r++) p[r] = A.pos_in[3 * (base + i) + r];
+            }
+            const float z = dep[i];
+            bool visited = false;
+            if (z > 0) {
+                if (z <= A.th_depth) {
+                    visited = true;
+                } else if (kb > 0) {
+                    const unsigned long long k = (unsigned long long)__float_as_uint(z) << 32 | (unsigned)i;
+                    if (kb == 1) {
+                        visited = k == s_min;
+                    } else {  // c < 100: rank among the beyond-threshold keys (rare)
+                        int rank = 0;
+                        for (int j = 0; j < n && rank < kb; j++) {
+                            const float zj = dep[j];
+                            if (zj > A.th_depth)
+                                rank += ((unsigned long long)__float_as_uint(zj) << 32 | (unsigned)j) < k;
+                        }
+                        visited = rank < kb;
+                    }
+                }
+            }
+            if (visited && obs < 1) {  // !pMP || pMP->Observations() < 1: new temporal MapPoint
+                const orbx_keypoint kp = A.kps[base + i];
+                const float x = (kp.x - A.cx) * z * invfx;
+                const float y = (kp.y - A.cy) * z * invfy;
+                for (int r = 0; r < 3; r++) p[r] = T[r] * x + T[4 + r] * y + T[8 + r] * z + Ow[r];
+                obs = 0;
+            }
+        }
+        A.mp_obs[base + i] = obs;
+        A.has_mp[base + i] = obs >= 0;
+        for (int r = 0; r < 3; r++) A.mp_pos[3 * (base + i) + r] = p[r];
+    }
+}
+
 }  // namespace orbx
 
 namespace {
@@ -352,6 +460,37 @@ int orbx_create_mappoints_device(int batch, const orbx_keypoint* d_kps, const in
     if (total >= (1ll << 31)) return fail(ORBX_ERR_ARG, "batch * cap too large");
     hipLaunchKernelGGL(k_create_mappoints, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A,
                        (int)total);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(ORBX_ERR_HIP, hipGetErrorString(e));
+    return ORBX_OK;
+}
+
+int orbx_update_last_frame_device(int batch, const orbx_keypoint* d_kps, const int32_t* d_n, int cap,
+                                  const float* d_depth, const float* d_Tcw, float fx, float fy, float cx, float cy,
+                                  float th_depth, const int32_t* d_obs_in, const float* d_pos_in, int32_t* d_mp_obs,
+                                  float* d_mp_pos, uint8_t* d_has_mp, void* stream) {
+    if (batch < 0 || cap <= 0) return fail(ORBX_ERR_ARG, "bad argument");
+    if (batch == 0) return ORBX_OK;
+    if (!d_kps || !d_n || !d_depth || !d_Tcw || !d_mp_obs || !d_mp_pos || !d_has_mp || (d_obs_in && !d_pos_in))
+        return fail(ORBX_ERR_ARG, "null buffer");
+    if (!(fx != 0.f) || !(fy != 0.f)) return fail(ORBX_ERR_ARG, "fx, fy must be non-zero");
+    LastFrameArgs A{};
+    A.kps = d_kps;
+    A.n = d_n;
+    A.cap = cap;
+    A.depth = d_depth;
+    A.Tcw = d_Tcw;
+    A.fx = fx;
+    A.fy = fy;
+    A.cx = cx;
+    A.cy = cy;
+    A.th_depth = th_depth;
+    A.obs_in = d_obs_in;
+    A.pos_in = d_pos_in;
+    A.mp_obs = d_mp_obs;
+    A.mp_pos = d_mp_pos;
+    A.has_mp = d_has_mp;
+    hipLaunchKernelGGL(k_update_last_frame, dim3(batch), dim3(kLastFrameThreads), 0, (hipStream_t)stream, A);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(ORBX_ERR_HIP, hipGetErrorString(e));
     return ORBX_OK;

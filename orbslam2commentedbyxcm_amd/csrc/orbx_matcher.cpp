@@ -710,6 +710,7 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
         return fail(ORBX_ERR_ARG, "null buffer");
     if ((long long)batch * cap >= kMaxMapPointIds) return fail(ORBX_ERR_ARG, "batch x cap MapPoint ids >= 2^30");
     if (!sq->mono && !(sq->b > 0.f)) return fail(ORBX_ERR_ARG, "stereo / RGB-D sequence needs the baseline mb > 0");
+    if (sq->mp_obs && !sq->global_ids) return fail(ORBX_ERR_ARG, "mp_obs is indexed by global MapPoint ids");
     int32_t* d_cur_mp = sq->cur_mp;
     int32_t* d_nmatches = sq->nmatches;
     HIP_TRY(hipSetDevice(m->device));
@@ -770,8 +771,10 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
     }
     HIP_TRY(launch_seq_build(A, npairs, d_q, d_prob, d_off, s));
     ProjParams P{};
-    P.mp_obs = nullptr;
-    P.blocked_mode = 1;  // every MapPoint of the sequence has Observations() > 0
+    // without mp_obs every MapPoint of the sequence has Observations() > 0; with it a claim
+    // blocks only when the claiming MapPoint's does (ORBmatcher.cc:1716-1718)
+    P.mp_obs = sq->mp_obs;
+    P.blocked_mode = sq->mp_obs ? 0 : 1;
     P.accept_th = TH_HIGH;
     P.ratio_mode = 0;
     P.check_ori = m->check_ori;

@@ -433,11 +433,12 @@ class ORBmatcher:
     def match_sequence_device_ex(self, d_kps, d_desc, d_n, d_Tcw, d_cur_mp, d_nmatches, scale_factors, fx, fy, cx,
                                  cy, width, height, th: float = 15.0, mono: bool = True, bf: float = 0.0,
                                  b: float = 0.0, d_u_right=None, d_mp_pos=None, d_has_mp=None, depth: float = 5.0,
-                                 global_ids: bool = False, stream=None) -> None:
+                                 global_ids: bool = False, d_mp_obs=None, stream=None) -> None:
         """orbx_match_sequence_device_ex: TrackWithMotionModel's SearchByProjection(frame b,
         frame b-1, th, mono) for every b >= 1 of a device sequence, stereo included
         (d_u_right (B, cap) f32), LastFrame MapPoints at d_mp_pos (B, cap, 3) f32 (or at
-        `depth` on the keypoint rays), d_has_mp (B, cap) u8 masking keypoints without one."""
+        `depth` on the keypoint rays), d_has_mp (B, cap) u8 masking keypoints without one,
+        d_mp_obs (B, cap) i32 their Observations() (global ids; default: all > 0)."""
         B, cap = d_desc.shape[0], d_desc.shape[1]
         sf = _f32(scale_factors)
         ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
@@ -451,6 +452,7 @@ class ORBmatcher:
         q.scale_factors = sf.ctypes.data_as(F32P)
         q.th, q.mono, q.global_ids = th, 1 if mono else 0, 1 if global_ids else 0
         q.cur_mp, q.nmatches = ptr(d_cur_mp), ptr(d_nmatches)
+        q.mp_obs = ptr(d_mp_obs)
         s = None if stream is None else C.c_void_p(getattr(stream, "cuda_stream", stream))
         L.check(L.lib().orbx_match_sequence_device_ex(self._h, C.byref(q), s))
 
@@ -534,6 +536,27 @@ def create_mappoints_device(d_kps, d_n, d_Tcw, scale_factors, fx, fy, cx, cy, ou
         B, ptr(d_kps), ptr(d_n), cap, ptr(d_depth), float(const_depth), ptr(d_Tcw), fx, fy, cx, cy,
         sf.ctypes.data_as(F32P), len(sf), ptr(out["pos"]), ptr(out["normal"]), ptr(out["max_distance"]),
         ptr(out["min_distance"]), ptr(out["observations"]), ptr(out["bad"]), s))
+
+
+def update_last_frame_device(d_kps, d_n, d_depth, d_Tcw, fx, fy, cx, cy, th_depth, out: dict, d_obs_in=None,
+                             d_pos_in=None, stream=None) -> None:
+    """orbx_update_last_frame_device: Tracking::UpdateLastFrame's temporal MapPoints for B
+    stereo LastFrames (device tensors; out: mp_obs (B, cap) i32, mp_pos (B, cap, 3) f32,
+    has_mp (B, cap) u8, e.g. from last_frame_table).  Asynchronous."""
+    B, cap = d_kps.shape[0], d_kps.shape[1]
+    ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
+    s = None if stream is None else C.c_void_p(getattr(stream, "cuda_stream", stream))
+    L.check(L.lib().orbx_update_last_frame_device(
+        B, ptr(d_kps), ptr(d_n), cap, ptr(d_depth), ptr(d_Tcw), fx, fy, cx, cy, float(th_depth), ptr(d_obs_in),
+        ptr(d_pos_in), ptr(out["mp_obs"]), ptr(out["mp_pos"]), ptr(out["has_mp"]), s))
+
+
+def last_frame_table(B: int, cap: int, device) -> dict:
+    """Device tensors for update_last_frame_device's outputs."""
+    import torch
+    return {"mp_obs": torch.empty((B, cap), dtype=torch.int32, device=device),
+            "mp_pos": torch.empty((B, cap, 3), dtype=torch.float32, device=device),
+            "has_mp": torch.empty((B, cap), dtype=torch.uint8, device=device)}
 
 
 def mappoint_table(B: int, cap: int, device) -> dict:

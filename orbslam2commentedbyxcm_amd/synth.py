@@ -166,6 +166,137 @@ def plane_views(seed: int, rel_poses, width: int = 640, height: int = 480, fx: f
     return views, depths
 
 
+def _plane_hits(T, width, height, fx, fy, cx, cy, z0, pixels=None):
+    """Canvas coordinates (px, py) and ray depth s where camera T's pixel rays meet the
+    plane Z = z0 of the reference camera (every pixel, or the (u, v) rows of `pixels`)."""
+    Kinv = np.array([[1 / fx, 0, -cx / fx], [0, 1 / fy, -cy / fy], [0, 0, 1]], np.float64)
+    if pixels is None:
+        vv, uu = np.mgrid[0:height, 0:width].astype(np.float64)
+        rays = np.stack([uu, vv, np.ones_like(uu)], -1) @ Kinv.T
+    else:
+        p = np.asarray(pixels, np.float64)
+        rays = np.stack([p[:, 0], p[:, 1], np.ones(len(p))], -1) @ Kinv.T
+    T = np.asarray(T, np.float64)
+    R, t = T[:3, :3], T[:3, 3]
+    C = -R.T @ t
+    a = rays @ R
+    if (a[..., 2] <= 0).any():
+        raise ValueError("a view looks away from the plane")
+    s = (z0 - C[2]) / a[..., 2]
+    if (s <= 0).any():
+        raise ValueError("the plane is behind a camera")
+    X = C + s[..., None] * a
+    return fx * X[..., 0] / z0 + cx, fy * X[..., 1] / z0 + cy, s
+
+
+_PLANE_CANVAS = None  # (canvas, mx, my): shared with forked render workers
+
+
+def _render_plane_view(args):
+    T, width, height, fx, fy, cx, cy, z0 = args
+    canvas, mx, my = _PLANE_CANVAS
+    H, W = canvas.shape
+    px, py, _ = _plane_hits(T, width, height, fx, fy, cx, cy, z0)
+    px = px + mx
+    py = py + my
+    x0 = np.clip(np.floor(px).astype(np.int64), 0, W - 2)
+    y0 = np.clip(np.floor(py).astype(np.int64), 0, H - 2)
+    ax = np.clip(px - x0, 0.0, 1.0)
+    ay = np.clip(py - y0, 0.0, 1.0)
+    v = ((1 - ax) * (1 - ay) * canvas[y0, x0] + ax * (1 - ay) * canvas[y0, x0 + 1]
+         + (1 - ax) * ay * canvas[y0 + 1, x0] + ax * ay * canvas[y0 + 1, x0 + 1])
+    return np.clip(np.rint(v), 0, 255).astype(np.uint8)
+
+
+def tiled_canvas(seed: int, width: int, height: int, workers: int = 1, tile=(640, 480)) -> np.ndarray:
+    """A large texture made of frame() tiles (seeds seed*1000 + k): the shapes keep a
+    640x480 frame's scale, and the cost grows with the area only."""
+    tw, th = tile
+    nx, ny = (width + tw - 1) // tw, (height + th - 1) // th
+    tiles = frames(nx * ny, tw, th, first_seed=int(seed) * 1000, workers=workers)
+    out = tiles.reshape(ny, nx, th, tw).transpose(0, 2, 1, 3).reshape(ny * th, nx * tw)
+    return np.ascontiguousarray(out[:height, :width])
+
+
+def plane_stereo_views(seed: int, rel_poses, baseline: float, width: int, height: int, fx: float, fy: float,
+                       cx: float, cy: float, z0: float, workers: int = 1):
+    """Rectified stereo pairs of one textured plane (the plane_views scene) under the left
+    cameras' poses rel_poses[k] (relative to the reference camera, 4x4): the right camera
+    has the left one's orientation and sits `baseline` along its x axis, so a point at depth
+    z appears fx*baseline/z px further left in it (Frame::ComputeStereoMatches' model).  The
+    canvas is sized from the views' corner rays (the pixel-to-canvas map is a homography,
+    so its extremes over the image are at the corners).  workers > 1 renders in a forked
+    process pool (before the process touches the GPU).
+    Returns (left (n, h, w) u8, right (n, h, w) u8)."""
+    global _PLANE_CANVAS
+    rights = []
+    for T in rel_poses:
+        T = np.asarray(T, np.float64)
+        Tr = T.copy()
+        Tr[0, 3] -= baseline  # C_r = C_l + R^T (b, 0, 0)  =>  t_r = t_l - (b, 0, 0)
+        rights.append(Tr)
+    poses = [np.asarray(T, np.float64) for T in rel_poses] + rights
+    corners = [(0, 0), (width - 1, 0), (0, height - 1), (width - 1, height - 1)]
+    hx, hy = [], []
+    for T in poses:
+        px, py, _ = _plane_hits(T, width, height, fx, fy, cx, cy, z0, corners)
+        hx += [px.min(), px.max()]
+        hy += [py.min(), py.max()]
+    mx = 3 - int(np.floor(min(hx)))  # canvas origin: the views' canvas coordinates + (mx, my)
+    my = 3 - int(np.floor(min(hy)))
+    W = int(np.ceil(max(hx))) + mx + 4
+    H = int(np.ceil(max(hy))) + my + 4
+    canvas = tiled_canvas(seed, W, H, workers).astype(np.float64)
+    _PLANE_CANVAS = (canvas, mx, my)
+    args = [(T, width, height, fx, fy, cx, cy, z0) for T in poses]
+    try:
+        if workers > 1 and len(args) > 1:
+            import multiprocessing as mp
+            pool = mp.get_context("fork").Pool(min(workers, len(args)))
+            try:
+                views = list(pool.imap(_render_plane_view, args, chunksize=2))
+            finally:
+                pool.close()
+                pool.join()
+        else:
+            views = [_render_plane_view(a) for a in args]
+    finally:
+        _PLANE_CANVAS = None
+    n = len(rel_poses)
+    return np.stack(views[:n]), np.stack(views[n:])
+
+
+def kitti_walk(seed: int, n: int, yaw0: float = 25.0):
+    """Relative poses (4x4, camera from reference) of a KITTI-like stereo walk past the
+    textured plane Z = 15 m: the cameras look at the plane yawed by yaw0 +- 4 degrees, so
+    depths across a 1241x376 view span about 12 m to 28 m (both sides of KITTI's mThDepth
+    = bf * 35 / fx = 18.8 m); each step moves the camera along its own optical axis by
+    0.6-0.95 m forward, 0.6-0.95 m back (|dz| > mb = 0.54 m: ORBmatcher.cc:1650-1651's
+    bForward / bBackward) or less than 0.3 m (a third each; the centre kept 12-18 m from the
+    plane and within 4 m of the reference camera sideways),
+    sideways by up to 0.15 m, and rolls it by 1-4 degrees either way (bounded by 10)."""
+    g = _rng(seed + 313)
+    yaw, roll, pitch = 0.0, 0.0, 0.0
+    c = np.zeros(3)
+    rels = []
+    for k in range(n):
+        if k:
+            kind = g.integers(0, 3)
+            dz = g.uniform(0.6, 0.95) if kind == 0 else (-g.uniform(0.6, 0.95) if kind == 1 else g.uniform(-0.3, 0.3))
+            step = g.uniform(1.0, 4.0) * (1 if g.random() < 0.5 else -1)
+            roll = roll + step if abs(roll + step) <= 10.0 else roll - step
+            yaw = float(np.clip(yaw + g.uniform(-1.0, 1.0), -4.0, 4.0))
+            pitch = float(np.clip(pitch + g.uniform(-0.4, 0.4), -1.5, 1.5))
+            R = rotation("y", yaw0 + yaw) @ rotation("z", roll) @ rotation("x", pitch)
+            d = R.T @ np.array([g.uniform(-0.15, 0.15), g.uniform(-0.05, 0.05), dz])
+            if not (-3.0 <= c[2] + d[2] <= 3.0 and -4.0 <= c[0] + d[0] <= 4.0):
+                d = -d
+            c = c + d
+        R = rotation("y", yaw0 + yaw) @ rotation("z", roll) @ rotation("x", pitch)
+        rels.append(camera_pose(R, c.copy()))
+    return rels
+
+
 def rotation(axis: str, degrees: float) -> np.ndarray:
     """3x3 rotation about the camera's x, y or z (optical) axis."""
     a = np.deg2rad(degrees)

@@ -300,7 +300,7 @@ def main(argv=None):
 
     out = None
     if rank == 0:
-        parity = {"octree_status_clean": status_ok}
+        parity = {"octree_status_clean": status_ok, "basis": __import__("bench").PARITY_BASIS}
         nchk = args.parity_frames if args.parity_frames >= 0 else (B if world == 1 else 16)
         threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         from oracle import oracle as O

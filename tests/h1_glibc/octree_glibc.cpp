@@ -22,15 +22,54 @@
 // StdMatAllocator data block + an 88-byte UMatData each; the level's vToDistributeKeys,
 // the per-cell FAST vectors, allKeypoints, the output keypoints).
 // thread 1: run in a std::thread (a non-main malloc arena, as ORB-SLAM2's Tracking thread).
+// mode 2: the octree's own allocations from a monotonic bump allocator (global operator
+// new replaced; delete frees nothing), reset at every level: a node created later always
+// has a higher address, which is the order SURVEY.md App. A H1 names and the oracle ships
+// ("later-created node splits first"), so this mode must equal the oracle on every level,
+// tie-deciding or not -- the check of the transcription on the levels glibc leaves open.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <list>
+#include <new>
 #include <thread>
 #include <utility>
 #include <vector>
+
+namespace {
+constexpr size_t kArenaBytes = size_t(512) << 20;
+char* g_arena = nullptr;
+size_t g_top = 0;
+bool g_bump = false;  // operator new bumps from g_arena (mode 2, while a level is distributed)
+
+void* bump(size_t n) {
+    const size_t at = (g_top + 15) & ~size_t(15);
+    if (at + n > kArenaBytes) {
+        std::fprintf(stderr, "bump arena exhausted\n");
+        std::abort();
+    }
+    g_top = at + n;
+    return g_arena + at;
+}
+bool in_arena(void* p) { return g_arena && (char*)p >= g_arena && (char*)p < g_arena + kArenaBytes; }
+}  // namespace
+
+// Outside mode 2 these forward to malloc / free, as the default operator new does, so the
+// glibc modes see the same requests as before.
+void* operator new(size_t n) {
+    if (g_bump) return bump(n ? n : 1);
+    void* p = std::malloc(n ? n : 1);
+    if (!p) throw std::bad_alloc();
+    return p;
+}
+void operator delete(void* p) noexcept {
+    if (p && !in_arena(p)) std::free(p);
+}
+void operator delete(void* p, size_t) noexcept {
+    if (p && !in_arena(p)) std::free(p);
+}
 
 struct KP28 {  // cv::KeyPoint: pt, size, angle, response, octave, class_id (28 bytes)
     float x, y, size, angle, response;
@@ -220,6 +259,10 @@ int main(int argc, char** argv) {
             }
         }
     std::fclose(fi);
+    if (mode == 2) {
+        g_arena = (char*)std::malloc(kArenaBytes);
+        if (!g_arena) return 4;
+    }
     std::vector<std::vector<std::vector<KP28>>> result(nframes);
     auto run = [&]() {
         std::vector<MatBuf> pyr(nlevels);
@@ -251,6 +294,19 @@ int main(int argc, char** argv) {
                     }
                 } else {
                     todist = L.cand;
+                }
+                if (mode == 2) {  // bump-allocated octree, written out before the arena is reused
+                    g_top = 0;
+                    g_bump = true;
+                    std::vector<KP28> keep = distribute(todist, L.minX, L.maxX, L.minY, L.maxY, L.N, nfeatures);
+                    g_bump = false;
+                    const int n = (int)keep.size();
+                    std::fwrite(&n, 4, 1, fo);
+                    for (const KP28& k : keep) {
+                        const float v[3] = {k.x, k.y, k.response};
+                        std::fwrite(v, 4, 3, fo);
+                    }
+                    continue;
                 }
                 std::vector<KP28>& keep = all[l];
                 keep.reserve(nfeatures);

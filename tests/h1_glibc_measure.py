@@ -15,7 +15,11 @@ allocations only) and "frame" (plus the surrounding per-frame allocations of
 ORBextractor::operator()), each in the main thread and in a second thread (a non-main
 malloc arena, like ORB-SLAM2's Tracking thread).
 
-    python tests/h1_glibc_measure.py [--frames 256] [--out profiles/r04_h1_glibc.json]
+    python tests/h1_glibc_measure.py [--frames 256] [--out profiles/r04_h1_glibc.json] [--bump-only]
+
+"bump_allocator": the same transcription with the octree's allocations from a monotonic
+bump allocator (mode 2): nodes created later have higher addresses, the order H1's shipped
+rule names, so it must equal the oracle on every level -- tie-deciding ones included.
 
 TEST INFRASTRUCTURE: the CPU oracle and a host C++ program only.
 """
@@ -147,10 +151,33 @@ def compare(glibc, rules):
             "by_level_tied_shipped_opposite": {str(k): v for k, v in sorted(per_level.items())}}
 
 
-def measure(frames, prm, threads, exe, tmp: Path) -> dict:
+def compare_bump(bump, rules):
+    """The bump-allocator run against the shipped rule on every level (tied or not)."""
+    same = lambda a, b: a.shape == b.shape and np.array_equal(a, b)  # noqa: E731
+    levels = tied = mism = mism_tied = 0
+    for f, fr in enumerate(bump):
+        for l, g in enumerate(fr):
+            a, b = rules[0][f][l], rules[1][f][l]
+            t = not same(a, b)
+            levels += 1
+            tied += t
+            if not same(g, a):
+                mism += 1
+                mism_tied += t
+    return {"levels": levels, "tie_deciding_levels": tied, "mismatched_vs_shipped": mism,
+            "tie_deciding_mismatched_vs_shipped": mism_tied}
+
+
+def measure(frames, prm, threads, exe, tmp: Path, bump_only: bool = False) -> dict:
     levels = level_inputs(frames, prm, threads)
     rules = oracle_rules(levels, threads)
     out = {"frames": len(frames), "levels": len(levels[0])}
+    fin, fout = tmp / "in_bump.bin", tmp / "out_bump.bin"
+    write_input(fin, levels, prm[0], 2, 0)
+    subprocess.run([str(exe), str(fin), str(fout)], check=True)
+    out["bump_allocator"] = compare_bump(read_output(fout, len(frames), len(levels[0])), rules)
+    if bump_only:
+        return out
     for mode, mname in ((0, "octree"), (1, "frame")):
         for thread in (0, 1):
             fin, fout = tmp / f"in_{mode}{thread}.bin", tmp / f"out_{mode}{thread}.bin"
@@ -165,6 +192,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=256)
     ap.add_argument("--out", default="")
+    ap.add_argument("--bump-only", action="store_true", help="only the monotonic bump-allocator check")
     a = ap.parse_args(argv)
     from orbslam2commentedbyxcm_amd import synth
     frames, _ = synth.sequence(1000, a.frames)  # bench.py's rank-0 batch
@@ -180,8 +208,8 @@ def main(argv=None):
                "libc": libc, "compiler": subprocess.run(["g++", "--version"], capture_output=True,
                                                          text=True).stdout.splitlines()[0],
                "workload": f"bench.py configs[1] batch (synth.sequence(1000, {a.frames})), 640x480"}
-        res["configs[1] C1 1000 x 8"] = measure(frames, (1000, 1.2, 8, 20, 7), th, exe, tmp)
-        res["configs[4] C5 5000 x 12"] = measure(frames, (5000, 1.2, 12, 20, 7), th, exe, tmp)
+        res["configs[1] C1 1000 x 8"] = measure(frames, (1000, 1.2, 8, 20, 7), th, exe, tmp, a.bump_only)
+        res["configs[4] C5 5000 x 12"] = measure(frames, (5000, 1.2, 12, 20, 7), th, exe, tmp, a.bump_only)
     print(json.dumps(res, indent=1))
     if a.out:
         Path(a.out).write_text(json.dumps(res, indent=1) + "\n")
