@@ -92,6 +92,10 @@ int orbx_extractor_max_keypoints(orbx_extractor* ex, int width, int height, int*
 int orbx_extract(orbx_extractor* ex, const uint8_t* img, int width, int height, size_t stride,
                  orbx_keypoint* kps, uint8_t* desc, int cap, int* n_out);
 
+/* Wall time (microseconds) of the newest orbx_extract / orbx_extract_batch host call on
+ * `ex`, entry to return: what a C++ caller pays per call (diagnostics; -1 for NULL). */
+double orbx_extractor_last_call_us(const orbx_extractor* ex);
+
 /* The same for B host images of one size; frame b writes kps[b*cap ...],
  * desc[b*cap*32 ...] and n_per_frame[b]. */
 int orbx_extract_batch(orbx_extractor* ex, int batch, const uint8_t* const* imgs, int width,

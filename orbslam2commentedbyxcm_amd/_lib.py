@@ -50,6 +50,7 @@ EXPORTED = [
     "orbx_extractor_set_node_capacity", "orbx_extractor_set_level0_in_place", "orbx_compute_stereo_matches_batch_device",
     "orbx_search_for_triangulation_batch_device", "orbx_match_sequence_device_ex",
     "orbx_search_local_points_device", "orbx_create_mappoints_device", "orbx_update_last_frame_device",
+    "orbx_extractor_last_call_us",
 ]
 
 
@@ -194,6 +195,8 @@ def lib() -> C.CDLL:
     L.orbx_matcher_last_ms.argtypes = [vp, fp]
     L.orbx_matcher_last_call_us.argtypes = [vp]
     L.orbx_matcher_last_call_us.restype = C.c_double
+    L.orbx_extractor_last_call_us.argtypes = [vp]
+    L.orbx_extractor_last_call_us.restype = C.c_double
     dp = C.POINTER(C.c_double)
     L.orbx_vocabulary_load_text_file.argtypes = [C.c_char_p, C.c_int, C.POINTER(vp)]
     L.orbx_vocabulary_load_text.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.POINTER(vp)]

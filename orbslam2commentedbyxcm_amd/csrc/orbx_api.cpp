@@ -6,6 +6,7 @@
 // last extraction until the next call.  No function throws across the ABI.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -81,6 +82,14 @@ struct orbx_extractor {
     orbx_keypoint* h_kps = nullptr;
     uint8_t* h_desc = nullptr;
     int* h_n = nullptr;
+    int* h_status = nullptr;
+    // the same pinned buffers as the device sees them (host-mapped, coherent): the single
+    // host calls read their frames and write their results through these, no DMA copies
+    const uint8_t* h_in_dev = nullptr;
+    orbx_keypoint* h_kps_dev = nullptr;
+    uint8_t* h_desc_dev = nullptr;
+    int* h_n_dev = nullptr;
+    int* h_status_dev = nullptr;
     orbx_keypoint* d_kps = nullptr;
     uint8_t* d_desc = nullptr;
     int* d_n = nullptr;
@@ -92,6 +101,7 @@ struct orbx_extractor {
     // orbx_extractor_set_stage_event: recorded after stage `stage_after` of every extraction
     hipEvent_t stage_ev = nullptr;
     int stage_after = 0;
+    double last_call_us = 0.0;  // wall time of the newest host-API extraction (orbx_extractor_last_call_us)
 };
 
 namespace {
@@ -158,7 +168,8 @@ int max_kps_of(const Plan& p) {
 }
 
 int run_device(orbx_extractor* ex, int batch, const uint8_t* d_imgs, size_t frame_pitch, int W, int H,
-               size_t stride, orbx_keypoint* d_kps, uint8_t* d_desc, int cap, int* d_n, hipStream_t stream) {
+               size_t stride, orbx_keypoint* d_kps, uint8_t* d_desc, int cap, int* d_n, hipStream_t stream,
+               bool allow_inplace = true, int* status_out = nullptr) {
     int rc = prepare(ex, W, H, batch);
     if (rc != ORBX_OK) return rc;
     hipEvent_t* ev = nullptr;
@@ -174,10 +185,10 @@ int run_device(orbx_extractor* ex, int batch, const uint8_t* d_imgs, size_t fram
             ev = sel;
         }
     }
-    const bool inplace = ex->l0_in_place && !ex->plan.desc_tiles && (uintptr_t)d_imgs % 16 == 0 && stride % 64 == 0 &&
-                         frame_pitch % 16 == 0;
+    const bool inplace = allow_inplace && ex->l0_in_place && !ex->plan.desc_tiles && (uintptr_t)d_imgs % 16 == 0 &&
+                         stride % 64 == 0 && frame_pitch % 16 == 0;
     hipError_t e = launch_extract(ex->plan, ex->db, batch, d_imgs, frame_pitch, stride, d_kps, d_desc, cap, d_n,
-                                  stream, ev, ex->stage_ev, ex->stage_after, inplace);
+                                  stream, ev, ex->stage_ev, ex->stage_after, inplace, status_out);
     ex->l0 = inplace ? d_imgs : nullptr;
     ex->l0_fp = frame_pitch;
     ex->l0_pitch = stride;
@@ -210,9 +221,14 @@ int run_device(orbx_extractor* ex, int batch, const uint8_t* d_imgs, size_t fram
     return ORBX_OK;
 }
 
-int check_status(orbx_extractor* ex, int batch) {
+// The octree status words of the last `batch` frames: read back from the device, or taken
+// from `known` (the host-mapped mirror a host call's describe kernel filled).
+int check_status(orbx_extractor* ex, int batch, const int* known = nullptr) {
     std::vector<int> st((size_t)batch);
-    HIP_TRY(hipMemcpy(st.data(), ex->db.status, sizeof(int) * (size_t)batch, hipMemcpyDeviceToHost));
+    if (known)
+        std::memcpy(st.data(), known, sizeof(int) * (size_t)batch);
+    else
+        HIP_TRY(hipMemcpy(st.data(), ex->db.status, sizeof(int) * (size_t)batch, hipMemcpyDeviceToHost));
     for (int b = 0; b < batch; b++)
         if (st[(size_t)b]) {
             char msg[160];
@@ -224,10 +240,15 @@ int check_status(orbx_extractor* ex, int batch) {
     return ORBX_OK;
 }
 
+// Pinned host memory, mapped into the device's address space and coherent (the GPU does
+// not cache it): the host calls' frames are read, and their results written, through the
+// device pointer (*dev), so a call needs no DMA copy and one synchronisation.
 template <typename T>
-hipError_t halloc(T** p, size_t n) {  // pinned host memory
+hipError_t halloc(T** p, size_t n, T** dev) {
     if (n == 0) n = 1;
-    return hipHostMalloc((void**)p, sizeof(T) * n, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc((void**)p, sizeof(T) * n, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) return e;
+    return hipHostGetDevicePointer((void**)dev, *p, 0);
 }
 
 void free_host_staging(orbx_extractor* ex) {
@@ -239,6 +260,13 @@ void free_host_staging(orbx_extractor* ex) {
     if (ex->h_kps) (void)hipHostFree(ex->h_kps);
     if (ex->h_desc) (void)hipHostFree(ex->h_desc);
     if (ex->h_n) (void)hipHostFree(ex->h_n);
+    if (ex->h_status) (void)hipHostFree(ex->h_status);
+    ex->h_status = nullptr;
+    ex->h_in_dev = nullptr;
+    ex->h_kps_dev = nullptr;
+    ex->h_desc_dev = nullptr;
+    ex->h_n_dev = nullptr;
+    ex->h_status_dev = nullptr;
     ex->d_in = nullptr;
     ex->d_kps = nullptr;
     ex->d_desc = nullptr;
@@ -260,7 +288,9 @@ int ensure_host_staging(orbx_extractor* ex, size_t in_bytes, size_t out_slots, i
         ex->h_in = nullptr;
         ex->d_in_bytes = 0;
         HIP_TRY(dalloc(&ex->d_in, in_bytes));
-        HIP_TRY(halloc(&ex->h_in, in_bytes));
+        uint8_t* dev = nullptr;
+        HIP_TRY(halloc(&ex->h_in, in_bytes, &dev));
+        ex->h_in_dev = dev;
         ex->d_in_bytes = in_bytes;
     }
     if (ex->d_out_cap < out_slots) {
@@ -275,18 +305,21 @@ int ensure_host_staging(orbx_extractor* ex, size_t in_bytes, size_t out_slots, i
         ex->d_out_cap = 0;
         HIP_TRY(dalloc(&ex->d_kps, out_slots));
         HIP_TRY(dalloc(&ex->d_desc, out_slots * 32));
-        HIP_TRY(halloc(&ex->h_kps, out_slots));
-        HIP_TRY(halloc(&ex->h_desc, out_slots * 32));
+        HIP_TRY(halloc(&ex->h_kps, out_slots, &ex->h_kps_dev));
+        HIP_TRY(halloc(&ex->h_desc, out_slots * 32, &ex->h_desc_dev));
         ex->d_out_cap = out_slots;
     }
     if (ex->d_n_cap < nframes) {
         if (ex->d_n) (void)hipFree(ex->d_n);
         if (ex->h_n) (void)hipHostFree(ex->h_n);
+        if (ex->h_status) (void)hipHostFree(ex->h_status);
         ex->d_n = nullptr;
         ex->h_n = nullptr;
+        ex->h_status = nullptr;
         ex->d_n_cap = 0;
         HIP_TRY(dalloc(&ex->d_n, (size_t)nframes));
-        HIP_TRY(halloc(&ex->h_n, (size_t)nframes));
+        HIP_TRY(halloc(&ex->h_n, (size_t)nframes, &ex->h_n_dev));
+        HIP_TRY(halloc(&ex->h_status, (size_t)nframes, &ex->h_status_dev));
         ex->d_n_cap = nframes;
     }
     return ORBX_OK;
@@ -541,8 +574,22 @@ int orbx_extract_batch_device(orbx_extractor* ex, int batch, const uint8_t* d_im
     return run_device(ex, batch, d_imgs, frame_pitch, width, height, stride, d_kps, d_desc, cap, d_n_per_frame, s);
 }
 
+namespace {
+// Scoped: the enclosing host call's wall time into ex->last_call_us.
+struct CallClock {
+    orbx_extractor* ex;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~CallClock() {
+        if (ex) ex->last_call_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    }
+};
+}  // namespace
+
+double orbx_extractor_last_call_us(const orbx_extractor* ex) { return ex ? ex->last_call_us : -1.0; }
+
 int orbx_extract_batch(orbx_extractor* ex, int batch, const uint8_t* const* imgs, int width, int height,
                        size_t stride, orbx_keypoint* kps, uint8_t* desc, int cap, int* n_per_frame) {
+    CallClock clock{ex};
     if (!ex || batch < 0 || cap < 0 || !imgs) return fail(ORBX_ERR_ARG, "bad argument");
     if (batch == 0) return ORBX_OK;
     if (width <= 0 || height <= 0) return ORBX_EMPTY;
@@ -559,6 +606,29 @@ int orbx_extract_batch(orbx_extractor* ex, int batch, const uint8_t* const* imgs
         } else {
             for (int y = 0; y < height; y++) std::memcpy(dst + (size_t)y * width, imgs[b] + (size_t)y * stride, width);
         }
+    }
+    // Default: the pyramid kernel reads the frames from the mapped pinned buffer and the
+    // describe kernel writes keypoints, descriptors, counts and status words straight into
+    // mapped pinned memory -- no DMA copy in either direction and one synchronisation per
+    // call.  ORBX_EXTRACT_DMA=1: the round-4 path (upload copy, results read back by copies).
+    static const bool dma = getenv("ORBX_EXTRACT_DMA") != nullptr;
+    if (!dma) {
+        rc = run_device(ex, batch, ex->h_in_dev, fbytes, width, height, (size_t)width, ex->h_kps_dev, ex->h_desc_dev,
+                        cap > 0 ? cap : 1, ex->h_n_dev, ex->stream, false, ex->h_status_dev);
+        if (rc != ORBX_OK) return rc;
+        HIP_TRY(hipStreamSynchronize(ex->stream));
+        std::memcpy(n_per_frame, ex->h_n, sizeof(int) * batch);
+        rc = check_status(ex, batch, ex->h_status);
+        if (rc != ORBX_OK) return rc;
+        int overflow = 0;
+        for (int b = 0; b < batch; b++) {
+            const int n = n_per_frame[b] < cap ? n_per_frame[b] : cap;
+            if (n_per_frame[b] > cap) overflow = 1;
+            if (n <= 0) continue;
+            if (kps) std::memcpy(kps + (size_t)b * cap, ex->h_kps + (size_t)b * cap, sizeof(orbx_keypoint) * n);
+            if (desc) std::memcpy(desc + (size_t)b * cap * 32, ex->h_desc + (size_t)b * cap * 32, (size_t)n * 32);
+        }
+        return overflow ? fail(ORBX_ERR_CAPACITY, "more keypoints than cap") : ORBX_OK;
     }
     HIP_TRY(hipMemcpyAsync(ex->d_in, ex->h_in, fbytes * batch, hipMemcpyHostToDevice, ex->stream));
     rc = run_device(ex, batch, ex->d_in, fbytes, width, height, (size_t)width, ex->d_kps, ex->d_desc,

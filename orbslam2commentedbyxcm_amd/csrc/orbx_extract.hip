@@ -178,9 +178,12 @@ __global__ __launch_bounds__(256) ORBX_PZ_ATTR void k_pyramid(const uint8_t* __r
                             const uint8_t* p = in + (size_t)y * stride + x;
                             if (vec4 && full) {
                                 v[k] = *(const uint32_t*)p;
-                            } else if (x + 8 <= g.w) {
+                            } else if (x >= 4 && x + 8 <= g.w) {
                                 // an unaligned row (e.g. 1241-byte KITTI rows): the two aligned
-                                // dwords around the quad, funnel-shifted (both inside the row)
+                                // dwords around the quad, funnel-shifted; both lie inside the
+                                // row (from x - 3 >= 1 to x + 7 < w), so the row's first quad
+                                // takes the byte loop below and nothing before the caller's
+                                // first row is read
                                 // (pointer arithmetic, not an integer round trip: the loads
                                 // stay global, not flat)
                                 const int sh = (int)((uintptr_t)p & 3);
@@ -1610,7 +1613,8 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
                                                    const int* __restrict__ kept_count,
                                                    orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                    int cap, int* __restrict__ n_out, int nframes,
-                                                   const uint8_t* __restrict__ l0, long long l0_fp, int l0_pitch) {
+                                                   const uint8_t* __restrict__ l0, long long l0_fp, int l0_pitch,
+                                                   const int* __restrict__ status, int* __restrict__ status_out) {
     // BRIEF patches: 37 rows of 48 bytes (16-byte chunks), or of 40 bytes -- the 37
     // columns x-18..x+18 from (x-18) & ~3 -- for the 4-byte DMA (six workgroups a CU)
     constexpr int kPP = STAGE == 2 ? 40 : 48;
@@ -1627,7 +1631,10 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     if (slot0 >= kept_pf) return;  // whole wave; no barriers below
     int l, base, total;
     desc_level_of(s_lv, L, slot, l, base, total);
-    if (slot0 == 0 && lane == 0) n_out[f] = total;
+    if (slot0 == 0 && lane == 0) {
+        n_out[f] = total;
+        if (status_out) status_out[f] = status[f];  // k_octree's word (earlier on this stream)
+    }
 #if ORBX_ABL_DESC == 2  // timing ablation only: no describe work at all
     return;
 #endif
@@ -1854,7 +1861,8 @@ __global__ __launch_bounds__(256) void k_describe_tiles(const uint8_t* __restric
                                                          const uint16_t* __restrict__ dt_list,
                                                          const uint32_t* __restrict__ dt_tile, int tiles_pf,
                                                          orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
-                                                         int cap, int* __restrict__ n_out, int nframes) {
+                                                         int cap, int* __restrict__ n_out, int nframes,
+                                                         const int* __restrict__ status, int* __restrict__ status_out) {
     __shared__ __align__(16) uint8_t s_raw[kDtRows][kDtP];
     __shared__ __align__(16) uint8_t s_blr[kDtRows][kDtP];
     int f, tile;
@@ -1865,6 +1873,7 @@ __global__ __launch_bounds__(256) void k_describe_tiles(const uint8_t* __restric
         int tot = 0;
         for (int l2 = 0; l2 < L; l2++) tot += kc[l2];
         n_out[f] = tot;
+        if (status_out) status_out[f] = status[f];
     }
     const uint32_t td = dt_tile[(size_t)f * tiles_pf + tile];
     const int cnt = (int)(td & 0xffffu), start = (int)(td >> 16);
@@ -2021,7 +2030,7 @@ __global__ __launch_bounds__(256) void k_describe_tiles(const uint8_t* __restric
 hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, const uint8_t* d_imgs,
                           size_t frame_pitch, size_t stride, void* kps, uint8_t* desc, int cap,
                           int* n_per_frame, hipStream_t stream, hipEvent_t* ev, hipEvent_t stage_ev,
-                          int stage_after, bool l0_in_place) {
+                          int stage_after, bool l0_in_place, int* status_out) {
     // level 0 read in place by k_level_tiles / k_describe (their 16-byte row loads need
     // 16-byte aligned frames and 64-byte aligned rows), not copied into the pyramid
     const uint8_t* l0 = l0_in_place ? d_imgs : nullptr;
@@ -2098,13 +2107,14 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
         if (plan.desc_tiles) {
             hipLaunchKernelGGL(k_describe_tiles, dim3(plan.tiles_total * batch), dim3(256), 0, stream, db.pyr,
                                db.blur, fb, db.lv, L, db.kept, plan.kept_per_frame, db.kept_count, db.dt_list,
-                               db.dt_tile, plan.tiles_total, (orbx_keypoint*)kps, desc, cap, n_per_frame, batch);
+                               db.dt_tile, plan.tiles_total, (orbx_keypoint*)kps, desc, cap, n_per_frame, batch,
+                               db.status, status_out);
         } else {
             dim3 grid(((plan.kept_per_frame + 15) / 16) * batch);
             auto kern = plan.kept_per_frame <= kDescGldsMaxSlots ? k_describe<ORBX_DESC_DMA> : k_describe<0>;
             hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, db.pyr, db.blur, fb, db.lv, L, db.kept,
                                plan.kept_per_frame, db.kept_count, (orbx_keypoint*)kps, desc, cap, n_per_frame, batch,
-                               l0, l0_fp, l0_pitch);
+                               l0, l0_fp, l0_pitch, db.status, status_out);
         }
     }
     if (ev && ev[5]) (void)hipEventRecord(ev[5], stream);

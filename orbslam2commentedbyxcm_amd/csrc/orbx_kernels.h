@@ -57,11 +57,14 @@ hipError_t upload_constants(const OrbParams& prm);
 
 // Enqueue the whole extraction of `batch` device frames on `stream`.
 // kps: orbx_keypoint[batch*cap], desc: uint8[batch*cap*32], n_per_frame: int[batch].
-// ev (nullable) holds kStages+1 events recorded between the stages.
+// ev (nullable) holds kStages+1 events recorded between the stages.  status_out (nullable,
+// e.g. host-mapped memory): the describe kernel copies each frame's octree status word there
+// beside its count, so a host call learns both without a separate read-back.
 hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, const uint8_t* d_imgs,
                           size_t frame_pitch, size_t stride, void* kps, uint8_t* desc, int cap,
                           int* n_per_frame, hipStream_t stream, hipEvent_t* ev,
-                          hipEvent_t stage_ev = nullptr, int stage_after = 0, bool l0_in_place = false);
+                          hipEvent_t stage_ev = nullptr, int stage_after = 0, bool l0_in_place = false,
+                          int* status_out = nullptr);
 
 // dist[i*nb+j] = Hamming(a_i, b_j)
 hipError_t launch_hamming_matrix(const uint8_t* a, int na, const uint8_t* b, int nb, int32_t* dist,

@@ -588,10 +588,10 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
 #if ORBX_SCORE_COUNT
     if (P.stamps && valid) {
         unsigned long long* sc = P.stamps + kStampWords * (size_t)blockIdx.x;
-        atomicAdd(sc + 16, n_pair);
-        atomicAdd(sc + 17, n_step);
-        atomicAdd(sc + 18, n_ok);
-        if (r == 0) atomicAdd(sc + 19, 1ull);
+        atomicAdd(sc + kStampScore, n_pair);
+        atomicAdd(sc + kStampScore + 1, n_step);
+        atomicAdd(sc + kStampScore + 2, n_ok);
+        if (r == 0) atomicAdd(sc + kStampScore + 3, 1ull);
     }
 #endif
     // Group top-kTopK: keys are unique (distinct positions), so one lane pops each minimum.
@@ -1044,6 +1044,7 @@ __device__ void proj_replay(const ProjProblem& pb, const ProjParams& P, const So
         st[8] = t_res;
         st[9] = t_first;
         st[14] = t_load;
+        st[kStampForm] = 64;
     }
 }
 
@@ -1359,6 +1360,7 @@ __device__ void proj_replay_block(const ProjProblem& pb, const ProjParams& P, co
         st[12] = nstop;
         st[14] = t_load;
         st[15] = t_commit;
+        st[kStampForm] = RT;
     }
     __syncthreads();
 }

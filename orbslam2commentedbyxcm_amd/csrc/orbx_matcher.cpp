@@ -364,17 +364,19 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
         HIP_TRY(m->arena.flush(s));
         HIP_TRY(launch_proj_search(d_prob, 1, P, d_scr, d_off, n, nq, s));
     }
+    // the caller's frame_mp is written only once the count says the replay converged: a
+    // failed call (ORBX_ERR_STATE below) leaves it as it was
     int nm = 0;
+    std::vector<int32_t> staged_mp;
     if (!mapped) {
-        HIP_TRY(m->arena.down(frame_mp, d_fmp, sizeof(int32_t) * n, s));
+        staged_mp.resize((size_t)n);
+        HIP_TRY(m->arena.down(staged_mp.data(), d_fmp, sizeof(int32_t) * n, s));
         HIP_TRY(m->arena.down(&nm, d_nm, sizeof(int32_t), s));
     }
     const auto t_enq = std::chrono::steady_clock::now();
     HIP_TRY(m->arena.sync(s));
-    if (mapped) {
-        std::memcpy(frame_mp, m->hmp + 1, sizeof(int32_t) * n);
-        nm = m->hmp[0];
-    }
+    if (mapped) nm = m->hmp[0];
+    if (nm >= 0) std::memcpy(frame_mp, mapped ? m->hmp + 1 : staged_mp.data(), sizeof(int32_t) * n);
     if (call_stamps) {
         const auto t_done = std::chrono::steady_clock::now();
         unsigned long long h[kStampWords];
@@ -382,12 +384,19 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
         HIP_TRY(hipFree(d_st));
         auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
         fprintf(stderr, "[orbx call] n=%d nq=%d | host staging %.1f us, enqueue %.1f us, wait %.1f us | grid: start %.1f, "
-                "sort %.1f, writes %.1f, colstart %.1f, runs %.1f us | replay %.1f us, %llu iterations, %llu re-scored "
-                "(%.1f us), chunk loads %.1f + first rounds %.1f us, after the loop %.1f us\n",
+                "sort %.1f, writes %.1f, colstart %.1f, runs %.1f us | replay (%llu threads) %.1f us, %llu iterations, "
+                "%llu re-scored (%.1f us), ",
                 n, nq, us(t_stage0, t_flush), us(t_flush, t_enq), us(t_enq, t_done), (double)(h[1] - h[0]) * 0.01,
                 (double)(h[2] - h[1]) * 0.01, (double)(h[4] - h[2]) * 0.01, (double)(h[10] - h[4]) * 0.01,
-                (double)(h[11] - h[10]) * 0.01, (double)(h[3] - h[13]) * 0.01, h[7], h[5], (double)h[8] * 0.01,
-                (double)h[14] * 0.01, (double)(h[9] - h[14]) * 0.01, h[15] ? (double)(h[3] - h[15]) * 0.01 : 0.0);
+                (double)(h[11] - h[10]) * 0.01, h[kStampForm], (double)(h[3] - h[13]) * 0.01, h[7], h[5],
+                (double)h[8] * 0.01);
+        if (h[kStampForm] == 64)  // one wave: 9 = loads + first rounds (cumulative), 15 = a clock reading
+            fprintf(stderr, "chunk loads %.1f + first rounds %.1f us, after the loop %.1f us\n", (double)h[14] * 0.01,
+                    h[9] >= h[14] ? (double)(h[9] - h[14]) * 0.01 : 0.0,
+                    h[15] && h[3] >= h[15] ? (double)(h[3] - h[15]) * 0.01 : 0.0);
+        else  // block replay: 9 / 14 / 15 are durations
+            fprintf(stderr, "chunk loads %.1f, rounds %.1f, commits %.1f us\n", (double)h[14] * 0.01,
+                    (double)h[9] * 0.01, (double)h[15] * 0.01);
     }
     if (nm < 0)  // the replay's iteration guard fired: frame_mp is partial, never report it as matches
         return fail(ORBX_ERR_STATE, "SearchByProjection replay did not converge (iteration guard)");
@@ -815,8 +824,12 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
                 }
                 const double d = (double)(r[3] - r[13]) * 0.01;
                 tl += (double)r[14] * 0.01;
-                tr += (double)r[9] * 0.01;
-                tcm += (double)r[15] * 0.01;
+                if (r[kStampForm] == 64) {  // one-wave replay: 9 = loads + first rounds; no commit duration
+                    tr += (double)(r[9] >= r[14] ? r[9] - r[14] : 0) * 0.01;
+                } else {  // block replay: rounds and commits as durations
+                    tr += (double)r[9] * 0.01;
+                    tcm += (double)r[15] * 0.01;
+                }
                 trs += (double)r[8] * 0.01;
                 nst += (double)r[12];
                 cm += d;
@@ -831,10 +844,10 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
                 double a = 0, b = 0, c = 0, n = 0;
                 for (int p = 0; p < npairs; p++) {
                     const unsigned long long* r = &h[(size_t)kStampWords * p];
-                    a += (double)r[16];
-                    b += (double)r[17];
-                    c += (double)r[18];
-                    n += (double)r[19];
+                    a += (double)r[kStampScore];
+                    b += (double)r[kStampScore + 1];
+                    c += (double)r[kStampScore + 2];
+                    n += (double)r[kStampScore + 3];
                 }
                 fprintf(stderr, "[orbx score counts] per scored query: %.1f (column, octave) visits, %.1f entry steps, "
                         "%.1f candidates in the window (summed over the query's lanes; %.0f queries)\n",

@@ -127,6 +127,10 @@ class ORBextractor:
     def stream_handle(self) -> int:
         return L.lib().orbx_extractor_stream(self._h) or 0
 
+    def last_call_us(self) -> float:
+        """orbx_extractor_last_call_us: in-library wall time of the newest host-API call."""
+        return L.lib().orbx_extractor_last_call_us(self._h)
+
     def set_stage_event(self, stage: int) -> int:
         """orbx_extractor_set_stage_event: every extraction records the returned hipEvent_t
         right after stage `stage` (1 pyramid, 2 blur + FAST strength, 3 FAST cells,

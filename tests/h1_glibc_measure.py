@@ -202,9 +202,15 @@ def main(argv=None):
     with tempfile.TemporaryDirectory() as d:
         tmp = Path(d)
         exe = build(tmp)
-        res = {"what": "DistributeOctTree final-phase tie order under glibc malloc (tests/h1_glibc/octree_glibc.cpp, "
-                       "one process per 256-frame sequence) vs the shipped rule (later-created node first) and the "
-                       "opposite (earlier-created first), per level of the bench frames",
+        what = ("DistributeOctTree final-phase tie order under glibc malloc (tests/h1_glibc/octree_glibc.cpp, "
+                "one process per 256-frame sequence) vs the shipped rule (later-created node first) and the "
+                "opposite (earlier-created first), per level of the bench frames")
+        if a.bump_only:
+            what = ("the same transcription (tests/h1_glibc/octree_glibc.cpp mode 2) with the octree's allocations "
+                    "from a monotonic bump allocator (global operator new replaced, reset per level), against the "
+                    "shipped rule on every level of the bench frames: 0 mismatches means the transcription is right "
+                    "on the tie-deciding levels too and the shipped rule is the bump-allocator order H1 names")
+        res = {"what": what,
                "libc": libc, "compiler": subprocess.run(["g++", "--version"], capture_output=True,
                                                          text=True).stdout.splitlines()[0],
                "workload": f"bench.py configs[1] batch (synth.sequence(1000, {a.frames})), 640x480"}

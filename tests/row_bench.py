@@ -46,7 +46,7 @@ def _eq(a, b) -> bool:
     return a == b
 
 
-def rows(O, reps: int):
+def rows(O, reps: int, only=None):
     import match_scenes as S
     from orbslam2commentedbyxcm_amd import ORBextractor, synth
     from orbslam2commentedbyxcm_amd import frame as FR
@@ -56,9 +56,11 @@ def rows(O, reps: int):
     out = []
 
     def add(row, ref, size, gpu_fn, cpu_fn, lib=None):
-        """lib: the ORBmatcher the GPU call runs on -- its in-library wall time per call
-        (orbx_matcher_last_call_us: what a C++ caller pays, without the ctypes binding) is
-        reported beside the Python-side time."""
+        """lib: the ORBmatcher / ORBextractor the GPU call runs on -- its in-library wall time
+        per call (orbx_matcher_last_call_us / orbx_extractor_last_call_us: what a C++ caller
+        pays, without the ctypes binding) is reported beside the Python-side time."""
+        if only and row not in only:
+            return
         gpu_fn()  # warm-up (device init, first allocation)
         lib_us = []
 
@@ -91,7 +93,7 @@ def rows(O, reps: int):
             k, d, _ = O.extract(img, p)
             return k.view(np.uint8).copy(), d.copy()
         add("a2", "ORBextractor::operator() ORBextractor.cc:1513-1629 (a1-a8)",
-            f"{tag}: {W}x{H}, {nf} features, {L} levels, one frame", ex_g, ex_c)
+            f"{tag}: {W}x{H}, {nf} features, {L} levels, one frame", ex_g, ex_c, lib=ex)
 
     A, B = S.two_views(O, 0)
     As, Bs = S.two_views(O, 2, stereo=True)
@@ -264,11 +266,12 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=None, help="alias of --reps (profiling scripts)")
     ap.add_argument("--warmup", type=int, default=None, help="ignored")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="ignored (the CPU leg is the comparison)")
+    ap.add_argument("--only", default="", help="comma-separated row ids (e.g. a2,a12); default every row")
     args = ap.parse_args(argv)
     reps = args.steps if args.steps else args.reps
     from oracle import oracle as O
     O.build()
-    res = rows(O, reps)
+    res = rows(O, reps, set(args.only.split(",")) if args.only else None)
     print(json.dumps({"metric": "per-row drop-in call latency (host API, GPU) vs CPU oracle", "unit": "ms",
                       "reps": reps, "rows": res,
                       "all_bit_exact": all(r["bit_exact"] for r in res)}), flush=True)
