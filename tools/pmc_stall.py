@@ -5,9 +5,9 @@ array's busy / bank-conflict cycles and the effective clock, and names the resou
 bounds each kernel.
 usage: python tools/pmc_stall.py TAG [KERNEL_TRACE_STATS_CSV]  ->  profiles/TAG_pmc_stall.json
 
-Occupancy needs each kernel's mean duration: taken from the kernel-trace stats CSV given
-(e.g. profiles/<tag>_tum_kernel_stats_timed.csv), else from GRBM_GUI_ACTIVE / 8 at the
-2.4 GHz clock.
+Occupancy and the issue / LDS fractions need each launch's cycles: GRBM_GUI_ACTIVE / 8
+from the same serialised counter run (the kernel alone), else the kernel-trace stats CSV
+given (e.g. profiles/<tag>_tum_kernel_stats_timed.csv) at 2.4 GHz.
 """
 import csv
 import json
@@ -69,25 +69,27 @@ def main():
         v["frac_wait"] = round(v.get("sq_wait_any", 0) / wc, 3)
         if "sq_lds_idx_active" in v:
             v["lds_conflict_frac"] = round(v.get("sq_lds_bank_conflict", 0) / max(v["sq_lds_idx_active"], 1), 3)
-        ns = durs.get(k)
-        if ns is None and v.get("grbm_gui_active"):
-            ns = v["grbm_gui_active"] / 8 / CLOCK_GHZ
-        if ns:
-            cyc = ns * CLOCK_GHZ  # shader cycles of the launch
-            v["duration_ns"] = round(ns)
+        # the launch's shader cycles: GRBM_GUI_ACTIVE (summed over the 8 XCDs) / 8 -- taken in
+        # the same serialised counter run, so it is the kernel alone at whatever clock it ran;
+        # else a kernel trace's mean duration at 2.4 GHz
+        cyc = v["grbm_gui_active"] / 8 if v.get("grbm_gui_active") else None
+        if cyc is None and durs.get(k):
+            cyc = durs[k] * CLOCK_GHZ
+        if cyc:
+            v["launch_cycles"] = round(cyc)
+            if durs.get(k):
+                v["trace_duration_ns"] = round(durs[k])
             v["mean_waves_per_simd"] = round(4 * wc / cyc / SIMDS, 2)   # wave-cycles are quad-cycles
             if "sq_insts_valu" in v:
                 v["valu_issue_frac"] = round(v["sq_insts_valu"] / (cyc * SIMDS / 2), 3)  # one wave64 VALU / 2 cyc / SIMD
             if "sq_lds_idx_active" in v:
-                v["lds_busy_frac"] = round(4 * v["sq_lds_idx_active"] / (cyc * CUS), 3)
-            if v.get("grbm_gui_active"):
-                v["clock_ghz"] = round(v["grbm_gui_active"] / 8 / ns, 3)
+                v["lds_busy_frac"] = round(v["sq_lds_idx_active"] / (cyc * CUS), 3)  # LDS-array cycles per CU-cycle
         v["bound"] = classify(v)
         res[k] = v
     out = ROOT / "profiles" / f"{tag}_pmc_stall.json"
     out.write_text(json.dumps({"units": "SQ cycle counters in quad-cycles, per launch, summed over waves",
                                "source_hash": bench_source_hash(base / f"{tag}_stallA.log"),
-                               "durations_from": sys.argv[2] if len(sys.argv) > 2 else "GRBM_GUI_ACTIVE",
+                               "cycles_from": "GRBM_GUI_ACTIVE / 8 (same counter run, dispatches serialised)",
                                "kernels": res}, indent=1))
     for k, v in res.items():
         print(f"{k:34s} waves/SIMD {v.get('mean_waves_per_simd', '-')} active {v['frac_active']:.2f} "
