@@ -93,6 +93,10 @@ __device__ __forceinline__ void xcd_frame_block(int per_frame, int nframes, int&
 
 typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
 
+#ifndef ORBX_PZ_QWORD
+#define ORBX_PZ_QWORD 0  // 1: k_pyramid<true> reads a source row window as two qword LDS reads (r05b: slower)
+#endif
+
 // 24 x 24 -> high 32 bits of the 48-bit product (v_mul_hi_u32_u24)
 __device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
     return (uint32_t)(((unsigned long long)(a & 0xffffff) * (b & 0xffffff)) >> 32);
@@ -314,10 +318,28 @@ __global__ __launch_bounds__(256) ORBX_PZ_ATTR void k_pyramid(const uint8_t* __r
                             srow += sstride;
                         }
                         if constexpr (WIN) {
+#if ORBX_PZ_QWORD
+                            // two 8-byte aligned qword reads: a wave's 32-lane group then
+                            // spans ~19 qwords over LDS's 64 dword banks (conflict-free),
+                            // where three dword reads spread ~38 dwords over 32 banks
+                            // (pointer arithmetic only: an integer round trip would turn the
+                            // reads into flat loads)
+                            const uint8_t* pw = srow + wbase + wsh;
+                            const int mis = (int)((uintptr_t)pw & 7);
+                            const uint2* qp = (const uint2*)(pw - mis);
+                            const uint2 qa = qp[0];
+                            asm volatile("" ::: "memory");  // two ds_read_b64, not one ds_read2_b64 (8 cycles)
+                            const uint2 qb = qp[1];
+                            const bool hi4 = (mis & 4) != 0;
+                            const uint32_t e0 = hi4 ? qa.y : qa.x, e1 = hi4 ? qb.x : qa.y, e2 = hi4 ? qb.y : qb.x;
+                            const uint32_t lo = __builtin_amdgcn_alignbyte(e1, e0, (uint32_t)mis & 3);
+                            const uint32_t hi = __builtin_amdgcn_alignbyte(e2, e1, (uint32_t)mis & 3);
+#else
                             const uint32_t* wp = (const uint32_t*)(srow + wbase);
                             const uint32_t d0 = wp[0], d1 = wp[1], d2 = wp[2];
                             const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, wsh);
                             const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, wsh);
+#endif
 #pragma unroll
                             for (int k = 0; k < 4; k++) {
                                 hp[k] = hc[k];

@@ -2433,7 +2433,8 @@ hipError_t launch_triangulation_batch(const TriBatch& tb, unsigned long long* sc
 // ------------------------------------------------------------------ stereo
 
 // Frame::ComputeStereoMatches (Frame.cc:673-885) for B left/right pairs, three launches:
-//   k_stereo_rows     vRowIndices (cc:693-708) of each pair as a CSR over image rows;
+//   k_stereo_index    vRowIndices (cc:693-708) of each pair, restated as a CSR over
+//                     (octave, row) plus each row's list size;
 //   k_stereo          a 16-lane row per left keypoint: row-band Hamming search, 11x11 SAD over
 //                     shifts -5..5 on the pyramid level, parabola fit (cc:720-866);
 //   k_stereo_outlier  this fork's outlier pass, which sits inside the iL loop
@@ -2472,44 +2473,58 @@ __device__ int block_exscan_inplace(int* a, int n, int* tmp) {
     return total;
 }
 
-constexpr int kStereoRowThreads = 1024;
+// vRowIndices (cc:693-708) restated for a search that keeps the smallest (distance, iR):
+// the reference pushes right keypoint iR into the list of every row floor(y - r) ..
+// ceil(y + r), r = 2 scale[octave], and a left keypoint at row (int)vL scans that row's
+// list, skipping octaves outside levelL +- 1.  Here each right keypoint is listed once,
+// under (octave, floor(y)); the search visits, per admissible octave, the few rows whose
+// keypoints can cover its row and tests the band exactly -- the same candidate set, without
+// the ~7x duplication of the row lists (round 4's k_stereo_rows: one 1024-thread workgroup
+// per pair pushing every band row, 0.79 ms per 128 KITTI pairs beside the extraction).
+// The reference also needs each row's list size (empty: the left keypoint is skipped,
+// cc:728): a difference array over the bands gives it.
+constexpr int kStereoIdxThreads = 256;
 
-__global__ __launch_bounds__(kStereoRowThreads) void k_stereo_rows(StereoBatch sb) {
-    extern __shared__ __align__(16) int s_rows[];  // cnt [rows + 1], then cursors [rows]
-    __shared__ int s_tmp[kStereoRowThreads];
+__global__ __launch_bounds__(kStereoIdxThreads) void k_stereo_index(StereoBatch sb) {
+    extern __shared__ __align__(16) int s_idx[];  // cnt [L * rows + 1], then cov [rows + 1]
+    __shared__ int s_tmp[kStereoIdxThreads];
     const int b = blockIdx.x, tid = threadIdx.x;
-    const int rows = sb.rows;
-    int* cnt = s_rows;
-    int* cur = s_rows + rows + 1;
+    const int rows = sb.rows, L = sb.nlevels, nb = L * rows;
+    int* cnt = s_idx;
+    int* cov = s_idx + nb + 1;
     const int nr = min(sb.n_r[b], sb.cap);
     const orbx_keypoint* kr = sb.keys_r + (size_t)b * sb.cap;
-    for (int y = tid; y <= rows; y += kStereoRowThreads) cnt[y] = 0;
+    for (int i = tid; i <= nb; i += kStereoIdxThreads) cnt[i] = 0;
+    for (int i = tid; i <= rows; i += kStereoIdxThreads) cov[i] = 0;
     __syncthreads();
-    // a right keypoint covers rows floor(y - r) .. ceil(y + r), r = 2 * scale[octave]
-    // (cc:695-707; rows outside the image, which keypoints >= 16 px inside never reach,
-    // are dropped)
-    for (int iR = tid; iR < nr; iR += kStereoRowThreads) {
-        const orbx_keypoint kp = kr[iR];
+    for (int iR = tid; iR < nr; iR += kStereoIdxThreads) {
+        const orbx_keypoint kp = ldg(kr + iR);
+        const int o = min(max(kp.octave, 0), L - 1);
+        const int yb = min(max((int)kp.y, 0), rows - 1);
+        atomicAdd(&cnt[o * rows + yb], 1);
+        // the rows this keypoint's list entries would cover (rows outside the image, which
+        // keypoints >= 16 px inside never reach, are dropped)
         const float r = 2.0f * sb.scale[kp.octave];
-        const int maxr = (int)ceilf(kp.y + r), minr = (int)floorf(kp.y - r);
-        for (int yi = max(minr, 0); yi <= min(maxr, rows - 1); yi++) atomicAdd(&cnt[yi], 1);
+        const int lo = max((int)floorf(kp.y - r), 0), hi = min((int)ceilf(kp.y + r), rows - 1);
+        if (lo <= hi) {
+            atomicAdd(&cov[lo], 1);
+            atomicAdd(&cov[hi + 1], -1);
+        }
     }
     __syncthreads();
-    const int total = block_exscan_inplace<kStereoRowThreads>(cnt, rows, s_tmp);
-    for (int y = tid; y < rows; y += kStereoRowThreads) cur[y] = cnt[y];
-    if (tid == 0) cnt[rows] = total;
-    __syncthreads();
-    int32_t* off = sb.row_off + (size_t)b * (rows + 1);
-    for (int y = tid; y <= rows; y += kStereoRowThreads) off[y] = cnt[y];
+    const int total = block_exscan_inplace<kStereoIdxThreads>(cnt, nb, s_tmp);
+    block_exscan_inplace<kStereoIdxThreads>(cov, rows + 1, s_tmp);  // cov[y + 1]: rows <= y summed
+    int32_t* off = sb.row_off + (size_t)b * (nb + 1 + rows);
+    for (int i = tid; i < nb; i += kStereoIdxThreads) off[i] = cnt[i];
+    if (tid == 0) off[nb] = total;
+    for (int y = tid; y < rows; y += kStereoIdxThreads) off[nb + 1 + y] = cov[y + 1];
+    __syncthreads();  // every offset read before the cursors below move them
     int32_t* idx = sb.row_idx + (size_t)b * sb.band_cap;
-    for (int iR = tid; iR < nr; iR += kStereoRowThreads) {
-        const orbx_keypoint kp = kr[iR];
-        const float r = 2.0f * sb.scale[kp.octave];
-        const int maxr = (int)ceilf(kp.y + r), minr = (int)floorf(kp.y - r);
-        for (int yi = max(minr, 0); yi <= min(maxr, rows - 1); yi++) {
-            const int pos = atomicAdd(&cur[yi], 1);
-            if (pos < sb.band_cap) idx[pos] = iR;
-        }
+    for (int iR = tid; iR < nr; iR += kStereoIdxThreads) {
+        const orbx_keypoint kp = ldg(kr + iR);
+        const int o = min(max(kp.octave, 0), L - 1);
+        const int yb = min(max((int)kp.y, 0), rows - 1);
+        idx[atomicAdd(&cnt[o * rows + yb], 1)] = iR;
     }
 }
 
@@ -2550,11 +2565,11 @@ __global__ __launch_bounds__(256) void k_stereo(StereoBatch sb) {
     const int levelL = kpL.octave;
     const float vL = kpL.y, uL = kpL.x;
     const int row = (int)vL;
-    const int32_t* roff = sb.row_off + (size_t)b * (sb.rows + 1);
-    const int cbeg = row >= 0 && row < sb.rows ? roff[row] : 0;
-    const int cend = row >= 0 && row < sb.rows ? min(roff[row + 1], sb.band_cap) : 0;
+    const int nb = sb.nlevels * sb.rows;
+    const int32_t* roff = sb.row_off + (size_t)b * (nb + 1 + sb.rows);
+    const bool listed = row >= 0 && row < sb.rows && roff[nb + 1 + row] > 0;  // !vRowIndices[vL].empty()
     const float minD = 0.f;
-    const bool scan = valid && cend != cbeg && uL - minD >= 0;  // cc:727-735
+    const bool scan = valid && listed && uL - minD >= 0;  // cc:727-735
     const float minU = uL - sb.max_d, maxU = uL - minD;
     const int32_t* ridx = sb.row_idx + (size_t)b * sb.band_cap;
     const orbx_keypoint* kr = sb.keys_r + (size_t)b * sb.cap;
@@ -2563,15 +2578,24 @@ __global__ __launch_bounds__(256) void k_stereo(StereoBatch sb) {
     if (scan) {
         const unsigned long long* dl = (const unsigned long long*)(sb.desc_l + ((size_t)b * sb.cap + iL) * 32);
         const unsigned long long q0 = dl[0], q1 = dl[1], q2 = dl[2], q3 = dl[3];
-        for (int p = cbeg + gl; p < cend; p += 16) {
-            const int iR = ridx[p];
-            const orbx_keypoint kpR = kr[iR];
-            if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
-            const float uR = kpR.x;
-            if (uR >= minU && uR <= maxU) {
-                const unsigned long long* t = (const unsigned long long*)(dr + (size_t)iR * 32);
-                const int d = __popcll(q0 ^ t[0]) + __popcll(q1 ^ t[1]) + __popcll(q2 ^ t[2]) + __popcll(q3 ^ t[3]);
-                best = umin_(best, ((unsigned)d << 23) | (unsigned)iR);
+        // octaves levelL - 1 .. levelL + 1 (cc:748-749); per octave o the keypoints whose band
+        // [floor(y - r), ceil(y + r)], r = 2 scale[o], covers `row` lie in the rows
+        // floor(y) = row - ceil(r) - 1 .. row + ceil(r) + 1, and are tested exactly
+        for (int o = max(levelL - 1, 0); o <= min(levelL + 1, sb.nlevels - 1); o++) {
+            const float r = 2.0f * sb.scale[o];
+            const int R = (int)ceilf(r) + 1;
+            const int y0 = max(row - R, 0), y1 = min(row + R, sb.rows - 1);
+            const int cbeg = roff[o * sb.rows + y0], cend = roff[o * sb.rows + y1 + 1];
+            for (int p = cbeg + gl; p < cend; p += 16) {
+                const int iR = ridx[p];
+                const orbx_keypoint kpR = kr[iR];
+                if ((int)floorf(kpR.y - r) > row || (int)ceilf(kpR.y + r) < row) continue;  // not in vRowIndices[row]
+                const float uR = kpR.x;
+                if (uR >= minU && uR <= maxU) {
+                    const unsigned long long* t = (const unsigned long long*)(dr + (size_t)iR * 32);
+                    const int d = __popcll(q0 ^ t[0]) + __popcll(q1 ^ t[1]) + __popcll(q2 ^ t[2]) + __popcll(q3 ^ t[3]);
+                    best = umin_(best, ((unsigned)d << 23) | (unsigned)iR);
+                }
             }
         }
     }
@@ -2849,15 +2873,15 @@ size_t stereo_outlier_lds(int cap) {
 
 hipError_t launch_stereo(const StereoBatch& sb, int batch, hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
-    if (sb.cap > kSortMaxKeys || sb.rows <= 0) return hipErrorInvalidValue;
-    const size_t rows_lds = (size_t)(2 * sb.rows + 1) * 4;
-    if (rows_lds > 150 * 1024) return hipErrorInvalidValue;
-    if (rows_lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_stereo_rows, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)rows_lds);
+    if (sb.cap > kSortMaxKeys || sb.rows <= 0 || sb.nlevels < 1 || sb.nlevels > 32) return hipErrorInvalidValue;
+    const size_t idx_lds = ((size_t)sb.nlevels * sb.rows + 1 + sb.rows + 1) * 4;
+    if (idx_lds > 150 * 1024) return hipErrorInvalidValue;
+    if (idx_lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_stereo_index, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)idx_lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_stereo_rows, dim3(batch), dim3(kStereoRowThreads), rows_lds, stream, sb);
+    hipLaunchKernelGGL(k_stereo_index, dim3(batch), dim3(kStereoIdxThreads), idx_lds, stream, sb);
     hipLaunchKernelGGL(k_stereo, dim3((sb.cap + 15) / 16, batch), dim3(256), 0, stream, sb);
     int n2 = kSortThreads;
     while (n2 < sb.cap) n2 <<= 1;

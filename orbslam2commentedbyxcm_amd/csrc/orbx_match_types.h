@@ -289,8 +289,13 @@ struct StereoBatch {
     const int32_t* n_r;
     int cap;                      // keypoint slots per frame
     int rows;                     // vRowIndices size: mvImagePyramid[0].rows
-    int band_cap;                 // row_idx slots per pair
-    int32_t* row_off;             // [B][rows + 1]  vRowIndices as CSR over image rows
+    int nlevels;                  // octaves of the keypoints (mvScaleFactors entries)
+    int band_cap;                 // row_idx slots per pair (= cap: every right keypoint once)
+    // vRowIndices, restated: the right keypoints as a CSR over (octave, floor(y)) --
+    // row_off[b][o * rows + y] .. [+1] into row_idx[b] -- then rows words: how many right
+    // keypoints' bands [floor(y - r), ceil(y + r)] cover each image row (the reference's
+    // vRowIndices[row].size(), whose emptiness decides whether a left keypoint is searched)
+    int32_t* row_off;             // [B][nlevels * rows + 1 + rows]
     int32_t* row_idx;             // [B][band_cap]
     const uint8_t* pyr_l;         // mvImagePyramid ROIs of the left / right extractor
     const uint8_t* pyr_r;

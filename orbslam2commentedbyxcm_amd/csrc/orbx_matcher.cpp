@@ -1825,7 +1825,7 @@ int orbx_compute_distinctive_descriptors(int device, int nmp, const int32_t* off
 }
 
 // Frame::ComputeStereoMatches, Frame.cc:673-885.  Both entry points fill a StereoBatch
-// and run k_stereo_rows / k_stereo / k_stereo_outlier (orbx_match.hip).
+// and run k_stereo_index / k_stereo / k_stereo_outlier (orbx_match.hip).
 namespace {
 
 // Level geometry of a stereo pair's pyramids; the two extractors must share it.
@@ -1849,16 +1849,17 @@ int stereo_levels(orbx_extractor* ex_l, orbx_extractor* ex_r, StereoBatch& sb, P
     }
     sb.fb_l = vl.frame_bytes;
     sb.fb_r = vr.frame_bytes;
-    // rows one right keypoint covers: ceil(y + r) - floor(y - r) + 1 <= 2r + 3, r = 2 scale[l]
-    int band = 0;
-    for (int l = 0; l < vl.L; l++) band = std::max(band, (int)std::ceil(4.0f * vl.scale[l]) + 3);
-    sb.band_cap = band * sb.cap;
+    sb.nlevels = vl.L;
+    sb.band_cap = sb.cap;  // the (octave, row) index holds every right keypoint once
     return ORBX_OK;
 }
 
+// words of the per-pair (octave, row) offsets + row coverage counts (StereoBatch::row_off)
+size_t stereo_off_words(const StereoBatch& sb) { return (size_t)sb.nlevels * sb.rows + 1 + sb.rows; }
+
 size_t stereo_scratch(const StereoBatch& sb, int batch) {
-    return pad(sizeof(int32_t) * (size_t)batch * (sb.rows + 1)) + pad(sizeof(int32_t) * (size_t)batch * sb.band_cap) +
-           pad(sizeof(StereoResult) * (size_t)batch * sb.cap);
+    return pad(sizeof(int32_t) * (size_t)batch * stereo_off_words(sb)) +
+           pad(sizeof(int32_t) * (size_t)batch * sb.band_cap) + pad(sizeof(StereoResult) * (size_t)batch * sb.cap);
 }
 
 }  // namespace
@@ -1908,7 +1909,7 @@ int orbx_compute_stereo_matches(orbx_matcher* m, orbx_extractor* ex_left, int le
     auto* d_nr = m->arena.take<int32_t>(1);
     auto* d_ur = m->arena.take<float>(sb.cap);
     auto* d_dp = m->arena.take<float>(sb.cap);
-    sb.row_off = m->arena.take<int32_t>((size_t)sb.rows + 1);
+    sb.row_off = m->arena.take<int32_t>(stereo_off_words(sb));
     sb.row_idx = m->arena.take<int32_t>((size_t)sb.band_cap);
     sb.res = m->arena.take<StereoResult>(sb.cap);
     // the extractors' streams produced the pyramids: order this stream after them
@@ -1971,7 +1972,7 @@ int orbx_compute_stereo_matches_batch_device(orbx_matcher* m, orbx_extractor* ex
     }
     char* p = m->dscr;
     sb.row_off = (int32_t*)p;
-    p += pad(sizeof(int32_t) * (size_t)batch * (sb.rows + 1));
+    p += pad(sizeof(int32_t) * (size_t)batch * stereo_off_words(sb));
     sb.row_idx = (int32_t*)p;
     p += pad(sizeof(int32_t) * (size_t)batch * sb.band_cap);
     sb.res = (StereoResult*)p;
