@@ -1593,7 +1593,10 @@ __device__ __forceinline__ void desc_level_of(const DescLevel* s, int L, int slo
 // beside the extraction sets the step, the extra waves cost the matcher more than they
 // save (configs[4] 100.6-100.9k -> 94.1-95.1k; capping them by LDS gives both back):
 // register staging above this many slots.
-constexpr int kDescGldsMaxSlots = 3000;
+#ifndef ORBX_DESC_GLDS_MAX
+#define ORBX_DESC_GLDS_MAX 3000
+#endif
+constexpr int kDescGldsMaxSlots = ORBX_DESC_GLDS_MAX;
 #ifndef ORBX_ABL_DESC
 #define ORBX_ABL_DESC 0  // timing ablations of k_describe (tools/ab_lib.sh); 0 in every shipped build
 #endif

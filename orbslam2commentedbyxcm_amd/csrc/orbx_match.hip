@@ -328,6 +328,9 @@ __device__ __forceinline__ int ent_dist(unsigned e) { return (int)(e >> 18); }
 __device__ __forceinline__ int ent_oct(unsigned e) { return (int)((e >> 13) & 31u); }
 __device__ __forceinline__ int ent_pos(unsigned e) { return (int)(e & 0x1fffu); }
 
+// The same over the 4 lanes of each DPP quad (quad_perm [1,0,3,2], [2,3,0,1]).
+__device__ __forceinline__ unsigned quad_min_u32(unsigned v);
+
 // Row minimum over the 16 lanes of each DPP row (quad_perm [1,0,3,2], [2,3,0,1],
 // row_half_mirror, row_mirror): every lane of the row ends with the row's minimum.
 // Must be called with the whole wave active.
@@ -346,6 +349,12 @@ __device__ __forceinline__ unsigned half_row_min_u32(unsigned v) {
     v = umin_(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));
     v = umin_(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));
     v = umin_(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false));
+    return v;
+}
+
+__device__ __forceinline__ unsigned quad_min_u32(unsigned v) {
+    v = umin_(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));
+    v = umin_(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));
     return v;
 }
 
@@ -430,6 +439,9 @@ __device__ __forceinline__ void sorted_insert(unsigned (&k)[L], unsigned key) {
 // row (out = kNoEntry).  Must be called with the whole wave active.
 // K = 64: one query per wave, all lanes over its window (the replay's re-scoring of a
 // query whose list ran out, a single query on the critical path).
+#ifndef ORBX_SCORE_KR_FIXED
+#define ORBX_SCORE_KR_FIXED 0
+#endif
 #ifndef ORBX_SCORE_PAIR
 // two bucket entries per scan step with descriptors from global memory (round 3): the
 // configs[4] matcher alone 1.114 -> 1.047 ms, the drop-in rows a11-a14 1-3 % faster,
@@ -439,7 +451,7 @@ __device__ __forceinline__ void sorted_insert(unsigned (&k)[L], unsigned key) {
 template <int K>
 __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const QueryReg& QR, bool valid,
                              const SortedGrid& G, const int* sfmp, unsigned out[kTopK]) {
-    static_assert(K == 8 || K == 16 || K == 64, "half a DPP row, a DPP row or a wave");
+    static_assert(K == 4 || K == 8 || K == 16 || K == 64, "a DPP quad, half a DPP row, a DPP row or a wave");
     const int r = threadIdx.x & (K - 1);
     const ProjQuery& Q = QR.q;
     constexpr int KL = kLaneTopK;
@@ -477,7 +489,9 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
             // lanes per column: the most (up to 4 in a row, 16 in a wave) that still cover
             // every column in one pass; shifts, no division
             int sh = 0;
-            if (K == 8) {
+            if (K == 4) {
+                sh = ncol <= 1 ? 2 : (ncol <= 2 ? 1 : 0);
+            } else if (K == 8) {
                 sh = ncol <= 2 ? 2 : (ncol <= 4 ? 1 : 0);
             } else if (K == 16) {
                 sh = ncol <= 4 ? 2 : (ncol <= 8 ? 1 : 0);
@@ -605,7 +619,7 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
         // a lane whose listed candidates are used up but that saw more makes the rest unknown
         const unsigned long long dry = __ballot(over && k[0] == kNoEntry);
         trunc = trunc || ((dry >> rsh) & gmask) != 0;
-        m[j] = K == 8 ? half_row_min_u32(k[0]) : row_min_u32(k[0]);
+        m[j] = K == 4 ? quad_min_u32(k[0]) : (K == 8 ? half_row_min_u32(k[0]) : row_min_u32(k[0]));
         if (K == 64) {  // the four rows' minima by v_readlane: wave-uniform, no LDS round trip
             m[j] = umin_(umin_((unsigned)__builtin_amdgcn_readlane((int)m[j], 0),
                                (unsigned)__builtin_amdgcn_readlane((int)m[j], 16)),
@@ -1476,24 +1490,58 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     __syncthreads();
     if (st && tid == 0) st[1] = wall_clock64();
     const SortedGrid G{skey, bstart, orun, sxy, sdesc, P.noct};
-    // KR lanes per query: 8 for pyramids of up to 8 levels (windows of a few cells: twice
-    // the queries per pass; C1 scoring 88 -> 68 us), 16 above (the top levels' windows
-    // span tens of columns; 8 lanes there truncate more lists and re-score more)
-    auto pass = [&](auto kr) {
+    // KR lanes per query, by the width of the query's cell window: a row's lanes split the
+    // window's columns, and its merge (kTopK rounds of a KR-lane minimum) costs the same
+    // however few candidates the window holds.  Until round 4 one KR for all queries (8 up
+    // to 8 pyramid levels, 16 above); now the queries are cut into three index ranges by a
+    // count of their window widths -- KR 4 for at most ~4 columns, 8 for ~8, 16 beyond --
+    // which are the exact classes when the queries come in octave order (TrackWithMotion-
+    // Model's LastFrame keypoints are level-major) and otherwise only a cost heuristic: the
+    // lists do not depend on KR.  ORBX_SCORE_KR_FIXED=1 builds the round-4 choice.
+    __shared__ int s_qcut[2];
+#if ORBX_SCORE_KR_FIXED
+    if (tid == 0) {
+        s_qcut[0] = 0;
+        s_qcut[1] = P.noct <= 8 ? nq : 0;
+    }
+#else
+    if (tid < 2) s_qcut[tid] = 0;
+    __syncthreads();
+    {
+        int c4 = 0, c8 = 0;
+        for (int q = tid; q < nq; q += NT) {
+            const float w = 2.0f * ldg(&pb.q[q].r) * pb.inv_w;  // window width in cells
+            c4 += w <= 2.0f;
+            c8 += w <= 6.0f;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            c4 += __shfl_xor(c4, o);
+            c8 += __shfl_xor(c8, o);
+        }
+        if (lane == 0 && (c4 | c8)) {
+            atomicAdd(&s_qcut[0], c4);
+            atomicAdd(&s_qcut[1], c8);
+        }
+    }
+#endif
+    __syncthreads();
+    const int qcut4 = s_qcut[0], qcut8 = s_qcut[1];
+    auto pass = [&](auto kr, int q0, int q1) {
         constexpr int KR = decltype(kr)::value;
         constexpr int kQw = 64 / KR;  // queries per wave and pass
         constexpr int kStep = kWaves * kQw;
-        int qb = wave * kQw;
+        int qb = q0 + wave * kQw;
         QueryReg cur;
-        if (qb < nq) cur = load_query(pb, min(qb + lane / KR, nq - 1));
-        for (; qb < nq; qb += kStep) {
+        if (qb < q1) cur = load_query(pb, min(qb + lane / KR, q1 - 1));
+        for (; qb < q1; qb += kStep) {
             const int q = qb + lane / KR;
             QueryReg nxt;
-            if (qb + kStep < nq) nxt = load_query(pb, min(q + kStep, nq - 1));  // prefetch
-            const int mp = q < nq ? cur.q.mp : -1;
+            if (qb + kStep < q1) nxt = load_query(pb, min(q + kStep, q1 - 1));  // prefetch
+            const int mp = q < q1 ? cur.q.mp : -1;
             unsigned e[kTopK];
             score_groupk<KR>(pb, P, cur, mp >= 0, G, SPLIT ? nullptr : sfmp, e);
-            if ((lane & (KR - 1)) == 0 && q < nq) {
+            if ((lane & (KR - 1)) == 0 && q < q1) {
 #pragma unroll
                 for (int v = 0; v < kListVec; v++)
                     qk[kListVec * q + v] = make_uint4(e[4 * v], e[4 * v + 1], e[4 * v + 2], e[4 * v + 3]);
@@ -1503,8 +1551,9 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
             cur = nxt;
         }
     };
-    if (P.noct <= 8) pass(std::integral_constant<int, 8>{});
-    else pass(std::integral_constant<int, 16>{});
+    if (qcut4 > 0) pass(std::integral_constant<int, 4>{}, 0, qcut4);
+    if (qcut8 > qcut4) pass(std::integral_constant<int, 8>{}, qcut4, qcut8);
+    if (nq > qcut8) pass(std::integral_constant<int, 16>{}, qcut8, nq);
     __syncthreads();
     if (st && tid == 0) st[2] = wall_clock64();
     if (SPLIT) {
