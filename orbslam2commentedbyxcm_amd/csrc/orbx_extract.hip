@@ -1594,7 +1594,11 @@ __device__ __forceinline__ void desc_level_of(const DescLevel* s, int L, int slo
 // save (configs[4] 100.6-100.9k -> 94.1-95.1k; capping them by LDS gives both back):
 // register staging above this many slots.
 #ifndef ORBX_DESC_GLDS_MAX
-#define ORBX_DESC_GLDS_MAX 3000
+// Since round 5 every frame size takes the LDS-DMA form: with lane 1 of a deep pyramid
+// (configs[4]) starting after lane 0's FAST cells instead of its octree, the DMA describe
+// (0.52-0.62 ms per launch beside the rest, against 1.0 ms) no longer slows the other
+// lane's blur: 110.5-111.4k frames/s against 111.0-111.1k for register staging (r05c)
+#define ORBX_DESC_GLDS_MAX 1000000
 #endif
 constexpr int kDescGldsMaxSlots = ORBX_DESC_GLDS_MAX;
 #ifndef ORBX_ABL_DESC

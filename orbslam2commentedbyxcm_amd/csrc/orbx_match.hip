@@ -1499,15 +1499,13 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
     // Model's LastFrame keypoints are level-major) and otherwise only a cost heuristic: the
     // lists do not depend on KR.  ORBX_SCORE_KR_FIXED=1 builds the round-4 choice.
     __shared__ int s_qcut[2];
-#if ORBX_SCORE_KR_FIXED
-    if (tid == 0) {
-        s_qcut[0] = 0;
-        s_qcut[1] = P.noct <= 8 ? nq : 0;
-    }
-#else
-    if (tid < 2) s_qcut[tid] = 0;
+    // Pyramids of up to 8 levels keep KR 8 for every query: the classes measured slower
+    // there (configs[1] 227.8-228.4k -> 224.3-225.9k frames/s) and faster above
+    // (configs[4] 108.2-108.3k -> 111.1-111.3k; r05c, interleaved on one box).
+    const bool one_kr = ORBX_SCORE_KR_FIXED || P.noct <= 8;  // uniform over the workgroup
+    if (tid < 2) s_qcut[tid] = one_kr && tid == 1 && P.noct <= 8 ? nq : 0;
     __syncthreads();
-    {
+    if (!one_kr) {
         int c4 = 0, c8 = 0;
         for (int q = tid; q < nq; q += NT) {
             const float w = 2.0f * ldg(&pb.q[q].r) * pb.inv_w;  // window width in cells
@@ -1524,7 +1522,6 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
             atomicAdd(&s_qcut[1], c8);
         }
     }
-#endif
     __syncthreads();
     const int qcut4 = s_qcut[0], qcut8 = s_qcut[1];
     auto pass = [&](auto kr, int q0, int q1) {

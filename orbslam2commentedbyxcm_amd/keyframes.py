@@ -170,29 +170,33 @@ def stream_poses(off: np.ndarray, fx: float, fy: float, depth: float) -> np.ndar
     return T
 
 
-def gather_slabs(slab, gathered, group=None, force: bool = False) -> None:
+def gather_slabs(slab, gathered, group=None, force: bool = False, async_op: bool = False):
     """Every rank's slab into `gathered` (world x slab bytes), rank order.  RCCL:
     one all_gather_into_tensor, device to device, enqueued behind the current stream's
-    work (ProcessGroupNCCL's stream waits on it, and the current stream waits on the
-    collective before anything enqueued after it).  gloo (the CPU tests, and the
-    several-ranks-on-one-GPU rehearsal): all_gather, staged through host memory for
-    device tensors.  World size 1 is a device copy unless `force`, which issues the
-    collective anyway (the one-GPU hardware test of the RCCL path)."""
+    work (ProcessGroupNCCL's stream waits on it).  async_op False: the current stream
+    waits on the collective before anything enqueued after it; True: nothing waits yet --
+    the returned work handle's wait() makes the stream current at that point wait (the
+    triangulation stream, so the matcher stream runs on past the exchange).  gloo (the
+    CPU tests, and the several-ranks-on-one-GPU rehearsal): all_gather, staged through
+    host memory for device tensors, synchronous.  World size 1 is a device copy unless
+    `force`, which issues the collective anyway (the one-GPU hardware test of the RCCL
+    path).  Returns the pending work handle or None."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     if world == 1 and not force:
         if gathered.data_ptr() != slab.data_ptr():
             gathered.copy_(slab)
-        return
+        return None
     if slab.is_cuda and dist.get_backend(group) != "gloo":
-        dist.all_gather_into_tensor(gathered, slab, group=group)
-        return
+        work = dist.all_gather_into_tensor(gathered, slab, group=group, async_op=async_op)
+        return work if async_op else None
     src = slab.cpu() if slab.is_cuda else slab
     dst = gathered.new_empty(gathered.shape, device="cpu") if gathered.is_cuda else gathered
     dist.all_gather(list(dst.view(world, -1).unbind(0)), src, group=group)
     if dst is not gathered:
         gathered.copy_(dst)
+    return None
 
 
 class StereoKeyFramePipeline:
@@ -215,6 +219,10 @@ class StereoKeyFramePipeline:
         # N-GPU data path -- collective, gathered buffers, keyframe tables into them -- is
         # the one under test on a single GPU; world > 1 always exchanges
         self.collective = self.world > 1 or bool(collective)
+        # the exchange's work handle is waited for on the triangulation stream only
+        # (ORBX_GATHER_SYNC=1: the round-4 order, the matcher stream waits for it)
+        import os
+        self.gather_async = os.environ.get("ORBX_GATHER_SYNC") != "1"
         self.W, self.H = s["width"], s["height"]
         self.dev = torch.device("cuda", device)
         self.mb = s["bf"] / s["fx"]
@@ -351,14 +359,25 @@ class StereoKeyFramePipeline:
         out = {"bow_word": bw["bow_word"], "bow_value": bw["bow_value"], "nbow": bw["nbow"],
                "fv_node": v["fv_node"], "fv_off": v["fv_off"], "fv_idx": v["fv_idx"], "nfv": v["nfv"]}
         self.voc.transform_batch_device(v["desc"], v["n"], self.cap, 4, out, stream=ms.cuda_stream)
+        work = None
         with torch.cuda.stream(ms):
             # Tracking::CreateNewKeyFrame: a MapPoint for every stereo point closer than mThDepth
             torch.logical_and(v["u_right"] >= 0, rt["depth"] < self.th_depth, out=v["has_mp"].view(torch.bool))
             if self.collective:
-                gather_slabs(self.slabs[k], self.gathered[k], self.group, force=True)
+                # off the matcher stream's path (round 5): the collective waits for this set's
+                # slab, the triangulation stream waits for the collective, and the matcher
+                # stream goes on to the next step's stereo matching meanwhile.  Reuse stays
+                # ordered: the next exchange into gathered[k] is issued behind the matcher
+                # stream's wait for set k's extraction, which waits for ev_m[k] -- this
+                # step's triangulation, the buffer's last reader
+                work = gather_slabs(self.slabs[k], self.gathered[k], self.group, force=True,
+                                    async_op=self.gather_async)
         self.ev_s[k].record(ms)
         ts = self.ts
         ts.wait_event(self.ev_s[k])
+        if work is not None:
+            with torch.cuda.stream(ts):
+                work.wait()
         if len(self.plan.pairs):
             self.tri.SearchForTriangulationBatchDevice(self._tabs[k], self.cam, self.plan.pairs, self.plan.F12,
                                                        self.cap, self.m12[k], self.tri_pairs[k], self.tri_n[k],

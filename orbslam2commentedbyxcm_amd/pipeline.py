@@ -126,8 +126,10 @@ class SequencePipeline:
         # best beside one lane's describe and the other's first stages (configs[4]
         # 99.8-101.0k -> 105.7-106.0k frames/s; configs[1] with 4: 214.5-215.4k against
         # 224.4-225.1k with 2; tools/g_r3zy.sh, tools/g_r3zz.sh)
+        # (round 5: 3 for deep pyramids, with the LDS-DMA describe at every frame size --
+        # offset 3 110.5-111.4k frames/s, 4 107.6-107.9k, 2 105.3-106.3k at configs[4], r05c)
         if lane_offset_stage is None:
-            lane_offset_stage = 4 if int(params[2]) > 8 else 2
+            lane_offset_stage = 3 if int(params[2]) > 8 else 2
         self.lane_offset_stage = int(lane_offset_stage)
         self.lane_ev = [e.set_stage_event(lane_offset_stage) for e in self.exs] \
             if (lane_offset_stage and not match_after_stage and self.S > 1) else None

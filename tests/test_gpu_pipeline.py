@@ -200,16 +200,17 @@ def test_sequence_pipeline_local_map_c5_large_local_map(oracle, orbx_built):
 
 def test_sequence_pipeline_configs4_bench_shape(oracle, orbx_built):
     """configs[4]'s bench shape exactly: B = 256 in two 128-frame lanes, 5000 features x 12
-    levels (two pyramid segments), the default lane offset for deep pyramids (4: lane 1
-    starts after lane 0's octree), the lean split matcher, pipelined; every frame and every
-    pair of the newest batch against the oracle."""
+    levels (two pyramid segments), the default lane offset for deep pyramids (3 since round
+    5: lane 1 starts after lane 0's FAST cells), the LDS-DMA describe, the lean split matcher
+    with its per-window-class scoring lanes, pipelined; every frame and every pair of the
+    newest batch against the oracle."""
     prm = (5000, 1.2, 12, 20, 7)
     import torch
 
     frames, off = synth.sequence(1000, 256)
     T = sequence_poses(off)
     pl = SequencePipeline(256, 640, 480, lanes=2, pipelined=True, params=prm)
-    assert pl.lane_offset_stage == 4 and pl.lane_ev is not None and pl.S == 2
+    assert pl.lane_offset_stage == 3 and pl.lane_ev is not None and pl.S == 2
     d_frames = torch.from_numpy(frames).to(pl.dev)
     d_T = torch.from_numpy(T).to(pl.dev)
     torch.cuda.synchronize()
