@@ -1,8 +1,10 @@
-"""Summarise tools/rccl_ab.sh: the interleaved in-place / --collective EuRoC bench lines
-(rate and step time per pair, the difference) and, from the kernel trace of the
---collective run, the RCCL kernels' durations and the idle time they leave on their queue
-(from the end of the kernel before each collective to the start of the kernel after it).
-usage: python tools/rccl_summary.py TAG  ->  profiles/TAG_rccl_ab.json
+"""Summarise tools/rccl_ab.sh: the interleaved EuRoC bench lines -- in place, the RCCL
+exchange waited for by the matcher stream ("sync", round 4's order) and waited for by the
+triangulation stream only ("collective", the default) -- and, from the kernel trace of a
+--collective run, what the exchange runs as on the GPU.  At world size 1 RCCL's
+all_gather_into_tensor of one rank is a device-to-device copy of the slab (a
+__amd_rocclr_copyBuffer launch on the communicator's queue), no RCCL kernel.
+usage: python tools/rccl_summary.py TAG [SLAB_MB]  ->  profiles/TAG_rccl_ab.json
 """
 import csv
 import glob
@@ -12,50 +14,45 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
+MODES = ("inplace", "sync", "collective")
 
 
 def main():
     tag = sys.argv[1]
+    slab_mb = float(sys.argv[2]) if len(sys.argv) > 2 else 6.1
     base = ROOT / "gpurun_out"
-    pairs = []
+    runs = {m: [] for m in MODES}
     i = 1
     while (base / f"{tag}_euroc_inplace_{i}.json").exists():
-        row = {}
-        for mode in ("inplace", "collective"):
-            d = json.loads((base / f"{tag}_euroc_{mode}_{i}.json").read_text().splitlines()[-1])
-            row[mode] = {"value": d["value"], "ms_per_step": d["ms_per_step"],
-                         "slab_exchange": d["config"].get("slab_exchange")}
-        row["step_ms_added"] = round(row["collective"]["ms_per_step"] - row["inplace"]["ms_per_step"], 4)
-        pairs.append(row)
+        for m in MODES:
+            f = base / f"{tag}_euroc_{m}_{i}.json"
+            if f.exists():
+                d = json.loads(f.read_text().splitlines()[-1])
+                runs[m].append({"value": d["value"], "ms_per_step": d["ms_per_step"],
+                                "slab_exchange": d["config"].get("slab_exchange")})
         i += 1
-    ev = []
+    med = {m: statistics.median(r["ms_per_step"] for r in v) for m, v in runs.items() if v}
+    copies = []
     for p in glob.glob(str(base / f"{tag}_rccl_prof" / "**" / "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(p)):
-            ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0],
-                       r.get("Queue_Id", r.get("Stream_Id"))))
-    ev.sort()
-    coll = [k for k, e in enumerate(ev) if any(t in e[2].lower() for t in ("nccl", "rccl"))]
-    durs, gaps = [], []
-    for k in coll:
-        s, e, _, q = ev[k]
-        durs.append((e - s) / 1e3)
-        prev = [x for x in ev[:k] if x[3] == q]
-        nxt = [x for x in ev[k + 1:] if x[3] == q]
-        if prev and nxt:
-            gaps.append((nxt[0][0] - prev[-1][1]) / 1e3)
-    out = {"what": "configs[3] EuRoC step with the RCCL all_gather_into_tensor of the keyframe slabs (world size 1: "
-                   "a self-gather through the process group) against the in-place step, interleaved on one box",
-           "pairs": pairs,
-           "step_ms_added_median": statistics.median(p["step_ms_added"] for p in pairs) if pairs else None,
-           "step_ms_inplace_median": statistics.median(p["inplace"]["ms_per_step"] for p in pairs) if pairs else None,
-           "rccl_kernels": {"launches": len(durs), "names": sorted({ev[k][2] for k in coll}),
-                            "duration_us_median": round(statistics.median(durs), 2) if durs else None,
-                            "queue_span_us_median": round(statistics.median(gaps), 2) if gaps else None,
-                            "note": "queue span: end of the kernel before the collective to the start of the kernel "
-                                    "after it on the same queue"}}
+            name = r["Kernel_Name"]
+            if "copyBuffer" in name and int(r.get("Grid_Size_X", 0)) >= 65536:  # the slab-sized copies
+                copies.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+            if any(t in name.lower() for t in ("nccl", "rccl")):
+                copies.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    out = {"what": "configs[3] EuRoC step: the RCCL all_gather_into_tensor of the keyframe slabs at world size 1 "
+                   "(bench.py --workload euroc --collective) against the in-place step, interleaved on one box",
+           "runs": runs, "ms_per_step_median": med,
+           "step_ms_added_sync": round(med["sync"] - med["inplace"], 4) if "sync" in med else None,
+           "step_ms_added_async": round(med["collective"] - med["inplace"], 4) if "collective" in med else None,
+           "exchange_on_gpu": {"launches": len(copies),
+                               "duration_us_median": round(statistics.median(copies), 1) if copies else None,
+                               "note": "world size 1: RCCL's one-rank all-gather is a device copy of the slab"},
+           "slab_mb": slab_mb}
     dst = ROOT / "profiles" / f"{tag}_rccl_ab.json"
     dst.write_text(json.dumps(out, indent=1))
-    print(json.dumps(out, indent=1))
+    print(json.dumps({k: out[k] for k in ("ms_per_step_median", "step_ms_added_sync", "step_ms_added_async",
+                                          "exchange_on_gpu")}, indent=1))
     print("->", dst)
 
 
