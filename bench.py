@@ -169,14 +169,20 @@ def rocprof_mean_ms(stage: str, workload: str):
     return (None if tot is None else tot * 1e-6), files[-1].name
 
 
+def dominant_stage_from_trace(stages, workload: str):
+    """The stage whose kernels run longest per launch in the committed kernel trace of this
+    workload's bench, or None when the trace does not cover every stage."""
+    prof = {k: rocprof_mean_ms(k, workload)[0] for k in stages}
+    if all(v is not None for v in prof.values()):
+        return max(prof, key=prof.get)
+    return None
+
+
 def dominant_stage(event_ms: dict, workload: str) -> str:
     """The stage whose kernels run longest per launch: by the committed kernel trace of
     this workload's bench when it covers every stage, else by the HIP-event times (which,
     pipelined, also hold the time a kernel waited for CUs held by other streams)."""
-    prof = {k: rocprof_mean_ms(k, workload)[0] for k in event_ms}
-    if all(v is not None for v in prof.values()):
-        return max(prof, key=prof.get)
-    return max(event_ms, key=event_ms.get)
+    return dominant_stage_from_trace(event_ms, workload) or max(event_ms, key=event_ms.get)
 
 
 OTHER_WORKLOADS = ("_tum5k_", "_kitti_", "_euroc_")
@@ -508,6 +514,15 @@ def main():
     # sets, read back after the loop, no synchronisation inside it): every recorded event
     # costs the pipelined step ~0.2 % (tools/timing_ab.py: all stages' events 1.3-1.6 %).
     wl = "tum5k" if c5 else "tum"
+    # the committed trace's choice of the dominant stage is read (files, hashes) before the
+    # warmup, not between the warmup and the timed region: ~13 ms of host work there left
+    # the GPU idle right before the timed steps
+    # (ORBX_BENCH_DOM_LATE=1, A/B knob: read it after the warmup as until round 4)
+    late = os.environ.get("ORBX_BENCH_DOM_LATE") == "1"
+    if not late:
+        source_hash()
+    dom_trace = None if late else \
+        dominant_stage_from_trace(["pyramid", "score_blur", "fast_cells", "octree", "describe"], wl)
     # the first warmup step (first-call costs) is not recorded: the stage table comes from
     # the W - 1 after it (one step when W <= 2)
     if args.warmup >= 2:
@@ -522,7 +537,7 @@ def main():
     # runs beside the next batch's extraction on its own stream, so the step is set by
     # whichever is longer: a lane's extraction (its longest stage is reported) or the
     # matcher (configs[4]: its launch is then the critical path).
-    dom = dominant_stage(kernels, wl)
+    dom = dominant_stage(kernels, wl) if late else (dom_trace or max(kernels, key=kernels.get))
     if match and pipeline and stage_ms.get("match", 0.0) > stage_ms.get("total", 0.0):
         dom = "match"
     # ORBX_BENCH_ALL_EVENTS=1 (A/B knob): every stage's events in the timed steps too

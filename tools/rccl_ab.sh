@@ -21,7 +21,7 @@ for i in $(seq 1 $N); do
   done
 done
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_rccl_prof -o run -- \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_rccl_prof -o run -- \
     python3 $R/bench.py --workload euroc --no-cpu-baseline --parity-frames 0 --collective \
     > $R/gpurun_out/${TAG}_rccl_prof.json 2> $R/gpurun_out/${TAG}_rccl_prof.err || exit 1
 echo "rccl_ab ok"
