@@ -1,11 +1,13 @@
 # A/B timing of bench.py argument sets, interleaved over ROUNDS rounds (one process per run).
-# usage: bash tools/ab_args.sh ROUNDS "ARGS1" "ARGS2" ...   (ARGS may start with ENV=V words)
+# usage: bash tools/ab_args.sh ROUNDS "ARGS1" "ARGS2" ...   (ARGS may start with ENV=V words;
+#   ':' stands for a space inside one ARGS, for tools/gpu_job.sh's run= step)
 set -o pipefail
 N=$1; shift
 mkdir -p gpurun_out
 for i in $(seq 1 $N); do
   j=0
   for a in "$@"; do
+    a=${a//:/ }
     j=$((j+1))
     env $(echo "$a" | tr ' ' '\n' | grep '=' | tr '\n' ' ') timeout -k 10 200 python bench.py --no-cpu-baseline \
         --parity-frames 0 --steps 30 $(echo "$a" | tr ' ' '\n' | grep -v '=' | tr '\n' ' ') \
