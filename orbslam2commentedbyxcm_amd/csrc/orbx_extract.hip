@@ -959,6 +959,16 @@ __device__ __forceinline__ void child_box(int q, int x0, int y0, int x1, int y1,
 
 // ------------------------------------------------------------------ octree
 
+// Full passes with at most this many nodes count their quadrants per distinct (node,
+// quadrant) of a wave (wave_count_q: a readlane / ballot / atomic loop); larger lists use
+// one LDS atomic per key.  Until round 5 the loop ran up to 64 nodes; one atomic per key
+// measured faster at every size (r05i, interleaved: configs[1] 228.5k -> 229.3-229.7k,
+// configs[4] 111.1-111.5k -> 113.4-113.7k frames/s; the single C1 / C3 / C5 call 144 /
+// 226 / 234 -> 137 / 206 / 212 us), so 0 turns it off.
+#ifndef ORBX_OCT_FEW
+#define ORBX_OCT_FEW 0
+#endif
+
 // Node list, stored in list order (front first).  Two buffers, swapped every step.
 constexpr int kOctKeysReg = 16 * 256;  // keys per level held in registers by k_octree
 
@@ -1231,7 +1241,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
         for (int j = tid; j < size; j += 256) ccnt[2 * j] = ccnt[2 * j + 1] = 0u;
         if (tid == 0) s_scal[1] = 0;
         __syncthreads();
-        const bool few = size <= 64;
+        const bool few = size <= ORBX_OCT_FEW;
         FOR_KEYS({
             const int nd = NN;
             if (A.cnt[nd] >= 2) {
