@@ -148,7 +148,7 @@ int prepare(orbx_extractor* ex, int W, int H, int batch) {
     HIP_TRY(dalloc(&db.dt_list, B * (size_t)p.kept_per_frame));
     HIP_TRY(dalloc(&db.dt_tile, B * (size_t)p.tiles_total));
     HIP_TRY(dalloc(&db.status, B));
-    if (getenv("ORBX_OCT_STAMPS")) HIP_TRY(dalloc(&db.oct_stamps, B * (size_t)p.L * 8));
+    if (getenv("ORBX_OCT_STAMPS")) HIP_TRY(dalloc(&db.oct_stamps, B * (size_t)p.L * 16));  // kOctStampWords
     HIP_TRY(hipMemcpyAsync(db.lv, p.lv, sizeof(LevelGeom) * kMaxLevels, hipMemcpyHostToDevice, ex->stream));
     HIP_TRY(hipMemcpyAsync(db.cells, p.cells.data(), sizeof(CellGeom) * p.cells.size(), hipMemcpyHostToDevice,
                            ex->stream));
@@ -195,13 +195,15 @@ int run_device(orbx_extractor* ex, int batch, const uint8_t* d_imgs, size_t fram
     if (e != hipSuccess) return hip_fail(e, "launch_extract");
     if (ex->db.oct_stamps) {  // diagnostics: per-level k_octree phase times (us) to stderr
         const int L = ex->plan.L;
-        std::vector<unsigned long long> h((size_t)batch * L * 8);
+        constexpr int W = 16;  // kOctStampWords
+        std::vector<unsigned long long> h((size_t)batch * L * W);
         HIP_TRY(hipStreamSynchronize(stream));
         HIP_TRY(hipMemcpy(h.data(), ex->db.oct_stamps, h.size() * 8, hipMemcpyDeviceToHost));
         for (int l = 0; l < L; l++) {
-            double ph[4] = {0, 0, 0, 0}, mx = 0, n = 0, g1 = 0, g2 = 0;
+            double ph[4] = {0, 0, 0, 0}, mx = 0, n = 0, g1 = 0, g2 = 0, rk = 0;
             for (int f = 0; f < batch; f++) {
-                const unsigned long long* r = &h[((size_t)f * L + l) * 8];
+                const unsigned long long* r = &h[((size_t)f * L + l) * W];
+                rk += (double)r[8] * 0.01;
                 for (int k = 0; k < 4; k++) ph[k] += (double)(r[k + 1] - r[k]) * 0.01;
                 const double tot = (double)(r[4] - r[0]) * 0.01;
                 mx = tot > mx ? tot : mx;
@@ -209,8 +211,10 @@ int run_device(orbx_extractor* ex, int batch, const uint8_t* d_imgs, size_t fram
                 g1 += (double)r[7];
                 g2 += (double)r[5];
             }
-            fprintf(stderr, "[orbx oct] L%d keys %.0f | gather %.1f passes %.1f (%.1f it) final %.1f (%.1f it) out %.1f | max %.1f us\n",
-                    l, n / batch, ph[0] / batch, ph[1] / batch, g1 / batch, ph[2] / batch, (g2 - g1) / batch,
+            fprintf(stderr,
+                    "[orbx oct] L%d keys %.0f | gather %.1f passes %.1f (%.1f it) final %.1f (%.1f it, ranking %.1f) out %.1f"
+                    " | max %.1f us\n",
+                    l, n / batch, ph[0] / batch, ph[1] / batch, g1 / batch, ph[2] / batch, (g2 - g1) / batch, rk / batch,
                     ph[3] / batch, mx);
         }
     }

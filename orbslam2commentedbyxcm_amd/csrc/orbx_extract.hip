@@ -1008,6 +1008,7 @@ __device__ __forceinline__ int get_q(const uint32_t* a, int nd, int q) {
 // Keys per level the packed counters and keys hold (u16 counts); a level with more
 // FAST keypoints is flagged kStatusNodeOverflow.
 constexpr int kOctMaxKeys = 65535;
+constexpr int kOctStampWords = 16;  // diagnostics row per (frame, level), ORBX_OCT_STAMPS
 constexpr int kOctNodeBytes = 4 + 8 + 8 + 8 + 2 + 4 + 16 + 2;  // best, ccnt, sa+sb, cnt x2, sc, crank x2, boxes, inV
 
 struct NodeBuf {
@@ -1063,8 +1064,11 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
         }
     }
     const int tid = threadIdx.x;
-    unsigned long long* st = stamps ? stamps + 8 * ((size_t)f * L + l) : nullptr;
-    if (st && tid == 0) st[0] = wall_clock64();
+    unsigned long long* st = stamps ? stamps + kOctStampWords * ((size_t)f * L + l) : nullptr;
+    if (st && tid == 0) {
+        st[0] = wall_clock64();
+        st[8] = 0;  // final phase: ticks spent ranking vPrev
+    }
     const int lane = tid & 63, wave = tid >> 6;
     const LevelGeom& g = lv[l];
     const int N = g.N;
@@ -1352,22 +1356,34 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
                 best[sa[j]] = ((uint32_t)A.cnt[j] << 16) | (uint32_t)(uint16_t)A.crank[j];
                 sb[sa[j]] = j;
             }
-        // pad to a multiple of 4 with keys never larger (past NC the reads land in the
-        // zeroed ccnt)
-        if (tid < 3 && nv + tid < NC) best[nv + tid] = 0u;
+        // pad to a multiple of 16 with keys never larger (past NC they land in ccnt, which
+        // is zero here)
+        if (tid < 15) best[nv + tid] = 0u;
         __syncthreads();
-        for (int p = tid; p < nv; p += 256) {
-            const uint32_t kp = best[p];
-            int r0 = 0, r1 = 0, r2 = 0, r3 = 0;
-            for (int i = 0; i < nv; i += 4) {
-                r0 += best[i] > kp;
-                r1 += best[i + 1] > kp;
-                r2 += best[i + 2] > kp;
-                r3 += best[i + 3] > kp;
+        const unsigned long long t_rank = st && tid == 0 ? wall_clock64() : 0;
+        // a member's rank counts the larger keys: two members per thread and pass, the keys
+        // read 16 at a time as four broadcast 16-byte LDS reads (latency, not the compares,
+        // bounds this loop in a workgroup that has its CU to itself)
+        for (int p0 = tid; p0 < nv; p0 += 512) {
+            const int p1 = p0 + 256;
+            const uint32_t k0 = best[p0], k1 = p1 < nv ? best[p1] : ~0u;
+            int r0 = 0, r1 = 0;
+            const uint4* b4 = (const uint4*)best;
+            for (int i = 0; i < nv; i += 16) {
+                uint4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) v[u] = b4[(i >> 2) + u];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    r0 += (v[u].x > k0) + (v[u].y > k0) + (v[u].z > k0) + (v[u].w > k0);
+                    r1 += (v[u].x > k1) + (v[u].y > k1) + (v[u].z > k1) + (v[u].w > k1);
+                }
             }
-            sc[sb[p]] = (int16_t)(r0 + r1 + r2 + r3);
+            sc[sb[p0]] = (int16_t)r0;
+            if (p1 < nv) sc[sb[p1]] = (int16_t)r1;
         }
         __syncthreads();
+        if (st && tid == 0) st[8] += wall_clock64() - t_rank;
         for (int j = tid; j < size; j += 256)
             if (sc[j] >= 0) sa[sc[j]] = j;  // sa[r] = node processed r-th
         FOR_KEYS({
