@@ -448,6 +448,8 @@ def main():
                     help="skip the host-fed leg (frames uploaded from pinned host memory every step)")
     ap.add_argument("--no-local-map", action="store_true",
                     help="skip the second measurement of the step with TrackLocalMap's SearchLocalPoints")
+    ap.add_argument("--no-exchange", action="store_true",
+                    help="at --gpus > 1, skip the configs[3] keyframe-exchange leg (RCCL all-gather between ranks)")
     ap.add_argument("--selftest-launch", action="store_true", help=argparse.SUPPRESS)
     args, _ = ap.parse_known_args()
 
@@ -478,13 +480,21 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # Rehearsal of the N-rank run on a one-GPU box (never the driver's run):
+    # ORBX_BENCH_SHARE_GPU=1 puts every rank on GPU 0 and ORBX_BENCH_PG=gloo carries the
+    # barriers, the max-over-ranks time and the slab exchange (staged through host memory),
+    # since RCCL needs one GPU per rank.
+    gpu = 0 if os.environ.get("ORBX_BENCH_SHARE_GPU") == "1" else local_rank
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+        if os.environ.get("ORBX_BENCH_PG", "nccl") == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
 
     pipeline = match and not args.no_pipeline
-    pl = SequencePipeline(B, W, H, lanes=args.lanes, pipelined=pipeline, match=match, device=local_rank,
+    pl = SequencePipeline(B, W, H, lanes=args.lanes, pipelined=pipeline, match=match, device=gpu,
                           params=prm, fx=FX, fy=FY, cx=CX, cy=CY, depth=DEPTH, th=TH,
                           match_stream=_match_stream(dev) if match else None,
                           nbuf=int(os.environ.get("ORBX_PIPE_NBUF", "2")),
@@ -650,7 +660,7 @@ def main():
     if match and not args.no_local_map:
         pl.close()
         del pl
-        pl2 = SequencePipeline(B, W, H, lanes=args.lanes, pipelined=pipeline, device=local_rank, params=prm, fx=FX,
+        pl2 = SequencePipeline(B, W, H, lanes=args.lanes, pipelined=pipeline, device=gpu, params=prm, fx=FX,
                                fy=FY, cx=CX, cy=CY, depth=DEPTH, th=TH, local_map=True)
         pl2.run(d_frames, d_T, max(args.warmup, 1))
         sync()
@@ -689,6 +699,30 @@ def main():
             pr["bit_exact"] = pr["bit_exact"] and pr["octree_status_clean"]
             local["parity"] = pr
         pl2.close()
+
+    # At world size > 1 the node's GPUs also run configs[3]'s step with its one real
+    # exchange -- the keyframe slabs all-gathered over RCCL between the ranks (DESIGN.md
+    # section 6) -- for a few timed steps, rank 0 checking its keyframes, the neighbours it
+    # received from the other ranks and its triangulation pairs against the oracle.  Not
+    # `value`; the headline step itself has no collective.
+    exchange = None
+    if world > 1 and not args.no_exchange:
+        sys.path.insert(0, str(ROOT / "tests"))
+        import euroc_bench
+        eargs = euroc_bench.parse(["--steps", "10", "--warmup", "3", "--no-cpu-baseline"])
+        line = euroc_bench.run(eargs, rank, world, gpu, True)
+        if line is not None:
+            c, pr = line["config"], line["parity"]
+            exchange = {"value": line["value"], "unit": line["unit"], "ms_per_step": line["ms_per_step"],
+                        "steps": line["steps"], "slab_exchange": c["slab_exchange"],
+                        "slab_mb_per_rank": c["slab_mb_per_rank"],
+                        "allgather_mb_per_rank_step": c["allgather_mb_per_rank_step"],
+                        "parity": {k: pr.get(k) for k in ("bit_exact", "keyframes_checked", "keyframes_mismatched",
+                                                          "gathered_neighbours_checked", "gathered_mismatched",
+                                                          "pairs_checked", "pairs_mismatched")},
+                        "step": "configs[3] (bench.py --workload euroc): extract L+R, ComputeStereoMatches, "
+                                "ComputeBoW, close-point MapPoints, RCCL all_gather_into_tensor of the keyframe "
+                                "slabs, SearchForTriangulation against the gathered neighbours"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -741,6 +775,7 @@ def main():
             "parity": parity,
             "with_local_map": local,
             "host_fed": host_fed,
+            "keyframe_exchange": exchange,
             "mean_keypoints_per_frame": round(mean_kps, 1),
             "mean_matches_per_pair": round(mean_matches, 1),
         }

@@ -211,7 +211,7 @@ def cpu_baseline(pl, O, text, seconds: float, threads: int) -> dict:
                       f"neighbours (average), over 32 distinct keyframes; scalar port built {flags}"}
 
 
-def main(argv=None):
+def parse(argv=None):
     ap = argparse.ArgumentParser(prog="bench.py --workload euroc")
     ap.add_argument("--workload", default="euroc")
     ap.add_argument("--gpus", type=int, default=1)
@@ -228,16 +228,17 @@ def main(argv=None):
                     help="exchange the slabs through an RCCL process group even at --gpus 1 (a one-rank "
                          "all_gather_into_tensor into gathered buffers: the N-GPU data path on one GPU)")
     args, _ = ap.parse_known_args(argv)
+    return args
+
+
+def main(argv=None):
+    args = parse(argv)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
-    B = args.batch
 
     import torch
     import torch.distributed as dist
-
-    from orbslam2commentedbyxcm_amd import ORBextractor, synth
-    from orbslam2commentedbyxcm_amd.keyframes import EUROC, StereoKeyFramePipeline
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
@@ -253,6 +254,27 @@ def main(argv=None):
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=dev)
+    out = run(args, rank, world, local_rank, collective)
+    if collective:
+        dist.barrier()
+        dist.destroy_process_group()
+    if out is not None:
+        print(json.dumps(out), flush=True)
+
+
+def run(args, rank: int, world: int, local_rank: int, collective: bool):
+    """The configs[3] step on this rank (the process group, when collective, is already
+    up): warmup, the timed steps (max over ranks), rank 0's parity and bench line (None
+    on the other ranks).  bench.py's headline run calls it at world size > 1 for its
+    keyframe-exchange leg."""
+    import torch
+    import torch.distributed as dist
+
+    from orbslam2commentedbyxcm_amd import ORBextractor, synth
+    from orbslam2commentedbyxcm_amd.keyframes import EUROC, StereoKeyFramePipeline
+
+    dev = torch.device("cuda", local_rank)
+    B = args.batch
     s = EUROC
     # the vocabulary's level-1 centres come from the stream's first left view (same on every rank)
     seq0 = synth.StereoSequence(3, 1, s["width"], s["height"], step=16, margin=256, disp=13)
@@ -343,8 +365,9 @@ def main(argv=None):
                                    f"keyframe vs its nn={args.nn} stream neighbours passing the baseline test",
                        "keyframes_per_gpu_step": B, "global_batch": B * world, "width": pl.W, "height": pl.H,
                        "parallelism": f"frame-sharded x{world} + all-gather", "slab_mb_per_rank": round(slab_mb, 2),
-                       "slab_exchange": ("rccl all_gather_into_tensor" if collective else "none (world 1: slabs read in "
-                                         "place)"),
+                       "slab_exchange": ("none (world 1: slabs read in place)" if not collective else
+                                         "rccl all_gather_into_tensor" if dist.get_backend() == "nccl" else
+                                         "gloo all_gather, staged through host memory (one-GPU rehearsal)"),
                        "allgather_mb_per_rank_step": round(slab_mb * world, 2),
                        "triangulation_pairs_per_step": tot_pairs, "baseline_skipped_per_step": tot_skipped,
                        "triangulation_matches_per_step": tot_matches},
@@ -361,11 +384,8 @@ def main(argv=None):
             "mean_stereo_matches_per_keyframe": round(float((res["ur"] >= 0).sum(axis=1).mean()), 1),
             "vocabulary_generate_s": round(gen_s, 2),
         }
-    if collective:
-        dist.barrier()
-        dist.destroy_process_group()
-    if out is not None:
-        print(json.dumps(out), flush=True)
+    pl.close()
+    return out
 
 
 if __name__ == "__main__":
