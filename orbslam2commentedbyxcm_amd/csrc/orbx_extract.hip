@@ -1009,11 +1009,11 @@ __device__ __forceinline__ int get_q(const uint32_t* a, int nd, int q) {
 // FAST keypoints is flagged kStatusNodeOverflow.
 constexpr int kOctMaxKeys = 65535;
 constexpr int kOctStampWords = 16;  // diagnostics row per (frame, level), ORBX_OCT_STAMPS
-constexpr int kOctNodeBytes = 4 + 8 + 8 + 8 + 2 + 4 + 16 + 2;  // best, ccnt, sa+sb, cnt x2, sc, crank x2, boxes, inV
+constexpr int kOctNodeBytes = 4 + 8 + 8 + 4 + 2 + 4 + 16 + 2;  // best, ccnt, sa+sb, cnt x2 (u16), sc, crank x2, boxes, inV
 
 struct NodeBuf {
     int16_t *x0, *y0, *x1, *y1;
-    int* cnt;
+    uint16_t* cnt;  // keys in the node (<= kOctMaxKeys)
     int16_t* crank;  // creation rank within the step that created the node (< NC)
     uint8_t* inV;   // member of vSizeAndPointerToNode (created last step with >1 key)
 };
@@ -1073,7 +1073,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
     const LevelGeom& g = lv[l];
     const int N = g.N;
 
-    // LDS carve-up (NC nodes, kOctNodeBytes = 52 B each: at configs[4]'s NC = 960 three
+    // LDS carve-up (NC nodes, kOctNodeBytes = 48 B each: at configs[4]'s NC = 960 three
     // workgroups fit a CU).  best: the final phase's (size << 16 | creation rank) keys,
     // then each node's (response << 24 | ~key index) maximum; ccnt: four u16 quadrant
     // counters per node, reused for the children's positions; sc: per-node ne / ranks.
@@ -1082,7 +1082,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
     uint16_t* cpos = (uint16_t*)ccnt;                                   // [4*NC] child positions
     int* sa = (int*)(ccnt + 2 * NC);                                    // NC
     int* sb = sa + NC;                                                  // NC
-    int* cntb = sb + NC;                                                // 2*NC
+    uint16_t* cntb = (uint16_t*)(sb + NC);                              // 2*NC
     int16_t* sc = (int16_t*)(cntb + 2 * NC);                            // NC
     int16_t* crkb = sc + NC;                                            // 2*NC
     int16_t* boxb = crkb + 2 * NC;                                      // 8*NC
@@ -1216,7 +1216,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
                 nb0.x1[j] = (int16_t)g.ini_x0[i + 1];
                 nb0.y0[j] = 0;
                 nb0.y1[j] = (int16_t)g.height_rel;
-                nb0.cnt[j] = s_icnt[i];
+                nb0.cnt[j] = (uint16_t)s_icnt[i];
                 nb0.crank[j] = i;
                 nb0.inV[j] = 0;
                 j++;
@@ -1290,7 +1290,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
                         B.y0[pos] = (int16_t)cy0;
                         B.x1[pos] = (int16_t)cx1;
                         B.y1[pos] = (int16_t)cy1;
-                        B.cnt[pos] = cq;
+                        B.cnt[pos] = (uint16_t)cq;
                         B.crank[pos] = (int16_t)(sa[j] + r);
                         B.inV[pos] = cq > 1;
                         cpos[4 * j + q] = (uint16_t)pos;
@@ -1459,7 +1459,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
                         B.y0[pos] = (int16_t)cy0;
                         B.x1[pos] = (int16_t)cx1;
                         B.y1[pos] = (int16_t)cy1;
-                        B.cnt[pos] = cq;
+                        B.cnt[pos] = (uint16_t)cq;
                         B.crank[pos] = (int16_t)(Er + rr);
                         B.inV[pos] = cq > 1;
                         cpos[4 * j + q] = (uint16_t)pos;
@@ -2142,7 +2142,10 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     if (stage_ev && stage_after == 3) (void)hipEventRecord(stage_ev, stream);
     for (int rep = 0; rep < (dup == 4 ? 2 : 1); rep++) {
         const int NC = (plan.max_ncap + 63) & ~63;
-        const size_t lds = (size_t)NC * kOctNodeBytes;
+#ifndef ORBX_EXP_OCT_LDS_PAD
+#define ORBX_EXP_OCT_LDS_PAD 0  // timing experiment: extra dynamic LDS per k_octree workgroup
+#endif
+        const size_t lds = (size_t)NC * kOctNodeBytes + ORBX_EXP_OCT_LDS_PAD;
         // int16 node ids / ranks, and one workgroup's LDS (beside its static arrays)
         if (NC > 32767 || lds > 152 * 1024) return hipErrorInvalidValue;
         if (lds > 64 * 1024) {

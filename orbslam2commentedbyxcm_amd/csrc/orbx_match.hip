@@ -1755,7 +1755,12 @@ hipError_t launch_stage_copy(const void* src, void* dst, size_t bytes, hipStream
 }
 
 // k_seq_commit's dynamic LDS: the replay's lists, then the claims and the owner map
-static size_t seq_commit_lds(int cap, int rt) { return (size_t)kTopK * rt * 4 + (size_t)cap * 8; }
+#ifndef ORBX_EXP_COMMIT_LDS_PAD
+#define ORBX_EXP_COMMIT_LDS_PAD 0  // timing experiment: extra dynamic LDS per k_seq_commit workgroup
+#endif
+static size_t seq_commit_lds(int cap, int rt) {
+    return (size_t)kTopK * rt * 4 + (size_t)cap * 8 + ORBX_EXP_COMMIT_LDS_PAD;
+}
 
 // Threads of the replay workgroup: `rt` if given (64, 256 or 1024), else ORBX_REPLAY_THREADS,
 // else 256 for a batch (four waves: configs[4] 93.4-94.2k -> 93.8-95.2k frames/s and
