@@ -1418,8 +1418,31 @@ __device__ __forceinline__ SortedGrid seq_grid(unsigned char* base, const SeqGri
 // QLDS: per-query state in LDS; otherwise in the problem's global scratch.
 // SPLIT: no replay here -- the sorted grid is published to `grids` (SeqGridLayout, no
 // sorted descriptors) and k_seq_commit replays with one wave and a small LDS footprint.
+// Register budgets (waves per SIMD) of the batched sequence matcher's two kernels, which run
+// beside the extraction lanes: every VGPR they hold for their whole launch is one the
+// extraction's waves on that SIMD cannot have.  0: the compiler's choice.  The scoring
+// kernel at 5 (96 VGPRs, 20 B of spill, against 100): configs[4] 107.3-108.6k ->
+// 109.5-109.7k frames/s, configs[1] +0.1-0.3 %; 6 and 8 (more spills) and the commit at
+// 3 or 4 measured slower (r05p, interleaved on one box).
+#ifndef ORBX_SCORE_WPE
+#define ORBX_SCORE_WPE 5
+#endif
+#ifndef ORBX_COMMIT_WPE
+#define ORBX_COMMIT_WPE 0
+#endif
+#if ORBX_SCORE_WPE
+#define ORBX_SCORE_ATTR __attribute__((amdgpu_waves_per_eu(ORBX_SCORE_WPE)))
+#else
+#define ORBX_SCORE_ATTR
+#endif
+#if ORBX_COMMIT_WPE
+#define ORBX_COMMIT_ATTR __attribute__((amdgpu_waves_per_eu(ORBX_COMMIT_WPE)))
+#else
+#define ORBX_COMMIT_ATTR
+#endif
+
 template <bool QLDS, bool DLDS, int NT, bool SPLIT = false>
-__global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restrict__ probs, ProjParams P,
+__global__ __launch_bounds__(NT) ORBX_SCORE_ATTR void k_proj_search(const ProjProblem* __restrict__ probs, ProjParams P,
                                                               unsigned long long* __restrict__ scratch,
                                                               const long long* __restrict__ scratch_off,
                                                               unsigned char* __restrict__ grids, int gcap) {
@@ -1696,7 +1719,7 @@ __global__ __launch_bounds__(kSeqScoreThreads) void k_seq_score(const ProjProble
 }
 
 template <int RT>
-__global__ __launch_bounds__(RT) void k_seq_commit(const ProjProblem* __restrict__ probs, ProjParams P,
+__global__ __launch_bounds__(RT) ORBX_COMMIT_ATTR void k_seq_commit(const ProjProblem* __restrict__ probs, ProjParams P,
                                                    unsigned char* __restrict__ grids, int cap,
                                                    unsigned long long* __restrict__ scratch,
                                                    const long long* __restrict__ scratch_off, int use_sdesc) {
@@ -2121,7 +2144,10 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
         if (small) return hipErrorInvalidValue;
         dlds = qlds = false;
     }
-    const size_t lds = ProjLds(max_n, max_nq, dlds, qlds, P.noct, split_grids == nullptr).total;
+#ifndef ORBX_EXP_SCORE_LDS_PAD
+#define ORBX_EXP_SCORE_LDS_PAD 0  // timing experiment: extra dynamic LDS per k_proj_search workgroup
+#endif
+    const size_t lds = ProjLds(max_n, max_nq, dlds, qlds, P.noct, split_grids == nullptr).total + ORBX_EXP_SCORE_LDS_PAD;
     if (lds > limit) return hipErrorInvalidValue;
     const void* fn;
     const int nt = tiny ? kProjThreadsTiny : (small ? kProjThreadsSmall : kProjThreads);
