@@ -1441,11 +1441,11 @@ __device__ __forceinline__ SortedGrid seq_grid(unsigned char* base, const SeqGri
 #define ORBX_COMMIT_ATTR
 #endif
 
-template <bool QLDS, bool DLDS, int NT, bool SPLIT = false>
-__global__ __launch_bounds__(NT) ORBX_SCORE_ATTR void k_proj_search(const ProjProblem* __restrict__ probs, ProjParams P,
-                                                              unsigned long long* __restrict__ scratch,
-                                                              const long long* __restrict__ scratch_off,
-                                                              unsigned char* __restrict__ grids, int gcap) {
+template <bool QLDS, bool DLDS, int NT, bool SPLIT>
+__device__ __forceinline__ void proj_search_body(const ProjProblem* __restrict__ probs, ProjParams P,
+                                                 unsigned long long* __restrict__ scratch,
+                                                 const long long* __restrict__ scratch_off,
+                                                 unsigned char* __restrict__ grids, int gcap) {
     static_assert(!SPLIT || !DLDS, "the split scoring tests the initial claims through the sorted keys only");
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_hist[kHistoLength];
@@ -1597,6 +1597,22 @@ __global__ __launch_bounds__(NT) ORBX_SCORE_ATTR void k_proj_search(const ProjPr
     wave_lds_fence();
     for (int p = lane; p < n; p += 64) pb.frame_mp[sk_idx(skey[p])] = claim_mp(sfmp[p]);
     if (st && lane == 0) st[4] = wall_clock64();
+}
+
+template <bool QLDS, bool DLDS, int NT, bool SPLIT = false>
+__global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restrict__ probs, ProjParams P,
+                                                    unsigned long long* __restrict__ scratch,
+                                                    const long long* __restrict__ scratch_off,
+                                                    unsigned char* __restrict__ grids, int gcap) {
+    proj_search_body<QLDS, DLDS, NT, SPLIT>(probs, P, scratch, scratch_off, grids, gcap);
+}
+
+// the sequence matcher's scoring form (beside the extraction lanes) with its register budget
+template <>
+__global__ __launch_bounds__(kProjThreads) ORBX_SCORE_ATTR void k_proj_search<false, false, kProjThreads, true>(
+    const ProjProblem* __restrict__ probs, ProjParams P, unsigned long long* __restrict__ scratch,
+    const long long* __restrict__ scratch_off, unsigned char* __restrict__ grids, int gcap) {
+    proj_search_body<false, false, kProjThreads, true>(probs, P, scratch, scratch_off, grids, gcap);
 }
 
 // ---- the batched sequence matcher in three launches (orbx_match_sequence_device)
