@@ -1801,21 +1801,22 @@ static size_t seq_commit_lds(int cap, int rt) {
     return (size_t)kTopK * rt * 4 + (size_t)cap * 8 + ORBX_EXP_COMMIT_LDS_PAD;
 }
 
-// Threads of the replay workgroup: `rt` if given (64, 256 or 1024), else ORBX_REPLAY_THREADS,
-// else 256 for a batch (four waves: configs[4] 93.4-94.2k -> 93.8-95.2k frames/s and
-// configs[1] 217.7-219.0k -> 222.3-223.8k against one wave; 1024 threads is slower in
-// both, its iterations cost more than the chains it shortens) and one wave for a single
+// Threads of the replay workgroup: `rt` if given (64, 128, 256, 512 or 1024), else
+// ORBX_REPLAY_THREADS, else 256 for a batch (four waves: configs[4] 93.4-94.2k -> 93.8-95.2k
+// frames/s and configs[1] 217.7-219.0k -> 222.3-223.8k against one wave; 1024 threads is
+// slower in both, its iterations cost more than the chains it shortens; r05q: 128 and 512
+// slower too, configs[4] 108.7-109.8k -> 105.7k / 104.9k) and one wave for a single
 // problem (the drop-in host calls: their scenes' conflict chains run across the whole
 // chunk, 90 iterations of ~1.9 us at 256 against 109 of ~1.2 us at 64 for a12).
 static int replay_threads(int rt, int nprob) {
-    if (rt != 64 && rt != 256 && rt != 1024) {
+    if (rt != 64 && rt != 128 && rt != 256 && rt != 512 && rt != 1024) {
         static const int env = [] {
             const char* v = getenv("ORBX_REPLAY_THREADS");
             return v ? atoi(v) : 0;
         }();
         rt = env;
     }
-    if (rt != 64 && rt != 256 && rt != 1024) rt = nprob == 1 ? 64 : 256;
+    if (rt != 64 && rt != 128 && rt != 256 && rt != 512 && rt != 1024) rt = nprob == 1 ? 64 : 256;
     return rt;
 }
 
@@ -1824,8 +1825,11 @@ static hipError_t launch_seq_commit(int rt, const ProjProblem* d_probs, int npro
                                     const long long* d_scratch_off, int use_sdesc, hipStream_t stream) {
     rt = replay_threads(rt, nprob);
     const size_t lds = seq_commit_lds(cap, rt);
-    const void* fn = rt == 64 ? (const void*)k_seq_commit<64>
-                              : (rt == 256 ? (const void*)k_seq_commit<256> : (const void*)k_seq_commit<1024>);
+    const void* fn = rt == 64    ? (const void*)k_seq_commit<64>
+                     : rt == 128 ? (const void*)k_seq_commit<128>
+                     : rt == 256 ? (const void*)k_seq_commit<256>
+                     : rt == 512 ? (const void*)k_seq_commit<512>
+                                 : (const void*)k_seq_commit<1024>;
     if (lds > 150 * 1024) return hipErrorInvalidValue;
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
