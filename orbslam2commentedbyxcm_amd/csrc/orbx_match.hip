@@ -717,16 +717,26 @@ __device__ void grid_sort(const ProjProblem& pb, unsigned* skey, unsigned* cnt) 
     __syncthreads();
 }
 
+// ORBX_SPLIT_SXY_GLOBAL=1: the sequence matcher's scoring form keeps the sorted keypoint
+// positions in its grid record in global memory (where k_seq_commit reads them) instead
+// of LDS -- 8 B per keypoint (40 KB at configs[4]) less LDS held beside the extraction
+// lanes.  Measured slower (r05r: configs[4] 106.6-108.5k -> 103.8-104.8k frames/s): the
+// scoring's own window reads cost more than the LDS frees.
+#ifndef ORBX_SPLIT_SXY_GLOBAL
+#define ORBX_SPLIT_SXY_GLOBAL 0
+#endif
+constexpr bool kSplitSxyGlobal = ORBX_SPLIT_SXY_GLOBAL != 0;
+
 // LDS layout of k_proj_search (byte offsets), shared by the kernel and its launcher.
 struct ProjLds {
     size_t skey, colstart, bstart, orun, sxy, sfmp, owner, sang, elist, sdesc, qk, qmp, qang, mlist, mbin, total;
-    __host__ __device__ ProjLds(int n, int nq, bool dlds, bool qlds, int noct, bool replay = true) {
+    __host__ __device__ ProjLds(int n, int nq, bool dlds, bool qlds, int noct, bool replay = true, bool xy = true) {
         skey = 0;
         colstart = align16((size_t)n * 4);
         bstart = align16(colstart + (size_t)(kGridCols + 1) * 2);
         orun = align16(bstart + (size_t)bucket_table_len(noct) * 2);
         sxy = align16(orun + (size_t)n * 2);
-        sfmp = sxy + (size_t)n * 8;
+        sfmp = sxy + (xy ? (size_t)n * 8 : 0);  // !xy: the positions live in global memory
         // the claims and the replay's owner map (neither without the replay: the split
         // scoring keeps a keypoint's initial claim as bit 31 of its sorted key)
         owner = sfmp + (replay ? (size_t)n * 4 : 0);
@@ -1455,12 +1465,19 @@ __device__ __forceinline__ void proj_search_body(const ProjProblem* __restrict__
     const int n = pb.n, nq = pb.nq;
     unsigned long long* st = P.stamps ? P.stamps + kStampWords * blockIdx.x : nullptr;
     if (st && tid == 0) st[0] = wall_clock64();
-    const ProjLds L(n, nq, DLDS, QLDS, P.noct, !SPLIT);
+    constexpr bool kXyGlobal = SPLIT && kSplitSxyGlobal;
+    const ProjLds L(n, nq, DLDS, QLDS, P.noct, !SPLIT, !kXyGlobal);
     unsigned* skey = (unsigned*)(smem + L.skey);
     uint16_t* colstart = (uint16_t*)(smem + L.colstart);
     uint16_t* bstart = (uint16_t*)(smem + L.bstart);
     uint16_t* orun = (uint16_t*)(smem + L.orun);
-    float2* sxy = (float2*)(smem + L.sxy);
+    float2* sxy;
+    if constexpr (kXyGlobal) {
+        const SeqGridLayout gl(gcap, P.noct);
+        sxy = (float2*)(grids + (size_t)blockIdx.x * gl.total + gl.sxy);
+    } else {
+        sxy = (float2*)(smem + L.sxy);
+    }
     int* sfmp = (int*)(smem + L.sfmp);
     int* owner = (int*)(smem + L.owner);
     float* sang = (float*)(smem + L.sang);
@@ -1583,7 +1600,7 @@ __device__ __forceinline__ void proj_search_body(const ProjProblem* __restrict__
         for (int p = tid; p < n; p += NT) {
             ((unsigned*)(gb + gl.skey))[p] = skey[p] & ~kKeyBlocked;
             ((uint16_t*)(gb + gl.orun))[p] = orun[p];
-            ((float2*)(gb + gl.sxy))[p] = sxy[p];
+            if (!kXyGlobal) ((float2*)(gb + gl.sxy))[p] = sxy[p];
             ((float*)(gb + gl.sang))[p] = ldg(&pb.keys[sk_idx(skey[p])].angle);
         }
         for (int t = tid; t < nb; t += NT) ((uint16_t*)(gb + gl.bstart))[t] = bstart[t];
@@ -2167,7 +2184,8 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
 #ifndef ORBX_EXP_SCORE_LDS_PAD
 #define ORBX_EXP_SCORE_LDS_PAD 0  // timing experiment: extra dynamic LDS per k_proj_search workgroup
 #endif
-    const size_t lds = ProjLds(max_n, max_nq, dlds, qlds, P.noct, split_grids == nullptr).total + ORBX_EXP_SCORE_LDS_PAD;
+    const size_t lds = ProjLds(max_n, max_nq, dlds, qlds, P.noct, split_grids == nullptr,
+                               !(split_grids && kSplitSxyGlobal)).total + ORBX_EXP_SCORE_LDS_PAD;
     if (lds > limit) return hipErrorInvalidValue;
     const void* fn;
     const int nt = tiny ? kProjThreadsTiny : (small ? kProjThreadsSmall : kProjThreads);
