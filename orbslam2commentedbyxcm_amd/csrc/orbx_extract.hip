@@ -1009,6 +1009,10 @@ __device__ __forceinline__ int get_q(const uint32_t* a, int nd, int q) {
 // FAST keypoints is flagged kStatusNodeOverflow.
 constexpr int kOctMaxKeys = 65535;
 constexpr int kOctStampWords = 16;  // diagnostics row per (frame, level), ORBX_OCT_STAMPS
+#ifndef ORBX_OCT_SPLIT_LEVELS
+#define ORBX_OCT_SPLIT_LEVELS 1  // batches: the small levels in a second k_octree launch (launch_extract)
+#endif
+constexpr bool kOctSplitLevels = ORBX_OCT_SPLIT_LEVELS != 0;
 constexpr int kOctNodeBytes = 4 + 8 + 8 + 4 + 2 + 4 + 16 + 2;  // best, ccnt, sa+sb, cnt x2 (u16), sc, crank x2, boxes, inV
 
 struct NodeBuf {
@@ -1039,7 +1043,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
                                                 int* __restrict__ kept_count, int* __restrict__ status,
                                                 int NC, int nframes, unsigned long long* __restrict__ stamps,
                                                 uint16_t* __restrict__ dt_list, uint32_t* __restrict__ dt_tile,
-                                                int tiles_pf) {
+                                                int tiles_pf, int l_first) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_tmp[8];
     __shared__ int s_scal[16];
@@ -1048,9 +1052,10 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
     __shared__ int s_map[kMaxIni];
     __shared__ int s_icnt[kMaxIni];
 
-    // Level-major order (all frames' level 0 first, then level 1, ...): the long level-0
-    // distributions start first and the short ones fill in behind them; frames keep their
-    // XCD (frame f on XCD f % 8) when nframes % 8 == 0.
+    // Level-major order (all frames' level l_first first, then the next level, ...): the
+    // long distributions start first and the short ones fill in behind them; frames keep
+    // their XCD (frame f on XCD f % 8) when nframes % 8 == 0.  A launch covers the levels
+    // l_first .. l_first + gridDim.x / nframes - 1.
     int f, l;
     {
         const int lin = blockIdx.x;
@@ -1062,6 +1067,7 @@ __global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__
             l = lin / nframes;
             f = lin - l * nframes;
         }
+        l += l_first;
     }
     const int tid = threadIdx.x;
     unsigned long long* st = stamps ? stamps + kOctStampWords * ((size_t)f * L + l) : nullptr;
@@ -2141,23 +2147,45 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     if (ev && ev[3]) (void)hipEventRecord(ev[3], stream);
     if (stage_ev && stage_after == 3) (void)hipEventRecord(stage_ev, stream);
     for (int rep = 0; rep < (dup == 4 ? 2 : 1); rep++) {
-        const int NC = (plan.max_ncap + 63) & ~63;
 #ifndef ORBX_EXP_OCT_LDS_PAD
 #define ORBX_EXP_OCT_LDS_PAD 0  // timing experiment: extra dynamic LDS per k_octree workgroup
 #endif
-        const size_t lds = (size_t)NC * kOctNodeBytes + ORBX_EXP_OCT_LDS_PAD;
-        // int16 node ids / ranks, and one workgroup's LDS (beside its static arrays)
-        if (NC > 32767 || lds > 152 * 1024) return hipErrorInvalidValue;
-        if (lds > 64 * 1024) {
-            const hipError_t e =
-                hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
+        // A launch's dynamic LDS is sized for its largest level.  For a batch whose level-0
+        // node table is large enough to limit the workgroups per CU (over 32 KB: fewer than
+        // the 5 its registers allow), the levels whose node capacity is at most 5/8 of level
+        // 0's go in a second launch sized for them (configs[4]: 27 KB instead of 46 KB for
+        // levels 3-11), so those workgroups hold less LDS beside the other kernels on their
+        // CU: configs[4] 107.2-109.2k -> 111.7-112.2k frames/s.  Below that the second
+        // launch only serialises the stage (configs[1] 226.5k -> 219.3k, KITTI -2.6 %; r05s).
+        int split = L;
+        const bool big = (size_t)((plan.max_ncap + 63) & ~63) * kOctNodeBytes > 32 * 1024;
+        if (batch >= 16 && big && !plan.desc_tiles && kOctSplitLevels)
+            for (int l = 1; l < L; l++)
+                if (plan.lv[l].ncap * 8 <= plan.lv[0].ncap * 5) {
+                    split = l;
+                    break;
+                }
+        for (int part = 0; part < 2; part++) {
+            const int la = part ? split : 0, lb = part ? L : split;
+            if (la >= lb) continue;
+            int mx = 0;
+            for (int l = la; l < lb; l++) mx = plan.lv[l].ncap > mx ? plan.lv[l].ncap : mx;
+            // the tile-major describe's bins need every level's tiles within NC (one launch)
+            const int NC = plan.desc_tiles ? (plan.max_ncap + 63) & ~63 : (mx + 63) & ~63;
+            const size_t lds = (size_t)NC * kOctNodeBytes + ORBX_EXP_OCT_LDS_PAD;
+            // int16 node ids / ranks, and one workgroup's LDS (beside its static arrays)
+            if (NC > 32767 || lds > 152 * 1024) return hipErrorInvalidValue;
+            if (lds > 64 * 1024) {
+                const hipError_t e =
+                    hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                if (e != hipSuccess) return e;
+            }
+            dim3 grid((lb - la) * batch);
+            hipLaunchKernelGGL(k_octree, grid, dim3(256), lds, stream, db.lv, L, db.slots, plan.slots_per_frame,
+                               db.cells, db.cell_count, ncells, db.keys, db.key_node, plan.keys_per_frame,
+                               db.kept, plan.kept_per_frame, db.kept_count, db.status, NC, batch, db.oct_stamps,
+                               plan.desc_tiles ? db.dt_list : nullptr, db.dt_tile, plan.tiles_total, la);
         }
-        dim3 grid(L * batch);
-        hipLaunchKernelGGL(k_octree, grid, dim3(256), lds, stream, db.lv, L, db.slots, plan.slots_per_frame,
-                           db.cells, db.cell_count, ncells, db.keys, db.key_node, plan.keys_per_frame,
-                           db.kept, plan.kept_per_frame, db.kept_count, db.status, NC, batch, db.oct_stamps,
-                           plan.desc_tiles ? db.dt_list : nullptr, db.dt_tile, plan.tiles_total);
     }
     if (ev && ev[4]) (void)hipEventRecord(ev[4], stream);
     if (stage_ev && stage_after == 4) (void)hipEventRecord(stage_ev, stream);

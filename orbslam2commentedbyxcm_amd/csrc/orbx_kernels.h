@@ -27,7 +27,7 @@ struct DeviceBuffers {
     uint16_t* dt_list = nullptr;     // [B][kept_per_frame] kept slots listed tile after tile (k_describe_tiles)
     uint32_t* dt_tile = nullptr;     // [B][tiles_total] per level tile: list start << 16 | count
     int* status = nullptr;           // [B] error flags
-    unsigned long long* oct_stamps = nullptr;  // [B][L][8] k_octree phase stamps (ORBX_OCT_STAMPS)
+    unsigned long long* oct_stamps = nullptr;  // [B][L][16] k_octree phase stamps (ORBX_OCT_STAMPS)
 };
 
 // Kernel status bits (DeviceBuffers::status)
