@@ -1013,6 +1013,10 @@ constexpr int kOctStampWords = 16;  // diagnostics row per (frame, level), ORBX_
 #define ORBX_OCT_SPLIT_LEVELS 1  // batches: the small levels in a second k_octree launch (launch_extract)
 #endif
 constexpr bool kOctSplitLevels = ORBX_OCT_SPLIT_LEVELS != 0;
+#ifndef ORBX_OCT_SPLIT_NUM  // the second launch takes the levels with ncap <= NUM / DEN of level 0's
+#define ORBX_OCT_SPLIT_NUM 3
+#define ORBX_OCT_SPLIT_DEN 8
+#endif
 constexpr int kOctNodeBytes = 4 + 8 + 8 + 4 + 2 + 4 + 16 + 2;  // best, ccnt, sa+sb, cnt x2 (u16), sc, crank x2, boxes, inV
 
 struct NodeBuf {
@@ -2152,16 +2156,18 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
 #endif
         // A launch's dynamic LDS is sized for its largest level.  For a batch whose level-0
         // node table is large enough to limit the workgroups per CU (over 32 KB: fewer than
-        // the 5 its registers allow), the levels whose node capacity is at most 5/8 of level
-        // 0's go in a second launch sized for them (configs[4]: 27 KB instead of 46 KB for
-        // levels 3-11), so those workgroups hold less LDS beside the other kernels on their
-        // CU: configs[4] 107.2-109.2k -> 111.7-112.2k frames/s.  Below that the second
+        // the 5 its registers allow), the levels whose node capacity is at most 3/8 of level
+        // 0's go in a second launch sized for them (configs[4]: levels 6-11 at 15 KB instead
+        // of 46 KB), so those workgroups hold less LDS beside the other kernels on their CU:
+        // configs[4] 107.4-108.9k -> 114.8-115.2k frames/s.  Splitting earlier leaves the
+        // first launch too few workgroups to cover its tail (after level 1: 102.6k; after 3:
+        // 111.4-112.0k; after 4: 113.2-114.5k; r05t-v).  Without a large table the second
         // launch only serialises the stage (configs[1] 226.5k -> 219.3k, KITTI -2.6 %; r05s).
         int split = L;
         const bool big = (size_t)((plan.max_ncap + 63) & ~63) * kOctNodeBytes > 32 * 1024;
         if (batch >= 16 && big && !plan.desc_tiles && kOctSplitLevels)
             for (int l = 1; l < L; l++)
-                if (plan.lv[l].ncap * 8 <= plan.lv[0].ncap * 5) {
+                if (plan.lv[l].ncap * ORBX_OCT_SPLIT_DEN <= plan.lv[0].ncap * ORBX_OCT_SPLIT_NUM) {
                     split = l;
                     break;
                 }
