@@ -306,6 +306,12 @@ __device__ void build_octave_runs(const unsigned* skey, const uint16_t* colstart
 constexpr int kProjThreads = 1024;      // default workgroup size of k_proj_search
 constexpr int kProjThreadsSmall = 256;  // small-footprint variant (overlapped with other work)
 constexpr int kProjThreadsTiny = 64;    // one wave per problem (a background stream's footprint)
+#ifndef ORBX_SPLIT_SCORE_THREADS
+#define ORBX_SPLIT_SCORE_THREADS 1024
+#endif
+// the sequence matcher's scoring workgroup (r05w: 512 threads within noise at configs[1],
+// configs[4] 113.6-115.4k -> 106.1-107.0k frames/s)
+constexpr int kSplitScoreThreads = ORBX_SPLIT_SCORE_THREADS;
 constexpr int kTopK = ORBX_TOPK;
 #ifndef ORBX_LANE_TOPK
 #define ORBX_LANE_TOPK 6
@@ -1626,10 +1632,10 @@ __global__ __launch_bounds__(NT) void k_proj_search(const ProjProblem* __restric
 
 // the sequence matcher's scoring form (beside the extraction lanes) with its register budget
 template <>
-__global__ __launch_bounds__(kProjThreads) ORBX_SCORE_ATTR void k_proj_search<false, false, kProjThreads, true>(
+__global__ __launch_bounds__(kSplitScoreThreads) ORBX_SCORE_ATTR void k_proj_search<false, false, kSplitScoreThreads, true>(
     const ProjProblem* __restrict__ probs, ProjParams P, unsigned long long* __restrict__ scratch,
     const long long* __restrict__ scratch_off, unsigned char* __restrict__ grids, int gcap) {
-    proj_search_body<false, false, kProjThreads, true>(probs, P, scratch, scratch_off, grids, gcap);
+    proj_search_body<false, false, kSplitScoreThreads, true>(probs, P, scratch, scratch_off, grids, gcap);
 }
 
 // ---- the batched sequence matcher in three launches (orbx_match_sequence_device)
@@ -2188,13 +2194,13 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
                                !(split_grids && kSplitSxyGlobal)).total + ORBX_EXP_SCORE_LDS_PAD;
     if (lds > limit) return hipErrorInvalidValue;
     const void* fn;
-    const int nt = tiny ? kProjThreadsTiny : (small ? kProjThreadsSmall : kProjThreads);
+    const int nt = tiny ? kProjThreadsTiny : (small ? kProjThreadsSmall : (split_grids ? kSplitScoreThreads : kProjThreads));
     if (tiny)
         fn = (const void*)k_proj_search<false, false, kProjThreadsTiny>;
     else if (small)
         fn = (const void*)k_proj_search<false, false, kProjThreadsSmall>;
     else if (split_grids)
-        fn = (const void*)k_proj_search<false, false, kProjThreads, true>;
+        fn = (const void*)k_proj_search<false, false, kSplitScoreThreads, true>;
     else
         fn = qlds ? (dlds ? (const void*)k_proj_search<true, true, kProjThreads>
                           : (const void*)k_proj_search<true, false, kProjThreads>)
