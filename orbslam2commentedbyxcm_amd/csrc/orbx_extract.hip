@@ -736,14 +736,27 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
 // the non-zero pixels in raster order (one ballot per row -- per row pair when the window
 // is at most 32 wide), tests only those against their neighbours, and writes the
 // survivors of the chosen threshold in the same order.
-constexpr int kFcStride = 68;  // staged window row pitch (64 + zero frame, bank spread)
+// Staged window row pitch: 68 bytes (64 + zero frame, an odd dword count).  ORBX_FC_TIGHT=1
+// sizes it to the widest window instead (36 bytes at 30-px cells, 4.4 KB less LDS per
+// workgroup; 16 KB more costs configs[1] 9 %, r05ab) -- and measured slower: configs[4]
+// 113.7-113.9k -> 106.3-107.4k frames/s, configs[1] within noise (r05ac).
+#ifndef ORBX_FC_TIGHT
+#define ORBX_FC_TIGHT 0
+#endif
+static int fast_cells_stride(int max_wc) {
+    if (!ORBX_FC_TIGHT) return 68;
+    int d = (max_wc + 2 + 3) / 4;
+    if (!(d & 1)) d++;
+    return 4 * d;
+}
 
 __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ score, long long fb,
                                                     const CellGeom* __restrict__ cells, int ncells,
                                                     int ini_th, int min_th, uint32_t* __restrict__ slots,
                                                     int slots_pf, int* __restrict__ cell_count, int nframes,
-                                                    int max_wr, int max_wc) {
-    // per wave: (max_wr + 2) framed rows of M, then a candidate list of max_wr*max_wc u16
+                                                    int max_wr, int max_wc, int kFcStride) {
+    // per wave: (max_wr + 2) framed rows of M (pitch kFcStride >= max_wc + 2), then a
+    // candidate list of max_wr*max_wc u16
     extern __shared__ __align__(16) uint8_t s_dyn[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int per_wave = (((max_wr + 2) * kFcStride + 2 * max_wr * max_wc) + 15) & ~15;
@@ -762,12 +775,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
         uint8_t* m = s_dyn + wave * per_wave;  // m[(r + 1) * kFcStride + c + 1] = M(r, c)
         uint16_t* list = (uint16_t*)(s_dyn + wave * per_wave + (max_wr + 2) * kFcStride);
         const unsigned long long below = (1ull << lane) - 1;
-        // zero frame: rows -1 and wr, column -1 (columns >= wc are written as 0 below)
-        m[lane] = 0;
-        m[(wr + 1) * kFcStride + lane] = 0;
-        if (lane < 4) {
-            m[64 + lane] = 0;
-            m[(wr + 1) * kFcStride + 64 + lane] = 0;
+        // zero frame: rows -1 and wr, column -1 (column wc is written as 0 below)
+        for (int i = lane; i < kFcStride; i += 64) {
+            m[i] = 0;
+            m[(wr + 1) * kFcStride + i] = 0;
         }
         for (int r = lane; r < wr + 2; r += 64) {  // columns -1 and wc
             m[r * kFcStride] = 0;
@@ -796,7 +807,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
                 const int rb = r0 + k * rstep;  // first row of this step (wave-uniform)
                 if (rb < wr) {
                     const int r = rb + half;
-                    if (r < wr) m[(r + 1) * kFcStride + col + 1] = (uint8_t)v[k];
+                    if (r < wr && col <= wc) m[(r + 1) * kFcStride + col + 1] = (uint8_t)v[k];
                     const unsigned long long b = __ballot(v[k] > tc);  // raster order: row rb, then rb+1
                     if ((b >> lane) & 1ull) list[n + __popcll(b & below)] = (uint16_t)((r << 8) | col);
                     n += __popcll(b);
@@ -2143,10 +2154,15 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     if (stage_ev && stage_after == 2) (void)hipEventRecord(stage_ev, stream);
     for (int rep = 0; rep < (dup == 3 ? 2 : 1); rep++) {
         dim3 grid(((ncells + 3) / 4) * batch);
-        const size_t fc_lds = 4 * (size_t)((((plan.fc_wr + 2) * kFcStride + 2 * plan.fc_wr * plan.fc_wc) + 15) & ~15);
+#ifndef ORBX_EXP_FC_LDS_PAD
+#define ORBX_EXP_FC_LDS_PAD 0  // timing experiment: extra dynamic LDS per k_fast_cells workgroup
+#endif
+        const int fcs = fast_cells_stride(plan.fc_wc);
+        const size_t fc_lds = 4 * (size_t)((((plan.fc_wr + 2) * fcs + 2 * plan.fc_wr * plan.fc_wc) + 15) & ~15) +
+                              ORBX_EXP_FC_LDS_PAD;
         hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), fc_lds, stream, db.score, fb, db.cells, ncells,
                            plan.prm.ini_th, plan.prm.min_th, db.slots, plan.slots_per_frame, db.cell_count, batch,
-                           plan.fc_wr, plan.fc_wc);
+                           plan.fc_wr, plan.fc_wc, fcs);
     }
     if (ev && ev[3]) (void)hipEventRecord(ev[3], stream);
     if (stage_ev && stage_after == 3) (void)hipEventRecord(stage_ev, stream);
@@ -2204,7 +2220,10 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
         } else {
             dim3 grid(((plan.kept_per_frame + 15) / 16) * batch);
             auto kern = plan.kept_per_frame <= kDescGldsMaxSlots ? k_describe<ORBX_DESC_DMA> : k_describe<0>;
-            hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, db.pyr, db.blur, fb, db.lv, L, db.kept,
+#ifndef ORBX_EXP_DESC_LDS_PAD
+#define ORBX_EXP_DESC_LDS_PAD 0  // timing experiment: extra dynamic LDS per k_describe workgroup
+#endif
+            hipLaunchKernelGGL(kern, grid, dim3(256), ORBX_EXP_DESC_LDS_PAD, stream, db.pyr, db.blur, fb, db.lv, L, db.kept,
                                plan.kept_per_frame, db.kept_count, (orbx_keypoint*)kps, desc, cap, n_per_frame, batch,
                                l0, l0_fp, l0_pitch, db.status, status_out);
         }
