@@ -1049,7 +1049,10 @@ struct NodeBuf {
 //    node first;
 //  * each surviving node keeps its max-response key, first (lowest index) on ties
 //    (cc:984-1009).
-__global__ __launch_bounds__(256, 5) void k_octree(const LevelGeom* __restrict__ lv, int L,
+#ifndef ORBX_OCT_WPE
+#define ORBX_OCT_WPE 5  // k_octree's register budget: waves per SIMD (5: <= 102 VGPRs)
+#endif
+__global__ __launch_bounds__(256, ORBX_OCT_WPE) void k_octree(const LevelGeom* __restrict__ lv, int L,
                                                 const uint32_t* __restrict__ slots, int slots_pf,
                                                 const CellGeom* __restrict__ cells,
                                                 const int* __restrict__ cell_count, int ncells_total,

@@ -1436,12 +1436,12 @@ __device__ __forceinline__ SortedGrid seq_grid(unsigned char* base, const SeqGri
 // sorted descriptors) and k_seq_commit replays with one wave and a small LDS footprint.
 // Register budgets (waves per SIMD) of the batched sequence matcher's two kernels, which run
 // beside the extraction lanes: every VGPR they hold for their whole launch is one the
-// extraction's waves on that SIMD cannot have.  0: the compiler's choice.  The scoring
-// kernel at 5 (96 VGPRs, 20 B of spill, against 100): configs[4] 107.3-108.6k ->
-// 109.5-109.7k frames/s, configs[1] +0.1-0.3 %; 6 and 8 (more spills) and the commit at
-// 3 or 4 measured slower (r05p, interleaved on one box).
+// extraction's waves on that SIMD cannot have.  0: the compiler's choice (100 VGPRs for
+// the scoring kernel).  The scoring kernel at 5 (96 VGPRs, 20 B of spill) measured +1-2 %
+// at configs[4] before the octree split (r05p) and within noise after it (r05af); 6 and 8
+// (more spills) and the commit at 3 or 4 measured slower (r05p).
 #ifndef ORBX_SCORE_WPE
-#define ORBX_SCORE_WPE 5
+#define ORBX_SCORE_WPE 0
 #endif
 #ifndef ORBX_COMMIT_WPE
 #define ORBX_COMMIT_WPE 0
