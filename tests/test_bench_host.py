@@ -277,3 +277,17 @@ def test_pmc_valu_reads_the_workload_file(tmp_path, monkeypatch):
 def test_source_hash_tracks_the_sources():
     h = bench.source_hash()
     assert len(h) == 16 and h == bench.source_hash()
+
+
+def test_exchange_leg_arguments():
+    # the N-GPU headline's keyframe-exchange leg: euroc_bench.parse / run as bench.py calls them
+    sys.path.insert(0, str(ROOT / "tests"))
+    import inspect
+
+    import euroc_bench
+    a = euroc_bench.parse(["--steps", "10", "--warmup", "3", "--no-cpu-baseline"])
+    assert (a.steps, a.warmup, a.batch, a.nn, a.no_cpu_baseline, a.parity_frames) == (10, 3, 64, 10, True, -1)
+    assert list(inspect.signature(euroc_bench.run).parameters) == ["args", "rank", "world", "local_rank", "collective"]
+    src = (ROOT / "bench.py").read_text()
+    assert '"--no-exchange"' in src and "euroc_bench.run(eargs, rank, world, gpu, True)" in src
+    assert '"keyframe_exchange": exchange' in src
