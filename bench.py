@@ -420,7 +420,7 @@ def selftest_launch(args, rank, world, local_rank):
 def main():
     # Secondary workloads and measurements (their implementations live under tests/: they
     # run the oracle as parity check and CPU baseline).
-    for flag, mod in (("--vocab", "vocab_bench"), ("--rows", "row_bench")):
+    for flag, mod in (("--vocab", "vocab_bench"), ("--rows", "row_bench"), ("--dropin", "dropin_bench")):
         if flag in sys.argv[1:]:
             sys.path.insert(0, str(ROOT / "tests"))
             return __import__(mod).main([a for a in sys.argv[1:] if a != flag])
