@@ -743,8 +743,11 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
 #ifndef ORBX_FC_TIGHT
 #define ORBX_FC_TIGHT 0
 #endif
+#ifndef ORBX_FC_PITCH  // r05al / r05am: 44-100 bytes all measured slower than 68 at configs[4] (up to -8 %)
+#define ORBX_FC_PITCH 68
+#endif
 static int fast_cells_stride(int max_wc) {
-    if (!ORBX_FC_TIGHT) return 68;
+    if (!ORBX_FC_TIGHT) return ORBX_FC_PITCH > max_wc + 2 ? ORBX_FC_PITCH : 68;
     int d = (max_wc + 2 + 3) / 4;
     if (!(d & 1)) d++;
     return 4 * d;
