@@ -252,7 +252,13 @@ class StereoKeyFramePipeline:
         # beside the stereo matching and BoW of step j + 1 instead of after them
         self._own_ts = stream_create(device, 1)
         self.ts = torch.cuda.ExternalStream(self._own_ts, device=self.dev)
-        self.sets = [(ORBextractor(*prm, device=device), ORBextractor(*prm, device=device)) for _ in range(2)]
+        # extractor pairs / slabs in rotation: a set is rewritten only after the triangulation
+        # that last read it (ev_m), so with two sets step j+1's extraction waited for step
+        # j-1's triangulation -- the GPU idled between the steps' extractions.  Three sets
+        # give that triangulation a whole step of slack (ORBX_KF_SETS=2: round 4's rotation)
+        self.nsets = max(2, int(os.environ.get("ORBX_KF_SETS", "3")))
+        self.sets = [(ORBextractor(*prm, device=device), ORBextractor(*prm, device=device))
+                     for _ in range(self.nsets)]
         self.sf = self.sets[0][0].GetScaleFactors()
         self.cap = self.sets[0][0].max_keypoints(self.W, self.H)
         self.stereo = ORBmatcher(0.6, True, device=device)
@@ -266,25 +272,25 @@ class StereoKeyFramePipeline:
         self.lay = SlabLayout(self.B, self.cap)
         u8 = dict(dtype=torch.uint8, device=self.dev)
         i32 = dict(dtype=torch.int32, device=self.dev)
-        self.slabs = [torch.zeros(self.lay.nbytes, **u8) for _ in range(2)]
+        self.slabs = [torch.zeros(self.lay.nbytes, **u8) for _ in range(self.nsets)]
         self.sv = [self.lay.views(sl) for sl in self.slabs]
         self.right = [{"kps": torch.empty((self.B, self.cap, 7), **i32),
                        "desc": torch.empty((self.B, self.cap, 32), **u8),
                        "n": torch.empty((self.B,), **i32),
                        "depth": torch.empty((self.B, self.cap), dtype=torch.float32, device=self.dev)}
-                      for _ in range(2)]
+                      for _ in range(self.nsets)]
         self.bow = [{"bow_word": torch.empty((self.B, self.cap), **i32),
                      "bow_value": torch.empty((self.B, self.cap), dtype=torch.float64, device=self.dev),
-                     "nbow": torch.empty((self.B,), **i32)} for _ in range(2)]
+                     "nbow": torch.empty((self.B,), **i32)} for _ in range(self.nsets)]
         # one gathered buffer per set: step j+1's all-gather (set k') must not overwrite the
         # neighbours step j's triangulation (set k) is reading on the other stream
-        self.gathered = [torch.zeros(self.world * self.lay.nbytes, **u8) for _ in range(2)] \
+        self.gathered = [torch.zeros(self.world * self.lay.nbytes, **u8) for _ in range(self.nsets)] \
             if self.collective else None
         self.plan = plan_neighbours(self.poses, self.rank, self.world, self.B, nn, self.mb, s)
         P = max(len(self.plan.pairs), 1)
-        self.m12 = [torch.empty((P, self.cap), **i32) for _ in range(2)]
-        self.tri_pairs = [torch.empty((P, self.cap, 2), **i32) for _ in range(2)]
-        self.tri_n = [torch.empty((P,), **i32) for _ in range(2)]
+        self.m12 = [torch.empty((P, self.cap), **i32) for _ in range(self.nsets)]
+        self.tri_pairs = [torch.empty((P, self.cap, 2), **i32) for _ in range(self.nsets)]
+        self.tri_n = [torch.empty((P,), **i32) for _ in range(self.nsets)]
         win_poses = [None] * (self.world * self.B)
         for g in range(self.world * self.B):
             win_poses[record_index(g, self.world, self.B)] = self.poses[g]
@@ -295,12 +301,12 @@ class StereoKeyFramePipeline:
                              max_y=float(self.H), scale_factors=self.sf, level_sigma2=self.sf * self.sf)
         self.streams = [(torch.cuda.ExternalStream(a.stream_handle(), device=self.dev),
                          torch.cuda.ExternalStream(b.stream_handle(), device=self.dev)) for a, b in self.sets]
-        self.ev_l = [torch.cuda.Event() for _ in range(2)]
-        self.ev_r = [torch.cuda.Event() for _ in range(2)]
-        self.ev_m = [torch.cuda.Event() for _ in range(2)]
-        self.ev_s = [torch.cuda.Event() for _ in range(2)]  # stereo + BoW (+ all-gather) of a set done
-        self.used = [False, False]
-        self.window_of = [0, 0]  # the window each set last held
+        self.ev_l = [torch.cuda.Event() for _ in range(self.nsets)]
+        self.ev_r = [torch.cuda.Event() for _ in range(self.nsets)]
+        self.ev_m = [torch.cuda.Event() for _ in range(self.nsets)]
+        self.ev_s = [torch.cuda.Event() for _ in range(self.nsets)]  # stereo + BoW (+ all-gather) of a set done
+        self.used = [False] * self.nsets
+        self.window_of = [0] * self.nsets  # the window each set last held
         # on_step_done(k): called after a step's triangulation is enqueued on self.ts and
         # before the event that releases set k -- consumer work enqueued on self.ts there
         # (e.g. copying the results out) finishes before the set is reused
@@ -337,7 +343,7 @@ class StereoKeyFramePipeline:
         """Issue one step (asynchronous)."""
         import torch
 
-        k = self.it % 2
+        k = self.it % self.nsets
         (exl, exr), (sl, sr) = self.sets[k], self.streams[k]
         v, rt, bw = self.sv[k], self.right[k], self.bow[k]
         if self.used[k]:  # the work that last read this set's pyramids, slab and gathered buffer is done
