@@ -52,7 +52,13 @@ class StereoSequencePipeline:
         # 
         self._own_ms = stream_create(device, 1, 0)
         self.ms = torch.cuda.ExternalStream(self._own_ms, device=self.dev)
-        self.sets = [(ORBextractor(*params, device=device), ORBextractor(*params, device=device)) for _ in range(2)]
+        # extractor pairs in rotation: a set is re-extracted only after the matching that last
+        # read it (ev_m).  Two: here the matching keeps up with the extraction, and a third
+        # set (ORBX_STEREO_SETS=3, which helps the keyframe stream) measured 0.8 % slower (r05ap)
+        import os
+        self.nsets = max(2, int(os.environ.get("ORBX_STEREO_SETS", "2")))
+        self.sets = [(ORBextractor(*params, device=device), ORBextractor(*params, device=device))
+                     for _ in range(self.nsets)]
         self.smatcher = ORBmatcher(0.6, True, device=device)  # ComputeStereoMatches' handle (stream, arena)
         self.tmatcher = ORBmatcher(nnratio, check_ori, device=device)  # TrackWithMotionModel: ORBmatcher(0.9, true)
         self.tmatcher.set_footprint(5 if matcher_mode is None else matcher_mode)
@@ -67,13 +73,13 @@ class StereoSequencePipeline:
                      "dr": torch.empty((B, cap, 32), **u8), "nr": torch.empty((B,), **i32),
                      "ur": torch.empty((B, cap), **f32), "dp": torch.empty((B, cap), **f32),
                      "mp": torch.empty((B, cap), **i32), "nm": torch.empty((B,), **i32),
-                     **last_frame_table(B, cap, self.dev)} for _ in range(2)]
+                     **last_frame_table(B, cap, self.dev)} for _ in range(self.nsets)]
         self.streams = [(torch.cuda.ExternalStream(a.stream_handle(), device=self.dev),
                          torch.cuda.ExternalStream(c.stream_handle(), device=self.dev)) for a, c in self.sets]
-        self.ev_l = [torch.cuda.Event() for _ in range(2)]
-        self.ev_r = [torch.cuda.Event() for _ in range(2)]
-        self.ev_m = [torch.cuda.Event() for _ in range(2)]
-        self.used = [False, False]
+        self.ev_l = [torch.cuda.Event() for _ in range(self.nsets)]
+        self.ev_r = [torch.cuda.Event() for _ in range(self.nsets)]
+        self.ev_m = [torch.cuda.Event() for _ in range(self.nsets)]
+        self.used = [False] * self.nsets
         self.it = 0
         self.last = None
         self._timing = False
@@ -99,7 +105,7 @@ class StereoSequencePipeline:
         or None.  Inputs must stay untouched until the step's matching is done."""
         import torch
 
-        k = self.it % 2
+        k = self.it % self.nsets
         (exl, exr), (sl, sr), bk = self.sets[k], self.streams[k], self.buf[k]
         if self.used[k]:  # the matching that last read this set's pyramids is done
             sl.wait_event(self.ev_m[k])
