@@ -406,9 +406,15 @@ class StereoKeyFramePipeline:
         self.tri.set_timing(enable)
 
     def stage_times(self) -> dict:
-        """HIP-event ms per launch: extraction stages averaged over the four extractors
-        (L and R of both sets), the stereo matching and the triangulation."""
-        per = [e.stage_times() for st in self.sets for e in st]
+        """HIP-event ms per launch: extraction stages averaged over the extractors (L and R
+        of every set) that ran a timed extraction, the stereo matching and the triangulation."""
+        from ._lib import OrbxError
+        per = []
+        for e in (e for st in self.sets for e in st):
+            try:
+                per.append(e.stage_times())
+            except OrbxError:  # a set not reached by the timed steps (fewer steps than sets)
+                pass
         st = {k: sum(p[k] for p in per) / len(per) for k in per[0]}
         st["stereo"] = self.stereo.last_ms()
         if len(self.plan.pairs):

@@ -175,7 +175,13 @@ class StereoSequencePipeline:
     def stage_times(self) -> dict:
         """HIP-event ms per launch: the extraction stages (averaged over every extractor's
         launches, left and right), "stereo" and "track" (UpdateLastFrame + the search)."""
-        per = [e.stage_times() for st in self.sets for e in st]
+        from ._lib import OrbxError
+        per = []
+        for e in (e for st in self.sets for e in st):
+            try:
+                per.append(e.stage_times())
+            except OrbxError:  # a set not reached by the timed steps (fewer steps than sets)
+                pass
         out = {s: sum(p[s] for p in per) / len(per) for s in per[0]}
         if self._st:
             out["stereo"] = sum(a.elapsed_time(b) for a, b, _ in self._st) / len(self._st)
