@@ -262,29 +262,29 @@ def main(argv=None):
         print(json.dumps(out), flush=True)
 
 
-def run(args, rank: int, world: int, local_rank: int, collective: bool):
-    """The configs[3] step on this rank (the process group, when collective, is already
-    up): warmup, the timed steps (max over ranks), rank 0's parity and bench line (None
-    on the other ranks).  bench.py's headline run calls it at world size > 1 for its
-    keyframe-exchange leg."""
+def run(args, rank: int, world: int, device: int, collective: bool):
+    """The configs[3] step on this rank, on GPU `device` (the process group, when
+    collective, is already up): warmup, the timed steps (max over ranks), rank 0's parity
+    and bench line (None on the other ranks).  bench.py's headline run calls it at world
+    size > 1 for its keyframe-exchange leg."""
     import torch
     import torch.distributed as dist
 
     from orbslam2commentedbyxcm_amd import ORBextractor, synth
     from orbslam2commentedbyxcm_amd.keyframes import EUROC, StereoKeyFramePipeline
 
-    dev = torch.device("cuda", local_rank)
+    dev = torch.device("cuda", device)
     B = args.batch
     s = EUROC
     # the vocabulary's level-1 centres come from the stream's first left view (same on every rank)
     seq0 = synth.StereoSequence(3, 1, s["width"], s["height"], step=16, margin=256, disp=13)
-    ex0 = ORBextractor(s["nfeatures"], s["scale"], s["nlevels"], s["ini_th"], s["min_th"], device=local_rank)
+    ex0 = ORBextractor(s["nfeatures"], s["scale"], s["nlevels"], s["ini_th"], s["min_th"], device=device)
     _, d0 = ex0(seq0.views([0])[0][0])
     del ex0
     t0 = time.perf_counter()
     text = synth.vocabulary_text(7, 10, 6, 0, 0, centres=d0)
     gen_s = time.perf_counter() - t0
-    pl = StereoKeyFramePipeline(B, rank, world, device=local_rank, nn=args.nn, vocab_text=text,
+    pl = StereoKeyFramePipeline(B, rank, world, device=device, nn=args.nn, vocab_text=text,
                                 collective=collective)
 
     def barrier():

@@ -287,7 +287,7 @@ def test_exchange_leg_arguments():
     import euroc_bench
     a = euroc_bench.parse(["--steps", "10", "--warmup", "3", "--no-cpu-baseline"])
     assert (a.steps, a.warmup, a.batch, a.nn, a.no_cpu_baseline, a.parity_frames) == (10, 3, 64, 10, True, -1)
-    assert list(inspect.signature(euroc_bench.run).parameters) == ["args", "rank", "world", "local_rank", "collective"]
+    assert list(inspect.signature(euroc_bench.run).parameters) == ["args", "rank", "world", "device", "collective"]
     src = (ROOT / "bench.py").read_text()
     assert '"--no-exchange"' in src and "euroc_bench.run(eargs, rank, world, gpu, True)" in src
     assert '"keyframe_exchange": exchange' in src
