@@ -818,6 +818,12 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
             }
         }
         wave_lds_fence();
+#ifdef ORBX_EXP_FC_STAGE_ONLY  // timing ablation only: staging and listing, no test or write-out
+        if (n >= 0) {
+            if (lane == 0) cell_count[(size_t)f * ncells + ci] = 0;  // no keypoints: later stages stay in bounds
+            return;
+        }
+#endif
         // neighbour test of the candidates (zero frame: no bounds checks), both thresholds
         auto keep_of = [&](int i, int& r, int& cc, int& M) -> bool {
             const int rc = list[i];
