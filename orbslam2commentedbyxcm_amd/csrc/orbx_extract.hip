@@ -743,6 +743,10 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
 #ifndef ORBX_FC_TIGHT
 #define ORBX_FC_TIGHT 0
 #endif
+#ifndef ORBX_FC_INFLIGHT
+#define ORBX_FC_INFLIGHT 8  // k_fast_cells: row steps of byte loads in flight (r05aw: 4 -2 %,
+                            // 16 -10 % at configs[1])
+#endif
 #ifndef ORBX_FC_PITCH  // r05al / r05am: 44-100 bytes all measured slower than 68 at configs[4] (up to -8 %)
 #define ORBX_FC_PITCH 68
 #endif
@@ -799,14 +803,19 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
         // has slack); the values are masked.  The row part of each offset is wave-uniform
         // (scalar adds to the base), the lane part a 32-bit vector offset.
         const uint32_t loff = (uint32_t)(half * c.pitch + col);
-        for (int r0 = 0; r0 < wr; r0 += 8 * rstep) {
-            int v[8];
+        constexpr int kIF = ORBX_FC_INFLIGHT;  // row steps of loads in flight
+        for (int r0 = 0; r0 < wr; r0 += kIF * rstep) {
+            int v[kIF];
 #pragma unroll
-            for (int k = 0; k < 8; k++) v[k] = src[(uint32_t)((r0 + k * rstep) * c.pitch) + loff];
+            for (int k = 0; k < kIF; k++) {
+                // more than 8 steps: rows clamped to the window (at most one row past it)
+                const int rk = kIF > 8 ? min(r0 + k * rstep, wr - 1) : r0 + k * rstep;
+                v[k] = src[(uint32_t)(rk * c.pitch) + loff];
+            }
 #pragma unroll
-            for (int k = 0; k < 8; k++) v[k] = (act && r0 + k * rstep + half < wr) ? v[k] : 0;
+            for (int k = 0; k < kIF; k++) v[k] = (act && r0 + k * rstep + half < wr) ? v[k] : 0;
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
+            for (int k = 0; k < kIF; k++) {
                 const int rb = r0 + k * rstep;  // first row of this step (wave-uniform)
                 if (rb < wr) {
                     const int r = rb + half;
