@@ -254,9 +254,11 @@ class StereoKeyFramePipeline:
         self.ts = torch.cuda.ExternalStream(self._own_ts, device=self.dev)
         # extractor pairs / slabs in rotation: a set is rewritten only after the triangulation
         # that last read it (ev_m), so with two sets step j+1's extraction waited for step
-        # j-1's triangulation -- the GPU idled between the steps' extractions.  Three sets
-        # give that triangulation a whole step of slack (ORBX_KF_SETS=2: round 4's rotation)
-        self.nsets = max(2, int(os.environ.get("ORBX_KF_SETS", "3")))
+        # j-1's triangulation -- the GPU idled between the steps' extractions.  Four sets
+        # give it slack (r05ao-az, interleaved: two 48.6-49.6k, three 49.0-50.2k, four
+        # 54.4-55.2k, five 52.8-54.5k, six and eight 50-52k keyframes/s: beyond four the
+        # eight extractor streams outnumber the hardware queues).  ORBX_KF_SETS overrides.
+        self.nsets = max(2, int(os.environ.get("ORBX_KF_SETS", "4")))
         self.sets = [(ORBextractor(*prm, device=device), ORBextractor(*prm, device=device))
                      for _ in range(self.nsets)]
         self.sf = self.sets[0][0].GetScaleFactors()
