@@ -19,11 +19,11 @@ One step on every rank = for its B stereo keyframes of a W*B-keyframe window:
    (ComputeF12, cc:606-625) and SearchForTriangulation (ORBmatcher.cc:850-1056) of every
    pair in one launch (orbx_search_for_triangulation_batch_device), ORBmatcher(0.6, false).
 
-Step k+1's extraction overlaps step k's stereo / BoW / gather / triangulation: two
-extractor pairs, two slabs, two gathered buffers and two sets of triangulation outputs
-alternate, and a set is reused only after the triangulation that last read it (its
-event) -- so the gather of step k+1 never overwrites neighbours that step k's
-triangulation is still reading.  `windows` > 1 gives each step its own keyframe window
+Step k+1's extraction overlaps step k's stereo / BoW / gather / triangulation: sets of
+extractor pairs, slabs, gathered buffers and triangulation outputs rotate (four by
+default, ORBX_KF_SETS), and a set is reused only after the triangulation that last read
+it (its event) -- so the gather of a later step never overwrites neighbours that an
+earlier step's triangulation is still reading.  `windows` > 1 gives each step its own keyframe window
 (same poses, another texture), so a cross-step ordering fault changes bytes.  The neighbour plan (covisibility proxy: the nn
 keyframes whose views overlap most, then the baseline skip) depends only on the poses and
 is made once on the host, as LocalMapping does per keyframe.
