@@ -52,6 +52,12 @@ class StereoSequencePipeline:
         # 
         self._own_ms = stream_create(device, 1, 0)
         self.ms = torch.cuda.ExternalStream(self._own_ms, device=self.dev)
+        # ORBX_STEREO_TRACK_STREAM=1: UpdateLastFrame + the search on a stream of their own,
+        # so step k's tracking runs beside step k+1's stereo matching (as the keyframe
+        # stream's triangulation does).  Off: r05bd measured it 1-2 % slower
+        import os
+        self._own_ts = stream_create(device, 1, 0) if os.environ.get("ORBX_STEREO_TRACK_STREAM") == "1" else None
+        self.ts = torch.cuda.ExternalStream(self._own_ts, device=self.dev) if self._own_ts else self.ms
         # extractor pairs in rotation: a set is re-extracted only after the matching that last
         # read it (ev_m).  Two: here the matching keeps up with the extraction, and a third
         # set (ORBX_STEREO_SETS=3, which helps the keyframe stream) measured 0.8 % slower (r05ap)
@@ -79,6 +85,7 @@ class StereoSequencePipeline:
         self.ev_l = [torch.cuda.Event() for _ in range(self.nsets)]
         self.ev_r = [torch.cuda.Event() for _ in range(self.nsets)]
         self.ev_m = [torch.cuda.Event() for _ in range(self.nsets)]
+        self.ev_s = [torch.cuda.Event() for _ in range(self.nsets)]  # a set's stereo matching done
         self.used = [False] * self.nsets
         self.it = 0
         self.last = None
@@ -86,8 +93,12 @@ class StereoSequencePipeline:
         self._st = []  # (stereo start, track start, end) events while timing
 
     def close(self):
+        from .extractor import stream_destroy
+        if self._own_ts:
+            self.ts.synchronize()
+            stream_destroy(self._own_ts)
+            self._own_ts = None
         if self._own_ms:
-            from .extractor import stream_destroy
             self.ms.synchronize()
             stream_destroy(self._own_ms)
             self._own_ms = None
@@ -124,11 +135,14 @@ class StereoSequencePipeline:
                                                       stream=self.ms)
         if self._timing:
             ev[1].record(self.ms)
+        if self.ts is not self.ms:
+            self.ev_s[k].record(self.ms)
+            self.ts.wait_event(self.ev_s[k])
         if self.track:
             if d_Tcw is None:
                 raise ValueError("tracking needs the frames' poses")
             self._last_T = d_Tcw
-            s = self.ms.cuda_stream
+            s = self.ts.cuda_stream
             update_last_frame_device(bk["kl"], bk["nl"], bk["dp"], d_Tcw, self.fx, self.fy, self.cx, self.cy,
                                      self.th_depth, bk, d_obs_in=obs_in, d_pos_in=pos_in, stream=s)
             self.tmatcher.match_sequence_device_ex(
@@ -136,9 +150,9 @@ class StereoSequencePipeline:
                 self.W, self.H, th=self.th, mono=False, bf=self.bf, b=self.b, d_u_right=bk["ur"],
                 d_mp_pos=bk["mp_pos"], d_has_mp=bk["has_mp"], d_mp_obs=bk["mp_obs"], global_ids=True, stream=s)
         if self._timing:
-            ev[2].record(self.ms)
+            ev[2].record(self.ts)
             self._st.append(ev)
-        self.ev_m[k].record(self.ms)
+        self.ev_m[k].record(self.ts)  # after the stereo matching (waited for) and the tracking
         self.used[k] = True
         self.last = k
         self.it += 1
