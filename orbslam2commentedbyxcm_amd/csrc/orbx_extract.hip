@@ -736,34 +736,28 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
 // the non-zero pixels in raster order (one ballot per row -- per row pair when the window
 // is at most 32 wide), tests only those against their neighbours, and writes the
 // survivors of the chosen threshold in the same order.
-// Staged window row pitch: 68 bytes (64 + zero frame, an odd dword count).  ORBX_FC_TIGHT=1
-// sizes it to the widest window instead (36 bytes at 30-px cells, 4.4 KB less LDS per
-// workgroup; 16 KB more costs configs[1] 9 %, r05ab) -- and measured slower: configs[4]
-// 113.7-113.9k -> 106.3-107.4k frames/s, configs[1] within noise (r05ac).
-#ifndef ORBX_FC_TIGHT
-#define ORBX_FC_TIGHT 0
+// Staged window row pitch: 68 bytes (64 + zero frame, an odd dword count), a compile-time
+// constant.  Measured alternatives (ORBX_FC_PITCH): 44-100 bytes all slower at configs[4]
+// (up to -8 %, r05al / r05am), and a pitch sized to the widest window (36 bytes at 30-px
+// cells, 4.4 KB less LDS per workgroup) -6 % there (r05ac).  Passing the pitch at run
+// time (as that experiment did) cost configs[1] 1.1 % by itself (r05bh).
+#ifndef ORBX_FC_PITCH
+#define ORBX_FC_PITCH 68
 #endif
+constexpr int kFcStride = ORBX_FC_PITCH;
 #ifndef ORBX_FC_INFLIGHT
 #define ORBX_FC_INFLIGHT 8  // k_fast_cells: row steps of byte loads in flight (r05aw: 4 -2 %,
                             // 16 -10 % at configs[1])
 #endif
-#ifndef ORBX_FC_PITCH  // r05al / r05am: 44-100 bytes all measured slower than 68 at configs[4] (up to -8 %)
-#define ORBX_FC_PITCH 68
-#endif
-static int fast_cells_stride(int max_wc) {
-    if (!ORBX_FC_TIGHT) return ORBX_FC_PITCH > max_wc + 2 ? ORBX_FC_PITCH : 68;
-    int d = (max_wc + 2 + 3) / 4;
-    if (!(d & 1)) d++;
-    return 4 * d;
-}
+static_assert(kFcStride % 4 == 0 && kFcStride >= 36, "fast_cells window pitch");
 
 __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ score, long long fb,
                                                     const CellGeom* __restrict__ cells, int ncells,
                                                     int ini_th, int min_th, uint32_t* __restrict__ slots,
                                                     int slots_pf, int* __restrict__ cell_count, int nframes,
-                                                    int max_wr, int max_wc, int kFcStride) {
-    // per wave: (max_wr + 2) framed rows of M (pitch kFcStride >= max_wc + 2), then a
-    // candidate list of max_wr*max_wc u16
+                                                    int max_wr, int max_wc) {
+    // per wave: (max_wr + 2) framed rows of M (pitch kFcStride >= max_wc + 2, checked by
+    // the launcher), then a candidate list of max_wr*max_wc u16
     extern __shared__ __align__(16) uint8_t s_dyn[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int per_wave = (((max_wr + 2) * kFcStride + 2 * max_wr * max_wc) + 15) & ~15;
@@ -819,7 +813,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
                 const int rb = r0 + k * rstep;  // first row of this step (wave-uniform)
                 if (rb < wr) {
                     const int r = rb + half;
-                    if (r < wr && col <= wc) m[(r + 1) * kFcStride + col + 1] = (uint8_t)v[k];
+                    // (a pitch of at least 65 holds every lane's column; a smaller one only
+                    // the window and its right frame)
+                    if (r < wr && (kFcStride >= 65 || col <= wc)) m[(r + 1) * kFcStride + col + 1] = (uint8_t)v[k];
                     const unsigned long long b = __ballot(v[k] > tc);  // raster order: row rb, then rb+1
                     if ((b >> lane) & 1ull) list[n + __popcll(b & below)] = (uint16_t)((r << 8) | col);
                     n += __popcll(b);
@@ -2178,12 +2174,12 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
 #ifndef ORBX_EXP_FC_LDS_PAD
 #define ORBX_EXP_FC_LDS_PAD 0  // timing experiment: extra dynamic LDS per k_fast_cells workgroup
 #endif
-        const int fcs = fast_cells_stride(plan.fc_wc);
-        const size_t fc_lds = 4 * (size_t)((((plan.fc_wr + 2) * fcs + 2 * plan.fc_wr * plan.fc_wc) + 15) & ~15) +
+        if (plan.fc_wc + 2 > kFcStride) return hipErrorInvalidValue;  // a window wider than the staged pitch
+        const size_t fc_lds = 4 * (size_t)((((plan.fc_wr + 2) * kFcStride + 2 * plan.fc_wr * plan.fc_wc) + 15) & ~15) +
                               ORBX_EXP_FC_LDS_PAD;
         hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), fc_lds, stream, db.score, fb, db.cells, ncells,
                            plan.prm.ini_th, plan.prm.min_th, db.slots, plan.slots_per_frame, db.cell_count, batch,
-                           plan.fc_wr, plan.fc_wc, fcs);
+                           plan.fc_wr, plan.fc_wc);
     }
     if (ev && ev[3]) (void)hipEventRecord(ev[3], stream);
     if (stage_ev && stage_after == 3) (void)hipEventRecord(stage_ev, stream);
