@@ -1283,7 +1283,7 @@ __global__ __launch_bounds__(256, ORBX_OCT_WPE) void k_octree(const LevelGeom* _
         for (int j = tid; j < size; j += 256) ccnt[2 * j] = ccnt[2 * j + 1] = 0u;
         if (tid == 0) s_scal[1] = 0;
         __syncthreads();
-        const bool few = size <= ORBX_OCT_FEW;
+        const bool few = ORBX_OCT_FEW > 0 && size <= ORBX_OCT_FEW;  // (compiled out at 0)
         FOR_KEYS({
             const int nd = NN;
             if (A.cnt[nd] >= 2) {
