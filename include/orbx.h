@@ -162,9 +162,10 @@ int orbx_extractor_set_node_capacity(orbx_extractor* ex, int cap);
  * copying it into the extractor's pyramid (when the frames are 16-byte aligned, their
  * frame pitch a multiple of 16 and their row stride a multiple of 64; otherwise it is
  * copied as before).  The frames must then stay unchanged while the pyramid is in use:
- * orbx_pyramid_level(_device) returns level 0 from them, and the stereo matchers, which
- * read the pyramid's own layout, refuse the extractor (ORBX_ERR_STATE).  For the
- * monocular front end (Frame's monocular constructor never reads mvImagePyramid). */
+ * orbx_pyramid_level(_device) returns level 0 from them, and the stereo matchers
+ * (orbx_compute_stereo_matches(_batch_device)) read the octave-0 SAD windows of
+ * Frame::ComputeStereoMatches (Frame.cc:800-835) there.  Frames in a pitched layout
+ * (rows a multiple of 64 bytes apart) qualify at any width. */
 int orbx_extractor_set_level0_in_place(orbx_extractor* ex, int enable);
 
 /* Per-stage HIP-event timing (ms) of extraction calls, averaged over the (up to 64)

@@ -331,10 +331,14 @@ int ensure_host_staging(orbx_extractor* ex, size_t in_bytes, size_t out_slots, i
 
 }  // namespace
 
-int orbx::extractor_pyramid(orbx_extractor* ex, PyrView* v) {
+int orbx::extractor_pyramid(orbx_extractor* ex, PyrView* v, bool allow_l0) {
     if (!ex || !v) return fail(ORBX_ERR_ARG, "null argument");
     if (!ex->have_pyramid) return fail(ORBX_ERR_STATE, "no extraction yet");
-    if (ex->l0) return fail(ORBX_ERR_STATE, "pyramid level 0 was read in place (orbx_extractor_set_level0_in_place)");
+    if (ex->l0 && !allow_l0)
+        return fail(ORBX_ERR_STATE, "pyramid level 0 was read in place (orbx_extractor_set_level0_in_place)");
+    v->l0 = ex->l0;
+    v->l0_fp = (long long)ex->l0_fp;
+    v->l0_pitch = (int)ex->l0_pitch;
     const Plan& p = ex->plan;
     v->base = ex->db.pyr;
     v->frame_bytes = p.pyr_frame_bytes;

@@ -45,9 +45,15 @@ struct PyrView {
     float scale[kMaxLevels], inv_scale[kMaxLevels];
     int device = 0;
     hipStream_t stream = nullptr;  // stream of the last extraction
+    // level 0 read in place (orbx_extractor_set_level0_in_place): frame f's level 0 is the
+    // caller's frame at l0 + f * l0_fp, rows l0_pitch apart (null: level 0 is in base)
+    const uint8_t* l0 = nullptr;
+    long long l0_fp = 0;
+    int l0_pitch = 0;
 };
-// Fills `v` for extractor `ex` (ORBX_ERR_STATE before any extraction).
-int extractor_pyramid(orbx_extractor* ex, PyrView* v);
+// Fills `v` for extractor `ex` (ORBX_ERR_STATE before any extraction, and, unless
+// allow_l0 -- a reader that takes level 0 from v->l0 --, after an in-place extraction).
+int extractor_pyramid(orbx_extractor* ex, PyrView* v, bool allow_l0 = false);
 
 constexpr int kStages = 6;
 extern const char* const kStageNames[kStages];

@@ -2743,9 +2743,14 @@ __global__ __launch_bounds__(256) void k_stereo(StereoBatch sb) {
     float vd[11];
     int bestDistS = 0x7fffffff, bestincR = 0;
     {
-        const int pitch = sad ? sb.level_pitch[levelL] : 0;
-        const uint8_t* IL = sb.pyr_l + (size_t)b * sb.fb_l + (sad ? sb.level_off[levelL] : 0);
-        const uint8_t* IR = sb.pyr_r + (size_t)b * sb.fb_r + (sad ? sb.level_off[levelL] : 0);
+        // level 0 from the caller's frames when the extraction read it in place
+        const bool inl = sad && levelL == 0 && sb.l0_l, inr = sad && levelL == 0 && sb.l0_r;
+        const int pitch = inl ? sb.l0_pitch_l : (sad ? sb.level_pitch[levelL] : 0);
+        const int pitchR = inr ? sb.l0_pitch_r : (sad ? sb.level_pitch[levelL] : 0);
+        const uint8_t* IL = inl ? sb.l0_l + (size_t)b * sb.l0_fp_l
+                                : sb.pyr_l + (size_t)b * sb.fb_l + (sad ? sb.level_off[levelL] : 0);
+        const uint8_t* IR = inr ? sb.l0_r + (size_t)b * sb.l0_fp_r
+                                : sb.pyr_r + (size_t)b * sb.fb_r + (sad ? sb.level_off[levelL] : 0);
         const int yl0 = (int)scaledvL - w, xl0 = (int)scaleduL - w;
         int cl = 0;
         int a8[8];
@@ -2763,13 +2768,13 @@ __global__ __launch_bounds__(256) void k_stereo(StereoBatch sb) {
             int acc = 0;
             if (sad) {
                 const int xr0 = (int)(scaleduR0 + incR - w);
-                const int cr = IR[(size_t)(yl0 + w) * pitch + xr0 + w];
+                const int cr = IR[(size_t)(yl0 + w) * pitchR + xr0 + w];
 #pragma unroll
                 for (int j = 0; j < 8; j++) {
                     const int k = gl + 16 * j;
                     if (k < 121) {
                         const int yy = k / 11, xx = k - yy * 11;
-                        const int c = (int)IR[(size_t)(yl0 + yy) * pitch + xr0 + xx] - cr;
+                        const int c = (int)IR[(size_t)(yl0 + yy) * pitchR + xr0 + xx] - cr;
                         acc += a8[j] > c ? a8[j] - c : c - a8[j];
                     }
                 }

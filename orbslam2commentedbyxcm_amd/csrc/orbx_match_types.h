@@ -300,6 +300,12 @@ struct StereoBatch {
     const uint8_t* pyr_l;         // mvImagePyramid ROIs of the left / right extractor
     const uint8_t* pyr_r;
     long long fb_l, fb_r;         // pyramid bytes per frame
+    // level 0 read in place by the extraction (orbx_extractor_set_level0_in_place): pair b's
+    // level 0 is the caller's frame at l0_* + b * l0_fp_*, rows l0_pitch_* apart (null: in pyr_*)
+    const uint8_t* l0_l;
+    const uint8_t* l0_r;
+    long long l0_fp_l, l0_fp_r;
+    int l0_pitch_l, l0_pitch_r;
     long long level_off[32];      // level l of a frame block at + level_off[l], rows level_pitch[l] apart
     int level_pitch[32];
     int level_w[32];

@@ -1830,9 +1830,9 @@ namespace {
 
 // Level geometry of a stereo pair's pyramids; the two extractors must share it.
 int stereo_levels(orbx_extractor* ex_l, orbx_extractor* ex_r, StereoBatch& sb, PyrView& vl, PyrView& vr) {
-    int rc = extractor_pyramid(ex_l, &vl);
+    int rc = extractor_pyramid(ex_l, &vl, true);
     if (rc != ORBX_OK) return rc;
-    rc = extractor_pyramid(ex_r, &vr);
+    rc = extractor_pyramid(ex_r, &vr, true);
     if (rc != ORBX_OK) return rc;
     if (vl.W != vr.W || vl.H != vr.H || vl.L != vr.L || vl.device != vr.device)
         return fail(ORBX_ERR_ARG, "left and right extractors hold pyramids of different geometry");
@@ -1852,6 +1852,17 @@ int stereo_levels(orbx_extractor* ex_l, orbx_extractor* ex_r, StereoBatch& sb, P
     sb.nlevels = vl.L;
     sb.band_cap = sb.cap;  // the (octave, row) index holds every right keypoint once
     return ORBX_OK;
+}
+
+// Level 0 of extractions that read it in place: the caller's frames (k_stereo's SAD
+// window at octave 0 reads them there).
+void stereo_level0(StereoBatch& sb, const PyrView& vl, const PyrView& vr, int left_frame, int right_frame) {
+    sb.l0_l = vl.l0 ? vl.l0 + (size_t)left_frame * vl.l0_fp : nullptr;
+    sb.l0_r = vr.l0 ? vr.l0 + (size_t)right_frame * vr.l0_fp : nullptr;
+    sb.l0_fp_l = vl.l0_fp;
+    sb.l0_fp_r = vr.l0_fp;
+    sb.l0_pitch_l = vl.l0_pitch;
+    sb.l0_pitch_r = vr.l0_pitch;
 }
 
 // words of the per-pair (octave, row) offsets + row coverage counts (StereoBatch::row_off)
@@ -1894,6 +1905,7 @@ int orbx_compute_stereo_matches(orbx_matcher* m, orbx_extractor* ex_left, int le
         if (keys_r[i].octave < 0 || keys_r[i].octave >= vl.L) return fail(ORBX_ERR_ARG, "right keypoint octave");
     sb.pyr_l = vl.base + (size_t)left_frame * vl.frame_bytes;
     sb.pyr_r = vr.base + (size_t)right_frame * vr.frame_bytes;
+    stereo_level0(sb, vl, vr, left_frame, right_frame);
     sb.bf = left->bf;
     sb.max_d = max_disparity;
     HIP_TRY(hipSetDevice(m->device));
@@ -1984,6 +1996,7 @@ int orbx_compute_stereo_matches_batch_device(orbx_matcher* m, orbx_extractor* ex
     sb.n_r = d_n_r;
     sb.pyr_l = vl.base + (size_t)left_frame0 * vl.frame_bytes;
     sb.pyr_r = vr.base + (size_t)right_frame0 * vr.frame_bytes;
+    stereo_level0(sb, vl, vr, left_frame0, right_frame0);
     sb.bf = bf;
     sb.max_d = max_disparity;
     sb.u_right = d_u_right;

@@ -164,7 +164,8 @@ class ORBextractor:
 
     def set_level0_in_place(self, enable: bool = True) -> None:
         """orbx_extractor_set_level0_in_place: level 0 read from the caller's device frames
-        (monocular front end; the frames must stay unchanged while the pyramid is used)."""
+        when their rows are 64-byte aligned (device_frames); the frames must stay unchanged
+        while the pyramid is used (the stereo matchers read level 0 from them)."""
         L.check(L.lib().orbx_extractor_set_level0_in_place(self._h, 1 if enable else 0))
 
     STAGES = ("pyramid", "score_blur", "fast_cells", "octree", "describe")
@@ -197,6 +198,22 @@ class ORBextractor:
         if self._pyr_cache is None:
             self._pyr_cache = [self.pyramid_level(lv) for lv in range(self.nlevels)]
         return self._pyr_cache
+
+
+def device_frames(frames, device, align: int = 64):
+    """(B, H, W) u8 frames copied into HBM with rows `align` bytes apart (a pitched layout,
+    as hipMallocPitch gives): a (B, H, W) view whose row stride is a multiple of 64, so an
+    extractor with set_level0_in_place reads level 0 from it in place whatever W is
+    (KITTI's 1241-byte and EuRoC's 752-byte rows included)."""
+    import torch
+
+    a = np.ascontiguousarray(frames, dtype=np.uint8)
+    B, H, W = a.shape
+    P = (W + align - 1) // align * align
+    buf = torch.zeros((B, H, P), dtype=torch.uint8, device=device)
+    view = buf[:, :, :W]
+    view.copy_(torch.from_numpy(a))
+    return view
 
 
 def stream_wait_event(stream: int, event: int) -> None:

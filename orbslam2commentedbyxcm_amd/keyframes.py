@@ -204,7 +204,7 @@ class StereoKeyFramePipeline:
 
     def __init__(self, batch: int, rank: int = 0, world: int = 1, device: int = 0, nn: int = 10, seq_seed: int = 3,
                  vocab_text: bytes | None = None, settings: dict | None = None, group=None, windows: int = 1,
-                 on_step_done=None, collective: bool = False):
+                 on_step_done=None, collective: bool = False, level0_in_place: bool = True):
         import torch
 
         from . import synth
@@ -261,6 +261,11 @@ class StereoKeyFramePipeline:
         self.nsets = max(2, int(os.environ.get("ORBX_KF_SETS", "4")))
         self.sets = [(ORBextractor(*prm, device=device), ORBextractor(*prm, device=device))
                      for _ in range(self.nsets)]
+        # level 0 read in place from the pitched input frames below (no copy into the
+        # pyramids; the stereo matching reads it there)
+        for pair in self.sets:
+            for e in pair:
+                e.set_level0_in_place(level0_in_place)
         self.sf = self.sets[0][0].GetScaleFactors()
         self.cap = self.sets[0][0].max_keypoints(self.W, self.H)
         self.stereo = ORBmatcher(0.6, True, device=device)
@@ -315,7 +320,8 @@ class StereoKeyFramePipeline:
         self.on_step_done = on_step_done
         self.it = 0
         self.last = 0
-        self.inputs = [(torch.from_numpy(lf).to(self.dev), torch.from_numpy(rg).to(self.dev)) for lf, rg in views]
+        from .extractor import device_frames
+        self.inputs = [(device_frames(lf, self.dev), device_frames(rg, self.dev)) for lf, rg in views]
         self.d_left, self.d_right = self.inputs[0]
         torch.cuda.synchronize(self.dev)
         # the keyframe tables are fixed per buffer: build the ctypes arrays once

@@ -36,7 +36,7 @@ class StereoSequencePipeline:
     def __init__(self, batch: int, width: int, height: int, fx: float, fy: float, cx: float, cy: float, bf: float,
                  params=(2000, 1.2, 8, 20, 7), track: bool = True, th: float = 7.0, nnratio: float = 0.9,
                  check_ori: bool = True, th_depth_factor: float = 35.0, max_d: float | None = None,
-                 matcher_mode: int | None = None, device: int = 0):
+                 matcher_mode: int | None = None, device: int = 0, level0_in_place: bool = True):
         import torch
 
         from .extractor import stream_create
@@ -65,6 +65,12 @@ class StereoSequencePipeline:
         self.nsets = max(2, int(os.environ.get("ORBX_STEREO_SETS", "2")))
         self.sets = [(ORBextractor(*params, device=device), ORBextractor(*params, device=device))
                      for _ in range(self.nsets)]
+        # level 0 read from the caller's frames when their rows are 64-byte aligned
+        # (extractor.device_frames): no copy into the pyramid, and ComputeStereoMatches'
+        # octave-0 SAD windows read it there (orbx_extractor_set_level0_in_place)
+        for pair in self.sets:
+            for e in pair:
+                e.set_level0_in_place(level0_in_place)
         self.smatcher = ORBmatcher(0.6, True, device=device)  # ComputeStereoMatches' handle (stream, arena)
         self.tmatcher = ORBmatcher(nnratio, check_ori, device=device)  # TrackWithMotionModel: ORBmatcher(0.9, true)
         self.tmatcher.set_footprint(5 if matcher_mode is None else matcher_mode)

@@ -224,6 +224,8 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--parity-frames", type=int, default=-1,
                     help="rank 0 keyframes to check (-1: all at world 1, 16 at world > 1; 0: none)")
+    ap.add_argument("--level0-copy", action="store_true",
+                    help="copy level 0 into the pyramids instead of reading it in place from the frames")
     ap.add_argument("--collective", action="store_true",
                     help="exchange the slabs through an RCCL process group even at --gpus 1 (a one-rank "
                          "all_gather_into_tensor into gathered buffers: the N-GPU data path on one GPU)")
@@ -285,7 +287,7 @@ def run(args, rank: int, world: int, device: int, collective: bool):
     text = synth.vocabulary_text(7, 10, 6, 0, 0, centres=d0)
     gen_s = time.perf_counter() - t0
     pl = StereoKeyFramePipeline(B, rank, world, device=device, nn=args.nn, vocab_text=text,
-                                collective=collective)
+                                collective=collective, level0_in_place=not getattr(args, "level0_copy", False))
 
     def barrier():
         if world > 1:

@@ -112,6 +112,9 @@ def main(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--parity-frames", type=int, default=-1, help="-1 = every frame and pair of the last step")
+    ap.add_argument("--packed-frames", action="store_true",
+                    help="frames in HBM with 1241-byte rows (level 0 then copied into the pyramids) instead of "
+                         "a 1280-byte row pitch (level 0 read in place)")
     args, _ = ap.parse_known_args(argv)
     B = args.batch
     track = not args.no_track
@@ -127,8 +130,12 @@ def main(argv=None):
     pl = StereoSequencePipeline(B, K.W, K.H, K.FX, K.FY, K.CX, K.CY, K.BF, params=K.PARAMS, track=track,
                                 th_depth_factor=K.TH_DEPTH_FACTOR)
     sf, cap = pl.sf, pl.cap
-    d_left = torch.from_numpy(left_np).to(dev)
-    d_right = torch.from_numpy(right_np).to(dev)
+    from orbslam2commentedbyxcm_amd.extractor import device_frames
+    if args.packed_frames:
+        d_left = torch.from_numpy(left_np).to(dev)
+        d_right = torch.from_numpy(right_np).to(dev)
+    else:  # rows 1280 bytes apart (hipMallocPitch's layout): level 0 read in place
+        d_left, d_right = device_frames(left_np, dev), device_frames(right_np, dev)
     d_T = torch.from_numpy(T_np).to(dev)
     tracked = K.tracked_mask(SEED, B, cap)
     torch.cuda.synchronize(dev)
@@ -229,7 +236,8 @@ def main(argv=None):
                                f"FAST 20/7, bf {K.BF}, fx {K.FX}, ThDepth {K.TH_DEPTH_FACTOR:g}; step = extract L and "
                                f"R on two extractors + Frame::ComputeStereoMatches (maxD = fx)" + leg,
                    "frames_per_step": B, "width": K.W, "height": K.H, "search_by_projection": track,
-                   "th_depth_m": round(pl.th_depth, 4)},
+                   "th_depth_m": round(pl.th_depth, 4),
+                   "frame_row_pitch": int(d_left.stride(1))},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      **bench.profile_fields(dom, bytes_pf[dom] * B, stage_ms[dom], "kitti"),

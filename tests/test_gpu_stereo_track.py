@@ -65,11 +65,21 @@ def _check_track(oracle, h, views, tracked, th_depth, cap, check_ori=True):
     return forward, backward
 
 
-def _run(pl, scene, tracked=None, steps=2):
+def _run(pl, scene, tracked=None, steps=2, pitched=True):
+    """pitched: the frames in HBM with 1280-byte rows (extractor.device_frames), so the
+    extractors read level 0 in place and ComputeStereoMatches reads it from the frames;
+    packed 1241-byte rows take the copy into the pyramids."""
     import torch
+
+    from orbslam2commentedbyxcm_amd.extractor import device_frames
     left, right, T = scene
     dev = pl.dev
-    d_left, d_right, d_T = (torch.from_numpy(a).to(dev) for a in (left, right, T))
+    if pitched:
+        d_left, d_right = device_frames(left, dev), device_frames(right, dev)
+        assert d_left.stride(1) == 1280
+    else:
+        d_left, d_right = (torch.from_numpy(a).to(dev) for a in (left, right))
+    d_T = torch.from_numpy(T).to(dev)
     obs_in = pos_in = None
     if tracked is not None:
         pl.step(d_left, d_right, d_T)
@@ -81,13 +91,15 @@ def _run(pl, scene, tracked=None, steps=2):
     return pl.host_results()
 
 
-def test_stereo_track_kitti_tracked_and_temporal(oracle, orbx_built, scene, oracle_views):
+@pytest.mark.parametrize("pitched", [True, False])
+def test_stereo_track_kitti_tracked_and_temporal(oracle, orbx_built, scene, oracle_views, pitched):
     """Half the LastFrame keypoints with depth already track map MapPoints (blocking
-    claims), the other visited ones get temporal points (non-blocking)."""
+    claims), the other visited ones get temporal points (non-blocking).  Frames with a
+    64-byte-multiple row pitch (level 0 read in place) and packed."""
     from orbslam2commentedbyxcm_amd.stereo import StereoSequencePipeline
     pl = StereoSequencePipeline(B, K.W, K.H, K.FX, K.FY, K.CX, K.CY, K.BF, params=K.PARAMS)
     tracked = K.tracked_mask(11, B, pl.cap)
-    h = _run(pl, scene, tracked)
+    h = _run(pl, scene, tracked, pitched=pitched)
     assert pl.status_clean()
     _check_frames(h, oracle_views)
     fwd, bwd = _check_track(oracle, h, oracle_views, tracked, pl.th_depth, pl.cap)
