@@ -266,6 +266,13 @@ class StereoKeyFramePipeline:
         for pair in self.sets:
             for e in pair:
                 e.set_level0_in_place(level0_in_place)
+        # lane offset: the right image's extraction starts once the left one's has passed
+        # stage 3 (FAST cells), so the two run out of phase instead of in step (r05bn,
+        # interleaved: in step 49.5-50.2k keyframes/s, after stage 2 49.4-51.9k, after
+        # stage 3 50.6-52.5k; r05bo: after stage 3 49.4-51.2k against 48.4-51.2k after
+        # stage 4).  ORBX_KF_LANE_OFFSET=k overrides (0: in step)
+        lo = int(os.environ.get("ORBX_KF_LANE_OFFSET", "3"))
+        self.lane_ev = [a.set_stage_event(lo) for a, _ in self.sets] if lo > 0 else None
         self.sf = self.sets[0][0].GetScaleFactors()
         self.cap = self.sets[0][0].max_keypoints(self.W, self.H)
         self.stereo = ORBmatcher(0.6, True, device=device)
@@ -361,6 +368,9 @@ class StereoKeyFramePipeline:
         self.window_of[k] = w
         d_left, d_right = self.inputs[w]
         exl.extract_batch_device(d_left, v["kps"], v["desc"], v["n"])
+        if self.lane_ev:
+            from .extractor import stream_wait_event
+            stream_wait_event(sr.cuda_stream, self.lane_ev[k])
         exr.extract_batch_device(d_right, rt["kps"], rt["desc"], rt["n"])
         self.ev_l[k].record(sl)
         self.ev_r[k].record(sr)

@@ -71,6 +71,13 @@ class StereoSequencePipeline:
         for pair in self.sets:
             for e in pair:
                 e.set_level0_in_place(level0_in_place)
+        # lane offset: the right image's extraction starts once the left one's has passed
+        # stage 2 (blur + FAST strength), as the monocular pipeline's lanes, so the two run
+        # out of phase instead of in step (r05bm, interleaved: 53.6-54.0k in step, 54.6-55.1k
+        # after stage 2, 54.0-55.1k after stage 3, 53.1-53.9k after stage 1).
+        # ORBX_STEREO_LANE_OFFSET=k overrides (0: in step)
+        lo = int(os.environ.get("ORBX_STEREO_LANE_OFFSET", "2"))
+        self.lane_ev = [a.set_stage_event(lo) for a, _ in self.sets] if lo > 0 else None
         self.smatcher = ORBmatcher(0.6, True, device=device)  # ComputeStereoMatches' handle (stream, arena)
         self.tmatcher = ORBmatcher(nnratio, check_ori, device=device)  # TrackWithMotionModel: ORBmatcher(0.9, true)
         self.tmatcher.set_footprint(5 if matcher_mode is None else matcher_mode)
@@ -128,6 +135,9 @@ class StereoSequencePipeline:
             sl.wait_event(self.ev_m[k])
             sr.wait_event(self.ev_m[k])
         exl.extract_batch_device(d_left, bk["kl"], bk["dl"], bk["nl"])
+        if self.lane_ev:
+            from .extractor import stream_wait_event
+            stream_wait_event(sr.cuda_stream, self.lane_ev[k])
         exr.extract_batch_device(d_right, bk["kr"], bk["dr"], bk["nr"])
         self.ev_l[k].record(sl)
         self.ev_r[k].record(sr)
