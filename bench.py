@@ -497,7 +497,10 @@ def main():
     pl = SequencePipeline(B, W, H, lanes=args.lanes, pipelined=pipeline, match=match, device=gpu,
                           params=prm, fx=FX, fy=FY, cx=CX, cy=CY, depth=DEPTH, th=TH,
                           match_stream=_match_stream(dev) if match else None,
-                          nbuf=int(os.environ.get("ORBX_PIPE_NBUF", "2")),
+                          # three buffer sets at <= 8 levels: extraction j + 2 need not wait for
+                          # matching j (configs[1] +0.6 %, 7 of 8 interleaved pairs at 20 / 50 steps,
+                          # r05bs-bt; configs[4] -0.3 %, two)
+                          nbuf=int(os.environ.get("ORBX_PIPE_NBUF", "3" if prm[2] <= 8 else "2")),
                           matcher_mode=None if "ORBX_MATCH_MODE" not in os.environ
                           else int(os.environ["ORBX_MATCH_MODE"]),
                           match_after_stage=int(os.environ.get("ORBX_MATCH_AFTER", "0")),
@@ -506,6 +509,7 @@ def main():
                           match_priority=int(os.environ.get("ORBX_MATCH_STREAM_PRIO", "0")),
                           level0_in_place=os.environ.get("ORBX_L0_COPY") != "1")
     S = pl.S
+    nbufs = len(pl.kps)  # output buffer sets in rotation
     lane_off = pl.lane_offset_stage if pl.lane_ev is not None else None  # None: no offset applied
     d_frames = torch.from_numpy(frames_np).to(dev)
     d_T = torch.from_numpy(T).to(dev)
@@ -609,14 +613,15 @@ def main():
     if match and not args.no_host_fed:
         pl.set_timing(False)
         h_frames = torch.from_numpy(frames_np).pin_memory()
-        d_buf = [torch.empty_like(d_frames) for _ in range(2)]
+        nb = len(pl.kps)
+        d_buf = [torch.empty_like(d_frames) for _ in range(nb)]
         cs = torch.cuda.Stream(device=dev)
-        ev_up = [torch.cuda.Event() for _ in range(2)]
+        ev_up = [torch.cuda.Event() for _ in range(nb)]
 
         def hf_step(j):
-            b = pl.it % 2  # the pipeline's buffer of this step (nbuf 2) = the upload buffer
+            b = pl.it % nb  # the pipeline's buffer of this step = the upload buffer
             with torch.cuda.stream(cs):
-                if j >= 2:  # the extraction two steps back (pipeline buffer b) read d_buf[b]
+                if j >= nb:  # the extraction nb steps back (pipeline buffer b) read d_buf[b]
                     for c in range(pl.S):
                         cs.wait_event(pl.ev_ex[b][c])
                 d_buf[b].copy_(h_frames, non_blocking=True)
@@ -625,31 +630,30 @@ def main():
                 pl.streams[c].wait_event(ev_up[b])
             pl.step(d_buf[b], d_T)
 
-        if pl.nbuf_ok():
-            for j in range(max(args.warmup, 1)):
-                hf_step(j)
-            pl.drain(d_T)
-            sync()
-            barrier()
-            sync()
-            t0 = time.perf_counter()
-            for j in range(args.steps):
-                hf_step(j + 2)  # d_buf[b] was read by an extraction two steps back
-            pl.drain(d_T)
-            sync()
-            barrier()
-            sync()
-            el3 = time.perf_counter() - t0
-            if world > 1:
-                t = torch.tensor([el3], dtype=torch.float64, device=dev)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                el3 = float(t.item())
-            host_fed = {"value": round(B * args.steps * world / el3, 2), "unit": "frames/s",
-                        "ms_per_step": round(el3 / args.steps * 1e3, 4),
-                        "upload_bytes_per_step": int(frames_np.nbytes),
-                        "upload_GBps": round(frames_np.nbytes * args.steps / el3 / 1e9, 2),
-                        "note": "frames uploaded from pinned host memory every step (copy stream, double-buffered, "
-                                "overlapped with the previous step's extraction and matching); results stay in HBM"}
+        for j in range(max(args.warmup, 1)):
+            hf_step(j)
+        pl.drain(d_T)
+        sync()
+        barrier()
+        sync()
+        t0 = time.perf_counter()
+        for j in range(args.steps):
+            hf_step(j + nb)  # d_buf[b] was read by an extraction nb steps back
+        pl.drain(d_T)
+        sync()
+        barrier()
+        sync()
+        el3 = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el3], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el3 = float(t.item())
+        host_fed = {"value": round(B * args.steps * world / el3, 2), "unit": "frames/s",
+                    "ms_per_step": round(el3 / args.steps * 1e3, 4),
+                    "upload_bytes_per_step": int(frames_np.nbytes),
+                    "upload_GBps": round(frames_np.nbytes * args.steps / el3 / 1e9, 2),
+                    "note": f"frames uploaded from pinned host memory every step (copy stream, {nb} buffers, "
+                            "overlapped with the previous step's extraction and matching); results stay in HBM"}
 
     # The same step with TrackLocalMap (SearchLocalPoints against the MapPoints of the three
     # previous frames, after TrackWithMotionModel against the previous frame's MapPoints):
@@ -753,7 +757,7 @@ def main():
                        "frames_per_gpu_step": B, "global_batch": B * world, "width": W, "height": H,
                        "parallelism": f"frame-sharded x{world}", "lanes_per_gpu": S,
                        "lane_offset_stage": lane_off,
-                       "pipelined_match": pipeline,
+                       "pipelined_match": pipeline, "buffer_sets": nbufs,
                        "match_cu_stride": match_cu},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), **prof,

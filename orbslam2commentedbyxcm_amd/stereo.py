@@ -13,8 +13,9 @@ tracking search that follows it):
      frame b-1, b >= 1: the stereo octave ranges (bForward / bBackward for motion along the
      optical axis beyond mb), the mvuRight gate, the rotation check, and the claims of the
      temporal points (Observations() == 0) not blocking later ones.
-Steps 2-4 run on one matcher stream beside the next step's extraction: two extractor pairs
-alternate, so a pair's pyramids stay untouched until its stereo matching is done.
+Steps 2-4 run on one matcher stream beside the next step's extraction: three extractor
+pairs in rotation, so a pair's pyramids stay untouched until its stereo matching is done;
+the right image's extraction starts after the left one's blur stage (out of phase).
 
 tests/stereo_bench.py (bench.py --workload kitti) times this object; tests/test_gpu_stereo_track.py
 checks every frame and pair of its output against the CPU parity oracle.
@@ -59,10 +60,11 @@ class StereoSequencePipeline:
         self._own_ts = stream_create(device, 1, 0) if os.environ.get("ORBX_STEREO_TRACK_STREAM") == "1" else None
         self.ts = torch.cuda.ExternalStream(self._own_ts, device=self.dev) if self._own_ts else self.ms
         # extractor pairs in rotation: a set is re-extracted only after the matching that last
-        # read it (ev_m).  Two: here the matching keeps up with the extraction, and a third
-        # set (ORBX_STEREO_SETS=3, which helps the keyframe stream) measured 0.8 % slower (r05ap)
-        import os
-        self.nsets = max(2, int(os.environ.get("ORBX_STEREO_SETS", "2")))
+        # read it (ev_m).  Three: with the right image's lane offset (below) the matching stream
+        # no longer keeps up with two (r05bq-br, interleaved: two sets 54.7-54.9k stereo
+        # frames/s, three 57.2-58.2k, four 56.6-57.6k; before the offset three measured 0.8 %
+        # slower, r05ap).  ORBX_STEREO_SETS overrides
+        self.nsets = max(2, int(os.environ.get("ORBX_STEREO_SETS", "3")))
         self.sets = [(ORBextractor(*params, device=device), ORBextractor(*params, device=device))
                      for _ in range(self.nsets)]
         # level 0 read from the caller's frames when their rows are 64-byte aligned

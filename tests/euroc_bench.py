@@ -367,6 +367,8 @@ def run(args, rank: int, world: int, device: int, collective: bool):
                                    f"keyframe vs its nn={args.nn} stream neighbours passing the baseline test",
                        "keyframes_per_gpu_step": B, "global_batch": B * world, "width": pl.W, "height": pl.H,
                        "parallelism": f"frame-sharded x{world} + all-gather", "slab_mb_per_rank": round(slab_mb, 2),
+                       "extractor_sets": pl.nsets, "frame_row_pitch": int(pl.inputs[0][0].stride(1)),
+                       "right_lane_offset_stage": int(os.environ.get("ORBX_KF_LANE_OFFSET", "3")),
                        "slab_exchange": ("none (world 1: slabs read in place)" if not collective else
                                          "rccl all_gather_into_tensor" if dist.get_backend() == "nccl" else
                                          "gloo all_gather, staged through host memory (one-GPU rehearsal)"),

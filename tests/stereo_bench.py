@@ -237,7 +237,8 @@ def main(argv=None):
                                f"R on two extractors + Frame::ComputeStereoMatches (maxD = fx)" + leg,
                    "frames_per_step": B, "width": K.W, "height": K.H, "search_by_projection": track,
                    "th_depth_m": round(pl.th_depth, 4),
-                   "frame_row_pitch": int(d_left.stride(1))},
+                   "frame_row_pitch": int(d_left.stride(1)), "extractor_sets": pl.nsets,
+                   "right_lane_offset_stage": int(os.environ.get("ORBX_STEREO_LANE_OFFSET", "2"))},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      **bench.profile_fields(dom, bytes_pf[dom] * B, stage_ms[dom], "kitti"),

@@ -100,14 +100,16 @@ def test_device_status_reports_forced_overflow(oracle, orbx_built):
     assert not ex.status().any()
 
 
-@pytest.mark.parametrize("B,lanes,pipelined,steps", [(16, 2, True, 5), (24, 3, True, 4), (12, 1, False, 3),
-                                                     (256, 2, True, 3)])
-def test_sequence_pipeline_distinct_batch_every_step(oracle, orbx_built, B, lanes, pipelined, steps):
+@pytest.mark.parametrize("B,lanes,pipelined,steps,nbuf", [(16, 2, True, 5, 2), (24, 3, True, 4, 2),
+                                                          (12, 1, False, 3, 2), (256, 2, True, 3, 2),
+                                                          (16, 2, True, 5, 3), (256, 2, True, 4, 3)])
+def test_sequence_pipeline_distinct_batch_every_step(oracle, orbx_built, B, lanes, pipelined, steps, nbuf):
     """Every step gets its own batch (its own canvas and poses) and steps are issued
     back to back with no host synchronisation; each batch's outputs are copied out on the
     matcher stream as soon as its matching is enqueued (SequencePipeline.on_matched, before
     the buffer is released), so a buffer reused too early, an event waited on the wrong
-    buffer or a batch matched with another batch's poses shows up as a mismatch."""
+    buffer or a batch matched with another batch's poses shows up as a mismatch.  Two
+    buffer sets and three (the bench's at <= 8 levels)."""
     import torch
 
     batches = [synth.sequence(2000 + j, B) for j in range(steps)]
@@ -118,7 +120,7 @@ def test_sequence_pipeline_distinct_batch_every_step(oracle, orbx_built, B, lane
         r = pl.results(b)
         snaps.append({k: v.clone() for k, v in r.items()})
 
-    pl = SequencePipeline(B, 640, 480, lanes=lanes, pipelined=pipelined, on_matched=grab)
+    pl = SequencePipeline(B, 640, 480, lanes=lanes, pipelined=pipelined, on_matched=grab, nbuf=nbuf)
     dev_in = [(torch.from_numpy(f).to(pl.dev), torch.from_numpy(sequence_poses(o)).to(pl.dev)) for f, o in batches]
     torch.cuda.synchronize()
     with torch.cuda.stream(pl.ms):  # the clones run on the matcher stream, after the matching
