@@ -13,9 +13,10 @@ tracking search that follows it):
      frame b-1, b >= 1: the stereo octave ranges (bForward / bBackward for motion along the
      optical axis beyond mb), the mvuRight gate, the rotation check, and the claims of the
      temporal points (Observations() == 0) not blocking later ones.
-Steps 2-4 run on one matcher stream beside the next step's extraction: three extractor
-pairs in rotation, so a pair's pyramids stay untouched until its stereo matching is done;
-the right image's extraction starts after the left one's blur stage (out of phase).
+Step 2 runs on a matcher stream and steps 3-4 on a tracking stream, beside the next
+steps' extraction: four extractor pairs in rotation, so a pair's pyramids and outputs stay
+untouched until its matching is done; the right image's extraction starts after the left
+one's blur stage (out of phase).
 
 tests/stereo_bench.py (bench.py --workload kitti) times this object; tests/test_gpu_stereo_track.py
 checks every frame and pair of its output against the CPU parity oracle.
@@ -53,18 +54,23 @@ class StereoSequencePipeline:
         # 
         self._own_ms = stream_create(device, 1, 0)
         self.ms = torch.cuda.ExternalStream(self._own_ms, device=self.dev)
-        # ORBX_STEREO_TRACK_STREAM=1: UpdateLastFrame + the search on a stream of their own,
-        # so step k's tracking runs beside step k+1's stereo matching (as the keyframe
-        # stream's triangulation does).  Off: r05bd measured it 1-2 % slower
+        # UpdateLastFrame + the search on a stream of their own, so step k's tracking runs
+        # beside step k+1's stereo matching (as the keyframe stream's triangulation does).
+        # With two extractor pairs and no lane offset it measured 1-2 % slower (r05bd); with
+        # the offset and four pairs it is the faster form (r05ca-cc, interleaved: three pairs
+        # on one stream 57.0-58.0k stereo frames/s, on two 58.4-59.3k, four pairs on two
+        # 59.8-60.7k, five 59.8-60.0k).  ORBX_STEREO_TRACK_STREAM=0: one stream
         import os
-        self._own_ts = stream_create(device, 1, 0) if os.environ.get("ORBX_STEREO_TRACK_STREAM") == "1" else None
+        self._own_ts = stream_create(device, 1, 0) if os.environ.get("ORBX_STEREO_TRACK_STREAM", "1") == "1" \
+            else None
         self.ts = torch.cuda.ExternalStream(self._own_ts, device=self.dev) if self._own_ts else self.ms
         # extractor pairs in rotation: a set is re-extracted only after the matching that last
-        # read it (ev_m).  Three: with the right image's lane offset (below) the matching stream
-        # no longer keeps up with two (r05bq-br, interleaved: two sets 54.7-54.9k stereo
-        # frames/s, three 57.2-58.2k, four 56.6-57.6k; before the offset three measured 0.8 %
-        # slower, r05ap).  ORBX_STEREO_SETS overrides
-        self.nsets = max(2, int(os.environ.get("ORBX_STEREO_SETS", "3")))
+        # read it (ev_m).  Four: with the right image's lane offset (below) the matching no
+        # longer keeps up with two (r05bq-br, one matcher stream, interleaved: two sets
+        # 54.7-54.9k stereo frames/s, three 57.2-58.2k, four 56.6-57.6k; before the offset
+        # three measured 0.8 % slower, r05ap), and with the tracking on its own stream four
+        # beat three (above).  ORBX_STEREO_SETS overrides
+        self.nsets = max(2, int(os.environ.get("ORBX_STEREO_SETS", "4")))
         self.sets = [(ORBextractor(*params, device=device), ORBextractor(*params, device=device))
                      for _ in range(self.nsets)]
         # level 0 read from the caller's frames when their rows are 64-byte aligned
