@@ -106,7 +106,10 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=128, help="stereo frames per step")
+    # 256 stereo frames per step, as configs[1]'s batch: 62.3k stereo frames/s against
+    # 59.5-60.4k at 128 and 55.7-55.9k at 64 (r05cj-ck, interleaved; bit-exact on all 256
+    # frames and 255 pairs)
+    ap.add_argument("--batch", type=int, default=256, help="stereo frames per step")
     ap.add_argument("--no-track", action="store_true", help="extraction + stereo matching only (round-4 step)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
