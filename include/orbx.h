@@ -350,6 +350,9 @@ typedef struct {
                                      NULL: every MapPoint has Observations() > 0.  A claim by a MapPoint
                                      with 0 observations (UpdateLastFrame's temporal points) does not
                                      block the keypoint (ORBmatcher.cc:1716-1718) */
+    int retry_below;              /* TrackWithMotionModel's retry (Tracking.cc:988-994): a pair with fewer
+                                     than retry_below matches is searched again from an empty
+                                     mvpMapPoints at 2*th (the reference: 20); 0 = one search */
 } orbx_sequence;
 int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* seq, void* stream);
 
@@ -626,6 +629,48 @@ int orbx_update_last_frame_device(int batch, const orbx_keypoint* d_kps, const i
                                   const float* d_depth, const float* d_Tcw, float fx, float fy, float cx, float cy,
                                   float th_depth, const int32_t* d_obs_in, const float* d_pos_in, int32_t* d_mp_obs,
                                   float* d_mp_pos, uint8_t* d_has_mp, void* stream);
+
+/* ---- RGB-D Frame (configs[4]) ----
+ * Frame::Frame(imGray, imDepth, ...) for RGB-D (Frame.cc:192-264) after ExtractORB:
+ * UndistortKeyPoints (Frame.cc:586-628) and ComputeStereoFromRGBD (Frame.cc:888-909), with
+ * Tracking::GrabImageRGBD's depth conversion (Tracking.cc:265-271) applied to the pixels the
+ * lookup reads.  For keypoint i (mvKeys[i] = kps, mvKeysUn[i] = kps_un):
+ *   d = imDepth.at<float>((int)kp.y, (int)kp.x), imDepth = the depth image converted to
+ *       CV_32F with scale mDepthMapFactor (= 1 / DepthMapFactor, Tracking.cc:166-170):
+ *       a u16 image always (d = (float)raw * factor), an f32 image only when
+ *       |factor - 1| > 1e-5 (d = raw * factor), else as is;
+ *   d > 0: mvDepth[i] = d, mvuRight[i] = kpU.x - mbf / d; otherwise both -1.
+ * A keypoint outside the depth image (never one the extractor produced) gets -1 (the
+ * reference's Mat::at would read out of bounds). */
+#define ORBX_DEPTH_U16 0
+#define ORBX_DEPTH_F32 1
+typedef struct {
+    int batch;                   /* B frames in the orbx_extract_batch_device layout */
+    const orbx_keypoint* kps;    /* [B][cap] mvKeys (device): the depth lookup positions */
+    orbx_keypoint* kps_un;       /* [B][cap] mvKeysUn (device): written when a camera is given,
+                                    read otherwise */
+    const int32_t* n;            /* [B] keypoint counts */
+    int cap;
+    const void* depth;           /* frame b's depth image at depth + b*frame_bytes, rows
+                                    row_bytes apart (device) */
+    int depth_type;              /* ORBX_DEPTH_U16 (TUM's 16-bit PNG) or ORBX_DEPTH_F32 */
+    int width, height;           /* depth image size (the gray image's) */
+    long long row_bytes, frame_bytes;
+    float depth_map_factor;      /* Tracking's mDepthMapFactor (1 / DepthMapFactor) */
+    float bf;                    /* mbf */
+    float* u_right;              /* [B][cap] out: mvuRight (slots >= n[b]: -1) */
+    float* depth_out;            /* [B][cap] out: mvDepth (slots >= n[b]: -1) */
+} orbx_rgbd_batch;
+/* cam non-NULL: UndistortKeyPoints into kps_un and the depth lookup in one pass; NULL:
+ * kps_un holds mvKeysUn already.  Asynchronous on `stream`. */
+int orbx_compute_stereo_from_rgbd_device(const orbx_camera* cam, const orbx_rgbd_batch* rb, void* stream);
+/* One RGB-D Frame from host buffers (the drop-in Frame constructor): n keypoints, a
+ * width x height depth image with rows row_bytes apart.  keys_un: out when cam is
+ * non-NULL, else in.  u_right / depth_out: n floats. */
+int orbx_compute_stereo_from_rgbd(int device, const orbx_camera* cam, const orbx_keypoint* keys, int n,
+                                  const void* depth, int depth_type, int width, int height, size_t row_bytes,
+                                  float depth_map_factor, float bf, orbx_keypoint* keys_un, float* u_right,
+                                  float* depth_out);
 
 /* ---- DBoW2 vocabulary (TemplatedVocabulary<FORB::TDescriptor, FORB>, §8(f) rank 1) ----
  * The tree lives in HBM as its CSR edge list.  Scoring / weighting

@@ -462,6 +462,47 @@ def sbp_frame(cur, cur_mp, last, last_mp, mps, th, mono, check_ori, last_outlier
                            1 if mono else 0, 1 if check_ori else 0)
 
 
+def track_motion_model(cur, cur_mp, last, last_mp, mps, th, mono, check_ori, last_outlier=None):
+    """Tracking::TrackWithMotionModel's search (Tracking.cc:975-994): SearchByProjection at th
+    and, with fewer than 20 matches, again from an empty cur_mp at 2*th.  cur_mp is
+    overwritten.  -> (nmatches, retried)."""
+    keep = []
+    fc = _frame(cur, keep)
+    fl = _frame(last, keep)
+    m = _mappoints(mps, keep)
+    lm = np.ascontiguousarray(last_mp, dtype=np.int32)
+    lo = None if last_outlier is None else np.ascontiguousarray(last_outlier, dtype=np.uint8)
+    retried = C.c_int()
+    L = lib()
+    L.ora_track_motion_model.argtypes = [C.c_void_p, I32P, C.c_void_p, I32P, U8P, C.c_void_p, C.c_float, C.c_int,
+                                         C.c_int, C.POINTER(C.c_int)]
+    nm = L.ora_track_motion_model(C.addressof(fc), cur_mp.ctypes.data_as(I32P), C.addressof(fl),
+                                  lm.ctypes.data_as(I32P), lo.ctypes.data_as(U8P) if lo is not None else None,
+                                  C.addressof(m), th, 1 if mono else 0, 1 if check_ori else 0, C.byref(retried))
+    return nm, bool(retried.value)
+
+
+def compute_stereo_from_rgbd(keys, keys_un, depth, bf, depth_map_factor):
+    """Frame::ComputeStereoFromRGBD (Frame.cc:888-909) on GrabImageRGBD's converted depth
+    image (Tracking.cc:265-271): depth (H, W) uint16 or float32 -> (mvuRight, mvDepth)."""
+    keys = np.ascontiguousarray(keys, dtype=KEYPOINT_DTYPE)
+    keys_un = np.ascontiguousarray(keys_un, dtype=KEYPOINT_DTYPE)
+    img = np.ascontiguousarray(depth)
+    if img.dtype not in (np.uint16, np.float32):
+        raise ValueError("depth image must be uint16 or float32")
+    n = len(keys)
+    ur = np.zeros(max(n, 1), np.float32)
+    dp = np.zeros(max(n, 1), np.float32)
+    L = lib()
+    L.ora_compute_stereo_from_rgbd.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int,
+                                               C.c_int, C.c_longlong, C.c_float, C.c_float, F32P, F32P]
+    L.ora_compute_stereo_from_rgbd.restype = None
+    L.ora_compute_stereo_from_rgbd(keys.ctypes.data, keys_un.ctypes.data, n, img.ctypes.data,
+                                   1 if img.dtype == np.float32 else 0, img.shape[1], img.shape[0], img.strides[0],
+                                   float(depth_map_factor), float(bf), ur.ctypes.data_as(F32P), dp.ctypes.data_as(F32P))
+    return ur[:n].copy(), dp[:n].copy()
+
+
 def sbp_keyframe(cur, cur_mp, kf, kf_mp, mps, th, orb_dist, check_ori, already_found=None):
     """ORBmatcher::SearchByProjection(Frame&, KeyFrame*, set, th, ORBdist) restated;
     cur_mp updated in place, returns nmatches."""

@@ -1368,3 +1368,56 @@ void ora_distinctive_descriptors(int nmp, const int32_t* off, const uint8_t* des
         free(row);
     }
 }
+
+/* ---------------------------------------------------------------- RGB-D Frame */
+
+/* Frame::ComputeStereoFromRGBD (Frame.cc:888-909) on the image Tracking::GrabImageRGBD
+ * hands the Frame (Tracking.cc:265-271): imDepth.convertTo(imDepth, CV_32F,
+ * mDepthMapFactor) whenever |mDepthMapFactor - 1| > 1e-5 or the image is not CV_32F.
+ * OpenCV 3.3.1's cvtScale16u32f / cvtScale32f compute in float: (float)src * (float)alpha
+ * + (float)beta with beta = 0 (recalled, unpinned; the + 0 is exact either way).  Then for
+ * keypoint i: d = imDepth.at<float>(v, u) with v = kp.pt.y, u = kp.pt.x of the distorted
+ * keypoint converted to int (truncation), and where d > 0: mvDepth[i] = d, mvuRight[i] =
+ * kpU.pt.x - mbf / d; otherwise both stay -1 (cc:889-890).  A keypoint outside the image
+ * (never one the extractor produced) is given -1 here; the reference reads out of bounds. */
+void ora_compute_stereo_from_rgbd(const ora_keypoint* keys, const ora_keypoint* keys_un, int n, const void* depth,
+                                  int depth_f32, int width, int height, long long row_bytes, float depth_map_factor,
+                                  float bf, float* u_right, float* out_depth) {
+    const int convert = (fabsf(depth_map_factor - 1.0f) > 1e-5f) || !depth_f32;
+    for (int i = 0; i < n; i++) {
+        u_right[i] = -1.0f;
+        out_depth[i] = -1.0f;
+        const float v = keys[i].y, u = keys[i].x;
+        const int iv = (int)v, iu = (int)u;
+        if (iv < 0 || iv >= height || iu < 0 || iu >= width) continue;
+        const unsigned char* row = (const unsigned char*)depth + (size_t)iv * (size_t)row_bytes;
+        float d;
+        if (depth_f32) {
+            d = ((const float*)row)[iu];
+            if (convert) d = d * depth_map_factor;
+        } else {
+            d = (float)((const uint16_t*)row)[iu] * depth_map_factor;
+        }
+        if (d > 0) {
+            out_depth[i] = d;
+            u_right[i] = keys_un[i].x - bf / d;
+        }
+    }
+}
+
+/* Tracking::TrackWithMotionModel's search (Tracking.cc:975-994): mvpMapPoints emptied,
+ * SearchByProjection(CurrentFrame, LastFrame, th, bMono); with fewer than 20 matches,
+ * emptied again and searched at 2*th.  *retried (optional) reports the second search. */
+int ora_track_motion_model(const ora_frame* cur, int32_t* cur_mp, const ora_frame* last, const int32_t* last_mp,
+                           const uint8_t* last_outlier, const ora_mappoints* mps, float th, int bMono, int check_ori,
+                           int* retried) {
+    for (int i = 0; i < cur->n; i++) cur_mp[i] = -1;
+    int nm = ora_sbp_frame(cur, cur_mp, last, last_mp, last_outlier, mps, th, bMono, check_ori);
+    if (retried) *retried = 0;
+    if (nm < 20) {
+        for (int i = 0; i < cur->n; i++) cur_mp[i] = -1;
+        nm = ora_sbp_frame(cur, cur_mp, last, last_mp, last_outlier, mps, 2 * th, bMono, check_ori);
+        if (retried) *retried = 1;
+    }
+    return nm;
+}

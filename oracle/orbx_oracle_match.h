@@ -104,6 +104,17 @@ void ora_compute_stereo_matches(const ora_frame* left, const ora_keypoint* keys_
                                 const uint8_t* const* levels_l, const uint8_t* const* levels_r, const int* level_w,
                                 const int* level_h, const float* inv_scale, float maxD, float* u_right, float* depth);
 
+/* Frame::ComputeStereoFromRGBD (Frame.cc:888-909) after Tracking::GrabImageRGBD's
+ * convertTo(CV_32F, mDepthMapFactor) (Tracking.cc:265-271). */
+void ora_compute_stereo_from_rgbd(const ora_keypoint* keys, const ora_keypoint* keys_un, int n, const void* depth,
+                                  int depth_f32, int width, int height, long long row_bytes, float depth_map_factor,
+                                  float bf, float* u_right, float* out_depth);
+/* Tracking::TrackWithMotionModel's search (Tracking.cc:975-994): SearchByProjection at th,
+ * again at 2*th from an empty mvpMapPoints when it found fewer than 20 matches. */
+int ora_track_motion_model(const ora_frame* cur, int32_t* cur_mp, const ora_frame* last, const int32_t* last_mp,
+                           const uint8_t* last_outlier, const ora_mappoints* mps, float th, int bMono, int check_ori,
+                           int* retried);
+
 /* H4: 1 (default) = the reference build's fused projection / epipolar forms, 0 = unfused */
 void ora_set_match_contract_mode(int mode);
 

@@ -50,8 +50,11 @@ EXPORTED = [
     "orbx_extractor_set_node_capacity", "orbx_extractor_set_level0_in_place", "orbx_compute_stereo_matches_batch_device",
     "orbx_search_for_triangulation_batch_device", "orbx_match_sequence_device_ex",
     "orbx_search_local_points_device", "orbx_create_mappoints_device", "orbx_update_last_frame_device",
-    "orbx_extractor_last_call_us",
+    "orbx_extractor_last_call_us", "orbx_compute_stereo_from_rgbd", "orbx_compute_stereo_from_rgbd_device",
 ]
+
+ORBX_DEPTH_U16 = 0
+ORBX_DEPTH_F32 = 1
 
 
 class Camera(C.Structure):
@@ -72,7 +75,16 @@ class Sequence(C.Structure):
                 ("bf", C.c_float), ("b", C.c_float), ("min_x", C.c_float), ("max_x", C.c_float),
                 ("min_y", C.c_float), ("max_y", C.c_float), ("nlevels", C.c_int),
                 ("scale_factors", C.POINTER(C.c_float)), ("th", C.c_float), ("mono", C.c_int),
-                ("global_ids", C.c_int), ("cur_mp", C.c_void_p), ("nmatches", C.c_void_p), ("mp_obs", C.c_void_p)]
+                ("global_ids", C.c_int), ("cur_mp", C.c_void_p), ("nmatches", C.c_void_p), ("mp_obs", C.c_void_p),
+                ("retry_below", C.c_int)]
+
+
+class RgbdBatch(C.Structure):
+    """orbx_rgbd_batch (include/orbx.h)."""
+    _fields_ = [("batch", C.c_int), ("kps", C.c_void_p), ("kps_un", C.c_void_p), ("n", C.c_void_p), ("cap", C.c_int),
+                ("depth", C.c_void_p), ("depth_type", C.c_int), ("width", C.c_int), ("height", C.c_int),
+                ("row_bytes", C.c_longlong), ("frame_bytes", C.c_longlong), ("depth_map_factor", C.c_float),
+                ("bf", C.c_float), ("u_right", C.c_void_p), ("depth_out", C.c_void_p)]
 
 
 class MapPointsDevice(C.Structure):
@@ -183,6 +195,9 @@ def lib() -> C.CDLL:
     L.orbx_undistort_keypoints.argtypes = [C.c_int, cp, vp, C.c_int, vp]
     L.orbx_undistort_keypoints_device.argtypes = [cp, C.c_int, vp, vp, C.c_int, vp, vp]
     L.orbx_compute_image_bounds.argtypes = [C.c_int, cp, C.c_int, C.c_int, fp]
+    L.orbx_compute_stereo_from_rgbd_device.argtypes = [cp, C.POINTER(RgbdBatch), vp]
+    L.orbx_compute_stereo_from_rgbd.argtypes = [C.c_int, cp, vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_size_t,
+                                                C.c_float, C.c_float, vp, fp, fp]
     L.orbx_assign_features_to_grid.argtypes = [C.c_int, vp, C.c_int, fp, i32p, i32p]
     L.orbx_assign_features_to_grid_device.argtypes = [C.c_int, vp, vp, C.c_int, fp, vp, vp, vp]
     L.orbx_fuse.argtypes = [vp, vp, i32p, C.c_int, u8p, vp, C.c_float, i32p]

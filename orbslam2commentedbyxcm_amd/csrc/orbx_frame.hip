@@ -13,6 +13,7 @@
 // ascending index order like the reference's push_back loop, and written as CSR.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -76,6 +77,68 @@ __global__ __launch_bounds__(256) void k_undistort(CamDev C, const orbx_keypoint
     orbx_keypoint kp = kin[s];
     if (C.enabled) undistort_point(C, kp.x, kp.y, kp.x, kp.y);
     kout[s] = kp;
+}
+
+// The RGB-D Frame's steps after ExtractORB (Frame.cc:227-230), one thread per keypoint
+// slot: UndistortKeyPoints (UNDIST; else mvKeysUn is read) and ComputeStereoFromRGBD
+// (Frame.cc:888-909) with GrabImageRGBD's convertTo(CV_32F, mDepthMapFactor)
+// (Tracking.cc:265-271) applied to the one pixel each keypoint reads -- the conversion is
+// per pixel, so converting only what is read gives the same floats without a pass over
+// the image.  OpenCV 3.3.1's cvtScale to 32F computes in float: d = (float)src * scale
+// (+ 0, exact).  The lookup index is imDepth.at<float>(v, u) of the distorted keypoint:
+// float -> int conversions, i.e. truncation (the coordinates are >= 0).
+struct RgbdArgs {
+    const orbx_keypoint* kps;
+    orbx_keypoint* kps_un;
+    const int32_t* n;
+    int cap;
+    const unsigned char* depth;
+    long long row_bytes, frame_bytes;
+    int width, height;
+    int f32;        // depth image of floats (else u16)
+    int scale;      // apply `factor` (u16: always; f32: when |factor - 1| > 1e-5)
+    float factor;   // mDepthMapFactor
+    float bf;
+    float* u_right;
+    float* depth_out;
+};
+
+template <bool UNDIST>
+__global__ __launch_bounds__(256) void k_rgbd_frame(CamDev C, RgbdArgs A) {
+    const int b = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= A.cap) return;
+    const int n = min(A.n[b], A.cap);
+    const size_t s = (size_t)b * A.cap + i;
+    float ur = -1.f, dd = -1.f;
+    if (i < n) {
+        const orbx_keypoint kp = A.kps[s];
+        orbx_keypoint kpu;
+        if constexpr (UNDIST) {
+            kpu = kp;
+            if (C.enabled) undistort_point(C, kp.x, kp.y, kpu.x, kpu.y);
+            A.kps_un[s] = kpu;
+        } else {
+            kpu = A.kps_un[s];
+        }
+        const int v = (int)kp.y, u = (int)kp.x;  // Mat::at<float>(int, int) of float arguments
+        if (v >= 0 && v < A.height && u >= 0 && u < A.width) {
+            const unsigned char* row = A.depth + (size_t)b * A.frame_bytes + (size_t)v * A.row_bytes;
+            float d;
+            if (A.f32) {
+                d = ((const float*)row)[u];
+                if (A.scale) d = __fmul_rn(d, A.factor);
+            } else {
+                d = __fmul_rn((float)((const uint16_t*)row)[u], A.factor);
+            }
+            if (d > 0) {
+                dd = d;
+                ur = __fsub_rn(kpu.x, __fdiv_rn(A.bf, d));  // kpU.pt.x - mbf / d
+            }
+        }
+    }
+    A.u_right[s] = ur;
+    A.depth_out[s] = dd;
 }
 
 // Image corners for ComputeImageBounds (4 points)
@@ -277,7 +340,7 @@ __global__ __launch_bounds__(kLastFrameThreads) void k_update_last_frame(LastFra
                         int rank = 0;
                         for (int j = 0; j < n && rank < kb; j++) {
                             const float zj = dep[j];
-                            if (zj > A.th_depth)
+                            if (zj > 0 && zj > A.th_depth)  // the pairs with depth only (cc:909-913)
                                 rank += ((unsigned long long)__float_as_uint(zj) << 32 | (unsigned)j) < k;
                         }
                         visited = rank < kb;
@@ -493,6 +556,100 @@ int orbx_update_last_frame_device(int batch, const orbx_keypoint* d_kps, const i
     hipLaunchKernelGGL(k_update_last_frame, dim3(batch), dim3(kLastFrameThreads), 0, (hipStream_t)stream, A);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(ORBX_ERR_HIP, hipGetErrorString(e));
+    return ORBX_OK;
+}
+
+int orbx_compute_stereo_from_rgbd_device(const orbx_camera* cam, const orbx_rgbd_batch* rb, void* stream) {
+    if (!rb || rb->batch < 0 || rb->cap < 0) return fail(ORBX_ERR_ARG, "bad argument");
+    if (!rb->batch || !rb->cap) return ORBX_OK;
+    if (!rb->kps || !rb->kps_un || !rb->n || !rb->depth || !rb->u_right || !rb->depth_out)
+        return fail(ORBX_ERR_ARG, "null buffer");
+    if (rb->depth_type != ORBX_DEPTH_U16 && rb->depth_type != ORBX_DEPTH_F32)
+        return fail(ORBX_ERR_ARG, "depth_type must be ORBX_DEPTH_U16 or ORBX_DEPTH_F32");
+    const long long px = rb->depth_type == ORBX_DEPTH_U16 ? 2 : 4;
+    if (rb->width <= 0 || rb->height <= 0 || rb->row_bytes < px * rb->width || rb->row_bytes % px ||
+        (rb->batch > 1 && rb->frame_bytes < rb->row_bytes * rb->height) || rb->frame_bytes % px ||
+        (uintptr_t)rb->depth % px)
+        return fail(ORBX_ERR_ARG, "depth image geometry (sizes, row / frame strides, alignment)");
+    RgbdArgs A{};
+    A.kps = rb->kps;
+    A.kps_un = rb->kps_un;
+    A.n = rb->n;
+    A.cap = rb->cap;
+    A.depth = (const unsigned char*)rb->depth;
+    A.row_bytes = rb->row_bytes;
+    A.frame_bytes = rb->frame_bytes;
+    A.width = rb->width;
+    A.height = rb->height;
+    A.f32 = rb->depth_type == ORBX_DEPTH_F32;
+    // Tracking.cc:266: a CV_32F image is converted only when the factor is not ~1; the
+    // conversion from 16U always runs (with alpha == 1 it is the plain conversion, equal
+    // to a multiply by 1.0f)
+    A.scale = !A.f32 || std::fabs(rb->depth_map_factor - 1.0f) > 1e-5;
+    A.factor = rb->depth_map_factor;
+    A.bf = rb->bf;
+    A.u_right = rb->u_right;
+    A.depth_out = rb->depth_out;
+    const dim3 g((rb->cap + 255) / 256, rb->batch);
+    if (cam) {
+        hipLaunchKernelGGL(k_rgbd_frame<true>, g, dim3(256), 0, (hipStream_t)stream, cam_dev(cam), A);
+    } else {
+        hipLaunchKernelGGL(k_rgbd_frame<false>, g, dim3(256), 0, (hipStream_t)stream, CamDev{}, A);
+    }
+    HIP_TRY(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbx_compute_stereo_from_rgbd(int device, const orbx_camera* cam, const orbx_keypoint* keys, int n,
+                                  const void* depth, int depth_type, int width, int height, size_t row_bytes,
+                                  float depth_map_factor, float bf, orbx_keypoint* keys_un, float* u_right,
+                                  float* depth_out) {
+    if (n < 0 || (n && (!keys || !keys_un || !u_right || !depth_out || !depth))) return fail(ORBX_ERR_ARG, "bad argument");
+    if (n == 0) return ORBX_OK;  // Frame.cc:223-224: no keypoints, nothing computed
+    if (depth_type != ORBX_DEPTH_U16 && depth_type != ORBX_DEPTH_F32) return fail(ORBX_ERR_ARG, "bad depth_type");
+    const size_t px = depth_type == ORBX_DEPTH_U16 ? 2 : 4;
+    if (width <= 0 || height <= 0 || row_bytes < px * (size_t)width) return fail(ORBX_ERR_ARG, "bad depth image");
+    HIP_TRY(hipSetDevice(device));
+    const size_t ib = px * (size_t)width * height, kb = sizeof(orbx_keypoint) * (size_t)n, fb = sizeof(float) * (size_t)n;
+    char* d = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, ib + 2 * kb + 2 * fb + 256));
+    orbx_keypoint* d_k = (orbx_keypoint*)d;
+    orbx_keypoint* d_ku = d_k + n;
+    float* d_ur = (float*)(d + 2 * kb);
+    float* d_dp = d_ur + n;
+    int32_t* d_n = (int32_t*)(d + 2 * kb + 2 * fb);
+    void* d_img = d + 2 * kb + 2 * fb + 16;
+    d_img = (void*)(((uintptr_t)d_img + 15) & ~(uintptr_t)15);
+    hipError_t e = hipMemcpy2D(d_img, px * width, depth, row_bytes, px * width, height, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_k, keys, kb, hipMemcpyHostToDevice);
+    if (e == hipSuccess && !cam) e = hipMemcpy(d_ku, keys_un, kb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_n, &n, sizeof(int32_t), hipMemcpyHostToDevice);
+    int rc = ORBX_OK;
+    if (e == hipSuccess) {
+        orbx_rgbd_batch rb{};
+        rb.batch = 1;
+        rb.kps = d_k;
+        rb.kps_un = d_ku;
+        rb.n = d_n;
+        rb.cap = n;
+        rb.depth = d_img;
+        rb.depth_type = depth_type;
+        rb.width = width;
+        rb.height = height;
+        rb.row_bytes = (long long)(px * width);
+        rb.frame_bytes = (long long)ib;
+        rb.depth_map_factor = depth_map_factor;
+        rb.bf = bf;
+        rb.u_right = d_ur;
+        rb.depth_out = d_dp;
+        rc = orbx_compute_stereo_from_rgbd_device(cam, &rb, nullptr);
+    }
+    if (e == hipSuccess && rc == ORBX_OK && cam) e = hipMemcpy(keys_un, d_ku, kb, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && rc == ORBX_OK) e = hipMemcpy(u_right, d_ur, fb, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && rc == ORBX_OK) e = hipMemcpy(depth_out, d_dp, fb, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (rc != ORBX_OK) return rc;
+    HIP_TRY(e);
     return ORBX_OK;
 }
 

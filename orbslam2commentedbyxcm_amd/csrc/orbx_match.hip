@@ -1466,6 +1466,7 @@ __device__ __forceinline__ void proj_search_body(const ProjProblem* __restrict__
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_hist[kHistoLength];
     const ProjProblem pb = probs[blockIdx.x];
+    if (pb.nq < 0) return;  // a pair the retry pass skips (k_seq_build): whole workgroup
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int kWaves = NT / 64;
     const int n = pb.n, nq = pb.nq;
@@ -1685,6 +1686,7 @@ __global__ __launch_bounds__(kSeqGridThreads) void k_seq_grid(const ProjProblem*
     if (st) st[0] = wall_clock64();
     if (st) st[1] = wall_clock64();
     const ProjProblem pb = probs[blockIdx.x];
+    if (pb.nq < 0) return;  // skipped by the retry pass
     const SeqGridLayout gl(cap, noct);
     unsigned char* gb = grids + (size_t)blockIdx.x * gl.total;
     const int tid = threadIdx.x, n = pb.n;
@@ -1770,6 +1772,7 @@ __global__ __launch_bounds__(RT) ORBX_COMMIT_ATTR void k_seq_commit(const ProjPr
     __builtin_amdgcn_s_setprio(3);
 #endif
     const ProjProblem pb = probs[blockIdx.x];
+    if (pb.nq < 0) return;  // skipped by the retry pass (k_seq_score's workgroups leave on nq too)
     unsigned long long* st = P.stamps ? P.stamps + kStampWords * blockIdx.x : nullptr;  // diagnostics
     if (st && threadIdx.x == 0) st[13] = wall_clock64();
     const SeqGridLayout gl(cap, P.noct);
@@ -1919,6 +1922,12 @@ __global__ __launch_bounds__(256) void k_seq_build(SeqArgs A, ProjQuery* __restr
     const int p = blockIdx.y;
     const int i = blockIdx.x * 256 + threadIdx.x;
     const int nlast = A.n[p];
+    // the retry pass (TrackWithMotionModel, Tracking.cc:988-994): only the pairs whose first
+    // search found fewer than retry_below matches are searched again, from an empty
+    // mvpMapPoints; the others keep the first search's results (problem nq = -1: every later
+    // kernel's workgroup leaves at once).  This launch never writes nmatches in the retry
+    // pass, so every thread of a pair reads the same gate.
+    const bool active = !A.retry_below || A.nmatches[p + 1] < A.retry_below;
     if (i == 0) {
         ProjProblem pb{};
         pb.keys = A.kps + (size_t)(p + 1) * A.cap;
@@ -1928,7 +1937,7 @@ __global__ __launch_bounds__(256) void k_seq_build(SeqArgs A, ProjQuery* __restr
         pb.n = A.n[p + 1] < A.cap ? A.n[p + 1] : A.cap;
         pb.q = queries + (size_t)p * A.cap;
         pb.qdesc = A.desc + (size_t)p * A.cap * 32;
-        pb.nq = nlast < A.cap ? nlast : A.cap;
+        pb.nq = !active ? -1 : (nlast < A.cap ? nlast : A.cap);
         pb.min_x = A.min_x;
         pb.min_y = A.min_y;
         pb.inv_w = (float)kGridCols / (A.max_x - A.min_x);
@@ -1937,13 +1946,16 @@ __global__ __launch_bounds__(256) void k_seq_build(SeqArgs A, ProjQuery* __restr
         probs[p] = pb;
         scratch_off[p] = (long long)p * kProjScratchWords * A.cap;
     }
-    if (i >= A.cap) return;
+    if (i >= A.cap || !active) return;
     // the outputs' initial state (no match), here rather than in two memsets: fewer
-    // launches on a stream that runs beside the extraction
+    // launches on a stream that runs beside the extraction (the retry pass: mvpMapPoints
+    // emptied again, Tracking.cc:990-991; its count is the replay's to write)
     A.cur_mp[(size_t)(p + 1) * A.cap + i] = -1;
-    if (p == 0) A.cur_mp[i] = -1;
-    if (i == 0) A.nmatches[p + 1] = 0;
-    if (p == 0 && i == 0) A.nmatches[0] = 0;
+    if (!A.retry_below) {
+        if (p == 0) A.cur_mp[i] = -1;
+        if (i == 0) A.nmatches[p + 1] = 0;
+        if (p == 0 && i == 0) A.nmatches[0] = 0;
+    }
     ProjQuery q{};
     q.mp = -1;
     const size_t slot = (size_t)p * A.cap + i;

@@ -97,6 +97,7 @@ struct SeqArgs {
     float scale[32];           // mvScaleFactors
     int32_t* cur_mp;           // [B][cap] out (pre-filled -1)
     int32_t* nmatches;         // [B] out
+    int retry_below;           // 0: the first search; > 0: the retry pass over the pairs with fewer matches
 };
 
 // Tracking::SearchLocalPoints over a batch of Frames (orbx_search_local_points_device):

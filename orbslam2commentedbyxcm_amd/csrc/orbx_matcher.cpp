@@ -720,6 +720,7 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
     if ((long long)batch * cap >= kMaxMapPointIds) return fail(ORBX_ERR_ARG, "batch x cap MapPoint ids >= 2^30");
     if (!sq->mono && !(sq->b > 0.f)) return fail(ORBX_ERR_ARG, "stereo / RGB-D sequence needs the baseline mb > 0");
     if (sq->mp_obs && !sq->global_ids) return fail(ORBX_ERR_ARG, "mp_obs is indexed by global MapPoint ids");
+    if (sq->retry_below < 0) return fail(ORBX_ERR_ARG, "retry_below must be >= 0");
     int32_t* d_cur_mp = sq->cur_mp;
     int32_t* d_nmatches = sq->nmatches;
     HIP_TRY(hipSetDevice(m->device));
@@ -803,6 +804,17 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
     } else {
         HIP_TRY(launch_proj_search(d_prob, npairs, P, d_scr, d_off, cap, cap, s, m->footprint == 1,
                                    m->footprint == 3, m->footprint == 4, m->footprint == 5 ? d_grids : nullptr));
+    }
+    if (sq->retry_below > 0) {
+        // Tracking::TrackWithMotionModel (Tracking.cc:988-994): pairs left with fewer than
+        // retry_below matches are searched again at 2*th.  The gate is read on the device
+        // (k_seq_build), so nothing synchronises; the skipped pairs' workgroups leave at
+        // once.  One lean launch (sort, scoring and replay in one workgroup per pair): the
+        // retried pairs are rare, the launch count is what the common case pays.
+        A.retry_below = sq->retry_below;
+        A.th = 2.f * sq->th;
+        HIP_TRY(launch_seq_build(A, npairs, d_q, d_prob, d_off, s));
+        HIP_TRY(launch_proj_search(d_prob, npairs, P, d_scr, d_off, cap, cap, s, false, false, true, nullptr));
     }
     if (m->timing) {
         HIP_TRY(hipEventRecord(ev[1], s));

@@ -57,3 +57,55 @@ def grid_device(d_keys_un, d_n, cap: int, bounds, d_cell_start, d_cell_idx, stre
                                                         C.c_void_p(d_cell_start.data_ptr()),
                                                         C.c_void_p(d_cell_idx.data_ptr()),
                                                         C.c_void_p(stream) if stream else None))
+
+
+def ComputeStereoFromRGBD(keys: np.ndarray, depth: np.ndarray, bf: float, depth_map_factor: float,
+                          cam: L.Camera | None = None, keys_un: np.ndarray | None = None, device: int = 0):
+    """The RGB-D Frame constructor's steps after ExtractORB (Frame.cc:227-230) for one frame
+    (orbx_compute_stereo_from_rgbd): UndistortKeyPoints when `cam` is given (else keys_un is
+    mvKeysUn), then ComputeStereoFromRGBD (Frame.cc:888-909) on the depth image (H, W)
+    uint16 or float32 converted as Tracking::GrabImageRGBD does (Tracking.cc:265-271, scale
+    depth_map_factor = mDepthMapFactor).  -> (mvKeysUn, mvuRight, mvDepth)."""
+    k = np.ascontiguousarray(keys, dtype=L.KEYPOINT_DTYPE)
+    img = np.ascontiguousarray(depth)
+    if img.dtype not in (np.uint16, np.float32):
+        raise ValueError("depth image must be uint16 or float32")
+    if cam is None:
+        if keys_un is None:
+            raise ValueError("keys_un is needed without a camera")
+        ku = np.array(keys_un, dtype=L.KEYPOINT_DTYPE, copy=True)
+    else:
+        ku = np.empty_like(k)
+    n = len(k)
+    ur = np.zeros(max(n, 1), np.float32)
+    dp = np.zeros(max(n, 1), np.float32)
+    L.check(L.lib().orbx_compute_stereo_from_rgbd(
+        device, C.byref(cam) if cam is not None else None, k.ctypes.data, n, img.ctypes.data,
+        L.ORBX_DEPTH_F32 if img.dtype == np.float32 else L.ORBX_DEPTH_U16, img.shape[1], img.shape[0],
+        img.strides[0], float(depth_map_factor), float(bf), ku.ctypes.data, ur.ctypes.data_as(F32P),
+        dp.ctypes.data_as(F32P)))
+    return ku, ur[:n].copy(), dp[:n].copy()
+
+
+def rgbd_device(cam, d_kps, d_n, d_depth, bf: float, depth_map_factor: float, d_kps_un, d_u_right, d_depth_out,
+                stream=None):
+    """Batched RGB-D Frame steps (orbx_compute_stereo_from_rgbd_device) over torch tensors:
+    d_kps / d_kps_un (B, cap, 7) int32 keypoint rows, d_n (B,), d_depth (B, H, W) uint16 or
+    float32 depth images (any row pitch), outputs d_u_right / d_depth_out (B, cap) float32.
+    cam None: d_kps_un already holds mvKeysUn.  Asynchronous."""
+    import torch
+    rb = L.RgbdBatch()
+    rb.batch, rb.cap = int(d_n.numel()), int(d_kps.shape[1])
+    rb.kps, rb.kps_un, rb.n = d_kps.data_ptr(), d_kps_un.data_ptr(), d_n.data_ptr()
+    rb.depth = d_depth.data_ptr()
+    rb.depth_type = L.ORBX_DEPTH_F32 if d_depth.dtype == torch.float32 else L.ORBX_DEPTH_U16
+    if d_depth.dtype not in (torch.float32, torch.uint16) or d_depth.stride(2) != 1:
+        raise ValueError("depth images must be uint16 or float32 with unit column stride")
+    es = d_depth.element_size()
+    rb.height, rb.width = int(d_depth.shape[1]), int(d_depth.shape[2])
+    rb.row_bytes, rb.frame_bytes = int(d_depth.stride(1)) * es, int(d_depth.stride(0)) * es
+    rb.depth_map_factor, rb.bf = float(depth_map_factor), float(bf)
+    rb.u_right, rb.depth_out = d_u_right.data_ptr(), d_depth_out.data_ptr()
+    L.check(L.lib().orbx_compute_stereo_from_rgbd_device(C.byref(cam) if cam is not None else None, C.byref(rb),
+                                                         C.c_void_p(getattr(stream, "cuda_stream", stream))
+                                                         if stream else None))

@@ -433,12 +433,16 @@ class ORBmatcher:
     def match_sequence_device_ex(self, d_kps, d_desc, d_n, d_Tcw, d_cur_mp, d_nmatches, scale_factors, fx, fy, cx,
                                  cy, width, height, th: float = 15.0, mono: bool = True, bf: float = 0.0,
                                  b: float = 0.0, d_u_right=None, d_mp_pos=None, d_has_mp=None, depth: float = 5.0,
-                                 global_ids: bool = False, d_mp_obs=None, stream=None) -> None:
+                                 global_ids: bool = False, d_mp_obs=None, retry_below: int = 0,
+                                 bounds=None, stream=None) -> None:
         """orbx_match_sequence_device_ex: TrackWithMotionModel's SearchByProjection(frame b,
         frame b-1, th, mono) for every b >= 1 of a device sequence, stereo included
         (d_u_right (B, cap) f32), LastFrame MapPoints at d_mp_pos (B, cap, 3) f32 (or at
         `depth` on the keypoint rays), d_has_mp (B, cap) u8 masking keypoints without one,
-        d_mp_obs (B, cap) i32 their Observations() (global ids; default: all > 0)."""
+        d_mp_obs (B, cap) i32 their Observations() (global ids; default: all > 0);
+        retry_below: TrackWithMotionModel's retry at 2*th of the pairs with fewer matches
+        (Tracking.cc:988-994: 20; 0 = none); bounds: (mnMinX, mnMaxX, mnMinY, mnMaxY)
+        (default: the image, 0..width x 0..height)."""
         B, cap = d_desc.shape[0], d_desc.shape[1]
         sf = _f32(scale_factors)
         ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
@@ -447,12 +451,14 @@ class ORBmatcher:
         q.kps, q.desc, q.n, q.Tcw = ptr(d_kps), ptr(d_desc), ptr(d_n), ptr(d_Tcw)
         q.u_right, q.mp_pos, q.has_mp = ptr(d_u_right), ptr(d_mp_pos), ptr(d_has_mp)
         q.depth, q.fx, q.fy, q.cx, q.cy, q.bf, q.b = depth, fx, fy, cx, cy, bf, b
-        q.min_x, q.max_x, q.min_y, q.max_y = 0.0, float(width), 0.0, float(height)
+        q.min_x, q.max_x, q.min_y, q.max_y = (0.0, float(width), 0.0, float(height)) if bounds is None \
+            else tuple(float(x) for x in bounds)
         q.nlevels = len(sf)
         q.scale_factors = sf.ctypes.data_as(F32P)
         q.th, q.mono, q.global_ids = th, 1 if mono else 0, 1 if global_ids else 0
         q.cur_mp, q.nmatches = ptr(d_cur_mp), ptr(d_nmatches)
         q.mp_obs = ptr(d_mp_obs)
+        q.retry_below = int(retry_below)
         s = None if stream is None else C.c_void_p(getattr(stream, "cuda_stream", stream))
         L.check(L.lib().orbx_match_sequence_device_ex(self._h, C.byref(q), s))
 

@@ -166,11 +166,14 @@ def plane_views(seed: int, rel_poses, width: int = 640, height: int = 480, fx: f
     return views, depths
 
 
-def _plane_hits(T, width, height, fx, fy, cx, cy, z0, pixels=None):
+def _plane_hits(T, width, height, fx, fy, cx, cy, z0, pixels=None, rays=None):
     """Canvas coordinates (px, py) and ray depth s where camera T's pixel rays meet the
-    plane Z = z0 of the reference camera (every pixel, or the (u, v) rows of `pixels`)."""
+    plane Z = z0 of the reference camera (every pixel, or the (u, v) rows of `pixels`, or
+    the given unit-z camera rays)."""
     Kinv = np.array([[1 / fx, 0, -cx / fx], [0, 1 / fy, -cy / fy], [0, 0, 1]], np.float64)
-    if pixels is None:
+    if rays is not None:
+        pass
+    elif pixels is None:
         vv, uu = np.mgrid[0:height, 0:width].astype(np.float64)
         rays = np.stack([uu, vv, np.ones_like(uu)], -1) @ Kinv.T
     else:
@@ -189,16 +192,23 @@ def _plane_hits(T, width, height, fx, fy, cx, cy, z0, pixels=None):
     return fx * X[..., 0] / z0 + cx, fy * X[..., 1] / z0 + cy, s
 
 
-_PLANE_CANVAS = None  # (canvas, mx, my): shared with forked render workers
+_PLANE_CANVAS = None  # (canvas, mx, my[, rays]): shared with forked render workers
 
 
 def _render_plane_view(args):
-    T, width, height, fx, fy, cx, cy, z0 = args
-    canvas, mx, my = _PLANE_CANVAS
+    T, width, height, fx, fy, cx, cy, z0 = args[:8]
+    canvas, mx, my = _PLANE_CANVAS[:3]
+    rays = _PLANE_CANVAS[3] if len(_PLANE_CANVAS) > 3 else None
+    px, py, s = _plane_hits(T, width, height, fx, fy, cx, cy, z0, rays=rays)
+    if len(args) > 8:  # RGB-D: the view and its registered depth image
+        img = _sample(canvas, px + mx, py + my)
+        return img, _depth_image(s, *args[8:])
+    return _sample(canvas, px + mx, py + my)
+
+
+def _sample(canvas, px, py):
+    """Bilinear canvas read at (px, py), rounded to u8."""
     H, W = canvas.shape
-    px, py, _ = _plane_hits(T, width, height, fx, fy, cx, cy, z0)
-    px = px + mx
-    py = py + my
     x0 = np.clip(np.floor(px).astype(np.int64), 0, W - 2)
     y0 = np.clip(np.floor(py).astype(np.int64), 0, H - 2)
     ax = np.clip(px - x0, 0.0, 1.0)
@@ -264,6 +274,119 @@ def plane_stereo_views(seed: int, rel_poses, baseline: float, width: int, height
         _PLANE_CANVAS = None
     n = len(rel_poses)
     return np.stack(views[:n]), np.stack(views[n:])
+
+
+# TUM freiburg1 (ORB-SLAM2's Examples/RGB-D/TUM1.yaml): intrinsics, distortion k1 k2 p1 p2
+# k3, Camera.bf, ThDepth, DepthMapFactor
+TUM1 = dict(fx=517.306408, fy=516.469215, cx=318.643040, cy=255.313989,
+            dist=(0.262383, -0.953104, -0.005358, 0.002628, 1.163314), bf=40.0, th_depth=40.0,
+            depth_map_factor=5000.0)
+
+
+def distorted_rays(width: int, height: int, fx: float, fy: float, cx: float, cy: float, dist, iters: int = 40):
+    """Unit-z camera rays (h, w, 3) of the pixels of a distorted image (OpenCV's
+    Brown-Conrady model, k1 k2 p1 p2 k3): each pixel's undistorted normalised coordinates by
+    fixed-point inversion in float64 (a rendering model, independent of the undistortion the
+    Frame restates)."""
+    k1, k2, p1, p2, k3 = (list(dist) + [0.0] * 5)[:5]
+    vv, uu = np.mgrid[0:height, 0:width].astype(np.float64)
+    xd, yd = (uu - cx) / fx, (vv - cy) / fy
+    x, y = xd.copy(), yd.copy()
+    for _ in range(iters):
+        r2 = x * x + y * y
+        radial = 1 + r2 * (k1 + r2 * (k2 + r2 * k3))
+        dx = 2 * p1 * x * y + p2 * (r2 + 2 * x * x)
+        dy = p1 * (r2 + 2 * y * y) + 2 * p2 * x * y
+        x, y = (xd - dx) / radial, (yd - dy) / radial
+    return np.stack([x, y, np.ones_like(x)], -1)
+
+
+def _depth_image(s, seed, depth_map_factor, holes):
+    """A TUM-style 16-bit depth image of per-pixel depths s (metres): round(s * factor),
+    saturated, with Kinect-like holes (0) when `holes`: a 6-12 px invalid band at the left
+    border (the projector's shadow), a few random blobs and 1 % speckle."""
+    d = np.clip(np.rint(s * depth_map_factor), 0, 65535).astype(np.uint16)
+    if holes:
+        g = _rng(seed)
+        h, w = d.shape
+        d[:, :int(g.integers(6, 13))] = 0
+        yy, xx = np.mgrid[0:h, 0:w]
+        for _ in range(int(g.integers(2, 6))):
+            cx, cy = g.integers(0, w), g.integers(0, h)
+            a, b = g.integers(8, 48), g.integers(8, 48)
+            d[((xx - cx) / a) ** 2 + ((yy - cy) / b) ** 2 <= 1.0] = 0
+        d[g.random((h, w)) < 0.01] = 0
+    return d
+
+
+def plane_rgbd_views(seed: int, rel_poses, width: int, height: int, fx: float, fy: float, cx: float, cy: float,
+                     dist, z0: float, depth_map_factor: float = 5000.0, holes: bool = True, workers: int = 1):
+    """RGB-D frames of one textured plane (the plane_views scene) seen by a camera with lens
+    distortion `dist`: the gray image is rendered through the distorted pixels' rays
+    (distorted_rays), and the depth image registered to it (TUM's depth is aligned with the
+    RGB image) holds each pixel's Z in its camera, as 16-bit round(Z * depth_map_factor),
+    with holes (_depth_image).  Returns (gray (n, h, w) u8, depth (n, h, w) u16)."""
+    global _PLANE_CANVAS
+    rays = distorted_rays(width, height, fx, fy, cx, cy, dist)
+    border = np.concatenate([rays[0], rays[-1], rays[:, 0], rays[:, -1]])
+    hx, hy = [], []
+    for T in rel_poses:
+        px, py, _ = _plane_hits(T, width, height, fx, fy, cx, cy, z0, rays=border)
+        hx += [px.min(), px.max()]
+        hy += [py.min(), py.max()]
+    mx = 3 - int(np.floor(min(hx)))
+    my = 3 - int(np.floor(min(hy)))
+    W = int(np.ceil(max(hx))) + mx + 4
+    H = int(np.ceil(max(hy))) + my + 4
+    canvas = tiled_canvas(seed, W, H, workers).astype(np.float64)
+    _PLANE_CANVAS = (canvas, mx, my, rays)
+    args = [(np.asarray(T, np.float64), width, height, fx, fy, cx, cy, z0, seed * 7919 + k, depth_map_factor, holes)
+            for k, T in enumerate(rel_poses)]
+    try:
+        if workers > 1 and len(args) > 1:
+            import multiprocessing as mp
+            pool = mp.get_context("fork").Pool(min(workers, len(args)))
+            try:
+                out = list(pool.imap(_render_plane_view, args, chunksize=2))
+            finally:
+                pool.close()
+                pool.join()
+        else:
+            out = [_render_plane_view(a) for a in args]
+    finally:
+        _PLANE_CANVAS = None
+    return np.stack([o[0] for o in out]), np.stack([o[1] for o in out])
+
+
+def tum_walk(seed: int, n: int, yaw0: float = 30.0, z0: float = 2.2):
+    """Relative poses (4x4, camera from reference) of a hand-held TUM-like RGB-D walk past
+    the textured plane Z = z0: the camera looks at the plane yawed by yaw0 +- 4 degrees, so
+    depths across a 640x480 view span about 1.9 m to 4.2 m (both sides of TUM1's mThDepth =
+    bf * 40 / fx = 3.09 m); per step it moves 0.09-0.13 m forward or back along its optical
+    axis (|dz| > mb = bf / fx = 0.077 m: ORBmatcher.cc:1650-1651's bForward / bBackward) or
+    less than 0.04 m (a third each; the centre kept within 0.45 m of the reference camera
+    along z and 0.6 m sideways), sideways by up to 0.03 m, and rolls 0.5-3 degrees either
+    way (bounded by 8)."""
+    g = _rng(seed + 911)
+    yaw, roll, pitch = 0.0, 0.0, 0.0
+    c = np.zeros(3)
+    rels = []
+    for k in range(n):
+        if k:
+            kind = g.integers(0, 3)
+            dz = g.uniform(0.09, 0.13) if kind == 0 else (-g.uniform(0.09, 0.13) if kind == 1 else g.uniform(-0.04, 0.04))
+            step = g.uniform(0.5, 3.0) * (1 if g.random() < 0.5 else -1)
+            roll = roll + step if abs(roll + step) <= 8.0 else roll - step
+            yaw = float(np.clip(yaw + g.uniform(-1.0, 1.0), -4.0, 4.0))
+            pitch = float(np.clip(pitch + g.uniform(-0.5, 0.5), -2.0, 2.0))
+            R = rotation("y", yaw0 + yaw) @ rotation("z", roll) @ rotation("x", pitch)
+            d = R.T @ np.array([g.uniform(-0.03, 0.03), g.uniform(-0.02, 0.02), dz])
+            if not (-0.45 <= c[2] + d[2] <= 0.45 and -0.6 <= c[0] + d[0] <= 0.6):
+                d = -d
+            c = c + d
+        R = rotation("y", yaw0 + yaw) @ rotation("z", roll) @ rotation("x", pitch)
+        rels.append(camera_pose(R, c.copy()))
+    return rels
 
 
 def kitti_walk(seed: int, n: int, yaw0: float = 25.0):
