@@ -16,7 +16,7 @@ views of one textured canvas along a random camera walk (data: synthetic).  One 
 N>1: one process per GPU over RCCL (`--gpus N` starts the N ranks itself when no
 launcher did), each rank its own batch (frames are independent: no data-path
 collective), "scaling": "weak".  --workload kitti / euroc: configs[2] / configs[3]
-(tests/stereo_bench.py, tests/euroc_bench.py).
+(benchmarks/stereo_bench.py, benchmarks/euroc_bench.py).
 
 Prints ONE JSON line on rank 0: value = frames/s of the whole job; roofline for the
 dominant kernel (HIP events on the extractor's stream; algorithmic bytes in
@@ -113,8 +113,15 @@ def _stage_sum(ks: dict, stage: str, field: str, count: str = None):
     then scaled by its launches per extraction (k_level_tiles runs once per extraction;
     k_pyramid once per pyramid segment: 2 at configs[4]'s 12 levels)."""
     def per_ex(k):
-        if not count or stage == "match":
+        if not count:
             return 1
+        if stage == "match":
+            # launches of this kernel per matcher call: the RGB-D step's retry pass adds a
+            # k_seq_build and a lean k_proj_search launch to every call (mostly empty)
+            com = [v for n, v in ks.items() if n.startswith("orbx::k_seq_commit")]
+            if not com or not com[0].get(count) or not ks[k].get(count):
+                return 1
+            return ks[k][count] / com[0][count]
         anchor = [v for n, v in ks.items() if n == "orbx::k_level_tiles"]
         if not anchor or not anchor[0].get(count) or not ks[k].get(count):
             return 1
@@ -185,7 +192,7 @@ def dominant_stage(event_ms: dict, workload: str) -> str:
     return dominant_stage_from_trace(event_ms, workload) or max(event_ms, key=event_ms.get)
 
 
-OTHER_WORKLOADS = ("_tum5k_", "_kitti_", "_euroc_")
+OTHER_WORKLOADS = ("_tum5k_", "_tum5k_mono_", "_kitti_", "_euroc_")
 
 
 def workload_profiles(kind: str, workload: str):
@@ -310,8 +317,9 @@ def cpu_baseline(frames_np, T, sf, seconds: float, threads: int, W=640, H=480, p
                            for c in range(3)], 1).astype(np.float32)
             mps = MapPoints(desc=ld, observations=np.ones(len(lk), np.int32), pos=Xw)
             out = np.full(len(ck), -1, np.int32)
-            return O.sbp_frame(view(ck, cd, T[i]), out, view(lk, ld, Tl), np.arange(len(lk), dtype=np.int32), mps,
-                               TH, True, True)
+            # TrackWithMotionModel's search: again at 2*th below 20 matches (Tracking.cc:988-994)
+            return O.track_motion_model(view(ck, cd, T[i]), out, view(lk, ld, Tl), np.arange(len(lk), dtype=np.int32),
+                                        mps, TH, True, True)[0]
 
         # same sources, other flags: the baseline build must reproduce the checker exactly
         k0, d0, _ = O.extract(frames_np[0], p)
@@ -364,8 +372,9 @@ def cpu_baseline(frames_np, T, sf, seconds: float, threads: int, W=640, H=480, p
             "cpu_model": cpu_model(), "host_cpus_visible": host, "flags": flags,
             "baseline_build_matches_checker": bool(same),
             "sample": f"{sum(done)} frames in {el:.1f}s on {threads} threads (+{one[0]} in {el1:.1f}s on 1 thread), "
-                      f"each = oracle C restatement of ORBextractor::operator() + SearchByProjection(CurrentFrame, "
-                      f"LastFrame, th={TH:g}, mono) against the previous frame, over {n} consecutive bench frames; "
+                      f"each = oracle C restatement of ORBextractor::operator() + TrackWithMotionModel's "
+                      f"SearchByProjection(CurrentFrame, LastFrame, th={TH:g}, mono; again at {2 * TH:g} below 20 "
+                      f"matches) against the previous frame, over {n} consecutive bench frames; "
                       f"scalar port built {flags} (no OpenCV / IPP SIMD)"}
 
 def _match_stream(dev):
@@ -422,7 +431,7 @@ def main():
     # run the oracle as parity check and CPU baseline).
     for flag, mod in (("--vocab", "vocab_bench"), ("--rows", "row_bench"), ("--dropin", "dropin_bench")):
         if flag in sys.argv[1:]:
-            sys.path.insert(0, str(ROOT / "tests"))
+            sys.path.insert(0, str(ROOT / "benchmarks"))
             return __import__(mod).main([a for a in sys.argv[1:] if a != flag])
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -431,9 +440,11 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
-    ap.add_argument("--workload", default="tum", choices=["tum", "tum5k", "kitti", "euroc"],
-                    help="tum: configs[1] (default, the headline); tum5k: configs[4] (5000 features x 12 levels); "
-                         "kitti: configs[2] stereo; euroc: configs[3]")
+    ap.add_argument("--workload", default="tum", choices=["tum", "tum5k", "tum5k_mono", "kitti", "euroc"],
+                    help="tum: configs[1] (default, the headline); tum5k: configs[4], the TUM RGB-D step (5000 "
+                         "features x 12 levels, benchmarks/rgbd_bench.py); tum5k_mono: the same extraction with "
+                         "the monocular search (round 5's configs[4] step); kitti: configs[2] stereo; euroc: "
+                         "configs[3]")
     ap.add_argument("--no-match", action="store_true", help="extraction only")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, available cores)")
@@ -462,14 +473,15 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     if args.selftest_launch:
         return selftest_launch(args, rank, world, local_rank)
-    if args.workload not in ("tum", "tum5k"):
-        sys.path.insert(0, str(ROOT / "tests"))
-        mod = {"kitti": "stereo_bench", "euroc": "euroc_bench"}[args.workload]
+    if args.workload not in ("tum", "tum5k_mono"):
+        sys.path.insert(0, str(ROOT / "benchmarks"))
+        mod = {"kitti": "stereo_bench", "euroc": "euroc_bench", "tum5k": "rgbd_bench"}[args.workload]
         return __import__(mod).main([a for a in sys.argv[1:]])
 
     B, W, H = args.batch, args.width, args.height
-    # configs[1] (the headline) or configs[4]: the TUM RGB-D settings at 5000 features x 12 levels
-    c5 = args.workload == "tum5k"
+    # configs[1] (the headline), or configs[4]'s extraction shape (5000 features x 12 levels)
+    # with the monocular search (tum5k_mono; the RGB-D step itself is --workload tum5k)
+    c5 = args.workload == "tum5k_mono"
     prm = (5000, 1.2, 12, 20, 7) if c5 else (1000, 1.2, 8, 20, 7)
     match = not args.no_match
     from orbslam2commentedbyxcm_amd import synth
@@ -527,7 +539,7 @@ def main():
     # steps then record only the dominant stage's two events per launch (a ring of event
     # sets, read back after the loop, no synchronisation inside it): every recorded event
     # costs the pipelined step ~0.2 % (tools/timing_ab.py: all stages' events 1.3-1.6 %).
-    wl = "tum5k" if c5 else "tum"
+    wl = "tum5k_mono" if c5 else "tum"
     # the committed trace's choice of the dominant stage is read (files, hashes) before the
     # warmup, not between the warmup and the timed region: ~13 ms of host work there left
     # the GPU idle right before the timed steps
@@ -711,7 +723,7 @@ def main():
     # `value`; the headline step itself has no collective.
     exchange = None
     if world > 1 and not args.no_exchange:
-        sys.path.insert(0, str(ROOT / "tests"))
+        sys.path.insert(0, str(ROOT / "benchmarks"))
         import euroc_bench
         eargs = euroc_bench.parse(["--steps", "10", "--warmup", "3", "--no-cpu-baseline"])
         line = euroc_bench.run(eargs, rank, world, gpu, True)
@@ -735,7 +747,8 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": ("frames/s ORB extract+match, 640x480 5000-feat 12-level (configs[4]), MI355X" if c5 else
+            "metric": ("frames/s ORB extract+match, 640x480 5000-feat 12-level monocular (configs[4] shape), MI355X"
+                       if c5 else
                        "frames/s ORB extract+match, 640x480 1000-feat, 1/2/4/8 MI355X"),
             "value": round(value, 2),
             "unit": "frames/s",
@@ -749,7 +762,8 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "source_hash": source_hash(),
-            "config": {"workload": f"{'configs[4]' if c5 else 'configs[1]'}: {B} synthetic 640x480 gray frames per GPU "
+            "config": {"workload": f"{'configs[4] extraction shape, monocular search' if c5 else 'configs[1]'}: {B} "
+                                   f"synthetic 640x480 gray frames per GPU "
                                    f"(views of one textured canvas along a random walk), nFeatures={prm[0]}, scale 1.2, "
                                    f"{prm[2]} levels, FAST 20/7; step = "
                                    "extract all frames + TrackWithMotionModel SearchByProjection of each frame "

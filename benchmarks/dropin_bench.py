@@ -13,7 +13,7 @@ measures how far that goes without the batched API.
 
     python bench.py --dropin [--threads 1,2,4,8,16] [--seconds 3]
 
-Lives under tests/ because it checks every thread's first results against the oracle
+Lives in benchmarks/ (bench.py --dropin); it checks every thread's first results against the oracle
 (test infrastructure), and builds the matching scene with it."""
 from __future__ import annotations
 
@@ -25,7 +25,7 @@ import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-for p in (ROOT, ROOT / "tests"):
+for p in (ROOT, ROOT / "benchmarks"):
     if str(p) not in sys.path:
         sys.path.insert(0, str(p))
 

@@ -4,8 +4,8 @@ cross-keyframe exchange, on 1..8 MI355X (one process per GPU).
 
     python bench.py --workload euroc [--gpus N] [--steps K] [--warmup W] [--batch B]
 
-(Lives under tests/ because it runs the oracle as its parity check and CPU baseline;
-bench.py --workload euroc is the entry point, and bench.py --gpus N starts the ranks.)
+(bench.py's configs[3] leg; it runs the oracle as its parity check and CPU baseline;
+bench.py --gpus N starts the ranks.)
 
 Workload (orbslam2commentedbyxcm_amd/keyframes.py): per rank and step, B = 64 stereo
 keyframes of a window of N*B (keyframe g on rank g % N) -- synthetic rectified 752x480
@@ -31,7 +31,7 @@ from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-for _p in (ROOT, ROOT / "tests"):
+for _p in (ROOT, ROOT / "benchmarks"):
     if str(_p) not in sys.path:
         sys.path.insert(0, str(_p))
 

@@ -2,7 +2,7 @@
 textured plane along synth.kitti_walk (motion along the optical axis beyond the baseline
 both ways, rolls, depths 12-28 m on both sides of mThDepth), KITTI 00-02's calibration.
 
-Shared by tests/stereo_bench.py (bench.py --workload kitti) and the GPU parity tests."""
+Shared by benchmarks/stereo_bench.py (bench.py --workload kitti) and the GPU parity tests."""
 from __future__ import annotations
 
 import numpy as np
@@ -50,7 +50,8 @@ def oracle_frame(O, p, sf, left, right, Tcw):
 
 def oracle_track(O, last, cur, tracked, th_depth, th=7.0, check_ori=True):
     """UpdateLastFrame of `last` (its tracked slots carry MapPoints at UnprojectStereo with
-    TRACKED_OBS observations) + SearchByProjection(cur, last, th, bMono=false).
+    TRACKED_OBS observations) + TrackWithMotionModel's SearchByProjection(cur, last, th,
+    bMono=false), again at 2*th below 20 matches.
     -> (cur_mp with ids = last keypoint index, nmatches, last's mp_obs, mp_pos)."""
     n = len(last.keys)
     obs_in = np.where(tracked[:n] & (last.depth > 0), TRACKED_OBS, -1).astype(np.int32)
@@ -59,5 +60,5 @@ def oracle_track(O, last, cur, tracked, th_depth, th=7.0, check_ori=True):
     last_mp = np.where(obs >= 0, np.arange(n), -1).astype(np.int32)
     mps = MapPoints(desc=last.desc, observations=np.maximum(obs, 0), pos=pos)
     ref = np.full(len(cur.keys), -1, np.int32)
-    nm = O.sbp_frame(cur, ref, last, last_mp, mps, th, False, check_ori)
+    nm, _ = O.track_motion_model(cur, ref, last, last_mp, mps, th, False, check_ori)  # retry at 2*th below 20
     return ref, nm, obs, pos

@@ -8,8 +8,8 @@ results compared byte for byte.
 The GPU figure is the wall time of the reference-shaped host call (arguments in host
 memory, as Tracking / LocalMapping would pass them): upload, kernels, download.  It is
 dominated by launch and PCIe latency at these sizes; the throughput paths are the
-batched device calls (bench.py for a1-a12, bench.py --vocab for f1).  Lives under
-tests/ because it runs the oracle (parity check and CPU baseline).
+batched device calls (bench.py for a1-a12, bench.py --vocab for f1).  bench.py --rows
+runs it; it runs the oracle too (parity check and CPU baseline).
 """
 from __future__ import annotations
 
@@ -21,7 +21,7 @@ import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-for p in (ROOT, ROOT / "tests"):
+for p in (ROOT, ROOT / "benchmarks"):
     if str(p) not in sys.path:
         sys.path.insert(0, str(p))
 

@@ -3,11 +3,10 @@
 
     python bench.py --workload kitti [--steps K] [--warmup W] [--batch B]
 
-(Lives under tests/ because it runs the oracle as its parity check and CPU baseline;
-bench.py --workload kitti is the entry point.)
+(bench.py's configs[2] leg; it runs the oracle as its parity check and CPU baseline.)
 
-Workload: B = 128 rectified 1241x376 stereo frames per step: a KITTI-like walk past a
-textured plane (tests/kitti_scenes.py: depths 12-28 m, motion along the optical axis beyond
+Workload: B = 256 rectified 1241x376 stereo frames per step: a KITTI-like walk past a
+textured plane (benchmarks/kitti_scenes.py: depths 12-28 m, motion along the optical axis beyond
 the baseline both ways, rolls), KITTI 00-02's calibration and ORB settings (2000
 features, scale 1.2, 8 levels, FAST 20/7), all frames distinct.  One step
 (orbslam2commentedbyxcm_amd/stereo.py, StereoSequencePipeline):
@@ -20,7 +19,9 @@ features, scale 1.2, 8 levels, FAST 20/7), all frames distinct.  One step
   4. TrackWithMotionModel's SearchByProjection(frame b, frame b-1, th = 7, bMono = false)
      (Tracking.cc:966-994, ORBmatcher.cc:1620-1789) for every b >= 1 -- configs[2]'s
      "L<->R SearchByProjection" leg (SURVEY.md §8(d) C3);
-steps 2-4 overlapped with the next step's extraction (two extractor pairs alternate).
+steps 2-4 overlapped with the next steps' extraction: four extractor pairs in rotation
+(StereoSequencePipeline.nsets, reported as config.extractor_sets), step 2 on a matcher
+stream and steps 3-4 on a tracking stream of their own.
 Inputs and outputs stay in HBM.
 
 Prints ONE JSON line: value = stereo frames (L+R pairs) per second, images_per_s = 2x;
@@ -41,7 +42,7 @@ from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-for _p in (ROOT, ROOT / "tests"):
+for _p in (ROOT, ROOT / "benchmarks"):
     if str(_p) not in sys.path:
         sys.path.insert(0, str(_p))
 

@@ -3,8 +3,7 @@
 
     python bench.py --vocab [--steps K] [--warmup W] [--batch B] [--k 10] [--L 6]
 
-(Lives under tests/ because it runs the oracle as its parity check and CPU baseline;
-bench.py --vocab is the entry point.)
+(bench.py --vocab; it runs the oracle as its parity check and CPU baseline;)
 
 Workload: B=256 synthetic 640x480 frames are extracted on the GPU (ORBextractor,
 nFeatures=1000; not timed) and their descriptors stay in HBM.  A synthetic vocabulary

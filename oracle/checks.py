@@ -47,10 +47,12 @@ def compare_extraction(ref, kps, desc, n) -> list[int]:
 
 
 def sequence_matches(ref, T: np.ndarray, sf, fx=500.0, fy=500.0, cx=320.0, cy=240.0, W=640, H=480, depth=5.0,
-                     th=15.0, check_ori=True, threads: int = 0):
+                     th=15.0, check_ori=True, threads: int = 0, retry: bool = True):
     """Oracle TrackWithMotionModel matching of frame b against b-1 for every b >= 1, on
     the oracle's own extraction `ref`, with the MapPoints orbx_match_sequence_device
-    defines (every last-frame keypoint i is MapPoint i at `depth` on its ray)."""
+    defines (every last-frame keypoint i is MapPoint i at `depth` on its ray); retry: the
+    second search at 2*th below 20 matches (SequencePipeline's default), else one search
+    (orbx_match_sequence_device)."""
     from orbslam2commentedbyxcm_amd.matcher import FrameView, MapPoints
     F32 = np.float32
 
@@ -68,8 +70,12 @@ def sequence_matches(ref, T: np.ndarray, sf, fx=500.0, fy=500.0, cx=320.0, cy=24
                        for c in range(3)], 1).astype(np.float32)
         mps = MapPoints(desc=ld, observations=np.ones(len(lk), np.int32), pos=Xw)
         cur = np.full(len(ck), -1, np.int32)
-        nr = O.sbp_frame(view(ck, cd, T[b]), cur, view(lk, ld, Tl), np.arange(len(lk), dtype=np.int32), mps, th,
-                         True, check_ori)
+        if retry:  # TrackWithMotionModel: again at 2*th below 20 matches (Tracking.cc:988-994)
+            nr, _ = O.track_motion_model(view(ck, cd, T[b]), cur, view(lk, ld, Tl), np.arange(len(lk), dtype=np.int32),
+                                         mps, th, True, check_ori)
+        else:
+            nr = O.sbp_frame(view(ck, cd, T[b]), cur, view(lk, ld, Tl), np.arange(len(lk), dtype=np.int32), mps, th,
+                             True, check_ori)
         return nr, cur
 
     with ThreadPoolExecutor(_threads(threads)) as ex:
@@ -135,7 +141,7 @@ def sequence_local(ref, T: np.ndarray, sf, cap: int, local_window: int = 3, fx=5
         cur = np.full(len(ck), -1, np.int32)
         last_mp = np.where(bad[(b - 1) * cap:(b - 1) * cap + len(lk)] == 0,
                            np.arange((b - 1) * cap, (b - 1) * cap + len(lk)), -1).astype(np.int32)
-        nm = O.sbp_frame(view(ck, cd, T[b]), cur, view(lk, ld, T[b - 1]), last_mp, mps, th, True, True)
+        nm, _ = O.track_motion_model(view(ck, cd, T[b]), cur, view(lk, ld, T[b - 1]), last_mp, mps, th, True, True)
         ids = np.concatenate([np.arange(f * cap, (f + 1) * cap, dtype=np.int32)
                               for f in range(max(0, b - local_window), b)])
         nl = O.search_local_points(view(ck, cd, T[b]), cur, ids, mps, local_th, 0.8)

@@ -28,7 +28,7 @@ earlier step's triangulation is still reading.  `windows` > 1 gives each step it
 keyframes whose views overlap most, then the baseline skip) depends only on the poses and
 is made once on the host, as LocalMapping does per keyframe.
 
-tests/euroc_bench.py (bench.py --workload euroc) times this object;
+benchmarks/euroc_bench.py (bench.py --workload euroc) times this object;
 tests/test_gpu_keyframes.py checks its output against the CPU parity oracle (also through
 a one-rank RCCL group with collective=True, the all_gather_into_tensor path), and
 tests/test_distributed.py covers the layout, the plan and the gather at world size 2 on

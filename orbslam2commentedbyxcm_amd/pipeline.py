@@ -11,7 +11,8 @@ frame against the MapPoints of its `local_window` predecessors, all in HBM:
   ORBextractor on its own HIP stream, so one chunk's latency-bound kernels (octree,
   describe) overlap another's;
 * one ORBmatcher matches all B-1 pairs on a third stream once every lane is done (a
-  stream of its own, created before the lanes' streams);
+  stream of its own, created before the lanes' streams), with TrackWithMotionModel's
+  second search at 2*th of a pair left under 20 matches (Tracking.cc:988-994);
 * pipelined (default): keypoint / descriptor / match buffers are double-buffered, so
   batch j is extracted while batch j-1 is matched; the next use of a buffer waits for
   the matching that last read it (events in both directions).  Not pipelined: the same
@@ -36,7 +37,7 @@ class SequencePipeline:
                  nbuf: int = 2, matcher_mode: int | None = None, match_after_stage: int = 0,
                  lane_offset_stage: int | None = None, match_cu_stride: int = 1,
                  match_priority: int = 0, on_matched=None, local_map: bool = False, local_window: int = 3,
-                 local_th: float = 1.0, level0_in_place: bool = True):
+                 local_th: float = 1.0, level0_in_place: bool = True, retry_below: int = 20):
         import torch
 
         self.B, self.W, self.H = int(batch), int(width), int(height)
@@ -45,6 +46,10 @@ class SequencePipeline:
         self.pipelined = bool(pipelined) and self.match
         self.dev = torch.device("cuda", device)
         self.fx, self.fy, self.cx, self.cy, self.depth, self.th = fx, fy, cx, cy, depth, th
+        # TrackWithMotionModel searches a pair again at 2*th when it found fewer than 20
+        # matches (Tracking.cc:988-994); 0: one search (the bare SearchByProjection)
+        import os
+        self.retry_below = int(os.environ.get("ORBX_TRACK_RETRY", retry_below))
         # The matcher's stream is created here, before the extraction lanes' streams
         # (orbx_stream_create; match_cu_stride k > 1 also confines it to CUs 0, k,
         # 2k, ...; match_priority: its HIP stream priority).  HIP hands out its hardware queues in stream-creation order, and
@@ -192,9 +197,10 @@ class SequencePipeline:
         if self.local_map:
             self._match_local(b, Tcw)
         else:
-            self.matcher.match_sequence_device(self.kps[b], self.desc[b], self.n[b], Tcw, self.mp[b], self.nm[b],
-                                               self.sf, self.fx, self.fy, self.cx, self.cy, self.W, self.H,
-                                               depth=self.depth, th=self.th, stream=self.ms.cuda_stream)
+            self.matcher.match_sequence_device_ex(self.kps[b], self.desc[b], self.n[b], Tcw, self.mp[b], self.nm[b],
+                                                  self.sf, self.fx, self.fy, self.cx, self.cy, self.W, self.H,
+                                                  depth=self.depth, th=self.th, retry_below=self.retry_below,
+                                                  stream=self.ms.cuda_stream)
         if self.on_matched is not None:
             self.on_matched(b)
         self.ev_m[b].record(self.ms)
@@ -210,7 +216,8 @@ class SequencePipeline:
                                 const_depth=self.depth, stream=s)
         self.matcher.match_sequence_device_ex(self.kps[b], self.desc[b], self.n[b], Tcw, self.mp[b], self.nm[b],
                                               self.sf, self.fx, self.fy, self.cx, self.cy, self.W, self.H,
-                                              th=self.th, d_mp_pos=tab["pos"], global_ids=True, stream=s)
+                                              th=self.th, d_mp_pos=tab["pos"], global_ids=True,
+                                              retry_below=self.retry_below, stream=s)
         timed = self._timing
         if timed:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))

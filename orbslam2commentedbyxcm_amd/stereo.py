@@ -11,14 +11,19 @@ tracking search that follows it):
   4. Tracking::TrackWithMotionModel's SearchByProjection(CurrentFrame, LastFrame, th = 7,
      bMono = false) (Tracking.cc:966-994, ORBmatcher.cc:1620-1789) of frame b against
      frame b-1, b >= 1: the stereo octave ranges (bForward / bBackward for motion along the
-     optical axis beyond mb), the mvuRight gate, the rotation check, and the claims of the
-     temporal points (Observations() == 0) not blocking later ones.
+     optical axis beyond mb), the mvuRight gate, the rotation check, the claims of the
+     temporal points (Observations() == 0) not blocking later ones, and the second search
+     at 2*th of a pair left under 20 matches.
+No frame of the sequence is a keyframe: UpdateLastFrame returns early for the last keyframe
+(Tracking.cc:902), which this pipeline does not model -- a caller with keyframes passes
+their LastFrames' MapPoints as obs_in / pos_in and must not step those frames' temporal
+points.
 Step 2 runs on a matcher stream and steps 3-4 on a tracking stream, beside the next
 steps' extraction: four extractor pairs in rotation, so a pair's pyramids and outputs stay
 untouched until its matching is done; the right image's extraction starts after the left
 one's blur stage (out of phase).
 
-tests/stereo_bench.py (bench.py --workload kitti) times this object; tests/test_gpu_stereo_track.py
+benchmarks/stereo_bench.py (bench.py --workload kitti) times this object; tests/test_gpu_stereo_track.py
 checks every frame and pair of its output against the CPU parity oracle.
 """
 from __future__ import annotations
@@ -38,7 +43,8 @@ class StereoSequencePipeline:
     def __init__(self, batch: int, width: int, height: int, fx: float, fy: float, cx: float, cy: float, bf: float,
                  params=(2000, 1.2, 8, 20, 7), track: bool = True, th: float = 7.0, nnratio: float = 0.9,
                  check_ori: bool = True, th_depth_factor: float = 35.0, max_d: float | None = None,
-                 matcher_mode: int | None = None, device: int = 0, level0_in_place: bool = True):
+                 matcher_mode: int | None = None, device: int = 0, level0_in_place: bool = True,
+                 retry_below: int = 20):
         import torch
 
         from .extractor import stream_create
@@ -47,6 +53,7 @@ class StereoSequencePipeline:
         self.b = float(np.float32(bf) / np.float32(fx))  # mb = mbf / fx (Frame.cc:61)
         self.max_d = float(fx) if max_d is None else float(max_d)  # maxD = mbf / minZ, minZ = mb
         self.th, self.track = float(th), bool(track)
+        self.retry_below = int(retry_below)  # TrackWithMotionModel's 2*th search below 20 matches (Tracking.cc:988-994)
         self.th_depth = th_depth(bf, fx, th_depth_factor)
         self.dev = torch.device("cuda", device)
         # the matcher stream first: HIP assigns hardware queues in stream-creation order, and
@@ -172,7 +179,8 @@ class StereoSequencePipeline:
             self.tmatcher.match_sequence_device_ex(
                 bk["kl"], bk["dl"], bk["nl"], d_Tcw, bk["mp"], bk["nm"], self.sf, self.fx, self.fy, self.cx, self.cy,
                 self.W, self.H, th=self.th, mono=False, bf=self.bf, b=self.b, d_u_right=bk["ur"],
-                d_mp_pos=bk["mp_pos"], d_has_mp=bk["has_mp"], d_mp_obs=bk["mp_obs"], global_ids=True, stream=s)
+                d_mp_pos=bk["mp_pos"], d_has_mp=bk["has_mp"], d_mp_obs=bk["mp_obs"], global_ids=True,
+                retry_below=self.retry_below, stream=s)
         if self._timing:
             ev[2].record(self.ts)
             self._st.append(ev)

@@ -6,6 +6,8 @@ import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
+# the benchmarks' scene modules (kitti_scenes, tum_rgbd_scenes, match_scenes) feed the tests too
+sys.path.insert(0, str(ROOT / "benchmarks"))
 
 
 def pytest_configure(config):

@@ -149,7 +149,7 @@ def test_h3_flip_count_runs(oracle):
     """cosf/sinf (the reference's literal H3 arithmetic) vs the shipped correctly rounded
     cos/sin: same keypoints; the descriptor difference is counted (profiles/r02_h3_flips.json
     holds the 256-frame figure)."""
-    sys.path.insert(0, str(ROOT / "tests"))
+    sys.path.insert(0, str(ROOT / "benchmarks"))
     import h3_flip_count
     from orbslam2commentedbyxcm_amd import synth
     r = h3_flip_count.count_flips(synth.frames(3, first_seed=90), threads=3)
@@ -281,7 +281,7 @@ def test_source_hash_tracks_the_sources():
 
 def test_exchange_leg_arguments():
     # the N-GPU headline's keyframe-exchange leg: euroc_bench.parse / run as bench.py calls them
-    sys.path.insert(0, str(ROOT / "tests"))
+    sys.path.insert(0, str(ROOT / "benchmarks"))
     import inspect
 
     import euroc_bench

@@ -48,7 +48,7 @@ def test_cpp_threads_dropin_calls_like_oracle(tmp_path, orbx_built, oracle):
     # at once (tests/cpp/dropin_mt.cpp): every thread's results equal the oracle's
     import json
     import sys
-    sys.path.insert(0, str(ROOT / "tests"))
+    sys.path.insert(0, str(ROOT / "benchmarks"))
     import dropin_bench as D
     import match_scenes as S
     img = synth.frame(11, 640, 480)

@@ -255,3 +255,38 @@ def test_sequence_pipeline_posed_b256(oracle, orbx_built):
         dom.append(int(np.argmax(h)))
     assert sum(d != 0 for d in dom) > 200, dom
     pl.close()
+
+
+def test_sequence_pipeline_retry_below_20(oracle, orbx_built):
+    """TrackWithMotionModel's second search (Tracking.cc:988-994): frame 5 keeps texture in
+    one 140 px window (about a hundred keypoints) and frame 6's pose is off by 25 px, so
+    pair 6's search at th = 15 finds fewer than 20 matches and the one at 30 more.  Every
+    frame and pair against the oracle, which searches
+    again the same way; and the same pipeline with the retry off against one search."""
+    import torch
+
+    from oracle import checks
+    from orbslam2commentedbyxcm_amd import synth
+    from orbslam2commentedbyxcm_amd.pipeline import SequencePipeline, sequence_poses
+    frames, off = synth.sequence(3, 8)
+    keep = np.zeros((480, 640), bool)
+    keep[200:340, 260:400] = True
+    frames[5][~keep] = 128
+    T = sequence_poses(off)
+    T[6, 3] += np.float32(25 * 5.0 / 500.0)
+    dev = torch.device("cuda", 0)
+    d_f, d_T = torch.from_numpy(frames).to(dev), torch.from_numpy(T).to(dev)
+    for retry in (20, 0):
+        pl = SequencePipeline(8, 640, 480, retry_below=retry)
+        pl.run(d_f, d_T, 2)
+        torch.cuda.synchronize(dev)
+        res = pl.host_results()
+        r = checks.check_sequence(frames, T, res, pl.sf, retry=bool(retry))
+        assert r["bit_exact"], r
+        nm = res["nm"]
+        assert min(nm[b] for b in (1, 2, 3, 4, 7)) > 200, nm
+        if retry:
+            assert nm[6] >= 20, nm
+        else:
+            assert nm[6] < 20, nm
+        pl.close()
