@@ -27,11 +27,16 @@ pair of the last batch against the oracle, plus the octree status words.
 from __future__ import annotations
 
 import argparse
+import faulthandler
 import json
 import os
 import sys
 import time
 from pathlib import Path
+
+# a fault anywhere in the run (a kernel's, a library's at exit) prints every thread's Python
+# stack to stderr before the process dies
+faulthandler.enable()
 
 ROOT = Path(__file__).resolve().parent
 SRC_ROOT = ROOT  # the sources source_hash() covers (ROOT may be redirected by tests)
@@ -387,6 +392,47 @@ def _match_stream(dev):
     return torch.cuda.Stream(device=dev, priority=int(os.environ["ORBX_MATCH_PRIO"]))
 
 
+def parity_threads(world: int) -> int:
+    """Oracle threads per rank for the parity check: the host's CPUs shared by the ranks."""
+    return max(2, min(16, len(os.sched_getaffinity(0)) // max(1, world)))
+
+
+def reduce_parity(parity: dict, world: int, dev) -> dict:
+    """Every rank checks its own last batch; the counts are summed over the ranks and the
+    line's verdict is the job's: parity.ranks_checked = the ranks that checked."""
+    keys = ("frames_checked", "frames_mismatched", "pairs_checked", "pairs_mismatched")
+    counts = [int(parity.get(k, 0)) for k in keys] + [int(not parity.get("octree_status_clean", True)),
+                                                     int("frames_checked" in parity)]
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor(counts, dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        counts = [int(x) for x in t.tolist()]
+    out = dict(parity)
+    out.update({f"{k}_all_ranks": c for k, c in zip(keys, counts)})
+    out["ranks_checked"] = counts[5]
+    if "bit_exact" in parity:
+        out["bit_exact"] = counts[1] == 0 and counts[3] == 0 and counts[4] == 0 and counts[5] == world
+    return out
+
+
+def teardown(world: int, dev=None) -> None:
+    """The run's explicit, ordered teardown (DESIGN.md §1 "Teardown"): every liborbx handle
+    owner still alive is closed, pipelines first (liborbx's handle registry), the device is
+    synchronised, and only then is the process group destroyed -- nothing of liborbx or of
+    RCCL is left for the C runtime's exit-time destructors."""
+    import torch
+    from orbslam2commentedbyxcm_amd import _lib
+    _lib.release_all()
+    if dev is not None:
+        torch.cuda.synchronize(dev)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def launch_ranks(n: int, argv) -> int:
     """bench.py --gpus N without a launcher: start N ranks of this script as child processes
     (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, 127.0.0.1 rendezvous) before this
@@ -607,15 +653,18 @@ def main():
                  "frac_all_lanes": round(rate * S / VALU_PEAK_GIPS, 4)}
 
     parity = {"octree_status_clean": not bool(status.any()), "basis": PARITY_BASIS}
-    if rank == 0 and args.parity_frames != 0:
+    if args.parity_frames != 0:
+        # every rank checks its own last batch (each extracts its own frames), counts summed
         from oracle import checks
         nchk = B if args.parity_frames < 0 else min(B, max(2, args.parity_frames))
         sub = {k: v[:nchk] for k, v in res.items()}
         if not match:
             sub.pop("mp"), sub.pop("nm")
         parity.update(checks.check_sequence(frames_np[:nchk], T[:nchk], sub, pl.sf, params=prm, fx=FX, fy=FY, cx=CX,
-                                            cy=CY, W=W, H=H, depth=DEPTH, th=TH))
+                                            cy=CY, W=W, H=H, depth=DEPTH, th=TH, threads=parity_threads(world),
+                                            retry=pl.retry_below > 0))
         parity["bit_exact"] = parity["bit_exact"] and parity["octree_status_clean"]
+        parity = reduce_parity(parity, world, dev)
 
     # The same step fed from host memory: every step's 256 frames are uploaded from pinned
     # host memory (double-buffered, on a copy stream beside the previous step's work) and
@@ -705,15 +754,16 @@ def main():
                  "stage_ms": {k: round(v, 4) for k, v in st2.items()},
                  "mean_matches_per_pair": round(float(res2["nm"][1:].mean()), 1),
                  "mean_local_matches_per_frame": round(float(res2["nm_local"][1:].mean()), 1)}
-        if rank == 0 and args.parity_frames != 0:
+        if args.parity_frames != 0:
             from oracle import checks
             nchk = B if args.parity_frames < 0 else min(B, max(2, args.parity_frames))
             sub = {k: v[:nchk] for k, v in res2.items()}
             pr = checks.check_sequence_local(frames_np[:nchk], T[:nchk], sub, pl2.sf, pl2.cap, params=prm, fx=FX,
-                                             fy=FY, cx=CX, cy=CY, W=W, H=H, depth=DEPTH, th=TH)
+                                             fy=FY, cx=CX, cy=CY, W=W, H=H, depth=DEPTH, th=TH,
+                                             threads=parity_threads(world))
             pr["octree_status_clean"] = not bool(pl2.status().any())
             pr["bit_exact"] = pr["bit_exact"] and pr["octree_status_clean"]
-            local["parity"] = pr
+            local["parity"] = reduce_parity(pr, world, dev)
         pl2.close()
 
     # At world size > 1 the node's GPUs also run configs[3]'s step with its one real
@@ -733,9 +783,11 @@ def main():
                         "steps": line["steps"], "slab_exchange": c["slab_exchange"],
                         "slab_mb_per_rank": c["slab_mb_per_rank"],
                         "allgather_mb_per_rank_step": c["allgather_mb_per_rank_step"],
-                        "parity": {k: pr.get(k) for k in ("bit_exact", "keyframes_checked", "keyframes_mismatched",
-                                                          "gathered_neighbours_checked", "gathered_mismatched",
-                                                          "pairs_checked", "pairs_mismatched")},
+                        "parity": {k: pr.get(k) for k in ("bit_exact", "ranks_checked", "keyframes_checked_all_ranks",
+                                                          "keyframes_mismatched_all_ranks",
+                                                          "gathered_neighbours_checked_all_ranks",
+                                                          "gathered_mismatched_all_ranks", "pairs_checked_all_ranks",
+                                                          "pairs_mismatched_all_ranks")},
                         "step": "configs[3] (bench.py --workload euroc): extract L+R, ComputeStereoMatches, "
                                 "ComputeBoW, close-point MapPoints, RCCL all_gather_into_tensor of the keyframe "
                                 "slabs, SearchForTriangulation against the gathered neighbours"}
@@ -798,9 +850,7 @@ def main():
             "mean_matches_per_pair": round(mean_matches, 1),
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    teardown(world, dev)
 
 
 if __name__ == "__main__":

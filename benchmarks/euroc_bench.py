@@ -16,7 +16,7 @@ all-gather of every rank's keyframe slab, and SearchForTriangulation of each loc
 keyframe against its nn = 10 stream neighbours that pass LocalMapping's baseline test.
 
 Prints ONE JSON line: value = keyframes/s over all ranks (max-over-ranks time); roofline of
-the dominant extraction kernel; parity = rank 0's keyframes (and the gathered copies of
+the dominant extraction kernel; parity = every rank's keyframes (and the gathered copies of
 their neighbours) and every one of their triangulation pair lists against the oracle;
 cpu_baseline = the oracle (-O3 -march=native) doing one keyframe's work on the host's cores.
 """
@@ -102,7 +102,7 @@ def _slab_fields(pl, buf: np.ndarray, rank: int, i: int) -> dict:
 
 
 def check(pl, ok: OracleKeyFrames, res: dict, nlocal: int, threads: int) -> dict:
-    """Rank 0's first `nlocal` keyframes (every field the step writes), the gathered
+    """This rank's first `nlocal` keyframes (every field the step writes), the gathered
     copies of their neighbours, and every pair list of theirs, bit-exact vs the oracle."""
     from orbslam2commentedbyxcm_amd.keyframes import record_index
     plan, B, world = pl.plan, pl.B, pl.world
@@ -257,16 +257,19 @@ def main(argv=None):
             os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=dev)
     out = run(args, rank, world, local_rank, collective)
-    if collective:
-        dist.barrier()
-        dist.destroy_process_group()
     if out is not None:
         print(json.dumps(out), flush=True)
+    # every pipeline, extractor, matcher and vocabulary closed and the device synchronised
+    # before the process group goes (r05e: an exit-time SIGSEGV, DESIGN.md §1 "Teardown")
+    import bench
+    bench.teardown(world if collective else 1, torch.device("cuda", local_rank))
+    if collective and world == 1:
+        dist.destroy_process_group()
 
 
 def run(args, rank: int, world: int, device: int, collective: bool):
     """The configs[3] step on this rank, on GPU `device` (the process group, when
-    collective, is already up): warmup, the timed steps (max over ranks), rank 0's parity
+    collective, is already up): warmup, the timed steps (max over ranks), every rank's parity (counts summed)
     and bench line (None on the other ranks).  bench.py's headline run calls it at world
     size > 1 for its keyframe-exchange leg."""
     import torch
@@ -323,16 +326,27 @@ def run(args, rank: int, world: int, device: int, collective: bool):
         tot_pairs, tot_skipped, tot_matches = npairs_local, pl.plan.skipped_baseline, int(res["tri_n"].sum())
 
     out = None
+    # every rank checks its own keyframes, the neighbours it received and its pair lists;
+    # the counts are summed over the ranks
+    parity = {"octree_status_clean": status_ok, "basis": __import__("bench").PARITY_BASIS}
+    nchk = args.parity_frames if args.parity_frames >= 0 else (B if world == 1 else 16)
+    threads = args.cpu_threads or __import__("bench").parity_threads(world)
+    from oracle import oracle as O
+    if nchk > 0:
+        O.build()
+        ok = OracleKeyFrames(O, pl, O.Vocab(text))
+        parity.update(check(pl, ok, res, min(nchk, B), threads))
+        keys = ("keyframes_checked", "keyframes_mismatched", "gathered_neighbours_checked", "gathered_mismatched",
+                "pairs_checked", "pairs_mismatched")
+        counts = [int(parity[k]) for k in keys] + [int(not status_ok), 1]
+        if world > 1:
+            t = torch.tensor(counts, dtype=torch.int64, device=dev)
+            dist.all_reduce(t)
+            counts = [int(x) for x in t.tolist()]
+        parity.update({f"{k}_all_ranks": c for k, c in zip(keys, counts)})
+        parity["ranks_checked"] = counts[-1]
+        parity["bit_exact"] = counts[1] == 0 and counts[3] == 0 and counts[5] == 0 and counts[6] == 0
     if rank == 0:
-        parity = {"octree_status_clean": status_ok, "basis": __import__("bench").PARITY_BASIS}
-        nchk = args.parity_frames if args.parity_frames >= 0 else (B if world == 1 else 16)
-        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        from oracle import oracle as O
-        if nchk > 0:
-            O.build()
-            ok = OracleKeyFrames(O, pl, O.Vocab(text))
-            parity.update(check(pl, ok, res, min(nchk, B), threads))
-            parity["bit_exact"] = parity["bit_exact"] and status_ok
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(pl, O, text, args.cpu_seconds, threads)

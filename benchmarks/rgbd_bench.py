@@ -243,18 +243,10 @@ def main(argv=None):
         O.build()
         nchk = B if args.parity_frames < 0 else min(B, max(2, args.parity_frames))
         pr = check_parity(O, gray, depth, T, h, tracked, sf, pl.image_bounds, pl.th_depth, cap, nchk,
-                          threads=max(1, workers // max(1, world)))
-        counts = [pr["frames_checked"], pr["frames_mismatched"], pr["pairs_checked"], pr["pairs_mismatched"],
-                  int(not status_ok), 1]
-        if world > 1:
-            t = torch.tensor(counts, dtype=torch.int64, device=dev)
-            dist.all_reduce(t)
-            counts = [int(x) for x in t.tolist()]
+                          threads=bench.parity_threads(world))
         parity.update(pr)
-        parity.update({"frames_checked_all_ranks": counts[0], "frames_mismatched_all_ranks": counts[1],
-                       "pairs_checked_all_ranks": counts[2], "pairs_mismatched_all_ranks": counts[3],
-                       "ranks_checked": counts[5],
-                       "bit_exact": counts[1] == 0 and counts[3] == 0 and counts[4] == 0})
+        parity["bit_exact"] = pr["frames_mismatched"] == 0 and pr["pairs_mismatched"] == 0 and status_ok
+        parity = bench.reduce_parity(parity, world, dev)
     n_mean = float(h["n"].mean())
     bytes_pf = bench.stage_bytes(S.W, S.H, n_mean, nlevels=S.PARAMS[2], scale=S.PARAMS[1])
     per_launch = (B - 1) if dom == "match" else (pl.bounds[0][1] - pl.bounds[0][0])
@@ -309,9 +301,7 @@ def main(argv=None):
         }
         print(json.dumps(out), flush=True)
     pl.close()
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    bench.teardown(world, dev)
 
 
 if __name__ == "__main__":

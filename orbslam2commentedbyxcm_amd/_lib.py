@@ -105,6 +105,54 @@ class LocalMapBatch(C.Structure):
                 ("frame_mp", C.c_void_p), ("nmatches", C.c_void_p)]
 
 
+# ---- handle lifetime (DESIGN.md §1 "Teardown") ------------------------------------
+# Every object that owns liborbx handles or HIP streams registers here.  At interpreter
+# exit the atexit hook synchronises the devices and closes them newest first -- while the
+# HIP runtime, RCCL and any profiler are still fully alive -- so no HIP object is left for
+# the C runtime's static destructors (HIP's own, RCCL's, a profiler tool's) to tear down in
+# whatever order they run.  __del__ does nothing once the interpreter is finalizing.
+_handles: list = []
+_hook = False
+
+
+def track(obj) -> None:
+    """Register a handle owner (it has close(): idempotent, synchronising what it frees)."""
+    global _hook
+    import weakref
+    if len(_handles) > 4096:  # drop the owners already freed
+        _handles[:] = [r for r in _handles if r() is not None]
+    _handles.append(weakref.ref(obj))
+    if not _hook:
+        # registered after torch's own exit hooks (lib() imports torch first), so it runs
+        # before them
+        import atexit
+        atexit.register(release_all)
+        _hook = True
+
+
+def release_all() -> int:
+    """Synchronise the devices the process used and close every live handle owner,
+    newest first; returns how many were closed."""
+    live = [o for o in (r() for r in reversed(_handles)) if o is not None]
+    _handles.clear()
+    if not live:
+        return 0
+    try:
+        import torch
+        if torch.cuda.is_initialized():
+            for d in range(torch.cuda.device_count()):
+                with torch.cuda.device(d):
+                    torch.cuda.synchronize()
+    except Exception:
+        pass
+    for o in live:
+        try:
+            o.close()
+        except Exception:
+            pass
+    return len(live)
+
+
 class OrbxError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"orbx error {code}: {msg}")

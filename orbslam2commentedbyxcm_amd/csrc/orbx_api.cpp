@@ -4,6 +4,7 @@
 // the device plan for the last frame size, device buffers sized for the largest
 // batch seen, and (like the reference's mvImagePyramid) keeps the pyramid of the
 // last extraction until the next call.  No function throws across the ABI.
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -23,10 +24,16 @@ using namespace orbx;
 namespace {
 
 thread_local std::string g_last_error;
+std::atomic<bool> g_unloading{false};
+
+// runs from the C runtime's exit / dlclose teardown of this library -- before that of the
+// HIP runtime it links against (dependents are finalised first)
+__attribute__((destructor)) void orbx_on_unload() { g_unloading.store(true); }
 
 }  // namespace
 
 void orbx::set_last_error(const std::string& msg) { g_last_error = msg; }
+bool orbx::unloading() { return g_unloading.load(); }
 
 namespace {
 
@@ -396,7 +403,7 @@ int orbx_extractor_create(const orbx_extractor_params* params, int device, orbx_
 }
 
 void orbx_extractor_destroy(orbx_extractor* ex) {
-    if (!ex) return;
+    if (!ex || orbx::unloading()) return;
     (void)hipSetDevice(ex->device);
     if (ex->stream) (void)hipStreamSynchronize(ex->stream);
     free_buffers(ex->db);
@@ -473,6 +480,7 @@ int orbx_stream_create(int device, int cu_stride, int priority, void** stream) {
 
 int orbx_stream_destroy(void* stream) {
     if (!stream) return fail(ORBX_ERR_ARG, "null stream");
+    if (orbx::unloading()) return ORBX_OK;
     HIP_TRY(hipStreamDestroy((hipStream_t)stream));
     return ORBX_OK;
 }

@@ -5,4 +5,9 @@
 
 namespace orbx {
 void set_last_error(const std::string& msg);
+// True once liborbx's own unload destructor has run (process exit, dlclose): the HIP
+// runtime, which liborbx depends on and which is therefore finalised after it, may be
+// going away, so the orbx_*_destroy entry points release nothing and leave the memory and
+// streams to the process teardown.  DESIGN.md §1 "Teardown".
+bool unloading();
 }

@@ -428,7 +428,7 @@ int orbx_matcher_create(int device, float nnratio, int check_ori, orbx_matcher**
 }
 
 void orbx_matcher_destroy(orbx_matcher* m) {
-    if (!m) return;
+    if (!m || orbx::unloading()) return;
     (void)hipSetDevice(m->device);
     if (m->stream) (void)hipStreamSynchronize(m->stream);
     m->arena.release();

@@ -533,7 +533,7 @@ int orbx_vocabulary_load_text_file(const char* path, int device, orbx_vocabulary
 }
 
 void orbx_vocabulary_destroy(orbx_vocabulary* v) {
-    if (!v) return;
+    if (!v || orbx::unloading()) return;
     (void)hipSetDevice(v->device);
     if (v->stream) (void)hipStreamSynchronize(v->stream);
     free_vocab(v);

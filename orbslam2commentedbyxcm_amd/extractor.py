@@ -9,6 +9,7 @@ Keypoints come back as a structured array with cv::KeyPoint's fields
 from __future__ import annotations
 
 import ctypes as C
+import sys
 
 import numpy as np
 
@@ -27,6 +28,7 @@ class ORBextractor:
         L.check(L.lib().orbx_extractor_create(C.byref(prm), int(device), C.byref(h)))
         self._destroy = L.lib().orbx_extractor_destroy  # held: module globals may be gone at exit
         self._h = h
+        L.track(self)
         self.nfeatures = int(nfeatures)
         self.scaleFactor = float(scaleFactor)
         self.nlevels = int(nlevels)
@@ -36,10 +38,15 @@ class ORBextractor:
         self._last_batch = 0
         self._pyr_cache = None
 
-    def __del__(self):
+    def close(self) -> None:
+        """Release the extractor (orbx_extractor_destroy: waits for its stream); idempotent."""
         if getattr(self, "_h", None):
             self._destroy(self._h)
             self._h = None
+
+    def __del__(self, _finalizing=sys.is_finalizing):
+        if not _finalizing():  # at interpreter exit the atexit hook has closed it already
+            self.close()
 
     # ---- getters (ORBextractor.h:119-159)
     def _levels(self):
@@ -231,3 +238,24 @@ def stream_create(device: int, cu_stride: int = 1, priority: int = 0) -> int:
 
 def stream_destroy(stream: int) -> None:
     L.check(L.lib().orbx_stream_destroy(C.c_void_p(stream)))
+
+
+def release_owned(obj, streams, owners, own_streams) -> None:
+    """A pipeline's close(): wait for its streams (torch stream objects, None skipped), close
+    the handle owners it holds (extractors, matchers, vocabularies: each waits for its own
+    stream), then destroy the streams it created (the attributes named in own_streams,
+    raw hipStream_t values, set to None).  Idempotent."""
+    if getattr(obj, "_released", False):
+        return
+    obj._released = True
+    for s in streams:
+        if s is not None:
+            s.synchronize()
+    for o in owners:
+        if o is not None:
+            o.close()
+    for a in own_streams:
+        h = getattr(obj, a, None)
+        if h:
+            setattr(obj, a, None)
+            stream_destroy(h)

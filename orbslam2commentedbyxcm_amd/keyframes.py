@@ -36,6 +36,7 @@ gloo.
 """
 from __future__ import annotations
 
+import sys
 from dataclasses import dataclass
 
 import numpy as np
@@ -283,6 +284,8 @@ class StereoKeyFramePipeline:
         self.vocab_text = vocab_text
         if not self.voc.loadFromText(vocab_text):
             raise RuntimeError("vocabulary rejected")
+        from . import _lib
+        _lib.track(self)
         self.lay = SlabLayout(self.B, self.cap)
         u8 = dict(dtype=torch.uint8, device=self.dev)
         i32 = dict(dtype=torch.int32, device=self.dev)
@@ -337,22 +340,20 @@ class StereoKeyFramePipeline:
         self._tabs = [keyframe_table(self.lay.records(b.data_ptr(), self.world, self._rec_poses)) for b in bufs]
 
     def close(self):
-        """Release the matcher stream this pipeline created (after synchronising)."""
-        from .extractor import stream_destroy
-        if self._own_ts:
-            self.ts.synchronize()
-            stream_destroy(self._own_ts)
-            self._own_ts = None
-        if self._own_ms:
-            self.ms.synchronize()
-            stream_destroy(self._own_ms)
-            self._own_ms = None
+        """Wait for this pipeline's work, then release its matchers, vocabulary, extractor
+        pairs and the streams it created (idempotent)."""
+        from .extractor import release_owned
+        release_owned(self, streams=[getattr(self, "ts", None), getattr(self, "ms", None)],
+                      owners=[getattr(self, "stereo", None), getattr(self, "tri", None), getattr(self, "voc", None),
+                              *(e for pair in getattr(self, "sets", []) for e in pair)],
+                      own_streams=["_own_ts", "_own_ms"])
 
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+    def __del__(self, _finalizing=sys.is_finalizing):
+        if not _finalizing():
+            try:
+                self.close()
+            except Exception:
+                pass
 
     def step(self):
         """Issue one step (asynchronous)."""

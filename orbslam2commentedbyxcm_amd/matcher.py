@@ -9,6 +9,7 @@ mvpMapPoints arrays hold ids (-1 = NULL).  Every call runs on the MI355X.
 from __future__ import annotations
 
 import ctypes as C
+import sys
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -190,11 +191,17 @@ class ORBmatcher:
         L.check(L.lib().orbx_matcher_create(self.device, self.mfNNratio, 1 if checkOri else 0, C.byref(h)))
         self._destroy = L.lib().orbx_matcher_destroy  # held: module globals may be gone at exit
         self._h = h
+        L.track(self)
 
-    def __del__(self):
+    def close(self) -> None:
+        """Release the matcher (orbx_matcher_destroy: waits for its stream); idempotent."""
         if getattr(self, "_h", None):
             self._destroy(self._h)
             self._h = None
+
+    def __del__(self, _finalizing=sys.is_finalizing):
+        if not _finalizing():
+            self.close()
 
     def last_call_us(self) -> float:
         """Wall time (us) of this matcher's newest host call inside liborbx (no binding

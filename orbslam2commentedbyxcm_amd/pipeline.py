@@ -23,6 +23,8 @@ pair of its output against the CPU parity oracle.
 """
 from __future__ import annotations
 
+import sys
+
 import numpy as np
 
 from .extractor import ORBextractor
@@ -145,6 +147,8 @@ class SequencePipeline:
         # enqueues on self.ms there (e.g. copying the results out) finishes before the
         # buffer is overwritten
         self.on_matched = on_matched
+        from . import _lib
+        _lib.track(self)
         self._timing = False
         self._ext_timed = self._match_timed = False
         self.it = 0            # extractions issued
@@ -152,18 +156,19 @@ class SequencePipeline:
         self.last = None       # buffer holding the newest complete result
 
     def close(self):
-        """Release the matcher stream this pipeline created (after synchronising)."""
-        if self._own_ms:
-            from .extractor import stream_destroy
-            self.ms.synchronize()
-            stream_destroy(self._own_ms)
-            self._own_ms = None
+        """Wait for this pipeline's work, then release its matchers, its extractors and the
+        matcher stream it created (idempotent; results are unreadable afterwards)."""
+        from .extractor import release_owned
+        release_owned(self, streams=[getattr(self, "ms", None)], owners=[
+            getattr(self, "matcher", None), getattr(self, "lmatcher", None), *getattr(self, "exs", [])],
+            own_streams=["_own_ms"])
 
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+    def __del__(self, _finalizing=sys.is_finalizing):
+        if not _finalizing():  # at interpreter exit the atexit hook has closed it already
+            try:
+                self.close()
+            except Exception:
+                pass
 
     # -- launches -----------------------------------------------------------------
     def _extract(self, frames, Tcw, b):

@@ -28,6 +28,8 @@ checks every frame and pair of its output against the CPU parity oracle.
 """
 from __future__ import annotations
 
+import sys
+
 import numpy as np
 
 from .extractor import ORBextractor
@@ -119,23 +121,24 @@ class StereoSequencePipeline:
         self.last = None
         self._timing = False
         self._st = []  # (stereo start, track start, end) events while timing
+        from . import _lib
+        _lib.track(self)
 
     def close(self):
-        from .extractor import stream_destroy
-        if self._own_ts:
-            self.ts.synchronize()
-            stream_destroy(self._own_ts)
-            self._own_ts = None
-        if self._own_ms:
-            self.ms.synchronize()
-            stream_destroy(self._own_ms)
-            self._own_ms = None
+        """Wait for this pipeline's work, then release its matchers, its extractor pairs and
+        the streams it created (idempotent)."""
+        from .extractor import release_owned
+        release_owned(self, streams=[getattr(self, "ts", None), getattr(self, "ms", None)],
+                      owners=[getattr(self, "smatcher", None), getattr(self, "tmatcher", None),
+                              *(e for pair in getattr(self, "sets", []) for e in pair)],
+                      own_streams=["_own_ts", "_own_ms"])
 
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+    def __del__(self, _finalizing=sys.is_finalizing):
+        if not _finalizing():
+            try:
+                self.close()
+            except Exception:
+                pass
 
     def step(self, d_left, d_right, d_Tcw=None, obs_in=None, pos_in=None):
         """Issue one step (asynchronous): B stereo frames d_left / d_right (B, H, W) u8 with

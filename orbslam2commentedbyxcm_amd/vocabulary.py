@@ -10,6 +10,7 @@ reference's ``std::map`` s.
 from __future__ import annotations
 
 import ctypes as C
+import sys
 
 import numpy as np
 
@@ -30,9 +31,15 @@ class ORBVocabulary:
         self.device = int(device)
         self._h = None
         self._destroy = L.lib().orbx_vocabulary_destroy  # held: module globals may be gone at exit
+        L.track(self)
 
-    def __del__(self):
+    def close(self) -> None:
+        """Release the vocabulary (orbx_vocabulary_destroy); idempotent."""
         self._release()
+
+    def __del__(self, _finalizing=sys.is_finalizing):
+        if not _finalizing():
+            self._release()
 
     def _release(self):
         if getattr(self, "_h", None):

@@ -4,10 +4,13 @@
 // per frame ORBextractor::operator() on a C1 image (ORBextractor.cc:1513-1629),
 // SearchByProjection(Frame&, const Frame&, th, bMono) (a12, ORBmatcher.cc:1620-1789) and
 // SearchByProjection(Frame&, vector<MapPoint*>, th) (a11, cc:61-173) on host arrays, for
-// a fixed wall time; every thread's first frame is compared with the expected results.
+// a fixed wall time.  Frame k of a thread extracts image (k + thread) % M of the scene's M
+// images, and EVERY frame's keypoints, descriptors and both searches' outputs are compared
+// with the oracle's (precomputed per image in the scene file).
 //   dropin_mt <scene.bin> <threads> <seconds>
-// prints one JSON object: {"threads": T, "frames": N, "seconds": s, "frames_per_s": r, "bit_exact": b}
-// scene.bin is written by tests/dropin_bench.py (layout in write_scene there).
+// prints one JSON object: {"threads": T, "frames": N, "seconds": s, "frames_per_s": r,
+//   "frames_checked": C, "frames_mismatched": X, "bit_exact": b}
+// scene.bin is written by benchmarks/dropin_bench.py (layout in write_scene there).
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -46,11 +49,11 @@ struct Scene {
     std::vector<uint8_t> in_view;
     std::vector<float> px, py, pxr, vcos;
     std::vector<int32_t> slev, queries, last_mp;
-    std::vector<uint8_t> img;
     int32_t n12, n11;
     std::vector<int32_t> c_ref, f_ref;
-    std::vector<orbx_keypoint> k_ref;
-    std::vector<uint8_t> d_ref;
+    std::vector<std::vector<uint8_t>> img;     // the M images
+    std::vector<std::vector<orbx_keypoint>> k_ref;  // the oracle's keypoints / descriptors per image
+    std::vector<std::vector<uint8_t>> d_ref;
 };
 
 Scene load(const char* path) {
@@ -68,11 +71,16 @@ Scene load(const char* path) {
     s.in_view = r.vec<uint8_t>(s.nA), s.px = r.vec<float>(s.nA), s.py = r.vec<float>(s.nA);
     s.pxr = r.vec<float>(s.nA), s.slev = r.vec<int32_t>(s.nA), s.vcos = r.vec<float>(s.nA);
     s.queries = r.vec<int32_t>(s.nq), s.last_mp = r.vec<int32_t>(s.nA);
-    s.img = r.vec<uint8_t>((size_t)s.W * s.H);
     s.n12 = r.one<int32_t>(), s.c_ref = r.vec<int32_t>(s.nB);
     s.n11 = r.one<int32_t>(), s.f_ref = r.vec<int32_t>(s.nB);
-    const int nk = r.one<int32_t>();
-    s.k_ref = r.vec<orbx_keypoint>(nk), s.d_ref = r.vec<uint8_t>((size_t)nk * 32);
+    const int M = r.one<int32_t>();
+    if (M < 1) throw std::runtime_error("no images in the scene file");
+    for (int j = 0; j < M; j++) {
+        s.img.push_back(r.vec<uint8_t>((size_t)s.W * s.H));
+        const int nk = r.one<int32_t>();
+        s.k_ref.push_back(r.vec<orbx_keypoint>(nk));
+        s.d_ref.push_back(r.vec<uint8_t>((size_t)nk * 32));
+    }
     std::fclose(r.f);
     return s;
 }
@@ -113,8 +121,8 @@ int main(int argc, char** argv) {
 
         std::atomic<int> ready{0};
         std::atomic<bool> go{false};
-        std::atomic<long> frames{0};
-        std::atomic<int> mismatched{0}, failed{0};
+        std::atomic<long> frames{0}, checked{0}, mismatched{0};
+        std::atomic<int> failed{0};
         std::chrono::steady_clock::time_point t_end;
         std::vector<double> span_start(T), span_end(T);
         const auto t_ref = std::chrono::steady_clock::now();
@@ -125,26 +133,32 @@ int main(int argc, char** argv) {
                 std::vector<orbx_keypoint> kps;
                 std::vector<uint8_t> desc;
                 std::vector<int32_t> cur(s.nB), loc(s.nB);
+                const int M = (int)s.img.size();
+                long k = i;  // this thread's frame counter (threads start on different images)
                 auto frame = [&]() -> bool {
-                    ex(s.img.data(), s.W, s.H, (size_t)s.W, kps, desc);
+                    const int j = (int)(k++ % M);
+                    ex(s.img[j].data(), s.W, s.H, (size_t)s.W, kps, desc);
                     std::fill(cur.begin(), cur.end(), -1);
                     const int n12 = m12.SearchByProjection(B, cur.data(), A, s.last_mp.data(), nullptr, mps, 15.f, true);
                     std::fill(loc.begin(), loc.end(), -1);
                     const int n11 = m11.SearchByProjection(B, loc.data(), s.queries, mps, trk, 3.f);
-                    return kps.size() == s.k_ref.size() &&
-                           std::memcmp(kps.data(), s.k_ref.data(), kps.size() * sizeof(orbx_keypoint)) == 0 &&
-                           desc == s.d_ref && n12 == s.n12 && cur == s.c_ref && n11 == s.n11 && loc == s.f_ref;
+                    return kps.size() == s.k_ref[j].size() &&
+                           std::memcmp(kps.data(), s.k_ref[j].data(), kps.size() * sizeof(orbx_keypoint)) == 0 &&
+                           desc == s.d_ref[j] && n12 == s.n12 && cur == s.c_ref && n11 == s.n11 && loc == s.f_ref;
                 };
-                if (!frame()) mismatched++;  // warm-up and parity
-                frame();
+                long bad = 0, n_chk = 0;
+                for (int w = 0; w < 2; w++, n_chk++) bad += !frame();  // warm-up (checked too)
                 ready++;
                 while (!go.load()) std::this_thread::yield();
                 const auto t0 = std::chrono::steady_clock::now();
                 long n = 0;
                 while (std::chrono::steady_clock::now() < t_end) {
-                    frame();
+                    bad += !frame();  // every frame compared
                     n++;
                 }
+                n_chk += n;
+                checked += n_chk;
+                mismatched += bad;
                 const auto t1 = std::chrono::steady_clock::now();
                 span_start[i] = std::chrono::duration<double>(t0 - t_ref).count();
                 span_end[i] = std::chrono::duration<double>(t1 - t_ref).count();
@@ -168,8 +182,10 @@ int main(int argc, char** argv) {
             b = span_end[i] > b ? span_end[i] : b;
         }
         const double el = b - a;
-        std::printf("{\"threads\": %d, \"frames\": %ld, \"seconds\": %.4f, \"frames_per_s\": %.1f, \"bit_exact\": %s}\n",
-                    T, frames.load(), el, frames.load() / el, mismatched.load() ? "false" : "true");
+        std::printf("{\"threads\": %d, \"frames\": %ld, \"seconds\": %.4f, \"frames_per_s\": %.1f, "
+                    "\"frames_checked\": %ld, \"frames_mismatched\": %ld, \"images\": %d, \"bit_exact\": %s}\n",
+                    T, frames.load(), el, frames.load() / el, checked.load(), mismatched.load(), (int)s.img.size(),
+                    mismatched.load() ? "false" : "true");
     } catch (const std::exception& e) {
         std::fprintf(stderr, "%s\n", e.what());
         return 1;

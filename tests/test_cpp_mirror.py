@@ -45,28 +45,38 @@ def test_cpp_mirror_extracts_like_oracle(tmp_path, orbx_built, oracle):
 @pytest.mark.gpu
 def test_cpp_threads_dropin_calls_like_oracle(tmp_path, orbx_built, oracle):
     # four C++ threads, each with its own extractor and matchers, calling extract + a12 + a11
-    # at once (tests/cpp/dropin_mt.cpp): every thread's results equal the oracle's
+    # at once (tests/cpp/dropin_mt.cpp) over three images: every frame's results equal the
+    # oracle's
     import json
     import sys
     sys.path.insert(0, str(ROOT / "benchmarks"))
     import dropin_bench as D
     import match_scenes as S
-    img = synth.frame(11, 640, 480)
+    imgs = [synth.frame(11 + j, 640, 480) for j in range(3)]
     A, B = S.two_views(oracle, 0)
     mps = S.mappoints_from(A, 0)
     trk = S.local_track(A, B, mps, 0)
     nA, nB = len(A.keys), len(B.keys)
     queries = np.random.default_rng(0).permutation(nA).astype(np.int32)
     last_mp = np.arange(nA, dtype=np.int32)
-    k, d, _ = oracle.extract(img, oracle.params(1000, 1.2, 8, 20, 7))
+    refs = [oracle.extract(im, oracle.params(1000, 1.2, 8, 20, 7))[:2] for im in imgs]
     c = np.full(nB, -1, np.int32)
     n12 = oracle.sbp_frame(B, c, A, last_mp, mps, 15.0, True, True)
     f = np.full(nB, -1, np.int32)
     n11 = oracle.sbp_local(B, f, queries, mps, trk, 3.0, 0.8)
-    D.write_scene(tmp_path / "scene.bin", img, A, B, mps, trk, queries, last_mp, n12, c, n11, f, k, d,
+    D.write_scene(tmp_path / "scene.bin", imgs, A, B, mps, trk, queries, last_mp, n12, c, n11, f, refs,
                   len(A.scale_factors))
     exe = D.build_driver(tmp_path / "dropin_mt")
     r = subprocess.run([str(exe), str(tmp_path / "scene.bin"), "4", "0.5"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     rec = json.loads(r.stdout.strip().splitlines()[-1])
-    assert rec["bit_exact"] and rec["frames"] > 4
+    assert rec["bit_exact"] and rec["frames"] > 4 and rec["images"] == 3
+    assert rec["frames_checked"] == rec["frames"] + 2 * 4 and rec["frames_mismatched"] == 0
+
+    # a wrong expectation for one image is caught on the frames that extract it
+    bad = [refs[0], (refs[1][0], refs[1][1] ^ 1), refs[2]]
+    D.write_scene(tmp_path / "bad.bin", imgs, A, B, mps, trk, queries, last_mp, n12, c, n11, f, bad,
+                  len(A.scale_factors))
+    r = subprocess.run([str(exe), str(tmp_path / "bad.bin"), "2", "0.2"], capture_output=True, text=True, timeout=120)
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert not rec["bit_exact"] and 0 < rec["frames_mismatched"] < rec["frames_checked"]
