@@ -565,7 +565,8 @@ def main():
                           lane_offset_stage=int(os.environ["ORBX_LANE_OFFSET"]) if "ORBX_LANE_OFFSET" in os.environ else None,
                           match_cu_stride=int(os.environ.get("ORBX_MATCH_CUSTRIDE", "1")),
                           match_priority=int(os.environ.get("ORBX_MATCH_STREAM_PRIO", "0")),
-                          level0_in_place=os.environ.get("ORBX_L0_COPY") != "1")
+                          level0_in_place=os.environ.get("ORBX_L0_COPY") != "1",
+                          first_in_phase=os.environ.get("ORBX_PIPE_FIRST_INPHASE", "0") == "1")
     S = pl.S
     nbufs = len(pl.kps)  # output buffer sets in rotation
     lane_off = pl.lane_offset_stage if pl.lane_ev is not None else None  # None: no offset applied

@@ -289,7 +289,12 @@ def run(args, rank: int, world: int, device: int, collective: bool):
     t0 = time.perf_counter()
     text = synth.vocabulary_text(7, 10, 6, 0, 0, centres=d0)
     gen_s = time.perf_counter() - t0
+    # A/B knobs of the bench (environment): keyframe sets, the right image's lane offset,
+    # where the slab exchange is waited for
     pl = StereoKeyFramePipeline(B, rank, world, device=device, nn=args.nn, vocab_text=text,
+                                nsets=int(os.environ.get("ORBX_KF_SETS", "4")),
+                                lane_offset_stage=int(os.environ.get("ORBX_KF_LANE_OFFSET", "3")),
+                                gather_async=os.environ.get("ORBX_GATHER_SYNC") != "1",
                                 collective=collective, level0_in_place=not getattr(args, "level0_copy", False))
 
     def barrier():

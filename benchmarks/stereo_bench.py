@@ -131,8 +131,12 @@ def main(argv=None):
 
     from orbslam2commentedbyxcm_amd.stereo import StereoSequencePipeline
     dev = torch.device("cuda", 0)
+    # A/B knobs of the bench (environment): extractor pairs, the right image's lane offset,
+    # the separate tracking stream
     pl = StereoSequencePipeline(B, K.W, K.H, K.FX, K.FY, K.CX, K.CY, K.BF, params=K.PARAMS, track=track,
-                                th_depth_factor=K.TH_DEPTH_FACTOR)
+                                th_depth_factor=K.TH_DEPTH_FACTOR, nsets=int(os.environ.get("ORBX_STEREO_SETS", "4")),
+                                lane_offset_stage=int(os.environ.get("ORBX_STEREO_LANE_OFFSET", "2")),
+                                track_stream=os.environ.get("ORBX_STEREO_TRACK_STREAM", "1") == "1")
     sf, cap = pl.sf, pl.cap
     from orbslam2commentedbyxcm_amd.extractor import device_frames
     if args.packed_frames:

@@ -729,6 +729,16 @@ int orbx_vocabulary_transform_batch_device(orbx_vocabulary* voc, int batch, cons
 int orbx_vocabulary_set_timing(orbx_vocabulary* voc, int enable);
 int orbx_vocabulary_stage_times(orbx_vocabulary* voc, float* walk_ms, float* frame_ms);
 
+/* Alternative kernel forms and diagnostics switches, process-wide (tests and A/B tools;
+ * the product reads no environment).  Names: "pz_seg" (pyramid levels per launch, 0 = one
+ * launch), "pz_byte" (byte-read k_pyramid), "desc_tiles" (tile-major describe),
+ * "extract_dma" (single host call through DMA copies), "replay_threads" (64..1024),
+ * "dup_stage" (launch extraction stage k twice), "oct_stamps" / "call_stamps" /
+ * "match_stamps" (phase stamps to stderr).  value < 0 restores the default; name NULL
+ * restores every default.  Every form gives the same results.  A frame size's plan reads
+ * pz_seg / pz_byte / desc_tiles when an extractor first plans it. */
+int orbx_debug_set(const char* name, int value);
+
 /* Library / device info. */
 const char* orbx_version(void);
 int orbx_device_count(int* n);

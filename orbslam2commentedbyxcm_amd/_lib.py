@@ -51,6 +51,7 @@ EXPORTED = [
     "orbx_search_for_triangulation_batch_device", "orbx_match_sequence_device_ex",
     "orbx_search_local_points_device", "orbx_create_mappoints_device", "orbx_update_last_frame_device",
     "orbx_extractor_last_call_us", "orbx_compute_stereo_from_rgbd", "orbx_compute_stereo_from_rgbd_device",
+    "orbx_debug_set",
 ]
 
 ORBX_DEPTH_U16 = 0
@@ -273,11 +274,18 @@ def lib() -> C.CDLL:
     L.orbx_vocabulary_transform_batch_device.argtypes = [vp, C.c_int, vp, vp, C.c_int, C.c_int] + [vp] * 9 + [vp]
     L.orbx_vocabulary_set_timing.argtypes = [vp, C.c_int]
     L.orbx_vocabulary_stage_times.argtypes = [vp, fp, fp]
+    L.orbx_debug_set.argtypes = [C.c_char_p, C.c_int]
     L.orbx_version.restype = C.c_char_p
     L.orbx_device_count.argtypes = [ip]
     L.orbx_last_error.restype = C.c_char_p
     _lib = L
     return L
+
+
+def debug_set(name: str | None, value: int = -1) -> None:
+    """orbx_debug_set: select an alternative kernel form or a diagnostics switch
+    (value < 0: the default; name None: every default).  Tests and A/B tools only."""
+    check(lib().orbx_debug_set(None if name is None else name.encode(), int(value)))
 
 
 def check(rc: int, allow=(ORBX_OK,)) -> int:

@@ -27,7 +27,7 @@ LIB = PKG / "liborbx.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ORBX_ARCH", "gfx950")
 
-SOURCES = ["orbx_geometry.cpp", "orbx_extract.hip", "orbx_match.hip", "orbx_api.cpp", "orbx_matcher.cpp", "orbx_vocab.hip", "orbx_bow.hip", "orbx_frame.hip", "orbx_fuse.hip"]
+SOURCES = ["orbx_geometry.cpp", "orbx_extract.hip", "orbx_match.hip", "orbx_api.cpp", "orbx_matcher.cpp", "orbx_vocab.hip", "orbx_bow.hip", "orbx_frame.hip", "orbx_fuse.hip", "orbx_runtime.cpp"]
 HEADERS = ["orbx_sincos.h", "orbx_block_sort.h", "orbx_geometry.h", "orbx_kernels.h", "orbx_match_types.h", "orbx_error.h", "orb_pattern.inc", "orbx_gmem.h"]
 FLAGS = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
          f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",

@@ -23,27 +23,13 @@ using namespace orbx;
 
 namespace {
 
-thread_local std::string g_last_error;
-std::atomic<bool> g_unloading{false};
-
-// runs from the C runtime's exit / dlclose teardown of this library -- before that of the
-// HIP runtime it links against (dependents are finalised first)
-__attribute__((destructor)) void orbx_on_unload() { g_unloading.store(true); }
-
-}  // namespace
-
-void orbx::set_last_error(const std::string& msg) { g_last_error = msg; }
-bool orbx::unloading() { return g_unloading.load(); }
-
-namespace {
-
 int fail(int code, const char* what) {
-    g_last_error = what ? what : "";
+    set_last_error(what ? what : "");
     return code;
 }
 
 int hip_fail(hipError_t e, const char* where) {
-    g_last_error = std::string(where) + ": " + hipGetErrorString(e);
+    set_last_error(std::string(where) + ": " + hipGetErrorString(e));
     return ORBX_ERR_HIP;
 }
 
@@ -155,7 +141,7 @@ int prepare(orbx_extractor* ex, int W, int H, int batch) {
     HIP_TRY(dalloc(&db.dt_list, B * (size_t)p.kept_per_frame));
     HIP_TRY(dalloc(&db.dt_tile, B * (size_t)p.tiles_total));
     HIP_TRY(dalloc(&db.status, B));
-    if (getenv("ORBX_OCT_STAMPS")) HIP_TRY(dalloc(&db.oct_stamps, B * (size_t)p.L * 16));  // kOctStampWords
+    if (tuning(Tune::OctStamps, 0) > 0) HIP_TRY(dalloc(&db.oct_stamps, B * (size_t)p.L * 16));  // kOctStampWords
     HIP_TRY(hipMemcpyAsync(db.lv, p.lv, sizeof(LevelGeom) * kMaxLevels, hipMemcpyHostToDevice, ex->stream));
     HIP_TRY(hipMemcpyAsync(db.cells, p.cells.data(), sizeof(CellGeom) * p.cells.size(), hipMemcpyHostToDevice,
                            ex->stream));
@@ -370,7 +356,6 @@ extern "C" {
 
 const char* orbx_version(void) { return "orbx 0.1 (gfx950)"; }
 
-const char* orbx_last_error(void) { return g_last_error.c_str(); }
 
 int orbx_device_count(int* n) {
     if (!n) return fail(ORBX_ERR_ARG, "null");
@@ -626,8 +611,9 @@ int orbx_extract_batch(orbx_extractor* ex, int batch, const uint8_t* const* imgs
     // Default: the pyramid kernel reads the frames from the mapped pinned buffer and the
     // describe kernel writes keypoints, descriptors, counts and status words straight into
     // mapped pinned memory -- no DMA copy in either direction and one synchronisation per
-    // call.  ORBX_EXTRACT_DMA=1: the round-4 path (upload copy, results read back by copies).
-    static const bool dma = getenv("ORBX_EXTRACT_DMA") != nullptr;
+    // call.  Switch extract_dma = 1 (orbx_debug_set): the round-4 path (upload copy, results
+    // read back by copies; tests/test_gpu_extract.py runs both).
+    const bool dma = tuning(Tune::ExtractDma, 0) > 0;
     if (!dma) {
         rc = run_device(ex, batch, ex->h_in_dev, fbytes, width, height, (size_t)width, ex->h_kps_dev, ex->h_desc_dev,
                         cap > 0 ? cap : 1, ex->h_n_dev, ex->stream, false, ex->h_status_dev);

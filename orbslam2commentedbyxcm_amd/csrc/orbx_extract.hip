@@ -17,6 +17,7 @@
 #include <cstring>
 #include <type_traits>
 
+#include "orbx_error.h"
 #include "orbx_kernels.h"
 #include "orbx_sincos.h"
 
@@ -221,9 +222,6 @@ __global__ __launch_bounds__(256) ORBX_PZ_ATTR void k_pyramid(const uint8_t* __r
     // h = S[sx0]*a0 + S[sx1]*a1 is kept as hm = h & ~15 and the vertical step
     // (b*(h>>4))>>16 = (b*hm)>>20 is one v_mul_hi_u32_u24 of (b << 12, hm).  The result
     // needs no saturation: a0 + a1 <= 2049 and b0 + b1 <= 2049 bound it by 255.
-#ifdef ORBX_EXP_PZ_L0ONLY
-    if (L > 0) return;  // timing ablation: level 0 only
-#endif
     for (int l = 1; l < L; l++) {
         const int16_t* Rp = R + 8 * (l - 1);
         const int16_t* Rl = R + 8 * l;
@@ -365,11 +363,7 @@ __global__ __launch_bounds__(256) ORBX_PZ_ATTR void k_pyramid(const uint8_t* __r
                         packed |= v << (8 * k);
                     }
                     *(uint32_t*)lp = packed;
-#ifdef ORBX_EXP_PZ_NOSTORE
-                    if (packed == 0x12345678u && own != 0 && r >= wlo && r < whi) {  // timing ablation
-#else
                     if (own != 0 && r >= wlo && r < whi) {
-#endif
                         if (own == 1) *(uint32_t*)gp = packed;
                         else
                             store_owned_quad(gp, x, ox0, ox1, packed);
@@ -565,7 +559,6 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
     // ---- FAST compass test on the detection area, compaction of the survivors.
     // A thread always owns columns 4j..4j+3 (j = tid & 15) of rows tid/16 + 16 i, so
     // its detection-area column mask is computed once.
-#ifndef ORBX_EXP_NO_COMPASS
     {
         const int j = tid & 15, c0 = kSX + 4 * j, x0 = X0 + 4 * j;
         unsigned colmask = 0;
@@ -639,21 +632,17 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
             }
         }
     }
-#endif
     __syncthreads();
     // ---- exact strength of the survivors
     const int n = s_n;
-#ifndef ORBX_EXP_NO_STRENGTH
     for (int i = tid; i < n; i += 256) {
         const int rc = s_list[i];
         const int r = rc >> 8, c = rc & 255;
         s_m[r][c] = (uint8_t)fast_strength(&s_in[r + 3][c + kSX], kSW);
     }
-#endif
     __syncthreads();
     // ---- blur rows (into the survivor list's buffer, free now): 2 rows x 4 columns per
     // task (dot4), stored as row-pair u16 dwords
-#ifndef ORBX_EXP_NO_BLURROW
     for (int i = tid; i < ((kTH + 6) / 2) * (kTW / 4); i += 256) {
         const int pr = i >> 4, c0 = kSX + 4 * (i & 15);
         const uint32_t* ra = (const uint32_t*)&s_in[2 * pr][c0];
@@ -664,7 +653,6 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
         *(uint4*)&s_rowp[pr][c0 - kSX] = make_uint4(a[0] | (b[0] << 16), a[1] | (b[1] << 16), a[2] | (b[2] << 16),
                                                   a[3] | (b[3] << 16));
     }
-#endif
     __syncthreads();
     // ---- blur columns and the strength map -> global, two rows x 4 columns per task:
     // rows 2p and 2p+1 read the same four row-pair dwords (staged rows 2p..2p+7), one
@@ -823,12 +811,6 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
             }
         }
         wave_lds_fence();
-#ifdef ORBX_EXP_FC_STAGE_ONLY  // timing ablation only: staging and listing, no test or write-out
-        if (n >= 0) {
-            if (lane == 0) cell_count[(size_t)f * ncells + ci] = 0;  // no keypoints: later stages stay in bounds
-            return;
-        }
-#endif
         // neighbour test of the candidates (zero frame: no bounds checks), both thresholds
         auto keep_of = [&](int i, int& r, int& cc, int& M) -> bool {
             const int rc = list[i];
@@ -1665,9 +1647,6 @@ __device__ __forceinline__ void desc_level_of(const DescLevel* s, int L, int slo
 #define ORBX_DESC_GLDS_MAX 1000000
 #endif
 constexpr int kDescGldsMaxSlots = ORBX_DESC_GLDS_MAX;
-#ifndef ORBX_ABL_DESC
-#define ORBX_ABL_DESC 0  // timing ablations of k_describe (tools/ab_lib.sh); 0 in every shipped build
-#endif
 #ifndef ORBX_DESC_DMA
 // the LDS-DMA form below kDescGldsMaxSlots: 1 = 16-byte pieces into 48-byte rows (five
 // workgroups a CU), 2 = 4-byte pieces into 40-byte rows (24.7 KB, six a CU: configs[1]
@@ -1728,9 +1707,6 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
         n_out[f] = total;
         if (status_out) status_out[f] = status[f];  // k_octree's word (earlier on this stream)
     }
-#if ORBX_ABL_DESC == 2  // timing ablation only: no describe work at all
-    return;
-#endif
     const DescLevel& g = s_lv[l];
     const int i = slot - g.out_off;
     const int o = base + i;
@@ -1759,18 +1735,12 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
         const int d0 = (x - 15) & 3;
         const uint8_t* prow1 = plevel + (uint32_t)((y + v1) * rpitch + xs);
         const uint8_t* prow2 = plevel + (uint32_t)((y + v2) * rpitch + xs);
-#if ORBX_ABL_DESC == 1  // timing ablation only: no staging loads (garbage patch, constant rows)
-        const uint4 p0 = make_uint4(x, y, x ^ y, 7), p1 = p0, r0 = make_uint4(y, x, 3, x + y), r1 = r0;
-        const uint32_t p2 = (uint32_t)x, r2 = (uint32_t)y;
-        (void)prow1; (void)prow2;
-#else
         const uint4 p0 = *(const uint4*)prow1, p1 = *(const uint4*)(prow1 + 16);
         const uint32_t p2 = *(const uint32_t*)(prow1 + 32);
         const uint4 r0 = *(const uint4*)prow2, r1 = *(const uint4*)(prow2 + 16);
         const uint32_t r2 = *(const uint32_t*)(prow2 + 32);
-#endif
         const uint8_t* bpatch = bframe + (uint32_t)(g.off + (long long)(y - 18) * pitch + xb);
-        if constexpr (STAGE == 1 && ORBX_ABL_DESC != 1) {
+        if constexpr (STAGE == 1) {
         // the four BRIEF patches go straight to LDS (global_load_lds_dwordx4: no VGPR
         // destinations, so more waves fit a SIMD): patch by patch, the whole wave loads
         // its 111 chunks (lane L chunks L and 64 + L), from the patch base of quarter q
@@ -1797,7 +1767,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
             }
         }
         }
-        if constexpr (STAGE == 2 && ORBX_ABL_DESC != 1) {
+        if constexpr (STAGE == 2) {
             // 4-byte pieces: patch q's 370 dwords (37 rows x 10), lane L dword L + 64 j
             const uint64_t mybase = (uint64_t)(uintptr_t)bpatch;
             uint8_t* const wbp = (uint8_t*)s_bpatch[wave * 4];
@@ -1824,11 +1794,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
 #pragma unroll
             for (int j = 0; j < 7; j++) {
                 const int c = min(ql + 16 * j, 110), row = (c * 171) >> 9;
-#if ORBX_ABL_DESC == 1
-                bch[j] = make_uint4(row, c, x, y);
-#else
                 bch[j] = *(const uint4*)(bpatch + (uint32_t)(row * pitch + 16 * (c - 3 * row)));
-#endif
             }
         }
         auto row_sums = [&](const uint4& a0, const uint4& a1, uint32_t a2, int av, uint32_t& cs, uint32_t& ws) {
@@ -2132,9 +2098,9 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     const int L = plan.L;
     const long long fb = plan.pyr_frame_bytes;
     const int ncells = (int)plan.cells.size();
-    // ORBX_DUP_STAGE=k (measurement knob): launch stage k (1 pyramid .. 5 describe) twice --
+    // switch dup_stage = k (measurement): launch stage k (1 pyramid .. 5 describe) twice --
     // every stage is idempotent -- so a pipelined run prices that stage's marginal cost
-    static const int dup = getenv("ORBX_DUP_STAGE") ? atoi(getenv("ORBX_DUP_STAGE")) : 0;
+    const int dup = tuning(Tune::DupStage, 0);
     if (ev && ev[0]) (void)hipEventRecord(ev[0], stream);
     for (int rep = 0; rep < (dup == 1 ? 2 : 1); rep++) {
         // one launch per pyramid segment (orbx_geometry.h): the first reads the input
@@ -2171,12 +2137,8 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     if (stage_ev && stage_after == 2) (void)hipEventRecord(stage_ev, stream);
     for (int rep = 0; rep < (dup == 3 ? 2 : 1); rep++) {
         dim3 grid(((ncells + 3) / 4) * batch);
-#ifndef ORBX_EXP_FC_LDS_PAD
-#define ORBX_EXP_FC_LDS_PAD 0  // timing experiment: extra dynamic LDS per k_fast_cells workgroup
-#endif
         if (plan.fc_wc + 2 > kFcStride) return hipErrorInvalidValue;  // a window wider than the staged pitch
-        const size_t fc_lds = 4 * (size_t)((((plan.fc_wr + 2) * kFcStride + 2 * plan.fc_wr * plan.fc_wc) + 15) & ~15) +
-                              ORBX_EXP_FC_LDS_PAD;
+        const size_t fc_lds = 4 * (size_t)((((plan.fc_wr + 2) * kFcStride + 2 * plan.fc_wr * plan.fc_wc) + 15) & ~15);
         hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), fc_lds, stream, db.score, fb, db.cells, ncells,
                            plan.prm.ini_th, plan.prm.min_th, db.slots, plan.slots_per_frame, db.cell_count, batch,
                            plan.fc_wr, plan.fc_wc);
@@ -2184,9 +2146,6 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
     if (ev && ev[3]) (void)hipEventRecord(ev[3], stream);
     if (stage_ev && stage_after == 3) (void)hipEventRecord(stage_ev, stream);
     for (int rep = 0; rep < (dup == 4 ? 2 : 1); rep++) {
-#ifndef ORBX_EXP_OCT_LDS_PAD
-#define ORBX_EXP_OCT_LDS_PAD 0  // timing experiment: extra dynamic LDS per k_octree workgroup
-#endif
         // A launch's dynamic LDS is sized for its largest level.  For a batch whose level-0
         // node table is large enough to limit the workgroups per CU (over 32 KB: fewer than
         // the 5 its registers allow), the levels whose node capacity is at most 3/8 of level
@@ -2211,7 +2170,7 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
             for (int l = la; l < lb; l++) mx = plan.lv[l].ncap > mx ? plan.lv[l].ncap : mx;
             // the tile-major describe's bins need every level's tiles within NC (one launch)
             const int NC = plan.desc_tiles ? (plan.max_ncap + 63) & ~63 : (mx + 63) & ~63;
-            const size_t lds = (size_t)NC * kOctNodeBytes + ORBX_EXP_OCT_LDS_PAD;
+            const size_t lds = (size_t)NC * kOctNodeBytes;
             // int16 node ids / ranks, and one workgroup's LDS (beside its static arrays)
             if (NC > 32767 || lds > 152 * 1024) return hipErrorInvalidValue;
             if (lds > 64 * 1024) {
@@ -2237,10 +2196,7 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
         } else {
             dim3 grid(((plan.kept_per_frame + 15) / 16) * batch);
             auto kern = plan.kept_per_frame <= kDescGldsMaxSlots ? k_describe<ORBX_DESC_DMA> : k_describe<0>;
-#ifndef ORBX_EXP_DESC_LDS_PAD
-#define ORBX_EXP_DESC_LDS_PAD 0  // timing experiment: extra dynamic LDS per k_describe workgroup
-#endif
-            hipLaunchKernelGGL(kern, grid, dim3(256), ORBX_EXP_DESC_LDS_PAD, stream, db.pyr, db.blur, fb, db.lv, L, db.kept,
+            hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, db.pyr, db.blur, fb, db.lv, L, db.kept,
                                plan.kept_per_frame, db.kept_count, (orbx_keypoint*)kps, desc, cap, n_per_frame, batch,
                                l0, l0_fp, l0_pitch, db.status, status_out);
         }

@@ -3,6 +3,7 @@
 // reference expression operation by operation.
 #include <algorithm>
 #include "orbx_geometry.h"
+#include "orbx_error.h"
 
 #include <cmath>
 #include <cstdio>
@@ -183,17 +184,18 @@ static bool pyramid_segment(Plan& plan, PzSeg& s, int tw, int th) {
 
 static bool pyramid_tiles(Plan& plan) {
     const int L = plan.L;
-    // ORBX_PZ_TILE=WxH / ORBX_PZ_TILE2=WxH override the first / later segments' tile size,
-    // ORBX_PZ_SEG=n the levels per segment (0: one segment); tuning, the output is the same
+    // debug builds: ORBX_PZ_TILE=WxH / ORBX_PZ_TILE2=WxH override the first / later
+    // segments' tile size; switch pz_seg = n the levels per segment (0: one segment);
+    // tuning, the output is the same
     int tw = kPzTW, th = kPzTH, tw2 = kPzTW2, th2 = kPzTH2, seg = kPzSegLevels;
     auto tile_env = [](const char* name, int& w, int& h) {
         int a = 0, b = 0;
-        if (const char* e = std::getenv(name))
+        if (const char* e = debug_env(name))
             if (std::sscanf(e, "%dx%d", &a, &b) == 2 && a >= 16 && b >= 16) { w = a; h = b; }
     };
     tile_env("ORBX_PZ_TILE", tw, th);
     tile_env("ORBX_PZ_TILE2", tw2, th2);
-    if (const char* e = std::getenv("ORBX_PZ_SEG")) seg = std::atoi(e);
+    seg = tuning(Tune::PzSeg, seg);
     if (seg < 2 || seg > L) seg = L;
     plan.pz_nseg = 0;
     for (int l0 = 0;;) {
@@ -207,8 +209,8 @@ static bool pyramid_tiles(Plan& plan) {
     }
     // k_pyramid<true> needs the source bytes of any 4 consecutive output columns (sx0 of the
     // first .. sx1 of the last) within 8 bytes: scale factors up to about 2
-    // (ORBX_PZ_BYTE=1 forces the byte-read form: tuning, the output is the same)
-    plan.pz_win = !std::getenv("ORBX_PZ_BYTE");
+    // (switch pz_byte = 1 forces the byte-read form: tuning, the output is the same)
+    plan.pz_win = tuning(Tune::PzByte, 0) <= 0;
     for (int l = 1; l < L && plan.pz_win; l++) {
         const LevelGeom& g = plan.lv[l];
         const int16_t* xt = plan.rtab.data() + g.xtab_off;
@@ -338,16 +340,14 @@ bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
     plan.kept_per_frame = out_off;
     plan.tiles_total = tile_first;
     {
-        // k_describe_tiles (ORBX_DESC_TILES=1; measured slower than k_describe, DESIGN.md
+        // k_describe_tiles (switch desc_tiles = 1; measured slower than k_describe, DESIGN.md
         // section 4 item 5): k_octree bins each level's kept slots into its tiles with
         // NC-entry LDS counters and 16-bit list offsets
         const int NC = (plan.max_ncap + 63) & ~63;
         bool fits = true;
         for (int l = 0; l < plan.L; l++)
             fits = fits && plan.lv[l].tiles_x * plan.lv[l].tiles_y <= NC && plan.lv[l].ncap < 65536;
-        const char* e = getenv("ORBX_DESC_TILES");
-        const int mode = e ? atoi(e) : -1;
-        plan.desc_tiles = fits && mode == 1;
+        plan.desc_tiles = fits && tuning(Tune::DescTiles, 0) == 1;
     }
     plan.rtab.resize(plan.rtab.size() + 64, 0);  // k_pyramid reads row taps in batches of 8 rows
     plan.ok = true;

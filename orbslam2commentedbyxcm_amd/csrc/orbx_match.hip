@@ -14,6 +14,7 @@
 
 #include "orbx_block_sort.h"
 #include "orbx_gmem.h"
+#include "orbx_error.h"
 #include "orbx_kernels.h"
 
 namespace orbx {
@@ -1820,11 +1821,8 @@ hipError_t launch_stage_copy(const void* src, void* dst, size_t bytes, hipStream
 }
 
 // k_seq_commit's dynamic LDS: the replay's lists, then the claims and the owner map
-#ifndef ORBX_EXP_COMMIT_LDS_PAD
-#define ORBX_EXP_COMMIT_LDS_PAD 0  // timing experiment: extra dynamic LDS per k_seq_commit workgroup
-#endif
 static size_t seq_commit_lds(int cap, int rt) {
-    return (size_t)kTopK * rt * 4 + (size_t)cap * 8 + ORBX_EXP_COMMIT_LDS_PAD;
+    return (size_t)kTopK * rt * 4 + (size_t)cap * 8;
 }
 
 // Threads of the replay workgroup: `rt` if given (64, 128, 256, 512 or 1024), else
@@ -1836,11 +1834,7 @@ static size_t seq_commit_lds(int cap, int rt) {
 // chunk, 90 iterations of ~1.9 us at 256 against 109 of ~1.2 us at 64 for a12).
 static int replay_threads(int rt, int nprob) {
     if (rt != 64 && rt != 128 && rt != 256 && rt != 512 && rt != 1024) {
-        static const int env = [] {
-            const char* v = getenv("ORBX_REPLAY_THREADS");
-            return v ? atoi(v) : 0;
-        }();
-        rt = env;
+        rt = tuning(Tune::ReplayThreads, 0);
     }
     if (rt != 64 && rt != 128 && rt != 256 && rt != 512 && rt != 1024) rt = nprob == 1 ? 64 : 256;
     return rt;
@@ -2199,11 +2193,8 @@ hipError_t launch_proj_search(const ProjProblem* d_probs, int nprob, const ProjP
         if (small) return hipErrorInvalidValue;
         dlds = qlds = false;
     }
-#ifndef ORBX_EXP_SCORE_LDS_PAD
-#define ORBX_EXP_SCORE_LDS_PAD 0  // timing experiment: extra dynamic LDS per k_proj_search workgroup
-#endif
     const size_t lds = ProjLds(max_n, max_nq, dlds, qlds, P.noct, split_grids == nullptr,
-                               !(split_grids && kSplitSxyGlobal)).total + ORBX_EXP_SCORE_LDS_PAD;
+                               !(split_grids && kSplitSxyGlobal)).total;
     if (lds > limit) return hipErrorInvalidValue;
     const void* fn;
     const int nt = tiny ? kProjThreadsTiny : (small ? kProjThreadsSmall : (split_grids ? kSplitScoreThreads : kProjThreads));

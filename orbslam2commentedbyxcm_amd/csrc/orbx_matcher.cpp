@@ -324,9 +324,9 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
     ProjParams P = base_params;
     P.mp_obs = d_obs;
     P.noct = noct;
-    // ORBX_CALL_STAMPS=1: the call's host phases and the replay's counters to stderr
+    // switch call_stamps = 1: the call's host phases and the replay's counters to stderr
     // (diagnostics only)
-    static const bool call_stamps = getenv("ORBX_CALL_STAMPS") != nullptr;
+    const bool call_stamps = tuning(Tune::CallStamps, 0) > 0;
     unsigned long long* d_st = nullptr;
     const auto t_flush = std::chrono::steady_clock::now();
     if (call_stamps) {
@@ -356,8 +356,8 @@ int run_proj(orbx_matcher* m, const orbx_frame_view* f, int32_t* frame_mp, const
     if (mapped) {
         // inputs copied in by k_stage_copy (no DMA), results written to mapped memory
         const size_t staged = m->arena.take_staged();
-        // replay width: the row's (replay_rt) unless ORBX_REPLAY_THREADS overrides it
-        static const bool rt_env = getenv("ORBX_REPLAY_THREADS") != nullptr;
+        // replay width: the row's (replay_rt) unless switch replay_threads overrides it
+        const bool rt_env = tuning(Tune::ReplayThreads, 0) > 0;
         HIP_TRY(launch_seq_split(d_prob, 1, P, d_grid, gcap, d_scr, d_off, s, 0, rt_env ? 0 : replay_rt,
                                  m->arena.host_dev, m->arena.base, staged));
     } else {
@@ -792,7 +792,7 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
     // ORBX_MATCH_STAMPS=1: per-phase wall-clock breakdown of the search kernel to stderr
     // (diagnostics only; synchronises the stream).
     // (with grids -- the split launches and the lean form -- the commit kernel's replay only)
-    const bool stamps = getenv("ORBX_MATCH_STAMPS") != nullptr;
+    const bool stamps = tuning(Tune::MatchStamps, 0) > 0;
     unsigned long long* d_st = nullptr;
     if (stamps) {
         HIP_TRY(hipMalloc(&d_st, sizeof(unsigned long long) * kStampWords * npairs));

@@ -21,7 +21,7 @@ One step on every rank = for its B stereo keyframes of a W*B-keyframe window:
 
 Step k+1's extraction overlaps step k's stereo / BoW / gather / triangulation: sets of
 extractor pairs, slabs, gathered buffers and triangulation outputs rotate (four by
-default, ORBX_KF_SETS), and a set is reused only after the triangulation that last read
+default, `nsets`), and a set is reused only after the triangulation that last read
 it (its event) -- so the gather of a later step never overwrites neighbours that an
 earlier step's triangulation is still reading.  `windows` > 1 gives each step its own keyframe window
 (same poses, another texture), so a cross-step ordering fault changes bytes.  The neighbour plan (covisibility proxy: the nn
@@ -205,7 +205,8 @@ class StereoKeyFramePipeline:
 
     def __init__(self, batch: int, rank: int = 0, world: int = 1, device: int = 0, nn: int = 10, seq_seed: int = 3,
                  vocab_text: bytes | None = None, settings: dict | None = None, group=None, windows: int = 1,
-                 on_step_done=None, collective: bool = False, level0_in_place: bool = True):
+                 on_step_done=None, collective: bool = False, level0_in_place: bool = True, nsets: int = 4,
+                 lane_offset_stage: int = 3, gather_async: bool = True):
         import torch
 
         from . import synth
@@ -221,9 +222,8 @@ class StereoKeyFramePipeline:
         # the one under test on a single GPU; world > 1 always exchanges
         self.collective = self.world > 1 or bool(collective)
         # the exchange's work handle is waited for on the triangulation stream only
-        # (ORBX_GATHER_SYNC=1: the round-4 order, the matcher stream waits for it)
-        import os
-        self.gather_async = os.environ.get("ORBX_GATHER_SYNC") != "1"
+        # (gather_async False: the round-4 order, the matcher stream waits for it)
+        self.gather_async = bool(gather_async)
         self.W, self.H = s["width"], s["height"]
         self.dev = torch.device("cuda", device)
         self.mb = s["bf"] / s["fx"]
@@ -258,8 +258,8 @@ class StereoKeyFramePipeline:
         # j-1's triangulation -- the GPU idled between the steps' extractions.  Four sets
         # give it slack (r05ao-az, interleaved: two 48.6-49.6k, three 49.0-50.2k, four
         # 54.4-55.2k, five 52.8-54.5k, six and eight 50-52k keyframes/s: beyond four the
-        # eight extractor streams outnumber the hardware queues).  ORBX_KF_SETS overrides.
-        self.nsets = max(2, int(os.environ.get("ORBX_KF_SETS", "4")))
+        # eight extractor streams outnumber the hardware queues)
+        self.nsets = max(2, int(nsets))
         self.sets = [(ORBextractor(*prm, device=device), ORBextractor(*prm, device=device))
                      for _ in range(self.nsets)]
         # level 0 read in place from the pitched input frames below (no copy into the
@@ -271,8 +271,8 @@ class StereoKeyFramePipeline:
         # stage 3 (FAST cells), so the two run out of phase instead of in step (r05bn,
         # interleaved: in step 49.5-50.2k keyframes/s, after stage 2 49.4-51.9k, after
         # stage 3 50.6-52.5k; r05bo: after stage 3 49.4-51.2k against 48.4-51.2k after
-        # stage 4).  ORBX_KF_LANE_OFFSET=k overrides (0: in step)
-        lo = int(os.environ.get("ORBX_KF_LANE_OFFSET", "3"))
+        # stage 4).  lane_offset_stage 0: in step
+        lo = int(lane_offset_stage)
         self.lane_ev = [a.set_stage_event(lo) for a, _ in self.sets] if lo > 0 else None
         self.sf = self.sets[0][0].GetScaleFactors()
         self.cap = self.sets[0][0].max_keypoints(self.W, self.H)

@@ -39,7 +39,8 @@ class SequencePipeline:
                  nbuf: int = 2, matcher_mode: int | None = None, match_after_stage: int = 0,
                  lane_offset_stage: int | None = None, match_cu_stride: int = 1,
                  match_priority: int = 0, on_matched=None, local_map: bool = False, local_window: int = 3,
-                 local_th: float = 1.0, level0_in_place: bool = True, retry_below: int = 20):
+                 local_th: float = 1.0, level0_in_place: bool = True, retry_below: int = 20,
+                 first_in_phase: bool = False):
         import torch
 
         self.B, self.W, self.H = int(batch), int(width), int(height)
@@ -50,8 +51,7 @@ class SequencePipeline:
         self.fx, self.fy, self.cx, self.cy, self.depth, self.th = fx, fy, cx, cy, depth, th
         # TrackWithMotionModel searches a pair again at 2*th when it found fewer than 20
         # matches (Tracking.cc:988-994); 0: one search (the bare SearchByProjection)
-        import os
-        self.retry_below = int(os.environ.get("ORBX_TRACK_RETRY", retry_below))
+        self.retry_below = int(retry_below)
         # The matcher's stream is created here, before the extraction lanes' streams
         # (orbx_stream_create; match_cu_stride k > 1 also confines it to CUs 0, k,
         # 2k, ...; match_priority: its HIP stream priority).  HIP hands out its hardware queues in stream-creation order, and
@@ -138,8 +138,7 @@ class SequencePipeline:
         if lane_offset_stage is None:
             lane_offset_stage = 3 if int(params[2]) > 8 else 2
         self.lane_offset_stage = int(lane_offset_stage)
-        import os
-        self.first_in_phase = os.environ.get("ORBX_PIPE_FIRST_INPHASE", "0") == "1"
+        self.first_in_phase = bool(first_in_phase)
         self.lane_ev = [e.set_stage_event(lane_offset_stage) for e in self.exs] \
             if (lane_offset_stage and not match_after_stage and self.S > 1) else None
         # on_matched(b): called right after a batch's matching is enqueued on self.ms and
@@ -181,7 +180,7 @@ class SequencePipeline:
             # first_in_phase, on a run's first batch (nothing pending to match): there the
             # lanes start together, and the offset forms on the second batch, where the
             # first batch's matching runs beside the waiting lane instead of nothing
-            # (ORBX_PIPE_FIRST_INPHASE=1; r05as: +0.4 % at 20 steps, within noise -- off)
+            # (first_in_phase; r05as: +0.4 % at 20 steps, within noise -- off)
             if self.lane_ev and c > 0 and not (self.first_in_phase and self.match and self.pipelined
                                                and self.pending is None):
                 from .extractor import stream_wait_event

@@ -46,7 +46,7 @@ class StereoSequencePipeline:
                  params=(2000, 1.2, 8, 20, 7), track: bool = True, th: float = 7.0, nnratio: float = 0.9,
                  check_ori: bool = True, th_depth_factor: float = 35.0, max_d: float | None = None,
                  matcher_mode: int | None = None, device: int = 0, level0_in_place: bool = True,
-                 retry_below: int = 20):
+                 retry_below: int = 20, nsets: int = 4, lane_offset_stage: int = 2, track_stream: bool = True):
         import torch
 
         from .extractor import stream_create
@@ -68,18 +68,16 @@ class StereoSequencePipeline:
         # With two extractor pairs and no lane offset it measured 1-2 % slower (r05bd); with
         # the offset and four pairs it is the faster form (r05ca-cc, interleaved: three pairs
         # on one stream 57.0-58.0k stereo frames/s, on two 58.4-59.3k, four pairs on two
-        # 59.8-60.7k, five 59.8-60.0k).  ORBX_STEREO_TRACK_STREAM=0: one stream
-        import os
-        self._own_ts = stream_create(device, 1, 0) if os.environ.get("ORBX_STEREO_TRACK_STREAM", "1") == "1" \
-            else None
+        # 59.8-60.7k, five 59.8-60.0k).  track_stream False: one stream
+        self._own_ts = stream_create(device, 1, 0) if track_stream else None
         self.ts = torch.cuda.ExternalStream(self._own_ts, device=self.dev) if self._own_ts else self.ms
         # extractor pairs in rotation: a set is re-extracted only after the matching that last
         # read it (ev_m).  Four: with the right image's lane offset (below) the matching no
         # longer keeps up with two (r05bq-br, one matcher stream, interleaved: two sets
         # 54.7-54.9k stereo frames/s, three 57.2-58.2k, four 56.6-57.6k; before the offset
         # three measured 0.8 % slower, r05ap), and with the tracking on its own stream four
-        # beat three (above).  ORBX_STEREO_SETS overrides
-        self.nsets = max(2, int(os.environ.get("ORBX_STEREO_SETS", "4")))
+        # beat three (above)
+        self.nsets = max(2, int(nsets))
         self.sets = [(ORBextractor(*params, device=device), ORBextractor(*params, device=device))
                      for _ in range(self.nsets)]
         # level 0 read from the caller's frames when their rows are 64-byte aligned
@@ -92,8 +90,8 @@ class StereoSequencePipeline:
         # stage 2 (blur + FAST strength), as the monocular pipeline's lanes, so the two run
         # out of phase instead of in step (r05bm, interleaved: 53.6-54.0k in step, 54.6-55.1k
         # after stage 2, 54.0-55.1k after stage 3, 53.1-53.9k after stage 1).
-        # ORBX_STEREO_LANE_OFFSET=k overrides (0: in step)
-        lo = int(os.environ.get("ORBX_STEREO_LANE_OFFSET", "2"))
+        # lane_offset_stage 0: in step
+        lo = int(lane_offset_stage)
         self.lane_ev = [a.set_stage_event(lo) for a, _ in self.sets] if lo > 0 else None
         self.smatcher = ORBmatcher(0.6, True, device=device)  # ComputeStereoMatches' handle (stream, arena)
         self.tmatcher = ORBmatcher(nnratio, check_ori, device=device)  # TrackWithMotionModel: ORBmatcher(0.9, true)

@@ -95,3 +95,22 @@ def test_stage_event_arguments(orbx_built):
     assert L.lib().orbx_stream_create(0, 4, 0, None) == L.ORBX_ERR_ARG
     assert L.lib().orbx_stream_create(0, 4, -1, C.byref(st)) == L.ORBX_ERR_ARG
     assert L.lib().orbx_stream_destroy(None) == L.ORBX_ERR_ARG
+
+
+def test_debug_switches_need_no_gpu_and_reject_unknown_names(orbx_built):
+    """orbx_debug_set (alternative kernel forms, diagnostics): known names set and reset
+    without a GPU, unknown names fail with ORBX_ERR_ARG; the product reads no environment
+    (no getenv outside the debug-build branch of orbx_runtime.cpp)."""
+    from orbslam2commentedbyxcm_amd import OrbxError
+    from orbslam2commentedbyxcm_amd import _lib as L
+    for name in ("pz_seg", "pz_byte", "desc_tiles", "extract_dma", "replay_threads", "dup_stage", "oct_stamps",
+                 "call_stamps", "match_stamps"):
+        L.debug_set(name, 1)
+        L.debug_set(name, -1)
+    L.debug_set(None)
+    with pytest.raises(OrbxError) as e:
+        L.debug_set("no_such_switch", 1)
+    assert e.value.code == L.ORBX_ERR_ARG
+    csrc = ROOT / "orbslam2commentedbyxcm_amd" / "csrc"
+    users = [f.name for f in csrc.iterdir() if f.suffix in (".cpp", ".hip", ".h") and "getenv(" in f.read_text()]
+    assert users == ["orbx_runtime.cpp"], users

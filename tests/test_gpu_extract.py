@@ -12,6 +12,14 @@ from orbslam2commentedbyxcm_amd import ORBextractor, synth
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture
+def switch():
+    """orbx_debug_set for one test: every switch back to its default afterwards."""
+    from orbslam2commentedbyxcm_amd import _lib as L
+    yield L.debug_set
+    L.debug_set(None)
+
+
 def _cmp(kp_gpu, desc_gpu, kp_ref, desc_ref):
     assert len(kp_gpu) == len(kp_ref), (len(kp_gpu), len(kp_ref))
     for f in ("x", "y", "size", "angle", "response", "octave", "class_id"):
@@ -42,12 +50,12 @@ def test_pyramid_matches_oracle(oracle, orbx_built):
 
 
 @pytest.mark.parametrize("sf,nl,byte", [(1.2, 8, True), (1.5, 6, False), (2.0, 3, False), (2.5, 3, False)])
-def test_pyramid_forms_match_oracle(oracle, orbx_built, monkeypatch, sf, nl, byte):
+def test_pyramid_forms_match_oracle(oracle, orbx_built, switch, sf, nl, byte):
     """Both k_pyramid forms: the dword-window one (any 4 columns' resize taps within 8
-    source bytes, scale factors up to 2) and the byte-read one (ORBX_PZ_BYTE=1, or a
+    source bytes, scale factors up to 2) and the byte-read one (switch pz_byte = 1, or a
     larger scale factor such as 2.5)."""
     if byte:
-        monkeypatch.setenv("ORBX_PZ_BYTE", "1")
+        switch("pz_byte", 1)
     img = synth.frame(12)
     ex = ORBextractor(1000, sf, nl, 20, 7)
     kps, desc = ex(img)
@@ -82,14 +90,14 @@ def test_other_configs_match_oracle(oracle, orbx_built, cfg):
 
 @pytest.mark.parametrize("prm,size,B", [((1000, 1.2, 8, 20, 7), (640, 480), 8), ((5000, 1.2, 12, 20, 7), (640, 480), 8),
                                         ((2000, 1.2, 8, 20, 7), (1241, 376), 4)])
-def test_describe_tiles_form_matches_oracle(oracle, orbx_built, monkeypatch, prm, size, B):
-    """The tile-major describe (ORBX_DESC_TILES=1: k_octree bins the kept slots by level
+def test_describe_tiles_form_matches_oracle(oracle, orbx_built, switch, prm, size, B):
+    """The tile-major describe (switch desc_tiles = 1: k_octree bins the kept slots by level
     tile, k_describe_tiles stages each tile once) gives the same keypoints and
     descriptors; the setting is read when an extractor plans a frame size."""
     import torch
 
     from oracle import checks
-    monkeypatch.setenv("ORBX_DESC_TILES", "1")
+    switch("desc_tiles", 1)
     W, H = size
     frames = synth.frames(B, W, H, first_seed=40)
     ex = ORBextractor(*prm)
@@ -165,3 +173,23 @@ def test_level0_in_place(oracle, orbx_built):
     for b in range(B):
         assert np.array_equal(u1[b, :n1[b]], u2[b, :n1[b]]) and np.array_equal(d1[b, :n1[b]], d2[b, :n1[b]]), b
     assert (u1[0, :n1[0]] >= 0).sum() > 100
+
+
+@pytest.mark.parametrize("dma", [0, 1])
+@pytest.mark.parametrize("W,H,prm", [(640, 480, (1000, 1.2, 8, 20, 7)), (1241, 376, (2000, 1.2, 8, 20, 7))])
+def test_host_call_paths_match_oracle(oracle, orbx_built, switch, dma, W, H, prm):
+    """The single / batched host calls through mapped memory (the default: the pyramid
+    reads the frames from pinned host memory, the describe kernel writes into it) and
+    through DMA copies (switch extract_dma = 1), at a packed 1241-px width too."""
+    switch("extract_dma", dma)
+    imgs = synth.frames(3, W, H, first_seed=70)
+    ex = ORBextractor(*prm)
+    p = oracle.params(*prm)
+    kps, desc = ex(imgs[0])
+    kr, dr, _ = oracle.extract(imgs[0], p)
+    _cmp(kps, desc, kr, dr)
+    kb, db, nb = ex.extract_batch(imgs)
+    for b in range(len(imgs)):
+        kr, dr, _ = oracle.extract(imgs[b], p)
+        _cmp(kb[b][: nb[b]], db[b][: nb[b]], kr, dr)
+

@@ -16,9 +16,10 @@ CSRC = ROOT / "orbslam2commentedbyxcm_amd" / "csrc"
 @pytest.fixture(scope="module")
 def plan_exe(tmp_path_factory):
     exe = tmp_path_factory.mktemp("pz") / "pyramid_plan"
-    subprocess.run(["g++", "-O1", "-std=c++17", f"-I{CSRC}", f"-I{ROOT / 'include'}",
-                    str(ROOT / "tests" / "cpp" / "pyramid_plan.cpp"), str(CSRC / "orbx_geometry.cpp"), "-o", str(exe)],
-                   check=True)
+    # a debug build of the planner (-DORBX_DEBUG=1): it reads ORBX_PZ_SEG from the environment
+    subprocess.run(["g++", "-O1", "-std=c++17", "-DORBX_DEBUG=1", f"-I{CSRC}", f"-I{ROOT / 'include'}",
+                    str(ROOT / "tests" / "cpp" / "pyramid_plan.cpp"), str(CSRC / "orbx_geometry.cpp"),
+                    str(CSRC / "orbx_runtime.cpp"), "-o", str(exe)], check=True)
     return exe
 
 
