@@ -507,6 +507,9 @@ def main():
                     help="skip the second measurement of the step with TrackLocalMap's SearchLocalPoints")
     ap.add_argument("--no-exchange", action="store_true",
                     help="at --gpus > 1, skip the configs[3] keyframe-exchange leg (RCCL all-gather between ranks)")
+    ap.add_argument("--track-retry", type=int, default=20,
+                    help="TrackWithMotionModel's second search at 2*th below this many matches (Tracking.cc:988-994; "
+                         "0 = one search, for pricing it)")
     ap.add_argument("--selftest-launch", action="store_true", help=argparse.SUPPRESS)
     args, _ = ap.parse_known_args()
 
@@ -566,7 +569,8 @@ def main():
                           match_cu_stride=int(os.environ.get("ORBX_MATCH_CUSTRIDE", "1")),
                           match_priority=int(os.environ.get("ORBX_MATCH_STREAM_PRIO", "0")),
                           level0_in_place=os.environ.get("ORBX_L0_COPY") != "1",
-                          first_in_phase=os.environ.get("ORBX_PIPE_FIRST_INPHASE", "0") == "1")
+                          first_in_phase=os.environ.get("ORBX_PIPE_FIRST_INPHASE", "0") == "1",
+                          retry_below=args.track_retry)
     S = pl.S
     nbufs = len(pl.kps)  # output buffer sets in rotation
     lane_off = pl.lane_offset_stage if pl.lane_ev is not None else None  # None: no offset applied

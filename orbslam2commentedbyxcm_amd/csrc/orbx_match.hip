@@ -2628,7 +2628,7 @@ __global__ __launch_bounds__(kStereoIdxThreads) void k_stereo_index(StereoBatch 
         atomicAdd(&cnt[o * rows + yb], 1);
         // the rows this keypoint's list entries would cover (rows outside the image, which
         // keypoints >= 16 px inside never reach, are dropped)
-        const float r = 2.0f * sb.scale[kp.octave];
+        const float r = 2.0f * sb.scale[o];  // the clamped octave k_stereo tests the band with
         const int lo = max((int)floorf(kp.y - r), 0), hi = min((int)ceilf(kp.y + r), rows - 1);
         if (lo <= hi) {
             atomicAdd(&cov[lo], 1);

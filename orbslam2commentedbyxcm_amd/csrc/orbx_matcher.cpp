@@ -809,12 +809,14 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
         // Tracking::TrackWithMotionModel (Tracking.cc:988-994): pairs left with fewer than
         // retry_below matches are searched again at 2*th.  The gate is read on the device
         // (k_seq_build), so nothing synchronises; the skipped pairs' workgroups leave at
-        // once.  One lean launch (sort, scoring and replay in one workgroup per pair): the
-        // retried pairs are rare, the launch count is what the common case pays.
+        // once.  One launch of the one-wave form (sort, scoring and replay in one wave per
+        // pair, the smallest footprint): the retried pairs are rare, and what the common case
+        // pays is getting the launch's workgroups onto CUs the extraction keeps busy -- the
+        // lean 1024-thread form took 282 us per launch there to skip every pair (r06d trace).
         A.retry_below = sq->retry_below;
         A.th = 2.f * sq->th;
         HIP_TRY(launch_seq_build(A, npairs, d_q, d_prob, d_off, s));
-        HIP_TRY(launch_proj_search(d_prob, npairs, P, d_scr, d_off, cap, cap, s, false, false, true, nullptr));
+        HIP_TRY(launch_proj_search(d_prob, npairs, P, d_scr, d_off, cap, cap, s, false, true, false, nullptr));
     }
     if (m->timing) {
         HIP_TRY(hipEventRecord(ev[1], s));
