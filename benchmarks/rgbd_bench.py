@@ -182,7 +182,9 @@ def main(argv=None):
     dev = torch.device("cuda", gpu)
     pl = RGBDSequencePipeline(B, S.W, S.H, S.FX, S.FY, S.CX, S.CY, S.DIST, S.BF, params=S.PARAMS,
                               depth_map_factor=S.DEPTH_MAP_FACTOR, th_depth_factor=S.TH_DEPTH_FACTOR,
-                              lanes=args.lanes, nbuf=int(os.environ.get("ORBX_PIPE_NBUF", "2")), device=gpu)
+                              lanes=args.lanes, nbuf=int(os.environ.get("ORBX_PIPE_NBUF", "2")), device=gpu,
+                              matcher_mode=None if "ORBX_MATCH_MODE" not in os.environ
+                              else int(os.environ["ORBX_MATCH_MODE"]))
     sf, cap = pl.sf, pl.cap
     d_gray = device_frames(gray, dev)
     d_depth = torch.from_numpy(depth).to(dev)

@@ -11,6 +11,7 @@
 #   rows                  bench.py --rows (single drop-in calls) -> gpurun_out/TAG_rows.json
 #   abenv=N,WL,ENV1,ENV2..  interleaved env A/B (tools/ab_envp.sh; ENV "K=V" or "-")
 #   ablib=N,WL,TAG1,TAG2..  interleaved library-build A/B (tools/ab_lib.sh)
+#   kprof=WL,TAG1,TAG2..    kernel-trace A/B of library builds (tools/kprof_lib.sh)
 #   run=CMD               any command (spaces as '+'), e.g. run=python+tests/foo.py
 # Args inside a step use ',' between fields and '+' for spaces.
 set -o pipefail
@@ -57,6 +58,9 @@ for step in "$@"; do
     ablib)
       IFS=',' read -r -a a <<< "$arg"
       bash tools/ab_lib.sh ${a[0]} ${a[1]} "${a[@]:2}" || exit 1 ;;
+    kprof)
+      IFS=',' read -r -a a <<< "$arg"
+      bash tools/kprof_lib.sh ${a[0]} "${a[@]:1}" || exit 1 ;;
     run)
       timeout -k 10 900 ${arg//+/ } || exit 1 ;;
     *)
