@@ -100,7 +100,7 @@ struct orbx_extractor {
 namespace {
 
 void free_buffers(DeviceBuffers& db) {
-    void* ptrs[] = {db.lv, db.cells, db.rtab, db.pyr, db.blur, db.surv, db.slots, db.cell_count,
+    void* ptrs[] = {db.lv, db.cells, db.rtab, db.pyr, db.blur, db.score, db.slots, db.cell_count,
                     db.keys, db.key_node, db.kept, db.kept_count, db.status, db.oct_stamps, db.dt_list,
                     db.dt_tile};
     for (void* p : ptrs)
@@ -131,7 +131,7 @@ int prepare(orbx_extractor* ex, int W, int H, int batch) {
     // slack: k_describe's dword patch loads may reach a few bytes past a level's last row
     HIP_TRY(dalloc(&db.pyr, B * (size_t)p.pyr_frame_bytes + 65536));
     HIP_TRY(dalloc(&db.blur, B * (size_t)p.pyr_frame_bytes + 65536));
-    HIP_TRY(dalloc(&db.surv, B * (size_t)p.tiles_total * kSurvBlock));
+    HIP_TRY(dalloc(&db.score, B * (size_t)p.pyr_frame_bytes + 65536));  // k_fast_cells reads past windows
     HIP_TRY(dalloc(&db.slots, B * (size_t)p.slots_per_frame));
     HIP_TRY(dalloc(&db.cell_count, B * p.cells.size()));
     HIP_TRY(dalloc(&db.keys, B * (size_t)p.keys_per_frame));

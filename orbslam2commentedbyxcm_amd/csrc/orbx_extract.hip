@@ -488,31 +488,14 @@ __device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
 //    non-zero NMS neighbour in k_fast_cells, and M > t requires two adjacent compass
 //    points (ring 0/4/8/12) beyond t on the same side (every 9-arc holds two).  So
 //    a cheap 4-pixels-per-lane compass test rejects most pixels (M := 0), the
-//    survivors are compacted and only they run the full 16-arc strength;
-//  * FAST's non-max suppression (round 6): cv::FAST(cell, t, true) keeps a corner p iff
-//    M_p > t and M_p beats every 8-neighbour inside the cell's detection area (k_fast_cells'
-//    comment), which is threshold-independent apart from M_p > t.  So the survivors of
-//    M_p > t_c = max(t_q, 1) and M_p > (the max of its same-cell neighbours' M) are the
-//    only pixels a cell can ever keep, at either threshold.  They are found here, where M
-//    already is in LDS (plus a 1-pixel ring of M around the tile for the neighbours in the
-//    next tiles), and written per tile in raster order (kSurvBlock) -- 2-3 % of the pixels
-//    -- instead of the dense M plane k_fast_cells used to read back (115.7 MB per 128-frame
-//    configs[1] launch).
-constexpr int kRY = 4;  // staged rows above (and below) the tile: FAST's 3 + the ring's 1
+//    survivors are compacted and only they run the full 16-arc strength.
 __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-                                                     uint8_t* __restrict__ surv, long long fb,
+                                                     uint8_t* __restrict__ score, long long fb,
                                                      const LevelGeom* __restrict__ lv, int L, int tiles_pf,
                                                      int nframes, int tq, const uint8_t* __restrict__ l0,
                                                      long long l0_fp, int l0_pitch) {
-    __shared__ __align__(16) uint8_t s_in[kTH + 2 * kRY][kSW];
-    // M of the tile and a 1-pixel ring: pixel (r, c), r in [-1, kTH], c in [-1, kTW], at
-    // s_m[r + 1][c + 1]
-    constexpr int kMP = kTW + 4;
-    __shared__ __align__(16) uint8_t s_m[kTH + 2][kMP];
-    __shared__ unsigned long long s_sbits[kTH];  // survivor bit per tile pixel, row by row
-    // FAST cell boundaries through the tile: bit 0 = the pixel's left (top) neighbour lies
-    // in another cell, bit 1 = its right (bottom) neighbour does
-    __shared__ uint8_t s_cbx[kTW], s_cby[kTH];
+    __shared__ __align__(16) uint8_t s_in[kTH + 6][kSW];
+    __shared__ __align__(16) uint8_t s_m[kTH][kTW];
     // the survivor list (+ per-lane dump slots for branch-free appends) and, after the
     // strength pass, the blur row sums as (row 2p, row 2p+1) u16 pairs share one buffer
     constexpr int kListB = (kTH * kTW + 128) * 2, kRowpB = (kTH + 6) / 2 * kTW * 4;
@@ -522,15 +505,7 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
     __shared__ __align__(16) uint8_t s_u[(kListB > kRowpB ? kListB : kRowpB) + ORBX_LT_LDS_PAD];
     uint16_t* const s_list = (uint16_t*)s_u;
     uint32_t (*const s_rowp)[kTW] = (uint32_t (*)[kTW])s_u;
-    // the compass survivors of the 1-pixel ring around the tile ((r + 1) << 8 | (c + 1))
-    constexpr int kRing = 2 * (kTW + 2) + 2 * kTH;
-    static_assert(kRing <= 256, "one ring pixel per thread");
-    __shared__ uint16_t s_ring[kRing];
-    // the tile pixels with M > t_c (the suppression's only subjects), compacted by the
-    // strength loop: ~5 % of the pixels, against the ~35 % the compass test passes
-    constexpr int kNmsCap = 1024;
-    __shared__ uint16_t s_nms[kNmsCap];
-    __shared__ int s_n, s_nr, s_nn;
+    __shared__ int s_n;
     int f, tile;
     xcd_frame_block(tiles_pf, nframes, f, tile);
     const int tid = threadIdx.x, lane = tid & 63;
@@ -544,11 +519,11 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
     const bool in0 = l == 0 && l0 != nullptr;
     const uint8_t* img = in0 ? l0 + (size_t)f * l0_fp : pyr + (size_t)f * fb + g.off;
     const int ipitch = in0 ? l0_pitch : g.pitch;
-    // ---- stage rows Y0-4 .. Y0+kTH+3, columns X0-16 .. X0+79 (REFLECT_101 at the ROI
+    // ---- stage rows Y0-3 .. Y0+kTH+2, columns X0-16 .. X0+79 (REFLECT_101 at the ROI
     // edges) as 16-byte loads (pitch and level offsets are multiples of 64); all loads
     // of a thread are issued before the LDS stores: no per-load round trip
     {
-        constexpr int kRow = (kTW + 2 * kSX) / kLU, kN = (kTH + 2 * kRY) * kRow, kPer = (kN + 255) / 256;
+        constexpr int kRow = (kTW + 2 * kSX) / kLU, kN = (kTH + 6) * kRow, kPer = (kN + 255) / 256;
         const bool edge = !(X0 >= kSX && X0 + kTW + kSX <= g.w);
         lt_load_t v[kPer];
 #pragma unroll
@@ -558,7 +533,7 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
             // edge tile: the start column clamped into the row (a load holding an in-range
             // column never clamps: X0 and pitch are multiples of 64)
             const int col = edge ? min(max(X0 - kSX + kLU * cu, 0), ipitch - kLU) : X0 - kSX + kLU * cu;
-            v[k] = *(const lt_load_t*)(img + (size_t)reflect101(Y0 + r - kRY, g.h) * ipitch + col);
+            v[k] = *(const lt_load_t*)(img + (size_t)reflect101(Y0 + r - 3, g.h) * ipitch + col);
         }
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
@@ -570,7 +545,7 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
             // the only reflected columns anything reads, -3..-1 and w..w+2 (the blur's
             // reach; FAST stays inside [16, w - 16)), are rewritten from the staged row
             __syncthreads();
-            for (int i = tid; i < (kTH + 2 * kRY) * 6; i += 256) {
+            for (int i = tid; i < (kTH + 6) * 6; i += 256) {
                 const int r = i / 6, k = i - 6 * r;
                 const int col = k < 3 ? -1 - k : g.w + k - 3;  // REFLECT_101 source: -col or 2w - 2 - col
                 const int sc = col - X0 + kSX, ss = (k < 3 ? -col : 2 * g.w - 2 - col) - X0 + kSX;
@@ -578,18 +553,8 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
             }
         }
     }
-    if (tid == 0) s_n = s_nr = s_nn = 0;
-    for (int i = tid; i < (kTH + 2) * kMP / 4; i += 256) ((uint32_t*)s_m)[i] = 0u;
-    if (tid < kTH) s_sbits[tid] = 0ull;
-    if (g.cell_w > 0 && tid < kTW + kTH) {  // one modulo per column / row, not per candidate
-        const bool col = tid < kTW;
-        const int cw = col ? g.cell_w : g.cell_h;
-        const int rel = (col ? X0 + tid : Y0 + tid - kTW) - kEdge;
-        const int m = ((rel % cw) + cw) % cw;
-        const uint8_t fl = (uint8_t)((m == 0 ? 1 : 0) | (m == cw - 1 ? 2 : 0));
-        if (col) s_cbx[tid] = fl;
-        else s_cby[tid - kTW] = fl;
-    }
+    if (tid == 0) s_n = 0;
+    for (int i = tid; i < kTH * kTW / 4; i += 256) ((uint32_t*)s_m)[i] = 0u;
     __syncthreads();
     // ---- FAST compass test on the detection area, compaction of the survivors.
     // A thread always owns columns 4j..4j+3 (j = tid & 15) of rows tid/16 + 16 i, so
@@ -606,10 +571,10 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
             const int r = (tid >> 4) + 16 * it;
             const int y = Y0 + r;
             if (colmask != 0 && y >= kEdge && y < g.h - kEdge) {
-                const uint32_t* rc = (const uint32_t*)&s_in[r + kRY][c0];
+                const uint32_t* rc = (const uint32_t*)&s_in[r + 3][c0];
                 const uint32_t V = rc[0];
-                const uint32_t C0 = *(const uint32_t*)&s_in[r + kRY + 3][c0];  // ring 0  (0, +3)
-                const uint32_t C8 = *(const uint32_t*)&s_in[r + kRY - 3][c0];  // ring 8  (0, -3)
+                const uint32_t C0 = *(const uint32_t*)&s_in[r + 6][c0];  // ring 0  (0, +3)
+                const uint32_t C8 = *(const uint32_t*)&s_in[r][c0];      // ring 8  (0, -3)
                 const uint32_t C4 = row_bytes(rc[-1], rc[0], rc[1], 3);   // ring 4  (+3, 0)
                 const uint32_t C12 = row_bytes(rc[-1], rc[0], rc[1], -3); // ring 12 (-3, 0)
                 uint32_t q[2];
@@ -666,99 +631,22 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
                 o += p;
             }
         }
-        // the ring: the same compass pre-test, one pixel per thread, appended to its own
-        // list so that the strength loop below balances both lists over the block
-        bool rp = false;
-        int rr = 0, rcc = 0;
-        if (tid < kRing && g.cell_w > 0) {
-            if (tid < kTW + 2) { rr = -1; rcc = tid - 1; }
-            else if (tid < 2 * (kTW + 2)) { rr = kTH; rcc = tid - (kTW + 2) - 1; }
-            else if (tid < 2 * (kTW + 2) + kTH) { rr = tid - 2 * (kTW + 2); rcc = -1; }
-            else { rr = tid - 2 * (kTW + 2) - kTH; rcc = kTW; }
-            const int y = Y0 + rr, x = X0 + rcc;
-            if (y >= kEdge && y < g.h - kEdge && x >= kEdge && x < g.w - kEdge) {
-                const uint8_t* q = &s_in[rr + kRY][rcc + kSX];
-                const int v = q[0];
-                const int a0 = q[3 * kSW] - v, a4 = q[3] - v, a8 = q[-3 * kSW] - v, a12 = q[-3] - v;
-                const int br = max(max(min(a0, a4), min(a4, a8)), max(min(a8, a12), min(a12, a0)));
-                const int dk = min(min(max(a0, a4), max(a4, a8)), min(max(a8, a12), max(a12, a0)));
-                rp = max(br, -dk) > tq;
-            }
-        }
-        const unsigned long long rb = __ballot(rp);
-        if (rb) {  // wave-uniform
-            int rbase = 0;
-            if (lane == 0) rbase = atomicAdd(&s_nr, (int)__popcll(rb));
-            rbase = __builtin_amdgcn_readfirstlane(rbase);
-            if (rp)
-                s_ring[rbase + (int)__popcll(rb & ((1ull << lane) - 1))] =
-                    (uint16_t)(((rr + 1) << 8) | (rcc + 1));
-        }
     }
     __syncthreads();
-    // ---- exact strength of the survivors, and of the compass survivors of the 1-pixel
-    // ring around the tile (the neighbours of its edge pixels in the next tiles); the tile
-    // pixels with M > t_c = max(t_q, 1) go on the suppression list (one wave append per
-    // round)
-    const int n = s_n, nall = n + s_nr;
-    const int tc = tq > 1 ? tq : 1;
-    const bool cells = g.cell_w > 0;
-    for (int i0 = 0; i0 < nall; i0 += 256) {  // block-uniform trip count (ballots below)
-        const int i = i0 + tid;
-        bool cand = false;
-        int rc = 0;
-        if (i < nall) {
-            rc = i < n ? s_list[i] + 0x101 : s_ring[i - n];  // (r + 1, c + 1)
-            const int r1 = rc >> 8, c1 = rc & 255;
-            const int M = fast_strength(&s_in[r1 - 1 + kRY][c1 - 1 + kSX], kSW);
-            s_m[r1][c1] = (uint8_t)M;
-            cand = cells && i < n && M > tc;
-        }
-        const unsigned long long cb = __ballot(cand);
-        if (cb) {  // wave-uniform
-            int base = 0;
-            if (lane == 0) base = atomicAdd(&s_nn, (int)__popcll(cb));
-            base = __builtin_amdgcn_readfirstlane(base);
-            const int o = base + (int)__popcll(cb & ((1ull << lane) - 1));
-            if (cand && o < kNmsCap) s_nms[o] = (uint16_t)rc;
-        }
+    // ---- exact strength of the survivors
+    const int n = s_n;
+    for (int i = tid; i < n; i += 256) {
+        const int rc = s_list[i];
+        const int r = rc >> 8, c = rc & 255;
+        s_m[r][c] = (uint8_t)fast_strength(&s_in[r + 3][c + kSX], kSW);
     }
     __syncthreads();
-    // ---- non-max suppression inside each FAST cell (cv::FAST's, ORBextractor.cc:1091-1104
-    // at either threshold): survivor bits of the pixels with M > t_c that beat every
-    // neighbour of their cell
-    auto suppress = [&](int r, int c) {  // tile pixel (r, c), M > t_c
-        const uint8_t* p = &s_m[r + 1][c + 1];
-        const int M = p[0];
-        // a neighbour across a cell boundary is outside this cell's FAST window: score 0
-        const int fx = s_cbx[c], fy = s_cby[r];
-        const int lm = (fx & 1) ? 0 : 255, rm = (fx & 2) ? 0 : 255;
-        const int um = (fy & 1) ? 0 : 255, dm = (fy & 2) ? 0 : 255;
-        const int up = max(max(p[-kMP - 1] & lm, (int)p[-kMP]), p[-kMP + 1] & rm) & um;
-        const int dn = max(max(p[kMP - 1] & lm, (int)p[kMP]), p[kMP + 1] & rm) & dm;
-        const int nb = max(max(up, dn), max(p[-1] & lm, p[1] & rm));
-        if (M > nb) atomicOr(&s_sbits[r], 1ull << c);
-    };
-    const int nn = s_nn;
-    if (nn <= kNmsCap) {
-        for (int i = tid; i < nn; i += 256) {
-            const int rc = s_nms[i];
-            suppress((rc >> 8) - 1, (rc & 255) - 1);
-        }
-    } else {  // (a list past its capacity: every compass survivor, before the blur rows
-              // reuse the list's buffer)
-        for (int i = tid; i < n; i += 256) {
-            const int rc = s_list[i];
-            if (s_m[(rc >> 8) + 1][(rc & 255) + 1] > tc) suppress(rc >> 8, rc & 255);
-        }
-        __syncthreads();
-    }
     // ---- blur rows (into the survivor list's buffer, free now): 2 rows x 4 columns per
     // task (dot4), stored as row-pair u16 dwords
     for (int i = tid; i < ((kTH + 6) / 2) * (kTW / 4); i += 256) {
         const int pr = i >> 4, c0 = kSX + 4 * (i & 15);
-        const uint32_t* ra = (const uint32_t*)&s_in[2 * pr + kRY - 3][c0];
-        const uint32_t* rb = (const uint32_t*)&s_in[2 * pr + kRY - 2][c0];
+        const uint32_t* ra = (const uint32_t*)&s_in[2 * pr][c0];
+        const uint32_t* rb = (const uint32_t*)&s_in[2 * pr + 1][c0];
         uint32_t a[4], b[4];
         blur_row4(ra[-1], ra[0], ra[1], a);
         blur_row4(rb[-1], rb[0], rb[1], b);
@@ -766,36 +654,11 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
                                                   a[3] | (b[3] << 16));
     }
     __syncthreads();
-    // ---- the survivors' row starts (each writing wave scans the row counts itself; wave 0
-    // also stores them as the block's header), then the entries: thread = (row, 16-column
-    // quarter), raster order
-    uint8_t* const sblk = surv + ((size_t)f * tiles_pf + tile) * kSurvBlock;
-    if (tid < kTH * 4) {
-        const uint32_t cnt = lane < kTH ? (uint32_t)__popcll(s_sbits[lane]) : 0u;
-        const uint32_t incl = wave_inclusive_sum(cnt);
-        const int ex = (int)(incl - cnt);
-        if (tid <= kTH) ((uint16_t*)sblk)[tid] = (uint16_t)min((uint32_t)ex, (uint32_t)kSurvCap);
-        const int r = tid >> 2, q = tid & 3;
-        const int rstart = __shfl(ex, r);
-        const unsigned long long row = s_sbits[r];
-        unsigned b = (unsigned)(row >> (16 * q)) & 0xffffu;
-        if (b) {
-            uint32_t o = (uint32_t)rstart + (uint32_t)__popcll(row & ((1ull << (16 * q)) - 1));
-            uint32_t* ent = (uint32_t*)(sblk + kSurvHdr);
-            const uint32_t yw = (uint32_t)(Y0 + r - kMinBorder) << 12;
-            while (b) {
-                const int c = 16 * q + __builtin_ctz(b);
-                b &= b - 1;
-                if (o < (uint32_t)kSurvCap)  // never reached (at most 884 survivors, orbx_geometry.h)
-                    ent[o] = (uint32_t)(X0 + c - kMinBorder) | yw | ((uint32_t)(s_m[r + 1][c + 1] - 1) << 24);
-                o++;
-            }
-        }
-    }
-    // ---- blur columns -> global, two rows x 4 columns per task:
+    // ---- blur columns and the strength map -> global, two rows x 4 columns per task:
     // rows 2p and 2p+1 read the same four row-pair dwords (staged rows 2p..2p+7), one
     // v_dot2_u32_u16 per pair, column and row, then (sum + 2^15) >> 16
     uint8_t* bout = blur + (size_t)f * fb + g.off;
+    uint8_t* mout = score + (size_t)f * fb + g.off;
     for (int i = tid; i < (kTH / 2) * (kTW / 4); i += 256) {
         const int rp = i >> 4, c = 4 * (i & 15);
         const int r = 2 * rp, y = Y0 + r, x = X0 + c;
@@ -826,14 +689,23 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
             pe |= (ve > 255 ? 255u : ve) << (8 * k);
             po |= (vo > 255 ? 255u : vo) << (8 * k);
         }
+        const uint32_t me = *(const uint32_t*)&s_m[r][c], mo = *(const uint32_t*)&s_m[r + 1][c];
         const size_t off = (size_t)y * g.pitch + x;
         if (x + 4 <= g.w) {
             *(uint32_t*)(bout + off) = pe;
-            if (two) *(uint32_t*)(bout + off + g.pitch) = po;
+            *(uint32_t*)(mout + off) = me;
+            if (two) {
+                *(uint32_t*)(bout + off + g.pitch) = po;
+                *(uint32_t*)(mout + off + g.pitch) = mo;
+            }
         } else {
             for (int k = 0; x + k < g.w; k++) {
                 bout[off + k] = (uint8_t)(pe >> (8 * k));
-                if (two) bout[off + g.pitch + k] = (uint8_t)(po >> (8 * k));
+                mout[off + k] = (uint8_t)(me >> (8 * k));
+                if (two) {
+                    bout[off + g.pitch + k] = (uint8_t)(po >> (8 * k));
+                    mout[off + g.pitch + k] = (uint8_t)(mo >> (8 * k));
+                }
             }
         }
     }
@@ -847,20 +719,36 @@ __global__ __launch_bounds__(256) void k_level_tiles(const uint8_t* __restrict__
 // the 8-neighbourhood, where neighbours outside the cell's detection window or below
 // the threshold score 0, keeps a corner p iff M_p > t, M_p >= 2 and M_p exceeds every
 // in-window neighbour's M (a neighbour with M_n >= M_p > t always suppresses; one below
-// M_p never does) -- threshold-independent apart from M_p > t.  k_level_tiles therefore
-// lists, per level tile and in raster order, the pixels that pass the suppression at the
-// lower threshold (M > max(min(iniTh, minTh), 1)) with their M; a cell's keypoints at
-// threshold t are its survivors with M > t, in raster order.  The wave reads the rows of
-// its detection window from the one or two tiles they cross: lane = (row, tile column)
-// in raster order, a u16 pair of row starts and the row's few entries each; the counts
-// at both thresholds decide (cc:1098-1104), one more wave scan places the chosen set.
-// (Until round 6 the wave staged its window of a dense M plane -- 115.7 MB per 128-frame
-// configs[1] launch -- and ran the suppression itself.)
-__global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ surv, int tiles_pf,
+// M_p never does) -- threshold-independent apart from M_p > t.  M is sparse (k_level_tiles
+// zeroes M <= min(iniTh, minTh)), so the wave stages the window with a zero frame, lists
+// the non-zero pixels in raster order (one ballot per row -- per row pair when the window
+// is at most 32 wide), tests only those against their neighbours, and writes the
+// survivors of the chosen threshold in the same order.
+// Staged window row pitch: 68 bytes (64 + zero frame, an odd dword count), a compile-time
+// constant.  Measured alternatives (ORBX_FC_PITCH): 44-100 bytes all slower at configs[4]
+// (up to -8 %, r05al / r05am), and a pitch sized to the widest window (36 bytes at 30-px
+// cells, 4.4 KB less LDS per workgroup) -6 % there (r05ac).  Passing the pitch at run
+// time (as that experiment did) cost configs[1] 1.1 % by itself (r05bh).
+#ifndef ORBX_FC_PITCH
+#define ORBX_FC_PITCH 68
+#endif
+constexpr int kFcStride = ORBX_FC_PITCH;
+#ifndef ORBX_FC_INFLIGHT
+#define ORBX_FC_INFLIGHT 8  // k_fast_cells: row steps of byte loads in flight (r05aw: 4 -2 %,
+                            // 16 -10 % at configs[1])
+#endif
+static_assert(kFcStride % 4 == 0 && kFcStride >= 36, "fast_cells window pitch");
+
+__global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ score, long long fb,
                                                     const CellGeom* __restrict__ cells, int ncells,
                                                     int ini_th, int min_th, uint32_t* __restrict__ slots,
-                                                    int slots_pf, int* __restrict__ cell_count, int nframes) {
+                                                    int slots_pf, int* __restrict__ cell_count, int nframes,
+                                                    int max_wr, int max_wc) {
+    // per wave: (max_wr + 2) framed rows of M (pitch kFcStride >= max_wc + 2, checked by
+    // the launcher), then a candidate list of max_wr*max_wc u16
+    extern __shared__ __align__(16) uint8_t s_dyn[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int per_wave = (((max_wr + 2) * kFcStride + 2 * max_wr * max_wc) + 15) & ~15;
     int f, cb;
     xcd_frame_block((ncells + 3) / 4, nframes, f, cb);
     const int ci = cb * 4 + wave;
@@ -871,64 +759,88 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
     if (wr > 0 && wc > 0) {
         const int ti = ini_th < 0 ? 0 : (ini_th > 255 ? 255 : ini_th);
         const int tm = min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th);
-        // the window's columns relative to minBorder, like the slot words
-        const int x0 = c.x0 + 3 - kMinBorder, x1 = x0 + wc;
-        const int y0 = c.y0 + 3;
-        const int tx0 = (c.x0 + 3) / kTW;
-        // a window (<= 64 px) crosses <= 2 tile columns: lane = row, or (row, tile column)
-        const int sh = (c.x0 + 3 + wc - 1) / kTW > tx0 ? 1 : 0;
-        const int items = wr << sh;  // <= 128
-        const uint8_t* fbase = surv + ((size_t)f * tiles_pf + c.tile_first) * kSurvBlock;
-        // per pass: the lane's run [sa, sb) of survivor words inside the window, the first
-        // four words of its row kept in registers (a row rarely holds more), the counts
-        const uint32_t* seg[2] = {nullptr, nullptr};
-        int ra[2] = {0, 0}, sa[2] = {0, 0}, sb[2] = {0, 0};
-        int ni[2] = {0, 0}, nm[2] = {0, 0};
-        uint32_t keep[2][4] = {};
-        int cnt_i = 0, cnt_m = 0;
+        const int tc = max(min(ti, tm), 1);  // candidates: M > tc
+        const uint8_t* src = score + (size_t)f * fb + c.src_off;
+        uint8_t* m = s_dyn + wave * per_wave;  // m[(r + 1) * kFcStride + c + 1] = M(r, c)
+        uint16_t* list = (uint16_t*)(s_dyn + wave * per_wave + (max_wr + 2) * kFcStride);
+        const unsigned long long below = (1ull << lane) - 1;
+        // zero frame: rows -1 and wr, column -1 (column wc is written as 0 below)
+        for (int i = lane; i < kFcStride; i += 64) {
+            m[i] = 0;
+            m[(wr + 1) * kFcStride + i] = 0;
+        }
+        for (int r = lane; r < wr + 2; r += 64) {  // columns -1 and wc
+            m[r * kFcStride] = 0;
+            m[r * kFcStride + wc + 1] = 0;
+        }
+        int n = 0;
+        const bool pairs = wc <= 32;
+        const int col = pairs ? (lane & 31) : lane;
+        const int half = pairs ? (lane >> 5) : 0;
+        const int rstep = pairs ? 2 : 1;
+        const bool act = col < wc;
+        // 8 row steps of loads in flight at a time.  The loads are unconditional: the
+        // window ends >= 19 rows above the level's bottom and rows are >= 64 wide, so up
+        // to 15 rows / 63 columns past it stay inside the frame's block (and the buffer
+        // has slack); the values are masked.  The row part of each offset is wave-uniform
+        // (scalar adds to the base), the lane part a 32-bit vector offset.
+        const uint32_t loff = (uint32_t)(half * c.pitch + col);
+        constexpr int kIF = ORBX_FC_INFLIGHT;  // row steps of loads in flight
+        for (int r0 = 0; r0 < wr; r0 += kIF * rstep) {
+            int v[kIF];
 #pragma unroll
-        for (int pass = 0; pass < 2; pass++) {
-            if (pass == 1 && items <= 64) break;  // wave-uniform
-            const int it = 64 * pass + lane;
-            if (it < items) {
-                const int y = y0 + (it >> sh), tx = tx0 + (it & sh);
-                const int ty = y / kTH, yy = y - ty * kTH;
-                const uint8_t* blk = fbase + (size_t)(ty * c.tiles_x + tx) * kSurvBlock;
-                const uint16_t* rsp = (const uint16_t*)blk;
-                const int a = rsp[yy], b = rsp[yy + 1];
-                const uint32_t* e = (const uint32_t*)(blk + kSurvHdr);
-                // the row's words (x ascending), four loads in flight at a time; the ones
-                // inside the window are a contiguous run [i, j)
-                int i = -1, j = -1, ki = 0, km = 0;
-                for (int q0 = a; q0 < b; q0 += 4) {
-                    uint32_t w[4];
-#pragma unroll
-                    for (int k = 0; k < 4; k++) w[k] = q0 + k < b ? e[q0 + k] : 0u;
-                    if (q0 == a) {
-#pragma unroll
-                        for (int k = 0; k < 4; k++) keep[pass][k] = w[k];
-                    }
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        const int x = (int)(w[k] & 0xfffu);
-                        if (q0 + k < b && x >= x0 && x < x1) {
-                            const int sc = (int)(w[k] >> 24);  // M - 1: M > t <=> sc >= t
-                            ki += sc >= ti;
-                            km += sc >= tm;
-                            if (i < 0) i = q0 + k;
-                            j = q0 + k + 1;
-                        }
-                    }
-                }
-                seg[pass] = e;
-                ra[pass] = a;
-                sa[pass] = i < 0 ? 0 : i;
-                sb[pass] = i < 0 ? 0 : j;
-                ni[pass] = ki;
-                nm[pass] = km;
+            for (int k = 0; k < kIF; k++) {
+                // more than 8 steps: rows clamped to the window (at most one row past it)
+                const int rk = kIF > 8 ? min(r0 + k * rstep, wr - 1) : r0 + k * rstep;
+                v[k] = src[(uint32_t)(rk * c.pitch) + loff];
             }
-            cnt_i += __builtin_amdgcn_readlane((int)wave_inclusive_sum((uint32_t)ni[pass]), 63);
-            cnt_m += __builtin_amdgcn_readlane((int)wave_inclusive_sum((uint32_t)nm[pass]), 63);
+#pragma unroll
+            for (int k = 0; k < kIF; k++) v[k] = (act && r0 + k * rstep + half < wr) ? v[k] : 0;
+#pragma unroll
+            for (int k = 0; k < kIF; k++) {
+                const int rb = r0 + k * rstep;  // first row of this step (wave-uniform)
+                if (rb < wr) {
+                    const int r = rb + half;
+                    // (a pitch of at least 65 holds every lane's column; a smaller one only
+                    // the window and its right frame)
+                    if (r < wr && (kFcStride >= 65 || col <= wc)) m[(r + 1) * kFcStride + col + 1] = (uint8_t)v[k];
+                    const unsigned long long b = __ballot(v[k] > tc);  // raster order: row rb, then rb+1
+                    if ((b >> lane) & 1ull) list[n + __popcll(b & below)] = (uint16_t)((r << 8) | col);
+                    n += __popcll(b);
+                }
+            }
+        }
+        wave_lds_fence();
+        // neighbour test of the candidates (zero frame: no bounds checks), both thresholds
+        auto keep_of = [&](int i, int& r, int& cc, int& M) -> bool {
+            const int rc = list[i];
+            r = rc >> 8;
+            cc = rc & 255;
+            const uint8_t* p = m + (r + 1) * kFcStride + cc + 1;
+            M = p[0];
+            const int nb = max(max(max(p[-kFcStride - 1], p[-kFcStride]), max(p[-kFcStride + 1], p[-1])),
+                               max(max(p[1], p[kFcStride - 1]), max(p[kFcStride], p[kFcStride + 1])));
+            return M > nb;  // M > tc >= 1, so M >= 2
+        };
+        // the first kFcKeep x 64 candidates' outcomes at both thresholds are kept as
+        // wave masks, so the write pass below re-tests only candidates past them
+        constexpr int kFcKeep = 4;
+        unsigned long long mi[kFcKeep], mm[kFcKeep];
+        int cnt_i = 0, cnt_m = 0;
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            bool ki = false, km = false;
+            if (i0 + lane < n) {
+                int r, cc, M;
+                const bool lm = keep_of(i0 + lane, r, cc, M);
+                ki = lm && M > ti;
+                km = lm && M > tm;
+            }
+            const unsigned long long bi = __ballot(ki), bm = __ballot(km);
+#pragma unroll
+            for (int u = 0; u < kFcKeep; u++)
+                if (i0 == 64 * u) { mi[u] = bi; mm[u] = bm; }
+            cnt_i += __popcll(bi);
+            cnt_m += __popcll(bm);
         }
         const bool use_ini = cnt_i > 0;
         count = use_ini ? cnt_i : cnt_m;
@@ -936,20 +848,31 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
         if (count > 0) {
             uint32_t* out = slots + (size_t)f * slots_pf + c.slot_off;
             int base = 0;
+            for (int i0 = 0; i0 < n; i0 += 64) {
+                bool keep = false;
+                int r = 0, cc = 0, M = 0;
+                if (i0 < 64 * kFcKeep) {
+                    unsigned long long km = 0;
 #pragma unroll
-            for (int pass = 0; pass < 2; pass++) {
-                if (pass == 1 && items <= 64) break;
-                const int k = use_ini ? ni[pass] : nm[pass];
-                const uint32_t incl = wave_inclusive_sum((uint32_t)k);
-                int o = base + (int)incl - k;
-                for (int q = sa[pass]; q < sb[pass]; q++) {
-                    const int d = q - ra[pass];
-                    const uint32_t w = d == 0 ? keep[pass][0]
-                                              : d == 1 ? keep[pass][1]
-                                                       : d == 2 ? keep[pass][2] : d == 3 ? keep[pass][3] : seg[pass][q];
-                    if ((int)(w >> 24) >= t) out[o++] = w;
+                    for (int u = 0; u < kFcKeep; u++)
+                        if (i0 == 64 * u) km = use_ini ? mi[u] : mm[u];
+                    keep = (km >> lane) & 1ull;
+                    if (keep) {
+                        const int rc = list[i0 + lane];
+                        r = rc >> 8;
+                        cc = rc & 255;
+                        M = m[(r + 1) * kFcStride + cc + 1];
+                    }
+                } else if (i0 + lane < n) {
+                    keep = keep_of(i0 + lane, r, cc, M) && M > t;
                 }
-                base += __builtin_amdgcn_readlane((int)incl, 63);
+                const unsigned long long b = __ballot(keep);
+                if (keep) {
+                    const int xr = c.x0 + 3 + cc - kMinBorder;  // relative to minBorderX
+                    const int yr = c.y0 + 3 + r - kMinBorder;
+                    out[base + __popcll(b & below)] = (uint32_t)xr | ((uint32_t)yr << 12) | ((uint32_t)(M - 1) << 24);
+                }
+                base += __popcll(b);
             }
         }
     }
@@ -2207,16 +2130,18 @@ hipError_t launch_extract(const Plan& plan, const DeviceBuffers& db, int batch, 
         dim3 grid(plan.tiles_total * batch);
         int tq = plan.prm.ini_th < plan.prm.min_th ? plan.prm.ini_th : plan.prm.min_th;
         tq = tq < 0 ? 0 : (tq > 255 ? 255 : tq);
-        hipLaunchKernelGGL(k_level_tiles, grid, dim3(256), 0, stream, db.pyr, db.blur, db.surv, fb, db.lv, L,
+        hipLaunchKernelGGL(k_level_tiles, grid, dim3(256), 0, stream, db.pyr, db.blur, db.score, fb, db.lv, L,
                            plan.tiles_total, batch, tq, l0, l0_fp, l0_pitch);
     }
     if (ev && ev[2]) (void)hipEventRecord(ev[2], stream);
     if (stage_ev && stage_after == 2) (void)hipEventRecord(stage_ev, stream);
     for (int rep = 0; rep < (dup == 3 ? 2 : 1); rep++) {
         dim3 grid(((ncells + 3) / 4) * batch);
-        hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), 0, stream, db.surv, plan.tiles_total, db.cells,
-                           ncells, plan.prm.ini_th, plan.prm.min_th, db.slots, plan.slots_per_frame, db.cell_count,
-                           batch);
+        if (plan.fc_wc + 2 > kFcStride) return hipErrorInvalidValue;  // a window wider than the staged pitch
+        const size_t fc_lds = 4 * (size_t)((((plan.fc_wr + 2) * kFcStride + 2 * plan.fc_wr * plan.fc_wc) + 15) & ~15);
+        hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), fc_lds, stream, db.score, fb, db.cells, ncells,
+                           plan.prm.ini_th, plan.prm.min_th, db.slots, plan.slots_per_frame, db.cell_count, batch,
+                           plan.fc_wr, plan.fc_wc);
     }
     if (ev && ev[3]) (void)hipEventRecord(ev[3], stream);
     if (stage_ev && stage_after == 3) (void)hipEventRecord(stage_ev, stream);

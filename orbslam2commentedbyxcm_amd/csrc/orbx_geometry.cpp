@@ -262,8 +262,6 @@ bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
         const int wCell = no_cells ? 0 : (int)std::ceil(width / nCols);
         const int hCell = no_cells ? 0 : (int)std::ceil(height / nRows);
         g.cell_first = cell_first;
-        g.cell_w = wCell;
-        g.cell_h = hCell;
         g.key_off = key_off;
         int level_cap = 0;
         for (int i = 0; i < (no_cells ? 0 : nRows); i++) {
@@ -286,8 +284,10 @@ bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
                 if (wc > kCellMax || wr > kCellMax) { plan.why = "FAST cell wider than 64 px"; return false; }
                 c.slot_off = slot_off;
                 c.slot_cap = ((wc + 1) / 2) * ((wr + 1) / 2);
+                c.pitch = g.pitch;
                 plan.fc_wr = std::max(plan.fc_wr, wr);
                 plan.fc_wc = std::max(plan.fc_wc, wc);
+                c.src_off = (int)(g.off + (long long)(c.y0 + 3) * g.pitch + c.x0 + 3);
                 slot_off += c.slot_cap;
                 level_cap += c.slot_cap;
                 plan.cells.push_back(c);
@@ -321,10 +321,6 @@ bool make_plan(Plan& plan, const OrbParams& prm, int W, int H) {
         g.tiles_y = (g.h + kLtTH - 1) / kLtTH;
         g.tile_first = tile_first;
         tile_first += g.tiles_x * g.tiles_y;
-        for (int i = g.cell_first; i < g.cell_first + g.ncells; i++) {
-            plan.cells[i].tile_first = g.tile_first;
-            plan.cells[i].tiles_x = g.tiles_x;
-        }
 
         // resize tables
         if (l > 0) {

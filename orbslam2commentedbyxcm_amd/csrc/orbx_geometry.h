@@ -67,21 +67,7 @@ struct LevelGeom {
     int tile_first, tiles_x, tiles_y;
     // resize tables (levels >= 1)
     int xtab_off, ytab_off;  // offsets (in int16 units) into the resize table buffer
-    // FAST cell grid: detection areas [kEdge + j*cell_w, ..) x [kEdge + i*cell_h, ..)
-    // (wCell, hCell of ORBextractor.cc:1042-1043; 0 when the level has no cells)
-    int cell_w, cell_h;
 };
-
-// k_level_tiles' FAST survivors per level tile (the pixels with M > max(min(iniTh,
-// minTh), 1) that beat every 8-neighbour of their own FAST cell), read by k_fast_cells:
-// a tile block holds row starts (u16, kLtTH + 1 of them, padded to kSurvHdr bytes) and
-// then the survivors in raster order as slot words (x - 16 | (y - 16) << 12 | (M - 1) << 24).
-// A cell's survivors form an independent set of the 8-neighbour graph, at most
-// ceil(a/2) ceil(b/2) in an a x b cell, and a 64 x 48 tile meets at most 4 x 3 cell
-// pieces (cells are >= 30 px): at most 34 x 26 = 884 < kSurvCap per tile.
-constexpr int kSurvHdr = 128;
-constexpr int kSurvCap = 1024;
-constexpr int kSurvBlock = kSurvHdr + 4 * kSurvCap;
 
 // One FAST cell: sub-image [y0, y0+rows) x [x0, x0+cols) of its level ROI.
 struct CellGeom {
@@ -89,8 +75,8 @@ struct CellGeom {
     int x0, y0, cols, rows;
     int slot_off;          // offset of this cell's candidate slots in the frame's slot array
     int slot_cap;
-    int tile_first;        // the level's first k_level_tiles tile (its survivor blocks)
-    int tiles_x;           // the level's tile columns
+    int src_off;           // level.off + (y0 + 3) * pitch + x0 + 3: detection window origin in a frame block
+    int pitch;             // level row pitch
 };
 
 // k_pyramid: one workgroup per (frame, tile) computes every level of its tile.  A

@@ -17,7 +17,7 @@ struct DeviceBuffers {
     int16_t* rtab = nullptr;         // resize tables
     uint8_t* pyr = nullptr;          // [B][pyr_frame_bytes] image pyramid (level ROIs)
     uint8_t* blur = nullptr;         // [B][pyr_frame_bytes] Gaussian-blurred levels
-    uint8_t* surv = nullptr;         // [B][tiles_total][kSurvBlock] FAST survivors per level tile
+    uint8_t* score = nullptr;        // [B][pyr_frame_bytes] FAST strength map M per level
     uint32_t* slots = nullptr;       // [B][slots_per_frame] packed FAST keypoints per cell
     int* cell_count = nullptr;       // [B][ncells]
     uint32_t* keys = nullptr;        // [B][keys_per_frame] packed candidates per level
