@@ -493,22 +493,22 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
             const int b0 = cr.y0 >> kRowBlkLog2, b1 = cr.y1 >> kRowBlkLog2;
             const int ylo = cr.y0 & (kRowBlk - 1), yhi = cr.y1 & (kRowBlk - 1);
             const int ncol = cr.x1 - cr.x0 + 1;
-            // lanes per column: the most (up to 4 in a row, 16 in a wave) that still cover
-            // every column in one pass; shifts, no division
+            // the (column, octave) visits of the window, octave fastest, dealt over the
+            // group's lanes: lanes per visit the most (a power of two) that still cover
+            // every visit in one pass; a visit's lanes split its scan.  (Until round 6 the
+            // lanes split the columns and each walked every octave of its column: the
+            // stereo / RGB-D searches' forward and backward ranges -- up to every level --
+            // then left each lane a dozen nearly empty visits.)
+            const int nor = bhi - blo + 1;
+            const int nv = nor > 0 ? ncol * nor : 0;
+            constexpr int kLog2K = K == 4 ? 2 : (K == 8 ? 3 : (K == 16 ? 4 : 6));
             int sh = 0;
-            if (K == 4) {
-                sh = ncol <= 1 ? 2 : (ncol <= 2 ? 1 : 0);
-            } else if (K == 8) {
-                sh = ncol <= 2 ? 2 : (ncol <= 4 ? 1 : 0);
-            } else if (K == 16) {
-                sh = ncol <= 4 ? 2 : (ncol <= 8 ? 1 : 0);
-            } else {
-                sh = ncol <= 4 ? 4 : (ncol <= 8 ? 3 : (ncol <= 16 ? 2 : (ncol <= 32 ? 1 : 0)));
-            }
-            const int lpc = 1 << sh, c0 = r >> sh, sub = r & (lpc - 1);
-            for (int c = c0; c < ncol; c += K) {
-                const int ix = cr.x0 + c;
-                for (int o = blo; o <= bhi; o++) {
+            while (sh < kLog2K && (nv << (sh + 1)) <= K) sh++;
+            const int lpc = 1 << sh, sub = r & (lpc - 1);
+            for (int v = r >> sh; v < nv; v += K >> sh) {
+                const int cq = v / nor;
+                const int ix = cr.x0 + cq, o = blo + (v - cq * nor);
+                {
                     // the rows y0..y1 of this column and octave: blocks b0..b1, whose
                     // first / last block also hold rows outside the window
                     const uint16_t* bt = G.bstart + (ix * noct + o) * kNumBlk;
