@@ -154,7 +154,7 @@ def test_rgbd_pipeline_configs4(oracle, orbx_built, scene, oracle_views):
 @pytest.mark.parametrize("footprint", [5, 0])
 def test_rgbd_pipeline_all_temporal(oracle, orbx_built, scene, oracle_views, footprint):
     """No tracked MapPoints (every visited point temporal, no claim blocks), one step, two
-    launch shapes of the first search (the retry pass is always the lean one-launch form)."""
+    launch shapes of the first search (the retry pass is always one launch of the one-wave form)."""
     from orbslam2commentedbyxcm_amd.rgbd import RGBDSequencePipeline
     pl = RGBDSequencePipeline(B, S.W, S.H, S.FX, S.FY, S.CX, S.CY, S.DIST, S.BF, params=S.PARAMS,
                               matcher_mode=footprint, pipelined=False)
