@@ -114,3 +114,41 @@ def test_debug_switches_need_no_gpu_and_reject_unknown_names(orbx_built):
     csrc = ROOT / "orbslam2commentedbyxcm_amd" / "csrc"
     users = [f.name for f in csrc.iterdir() if f.suffix in (".cpp", ".hip", ".h") and "getenv(" in f.read_text()]
     assert users == ["orbx_runtime.cpp"], users
+
+
+def test_rgbd_arguments_rejected_without_gpu(orbx_built):
+    """orbx_compute_stereo_from_rgbd(_device) check their arguments before any device call:
+    bad depth types, null buffers, image geometry (row / frame strides below the row, odd
+    strides, a misaligned image); no keypoints or an empty batch is a no-op."""
+    import ctypes as C
+
+    from orbslam2commentedbyxcm_amd import _lib as L
+    lib = L.lib()
+    fake = C.c_void_p(0x1000)  # never dereferenced: every case fails (or returns) first
+
+    def batch(**kw):
+        rb = L.RgbdBatch(batch=2, kps=fake, kps_un=fake, n=fake, cap=8, depth=fake, depth_type=L.ORBX_DEPTH_U16,
+                         width=64, height=48, row_bytes=128, frame_bytes=128 * 48, depth_map_factor=2e-4, bf=40.0,
+                         u_right=fake, depth_out=fake)
+        for k, v in kw.items():
+            setattr(rb, k, v)
+        return rb
+
+    dev = lib.orbx_compute_stereo_from_rgbd_device
+    assert dev(None, None, None) == L.ORBX_ERR_ARG
+    for kw in (dict(batch=-1), dict(cap=-1), dict(kps=None), dict(kps_un=None), dict(n=None), dict(depth=None),
+               dict(u_right=None), dict(depth_out=None), dict(depth_type=7), dict(width=0), dict(height=-2),
+               dict(row_bytes=126), dict(row_bytes=129), dict(frame_bytes=128 * 47), dict(frame_bytes=128 * 48 + 1),
+               dict(depth=C.c_void_p(0x1001)), dict(depth_type=L.ORBX_DEPTH_F32)):  # F32: 256-byte rows needed
+        rb = batch(**kw)
+        assert dev(None, C.byref(rb), None) == L.ORBX_ERR_ARG, kw
+    assert dev(None, C.byref(batch(batch=0)), None) == L.ORBX_OK
+    assert dev(None, C.byref(batch(cap=0)), None) == L.ORBX_OK
+    host = lib.orbx_compute_stereo_from_rgbd
+    kp = (C.c_byte * 28)()
+    out = (C.c_float * 4)()
+    assert host(0, None, kp, -1, kp, L.ORBX_DEPTH_U16, 4, 4, 8, 1.0, 40.0, kp, out, out) == L.ORBX_ERR_ARG
+    assert host(0, None, None, 1, kp, L.ORBX_DEPTH_U16, 4, 4, 8, 1.0, 40.0, kp, out, out) == L.ORBX_ERR_ARG
+    assert host(0, None, kp, 1, kp, 3, 4, 4, 8, 1.0, 40.0, kp, out, out) == L.ORBX_ERR_ARG
+    assert host(0, None, kp, 1, kp, L.ORBX_DEPTH_F32, 4, 4, 8, 1.0, 40.0, kp, out, out) == L.ORBX_ERR_ARG
+    assert host(0, None, kp, 0, None, 3, 0, 0, 0, 1.0, 40.0, None, None, None) == L.ORBX_OK
