@@ -216,4 +216,22 @@ private:
     orbx_matcher* h_ = nullptr;
 };
 
+// The RGB-D Frame constructor's steps after ExtractORB (Frame.cc:192-264, 227-230):
+// UndistortKeyPoints (Frame.cc:586-628) and ComputeStereoFromRGBD (Frame.cc:888-909) over
+// the depth image as GrabImageRGBD receives it -- ORBX_DEPTH_U16 (the library applies
+// mDepthMapFactor, Tracking.cc:265-271) or ORBX_DEPTH_F32 -- with mDepthMapFactor =
+// 1 / DepthMapFactor (Tracking.cc:166-170) and mbf.  mvuRight / mvDepth are -1 where the
+// depth is not positive, as the reference's vectors are initialised.
+inline void ComputeStereoFromRGBD(const orbx_camera& cam, const std::vector<orbx_keypoint>& mvKeys,
+                                  const void* depth, int depthType, int width, int height, size_t rowBytes,
+                                  float mDepthMapFactor, float mbf, std::vector<orbx_keypoint>& mvKeysUn,
+                                  std::vector<float>& mvuRight, std::vector<float>& mvDepth, int device = 0) {
+    const int n = (int)mvKeys.size();
+    mvKeysUn.resize((size_t)n);
+    mvuRight.assign((size_t)n, -1.0f);
+    mvDepth.assign((size_t)n, -1.0f);
+    check(orbx_compute_stereo_from_rgbd(device, &cam, mvKeys.data(), n, depth, depthType, width, height, rowBytes,
+                                        mDepthMapFactor, mbf, mvKeysUn.data(), mvuRight.data(), mvDepth.data()));
+}
+
 }  // namespace orbx

@@ -80,3 +80,54 @@ def test_cpp_threads_dropin_calls_like_oracle(tmp_path, orbx_built, oracle):
     r = subprocess.run([str(exe), str(tmp_path / "bad.bin"), "2", "0.2"], capture_output=True, text=True, timeout=120)
     rec = json.loads(r.stdout.strip().splitlines()[-1])
     assert not rec["bit_exact"] and 0 < rec["frames_mismatched"] < rec["frames_checked"]
+
+
+RGBD_SRC = ROOT / "tests" / "cpp" / "rgbd_cli.cpp"
+
+
+def _build_rgbd(tmp_path, orbx_built):
+    exe = tmp_path / "rgbd_cli"
+    lib_dir = Path(orbx_built).parent
+    subprocess.run(["g++", "-O2", "-std=c++17", f"-I{ROOT / 'include'}", str(RGBD_SRC), "-o", str(exe),
+                    f"-L{lib_dir}", "-lorbx", f"-Wl,-rpath,{lib_dir}"], check=True)
+    return exe
+
+
+def test_cpp_rgbd_mirror_builds(tmp_path, orbx_built):
+    assert _build_rgbd(tmp_path, orbx_built).exists()
+
+
+@pytest.mark.gpu
+def test_cpp_rgbd_frame_like_oracle(tmp_path, orbx_built, oracle):
+    """orbx::ComputeStereoFromRGBD from C++ (the RGB-D Frame constructor's steps after
+    ExtractORB, Frame.cc:217-230, on a TUM-like 16-bit depth image with holes): mvKeys,
+    mvKeysUn, mvuRight and mvDepth equal the oracle's."""
+    import tum_rgbd_scenes as S
+    gray, depth, _ = S.sequence(4100, 1)
+    (tmp_path / "g.raw").write_bytes(gray[0].tobytes())
+    (tmp_path / "d.raw").write_bytes(np.ascontiguousarray(depth[0], np.uint16).tobytes())
+    out = tmp_path / "out.bin"
+    f32 = lambda x: "%.9g" % float(np.float32(x))  # noqa: E731 -- exact float32 through strtof
+    cam = [f32(x) for x in (*S.K, *S.DIST)]
+    exe = _build_rgbd(tmp_path, orbx_built)
+    r = subprocess.run([str(exe), str(tmp_path / "g.raw"), str(tmp_path / "d.raw"), str(S.W), str(S.H), *cam,
+                        f32(S.DEPTH_MAP_FACTOR), f32(S.BF), str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    raw = out.read_bytes()
+    n = int(np.frombuffer(raw[:4], np.int32)[0])
+    o = 4
+    kd = np.frombuffer(raw[o:o + 28 * n], np.uint8).reshape(n, 28)
+    o += 28 * n
+    ku = np.frombuffer(raw[o:o + 28 * n], np.uint8).reshape(n, 28)
+    o += 28 * n
+    ur = np.frombuffer(raw[o:o + 4 * n], np.float32)
+    dp = np.frombuffer(raw[o + 4 * n:o + 8 * n], np.float32)
+    p = oracle.params(*S.PARAMS)
+    kr, _, _ = oracle.extract(gray[0], p)
+    kur = oracle.undistort_keypoints(S.K, S.DIST, kr)
+    urr, dpr = oracle.compute_stereo_from_rgbd(kr, kur, depth[0], S.BF, S.M_DEPTH_MAP_FACTOR)
+    assert n == len(kr) and n > 3000
+    assert np.array_equal(kd, kr.view(np.uint8).reshape(-1, 28))
+    assert np.array_equal(ku, kur.view(np.uint8).reshape(-1, 28))
+    assert np.array_equal(ur, urr) and np.array_equal(dp, dpr)
+    assert (dp > 0).sum() > n // 2 and (dp == -1).any()
