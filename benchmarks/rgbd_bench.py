@@ -184,7 +184,9 @@ def main(argv=None):
                               depth_map_factor=S.DEPTH_MAP_FACTOR, th_depth_factor=S.TH_DEPTH_FACTOR,
                               lanes=args.lanes, nbuf=int(os.environ.get("ORBX_PIPE_NBUF", "2")), device=gpu,
                               matcher_mode=None if "ORBX_MATCH_MODE" not in os.environ
-                              else int(os.environ["ORBX_MATCH_MODE"]))
+                              else int(os.environ["ORBX_MATCH_MODE"]),
+                              **({"lane_offset_stage": int(os.environ["ORBX_LANE_OFFSET"])}
+                                 if "ORBX_LANE_OFFSET" in os.environ else {}))
     sf, cap = pl.sf, pl.cap
     d_gray = device_frames(gray, dev)
     d_depth = torch.from_numpy(depth).to(dev)

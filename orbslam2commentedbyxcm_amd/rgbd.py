@@ -43,6 +43,12 @@ class RGBDSequencePipeline(SequencePipeline):
     def __init__(self, batch: int, width: int, height: int, fx: float, fy: float, cx: float, cy: float, dist,
                  bf: float, depth_map_factor: float = 5000.0, th_depth_factor: float = 40.0,
                  params=(5000, 1.2, 12, 20, 7), th: float = 15.0, retry_below: int = RETRY_BELOW, **kw):
+        # lane 1 starts each batch after lane 0's octree (stage 4): the RGB-D step's matcher
+        # (steps 2-4, far heavier than the monocular search) then runs beside one lane's
+        # describe and the other's first stages -- 87.0-87.1k RGB-D frames/s against
+        # 83.2-85.7k after the FAST cells (3, SequencePipeline's deep-pyramid default), 85.1-86.1k
+        # after the blur (2), 82.1-83.3k after the pyramid (1) (profiles/r06_rgbd_lane_offset_ab.txt)
+        kw.setdefault("lane_offset_stage", 4)
         super().__init__(batch, width, height, params=params, fx=fx, fy=fy, cx=cx, cy=cy, th=th, **kw)
         import torch
 
