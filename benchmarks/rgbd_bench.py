@@ -185,6 +185,7 @@ def main(argv=None):
                               lanes=args.lanes, nbuf=int(os.environ.get("ORBX_PIPE_NBUF", "2")), device=gpu,
                               matcher_mode=None if "ORBX_MATCH_MODE" not in os.environ
                               else int(os.environ["ORBX_MATCH_MODE"]),
+                              match_after_stage=int(os.environ.get("ORBX_MATCH_AFTER", "0")),
                               **({"lane_offset_stage": int(os.environ["ORBX_LANE_OFFSET"])}
                                  if "ORBX_LANE_OFFSET" in os.environ else {}))
     sf, cap = pl.sf, pl.cap
