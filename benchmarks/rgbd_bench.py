@@ -186,6 +186,7 @@ def main(argv=None):
                               matcher_mode=None if "ORBX_MATCH_MODE" not in os.environ
                               else int(os.environ["ORBX_MATCH_MODE"]),
                               match_after_stage=int(os.environ.get("ORBX_MATCH_AFTER", "0")),
+                              frame_on_lanes=os.environ.get("ORBX_RGBD_FRAME_LANES", "1") != "0",
                               **({"lane_offset_stage": int(os.environ["ORBX_LANE_OFFSET"])}
                                  if "ORBX_LANE_OFFSET" in os.environ else {}))
     sf, cap = pl.sf, pl.cap

@@ -187,8 +187,13 @@ class SequencePipeline:
                 stream_wait_event(self.streams[c].cuda_stream, self.lane_ev[c - 1])
             self.exs[c].extract_batch_device(frames[b0:b1], self.kps[b][b0:b1], self.desc[b][b0:b1],
                                              self.n[b][b0:b1])
+            self._lane_tail(b, c)
             self.ev_ex[b][c].record(self.streams[c])
         self.used[b] = True
+
+    def _lane_tail(self, b, c):
+        """Per-frame work a subclass enqueues on lane c's stream after its extraction of
+        buffer b (before the event the matcher waits for)."""
 
     def _match(self, b, after_next=False):
         Tcw = self.T_of[b]

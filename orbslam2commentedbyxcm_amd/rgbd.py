@@ -18,7 +18,8 @@ follows it:
      (Tracking.cc:988-994): the stereo octave ranges for motion along the optical axis
      beyond mb, the mvuRight gate, the rotation check, temporal claims not blocking, the
      undistorted image bounds (Frame::ComputeImageBounds) for the grid.
-Steps 2-4 run on the matcher stream beside the next batch's extraction.  No frame of the
+Steps 2-3 run per frame on each extraction lane's stream right after its frames, step 4
+on the matcher stream beside the next batch's extraction.  No frame of the
 sequence is a keyframe (UpdateLastFrame returns early for the last keyframe, Tracking.cc:
 902; a caller with keyframes passes their LastFrames' MapPoints through set_tracked and
 skips those frames' temporal points itself).  Optimizer::PoseOptimization, which consumes
@@ -49,6 +50,10 @@ class RGBDSequencePipeline(SequencePipeline):
         # 83.2-85.7k after the FAST cells (3, SequencePipeline's deep-pyramid default), 85.1-86.1k
         # after the blur (2), 82.1-83.3k after the pyramid (1) (profiles/r06_rgbd_lane_offset_ab.txt)
         kw.setdefault("lane_offset_stage", 4)
+        # steps 2-3 (the RGB-D Frame, UpdateLastFrame) per frame, so on each extraction
+        # lane's stream right after its frames (frame_on_lanes) or on the matcher stream
+        # before the search
+        self.frame_on_lanes = bool(kw.pop("frame_on_lanes", True))
         super().__init__(batch, width, height, params=params, fx=fx, fy=fy, cx=cx, cy=cy, th=th, **kw)
         import torch
 
@@ -93,6 +98,22 @@ class RGBDSequencePipeline(SequencePipeline):
         self.D_of[b] = self._next_depth
         super()._extract(frames, Tcw, b)
 
+    def _frame_steps(self, b, b0, b1, stream):
+        """Steps 2-3 for frames b0..b1-1 of buffer b on `stream`."""
+        T = self.T_of[b][b0:b1]
+        lf = {k: v[b0:b1] for k, v in self.lf[b].items()}
+        rgbd_device(self.cam, self.kps[b][b0:b1], self.n[b][b0:b1], self.D_of[b][b0:b1], self.bf,
+                    self.depth_map_factor, self.kpu[b][b0:b1], self.ur[b][b0:b1], self.dp[b][b0:b1], stream=stream)
+        update_last_frame_device(self.kpu[b][b0:b1], self.n[b][b0:b1], self.dp[b][b0:b1], T, self.fx, self.fy,
+                                 self.cx, self.cy, self.th_depth, lf,
+                                 d_obs_in=None if self.obs_in is None else self.obs_in[b0:b1],
+                                 d_pos_in=None if self.pos_in is None else self.pos_in[b0:b1], stream=stream)
+
+    def _lane_tail(self, b, c):
+        if self.frame_on_lanes:
+            b0, b1 = self.bounds[c]
+            self._frame_steps(b, b0, b1, self.streams[c].cuda_stream)
+
     def _match(self, b, after_next=False):
         import torch
         T = self.T_of[b]
@@ -107,10 +128,8 @@ class RGBDSequencePipeline(SequencePipeline):
             ev[0].record(self.ms)
         s = self.ms.cuda_stream
         lf = self.lf[b]
-        rgbd_device(self.cam, self.kps[b], self.n[b], self.D_of[b], self.bf, self.depth_map_factor, self.kpu[b],
-                    self.ur[b], self.dp[b], stream=s)
-        update_last_frame_device(self.kpu[b], self.n[b], self.dp[b], T, self.fx, self.fy, self.cx, self.cy,
-                                 self.th_depth, lf, d_obs_in=self.obs_in, d_pos_in=self.pos_in, stream=s)
+        if not self.frame_on_lanes:
+            self._frame_steps(b, 0, self.B, s)
         self.matcher.match_sequence_device_ex(
             self.kpu[b], self.desc[b], self.n[b], T, self.mp[b], self.nm[b], self.sf, self.fx, self.fy, self.cx,
             self.cy, self.W, self.H, th=self.th, mono=False, bf=self.bf, b=self.mb, d_u_right=self.ur[b],
