@@ -187,6 +187,8 @@ def main(argv=None):
                               else int(os.environ["ORBX_MATCH_MODE"]),
                               match_after_stage=int(os.environ.get("ORBX_MATCH_AFTER", "0")),
                               frame_on_lanes=os.environ.get("ORBX_RGBD_FRAME_LANES", "1") != "0",
+                              match_priority=int(os.environ.get("ORBX_MATCH_PRIORITY", "0")),
+                              match_cu_stride=int(os.environ.get("ORBX_MATCH_CUSTRIDE", "1")),
                               **({"lane_offset_stage": int(os.environ["ORBX_LANE_OFFSET"])}
                                  if "ORBX_LANE_OFFSET" in os.environ else {}))
     sf, cap = pl.sf, pl.cap
