@@ -569,7 +569,7 @@ def main():
                           match_cu_stride=int(os.environ.get("ORBX_MATCH_CUSTRIDE", "1")),
                           match_priority=int(os.environ.get("ORBX_MATCH_STREAM_PRIO", "0")),
                           level0_in_place=os.environ.get("ORBX_L0_COPY") != "1",
-                          first_in_phase=os.environ.get("ORBX_PIPE_FIRST_INPHASE", "0") == "1",
+                          first_in_phase=os.environ.get("ORBX_PIPE_FIRST_INPHASE", "1") == "1",
                           retry_below=args.track_retry)
     S = pl.S
     nbufs = len(pl.kps)  # output buffer sets in rotation

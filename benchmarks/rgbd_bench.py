@@ -188,6 +188,7 @@ def main(argv=None):
                               match_after_stage=int(os.environ.get("ORBX_MATCH_AFTER", "0")),
                               frame_on_lanes=os.environ.get("ORBX_RGBD_FRAME_LANES", "1") != "0",
                               match_priority=int(os.environ.get("ORBX_MATCH_PRIORITY", "0")),
+                              first_in_phase=os.environ.get("ORBX_PIPE_FIRST_INPHASE", "1") == "1",
                               match_cu_stride=int(os.environ.get("ORBX_MATCH_CUSTRIDE", "1")),
                               **({"lane_offset_stage": int(os.environ["ORBX_LANE_OFFSET"])}
                                  if "ORBX_LANE_OFFSET" in os.environ else {}))

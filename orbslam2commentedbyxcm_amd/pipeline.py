@@ -40,7 +40,7 @@ class SequencePipeline:
                  lane_offset_stage: int | None = None, match_cu_stride: int = 1,
                  match_priority: int = 0, on_matched=None, local_map: bool = False, local_window: int = 3,
                  local_th: float = 1.0, level0_in_place: bool = True, retry_below: int = 20,
-                 first_in_phase: bool = False):
+                 first_in_phase: bool = True):
         import torch
 
         self.B, self.W, self.H = int(batch), int(width), int(height)
@@ -180,7 +180,8 @@ class SequencePipeline:
             # first_in_phase, on a run's first batch (nothing pending to match): there the
             # lanes start together, and the offset forms on the second batch, where the
             # first batch's matching runs beside the waiting lane instead of nothing
-            # (first_in_phase; r05as: +0.4 % at 20 steps, within noise -- off)
+            # (first_in_phase; r05as: +0.4 % at 20 steps, within noise; r06fp: +0.6 % over six
+            # interleaved pairs at 20 steps, five of them faster -- on since round 6)
             if self.lane_ev and c > 0 and not (self.first_in_phase and self.match and self.pipelined
                                                and self.pending is None):
                 from .extractor import stream_wait_event
