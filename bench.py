@@ -571,6 +571,7 @@ def main():
                           level0_in_place=os.environ.get("ORBX_L0_COPY") != "1",
                           first_in_phase=os.environ.get("ORBX_PIPE_FIRST_INPHASE", "1") == "1",
                           retry_below=args.track_retry)
+    first_in_phase = bool(pl.first_in_phase)
     S = pl.S
     nbufs = len(pl.kps)  # output buffer sets in rotation
     lane_off = pl.lane_offset_stage if pl.lane_ev is not None else None  # None: no offset applied
@@ -829,6 +830,7 @@ def main():
                        "parallelism": f"frame-sharded x{world}", "lanes_per_gpu": S,
                        "lane_offset_stage": lane_off,
                        "pipelined_match": pipeline, "buffer_sets": nbufs,
+                       "first_batch_lanes_in_phase": first_in_phase,
                        "match_cu_stride": match_cu},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), **prof,

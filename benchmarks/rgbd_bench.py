@@ -292,7 +292,9 @@ def main(argv=None):
                        "sensor": "RGB-D",
                        "frames_per_gpu_step": B, "global_batch": B * world, "width": S.W, "height": S.H,
                        "parallelism": f"frame-sharded x{world}", "lanes_per_gpu": pl.S,
-                       "buffer_sets": len(pl.kps), "th_depth_m": round(pl.th_depth, 4),
+                       "buffer_sets": len(pl.kps), "lane_offset_stage": pl.lane_offset_stage,
+                       "first_batch_lanes_in_phase": pl.first_in_phase,
+                       "frame_steps_on_lanes": pl.frame_on_lanes, "th_depth_m": round(pl.th_depth, 4),
                        "image_bounds": [round(float(x), 4) for x in pl.image_bounds]},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
