@@ -100,16 +100,18 @@ def test_device_status_reports_forced_overflow(oracle, orbx_built):
     assert not ex.status().any()
 
 
-@pytest.mark.parametrize("B,lanes,pipelined,steps,nbuf", [(16, 2, True, 5, 2), (24, 3, True, 4, 2),
-                                                          (12, 1, False, 3, 2), (256, 2, True, 3, 2),
-                                                          (16, 2, True, 5, 3), (256, 2, True, 4, 3)])
-def test_sequence_pipeline_distinct_batch_every_step(oracle, orbx_built, B, lanes, pipelined, steps, nbuf):
+@pytest.mark.parametrize("B,lanes,pipelined,steps,nbuf,fip", [(16, 2, True, 5, 2, True), (24, 3, True, 4, 2, True),
+                                                              (12, 1, False, 3, 2, True), (256, 2, True, 3, 2, True),
+                                                              (16, 2, True, 5, 3, True), (256, 2, True, 4, 3, True),
+                                                              (16, 2, True, 5, 3, False)])
+def test_sequence_pipeline_distinct_batch_every_step(oracle, orbx_built, B, lanes, pipelined, steps, nbuf, fip):
     """Every step gets its own batch (its own canvas and poses) and steps are issued
     back to back with no host synchronisation; each batch's outputs are copied out on the
     matcher stream as soon as its matching is enqueued (SequencePipeline.on_matched, before
     the buffer is released), so a buffer reused too early, an event waited on the wrong
     buffer or a batch matched with another batch's poses shows up as a mismatch.  Two
-    buffer sets and three (the bench's at <= 8 levels)."""
+    buffer sets and three (the bench's at <= 8 levels); the first batch's lanes in phase
+    (the default) or offset from the start."""
     import torch
 
     batches = [synth.sequence(2000 + j, B) for j in range(steps)]
@@ -120,7 +122,8 @@ def test_sequence_pipeline_distinct_batch_every_step(oracle, orbx_built, B, lane
         r = pl.results(b)
         snaps.append({k: v.clone() for k, v in r.items()})
 
-    pl = SequencePipeline(B, 640, 480, lanes=lanes, pipelined=pipelined, on_matched=grab, nbuf=nbuf)
+    pl = SequencePipeline(B, 640, 480, lanes=lanes, pipelined=pipelined, on_matched=grab, nbuf=nbuf,
+                          first_in_phase=fip)
     dev_in = [(torch.from_numpy(f).to(pl.dev), torch.from_numpy(sequence_poses(o)).to(pl.dev)) for f, o in batches]
     torch.cuda.synchronize()
     with torch.cuda.stream(pl.ms):  # the clones run on the matcher stream, after the matching
