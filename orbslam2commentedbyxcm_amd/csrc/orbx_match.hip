@@ -322,6 +322,20 @@ constexpr int kTopK = ORBX_TOPK;
 // 6 measured configs[4] 81.5k frames/s against 77.0k for 4 and 81.0k for 8, configs[1]
 // unchanged (profiles/r02_n_lane_topk_ab.log)
 constexpr int kLaneTopK = ORBX_LANE_TOPK;           // candidate-list length per query
+// The sequence matcher's split scoring kernel runs beside the extraction lanes, where its
+// registers are what counts (4 waves a SIMD: every VGPR it holds is 4 the extraction's waves
+// on that SIMD cannot have).  Without the next-query prefetch it holds 83 VGPRs instead of
+// 102 and 80 with lane lists of 4: RGB-D configs[4] 88.3-88.4k -> 89.3-89.5k (no prefetch)
+// -> 90.6-91.0k frames/s (lists of 4; 3 and 5 measured 89.8k and 89.3-89.6k), configs[1]
+// 228.0-228.8k -> 229.4-230.0k (profiles/r06_scoring_registers_ab.txt).  The single calls
+// keep both (their latency is the query loads').
+#ifndef ORBX_SPLIT_LANE_TOPK
+#define ORBX_SPLIT_LANE_TOPK 4
+#endif
+#ifndef ORBX_SPLIT_PREFETCH
+#define ORBX_SPLIT_PREFETCH 0
+#endif
+constexpr int kSplitLaneTopK = ORBX_SPLIT_LANE_TOPK;
 static_assert(kTopK % 4 == 0, "lists are stored as uint4s");
 constexpr int kListVec = kTopK / 4;        // uint4s per stored list
 constexpr int kListWords = kTopK / 2;      // u64 words per stored list
@@ -455,13 +469,12 @@ __device__ __forceinline__ void sorted_insert(unsigned (&k)[L], unsigned key) {
 // pipelined steps unchanged (within noise)
 #define ORBX_SCORE_PAIR 1
 #endif
-template <int K>
+template <int K, int KL = kLaneTopK>
 __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const QueryReg& QR, bool valid,
                              const SortedGrid& G, const int* sfmp, unsigned out[kTopK]) {
     static_assert(K == 4 || K == 8 || K == 16 || K == 64, "a DPP quad, half a DPP row, a DPP row or a wave");
     const int r = threadIdx.x & (K - 1);
     const ProjQuery& Q = QR.q;
-    constexpr int KL = kLaneTopK;
     unsigned k[KL];
 #pragma unroll
     for (int i = 0; i < KL; i++) k[i] = kNoEntry;
@@ -1572,6 +1585,7 @@ __device__ __forceinline__ void proj_search_body(const ProjProblem* __restrict__
     }
     __syncthreads();
     const int qcut4 = s_qcut[0], qcut8 = s_qcut[1];
+    constexpr bool kPrefetch = !SPLIT || ORBX_SPLIT_PREFETCH;  // the next queries' loads during the current ones
     auto pass = [&](auto kr, int q0, int q1) {
         constexpr int KR = decltype(kr)::value;
         constexpr int kQw = 64 / KR;  // queries per wave and pass
@@ -1582,10 +1596,10 @@ __device__ __forceinline__ void proj_search_body(const ProjProblem* __restrict__
         for (; qb < q1; qb += kStep) {
             const int q = qb + lane / KR;
             QueryReg nxt;
-            if (qb + kStep < q1) nxt = load_query(pb, min(q + kStep, q1 - 1));  // prefetch
+            if (kPrefetch && qb + kStep < q1) nxt = load_query(pb, min(q + kStep, q1 - 1));  // prefetch
             const int mp = q < q1 ? cur.q.mp : -1;
             unsigned e[kTopK];
-            score_groupk<KR>(pb, P, cur, mp >= 0, G, SPLIT ? nullptr : sfmp, e);
+            score_groupk<KR, SPLIT ? kSplitLaneTopK : kLaneTopK>(pb, P, cur, mp >= 0, G, SPLIT ? nullptr : sfmp, e);
             if ((lane & (KR - 1)) == 0 && q < q1) {
 #pragma unroll
                 for (int v = 0; v < kListVec; v++)
@@ -1593,7 +1607,10 @@ __device__ __forceinline__ void proj_search_body(const ProjProblem* __restrict__
                 qmp[q] = claim_word(mp, P);
                 qang[q] = cur.q.angle;
             }
-            cur = nxt;
+            if (kPrefetch)
+                cur = nxt;
+            else if (qb + kStep < q1)
+                cur = load_query(pb, min(q + kStep, q1 - 1));
         }
     };
     if (qcut4 > 0) pass(std::integral_constant<int, 4>{}, 0, qcut4);
