@@ -463,6 +463,9 @@ __device__ __forceinline__ void sorted_insert(unsigned (&k)[L], unsigned key) {
 #ifndef ORBX_SCORE_KR_FIXED
 #define ORBX_SCORE_KR_FIXED 0
 #endif
+#ifndef ORBX_VISIT_RCP
+#define ORBX_VISIT_RCP 1
+#endif
 #ifndef ORBX_SCORE_PAIR
 // two bucket entries per scan step with descriptors from global memory (round 3): the
 // configs[4] matcher alone 1.114 -> 1.047 ms, the drop-in rows a11-a14 1-3 % faster,
@@ -518,8 +521,18 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
             int sh = 0;
             while (sh < kLog2K && (nv << (sh + 1)) <= K) sh++;
             const int lpc = 1 << sh, sub = r & (lpc - 1);
+#if ORBX_VISIT_RCP
+            // v / nor without an integer division (~25 VALU): (v + 0.5) / nor lies at least
+            // 0.5 / nor >= 1/64 from an integer (nor <= 32, v < 2^11), far above the error of
+            // v_rcp_f32 and one multiply
+            const float inv_nor = __builtin_amdgcn_rcpf((float)max(nor, 1));
+#endif
             for (int v = r >> sh; v < nv; v += K >> sh) {
+#if ORBX_VISIT_RCP
+                const int cq = (int)(((float)v + 0.5f) * inv_nor);
+#else
                 const int cq = v / nor;
+#endif
                 const int ix = cr.x0 + cq, o = blo + (v - cq * nor);
                 {
                     // the rows y0..y1 of this column and octave: blocks b0..b1, whose
