@@ -633,12 +633,21 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
         }
     }
 #if ORBX_SCORE_COUNT
+    // balance: a lane's work (visits + scan steps), its group's maximum and its wave's
+    int gmax = valid ? (int)(n_pair + n_step) : 0;
+    for (int o = K / 2; o > 0; o >>= 1) gmax = max(gmax, __shfl_xor(gmax, o));
+    int wmax = gmax;
+    for (int o = 32; o >= K; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o));
     if (P.stamps && valid) {
         unsigned long long* sc = P.stamps + kStampWords * (size_t)blockIdx.x;
         atomicAdd(sc + kStampScore, n_pair);
         atomicAdd(sc + kStampScore + 1, n_step);
         atomicAdd(sc + kStampScore + 2, n_ok);
-        if (r == 0) atomicAdd(sc + kStampScore + 3, 1ull);
+        if (r == 0) {
+            atomicAdd(sc + kStampScore + 3, 1ull);
+            atomicAdd(sc + kStampScore + 4, (unsigned long long)gmax);
+            atomicAdd(sc + kStampScore + 5, (unsigned long long)wmax);
+        }
     }
 #endif
     // Group top-kTopK: keys are unique (distinct positions), so one lane pops each minimum.

@@ -53,7 +53,7 @@ struct ProjProblem {
 constexpr int kProjScratchWords = ORBX_TOPK / 2 + 2;
 
 #ifndef ORBX_SCORE_COUNT
-#define ORBX_SCORE_COUNT 0  // diagnostics build: the scoring loop's visit counts in stamp words 17-20
+#define ORBX_SCORE_COUNT 0  // diagnostics build: the scoring loop's visit counts in stamp words 17-22
 #endif
 // ProjParams::stamps words per problem.  The replay forms use words 9, 14 and 15
 // differently, so word kStampForm records which one wrote them: 64 for the one-wave replay
@@ -61,7 +61,7 @@ constexpr int kProjScratchWords = ORBX_TOPK / 2 + 2;
 // block replay (9 = rounds, 14 = chunk loads, 15 = commits: durations).
 constexpr int kStampForm = 16;
 constexpr int kStampScore = 17;
-constexpr int kStampWords = ORBX_SCORE_COUNT ? 21 : 17;
+constexpr int kStampWords = ORBX_SCORE_COUNT ? 23 : 17;
 
 // Call-level semantics of the SearchByProjection overload being executed.
 struct ProjParams {

@@ -855,17 +855,20 @@ int orbx_match_sequence_device_ex(orbx_matcher* m, const orbx_sequence* sq, void
             }
 #if ORBX_SCORE_COUNT
             {
-                double a = 0, b = 0, c = 0, n = 0;
+                double a = 0, b = 0, c = 0, n = 0, gm = 0, wm = 0;
                 for (int p = 0; p < npairs; p++) {
                     const unsigned long long* r = &h[(size_t)kStampWords * p];
                     a += (double)r[kStampScore];
                     b += (double)r[kStampScore + 1];
                     c += (double)r[kStampScore + 2];
                     n += (double)r[kStampScore + 3];
+                    gm += (double)r[kStampScore + 4];
+                    wm += (double)r[kStampScore + 5];
                 }
                 fprintf(stderr, "[orbx score counts] per scored query: %.1f (column, octave) visits, %.1f entry steps, "
-                        "%.1f candidates in the window (summed over the query's lanes; %.0f queries)\n",
-                        a / n, b / n, c / n, n);
+                        "%.1f candidates in the window (summed over the query's lanes; %.0f queries); lane work "
+                        "(visits + steps) group max %.2f, wave max %.2f\n",
+                        a / n, b / n, c / n, n, gm / n, wm / n);
             }
 #endif
             fprintf(stderr,
