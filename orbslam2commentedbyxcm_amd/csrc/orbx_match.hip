@@ -336,6 +336,24 @@ constexpr int kLaneTopK = ORBX_LANE_TOPK;           // candidate-list length per
 #define ORBX_SPLIT_PREFETCH 0
 #endif
 constexpr int kSplitLaneTopK = ORBX_SPLIT_LANE_TOPK;
+// Lanes per query of the split scoring (0: by window width, 4 / 8 / 16 as the other forms).
+// Two: the balance counters (-DORBX_SCORE_COUNT) showed a 16-lane group's busiest lane with
+// twice its mean work and the wave's with 2.5 times, which smaller groups cut; a pair
+// merges with one DPP step and keeps lists of 6 per lane.  RGB-D configs[4] 91.8-91.9k (by
+// width) -> 94.0-94.2k frames/s; one lane (lists of 12) 84.6-84.8k, four 91.5-91.6k; lists of
+// 4 / 5 / 8 for the pair 90.5-90.7k / 91.0-91.5k / 93.1-93.6k against 93.1-93.6k for 6;
+// configs[1] 228.9-230.0k -> 230.8-232.5k (profiles/r06_scoring_registers_ab.txt).
+#ifndef ORBX_SPLIT_KR_ALL
+#define ORBX_SPLIT_KR_ALL 2
+#endif
+constexpr int kSplitKr = ORBX_SPLIT_KR_ALL;
+#ifndef ORBX_SPLIT_KR2_TOPK
+#define ORBX_SPLIT_KR2_TOPK 6
+#endif
+// a lane's list length in a KR-lane group of the split scoring: a lone lane keeps the whole list
+__host__ __device__ constexpr int split_lane_topk(int kr) {
+    return kr == 1 ? kTopK : kr == 2 ? ORBX_SPLIT_KR2_TOPK : kSplitLaneTopK;
+}
 static_assert(kTopK % 4 == 0, "lists are stored as uint4s");
 constexpr int kListVec = kTopK / 4;        // uint4s per stored list
 constexpr int kListWords = kTopK / 2;      // u64 words per stored list
@@ -371,6 +389,10 @@ __device__ __forceinline__ unsigned half_row_min_u32(unsigned v) {
     v = umin_(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));
     v = umin_(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false));
     return v;
+}
+
+__device__ __forceinline__ unsigned pair_min_u32(unsigned v) {  // lane pairs: quad_perm [1,0,3,2]
+    return umin_(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));
 }
 
 __device__ __forceinline__ unsigned quad_min_u32(unsigned v) {
@@ -475,7 +497,8 @@ __device__ __forceinline__ void sorted_insert(unsigned (&k)[L], unsigned key) {
 template <int K, int KL = kLaneTopK>
 __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const QueryReg& QR, bool valid,
                              const SortedGrid& G, const int* sfmp, unsigned out[kTopK]) {
-    static_assert(K == 4 || K == 8 || K == 16 || K == 64, "a DPP quad, half a DPP row, a DPP row or a wave");
+    static_assert(K == 1 || K == 2 || K == 4 || K == 8 || K == 16 || K == 64,
+                  "a lane, a lane pair, a DPP quad, half a DPP row, a DPP row or a wave");
     const int r = threadIdx.x & (K - 1);
     const ProjQuery& Q = QR.q;
     unsigned k[KL];
@@ -517,7 +540,7 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
             // then left each lane a dozen nearly empty visits.)
             const int nor = bhi - blo + 1;
             const int nv = nor > 0 ? ncol * nor : 0;
-            constexpr int kLog2K = K == 4 ? 2 : (K == 8 ? 3 : (K == 16 ? 4 : 6));
+            constexpr int kLog2K = K == 1 ? 0 : K == 2 ? 1 : K == 4 ? 2 : (K == 8 ? 3 : (K == 16 ? 4 : 6));
             int sh = 0;
             while (sh < kLog2K && (nv << (sh + 1)) <= K) sh++;
             const int lpc = 1 << sh, sub = r & (lpc - 1);
@@ -661,7 +684,10 @@ __device__ void score_groupk(const ProjProblem& pb, const ProjParams& P, const Q
         // a lane whose listed candidates are used up but that saw more makes the rest unknown
         const unsigned long long dry = __ballot(over && k[0] == kNoEntry);
         trunc = trunc || ((dry >> rsh) & gmask) != 0;
-        m[j] = K == 4 ? quad_min_u32(k[0]) : (K == 8 ? half_row_min_u32(k[0]) : row_min_u32(k[0]));
+        m[j] = K == 1   ? k[0]
+               : K == 2 ? pair_min_u32(k[0])
+               : K == 4 ? quad_min_u32(k[0])
+                        : (K == 8 ? half_row_min_u32(k[0]) : row_min_u32(k[0]));
         if (K == 64) {  // the four rows' minima by v_readlane: wave-uniform, no LDS round trip
             m[j] = umin_(umin_((unsigned)__builtin_amdgcn_readlane((int)m[j], 0),
                                (unsigned)__builtin_amdgcn_readlane((int)m[j], 16)),
@@ -1585,7 +1611,9 @@ __device__ __forceinline__ void proj_search_body(const ProjProblem* __restrict__
     // Pyramids of up to 8 levels keep KR 8 for every query: the classes measured slower
     // there (configs[1] 227.8-228.4k -> 224.3-225.9k frames/s) and faster above
     // (configs[4] 108.2-108.3k -> 111.1-111.3k; r05c, interleaved on one box).
-    const bool one_kr = ORBX_SCORE_KR_FIXED || P.noct <= 8;  // uniform over the workgroup
+    // The split scoring (the sequence matcher beside the extraction) gives every query the
+    // same kSplitKr lanes instead.
+    const bool one_kr = ORBX_SCORE_KR_FIXED || P.noct <= 8 || (SPLIT && kSplitKr > 0);  // uniform over the workgroup
     if (tid < 2) s_qcut[tid] = one_kr && tid == 1 && P.noct <= 8 ? nq : 0;
     __syncthreads();
     if (!one_kr) {
@@ -1621,7 +1649,7 @@ __device__ __forceinline__ void proj_search_body(const ProjProblem* __restrict__
             if (kPrefetch && qb + kStep < q1) nxt = load_query(pb, min(q + kStep, q1 - 1));  // prefetch
             const int mp = q < q1 ? cur.q.mp : -1;
             unsigned e[kTopK];
-            score_groupk<KR, SPLIT ? kSplitLaneTopK : kLaneTopK>(pb, P, cur, mp >= 0, G, SPLIT ? nullptr : sfmp, e);
+            score_groupk<KR, SPLIT ? split_lane_topk(KR) : kLaneTopK>(pb, P, cur, mp >= 0, G, SPLIT ? nullptr : sfmp, e);
             if ((lane & (KR - 1)) == 0 && q < q1) {
 #pragma unroll
                 for (int v = 0; v < kListVec; v++)
@@ -1635,9 +1663,13 @@ __device__ __forceinline__ void proj_search_body(const ProjProblem* __restrict__
                 cur = load_query(pb, min(q + kStep, q1 - 1));
         }
     };
-    if (qcut4 > 0) pass(std::integral_constant<int, 4>{}, 0, qcut4);
-    if (qcut8 > qcut4) pass(std::integral_constant<int, 8>{}, qcut4, qcut8);
-    if (nq > qcut8) pass(std::integral_constant<int, 16>{}, qcut8, nq);
+    if constexpr (SPLIT && kSplitKr > 0) {
+        pass(std::integral_constant<int, (kSplitKr > 0 ? kSplitKr : 1)>{}, 0, nq);
+    } else {
+        if (qcut4 > 0) pass(std::integral_constant<int, 4>{}, 0, qcut4);
+        if (qcut8 > qcut4) pass(std::integral_constant<int, 8>{}, qcut4, qcut8);
+        if (nq > qcut8) pass(std::integral_constant<int, 16>{}, qcut8, nq);
+    }
     __syncthreads();
     if (st && tid == 0) st[2] = wall_clock64();
     if (SPLIT) {
