@@ -714,6 +714,176 @@ __device__ __forceinline__ void score_rowk(const ProjProblem& pb, const ProjPara
     score_groupk<kScoreRow>(pb, P, QR, valid, G, sfmp, out);
 }
 
+#ifndef ORBX_SPLIT_PERSIST
+#define ORBX_SPLIT_PERSIST 1
+#endif
+#ifndef ORBX_PERSIST_BATCH
+#define ORBX_PERSIST_BATCH 32
+#endif
+// The split scoring's lane pairs without lockstep between pairs (ORBX_SPLIT_PERSIST): a pair
+// walks its query's visits and scans as score_groupk<2> does, and when both its lanes are
+// through it merges, writes the list and takes the workgroup's next query from an LDS
+// counter.  In lockstep a wave's 32 pairs wait for the busiest on every query (1.4 times
+// the mean work, -DORBX_SCORE_COUNT); here a wave's iteration is one visit step and one
+// scan step of every lane with work.  Merges, list writes and query loads run for
+// kPersistBatch lanes at a time (or when no lane is left scanning), so that block runs once
+// per several queries.  Same lists as score_groupk<2>.
+constexpr int kPersistBatch = ORBX_PERSIST_BATCH;
+__device__ void score_pairs(const ProjProblem& pb, const ProjParams& P, const SortedGrid& G, uint4* qk, int* qmp,
+                            float* qang, int* s_next) {
+    constexpr int KL = split_lane_topk(2);
+    const int nq = pb.nq, noct = G.noct;
+    const int lane = threadIdx.x & 63, r = lane & 1;
+    int q = -1;  // current query; >= nq: retired
+    bool fresh = true;
+    unsigned long long q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+    float qu = 0.f, qv = 0.f, qr = 0.f, qur = 0.f, qer = -1.f, ang = 0.f;
+    int mp = -1;
+    int x0 = 0, nor = 1, nv = 0, blo = 0, b0 = 0, b1 = 0, ylo = 0, yhi = 0, v = 0, vstep = 2, sub = 0, lpc = 1;
+    float inv_nor = 1.f;
+    int a = 0, e0 = 0, s1 = 0, e1 = 0;
+    unsigned k[KL];
+#pragma unroll
+    for (int i = 0; i < KL; i++) k[i] = kNoEntry;
+    int seen = 0;
+    const bool ur_check = pb.u_right != nullptr;
+    while (true) {
+        const bool ldone = !fresh && q < nq && v >= nv && a >= e1;
+        const bool pdone = ldone && __builtin_amdgcn_update_dpp(0, (int)ldone, 0xB1, 0xF, 0xF, false) != 0;
+        const bool want = fresh || pdone;
+        const unsigned long long wm = __ballot(want), busy = __ballot(!want && q < nq);
+        if (__popcll(wm) >= kPersistBatch || busy == 0) {
+            // the pairs' merges (score_groupk's, on copies: the other pairs keep scanning)
+            unsigned c[KL];
+#pragma unroll
+            for (int i = 0; i < KL; i++) c[i] = k[i];
+            const bool over = seen > KL;
+            bool trunc = false;
+            unsigned m[kTopK];
+#pragma unroll
+            for (int j = 0; j < kTopK; j++) {
+                const unsigned long long dry = __ballot(over && c[0] == kNoEntry);
+                trunc = trunc || ((dry >> (lane & ~1)) & 3ull) != 0;
+                m[j] = pair_min_u32(c[0]);
+                if (c[0] == m[j] && m[j] != kNoEntry) {
+#pragma unroll
+                    for (int i = 0; i < KL - 1; i++) c[i] = c[i + 1];
+                    c[KL - 1] = kNoEntry;
+                }
+                if (trunc) m[j] = kTrunc;
+            }
+            if (pdone && r == 0) {
+#pragma unroll
+                for (int j = 0; j < kTopK; j++)
+                    m[j] = m[j] >= kTrunc ? m[j]
+                                          : ((m[j] >> 13) << 18) | ((unsigned)sk_oct(G.skey[m[j] & 0x1fffu]) << 13) |
+                                                (m[j] & 0x1fffu);
+#pragma unroll
+                for (int w = 0; w < kListVec; w++)
+                    qk[kListVec * q + w] = make_uint4(m[4 * w], m[4 * w + 1], m[4 * w + 2], m[4 * w + 3]);
+                qmp[q] = claim_word(mp, P);
+                qang[q] = ang;
+            }
+            int nqi = 0;
+            if (want && r == 0) nqi = atomicAdd(s_next, 1);
+            nqi = __builtin_amdgcn_update_dpp(0, nqi, 0xA0, 0xF, 0xF, false);  // the pair's first lane's
+            if (want) {
+                q = nqi;
+                fresh = false;
+                nv = 0;
+                v = 0;
+                a = e1 = 0;
+                seen = 0;
+#pragma unroll
+                for (int i = 0; i < KL; i++) k[i] = kNoEntry;
+                if (q < nq) {
+                    const QueryReg QR = load_query(pb, q);
+                    const ProjQuery& Q = QR.q;
+                    mp = Q.mp;
+                    ang = Q.angle;
+                    qu = Q.u, qv = Q.v, qr = Q.r, qur = Q.ur, qer = Q.er_max;
+                    if (mp >= 0) {
+                        const CellRange cr = cell_range(pb, Q.u, Q.v, Q.r);
+                        if (!cr.empty) {
+                            q0 = (unsigned long long)QR.d0.y << 32 | QR.d0.x;
+                            q1 = (unsigned long long)QR.d0.w << 32 | QR.d0.z;
+                            q2 = (unsigned long long)QR.d1.y << 32 | QR.d1.x;
+                            q3 = (unsigned long long)QR.d1.w << 32 | QR.d1.z;
+                            int olo = 0, ohi = 31;  // the octave range, as score_groupk
+                            if ((Q.min_level > 0) || (Q.max_level >= 0)) {
+                                olo = Q.min_level > 0 ? Q.min_level : 0;
+                                if (Q.max_level >= 0) ohi = Q.max_level;
+                            }
+                            if (Q.post_max >= 0) {
+                                olo = max(olo, Q.post_min);
+                                ohi = min(ohi, Q.post_max);
+                            }
+                            blo = min(olo, noct - 1);
+                            const int bhi = olo > ohi ? -1 : min(ohi, noct - 1);
+                            b0 = cr.y0 >> kRowBlkLog2, b1 = cr.y1 >> kRowBlkLog2;
+                            ylo = cr.y0 & (kRowBlk - 1), yhi = cr.y1 & (kRowBlk - 1);
+                            x0 = cr.x0;
+                            nor = bhi - blo + 1;
+                            nv = nor > 0 ? (cr.x1 - cr.x0 + 1) * nor : 0;
+                            inv_nor = __builtin_amdgcn_rcpf((float)max(nor, 1));
+                            const int sh = nv <= 1 ? 1 : 0;  // score_groupk<2>'s lanes per visit
+                            lpc = 1 << sh, sub = r & (lpc - 1), v = r >> sh, vstep = 2 >> sh;
+                        }
+                    }
+                } else {
+                    q = nq;
+                }
+            }
+        }
+        if (__ballot(q < nq) == 0) break;
+        // the next (column, octave) visit of a lane whose scan is through
+        if (!fresh && q < nq && a >= e1 && v < nv) {
+            const int cq = (int)(((float)v + 0.5f) * inv_nor);
+            const int ix = x0 + cq, o = blo + (v - cq * nor);
+            const uint16_t* bt = G.bstart + (ix * noct + o) * kNumBlk;
+            a = bt[b0] + sub, e0 = bt[b0 + 1], s1 = bt[b1], e1 = bt[b1 + 1];
+            v += vstep;
+        }
+        // one scan step: entries a and a + lpc (score_groupk's pair form)
+        if (!fresh && q < nq && a < e1) {
+            const int a2 = a + lpc;
+            const bool h2 = a2 < e1;
+            const int entA = G.orun[a], entB = G.orun[h2 ? a2 : a];
+            const int pA = entA & 0x1fff, pB = entB & 0x1fff;
+            const float2 kA = G.sxy[pA], kB = G.sxy[pB];
+            const unsigned kkA = G.skey[pA], kkB = G.skey[pB];
+            auto test = [&](int at, int ent, float2 kp, unsigned kk) {
+                const int yr = ent >> 13;
+                if ((at < e0 && yr < ylo) || (at >= s1 && yr > yhi)) return false;
+                if (!(fabsf(kp.x - qu) < qr && fabsf(kp.y - qv) < qr)) return false;
+                return (kk & kKeyBlocked) == 0u;
+            };
+            const bool okA = test(a, entA, kA, kkA);
+            const bool okB = h2 && test(a2, entB, kB, kkB);
+            a += 2 * lpc;
+            if (okA || okB) {
+                const int iA = sk_idx(kkA), iB = sk_idx(okB ? kkB : kkA);
+                const ulonglong2* tA = (const ulonglong2*)(pb.desc + (size_t)iA * 32);
+                const ulonglong2* tB = (const ulonglong2*)(pb.desc + (size_t)iB * 32);
+                const ulonglong2 yA0 = ldg(tA), yA1 = ldg(tA + 1), yB0 = ldg(tB), yB1 = ldg(tB + 1);
+                float urA = 0.f, urB = 0.f;
+                if (qer >= 0.f && ur_check) {
+                    urA = ldg(pb.u_right + iA);
+                    urB = ldg(pb.u_right + iB);
+                }
+                auto take = [&](bool ok, float ur, int p, const ulonglong2& y0, const ulonglong2& y1) {
+                    if (!ok || (ur > 0 && fabsf(qur - ur) > qer)) return;
+                    const int d = __popcll(q0 ^ y0.x) + __popcll(q1 ^ y0.y) + __popcll(q2 ^ y1.x) + __popcll(q3 ^ y1.y);
+                    seen++;
+                    sorted_insert<KL>(k, ((unsigned)d << 13) | (unsigned)p);
+                };
+                take(okA, urA, pA, yA0, yA1);
+                take(okB, urB, pB, yB0, yB1);
+            }
+        }
+    }
+}
+
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // LDS scratch of grid_sort: one u32 counter per grid cell + the off-grid bucket
@@ -1614,7 +1784,9 @@ __device__ __forceinline__ void proj_search_body(const ProjProblem* __restrict__
     // The split scoring (the sequence matcher beside the extraction) gives every query the
     // same kSplitKr lanes instead.
     const bool one_kr = ORBX_SCORE_KR_FIXED || P.noct <= 8 || (SPLIT && kSplitKr > 0);  // uniform over the workgroup
+    __shared__ int s_next;  // score_pairs' query counter
     if (tid < 2) s_qcut[tid] = one_kr && tid == 1 && P.noct <= 8 ? nq : 0;
+    if (tid == 0) s_next = 0;
     __syncthreads();
     if (!one_kr) {
         int c4 = 0, c8 = 0;
@@ -1664,7 +1836,12 @@ __device__ __forceinline__ void proj_search_body(const ProjProblem* __restrict__
         }
     };
     if constexpr (SPLIT && kSplitKr > 0) {
-        pass(std::integral_constant<int, (kSplitKr > 0 ? kSplitKr : 1)>{}, 0, nq);
+        // pyramids above eight levels: the pairs without lockstep (configs[4] RGB-D +2.2 %; at
+        // configs[1] they measured 1 % slower than the lockstep pairs, r06pq)
+        if (ORBX_SPLIT_PERSIST && P.noct > 8)
+            score_pairs(pb, P, G, qk, qmp, qang, &s_next);
+        else
+            pass(std::integral_constant<int, (kSplitKr > 0 ? kSplitKr : 1)>{}, 0, nq);
     } else {
         if (qcut4 > 0) pass(std::integral_constant<int, 4>{}, 0, qcut4);
         if (qcut8 > qcut4) pass(std::integral_constant<int, 8>{}, qcut4, qcut8);
